@@ -1,0 +1,76 @@
+"""Shared test helpers: fixture loading and oracle evaluation (test infra)."""
+from __future__ import annotations
+
+from pathlib import Path
+from typing import Dict
+
+import numpy as np
+import torch
+
+from cases import (CMACase, HybridCase, cma_inputs, cma_state, hybrid_inputs,
+                   hybrid_state, pair_names)
+
+GOLDEN = Path(__file__).resolve().parent / "golden"
+
+
+def load_fixture(name: str) -> Dict[str, np.ndarray]:
+    with np.load(GOLDEN / f"{name}.npz", allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def oracle_hybrid(case: HybridCase, dtype=torch.float32):
+    """Run the CPU oracle on the case; returns (outputs dict, param grads, input grads)."""
+    from oracle.hybrid_cpu import hybrid_forward
+    sd = hybrid_state(case.names, case.dims, case.hidden, case.classes, case.seed, case.deleted)
+    params = {k: torch.from_numpy(v).to(dtype).requires_grad_(True) for k, v in sd.items()}
+    feats_np, mask_np, grad_np = hybrid_inputs(case)
+    feats = {m: torch.from_numpy(v).to(dtype).requires_grad_(True) for m, v in feats_np.items()}
+    logits, info = hybrid_forward(params, case.names, feats, torch.from_numpy(mask_np).to(dtype),
+                                  case.heads)
+    (logits * torch.from_numpy(grad_np).to(dtype)).sum().backward()
+    out = {"logits": logits.detach(), "fusion_weights": info["fusion_weights"].detach(),
+           "pooled": info["pooled"].detach()}
+    for k, v in info["attention_maps"].items():
+        out[f"attn/{k}"] = v.detach()
+    grads = {k: (p.grad if p.grad is not None else torch.zeros_like(p)).detach()
+             for k, p in params.items()}
+    dx = {m: t.grad.detach() for m, t in feats.items()}
+    return out, grads, dx
+
+
+def oracle_cma(case: CMACase, dtype=torch.float32):
+    from oracle.hybrid_cpu import cma_forward
+    sd = cma_state(case.query_dim, case.key_dim, case.hidden, case.seed)
+    params = {k: torch.from_numpy(v).to(dtype).requires_grad_(True) for k, v in sd.items()}
+    q, k, v, mask, grad = cma_inputs(case)
+    qt, kt, vt = (torch.from_numpy(a).to(dtype).requires_grad_(True) for a in (q, k, v))
+    mt = torch.from_numpy(mask).to(dtype) if mask is not None else None
+    att, w = cma_forward(params, "", qt, kt, vt, case.heads, mask=mt)
+    (att * torch.from_numpy(grad).to(dtype)).sum().backward()
+    out = {"attended": att.detach(), "weights": w.detach(), "dquery": qt.grad, "dkey": kt.grad,
+           "dvalue": vt.grad}
+    for name, p in params.items():
+        out[f"grad/{name}"] = p.grad
+    return out
+
+
+def rel_err(got, ref) -> float:
+    """max|got-ref| / max(max|ref|, 1e-6)  (SURVEY §8d parity metric)."""
+    got = torch.as_tensor(np.asarray(got) if not torch.is_tensor(got) else got).double().cpu()
+    ref = torch.as_tensor(np.asarray(ref) if not torch.is_tensor(ref) else ref).double().cpu()
+    assert got.shape == ref.shape, (tuple(got.shape), tuple(ref.shape))
+    if ref.numel() == 0:
+        return 0.0
+    return float((got - ref).abs().max() / max(float(ref.abs().max()), 1e-6))
+
+
+def close(got, ref, rtol: float, atol: float = 0.0) -> bool:
+    """max|got-ref| <= rtol*max|ref| + atol.  atol only matters for tensors whose
+    reference is mathematically zero (e.g. key_proj.bias grads: softmax is
+    shift-invariant) and holds pure rounding noise."""
+    got = torch.as_tensor(np.asarray(got) if not torch.is_tensor(got) else got).double().cpu()
+    ref = torch.as_tensor(np.asarray(ref) if not torch.is_tensor(ref) else ref).double().cpu()
+    assert got.shape == ref.shape, (tuple(got.shape), tuple(ref.shape))
+    if ref.numel() == 0:
+        return True
+    return float((got - ref).abs().max()) <= rtol * float(ref.abs().max()) + atol

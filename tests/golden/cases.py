@@ -1,0 +1,212 @@
+"""Deterministic parity cases shared by the fixture generator and the tests.
+
+Test infrastructure only.  Every tensor here (weights, inputs, upstream
+gradients) is a pure function of a seed through numpy's PCG64
+(``numpy.random.default_rng``), which is stable across numpy versions, so the
+GPU box can rebuild the exact inputs the golden outputs were produced from
+without ever seeing ``/root/reference``.
+
+Weight key names follow the reference's ``state_dict`` layout:
+``projections.{m}.0.{weight,bias}`` (src/fusion.py:291-298),
+``attention_modules.{q}_to_{k}.{query,key,value,out}_proj.{weight,bias}``
+(src/fusion.py:300-314, src/attention.py:61-64),
+``gating_layers.{m}.{weight,bias}`` (src/fusion.py:316-321),
+``classifier.{0,3}.{weight,bias}`` (src/fusion.py:323-328).
+Init bounds follow nn.Linear's default U(-1/sqrt(fan_in), 1/sqrt(fan_in)).
+"""
+
+from __future__ import annotations
+
+from collections import OrderedDict
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+
+def _linear(rng: np.random.Generator, out_f: int, in_f: int) -> Tuple[np.ndarray, np.ndarray]:
+    bound = 1.0 / np.sqrt(max(in_f, 1))
+    w = rng.uniform(-bound, bound, size=(out_f, in_f)).astype(np.float32)
+    b = rng.uniform(-bound, bound, size=(out_f,)).astype(np.float32)
+    return w, b
+
+
+def pair_names(names: Sequence[str], deleted: Sequence[str] = ()) -> List[str]:
+    out = []
+    for q in names:
+        for k in names:
+            if q != k and f"{q}_to_{k}" not in deleted:
+                out.append(f"{q}_to_{k}")
+    return out
+
+
+def hybrid_state(names: Sequence[str], dims: Dict[str, int], hidden: int,
+                 num_classes: int, seed: int, deleted: Sequence[str] = ()) -> "OrderedDict[str, np.ndarray]":
+    rng = np.random.default_rng(seed)
+    sd: "OrderedDict[str, np.ndarray]" = OrderedDict()
+    for m in names:
+        w, b = _linear(rng, hidden, dims[m])
+        sd[f"projections.{m}.0.weight"] = w
+        sd[f"projections.{m}.0.bias"] = b
+    for q in names:
+        for k in names:
+            if q == k:
+                continue
+            for proj in ("query_proj", "key_proj", "value_proj", "out_proj"):
+                w, b = _linear(rng, hidden, hidden)
+                if f"{q}_to_{k}" in deleted:
+                    continue  # keep the rng stream identical with/without deletion
+                sd[f"attention_modules.{q}_to_{k}.{proj}.weight"] = w
+                sd[f"attention_modules.{q}_to_{k}.{proj}.bias"] = b
+    for m in names:
+        w, b = _linear(rng, 1, hidden)
+        sd[f"gating_layers.{m}.weight"] = w
+        sd[f"gating_layers.{m}.bias"] = b
+    w, b = _linear(rng, hidden, hidden)
+    sd["classifier.0.weight"] = w
+    sd["classifier.0.bias"] = b
+    w, b = _linear(rng, num_classes, hidden)
+    sd["classifier.3.weight"] = w
+    sd["classifier.3.bias"] = b
+    return sd
+
+
+def cma_state(query_dim: int, key_dim: int, hidden: int, seed: int) -> "OrderedDict[str, np.ndarray]":
+    rng = np.random.default_rng(seed)
+    sd: "OrderedDict[str, np.ndarray]" = OrderedDict()
+    for proj, fan_in in (("query_proj", query_dim), ("key_proj", key_dim),
+                         ("value_proj", key_dim), ("out_proj", hidden)):
+        w, b = _linear(rng, hidden, fan_in)
+        sd[f"{proj}.weight"] = w
+        sd[f"{proj}.bias"] = b
+    return sd
+
+
+@dataclass
+class HybridCase:
+    """One HybridFusion parity case (eval mode: dropout is identity)."""
+    name: str
+    names: List[str]
+    dims: Dict[str, int]
+    seq: Dict[str, int]          # per-modality sequence length; 0 => 2-D (B, D) input
+    batch: int
+    hidden: int
+    heads: int
+    classes: int
+    seed: int
+    mask: Optional[List[List[float]]] = None     # explicit mask rows (cycled); None => seeded
+    mask_keep: float = 1.0                       # seeded Bernoulli keep-rate when mask is None
+    deleted: List[str] = field(default_factory=list)
+    full: bool = True            # store full gradient tensors (small cases)
+
+    @property
+    def seq_mode(self) -> bool:
+        return any(v > 0 for v in self.seq.values())
+
+
+def hybrid_inputs(case: HybridCase) -> Tuple[Dict[str, np.ndarray], np.ndarray, np.ndarray]:
+    """Returns (features, mask (B,M) float32, upstream grad dlogits (B,C))."""
+    rng = np.random.default_rng(case.seed + 7919)
+    feats: Dict[str, np.ndarray] = {}
+    for m in case.names:
+        L = case.seq[m]
+        shape = (case.batch, L, case.dims[m]) if L > 0 else (case.batch, case.dims[m])
+        feats[m] = rng.standard_normal(shape).astype(np.float32)
+    M = len(case.names)
+    if case.mask is not None:
+        rows = [case.mask[i % len(case.mask)] for i in range(case.batch)]
+        mask = np.asarray(rows, dtype=np.float32)
+    else:
+        mask = (rng.uniform(size=(case.batch, M)) < case.mask_keep).astype(np.float32)
+        # keep >= 1 modality per row except ~1% all-masked rows (SURVEY §8d C5 recipe)
+        for b in range(case.batch):
+            if mask[b].sum() == 0 and rng.uniform() > 0.01:
+                mask[b, rng.integers(M)] = 1.0
+    grad = rng.standard_normal((case.batch, case.classes)).astype(np.float32)
+    return feats, mask, grad
+
+
+@dataclass
+class CMACase:
+    """Standalone CrossModalAttention parity case (eval mode)."""
+    name: str
+    batch: int
+    lq: int        # 0 => 2-D query (B, Dq)
+    lk: int        # 0 => 2-D key/value (B, Dk)
+    query_dim: int
+    key_dim: int
+    hidden: int
+    heads: int
+    seed: int
+    mask_kind: str = "none"    # none | 1d | 2d
+    mask_1d: Optional[List[float]] = None
+
+
+def cma_inputs(case: CMACase):
+    rng = np.random.default_rng(case.seed + 104729)
+    qs = (case.batch, case.lq, case.query_dim) if case.lq else (case.batch, case.query_dim)
+    ks = (case.batch, case.lk, case.key_dim) if case.lk else (case.batch, case.key_dim)
+    query = rng.standard_normal(qs).astype(np.float32)
+    key = rng.standard_normal(ks).astype(np.float32)
+    value = rng.standard_normal(ks).astype(np.float32)
+    mask = None
+    if case.mask_kind == "1d":
+        mask = np.asarray(case.mask_1d, dtype=np.float32)
+    elif case.mask_kind == "2d":
+        lk = max(case.lk, 1)
+        mask = (rng.uniform(size=(case.batch, lk)) < 0.7).astype(np.float32)
+        mask[0, :] = 0.0          # a fully masked sample -> NaN -> 0 path
+        mask[1, :] = 1.0
+    lq = max(case.lq, 1)
+    gshape = (case.batch, lq, case.hidden) if case.lq else (case.batch, case.hidden)
+    grad = rng.standard_normal(gshape).astype(np.float32)
+    return query, key, value, mask, grad
+
+
+_MASK_ROWS = [[1, 1, 1], [1, 0, 1], [0, 0, 1], [0, 0, 0], [1, 1, 0], [0, 1, 0], [0.5, 1, 1], [1, 1, 0.25]]
+
+HYBRID_CASES: List[HybridCase] = [
+    # Reference semantics (2-D inputs, L=1 attention), small, full gradients.
+    HybridCase("tiny_l1", ["m0", "m1", "m2"], {"m0": 12, "m1": 20, "m2": 16},
+               {"m0": 0, "m1": 0, "m2": 0}, batch=8, hidden=32, heads=4, classes=5,
+               seed=11, mask=_MASK_ROWS),
+    HybridCase("tiny_l1_deleted_pair", ["m0", "m1", "m2"], {"m0": 12, "m1": 20, "m2": 16},
+               {"m0": 0, "m1": 0, "m2": 0}, batch=8, hidden=32, heads=4, classes=5,
+               seed=12, mask=_MASK_ROWS, deleted=["m0_to_m1", "m2_to_m0"]),
+    # tests/test_fusion.py:50-80 shape: video/imu, hidden 8, heads 1.
+    HybridCase("known_answer_2mod", ["video", "imu"], {"video": 4, "imu": 4},
+               {"video": 0, "imu": 0}, batch=3, hidden=8, heads=1, classes=3,
+               seed=13, mask=[[1, 1], [1, 0], [0, 0]]),
+    # BASELINE config 2 at reference semantics (L=1): B=256, M=3, D=H=128, h=4, C=5.
+    HybridCase("c2_l1", ["m0", "m1", "m2"], {"m0": 128, "m1": 128, "m2": 128},
+               {"m0": 0, "m1": 0, "m2": 0}, batch=256, hidden=128, heads=4, classes=5,
+               seed=21, mask_keep=0.9, full=False),
+    # Sequence mode (composed oracle): equal and mixed lengths.
+    HybridCase("seq_equal", ["m0", "m1", "m2"], {"m0": 24, "m1": 32, "m2": 16},
+               {"m0": 16, "m1": 16, "m2": 16}, batch=4, hidden=32, heads=4, classes=5,
+               seed=31, mask=[[1, 1, 1], [1, 0, 1], [0, 0, 0], [0.5, 1, 0]]),
+    HybridCase("seq_mixed", ["video", "imu", "hr"], {"video": 40, "imu": 24, "hr": 8},
+               {"video": 30, "imu": 50, "hr": 20}, batch=3, hidden=64, heads=4, classes=11,
+               seed=32, mask=[[1, 1, 1], [0, 1, 1], [1, 0, 0]]),
+    HybridCase("seq_hd64", ["m0", "m1"], {"m0": 32, "m1": 48},
+               {"m0": 40, "m1": 72}, batch=2, hidden=128, heads=2, classes=4,
+               seed=33, mask=[[1, 1], [1, 0]]),
+]
+
+CMA_CASES: List[CMACase] = [
+    CMACase("cma_2d_mask1d", batch=4, lq=0, lk=0, query_dim=512, key_dim=64, hidden=256,
+            heads=4, seed=41, mask_kind="1d", mask_1d=[1, 1, 0, 1]),
+    CMACase("cma_3d_mask2d", batch=4, lq=30, lk=50, query_dim=24, key_dim=40, hidden=64,
+            heads=4, seed=42, mask_kind="2d"),
+    CMACase("cma_3d_nomask_hd8", batch=3, lq=17, lk=9, query_dim=16, key_dim=16, hidden=32,
+            heads=4, seed=43),
+    CMACase("cma_3d_long", batch=2, lq=160, lk=200, query_dim=32, key_dim=32, hidden=128,
+            heads=4, seed=44, mask_kind="1d", mask_1d=[1, 0]),
+]
+
+
+def case_by_name(name: str):
+    for c in HYBRID_CASES + CMA_CASES:
+        if c.name == name:
+            return c
+    raise KeyError(name)

@@ -1,0 +1,171 @@
+"""Generate golden parity fixtures by running the REFERENCE implementation.
+
+Container-only tool: it imports ``/root/reference/src`` (read-only, never copied)
+and writes small ``.npz`` fixtures next to this file.  The GPU box never runs
+it; tests there rebuild the inputs from the seeds in ``cases.py`` and compare
+against the stored outputs.
+
+What is recorded (eval mode, ``torch.set_float32_matmul_precision("highest")``):
+  * HybridFusion, 2-D inputs (reference semantics, L=1): the reference module's
+    own ``forward(..., return_attention=True)`` (src/fusion.py:331-427).
+  * HybridFusion, 3-D inputs (sequence mode): the composed oracle of SURVEY §8c,
+    built only from the reference module's own sub-modules: ``projections``,
+    ``attention_modules`` called on 3-D tensors (src/attention.py:92-146),
+    mean over the per-modality list, x mask, mean-pool over L,
+    ``compute_adaptive_weights`` (src/fusion.py:429-479), ``classifier``.
+  * standalone CrossModalAttention (src/attention.py:68-146).
+  * for a fixed upstream gradient G: d(sum(out * G)) w.r.t. inputs and params.
+
+Run:  python tests/golden/gen_golden.py
+"""
+
+from __future__ import annotations
+
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+HERE = Path(__file__).resolve().parent
+sys.path.insert(0, str(HERE))
+REF_SRC = Path("/root/reference/src")
+
+from cases import (CMA_CASES, HYBRID_CASES, cma_inputs, cma_state,  # noqa: E402
+                   hybrid_inputs, hybrid_state, pair_names)
+
+
+def _load_reference():
+    sys.path.insert(0, str(REF_SRC))
+    import attention as ref_attention  # noqa: F401
+    import fusion as ref_fusion
+    return ref_fusion, ref_attention
+
+
+def composed_seq_forward(model, feats, mask):
+    """SURVEY §8c composed oracle: reference sub-modules only, pooled over L."""
+    names = model.modality_names
+    P = {}
+    for i, m in enumerate(names):
+        x = feats[m]
+        mk = mask[:, i].reshape(-1, *([1] * (x.dim() - 1)))
+        P[m] = model.projections[m](model.dropout(x * mk))
+    lists = {m: [P[m]] for m in names}
+    maps = {}
+    for q in names:
+        for k in names:
+            if q == k:
+                continue
+            key = f"{q}_to_{k}"
+            if key not in model.attention_modules:
+                continue
+            ki = names.index(k)
+            att, w = model.attention_modules[key](P[q], P[k], P[k], mask=mask[:, ki])
+            lists[q].append(att)
+            maps[key] = w
+    pooled = {}
+    for i, m in enumerate(names):
+        agg = torch.stack(lists[m], dim=0).mean(dim=0)
+        mk = mask[:, i].reshape(-1, *([1] * (agg.dim() - 1)))
+        agg = agg * mk
+        pooled[m] = agg.mean(dim=1) if agg.dim() == 3 else agg
+    weights = model.compute_adaptive_weights(pooled, mask)
+    stacked = torch.stack([pooled[m] for m in names], dim=1)
+    fused = (stacked * weights.unsqueeze(-1)).sum(dim=1)
+    logits = model.classifier(fused)
+    return logits, {"attention_maps": maps, "fusion_weights": weights, "pooled": stacked}
+
+
+def gen_hybrid(ref_fusion, case):
+    dims = {m: case.dims[m] for m in case.names}
+    model = ref_fusion.HybridFusion(dims, hidden_dim=case.hidden, num_classes=case.classes,
+                                    num_heads=case.heads, dropout=0.1)
+    for key in case.deleted:
+        del model.attention_modules[key]
+    sd = hybrid_state(case.names, case.dims, case.hidden, case.classes, case.seed, case.deleted)
+    missing, unexpected = model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()},
+                                                strict=True)
+    assert not missing and not unexpected
+    model.eval()
+    feats_np, mask_np, grad_np = hybrid_inputs(case)
+    feats = {m: torch.from_numpy(v).requires_grad_(True) for m, v in feats_np.items()}
+    mask = torch.from_numpy(mask_np)
+
+    pooled_hook = {}
+    if case.seq_mode:
+        logits, info = composed_seq_forward(model, feats, mask)
+        pooled = info["pooled"]
+    else:
+        # capture the aggregated (B,M,H) tensor the reference feeds to the weighting
+        orig = model.compute_adaptive_weights
+
+        def hook(features, m):
+            pooled_hook["pooled"] = torch.stack([features[n] for n in model.modality_names], 1)
+            return orig(features, m)
+        model.compute_adaptive_weights = hook
+        logits, info = model(feats, mask, return_attention=True)
+        pooled = pooled_hook["pooled"]
+        # reference-vs-composed self check at L=1 (bit-identical)
+        del model.compute_adaptive_weights
+        logits2, _ = composed_seq_forward(model, {m: t.detach() for m, t in feats.items()}, mask)
+        assert torch.equal(logits.detach(), logits2.detach()), "composed oracle != reference at L=1"
+
+    (logits * torch.from_numpy(grad_np)).sum().backward()
+    out = {
+        "logits": logits.detach().numpy(),
+        "fusion_weights": info["fusion_weights"].detach().numpy(),
+        "pooled": pooled.detach().numpy(),
+        "mask": mask_np,
+    }
+    for key in pair_names(case.names, case.deleted):
+        out[f"attn/{key}"] = info["attention_maps"][key].detach().numpy()
+    for m in case.names:
+        g = feats[m].grad.numpy()
+        out[f"dx/{m}"] = g
+    for k, p in model.named_parameters():
+        g = p.grad.numpy() if p.grad is not None else np.zeros_like(p.detach().numpy())
+        if case.full:
+            out[f"grad/{k}"] = g
+        else:
+            flat = g.reshape(-1)
+            out[f"gradnorm/{k}"] = np.asarray([np.linalg.norm(flat.astype(np.float64))])
+            out[f"gradslice/{k}"] = flat[::37].copy()
+    return out
+
+
+def gen_cma(ref_attention, case):
+    model = ref_attention.CrossModalAttention(case.query_dim, case.key_dim, hidden_dim=case.hidden,
+                                              num_heads=case.heads, dropout=0.1)
+    sd = cma_state(case.query_dim, case.key_dim, case.hidden, case.seed)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    model.eval()
+    q, k, v, mask, grad = cma_inputs(case)
+    qt = torch.from_numpy(q).requires_grad_(True)
+    kt = torch.from_numpy(k).requires_grad_(True)
+    vt = torch.from_numpy(v).requires_grad_(True)
+    mt = torch.from_numpy(mask) if mask is not None else None
+    att, w = model(qt, kt, vt, mt)
+    (att * torch.from_numpy(grad)).sum().backward()
+    out = {"attended": att.detach().numpy(), "weights": w.detach().numpy(),
+           "dquery": qt.grad.numpy(), "dkey": kt.grad.numpy(), "dvalue": vt.grad.numpy()}
+    for name, p in model.named_parameters():
+        out[f"grad/{name}"] = p.grad.numpy()
+    return out
+
+
+def main():
+    torch.set_float32_matmul_precision("highest")
+    torch.set_num_threads(4)
+    ref_fusion, ref_attention = _load_reference()
+    for case in HYBRID_CASES:
+        out = gen_hybrid(ref_fusion, case)
+        np.savez_compressed(HERE / f"{case.name}.npz", **out)
+        print(f"wrote {case.name}.npz ({sum(a.nbytes for a in out.values())} B raw)")
+    for case in CMA_CASES:
+        out = gen_cma(ref_attention, case)
+        np.savez_compressed(HERE / f"{case.name}.npz", **out)
+        print(f"wrote {case.name}.npz ({sum(a.nbytes for a in out.values())} B raw)")
+
+
+if __name__ == "__main__":
+    main()

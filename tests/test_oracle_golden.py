@@ -1,0 +1,61 @@
+"""Pin the CPU oracle against outputs of the reference itself (golden fixtures).
+
+CPU-only.  The fixtures were produced by tests/golden/gen_golden.py running the
+reference HybridFusion / CrossModalAttention (src/fusion.py:331-479,
+src/attention.py:68-146) in eval mode.  The oracle is an independent
+restatement, so agreement here is at fp32 reassociation level (<=1e-5 rel).
+"""
+import numpy as np
+import pytest
+import torch
+
+from _util import close, load_fixture, oracle_cma, oracle_hybrid, rel_err
+from cases import CMA_CASES, HYBRID_CASES
+
+TOL = 1e-5
+
+
+@pytest.mark.parametrize("case", HYBRID_CASES, ids=lambda c: c.name)
+def test_oracle_hybrid_matches_reference(case):
+    fx = load_fixture(case.name)
+    out, grads, dx = oracle_hybrid(case)
+    assert rel_err(out["logits"], fx["logits"]) <= TOL
+    assert rel_err(out["fusion_weights"], fx["fusion_weights"]) <= TOL
+    assert rel_err(out["pooled"], fx["pooled"]) <= TOL
+    for k in fx:
+        if k.startswith("attn/"):
+            assert rel_err(out[k], fx[k]) <= TOL, k
+    for m in case.names:
+        assert rel_err(dx[m], fx[f"dx/{m}"]) <= TOL, m
+    for k, g in grads.items():
+        if case.full:
+            assert close(g, fx[f"grad/{k}"], TOL, 1e-6), k
+        else:
+            n = float(np.linalg.norm(g.double().numpy().reshape(-1)))
+            assert abs(n - float(fx[f"gradnorm/{k}"][0])) <= TOL * max(n, 1e-6) + 1e-6, k
+            assert close(g.reshape(-1)[::37], fx[f"gradslice/{k}"], TOL, 1e-6), k
+
+
+@pytest.mark.parametrize("case", CMA_CASES, ids=lambda c: c.name)
+def test_oracle_cma_matches_reference(case):
+    fx = load_fixture(case.name)
+    out = oracle_cma(case)
+    for k in fx:
+        assert close(out[k], fx[k], TOL, 1e-6), k
+
+
+def test_known_answer_weights():
+    """tests/test_fusion.py:50-80 semantics: [1,1] sums to 1, [1,0] -> [1,0], [0,0] -> [.5,.5]."""
+    fx = load_fixture("known_answer_2mod")
+    w = torch.from_numpy(fx["fusion_weights"])
+    assert torch.allclose(w[0].sum(), torch.tensor(1.0), atol=1e-6)
+    assert torch.allclose(w[1], torch.tensor([1.0, 0.0]), atol=1e-6)
+    assert torch.allclose(w[2], torch.full((2,), 0.5), atol=1e-6)
+
+
+def test_l1_zero_qk_grads():
+    """At L=1 the softmax over one key is constant: q/k projection grads are exactly 0."""
+    fx = load_fixture("tiny_l1")
+    for k, v in fx.items():
+        if k.startswith("grad/attention_modules") and ("query_proj" in k or "key_proj" in k):
+            assert np.all(v == 0.0), k
