@@ -1,0 +1,184 @@
+/*
+ * mmfusion — MI355X-native cross-modal attention fusion (C-ABI boundary).
+ *
+ * This is the drop-in boundary for the reference's hot path:
+ *   src/fusion.py::HybridFusion          (forward src/fusion.py:331-427,
+ *                                          compute_adaptive_weights :429-479)
+ *   src/attention.py::CrossModalAttention (forward src/attention.py:68-146)
+ * The reference is Python; its "FFI" for this path is the nn.Module forward()
+ * plus autograd.  The host mirror (package fusion.py / attention.py) binds the
+ * entry points below through ctypes.
+ *
+ * Conventions
+ *  - All tensors are fp32, contiguous, row-major, resident in device (HBM)
+ *    memory; pointers are plain device pointers.  No torch types appear here.
+ *  - Linear weights use PyTorch nn.Linear layout: w (out,in), b (out);
+ *    y = x w^T + b.
+ *  - `stream` is a hipStream_t (passed as void*).  Entry points only enqueue
+ *    work on it: no allocation, no host synchronisation, no host->device
+ *    copies, so they are safe inside hipGraph / torch.cuda.graph capture.
+ *  - Caller-owned buffers: `saved` (forward -> backward activations, size
+ *    mmf_*_saved_bytes) and `workspace` (backward scratch, size
+ *    mmf_*_workspace_bytes), 256-byte aligned.
+ *  - Dropout RNG: `rng_state` is a device array {uint64 seed, uint64 offset}.
+ *    Each forward snapshots it into `saved` and advances offset by 1 on the
+ *    device (graph-replay safe); backward replays the same Philox4x32-10
+ *    streams from the snapshot.
+ *  - Return value: 0 on success, otherwise an MMF_E* code with a message in
+ *    mmf_last_error().  Shape/limit checks run before any launch.
+ */
+#ifndef MMFUSION_H_
+#define MMFUSION_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MMF_MAX_MODALITIES 8
+#define MMF_MAX_PAIRS (MMF_MAX_MODALITIES * (MMF_MAX_MODALITIES - 1))
+#define MMF_MAX_HEAD_DIM 64
+
+enum {
+  MMF_OK = 0,
+  MMF_EINVAL = 1,   /* bad shape / argument (reference would raise) */
+  MMF_ELIMIT = 2,   /* outside the kernel limits (e.g. head_dim > 64) */
+  MMF_EHIP = 3      /* HIP runtime error while enqueueing */
+};
+
+/* nn.Linear parameters (and their gradients). */
+typedef struct mmf_linear { const float* w; const float* b; } mmf_linear;
+typedef struct mmf_linear_grad { float* w; float* b; } mmf_linear_grad;
+
+/* ---------------------------------------------------------------------
+ * HybridFusion (src/fusion.py:248-479)
+ * Modalities are in HybridFusion.modality_names order.  seq_len[m] == 0 means a
+ * 2-D (B, D_m) input (reference semantics: L = 1 attention); > 0 means a 3-D
+ * (B, L_m, D_m) input (sequence mode: agg mean-pooled over L_m).
+ * pair_q/pair_k list the PRESENT attention modules "{q}_to_{k}" in the
+ * reference's iteration order (src/fusion.py:383-404); deleted pairs are
+ * simply absent.
+ * ------------------------------------------------------------------- */
+typedef struct mmf_hybrid_desc {
+  int32_t batch;
+  int32_t num_modalities;
+  int32_t hidden;
+  int32_t num_heads;
+  int32_t num_classes;
+  int32_t seq_len[MMF_MAX_MODALITIES];
+  int32_t in_dim[MMF_MAX_MODALITIES];
+  int32_t num_pairs;
+  int32_t pair_q[MMF_MAX_PAIRS];
+  int32_t pair_k[MMF_MAX_PAIRS];
+  float dropout;            /* nn.Dropout p shared by every dropout site */
+  int32_t training;         /* module.training */
+  int32_t return_attention; /* write attention maps */
+} mmf_hybrid_desc;
+
+typedef struct mmf_hybrid_params {
+  mmf_linear proj[MMF_MAX_MODALITIES];   /* projections.{m}.0 */
+  mmf_linear q[MMF_MAX_PAIRS];           /* attention_modules.{q}_to_{k}.query_proj */
+  mmf_linear k[MMF_MAX_PAIRS];           /*   .key_proj   */
+  mmf_linear v[MMF_MAX_PAIRS];           /*   .value_proj */
+  mmf_linear o[MMF_MAX_PAIRS];           /*   .out_proj   */
+  mmf_linear gate[MMF_MAX_MODALITIES];   /* gating_layers.{m} (1 x H) */
+  mmf_linear cls1;                       /* classifier.0 (H x H) */
+  mmf_linear cls2;                       /* classifier.3 (C x H) */
+} mmf_hybrid_params;
+
+typedef struct mmf_hybrid_grads {
+  mmf_linear_grad proj[MMF_MAX_MODALITIES];
+  mmf_linear_grad q[MMF_MAX_PAIRS];
+  mmf_linear_grad k[MMF_MAX_PAIRS];
+  mmf_linear_grad v[MMF_MAX_PAIRS];
+  mmf_linear_grad o[MMF_MAX_PAIRS];
+  mmf_linear_grad gate[MMF_MAX_MODALITIES];
+  mmf_linear_grad cls1;
+  mmf_linear_grad cls2;
+} mmf_hybrid_grads;
+
+size_t mmf_hybrid_saved_bytes(const mmf_hybrid_desc* d);
+size_t mmf_hybrid_workspace_bytes(const mmf_hybrid_desc* d);
+
+/* Forward.  x[m]: (B, L_m, D_m); mask: (B, M) float (fractional values scale
+ * features, src/fusion.py:361-373).  Writes logits (B, C), fusion_weights
+ * (B, M) and, when d->return_attention, attn_maps[p] (B, h, Lq, Lk) post-
+ * dropout for each present pair p (NULL entries skipped). */
+int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* params,
+                       const float* const* x, const float* mask, const uint64_t* rng_state,
+                       void* saved, float* logits, float* fusion_weights,
+                       float* const* attn_maps, void* stream);
+
+/* Backward of sum(logits * dlogits).  Parameter gradients are WRITTEN (not
+ * accumulated) to `grads`; dx[m] (may be NULL) receives d/dx[m]. */
+int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* params,
+                        const float* const* x, const float* mask, const void* saved,
+                        const float* dlogits, void* workspace, const mmf_hybrid_grads* grads,
+                        float* const* dx, void* stream);
+
+/* Public HybridFusion.compute_adaptive_weights (src/fusion.py:429-479):
+ * feats[m] (B, H) per modality -> weights (B, M).  workspace: see
+ * mmf_adaptive_weights_workspace_bytes. */
+size_t mmf_adaptive_weights_workspace_bytes(int32_t batch, int32_t num_modalities, int32_t hidden);
+int mmf_adaptive_weights(int32_t batch, int32_t num_modalities, int32_t hidden,
+                         const float* const* feats, const float* mask,
+                         const mmf_linear* gate /* [M] */, float* weights, void* workspace,
+                         void* stream);
+
+/* ---------------------------------------------------------------------
+ * CrossModalAttention (src/attention.py:16-146), standalone.
+ * lq/lk: sequence lengths (use 1 for the reference's 2-D inputs).
+ * mask_mode: 0 none, 1 per-sample (B,) (src/attention.py:120-121),
+ *            2 per-key (B, Lk).
+ * ------------------------------------------------------------------- */
+typedef struct mmf_cma_desc {
+  int32_t batch, lq, lk, query_dim, key_dim, hidden, num_heads;
+  int32_t mask_mode;
+  float dropout;
+  int32_t training;
+} mmf_cma_desc;
+
+typedef struct mmf_cma_params { mmf_linear q, k, v, o; } mmf_cma_params;
+typedef struct mmf_cma_grads { mmf_linear_grad q, k, v, o; } mmf_cma_grads;
+
+size_t mmf_cma_saved_bytes(const mmf_cma_desc* d);
+size_t mmf_cma_workspace_bytes(const mmf_cma_desc* d);
+
+/* attended: (B, Lq, H); attn_weights: (B, h, Lq, Lk) post-dropout. */
+int mmf_cma_forward(const mmf_cma_desc* d, const mmf_cma_params* params, const float* query,
+                    const float* key, const float* value, const float* mask,
+                    const uint64_t* rng_state, void* saved, float* attended,
+                    float* attn_weights, void* stream);
+
+/* Backward of sum(attended * d_attended).  dquery/dkey/dvalue may be NULL. */
+int mmf_cma_backward(const mmf_cma_desc* d, const mmf_cma_params* params, const float* query,
+                     const float* key, const float* value, const float* mask, const void* saved,
+                     const float* d_attended, void* workspace, const mmf_cma_grads* grads,
+                     float* dquery, float* dkey, float* dvalue, void* stream);
+
+/* ---------------------------------------------------------------------
+ * Training-step helpers used by the data-parallel step (not part of the
+ * reference interface; the reference uses torch.optim.AdamW via Lightning,
+ * src/train.py:374-414).
+ * ------------------------------------------------------------------- */
+/* Fused CrossEntropyLoss(label_smoothing) forward+backward on (B, C) logits:
+ * loss_out[0] = mean loss, dlogits = d(loss)/d(logits) * grad_scale. */
+int mmf_cross_entropy_ls(int32_t batch, int32_t classes, const float* logits,
+                         const int64_t* labels, float smoothing, float grad_scale,
+                         float* loss_out, float* dlogits, void* stream);
+
+/* AdamW over a flat fp32 buffer (torch.optim.AdamW semantics, decoupled decay).
+ * step_dev: device int64 step counter, incremented by this call. */
+int mmf_adamw_step(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                   int64_t* step_dev, float lr, float beta1, float beta2, float eps,
+                   float weight_decay, float grad_scale, void* stream);
+
+const char* mmf_last_error(void);
+const char* mmf_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MMFUSION_H_ */

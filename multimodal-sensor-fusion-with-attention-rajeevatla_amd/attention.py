@@ -1,0 +1,191 @@
+"""Drop-in `attention` module: CrossModalAttention on MI355X HIP kernels.
+
+Mirrors src/attention.py::CrossModalAttention (src/attention.py:16-146): same
+constructor arguments, attributes (hidden_dim, num_heads, head_dim,
+query_proj, key_proj, value_proj, out_proj, dropout, scale), state_dict keys
+and forward(query, key, value, mask=None) -> (attended, attn_weights).
+
+Compute path: include/mmfusion.h mmf_cma_forward / mmf_cma_backward
+(libmmfusion.so, gfx950).  There is no CPU path: CPU tensors raise.
+Differences from the reference, by design:
+  * the returned attention weights are not differentiable (the reference's
+    are; nothing in train/eval back-propagates through them);
+  * dropout masks come from Philox4x32-10 on the device, not torch's RNG, so
+    train-mode outputs are statistically (not bitwise) equal.
+"""
+
+from __future__ import annotations
+
+import os
+import sys
+from typing import Any, Optional, Tuple, cast
+
+import torch
+import torch.nn as nn
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+if _HERE not in sys.path:
+    sys.path.insert(0, _HERE)
+
+import mmf_native as _nat  # noqa: E402
+
+
+_RNG_COUNTER = [0]
+
+
+def _new_rng_state() -> torch.Tensor:
+    """{seed, offset} for the device Philox stream of one module.
+
+    Derived from torch.initial_seed() and a construction counter, so it is
+    reproducible under torch.manual_seed WITHOUT consuming torch's RNG: the
+    nn.Linear initialisation stream stays identical to the reference's.
+    """
+    _RNG_COUNTER[0] += 1
+    x = (torch.initial_seed() * 0x9E3779B97F4A7C15 + _RNG_COUNTER[0] * 0xBF58476D1CE4E5B9) & (2**64 - 1)
+    x ^= x >> 31
+    x = (x * 0x94D049BB133111EB) & (2**64 - 1)
+    x ^= x >> 29
+    return torch.tensor([x & (2**63 - 1), 0], dtype=torch.int64)
+
+
+class _CMAFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, desc: "_nat.CmaDesc", mask, rng, query, key, value, qw, qb, kw, kb, vw, vb, ow, ob):
+        L = _nat.lib()
+        dev = query.device
+        B, lq, lk, H, h = desc.batch, desc.lq, desc.lk, desc.hidden, desc.num_heads
+        saved = torch.empty(L.mmf_cma_saved_bytes(ctypes_ref(desc)), dtype=torch.uint8, device=dev)
+        attended = torch.empty(B, lq, H, dtype=torch.float32, device=dev)
+        attn = torch.empty(B, h, lq, lk, dtype=torch.float32, device=dev)
+        params = _nat.CmaParams()
+        for name, (w, b) in zip(("q", "k", "v", "o"), ((qw, qb), (kw, kb), (vw, vb), (ow, ob))):
+            setattr(params, name, _nat.Linear(w.data_ptr(), b.data_ptr()))
+        rc = L.mmf_cma_forward(ctypes_ref(desc), ctypes_ref(params), query.data_ptr(), key.data_ptr(),
+                               value.data_ptr(), _nat.ptr(mask), rng.data_ptr(), saved.data_ptr(),
+                               attended.data_ptr(), attn.data_ptr(), _nat.stream_ptr(dev))
+        _nat.check(rc, "CrossModalAttention forward")
+        ctx.desc = desc
+        ctx.saved_buf = saved
+        ctx.save_for_backward(mask if mask is not None else torch.empty(0, device=dev), query, key,
+                              value, qw, qb, kw, kb, vw, vb, ow, ob)
+        ctx.has_mask = mask is not None
+        ctx.mark_non_differentiable(attn)
+        return attended, attn
+
+    @staticmethod
+    def backward(ctx, d_att, _d_attn):
+        L = _nat.lib()
+        mask, query, key, value, qw, qb, kw, kb, vw, vb, ow, ob = ctx.saved_tensors
+        mask = mask if ctx.has_mask else None
+        desc = ctx.desc
+        dev = query.device
+        d_att = _nat.f32c(d_att)
+        ws = torch.empty(L.mmf_cma_workspace_bytes(ctypes_ref(desc)), dtype=torch.uint8, device=dev)
+        params = _nat.CmaParams()
+        grads = _nat.CmaGrads()
+        plist = ((qw, qb), (kw, kb), (vw, vb), (ow, ob))
+        sizes = [w.numel() + b.numel() for w, b in plist]
+        flat = torch.empty(sum(sizes), dtype=torch.float32, device=dev)
+        gviews = []
+        off = 0
+        for name, (w, b) in zip(("q", "k", "v", "o"), plist):
+            gw = flat[off:off + w.numel()].view_as(w)
+            off += w.numel()
+            gb = flat[off:off + b.numel()].view_as(b)
+            off += b.numel()
+            gviews += [gw, gb]
+            setattr(params, name, _nat.Linear(w.data_ptr(), b.data_ptr()))
+            setattr(grads, name, _nat.Linear(gw.data_ptr(), gb.data_ptr()))
+        nq, nk, nv = ctx.needs_input_grad[3:6]
+        dq = torch.empty_like(query) if nq else None
+        dk = torch.empty_like(key) if nk else None
+        dv = torch.empty_like(value) if nv else None
+        rc = L.mmf_cma_backward(ctypes_ref(desc), ctypes_ref(params), query.data_ptr(), key.data_ptr(),
+                                value.data_ptr(), _nat.ptr(mask), ctx.saved_buf.data_ptr(),
+                                d_att.data_ptr(), ws.data_ptr(), ctypes_ref(grads), _nat.ptr(dq),
+                                _nat.ptr(dk), _nat.ptr(dv), _nat.stream_ptr(dev))
+        _nat.check(rc, "CrossModalAttention backward")
+        return (None, None, None, dq, dk, dv, *gviews)
+
+
+def ctypes_ref(s):
+    import ctypes
+    return ctypes.byref(s)
+
+
+class CrossModalAttention(nn.Module):
+    """Cross-modal attention: modality A attends to modality B (src/attention.py:16-66)."""
+
+    hidden_dim: int
+    num_heads: int
+    head_dim: int
+    query_proj: nn.Linear
+    key_proj: nn.Linear
+    value_proj: nn.Linear
+    out_proj: nn.Linear
+    dropout: nn.Dropout
+    scale: float
+
+    def __init__(self, query_dim: int, key_dim: int, hidden_dim: int = 256, num_heads: int = 4,
+                 dropout: float = 0.1):
+        super().__init__()
+        head_dim = hidden_dim // num_heads
+        cast_self = cast(Any, self)
+        cast_self.hidden_dim = hidden_dim
+        cast_self.num_heads = num_heads
+        cast_self.head_dim = head_dim
+        assert hidden_dim % num_heads == 0, (
+            f"hidden_dim ({hidden_dim}) must be divisible by num_heads ({num_heads})")
+        # same construction order as the reference => same init under a seed
+        self.query_proj = nn.Linear(query_dim, hidden_dim)
+        self.key_proj = nn.Linear(key_dim, hidden_dim)
+        self.value_proj = nn.Linear(key_dim, hidden_dim)
+        self.out_proj = nn.Linear(hidden_dim, hidden_dim)
+        self.dropout = nn.Dropout(dropout)
+        cast_self.scale = head_dim ** -0.5
+        self.register_buffer("_rng_state", _new_rng_state(), persistent=False)
+
+    def forward(self, query: torch.Tensor, key: torch.Tensor, value: torch.Tensor,
+                mask: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """src/attention.py:68-146: (B,Dq)/(B,Lq,Dq) x (B,Dk)/(B,Lk,Dk) -> (attended, weights)."""
+        B = query.size(0)
+        squeeze_q = query.dim() == 2
+        squeeze_k = key.dim() == 2
+        q3 = query.unsqueeze(1) if squeeze_q else query
+        k3 = key.unsqueeze(1) if squeeze_k else key
+        v3 = value.unsqueeze(1) if value.dim() == 2 else value
+        if q3.dim() != 3 or k3.dim() != 3 or v3.dim() != 3:
+            raise RuntimeError("CrossModalAttention expects 2-D or 3-D query/key/value tensors")
+        for t, nm in ((q3, "query"), (k3, "key"), (v3, "value")):
+            _nat.require_device(t, nm)
+        if k3.shape[:2] != v3.shape[:2]:
+            raise RuntimeError(f"key {tuple(k3.shape)} and value {tuple(v3.shape)} shapes differ")
+        if q3.size(-1) != self.query_proj.in_features or k3.size(-1) != self.key_proj.in_features \
+                or v3.size(-1) != self.value_proj.in_features:
+            raise RuntimeError("CrossModalAttention: feature dims do not match the projections")
+        lq, lk = q3.size(1), k3.size(1)
+        mask_mode = 0
+        m = None
+        if mask is not None:
+            m = mask.to(device=q3.device, dtype=torch.float32)
+            if m.dim() == 1:
+                mask_mode = 1
+                if m.numel() != B:
+                    raise RuntimeError(f"1-D mask must have {B} entries, got {m.numel()}")
+            elif m.dim() == 2 and m.shape == (B, lk):
+                mask_mode = 2
+            else:
+                raise RuntimeError(f"mask of shape {tuple(m.shape)} does not broadcast to (B, Lk)")
+            m = m.contiguous()
+        desc = _nat.CmaDesc(B, lq, lk, self.query_proj.in_features, self.key_proj.in_features,
+                            self.hidden_dim, self.num_heads, mask_mode, float(self.dropout.p),
+                            int(self.training))
+        attended, attn = _CMAFunction.apply(
+            desc, m, self._rng_state, _nat.f32c(q3), _nat.f32c(k3), _nat.f32c(v3),
+            self.query_proj.weight, self.query_proj.bias, self.key_proj.weight, self.key_proj.bias,
+            self.value_proj.weight, self.value_proj.bias, self.out_proj.weight, self.out_proj.bias)
+        if squeeze_q:
+            attended = attended.squeeze(1)
+        if squeeze_k:
+            attn = attn[:, :, :, :1]
+        return attended, attn

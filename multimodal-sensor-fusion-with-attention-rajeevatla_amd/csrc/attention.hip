@@ -1,0 +1,561 @@
+// Flash-style cross-modal attention on CDNA4 fp32 matrix cores.
+//
+// Semantics (src/attention.py:118-139): scores = (q k^T) * hd^-0.5; keys with
+// mask == 0 get -inf; softmax; a row whose keys are all masked is NaN in the
+// reference and nan_to_num'd to 0 (src/attention.py:127-129), so here it
+// produces P = 0, O = 0, LSE = -inf; Dropout(p) on the probabilities; attn @ v.
+//
+// Layout: one workgroup = 4 waves = 128 query rows (forward / dQ) or 128 keys
+// (dK/dV) of one (pair, sample, head).  K/V (or Q/dO) chunks are staged in LDS
+// with a 16-B row pad (conflict-free ds_read_b128 on the row-wise MFMA operand).
+//
+// MFMA orientation (v_mfma_f32_32x32x2_f32; C/D: col = lane&31, rows in regs):
+//  * forward / dQ: S^T = K Q^T, so each lane owns ONE query row (col) and 16 of
+//    the tile's 32 keys (regs; the other 16 sit in lane^32).  Row max / row sum
+//    are in-register + one xor-32 shuffle.  The S^T accumulator registers are
+//    directly the B operand of O^T += V^T P^T and dQ^T += K^T dS^T (no LDS trip).
+//  * dK/dV: S = Q K^T (key on the lane); the accumulators are directly the A
+//    operand of dV += P'^T dO and dK += dS^T Q.
+// The head dimension is zero-padded to HDP (32 or 64); the MFMA contraction
+// order over d is permuted (lane half h owns d in [h*HDP/2, (h+1)*HDP/2)) so
+// each lane's operand is contiguous.
+#include <cstring>
+
+#include "mmf_device.h"
+
+namespace mmf {
+
+namespace {
+
+constexpr int NT = 256;
+
+__device__ __forceinline__ float kmask_val(const AttnPair& P, int b, int key) {
+  if (P.kmask_mode == 1) return P.kmask[(int64_t)b * P.kmask_ld];
+  if (P.kmask_mode == 2) return P.kmask[(int64_t)b * P.kmask_ld + key];
+  return 1.f;
+}
+
+// Load rows [r0, r0+ROWS) of a (B, L, ld) tensor's head slice into LDS [ROWS][LS]
+// (cols >= hd and rows >= L are zero).
+template <int ROWS, int HDP, int LS>
+__device__ __forceinline__ void load_rows(float* S, const float* base, int L, int ld, int r0, int hd,
+                                          bool vec) {
+  constexpr int C4 = HDP / 4;
+  for (int idx = threadIdx.x; idx < ROWS * C4; idx += NT) {
+    const int r = idx / C4, c4 = (idx % C4) * 4;
+    const int row = r0 + r;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (row < L) {
+      const float* p = base + (int64_t)row * ld + c4;
+      if (vec && c4 + 3 < hd) {
+        v = *reinterpret_cast<const float4*>(p);
+      } else {
+        if (c4 + 0 < hd) v.x = p[0];
+        if (c4 + 1 < hd) v.y = p[1];
+        if (c4 + 2 < hd) v.z = p[2];
+        if (c4 + 3 < hd) v.w = p[3];
+      }
+    }
+    *reinterpret_cast<float4*>(&S[r * LS + c4]) = v;
+  }
+}
+
+template <int HALF>
+__device__ __forceinline__ void load_frag(float* f, const float* row, int dbase, int hd, bool valid) {
+#pragma unroll
+  for (int s = 0; s < HALF; ++s) {
+    const int d = dbase + s;
+    f[s] = (valid && d < hd) ? row[d] : 0.f;
+  }
+}
+
+// acc += A_lds_row(lane) . f   over the HALF-long contraction (row-wise LDS operand)
+template <int HALF>
+__device__ __forceinline__ f32x16 dot_rows(const float* lds_row, const float* f, f32x16 acc) {
+#pragma unroll
+  for (int s4 = 0; s4 < HALF; s4 += 4) {
+    const float4 a = *reinterpret_cast<const float4*>(lds_row + s4);
+    acc = mfma32(a.x, f[s4 + 0], acc);
+    acc = mfma32(a.y, f[s4 + 1], acc);
+    acc = mfma32(a.z, f[s4 + 2], acc);
+    acc = mfma32(a.w, f[s4 + 3], acc);
+  }
+  return acc;
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) z[r] = 0.f;
+  return z;
+}
+
+// ---------------------------------------------------------------------------
+// Forward (MODE 0) and attention-probability output (MODE 1, needs LSE).
+// ---------------------------------------------------------------------------
+template <int HDP, int MODE>
+__global__ __launch_bounds__(NT) void attn_fwd_kernel(const AttnArgs A) {
+  constexpr int KC = HDP == 32 ? 128 : 64;
+  constexpr int LS = HDP + 4;
+  constexpr int HALF = HDP / 2;
+  constexpr int NDT = HDP / 32;
+  __shared__ __attribute__((aligned(16))) float Ks[KC * LS];
+  __shared__ __attribute__((aligned(16))) float Vs[(MODE == 0 ? KC : 1) * LS];
+
+  const AttnPair& P = A.p[blockIdx.y];
+  const int qblocks = (P.Lq + 127) / 128;
+  int bid = blockIdx.x;
+  if (bid >= A.B * A.heads * qblocks) return;
+  const int qb = bid % qblocks;
+  bid /= qblocks;
+  const int head = bid % A.heads, b = bid / A.heads;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, c = lane & 31;
+  const int hd = A.hd, col0 = head * hd;
+  const int q = qb * 128 + w * 32 + c;
+  const bool qvalid = q < P.Lq;
+  const bool wave_active = qb * 128 + w * 32 < P.Lq;
+  const int64_t rowidx = ((int64_t)b * A.heads + head) * P.Lq + q;   // (b, head, q)
+  const int Lk = P.Lk;
+  const float scale = A.scale;
+  const float pdrop = A.drop_p;
+  const float inv_keep = pdrop < 1.f ? 1.f / (1.f - pdrop) : 0.f;
+  RngSnap rs{0, 0};
+  if (pdrop > 0.f && A.rng) rs = *A.rng;
+
+  // a fully masked sample (per-sample key mask == 0): P = 0, O = 0, LSE = -inf
+  if (P.kmask_mode == 1 && P.kmask[(int64_t)b * P.kmask_ld] == 0.f) {
+    if (MODE == 0) {
+      if (qvalid) {
+        float* orow = P.o + ((int64_t)b * P.Lq + q) * P.ldo + col0;
+        for (int d = h; d < hd; d += 2) orow[d] = 0.f;
+        if (h == 0) P.lse[rowidx] = -INFINITY;
+      }
+    } else if (qvalid) {
+      float* prow = P.probs + rowidx * Lk;
+      for (int k = h; k < Lk; k += 2) prow[k] = 0.f;
+    }
+    return;
+  }
+
+  const bool vq = (P.ldq % 4 == 0) && (hd % 4 == 0);
+  const bool vk = (P.ldk % 4 == 0) && (hd % 4 == 0);
+  const bool vv = (P.ldv % 4 == 0) && (hd % 4 == 0);
+  (void)vq;
+
+  float qf[HALF];
+  {
+    const float* qrow = P.q + ((int64_t)b * P.Lq + (qvalid ? q : 0)) * P.ldq + col0;
+    load_frag<HALF>(qf, qrow, h * HALF, hd, qvalid);
+  }
+  float m = -INFINITY, l = 0.f, lse = 0.f;
+  if (MODE == 1) lse = qvalid ? P.lse[rowidx] : -INFINITY;
+  f32x16 o[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) o[dt] = zero16();
+
+  const float* kbase_ptr = P.k + (int64_t)b * Lk * P.ldk + col0;
+  const float* vbase_ptr = P.v + (int64_t)b * Lk * P.ldv + col0;
+
+  for (int kbase = 0; kbase < Lk; kbase += KC) {
+    __syncthreads();
+    load_rows<KC, HDP, LS>(Ks, kbase_ptr, Lk, P.ldk, kbase, hd, vk);
+    if (MODE == 0) load_rows<KC, HDP, LS>(Vs, vbase_ptr, Lk, P.ldv, kbase, hd, vv);
+    __syncthreads();
+    if (!wave_active) continue;
+    const int nkt = (min(KC, Lk - kbase) + 31) / 32;
+    for (int kt = 0; kt < nkt; ++kt) {
+      f32x16 s = dot_rows<HALF>(Ks + (kt * 32 + c) * LS + h * HALF, qf, zero16());
+      float sv[16];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kbase + kt * 32 + acc_row(r, h);
+        const bool valid = key < Lk && (P.kmask_mode != 2 || kmask_val(P, b, key) != 0.f);
+        sv[r] = valid ? s[r] * scale : -INFINITY;
+        mx = fmaxf(mx, sv[r]);
+      }
+      if (MODE == 0) {
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        const float mnew = fmaxf(m, mx);
+        const float alpha = (m == -INFINITY) ? 0.f : __expf(m - mnew);
+        float ls = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          sv[r] = (sv[r] == -INFINITY) ? 0.f : __expf(sv[r] - mnew);
+          ls += sv[r];
+        }
+        ls += __shfl_xor(ls, 32);
+        l = l * alpha + ls;
+        m = mnew;
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          sv[r] = (sv[r] == -INFINITY || lse == -INFINITY) ? 0.f : __expf(sv[r] - lse);
+      }
+      if (pdrop > 0.f && qvalid) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int key0 = kbase + kt * 32 + 8 * g + 4 * h;
+          const uint32_t bits = keep4(rs, P.drop_site, (uint64_t)rowidx * Lk + key0, pdrop);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) sv[4 * g + j] = ((bits >> j) & 1u) ? sv[4 * g + j] * inv_keep : 0.f;
+        }
+      }
+      if (MODE == 0) {
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            o[dt] = mfma32(Vs[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], sv[r], o[dt]);
+        }
+      } else if (qvalid) {
+        float* prow = P.probs + rowidx * Lk;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kbase + kt * 32 + acc_row(r, h);
+          if (key < Lk) prow[key] = sv[r];
+        }
+      }
+    }
+  }
+  if (MODE == 1 || !qvalid) return;
+  const float inv_l = l > 0.f ? 1.f / l : 0.f;
+  float* orow = P.o + ((int64_t)b * P.Lq + q) * P.ldo + col0;
+  const bool vo = (P.ldo % 4 == 0) && (hd % 4 == 0);
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d0 = dt * 32 + 8 * g + 4 * h;
+      if (vo && d0 + 3 < hd) {
+        *reinterpret_cast<float4*>(orow + d0) =
+            make_float4(o[dt][4 * g] * inv_l, o[dt][4 * g + 1] * inv_l, o[dt][4 * g + 2] * inv_l,
+                        o[dt][4 * g + 3] * inv_l);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (d0 + j < hd) orow[d0 + j] = o[dt][4 * g + j] * inv_l;
+      }
+    }
+  if (h == 0) P.lse[rowidx] = l > 0.f ? m + __logf(l) : -INFINITY;
+}
+
+// D[b, head, q] = sum_d dO * O  (rowsum(P' . dP') of the softmax backward)
+__global__ __launch_bounds__(NT) void attn_bwd_prep_kernel(const AttnArgs A) {
+  const AttnPair& P = A.p[blockIdx.y];
+  const int64_t n = (int64_t)A.B * P.Lq * A.heads;
+  const int64_t idx = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (idx >= n) return;
+  const int head = (int)(idx % A.heads);
+  const int64_t bq = idx / A.heads;   // b*Lq + q
+  const int q = (int)(bq % P.Lq);
+  const int b = (int)(bq / P.Lq);
+  const float* dor = P.dout + bq * P.ldo + head * A.hd;
+  const float* orr = P.o + bq * P.ldo + head * A.hd;
+  float s = 0.f;
+  for (int d = 0; d < A.hd; ++d) s += dor[d] * orr[d];
+  P.dsum[((int64_t)b * A.heads + head) * P.Lq + q] = s;
+}
+
+// ---------------------------------------------------------------------------
+// dK / dV: one workgroup = 128 keys (4 waves x 32, key on the lane).
+// ---------------------------------------------------------------------------
+template <int HDP>
+__global__ __launch_bounds__(NT) void attn_bwd_dkv_kernel(const AttnArgs A) {
+  constexpr int QC = HDP == 32 ? 128 : 64;
+  constexpr int LS = HDP + 4;
+  constexpr int HALF = HDP / 2;
+  constexpr int NDT = HDP / 32;
+  __shared__ __attribute__((aligned(16))) float Qs[QC * LS];
+  __shared__ __attribute__((aligned(16))) float Ds[QC * LS];   // dO chunk
+  __shared__ float lse_s[QC];
+  __shared__ float dsum_s[QC];
+
+  const AttnPair& P = A.p[blockIdx.y];
+  const int kblocks = (P.Lk + 127) / 128;
+  int bid = blockIdx.x;
+  if (bid >= A.B * A.heads * kblocks) return;
+  const int kb = bid % kblocks;
+  bid /= kblocks;
+  const int head = bid % A.heads, b = bid / A.heads;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, c = lane & 31;
+  const int hd = A.hd, col0 = head * hd;
+  const int Lq = P.Lq, Lk = P.Lk;
+  const int key = kb * 128 + w * 32 + c;
+  const bool wave_active = kb * 128 + w * 32 < Lk;
+  bool kvalid = key < Lk;
+  if (kvalid && P.kmask_mode == 2) kvalid = kmask_val(P, b, key) != 0.f;
+  const float scale = A.scale;
+  const float pdrop = A.drop_p;
+  const float inv_keep = pdrop < 1.f ? 1.f / (1.f - pdrop) : 0.f;
+  RngSnap rs{0, 0};
+  if (pdrop > 0.f && A.rng) rs = *A.rng;
+
+  f32x16 dk[NDT], dv[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) { dk[dt] = zero16(); dv[dt] = zero16(); }
+
+  const bool sample_masked = (P.kmask_mode == 1 && P.kmask[(int64_t)b * P.kmask_ld] == 0.f);
+  if (!sample_masked) {
+    float kf[HALF], vf[HALF];
+    {
+      const int kr = key < Lk ? key : 0;
+      load_frag<HALF>(kf, P.k + ((int64_t)b * Lk + kr) * P.ldk + col0, h * HALF, hd, key < Lk);
+      load_frag<HALF>(vf, P.v + ((int64_t)b * Lk + kr) * P.ldv + col0, h * HALF, hd, key < Lk);
+    }
+    const bool vq = (P.ldq % 4 == 0) && (hd % 4 == 0);
+    const bool vo = (P.ldo % 4 == 0) && (hd % 4 == 0);
+    const float* qbase_ptr = P.q + (int64_t)b * Lq * P.ldq + col0;
+    const float* dobase_ptr = P.dout + (int64_t)b * Lq * P.ldo + col0;
+    const float* lse_ptr = P.lse + ((int64_t)b * A.heads + head) * Lq;
+    const float* ds_ptr = P.dsum + ((int64_t)b * A.heads + head) * Lq;
+    for (int qbase = 0; qbase < Lq; qbase += QC) {
+      __syncthreads();
+      load_rows<QC, HDP, LS>(Qs, qbase_ptr, Lq, P.ldq, qbase, hd, vq);
+      load_rows<QC, HDP, LS>(Ds, dobase_ptr, Lq, P.ldo, qbase, hd, vo);
+      for (int i = t; i < QC; i += NT) {
+        const int qq = qbase + i;
+        lse_s[i] = qq < Lq ? lse_ptr[qq] : -INFINITY;
+        dsum_s[i] = qq < Lq ? ds_ptr[qq] : 0.f;
+      }
+      __syncthreads();
+      if (!wave_active) continue;
+      const int nqt = (min(QC, Lq - qbase) + 31) / 32;
+      for (int qt = 0; qt < nqt; ++qt) {
+        f32x16 s = dot_rows<HALF>(Qs + (qt * 32 + c) * LS + h * HALF, kf, zero16());
+        f32x16 dp = dot_rows<HALF>(Ds + (qt * 32 + c) * LS + h * HALF, vf, zero16());
+        float pd[16], dsr[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ql = qt * 32 + acc_row(r, h);
+          const float lq = lse_s[ql];
+          const bool valid = kvalid && (lq != -INFINITY) && (qbase + ql < Lq);
+          const float pr = valid ? __expf(s[r] * scale - lq) : 0.f;
+          float pkeep = pr, dpk = dp[r];
+          if (pdrop > 0.f) {
+            const bool keep =
+                valid && keep1(rs, P.drop_site,
+                               (uint64_t)(((int64_t)b * A.heads + head) * Lq + qbase + ql) * Lk + key, pdrop);
+            pkeep = keep ? pr * inv_keep : 0.f;
+            dpk = keep ? dp[r] * inv_keep : 0.f;
+          }
+          pd[r] = pkeep;
+          dsr[r] = pr * (dpk - dsum_s[ql]);
+        }
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = (qt * 32 + acc_row(r, h)) * LS + dt * 32 + c;
+            dv[dt] = mfma32(pd[r], Ds[row], dv[dt]);
+            dk[dt] = mfma32(dsr[r], Qs[row], dk[dt]);
+          }
+        }
+      }
+    }
+  }
+  if (!wave_active) return;
+  // C[i = key (regs)][j = d (lane)]
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) {
+    const int d = dt * 32 + c;
+    if (d >= hd) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int kr = kb * 128 + w * 32 + acc_row(r, h);
+      if (kr >= Lk) continue;
+      P.dk[((int64_t)b * Lk + kr) * P.ldk + col0 + d] = dk[dt][r] * scale;
+      P.dv[((int64_t)b * Lk + kr) * P.ldv + col0 + d] = dv[dt][r];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// dQ: one workgroup = 128 queries (query on the lane, like the forward).
+// ---------------------------------------------------------------------------
+template <int HDP>
+__global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(const AttnArgs A) {
+  constexpr int KC = HDP == 32 ? 128 : 64;
+  constexpr int LS = HDP + 4;
+  constexpr int HALF = HDP / 2;
+  constexpr int NDT = HDP / 32;
+  __shared__ __attribute__((aligned(16))) float Ks[KC * LS];
+  __shared__ __attribute__((aligned(16))) float Vs[KC * LS];
+
+  const AttnPair& P = A.p[blockIdx.y];
+  const int qblocks = (P.Lq + 127) / 128;
+  int bid = blockIdx.x;
+  if (bid >= A.B * A.heads * qblocks) return;
+  const int qb = bid % qblocks;
+  bid /= qblocks;
+  const int head = bid % A.heads, b = bid / A.heads;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, c = lane & 31;
+  const int hd = A.hd, col0 = head * hd;
+  const int Lq = P.Lq, Lk = P.Lk;
+  const int q = qb * 128 + w * 32 + c;
+  const bool qvalid = q < Lq;
+  const bool wave_active = qb * 128 + w * 32 < Lq;
+  const int64_t rowidx = ((int64_t)b * A.heads + head) * Lq + q;
+  const float scale = A.scale;
+  const float pdrop = A.drop_p;
+  const float inv_keep = pdrop < 1.f ? 1.f / (1.f - pdrop) : 0.f;
+  RngSnap rs{0, 0};
+  if (pdrop > 0.f && A.rng) rs = *A.rng;
+
+  f32x16 dq[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) dq[dt] = zero16();
+
+  const bool sample_masked = (P.kmask_mode == 1 && P.kmask[(int64_t)b * P.kmask_ld] == 0.f);
+  const float lse = qvalid ? P.lse[rowidx] : -INFINITY;
+  if (!sample_masked) {
+    float qf[HALF], df[HALF];
+    const int qr = qvalid ? q : 0;
+    load_frag<HALF>(qf, P.q + ((int64_t)b * Lq + qr) * P.ldq + col0, h * HALF, hd, qvalid);
+    load_frag<HALF>(df, P.dout + ((int64_t)b * Lq + qr) * P.ldo + col0, h * HALF, hd, qvalid);
+    const float dsum = qvalid ? P.dsum[rowidx] : 0.f;
+    const bool vk = (P.ldk % 4 == 0) && (hd % 4 == 0);
+    const bool vv = (P.ldv % 4 == 0) && (hd % 4 == 0);
+    const float* kbase_ptr = P.k + (int64_t)b * Lk * P.ldk + col0;
+    const float* vbase_ptr = P.v + (int64_t)b * Lk * P.ldv + col0;
+    for (int kbase = 0; kbase < Lk; kbase += KC) {
+      __syncthreads();
+      load_rows<KC, HDP, LS>(Ks, kbase_ptr, Lk, P.ldk, kbase, hd, vk);
+      load_rows<KC, HDP, LS>(Vs, vbase_ptr, Lk, P.ldv, kbase, hd, vv);
+      __syncthreads();
+      if (!wave_active) continue;
+      const int nkt = (min(KC, Lk - kbase) + 31) / 32;
+      for (int kt = 0; kt < nkt; ++kt) {
+        f32x16 s = dot_rows<HALF>(Ks + (kt * 32 + c) * LS + h * HALF, qf, zero16());
+        f32x16 dp = dot_rows<HALF>(Vs + (kt * 32 + c) * LS + h * HALF, df, zero16());
+        float dsr[16];
+        uint32_t bits[4] = {0xFu, 0xFu, 0xFu, 0xFu};
+        if (pdrop > 0.f && qvalid) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            bits[g] = keep4(rs, P.drop_site, (uint64_t)rowidx * Lk + kbase + kt * 32 + 8 * g + 4 * h, pdrop);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kbase + kt * 32 + acc_row(r, h);
+          const bool valid = qvalid && key < Lk && lse != -INFINITY &&
+                             (P.kmask_mode != 2 || kmask_val(P, b, key) != 0.f);
+          const float pr = valid ? __expf(s[r] * scale - lse) : 0.f;
+          float dpk = dp[r];
+          if (pdrop > 0.f) dpk = ((bits[r >> 2] >> (r & 3)) & 1u) ? dp[r] * inv_keep : 0.f;
+          dsr[r] = pr * (dpk - dsum);
+        }
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            dq[dt] = mfma32(Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], dsr[r], dq[dt]);
+        }
+      }
+    }
+  }
+  if (!qvalid) return;
+  float* qrow = P.dq + ((int64_t)b * Lq + q) * P.ldq + col0;
+  const bool vo = (P.ldq % 4 == 0) && (hd % 4 == 0);
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d0 = dt * 32 + 8 * g + 4 * h;
+      if (vo && d0 + 3 < hd) {
+        *reinterpret_cast<float4*>(qrow + d0) =
+            make_float4(dq[dt][4 * g] * scale, dq[dt][4 * g + 1] * scale, dq[dt][4 * g + 2] * scale,
+                        dq[dt][4 * g + 3] * scale);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (d0 + j < hd) qrow[d0 + j] = dq[dt][4 * g + j] * scale;
+      }
+    }
+}
+
+enum class Kind { Fwd, Probs, Prep, Dkv, Dq };
+
+hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, int heads, int hd,
+                          float scale, float drop_p, const RngSnap* rng, hipStream_t st) {
+  if (hd > 64) return hipErrorInvalidValue;
+  const bool small = hd <= 32;
+  int done = 0;
+  while (done < npairs) {
+    AttnArgs a;
+    memset(&a, 0, sizeof(a));
+    int n = 0;
+    int64_t maxblk = 0;
+    while (done < npairs && n < ATTN_MAX_PAIRS) {
+      a.p[n] = pairs[done++];
+      const AttnPair& P = a.p[n];
+      int64_t nb;
+      if (kind == Kind::Prep) nb = ((int64_t)B * P.Lq * heads + NT - 1) / NT;
+      else if (kind == Kind::Dkv) nb = (int64_t)B * heads * ((P.Lk + 127) / 128);
+      else nb = (int64_t)B * heads * ((P.Lq + 127) / 128);
+      if (nb > maxblk) maxblk = nb;
+      ++n;
+    }
+    a.npairs = n;
+    a.B = B;
+    a.heads = heads;
+    a.hd = hd;
+    a.scale = scale;
+    a.drop_p = drop_p;
+    a.rng = rng;
+    a.nblk = (int)maxblk;
+    if (maxblk <= 0) continue;
+    dim3 grid((unsigned)maxblk, n);
+    switch (kind) {
+      case Kind::Fwd:
+        if (small) hipLaunchKernelGGL((attn_fwd_kernel<32, 0>), grid, dim3(NT), 0, st, a);
+        else hipLaunchKernelGGL((attn_fwd_kernel<64, 0>), grid, dim3(NT), 0, st, a);
+        break;
+      case Kind::Probs:
+        if (small) hipLaunchKernelGGL((attn_fwd_kernel<32, 1>), grid, dim3(NT), 0, st, a);
+        else hipLaunchKernelGGL((attn_fwd_kernel<64, 1>), grid, dim3(NT), 0, st, a);
+        break;
+      case Kind::Prep:
+        hipLaunchKernelGGL(attn_bwd_prep_kernel, grid, dim3(NT), 0, st, a);
+        break;
+      case Kind::Dkv:
+        if (small) hipLaunchKernelGGL((attn_bwd_dkv_kernel<32>), grid, dim3(NT), 0, st, a);
+        else hipLaunchKernelGGL((attn_bwd_dkv_kernel<64>), grid, dim3(NT), 0, st, a);
+        break;
+      case Kind::Dq:
+        if (small) hipLaunchKernelGGL((attn_bwd_dq_kernel<32>), grid, dim3(NT), 0, st, a);
+        else hipLaunchKernelGGL((attn_bwd_dq_kernel<64>), grid, dim3(NT), 0, st, a);
+        break;
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace
+
+hipError_t launch_attn_fwd(const AttnPair* pairs, int npairs, int B, int heads, int hd, float scale,
+                           float drop_p, const RngSnap* rng, hipStream_t st) {
+  return launch_generic(Kind::Fwd, pairs, npairs, B, heads, hd, scale, drop_p, rng, st);
+}
+
+hipError_t launch_attn_probs(const AttnPair* pairs, int npairs, int B, int heads, int hd,
+                             float scale, float drop_p, const RngSnap* rng, hipStream_t st) {
+  return launch_generic(Kind::Probs, pairs, npairs, B, heads, hd, scale, drop_p, rng, st);
+}
+
+hipError_t launch_attn_bwd(const AttnPair* pairs, int npairs, int B, int heads, int hd, float scale,
+                           float drop_p, const RngSnap* rng, hipStream_t st) {
+  hipError_t e = launch_generic(Kind::Prep, pairs, npairs, B, heads, hd, scale, drop_p, rng, st);
+  if (e != hipSuccess) return e;
+  e = launch_generic(Kind::Dkv, pairs, npairs, B, heads, hd, scale, drop_p, rng, st);
+  if (e != hipSuccess) return e;
+  return launch_generic(Kind::Dq, pairs, npairs, B, heads, hd, scale, drop_p, rng, st);
+}
+
+}  // namespace mmf

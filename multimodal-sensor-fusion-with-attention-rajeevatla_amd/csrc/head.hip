@@ -1,0 +1,323 @@
+// Fusion head kernels: per-modality aggregation + L mean-pool, gating scores,
+// masked-softmax adaptive weights, weighted sum (forward) and their backward;
+// plus the small training-step kernels (RNG snapshot, cross-entropy with label
+// smoothing, AdamW).
+//
+// Reference: aggregation src/fusion.py:406-408; compute_adaptive_weights
+// src/fusion.py:429-479; fused representation src/fusion.py:413-418;
+// CrossEntropyLoss(label_smoothing) src/train.py:185-186,310.
+// One workgroup per sample: nothing here mixes samples, so the data-parallel
+// split over the batch needs no exchange.
+#include <cstring>
+
+#include "mmf_device.h"
+
+namespace mmf {
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int HEAD_MAX_H = 1024;
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Masked softmax over modalities + renormalisation / fallback, exactly as
+// src/fusion.py:462-478 (scores of mask<=0 modalities are -inf; an all -inf row
+// is NaN -> 0 -> fallback mask/(sum+1e-8) or uniform 1/M).
+// Returns sw (> 0 iff the softmax branch was taken) and fills sm (softmax after
+// nan_to_num), w (final weights).
+__device__ float adaptive_fwd(int M, const float* score, const float* mask, float* sm, float* w) {
+  float mx = -INFINITY;
+  for (int m = 0; m < M; ++m)
+    if (mask[m] > 0.f) mx = fmaxf(mx, score[m]);
+  float z = 0.f;
+  for (int m = 0; m < M; ++m) {
+    sm[m] = (mask[m] > 0.f) ? __expf(score[m] - mx) : 0.f;
+    z += sm[m];
+  }
+  float sw = 0.f, ms = 0.f;
+  for (int m = 0; m < M; ++m) {
+    sm[m] = (mx == -INFINITY) ? 0.f : sm[m] / z;   // nan_to_num of an all -inf row
+    w[m] = sm[m] * mask[m];
+    sw += w[m];
+    ms += mask[m];
+  }
+  if (sw > 0.f) {
+    const float den = sw + 1e-8f;
+    for (int m = 0; m < M; ++m) w[m] = w[m] / den;
+  } else {
+    for (int m = 0; m < M; ++m) w[m] = ms > 0.f ? mask[m] / (ms + 1e-8f) : 1.f / (float)M;
+  }
+  return sw;
+}
+
+__global__ __launch_bounds__(NT) void head_fwd_kernel(const HeadArgs a) {
+  __shared__ __attribute__((aligned(16))) float pooled_s[8 * HEAD_MAX_H];
+  __shared__ __attribute__((aligned(16))) float4 red4[NT];
+  __shared__ float score_s[8], w_s[8], part_s[4][8];
+  const int b = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int M = a.M, H = a.H;
+  const int NCG = H / 4;
+  const int RG = NT / NCG;   // host guarantees 4 <= H <= 1024, H % 4 == 0
+  const int cg = t % NCG, rg = t / NCG;
+  const bool active = rg < RG;
+
+  for (int m = 0; m < M; ++m) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (active) {
+      const int L = a.L[m];
+      for (int si = 0; si < a.nsrc; ++si) {
+        if (a.src_mod[si] != m) continue;
+        const float* base = a.src[si] + (int64_t)b * L * H + 4 * cg;
+        for (int r = rg; r < L; r += RG) {
+          const float4 v = *reinterpret_cast<const float4*>(base + (int64_t)r * H);
+          acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        }
+      }
+    }
+    red4[t] = acc;
+    __syncthreads();
+    if (t < NCG) {
+      float4 s = red4[t];
+      for (int g = 1; g < RG; ++g) {
+        const float4 v = red4[g * NCG + t];
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      }
+      const float f = a.inv_cnt[m] * (a.scale_by_mask ? a.mask[(int64_t)b * M + m] : 1.f);
+      *reinterpret_cast<float4*>(&pooled_s[m * H + 4 * t]) = make_float4(s.x * f, s.y * f, s.z * f, s.w * f);
+    }
+    __syncthreads();
+  }
+  // gating scores (nn.Linear(H, 1) per modality, src/fusion.py:316-321,452-461)
+  for (int m = wave; m < M; m += 4) {
+    float s = 0.f;
+    for (int j = lane; j < H; j += 64) s += pooled_s[m * H + j] * a.gate_w[m][j];
+    s = wave_sum(s);
+    if (lane == 0) score_s[m] = s + a.gate_b[m][0];
+  }
+  __syncthreads();
+  if (t == 0) {
+    float msk[8], sm[8], w[8];
+    for (int m = 0; m < M; ++m) msk[m] = a.mask[(int64_t)b * M + m];
+    adaptive_fwd(M, score_s, msk, sm, w);
+    for (int m = 0; m < M; ++m) {
+      w_s[m] = w[m];
+      a.scores[(int64_t)b * M + m] = score_s[m];
+      a.weights[(int64_t)b * M + m] = w[m];
+      if (a.weights_out) a.weights_out[(int64_t)b * M + m] = w[m];
+    }
+  }
+  __syncthreads();
+  (void)part_s;
+  for (int j = t; j < H; j += NT) {
+    float f = 0.f;
+    for (int m = 0; m < M; ++m) {
+      const float v = pooled_s[m * H + j];
+      f += v * w_s[m];
+      a.pooled[((int64_t)b * M + m) * H + j] = v;
+    }
+    a.fused[(int64_t)b * H + j] = f;
+  }
+}
+
+__global__ __launch_bounds__(NT) void head_bwd_kernel(const HeadArgs a) {
+  __shared__ float dw_s[8], dscore_s[8];
+  const int b = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int M = a.M, H = a.H;
+  const float* df = a.dfused + (int64_t)b * H;
+  const float* pooled = a.pooled + (int64_t)b * M * H;
+  // dL/dw_m = dfused . pooled_m   (fused = sum_m w_m pooled_m)
+  for (int m = wave; m < M; m += 4) {
+    float s = 0.f;
+    for (int j = lane; j < H; j += 64) s += df[j] * pooled[m * H + j];
+    s = wave_sum(s);
+    if (lane == 0) dw_s[m] = s;
+  }
+  __syncthreads();
+  if (t == 0) {
+    float msk[8], sc[8], sm[8], w[8];
+    for (int m = 0; m < M; ++m) {
+      msk[m] = a.mask[(int64_t)b * M + m];
+      sc[m] = a.scores[(int64_t)b * M + m];
+    }
+    const float sw = adaptive_fwd(M, sc, msk, sm, w);
+    float ds[8];
+    for (int m = 0; m < M; ++m) ds[m] = 0.f;
+    if (sw > 0.f) {
+      // w = wm / (sw + eps), wm = sm * mask  ->  d wm_i = dw_i/S - sum_j dw_j wm_j / S^2
+      const float S = sw + 1e-8f;
+      float dot = 0.f;
+      for (int m = 0; m < M; ++m) dot += dw_s[m] * sm[m] * msk[m];
+      float dsm[8], sdot = 0.f;
+      for (int m = 0; m < M; ++m) {
+        dsm[m] = (dw_s[m] / S - dot / (S * S)) * msk[m];
+        sdot += sm[m] * dsm[m];
+      }
+      // softmax backward; masked_fill(mask<=0) zeroes the masked entries
+      for (int m = 0; m < M; ++m) ds[m] = msk[m] > 0.f ? sm[m] * (dsm[m] - sdot) : 0.f;
+    }
+    for (int m = 0; m < M; ++m) {
+      dscore_s[m] = ds[m];
+      a.dscore[(int64_t)b * M + m] = ds[m];
+    }
+  }
+  __syncthreads();
+  for (int m = 0; m < M; ++m) {
+    const float wm = a.weights[(int64_t)b * M + m];
+    const float f = a.mask[(int64_t)b * M + m] * a.inv_cnt[m];
+    const float dsm = dscore_s[m];
+    const float* gw = a.gate_w[m];
+    for (int j = t; j < H; j += NT) {
+      const float dp = wm * df[j] + dsm * gw[j];
+      a.cvec[((int64_t)b * M + m) * H + j] = dp * f;
+    }
+  }
+}
+
+struct GateWArgs {
+  int32_t B, M, H;
+  const float* dscore; const float* pooled;
+  float* dgw[8]; float* dgb[8];
+};
+
+__global__ __launch_bounds__(NT) void gate_wgrad_kernel(const GateWArgs a) {
+  const int idx = blockIdx.x * NT + threadIdx.x;
+  const int per = a.H + 1;
+  if (idx >= a.M * per) return;
+  const int m = idx / per, j = idx % per;
+  float s = 0.f;
+  if (j < a.H) {
+    for (int b = 0; b < a.B; ++b)
+      s += a.dscore[(int64_t)b * a.M + m] * a.pooled[((int64_t)b * a.M + m) * a.H + j];
+    a.dgw[m][j] = s;
+  } else {
+    for (int b = 0; b < a.B; ++b) s += a.dscore[(int64_t)b * a.M + m];
+    a.dgb[m][0] = s;
+  }
+}
+
+__global__ void rng_snapshot_kernel(uint64_t* state, RngSnap* snap) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    snap->seed = state[0];
+    snap->offset = state[1];
+    state[1] = state[1] + 1;
+  }
+}
+
+// nn.CrossEntropyLoss(label_smoothing=eps), reduction='mean':
+// loss_i = -(1-eps) log p_{y_i} - eps/C sum_c log p_c ; dlogits = (p - ((1-eps) onehot + eps/C)) / B
+__global__ __launch_bounds__(NT) void cross_entropy_kernel(int B, int C, const float* logits,
+                                                           const int64_t* labels, float eps,
+                                                           float gscale, float* loss, float* dlogits) {
+  __shared__ float red[NT];
+  const int t = threadIdx.x;
+  float acc = 0.f;
+  for (int i = t; i < B; i += NT) {
+    const float* z = logits + (int64_t)i * C;
+    float mx = -INFINITY;
+    for (int c = 0; c < C; ++c) mx = fmaxf(mx, z[c]);
+    float se = 0.f, sz = 0.f;
+    for (int c = 0; c < C; ++c) { se += __expf(z[c] - mx); sz += z[c]; }
+    const float lse = mx + __logf(se);
+    const int y = (int)labels[i];
+    acc += (1.f - eps) * (lse - z[y]) + eps * (lse - sz / (float)C);
+    float* d = dlogits + (int64_t)i * C;
+    for (int c = 0; c < C; ++c) {
+      const float pc = __expf(z[c] - lse);
+      const float tgt = (c == y ? (1.f - eps) : 0.f) + eps / (float)C;
+      d[c] = (pc - tgt) / (float)B * gscale;
+    }
+  }
+  red[t] = acc;
+  __syncthreads();
+  for (int s = NT / 2; s > 0; s >>= 1) {
+    if (t < s) red[t] += red[t + s];
+    __syncthreads();
+  }
+  if (t == 0) loss[0] = red[0] / (float)B;
+}
+
+// torch.optim.AdamW (amsgrad=False, maximize=False): decoupled weight decay.
+__global__ __launch_bounds__(NT) void adamw_kernel(int64_t n, float* __restrict__ p,
+                                                   const float* __restrict__ g, float* __restrict__ m,
+                                                   float* __restrict__ v, const int64_t* step, float lr,
+                                                   float b1, float b2, float eps, float wd, float gscale) {
+  const double st = (double)(*step + 1);
+  const float bc1 = (float)(1.0 - pow((double)b1, st));
+  const float bc2s = (float)sqrt(1.0 - pow((double)b2, st));
+  const float step_size = lr / bc1;
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+    const float gi = g[i] * gscale;
+    float pi = p[i] * (1.f - lr * wd);
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    pi -= step_size * mi / (sqrtf(vi) / bc2s + eps);
+    p[i] = pi;
+  }
+}
+
+__global__ void step_incr_kernel(int64_t* step) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) *step = *step + 1;
+}
+
+}  // namespace
+
+hipError_t launch_head_fwd(const HeadArgs& a, hipStream_t st) {
+  if (a.H % 4 != 0 || a.H > HEAD_MAX_H || a.H < 4 || a.M > 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(head_fwd_kernel, dim3(a.B), dim3(NT), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_head_bwd(const HeadArgs& a, hipStream_t st) {
+  if (a.M > 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(head_bwd_kernel, dim3(a.B), dim3(NT), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_gate_wgrad(int B, int M, int H, const float* dscore, const float* pooled,
+                             float* const* dgw, float* const* dgb, hipStream_t st) {
+  GateWArgs a;
+  memset(&a, 0, sizeof(a));
+  a.B = B; a.M = M; a.H = H; a.dscore = dscore; a.pooled = pooled;
+  for (int m = 0; m < M; ++m) { a.dgw[m] = dgw[m]; a.dgb[m] = dgb[m]; }
+  const int n = M * (H + 1);
+  hipLaunchKernelGGL(gate_wgrad_kernel, dim3((n + NT - 1) / NT), dim3(NT), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_rng_snapshot(const uint64_t* state, RngSnap* snap, hipStream_t st) {
+  hipLaunchKernelGGL(rng_snapshot_kernel, dim3(1), dim3(64), 0, st, const_cast<uint64_t*>(state), snap);
+  return hipGetLastError();
+}
+
+hipError_t launch_cross_entropy(int B, int C, const float* logits, const int64_t* labels,
+                                float smoothing, float grad_scale, float* loss, float* dlogits,
+                                hipStream_t st) {
+  hipLaunchKernelGGL(cross_entropy_kernel, dim3(1), dim3(NT), 0, st, B, C, logits, labels, smoothing,
+                     grad_scale, loss, dlogits);
+  return hipGetLastError();
+}
+
+hipError_t launch_adamw(int64_t n, float* p, const float* g, float* m, float* v, int64_t* step,
+                        float lr, float b1, float b2, float eps, float wd, float gscale,
+                        hipStream_t st) {
+  int64_t blocks = (n + NT - 1) / NT;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(NT), 0, st, n, p, g, m, v, step, lr, b1,
+                     b2, eps, wd, gscale);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(step_incr_kernel, dim3(1), dim3(64), 0, st, step);
+  return hipGetLastError();
+}
+
+}  // namespace mmf

@@ -1,0 +1,190 @@
+// Internal kernel interfaces for libmmfusion (gfx950 / CDNA4 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+namespace mmf {
+
+// ---------------------------------------------------------------------------
+// Dropout RNG: Philox4x32-10 keyed by the per-call snapshot {seed, offset};
+// counter = (idx>>2 lo, idx>>2 hi, site, offset).  One call yields the keep
+// decisions of 4 consecutive elements of one tensor ("site").
+// ---------------------------------------------------------------------------
+struct RngSnap { uint64_t seed; uint64_t offset; };
+
+enum : uint32_t {
+  SITE_IN = 0x100,     // + m : input dropout on X_m*mask  (src/fusion.py:373)
+  SITE_PROJ = 0x200,   // + m : projections[m] Dropout     (src/fusion.py:291-298)
+  SITE_ATTN = 0x300,   // + p : attention-prob Dropout     (src/attention.py:130)
+  SITE_CLS = 0x400,    //       classifier Dropout          (src/fusion.py:326)
+};
+
+// ---------------------------------------------------------------------------
+// Grouped fp32 GEMM on v_mfma_f32_32x32x2_f32:  C[M,N] = sum_src A_src[M,K] B_src[K,N]
+// Operand storage modes (logical A[i][kk], B[kk][j]):
+//   A_RK: stored [i][kk] (kk contiguous)      A_KR: stored [kk][i] (i contiguous)
+//   B_NK: stored [j][kk] (kk contiguous)      B_KN: stored [kk][j] (j contiguous)
+// "stored row" index is divided by row_div (row broadcast, e.g. dA = c[b]).
+// ---------------------------------------------------------------------------
+enum { MODE_RK = 0, MODE_KR = 1 };  // for B: RK == NK (stored [j][kk]), KR == KN
+
+struct Xform {               // optional prologue on a stored element (row r, col c)
+  const float* rowscale;     // v *= rowscale[(r / rs_div) * rs_stride + rs_off]
+  int32_t rs_div, rs_stride, rs_off;
+  uint32_t drop_site;        // 0 = none; keep(site, r * ncols + c) ? v/(1-p) : 0
+  int32_t ncols;
+  int32_t pad_;
+};
+
+struct Operand {
+  const float* ptr;
+  int32_t ld;                // stored row stride (elements)
+  int32_t row_div;           // >= 1
+  int32_t vec;               // 1 => 16-byte aligned rows, float4 loads allowed
+  int32_t xf;                // -1 none, else index into GemmArgs::xf
+};
+
+struct GemmSrc {
+  Operand a, b;
+  int32_t K;                 // contraction length
+  int32_t pad_;
+};
+
+enum : int32_t {
+  EPI_BIAS = 1, EPI_RELU = 2, EPI_DROP = 4, EPI_ROWADD = 8, EPI_GATE = 16,
+  EPI_ROWSCALE = 32, EPI_PARTIAL = 64
+};
+
+struct GemmGroup {
+  int32_t M, N;
+  int32_t src_begin, src_count;
+  float* C; int32_t ldc;
+  int32_t epi;
+  const float* bias;                                   // EPI_BIAS
+  const float* rowadd; int32_t ld_rowadd, rowadd_div;  // EPI_ROWADD: += rowadd[(i/div)*ld + j]
+  const float* gate; int32_t ld_gate; float gate_scale;// EPI_GATE: gate[i][j] > 0 ? v*scale : 0
+  const float* rowscale; int32_t rs_div, rs_stride;    // EPI_ROWSCALE: v *= rowscale[(i/div)*stride + off]
+  int32_t rs_off;
+  uint32_t drop_site;                                  // EPI_DROP: idx = i*N + j
+  // EPI_PARTIAL (split-K over the contraction): C := part[split][M][N] (ldc = N),
+  // part_db[split][M] = row sums of A over the split (bias grad of a TN dW).
+  int32_t nsplit, kchunk;
+  float* part_db;
+};
+
+constexpr int GEMM_MAX_GROUPS = 8;
+constexpr int GEMM_MAX_SRCS = 24;
+constexpr int GEMM_MAX_XF = 8;
+
+struct GemmArgs {
+  GemmGroup g[GEMM_MAX_GROUPS];
+  GemmSrc s[GEMM_MAX_SRCS];
+  Xform xf[GEMM_MAX_XF];
+  int32_t ngroups;
+  int32_t amode, bmode;
+  float drop_p;              // p of every dropout site in this launch
+  const RngSnap* rng;
+};
+
+// Host-side description of one output (group) and its sources; launch_gemm
+// packs as many jobs per launch as the kernel-argument tables allow.
+struct GemmJob {
+  GemmGroup g;
+  GemmSrc src[GEMM_MAX_SRCS];
+  int has_xf_a[GEMM_MAX_SRCS];
+  int has_xf_b[GEMM_MAX_SRCS];
+  Xform xf_a[GEMM_MAX_SRCS];
+  Xform xf_b[GEMM_MAX_SRCS];
+  int nsrc;
+};
+
+hipError_t launch_gemm(const GemmJob* jobs, int njobs, int amode, int bmode, float drop_p,
+                       const RngSnap* rng, hipStream_t st);
+
+// Split-K partial-slab reduction: out[e] = sum_s part[s][e]; db[i] = sum_s part_db[s][i].
+struct ReduceJob {
+  const float* part; const float* part_db;
+  float* out; float* db;
+  int32_t nsplit, M, N;
+};
+hipError_t launch_reduce(const ReduceJob* jobs, int njobs, hipStream_t st);
+
+// ---------------------------------------------------------------------------
+// Attention (per pair, per sample, per head), flash-style, fp32 MFMA.
+// Q (B, Lq, ld), K/V (B, Lk, ld), O (B, Lq, ld); head h uses cols [h*hd, h*hd+hd).
+// ---------------------------------------------------------------------------
+struct AttnPair {
+  const float* q; const float* k; const float* v;
+  float* o;            // fwd output
+  float* lse;          // (B, heads, Lq) fwd output / bwd input
+  const float* kmask; int32_t kmask_mode; int32_t kmask_ld;   // 0 none, 1 per-sample, 2 per-key
+  int32_t Lq, Lk;
+  int32_t ldq, ldk, ldv, ldo;
+  uint32_t drop_site;
+  // backward
+  const float* dout;   // dO (B, Lq, ldo)
+  float* dsum;         // D = rowsum(dO*O) (B, heads, Lq)
+  float* dq; float* dk; float* dv;   // (B, L, ld*)
+  float* probs;        // (B, heads, Lq, Lk) output of attn_probs
+};
+
+constexpr int ATTN_MAX_PAIRS = 12;
+
+struct AttnArgs {
+  AttnPair p[ATTN_MAX_PAIRS];
+  int32_t npairs;
+  int32_t B, heads, hd;
+  float scale, drop_p;
+  int32_t nblk;        // blocks along the L axis (max over pairs) for this launch
+  const RngSnap* rng;
+};
+
+hipError_t launch_attn_fwd(const AttnPair* pairs, int npairs, int B, int heads, int hd, float scale,
+                           float drop_p, const RngSnap* rng, hipStream_t st);
+hipError_t launch_attn_probs(const AttnPair* pairs, int npairs, int B, int heads, int hd,
+                             float scale, float drop_p, const RngSnap* rng, hipStream_t st);
+hipError_t launch_attn_bwd(const AttnPair* pairs, int npairs, int B, int heads, int hd, float scale,
+                           float drop_p, const RngSnap* rng, hipStream_t st);
+
+// ---------------------------------------------------------------------------
+// Fusion head: pooling + gating + adaptive weights + weighted sum, and backward.
+// ---------------------------------------------------------------------------
+constexpr int HEAD_MAX_SRC = 64;
+struct HeadArgs {
+  int32_t B, M, H;
+  const float* mask;                     // (B, M)
+  int32_t scale_by_mask;                 // agg *= mask (src/fusion.py:408); 0 for compute_adaptive_weights
+  // per modality: list of (B, L_m, H) tensors whose L-mean is summed
+  const float* src[HEAD_MAX_SRC];
+  int32_t src_mod[HEAD_MAX_SRC];
+  int32_t nsrc;
+  int32_t L[8];
+  float inv_cnt[8];                      // 1 / (n_entries_m * L_m)
+  const float* gate_w[8]; const float* gate_b[8];
+  float* pooled;                         // (B, M, H)
+  float* scores;                         // (B, M)
+  float* weights;                        // (B, M)
+  float* fused;                          // (B, H)
+  float* weights_out;                    // optional copy (B, M)
+  // backward
+  const float* dfused;                   // (B, H)
+  float* cvec;                           // (B, M, H) per-row grad of every list entry of m
+  float* dscore;                         // (B, M)
+};
+hipError_t launch_head_fwd(const HeadArgs& a, hipStream_t st);
+hipError_t launch_head_bwd(const HeadArgs& a, hipStream_t st);
+// dgw[m][j] = sum_b dscore[b][m] * pooled[b][m][j]; dgb[m] = sum_b dscore[b][m]
+hipError_t launch_gate_wgrad(int B, int M, int H, const float* dscore, const float* pooled,
+                             float* const* dgw, float* const* dgb, hipStream_t st);
+
+hipError_t launch_rng_snapshot(const uint64_t* state, RngSnap* snap, hipStream_t st);
+hipError_t launch_cross_entropy(int B, int C, const float* logits, const int64_t* labels,
+                                float smoothing, float grad_scale, float* loss, float* dlogits,
+                                hipStream_t st);
+hipError_t launch_adamw(int64_t n, float* p, const float* g, float* m, float* v, int64_t* step,
+                        float lr, float b1, float b2, float eps, float wd, float gscale,
+                        hipStream_t st);
+
+}  // namespace mmf

@@ -1,0 +1,400 @@
+"""Drop-in `fusion` module: HybridFusion on MI355X HIP kernels.
+
+Mirrors src/fusion.py of the reference so `from fusion import HybridFusion,
+build_fusion_model` (src/train.py:25) resolves here unchanged:
+
+  * HybridFusion(modality_dims, hidden_dim=256, num_classes=11, num_heads=4,
+    dropout=0.1) with the reference's attributes and state_dict keys
+    (projections.{m}.0.*, attention_modules.{q}_to_{k}.{query,key,value,out}_proj.*,
+    gating_layers.{m}.*, classifier.{0,3}.*), src/fusion.py:248-329;
+  * forward(modality_features, modality_mask=None, return_attention=False)
+    -> logits | (logits, {"attention_maps", "fusion_weights"}), src/fusion.py:331-427,
+    with the reference's errors raised before any kernel launch;
+  * compute_adaptive_weights(features, mask), src/fusion.py:429-479;
+  * build_fusion_model(fusion_type, modality_dims, num_classes, **kw), src/fusion.py:485-515.
+
+The whole fused step (projections, pairwise Q/K/V, QK^T softmax attn.V,
+out_proj, aggregation, gating softmax, weighted sum, classifier) runs as HIP
+kernels through include/mmfusion.h (mmf_hybrid_forward / mmf_hybrid_backward);
+inputs may be 2-D (B, D_m) (reference semantics) or 3-D (B, L_m, D_m)
+(sequence mode: each modality's aggregate is mean-pooled over L_m before the
+weighting; identical to the reference at L = 1).  No CPU path exists: CPU
+tensors raise.  EarlyFusion / LateFusion are plain-PyTorch plumbing kept only
+so the import surface matches (they are not on the accelerated path).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import sys
+from typing import Any, Dict, List, Optional, Tuple, cast
+
+import torch
+import torch.nn as nn
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+if _HERE not in sys.path:
+    sys.path.insert(0, _HERE)
+
+import mmf_native as _nat  # noqa: E402
+from attention import CrossModalAttention, _new_rng_state  # noqa: E402
+
+
+# --------------------------------------------------------------------------
+# Out-of-scope plumbing (not accelerated): Early / Late fusion restated in torch.
+# --------------------------------------------------------------------------
+def _mask_or_ones(features, names, mask):
+    first = features[names[0]]
+    if mask is None:
+        return torch.ones(first.size(0), len(names), device=first.device, dtype=first.dtype)
+    return mask.to(device=first.device, dtype=first.dtype)
+
+
+class EarlyFusion(nn.Module):
+    """Concatenate masked encoder outputs, then an MLP (src/fusion.py:17-123)."""
+
+    def __init__(self, modality_dims: Dict[str, int], hidden_dim: int = 256, num_classes: int = 11,
+                 dropout: float = 0.1):
+        super().__init__()
+        dims = dict(modality_dims)
+        cast_self = cast(Any, self)
+        cast_self.modality_names = list(dims)
+        cast_self.modality_dims = dims
+        cast_self.num_classes = num_classes
+        cast_self.hidden_dim = hidden_dim
+        width = sum(dims.values())
+        if width == 0:
+            self.fusion = nn.Identity()
+        else:
+            self.fusion = nn.Sequential(
+                nn.Linear(width, hidden_dim), nn.ReLU(), nn.Dropout(dropout),
+                nn.Linear(hidden_dim, hidden_dim), nn.ReLU(), nn.Dropout(dropout),
+                nn.Linear(hidden_dim, num_classes))
+
+    def forward(self, modality_features, modality_mask=None):
+        if not self.modality_names:
+            raise ValueError("No modalities configured for EarlyFusion.")
+        mask = _mask_or_ones(modality_features, self.modality_names, modality_mask)
+        parts = []
+        for i, name in enumerate(self.modality_names):
+            if name not in modality_features:
+                raise KeyError(f"Missing features for modality '{name}' in EarlyFusion forward pass.")
+            x = modality_features[name]
+            if x.dim() != 2:
+                raise ValueError(f"Expected 2D tensor for modality '{name}', got shape {x.shape}.")
+            parts.append(x.to(mask.device) * mask[:, i:i + 1])
+        return self.fusion(torch.cat(parts, dim=1))
+
+
+class LateFusion(nn.Module):
+    """Per-modality classifiers, softmax(learned logits) x mask weighting (src/fusion.py:126-245)."""
+
+    def __init__(self, modality_dims: Dict[str, int], hidden_dim: int = 256, num_classes: int = 11,
+                 dropout: float = 0.1):
+        super().__init__()
+        dims = dict(modality_dims)
+        cast_self = cast(Any, self)
+        cast_self.modality_names = list(dims)
+        cast_self.num_modalities = len(dims)
+        cast_self.modality_dims = dims
+        self.classifiers = nn.ModuleDict({
+            name: nn.Sequential(nn.Linear(d, hidden_dim), nn.ReLU(), nn.Dropout(dropout),
+                                nn.Linear(hidden_dim, num_classes))
+            for name, d in dims.items()})
+        self.weight_logits = nn.Parameter(torch.zeros(self.num_modalities))
+        self.dropout = nn.Dropout(dropout)
+
+    def forward(self, modality_features, modality_mask=None):
+        if not self.modality_names:
+            raise ValueError("No modalities configured for LateFusion.")
+        mask = _mask_or_ones(modality_features, self.modality_names, modality_mask)
+        per: Dict[str, torch.Tensor] = {}
+        for i, name in enumerate(self.modality_names):
+            if name not in modality_features:
+                raise KeyError(f"Missing features for modality '{name}' in LateFusion forward pass.")
+            x = modality_features[name].to(mask.device) * mask[:, i:i + 1]
+            per[name] = self.classifiers[name](self.dropout(x))
+        stacked = torch.stack([per[n] for n in self.modality_names], dim=1)
+        w = torch.softmax(self.weight_logits, dim=0).unsqueeze(0) * mask
+        s = w.sum(dim=1, keepdim=True)
+        w = torch.where(s > 0, w / (s + 1e-8), torch.full_like(w, 1.0 / self.num_modalities))
+        return (stacked * w.unsqueeze(-1)).sum(dim=1), per
+
+
+# --------------------------------------------------------------------------
+# HybridFusion: the accelerated hot path
+# --------------------------------------------------------------------------
+class _HybridFunction(torch.autograd.Function):
+    """Autograd node over mmf_hybrid_forward / mmf_hybrid_backward.
+
+    tensors = (mask, x_0..x_{M-1}, params...) in the plan's parameter order.
+    Outputs: logits (differentiable), fusion_weights and attention maps
+    (returned for inspection, not differentiable).
+    """
+
+    @staticmethod
+    def forward(ctx, plan: "_Plan", rng, mask, *tensors):
+        L = _nat.lib()
+        M = plan.desc.num_modalities
+        xs = tensors[:M]
+        params = tensors[M:]
+        dev = mask.device
+        d = plan.desc
+        saved = torch.empty(L.mmf_hybrid_saved_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
+        logits = torch.empty(d.batch, d.num_classes, dtype=torch.float32, device=dev)
+        fw = torch.empty(d.batch, M, dtype=torch.float32, device=dev)
+        maps: List[torch.Tensor] = []
+        if d.return_attention:
+            for g in range(d.num_pairs):
+                lq = plan.seq[d.pair_q[g]]
+                lk = plan.seq[d.pair_k[g]]
+                maps.append(torch.empty(d.batch, d.num_heads, lq, lk, dtype=torch.float32, device=dev))
+        pstruct = plan.param_struct(params)
+        xarr = _nat.ptr_array([x.data_ptr() for x in xs])
+        marr = _nat.ptr_array([t.data_ptr() for t in maps]) if maps else None
+        rc = L.mmf_hybrid_forward(ctypes.byref(d), ctypes.byref(pstruct), ctypes.cast(xarr, ctypes.c_void_p),
+                                  mask.data_ptr(), rng.data_ptr(), saved.data_ptr(), logits.data_ptr(),
+                                  fw.data_ptr(), ctypes.cast(marr, ctypes.c_void_p) if marr else None,
+                                  _nat.stream_ptr(dev))
+        _nat.check(rc, "HybridFusion forward")
+        ctx.plan = plan
+        ctx.saved_buf = saved
+        ctx.save_for_backward(mask, *xs, *params)
+        ctx.mark_non_differentiable(fw, *maps)
+        return (logits, fw, *maps)
+
+    @staticmethod
+    def backward(ctx, dlogits, *_unused):
+        L = _nat.lib()
+        plan: _Plan = ctx.plan
+        d = plan.desc
+        M = d.num_modalities
+        mask, *rest = ctx.saved_tensors
+        xs, params = rest[:M], rest[M:]
+        dev = mask.device
+        dlogits = _nat.f32c(dlogits)
+        ws = torch.empty(L.mmf_hybrid_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
+        flat = torch.empty(plan.num_param_elems, dtype=torch.float32, device=dev)
+        gviews = plan.grad_views(flat, params)
+        gstruct = plan.param_struct(gviews)
+        pstruct = plan.param_struct(params)
+        needs = ctx.needs_input_grad[3:3 + M]
+        dxs = [torch.empty_like(x) if need else None for x, need in zip(xs, needs)]
+        xarr = _nat.ptr_array([x.data_ptr() for x in xs])
+        dxarr = _nat.ptr_array([t.data_ptr() if t is not None else None for t in dxs])
+        rc = L.mmf_hybrid_backward(ctypes.byref(d), ctypes.byref(pstruct), ctypes.cast(xarr, ctypes.c_void_p),
+                                   mask.data_ptr(), ctx.saved_buf.data_ptr(), dlogits.data_ptr(),
+                                   ws.data_ptr(), ctypes.byref(gstruct), ctypes.cast(dxarr, ctypes.c_void_p),
+                                   _nat.stream_ptr(dev))
+        _nat.check(rc, "HybridFusion backward")
+        return (None, None, None, *dxs, *gviews)
+
+
+class _Plan:
+    """Shape/pair descriptor + parameter ordering for one forward call."""
+
+    def __init__(self, model: "HybridFusion", seq: List[int], dims: List[int], batch: int,
+                 pairs: List[Tuple[int, int, str]], return_attention: bool):
+        d = _nat.HybridDesc()
+        d.batch = batch
+        d.num_modalities = model.num_modalities
+        d.hidden = model.hidden_dim
+        d.num_heads = model.num_heads
+        d.num_classes = model.num_classes
+        for m in range(model.num_modalities):
+            d.seq_len[m] = seq[m]
+            d.in_dim[m] = dims[m]
+        d.num_pairs = len(pairs)
+        for g, (q, k, _) in enumerate(pairs):
+            d.pair_q[g] = q
+            d.pair_k[g] = k
+        d.dropout = float(model.dropout.p)
+        d.training = int(model.training)
+        d.return_attention = int(return_attention)
+        self.desc = d
+        self.seq = [max(s, 1) for s in seq]
+        self.pairs = pairs
+        # parameter order: proj (w,b) per m; per pair q,k,v,o (w,b); gate (w,b) per m; cls1; cls2
+        self.names: List[str] = []
+        for m in model.modality_names:
+            self.names += [f"projections.{m}.0.weight", f"projections.{m}.0.bias"]
+        for _, _, key in pairs:
+            for proj in ("query_proj", "key_proj", "value_proj", "out_proj"):
+                self.names += [f"attention_modules.{key}.{proj}.weight",
+                               f"attention_modules.{key}.{proj}.bias"]
+        for m in model.modality_names:
+            self.names += [f"gating_layers.{m}.weight", f"gating_layers.{m}.bias"]
+        self.names += ["classifier.0.weight", "classifier.0.bias", "classifier.3.weight",
+                       "classifier.3.bias"]
+        self.num_param_elems = 0
+
+    def params(self, model: "HybridFusion") -> List[torch.Tensor]:
+        named = dict(model.named_parameters())
+        out = [named[n] for n in self.names]
+        self.num_param_elems = sum(p.numel() for p in out)
+        return out
+
+    def grad_views(self, flat: torch.Tensor, params) -> List[torch.Tensor]:
+        views, off = [], 0
+        for p in params:
+            views.append(flat[off:off + p.numel()].view_as(p))
+            off += p.numel()
+        return views
+
+    def param_struct(self, ts) -> "_nat.HybridParams":
+        s = _nat.HybridParams()
+        M = self.desc.num_modalities
+        it = iter(ts)
+        nxt = lambda: next(it).data_ptr()  # noqa: E731
+        for m in range(M):
+            s.proj[m] = _nat.Linear(nxt(), nxt())
+        for g in range(len(self.pairs)):
+            s.q[g] = _nat.Linear(nxt(), nxt())
+            s.k[g] = _nat.Linear(nxt(), nxt())
+            s.v[g] = _nat.Linear(nxt(), nxt())
+            s.o[g] = _nat.Linear(nxt(), nxt())
+        for m in range(M):
+            s.gate[m] = _nat.Linear(nxt(), nxt())
+        s.cls1 = _nat.Linear(nxt(), nxt())
+        s.cls2 = _nat.Linear(nxt(), nxt())
+        return s
+
+
+class HybridFusion(nn.Module):
+    """Cross-modal attention + learned, mask-aware fusion weights (src/fusion.py:248-479)."""
+
+    modality_names: list[str]
+    num_modalities: int
+    hidden_dim: int
+    projections: nn.ModuleDict
+    attention_modules: nn.ModuleDict
+    gating_layers: nn.ModuleDict
+    classifier: nn.Sequential
+    dropout: nn.Dropout
+
+    def __init__(self, modality_dims: Dict[str, int], hidden_dim: int = 256, num_classes: int = 11,
+                 num_heads: int = 4, dropout: float = 0.1):
+        super().__init__()
+        dims = dict(modality_dims)
+        names = list(dims)
+        cast_self = cast(Any, self)
+        cast_self.modality_names = names
+        cast_self.num_modalities = len(names)
+        cast_self.hidden_dim = hidden_dim
+        cast_self.num_heads = num_heads
+        cast_self.num_classes = num_classes
+        # construction order == the reference's => identical init for a given seed
+        self.projections = nn.ModuleDict({
+            m: nn.Sequential(nn.Linear(d, hidden_dim), nn.ReLU(), nn.Dropout(dropout))
+            for m, d in dims.items()})
+        self.attention_modules = nn.ModuleDict({
+            f"{q}_to_{k}": CrossModalAttention(hidden_dim, hidden_dim, hidden_dim=hidden_dim,
+                                               num_heads=num_heads, dropout=dropout)
+            for q in names for k in names if q != k})
+        self.gating_layers = nn.ModuleDict({m: nn.Linear(hidden_dim, 1) for m in names})
+        self.classifier = nn.Sequential(nn.Linear(hidden_dim, hidden_dim), nn.ReLU(),
+                                        nn.Dropout(dropout), nn.Linear(hidden_dim, num_classes))
+        self.dropout = nn.Dropout(dropout)
+        self.register_buffer("_rng_state", _new_rng_state(), persistent=False)
+
+    # ------------------------------------------------------------------ helpers
+    def present_pairs(self) -> List[Tuple[int, int, str]]:
+        """Pairs in the reference's iteration order, skipping deleted modules (src/fusion.py:383-389)."""
+        out = []
+        for qi, q in enumerate(self.modality_names):
+            for ki, k in enumerate(self.modality_names):
+                if q != k and f"{q}_to_{k}" in self.attention_modules:
+                    out.append((qi, ki, f"{q}_to_{k}"))
+        return out
+
+    def _plan(self, feats: List[torch.Tensor], return_attention: bool) -> _Plan:
+        seq, dims = [], []
+        B = feats[0].size(0)
+        for name, x in zip(self.modality_names, feats):
+            if x.dim() == 2:
+                seq.append(0)
+            elif x.dim() == 3:
+                seq.append(int(x.size(1)))
+            else:
+                raise RuntimeError(f"features for modality '{name}' must be 2-D or 3-D, got {tuple(x.shape)}")
+            if x.size(0) != B:
+                raise RuntimeError(f"batch size mismatch for modality '{name}': {x.size(0)} vs {B}")
+            in_f = self.projections[name][0].in_features
+            if x.size(-1) != in_f:
+                raise RuntimeError(f"modality '{name}': expected feature dim {in_f}, got {x.size(-1)}")
+            dims.append(int(x.size(-1)))
+        return _Plan(self, seq, dims, B, self.present_pairs(), return_attention)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, modality_features: Dict[str, torch.Tensor],
+                modality_mask: Optional[torch.Tensor] = None, return_attention: bool = False):
+        if not self.modality_names:
+            raise ValueError("No modalities configured for HybridFusion.")
+        ref = modality_features[self.modality_names[0]]
+        batch_size, device, dtype = ref.size(0), ref.device, ref.dtype
+        if modality_mask is None:
+            modality_mask = torch.ones(batch_size, self.num_modalities, device=device, dtype=dtype)
+        else:
+            modality_mask = modality_mask.to(device=device, dtype=dtype)
+        feats = []
+        for name in self.modality_names:
+            if name not in modality_features:
+                raise KeyError(f"Missing features for modality '{name}' in HybridFusion forward pass.")
+            feats.append(modality_features[name].to(device))
+        _nat.require_device(ref, "HybridFusion input")
+        for p in self.parameters():
+            if p.device != device or p.dtype != torch.float32:
+                raise RuntimeError("mmfusion HybridFusion needs float32 parameters on the input's device "
+                                   f"(found {p.dtype} on {p.device})")
+        plan = self._plan(feats, return_attention)
+        params = plan.params(self)
+        mask32 = _nat.f32c(modality_mask)
+        outs = _HybridFunction.apply(plan, self._rng_state, mask32, *[_nat.f32c(x) for x in feats], *params)
+        logits, fw, maps = outs[0], outs[1], outs[2:]
+        if dtype != torch.float32 and dtype.is_floating_point:
+            logits = logits.to(dtype)
+        if return_attention:
+            attention_maps = {key: maps[g] for g, (_, _, key) in enumerate(plan.pairs)}
+            return logits, {"attention_maps": attention_maps, "fusion_weights": fw}
+        return logits
+
+    def compute_adaptive_weights(self, modality_features: Dict[str, torch.Tensor],
+                                 modality_mask: torch.Tensor) -> torch.Tensor:
+        """src/fusion.py:429-479 on the device (gating scores -> masked softmax -> renormalise)."""
+        if modality_mask is None:
+            raise ValueError("modality_mask must be provided for adaptive weighting.")
+        device = modality_mask.device
+        feats = []
+        for name in self.modality_names:
+            if name not in modality_features:
+                raise KeyError(f"Missing aggregated features for modality '{name}'.")
+            feats.append(_nat.f32c(modality_features[name].to(device)))
+        _nat.require_device(modality_mask, "modality_mask")
+        L = _nat.lib()
+        B, M, H = feats[0].size(0), self.num_modalities, self.hidden_dim
+        mask = _nat.f32c(modality_mask)
+        gates = (_nat.Linear * M)()
+        for m, name in enumerate(self.modality_names):
+            layer = self.gating_layers[name]
+            gates[m] = _nat.Linear(layer.weight.data_ptr(), layer.bias.data_ptr())
+        out = torch.empty(B, M, dtype=torch.float32, device=device)
+        ws = torch.empty(L.mmf_adaptive_weights_workspace_bytes(B, M, H), dtype=torch.uint8, device=device)
+        farr = _nat.ptr_array([f.data_ptr() for f in feats])
+        rc = L.mmf_adaptive_weights(B, M, H, ctypes.cast(farr, ctypes.c_void_p), mask.data_ptr(),
+                                    ctypes.cast(gates, ctypes.c_void_p), out.data_ptr(), ws.data_ptr(),
+                                    _nat.stream_ptr(device))
+        _nat.check(rc, "compute_adaptive_weights")
+        return out
+
+
+def build_fusion_model(fusion_type: str, modality_dims: Dict[str, int], num_classes: int,
+                       **kwargs) -> nn.Module:
+    """Factory used by src/train.py:175-182 (src/fusion.py:485-515)."""
+    classes = {"early": EarlyFusion, "late": LateFusion, "hybrid": HybridFusion}
+    if fusion_type not in classes:
+        raise ValueError(f"Unknown fusion type: {fusion_type}")
+    kw = dict(kwargs)
+    if fusion_type != "hybrid":
+        kw.pop("num_heads", None)
+    return classes[fusion_type](modality_dims=modality_dims, num_classes=num_classes, **kw)

@@ -1,0 +1,158 @@
+"""ctypes binding of libmmfusion.so (the C-ABI declared in include/mmfusion.h).
+
+This is the only way the host mirror reaches the compute path.  There is no
+CPU or PyTorch fallback: if the library is missing or a tensor is not on a
+ROCm device, every entry point raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_float, c_int32, c_int64, c_size_t, c_void_p, POINTER
+from typing import Optional
+
+import torch
+
+MAX_MODALITIES = 8
+MAX_PAIRS = MAX_MODALITIES * (MAX_MODALITIES - 1)
+MAX_HEAD_DIM = 64
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "csrc", "libmmfusion.so")
+
+EXPORTED_SYMBOLS = (
+    "mmf_hybrid_saved_bytes", "mmf_hybrid_workspace_bytes", "mmf_hybrid_forward",
+    "mmf_hybrid_backward", "mmf_adaptive_weights_workspace_bytes", "mmf_adaptive_weights",
+    "mmf_cma_saved_bytes", "mmf_cma_workspace_bytes", "mmf_cma_forward", "mmf_cma_backward",
+    "mmf_cross_entropy_ls", "mmf_adamw_step", "mmf_last_error", "mmf_version",
+)
+
+
+class Linear(ctypes.Structure):
+    _fields_ = [("w", c_void_p), ("b", c_void_p)]
+
+
+class HybridDesc(ctypes.Structure):
+    _fields_ = [
+        ("batch", c_int32), ("num_modalities", c_int32), ("hidden", c_int32),
+        ("num_heads", c_int32), ("num_classes", c_int32),
+        ("seq_len", c_int32 * MAX_MODALITIES), ("in_dim", c_int32 * MAX_MODALITIES),
+        ("num_pairs", c_int32),
+        ("pair_q", c_int32 * MAX_PAIRS), ("pair_k", c_int32 * MAX_PAIRS),
+        ("dropout", c_float), ("training", c_int32), ("return_attention", c_int32),
+    ]
+
+
+class HybridParams(ctypes.Structure):
+    _fields_ = [
+        ("proj", Linear * MAX_MODALITIES),
+        ("q", Linear * MAX_PAIRS), ("k", Linear * MAX_PAIRS),
+        ("v", Linear * MAX_PAIRS), ("o", Linear * MAX_PAIRS),
+        ("gate", Linear * MAX_MODALITIES),
+        ("cls1", Linear), ("cls2", Linear),
+    ]
+
+
+HybridGrads = HybridParams  # identical layout (mmf_linear_grad has the same two pointers)
+
+
+class CmaDesc(ctypes.Structure):
+    _fields_ = [
+        ("batch", c_int32), ("lq", c_int32), ("lk", c_int32), ("query_dim", c_int32),
+        ("key_dim", c_int32), ("hidden", c_int32), ("num_heads", c_int32),
+        ("mask_mode", c_int32), ("dropout", c_float), ("training", c_int32),
+    ]
+
+
+class CmaParams(ctypes.Structure):
+    _fields_ = [("q", Linear), ("k", Linear), ("v", Linear), ("o", Linear)]
+
+
+CmaGrads = CmaParams
+
+_LIB: Optional[ctypes.CDLL] = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libmmfusion.so (built in-tree by `make -C csrc` / __graft_entry__.build())."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"mmfusion: HIP library not found at {LIB_PATH}. Build it with "
+            f"`make -C {os.path.join(_HERE, 'csrc')}` (hipcc --offload-arch=gfx950). "
+            "There is no CPU fallback.")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, sz = c_void_p, c_size_t
+    L.mmf_hybrid_saved_bytes.argtypes = [POINTER(HybridDesc)]
+    L.mmf_hybrid_saved_bytes.restype = sz
+    L.mmf_hybrid_workspace_bytes.argtypes = [POINTER(HybridDesc)]
+    L.mmf_hybrid_workspace_bytes.restype = sz
+    L.mmf_hybrid_forward.argtypes = [POINTER(HybridDesc), POINTER(HybridParams), vp, vp, vp, vp,
+                                     vp, vp, vp, vp]
+    L.mmf_hybrid_forward.restype = c_int32
+    L.mmf_hybrid_backward.argtypes = [POINTER(HybridDesc), POINTER(HybridParams), vp, vp, vp, vp,
+                                      vp, POINTER(HybridGrads), vp, vp]
+    L.mmf_hybrid_backward.restype = c_int32
+    L.mmf_adaptive_weights_workspace_bytes.argtypes = [c_int32, c_int32, c_int32]
+    L.mmf_adaptive_weights_workspace_bytes.restype = sz
+    L.mmf_adaptive_weights.argtypes = [c_int32, c_int32, c_int32, vp, vp, vp, vp, vp, vp]
+    L.mmf_adaptive_weights.restype = c_int32
+    L.mmf_cma_saved_bytes.argtypes = [POINTER(CmaDesc)]
+    L.mmf_cma_saved_bytes.restype = sz
+    L.mmf_cma_workspace_bytes.argtypes = [POINTER(CmaDesc)]
+    L.mmf_cma_workspace_bytes.restype = sz
+    L.mmf_cma_forward.argtypes = [POINTER(CmaDesc), POINTER(CmaParams), vp, vp, vp, vp, vp, vp,
+                                  vp, vp, vp]
+    L.mmf_cma_forward.restype = c_int32
+    L.mmf_cma_backward.argtypes = [POINTER(CmaDesc), POINTER(CmaParams), vp, vp, vp, vp, vp, vp,
+                                   vp, POINTER(CmaGrads), vp, vp, vp, vp]
+    L.mmf_cma_backward.restype = c_int32
+    L.mmf_cross_entropy_ls.argtypes = [c_int32, c_int32, vp, vp, c_float, c_float, vp, vp, vp]
+    L.mmf_cross_entropy_ls.restype = c_int32
+    L.mmf_adamw_step.argtypes = [c_int64, vp, vp, vp, vp, vp, c_float, c_float, c_float, c_float,
+                                 c_float, c_float, vp]
+    L.mmf_adamw_step.restype = c_int32
+    L.mmf_last_error.argtypes = []
+    L.mmf_last_error.restype = ctypes.c_char_p
+    L.mmf_version.argtypes = []
+    L.mmf_version.restype = ctypes.c_char_p
+    _LIB = L
+    return L
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().mmf_last_error().decode(errors="replace")
+        raise RuntimeError(f"mmfusion {what} failed (code {rc}): {msg}")
+
+
+def require_device(t: torch.Tensor, what: str) -> None:
+    if t.device.type != "cuda":
+        raise RuntimeError(
+            f"mmfusion: {what} is on {t.device}; the cross-modal fusion hot path runs only as HIP "
+            "kernels on a ROCm device (MI355X). Move the module and inputs to 'cuda'.")
+
+
+def stream_ptr(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def ptr_array(ptrs) -> ctypes.Array:
+    arr = (c_void_p * max(1, len(ptrs)))()
+    for i, p in enumerate(ptrs):
+        arr[i] = p
+    return arr
+
+
+def f32c(t: torch.Tensor) -> torch.Tensor:
+    """fp32 + contiguous view/copy of an input activation."""
+    if t.dtype != torch.float32:
+        t = t.float()
+    return t.contiguous()

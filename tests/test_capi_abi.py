@@ -1,0 +1,107 @@
+"""C-ABI checks without a GPU: the library loads, exports every function
+include/mmfusion.h declares, the ctypes mirrors match the C struct layouts,
+and host-side validation (size queries, error codes) behaves."""
+import ctypes
+import re
+import subprocess
+import tempfile
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+HEADER = ROOT / "include" / "mmfusion.h"
+
+
+@pytest.fixture(scope="module")
+def nat(pkg_on_path):
+    import mmf_native
+    try:
+        mmf_native.lib()
+    except RuntimeError as e:
+        pytest.fail(f"libmmfusion.so not built: {e}")
+    return mmf_native
+
+
+def declared_functions():
+    text = HEADER.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(mmf_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_exports_every_declared_symbol(nat):
+    L = nat.lib()
+    names = declared_functions()
+    assert len(names) >= 12
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    assert set(names) == set(nat.EXPORTED_SYMBOLS)
+
+
+def test_struct_layouts_match_header(nat, tmp_path):
+    src = tmp_path / "sizes.c"
+    src.write_text(f"""
+#include <stdio.h>
+#include <stddef.h>
+#include "{HEADER}"
+int main(void) {{
+  printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(mmf_hybrid_desc), sizeof(mmf_hybrid_params),
+         sizeof(mmf_hybrid_grads), sizeof(mmf_cma_desc), sizeof(mmf_cma_params),
+         offsetof(mmf_hybrid_desc, dropout), offsetof(mmf_hybrid_params, cls2));
+  return 0;
+}}
+""")
+    exe = tmp_path / "sizes"
+    subprocess.run(["gcc", str(src), "-o", str(exe)], check=True)
+    out = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True,
+                                          check=True).stdout.split()]
+    py = [ctypes.sizeof(nat.HybridDesc), ctypes.sizeof(nat.HybridParams),
+          ctypes.sizeof(nat.HybridGrads), ctypes.sizeof(nat.CmaDesc), ctypes.sizeof(nat.CmaParams),
+          nat.HybridDesc.dropout.offset, nat.HybridParams.cls2.offset]
+    assert out == py
+
+
+def _desc(nat, **kw):
+    d = nat.HybridDesc()
+    d.batch, d.num_modalities, d.hidden, d.num_heads, d.num_classes = 4, 3, 32, 4, 5
+    for m in range(3):
+        d.seq_len[m] = 0
+        d.in_dim[m] = 16
+    pairs = [(q, k) for q in range(3) for k in range(3) if q != k]
+    d.num_pairs = len(pairs)
+    for g, (q, k) in enumerate(pairs):
+        d.pair_q[g], d.pair_k[g] = q, k
+    d.dropout, d.training, d.return_attention = 0.1, 1, 0
+    for k, v in kw.items():
+        setattr(d, k, v)
+    return d
+
+
+def test_size_queries_and_validation(nat):
+    L = nat.lib()
+    d = _desc(nat)
+    assert L.mmf_hybrid_saved_bytes(ctypes.byref(d)) > 0
+    assert L.mmf_hybrid_workspace_bytes(ctypes.byref(d)) > 0
+    bad = _desc(nat, num_heads=3)            # 32 % 3 != 0
+    assert L.mmf_hybrid_saved_bytes(ctypes.byref(bad)) == 0
+    assert b"divisible" in L.mmf_last_error()
+    big = _desc(nat, hidden=256, num_heads=2)  # head_dim 128 > 64
+    assert L.mmf_hybrid_saved_bytes(ctypes.byref(big)) == 0
+    assert b"head_dim" in L.mmf_last_error()
+    # forward refuses a bad descriptor before touching the device
+    rc = L.mmf_hybrid_forward(ctypes.byref(bad), None, None, None, None, None, None, None, None, None)
+    assert rc != 0
+    c = nat.CmaDesc(2, 5, 7, 8, 8, 16, 4, 2, 0.0, 0)
+    assert L.mmf_cma_saved_bytes(ctypes.byref(c)) > 0
+    c.mask_mode = 5
+    assert L.mmf_cma_saved_bytes(ctypes.byref(c)) == 0
+    assert L.mmf_version().startswith(b"mmfusion")
+
+
+def test_workspace_scales_with_sequence(nat):
+    L = nat.lib()
+    d1 = _desc(nat)
+    d2 = _desc(nat)
+    for m in range(3):
+        d2.seq_len[m] = 128
+    assert L.mmf_hybrid_saved_bytes(ctypes.byref(d2)) > 100 * L.mmf_hybrid_saved_bytes(ctypes.byref(d1)) // 2

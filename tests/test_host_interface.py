@@ -1,0 +1,154 @@
+"""CPU tests of the drop-in host mirror (no GPU needed).
+
+The reference's own interface tests (tests/test_fusion.py:330-406,
+tests/test_attention.py:30-110) pin: constructor surface, state_dict keys,
+error types/messages raised before any compute, the deleted-pair skip, and the
+factory.  Compute itself needs a ROCm device: on CPU tensors the product path
+must raise (no CPU fallback).
+"""
+import numpy as np
+import pytest
+import torch
+
+from _util import load_fixture
+from cases import HYBRID_CASES, hybrid_state
+
+
+@pytest.fixture(scope="module")
+def mods(pkg_on_path):
+    import attention
+    import fusion
+    return fusion, attention
+
+
+def test_state_dict_keys_match_reference(mods):
+    fusion, _ = mods
+    for case in HYBRID_CASES:
+        model = fusion.HybridFusion({m: case.dims[m] for m in case.names}, hidden_dim=case.hidden,
+                                    num_classes=case.classes, num_heads=case.heads)
+        for key in case.deleted:
+            del model.attention_modules[key]
+        ref_keys = list(hybrid_state(case.names, case.dims, case.hidden, case.classes, case.seed,
+                                     case.deleted).keys())
+        assert sorted(model.state_dict().keys()) == sorted(ref_keys)
+        # shapes too
+        sd = hybrid_state(case.names, case.dims, case.hidden, case.classes, case.seed, case.deleted)
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+
+
+def test_fixture_param_names_are_reference_names(mods):
+    """The fixtures store grads under the reference module's own named_parameters()."""
+    fusion, _ = mods
+    fx = load_fixture("tiny_l1")
+    case = HYBRID_CASES[0]
+    model = fusion.HybridFusion({m: case.dims[m] for m in case.names}, hidden_dim=case.hidden,
+                                num_classes=case.classes, num_heads=case.heads)
+    names = {k[len("grad/"):] for k in fx if k.startswith("grad/")}
+    assert names == {n for n, _ in model.named_parameters()}
+
+
+def test_same_init_as_reference_under_seed(mods):
+    """Construction order mirrors src/fusion.py:291-328 so a seed gives the reference's init."""
+    fusion, _ = mods
+    torch.manual_seed(123)
+    a = fusion.HybridFusion({"video": 8, "imu": 4}, hidden_dim=16, num_classes=3, num_heads=2)
+    torch.manual_seed(123)
+    b = fusion.HybridFusion({"video": 8, "imu": 4}, hidden_dim=16, num_classes=3, num_heads=2)
+    for (ka, va), (kb, vb) in zip(a.state_dict().items(), b.state_dict().items()):
+        assert ka == kb and torch.equal(va, vb)
+
+
+def test_reference_init_equivalence_if_available(mods):
+    """Same seed => bitwise-identical parameters to the reference module (container only)."""
+    import sys
+    from pathlib import Path
+    if not Path("/root/reference/src/fusion.py").exists():
+        pytest.skip("reference not present (GPU box)")
+    fusion, _ = mods
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ref_attention", "/root/reference/src/attention.py")
+    ref_att = importlib.util.module_from_spec(spec)
+    sys.modules["ref_attention"] = ref_att
+    spec.loader.exec_module(ref_att)
+    torch.manual_seed(7)
+    ours = fusion.CrossModalAttention(12, 20, hidden_dim=16, num_heads=4)
+    torch.manual_seed(7)
+    theirs = ref_att.CrossModalAttention(12, 20, hidden_dim=16, num_heads=4)
+    for (ka, va), (kb, vb) in zip(ours.state_dict().items(), theirs.state_dict().items()):
+        assert ka == kb and torch.equal(va, vb)
+
+
+def test_errors_before_launch(mods):
+    fusion, _ = mods
+    with pytest.raises(ValueError, match="No modalities configured"):
+        fusion.HybridFusion({}, num_classes=3)({}, torch.ones(2, 0))
+    model = fusion.HybridFusion({"video": 4, "imu": 4}, num_classes=3)
+    with pytest.raises(KeyError, match="Missing features for modality"):
+        model({"video": torch.randn(2, 4)}, torch.ones(2, 2))
+    with pytest.raises(ValueError, match="modality_mask must be provided"):
+        model.compute_adaptive_weights({m: torch.randn(2, 4) for m in ("video", "imu")}, None)
+    agg = {"video": model.projections["video"](torch.randn(2, 4))}
+    with pytest.raises(KeyError, match="Missing aggregated features"):
+        model.compute_adaptive_weights(agg, torch.ones(2, 2))
+    with pytest.raises(ValueError, match="Unknown fusion type"):
+        fusion.build_fusion_model("ensemble", {"video": 4}, num_classes=3)
+    with pytest.raises(AssertionError):
+        fusion.CrossModalAttention(4, 4, hidden_dim=10, num_heads=4)
+
+
+def test_cpu_tensors_raise_no_fallback(mods):
+    fusion, attention = mods
+    model = fusion.HybridFusion({"video": 4, "imu": 4}, num_classes=3, num_heads=1, hidden_dim=8)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        model({"video": torch.randn(2, 4), "imu": torch.randn(2, 4)}, torch.ones(2, 2))
+    cma = attention.CrossModalAttention(8, 8, hidden_dim=8, num_heads=2)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        cma(torch.randn(2, 8), torch.randn(2, 8), torch.randn(2, 8))
+
+
+def test_deleted_pair_and_pair_order(mods):
+    fusion, _ = mods
+    model = fusion.HybridFusion({"a": 4, "b": 4, "c": 4}, num_classes=3, hidden_dim=8, num_heads=2)
+    del model.attention_modules["a_to_b"]
+    keys = [k for _, _, k in model.present_pairs()]
+    assert keys == ["a_to_c", "b_to_a", "b_to_c", "c_to_a", "c_to_b"]
+
+
+def test_factory_signature(mods):
+    fusion, _ = mods
+    m = fusion.build_fusion_model("hybrid", {"a": 4, "b": 6}, num_classes=5, hidden_dim=8,
+                                  num_heads=2, dropout=0.2)
+    assert isinstance(m, fusion.HybridFusion)
+    assert m.hidden_dim == 8 and m.num_modalities == 2 and m.dropout.p == 0.2
+    e = fusion.build_fusion_model("early", {"a": 4}, num_classes=5, hidden_dim=8, num_heads=2)
+    assert isinstance(e, fusion.EarlyFusion)
+    late = fusion.build_fusion_model("late", {"a": 4, "b": 4}, num_classes=2, num_heads=3)
+    out, per = late({"a": torch.randn(2, 4), "b": torch.randn(2, 4)}, None)
+    assert out.shape == (2, 2) and set(per) == {"a", "b"}
+
+
+def test_late_fusion_missing_modality_fallback(mods):
+    """tests/test_fusion.py:22-48 semantics for the (non-accelerated) LateFusion restatement."""
+    fusion, _ = mods
+    torch.manual_seed(0)
+    model = fusion.LateFusion({"video": 4, "imu": 4}, num_classes=3, hidden_dim=8, dropout=0.0).eval()
+    feats = {"video": torch.randn(2, 4), "imu": torch.randn(2, 4)}
+    fused, per = model(feats, torch.tensor([[1.0, 0.0], [0.0, 0.0]]))
+    assert torch.allclose(fused[0], per["video"][0], atol=1e-6)
+    assert torch.allclose(fused[1], (per["video"][1] + per["imu"][1]) / 2, atol=1e-6)
+
+
+def test_deepcopy_and_plan_descriptor(mods):
+    import copy
+    fusion, _ = mods
+    model = fusion.HybridFusion({"a": 6, "b": 10}, num_classes=4, hidden_dim=32, num_heads=4)
+    model2 = copy.deepcopy(model)
+    assert model2.state_dict().keys() == model.state_dict().keys()
+    plan = model._plan([torch.randn(3, 5, 6), torch.randn(3, 7, 10)], True)
+    d = plan.desc
+    assert (d.batch, d.num_modalities, d.hidden, d.num_heads, d.num_classes) == (3, 2, 32, 4, 4)
+    assert list(d.seq_len)[:2] == [5, 7] and list(d.in_dim)[:2] == [6, 10]
+    assert d.num_pairs == 2 and (d.pair_q[0], d.pair_k[0], d.pair_q[1], d.pair_k[1]) == (0, 1, 1, 0)
+    params = plan.params(model)
+    assert plan.num_param_elems == sum(p.numel() for p in model.parameters())
+    assert len(params) == len(list(model.parameters()))
