@@ -244,7 +244,32 @@ __global__ __launch_bounds__(NT) void attn_fwd_kernel(const AttnArgs A) {
   if (h == 0) P.lse[rowidx] = l > 0.f ? m + __logf(l) : -INFINITY;
 }
 
-// D[b, head, q] = sum_d dO * O  (rowsum(P' . dP') of the softmax backward)
+// D[b, head, q] = sum_d dO * O  (rowsum(P' . dP') of the softmax backward).
+// Vectorised form: one thread per float4 of a row, a head = G = hd/4 consecutive
+// lanes reduced by xor-shuffles (needs hd % 4 == 0, G a power of two, ld % 4 == 0).
+__global__ __launch_bounds__(NT) void attn_bwd_prep_vec_kernel(const AttnArgs A) {
+  const AttnPair& P = A.p[blockIdx.y];
+  const int hd = A.hd, G = hd / 4, H4 = (A.heads * hd) / 4;
+  const int64_t n = (int64_t)A.B * P.Lq * H4;
+  const int64_t idx = (int64_t)blockIdx.x * NT + threadIdx.x;
+  float s = 0.f;
+  int64_t row = 0;
+  int c4 = 0;
+  if (idx < n) {
+    row = idx / H4;              // b*Lq + q
+    c4 = (int)(idx % H4);
+    const float4 x = *reinterpret_cast<const float4*>(P.dout + row * P.ldo + 4 * c4);
+    const float4 y = *reinterpret_cast<const float4*>(P.o + row * P.ldo + 4 * c4);
+    s = x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
+  }
+  for (int o = G >> 1; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+  if (idx < n && (c4 % G) == 0) {
+    const int head = c4 / G;
+    const int q = (int)(row % P.Lq), b = (int)(row / P.Lq);
+    P.dsum[((int64_t)b * A.heads + head) * P.Lq + q] = s;
+  }
+}
+
 __global__ __launch_bounds__(NT) void attn_bwd_prep_kernel(const AttnArgs A) {
   const AttnPair& P = A.p[blockIdx.y];
   const int64_t n = (int64_t)A.B * P.Lq * A.heads;
@@ -484,6 +509,10 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
                           float scale, float drop_p, const RngSnap* rng, hipStream_t st) {
   if (hd > 64) return hipErrorInvalidValue;
   const bool small = hd <= 32;
+  bool prep_vec = (hd % 4 == 0) && (((hd / 4) & (hd / 4 - 1)) == 0);
+  for (int i = 0; i < npairs && prep_vec; ++i)
+    prep_vec = (pairs[i].ldo % 4 == 0) && (((uintptr_t)pairs[i].dout & 15) == 0) &&
+               (((uintptr_t)pairs[i].o & 15) == 0) && pairs[i].ldo == heads * hd;
   int done = 0;
   while (done < npairs) {
     AttnArgs a;
@@ -494,7 +523,9 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
       a.p[n] = pairs[done++];
       const AttnPair& P = a.p[n];
       int64_t nb;
-      if (kind == Kind::Prep) nb = ((int64_t)B * P.Lq * heads + NT - 1) / NT;
+      if (kind == Kind::Prep)
+        nb = prep_vec ? ((int64_t)B * P.Lq * (heads * hd / 4) + NT - 1) / NT
+                      : ((int64_t)B * P.Lq * heads + NT - 1) / NT;
       else if (kind == Kind::Dkv) nb = (int64_t)B * heads * ((P.Lk + 127) / 128);
       else nb = (int64_t)B * heads * ((P.Lq + 127) / 128);
       if (nb > maxblk) maxblk = nb;
@@ -520,7 +551,8 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
         else hipLaunchKernelGGL((attn_fwd_kernel<64, 1>), grid, dim3(NT), 0, st, a);
         break;
       case Kind::Prep:
-        hipLaunchKernelGGL(attn_bwd_prep_kernel, grid, dim3(NT), 0, st, a);
+        if (prep_vec) hipLaunchKernelGGL(attn_bwd_prep_vec_kernel, grid, dim3(NT), 0, st, a);
+        else hipLaunchKernelGGL(attn_bwd_prep_kernel, grid, dim3(NT), 0, st, a);
         break;
       case Kind::Dkv:
         if (small) hipLaunchKernelGGL((attn_bwd_dkv_kernel<32>), grid, dim3(NT), 0, st, a);
@@ -547,6 +579,12 @@ hipError_t launch_attn_fwd(const AttnPair* pairs, int npairs, int B, int heads, 
 hipError_t launch_attn_probs(const AttnPair* pairs, int npairs, int B, int heads, int hd,
                              float scale, float drop_p, const RngSnap* rng, hipStream_t st) {
   return launch_generic(Kind::Probs, pairs, npairs, B, heads, hd, scale, drop_p, rng, st);
+}
+
+hipError_t launch_attn_bwd_stage(int stage, const AttnPair* pairs, int npairs, int B, int heads, int hd,
+                                 float scale, float drop_p, const RngSnap* rng, hipStream_t st) {
+  const Kind k = stage == 0 ? Kind::Prep : (stage == 1 ? Kind::Dkv : Kind::Dq);
+  return launch_generic(k, pairs, npairs, B, heads, hd, scale, drop_p, rng, st);
 }
 
 hipError_t launch_attn_bwd(const AttnPair* pairs, int npairs, int B, int heads, int hd, float scale,

@@ -29,11 +29,60 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 
+// ---------------------------------------------------------------- profiling
+// Optional per-stage hipEvent timing (mmf_profile_begin/_end): every launch
+// group is bracketed by two events on the caller's stream.  Off by default
+// (then a Stage costs one branch).  Not for use under graph capture.
+struct ProfRec { const char* name; hipEvent_t a, b; };
+struct Prof {
+  bool on = false;
+  std::vector<ProfRec> recs;
+  std::vector<hipEvent_t> pool;
+  size_t next = 0;
+  hipEvent_t ev() {
+    if (next == pool.size()) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return nullptr;
+      pool.push_back(e);
+    }
+    return pool[next++];
+  }
+};
+Prof g_prof;
+
+struct Stage {
+  const char* name;
+  hipStream_t st;
+  hipEvent_t a = nullptr;
+  Stage(const char* n, hipStream_t s) : name(n), st(s) {
+    if (g_prof.on) {
+      a = g_prof.ev();
+      if (a) (void)hipEventRecord(a, st);
+    }
+  }
+  ~Stage() {
+    if (g_prof.on && a) {
+      hipEvent_t b = g_prof.ev();
+      if (b) {
+        (void)hipEventRecord(b, st);
+        g_prof.recs.push_back({name, a, b});
+      }
+    }
+  }
+};
+
 #define HIP_TRY(expr)                                                                   \
   do {                                                                                  \
     hipError_t e_ = (expr);                                                             \
     if (e_ != hipSuccess)                                                               \
       return fail(MMF_EHIP, "%s failed: %s", #expr, hipGetErrorString(e_));             \
+  } while (0)
+
+// Launch group wrapped in a profiling stage.
+#define STAGE_TRY(name, expr)                                                           \
+  do {                                                                                  \
+    Stage stage_(name, st);                                                             \
+    HIP_TRY(expr);                                                                      \
   } while (0)
 
 struct Bump {
@@ -230,6 +279,7 @@ size_t hybrid_partials_bytes(const mmf_hybrid_desc* d) {
     total += slab(H, H, B * lq, true) * 2 + slab(H, H, B * lk, true) * 2;
   }
   for (int m = 0; m < d->num_modalities; ++m) total += slab(H, d->in_dim[m], B * Lm(d, m), true);
+  for (int m = 0; m < d->num_modalities; ++m) total += slab(1, H, B, true);   // gating layers
   return total;
 }
 
@@ -238,6 +288,34 @@ size_t hybrid_partials_bytes(const mmf_hybrid_desc* d) {
 extern "C" {
 
 const char* mmf_last_error(void) { return g_err.c_str(); }
+
+void mmf_profile_begin(void) {
+  g_prof.on = true;
+  g_prof.recs.clear();
+  g_prof.next = 0;
+}
+
+// Ends profiling: waits for the recorded events and writes "name ms\n" lines
+// (one per launch group, in launch order) into out.  Returns the bytes needed.
+size_t mmf_profile_end(char* out, size_t cap) {
+  std::string s;
+  for (const ProfRec& r : g_prof.recs) {
+    float ms = 0.f;
+    if (hipEventSynchronize(r.b) == hipSuccess) (void)hipEventElapsedTime(&ms, r.a, r.b);
+    char line[160];
+    snprintf(line, sizeof(line), "%s %.6f\n", r.name, (double)ms);
+    s += line;
+  }
+  g_prof.on = false;
+  g_prof.recs.clear();
+  g_prof.next = 0;
+  if (out && cap) {
+    const size_t n = s.size() < cap - 1 ? s.size() : cap - 1;
+    memcpy(out, s.data(), n);
+    out[n] = 0;
+  }
+  return s.size() + 1;
+}
 const char* mmf_version(void) { return "mmfusion 0.1 (gfx950, fp32 MFMA)"; }
 
 size_t mmf_hybrid_saved_bytes(const mmf_hybrid_desc* d) {
@@ -272,7 +350,7 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
   Bump bp(saved);
   HySaved s;
   layout_saved(d, bp, s);
-  if (rng_state) HIP_TRY(launch_rng_snapshot(rng_state, s.rng, st));
+  if (rng_state) STAGE_TRY("fwd.rng", launch_rng_snapshot(rng_state, s.rng, st));
   const RngSnap* rng = rng_state ? s.rng : nullptr;
 
   // (1) per-modality projection: P_m = Drop(ReLU((Drop(X_m*mask)) W_m^T + b_m))
@@ -294,7 +372,7 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
       xf.ncols = D;
       jobs.push_back(j);
     }
-    HIP_TRY(launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, p, rng, st));
+    STAGE_TRY("fwd.proj_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, p, rng, st));
   }
   // (2) Q/K/V projections of every present pair (src/attention.py:104-106)
   {
@@ -315,7 +393,7 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
       jobs.push_back(jk);
       jobs.push_back(jv);
     }
-    if (!jobs.empty()) HIP_TRY(launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, 0.f, rng, st));
+    if (!jobs.empty()) STAGE_TRY("fwd.qkv_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, 0.f, rng, st));
   }
   // (3) attention per pair (key mask = modality mask column k, src/fusion.py:391-401)
   std::vector<AttnPair> pairs(d->num_pairs);
@@ -332,7 +410,7 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
   }
   const float scale = 1.0f / std::sqrt((float)hd);
   if (d->num_pairs) {
-    HIP_TRY(launch_attn_fwd(pairs.data(), d->num_pairs, B, d->num_heads, hd, scale, p, rng, st));
+    STAGE_TRY("fwd.attn", launch_attn_fwd(pairs.data(), d->num_pairs, B, d->num_heads, hd, scale, p, rng, st));
     // (4) out_proj
     std::vector<GemmJob> jobs;
     for (int g = 0; g < d->num_pairs; ++g) {
@@ -342,7 +420,7 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
       add_src(j, opnd(s.O[g], H), opnd(W->o[g].w, H), H);
       jobs.push_back(j);
     }
-    HIP_TRY(launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, 0.f, rng, st));
+    STAGE_TRY("fwd.out_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, 0.f, rng, st));
   }
   // (5) aggregation + pooling + gating + adaptive weights + weighted sum
   HeadArgs ha;
@@ -366,18 +444,18 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
   for (int m = 0; m < M; ++m) ha.inv_cnt[m] = 1.0f / ((float)cnt[m] * (float)Lm(d, m));
   ha.pooled = s.pooled; ha.scores = s.scores; ha.weights = s.weights; ha.fused = s.fused;
   ha.weights_out = fusion_weights;
-  HIP_TRY(launch_head_fwd(ha, st));
+  STAGE_TRY("fwd.head", launch_head_fwd(ha, st));
   // (6) classifier: Linear -> ReLU -> Dropout -> Linear
   {
     GemmJob j = make_job(B, H, s.h1, H, EPI_BIAS | EPI_RELU | (drop ? EPI_DROP : 0));
     j.g.bias = W->cls1.b;
     j.g.drop_site = SITE_CLS;
     add_src(j, opnd(s.fused, H), opnd(W->cls1.w, H), H);
-    HIP_TRY(launch_gemm(&j, 1, MODE_RK, MODE_RK, p, rng, st));
+    STAGE_TRY("fwd.cls1_gemm", launch_gemm(&j, 1, MODE_RK, MODE_RK, p, rng, st));
     GemmJob j2 = make_job(B, C, logits, C, EPI_BIAS);
     j2.g.bias = W->cls2.b;
     add_src(j2, opnd(s.h1, H), opnd(W->cls2.w, H), H);
-    HIP_TRY(launch_gemm(&j2, 1, MODE_RK, MODE_RK, 0.f, rng, st));
+    STAGE_TRY("fwd.cls2_gemm", launch_gemm(&j2, 1, MODE_RK, MODE_RK, 0.f, rng, st));
   }
   // (7) optional attention maps (post-dropout, src/attention.py:130,144-146)
   if (d->return_attention && attn_maps && d->num_pairs) {
@@ -385,7 +463,7 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
     for (int g = 0; g < d->num_pairs; ++g)
       if (pairs[g].probs) pp.push_back(pairs[g]);
     if (!pp.empty())
-      HIP_TRY(launch_attn_probs(pp.data(), (int)pp.size(), B, d->num_heads, hd, scale, p, rng, st));
+      STAGE_TRY("fwd.attn_probs", launch_attn_probs(pp.data(), (int)pp.size(), B, d->num_heads, hd, scale, p, rng, st));
   }
   return MMF_OK;
 }
@@ -418,10 +496,10 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
     GemmJob j = make_job(B, H, w.dz1, H, EPI_GATE);
     j.g.gate = s.h1; j.g.ld_gate = H; j.g.gate_scale = gscale;
     add_src(j, opnd(dlogits, C), opnd(W->cls2.w, H), C);
-    HIP_TRY(launch_gemm(&j, 1, MODE_RK, MODE_KR, 0.f, rng, st));
+    STAGE_TRY("bwd.cls_dz1_gemm", launch_gemm(&j, 1, MODE_RK, MODE_KR, 0.f, rng, st));
     GemmJob j2 = make_job(B, H, w.dfused, H, 0);
     add_src(j2, opnd(w.dz1, H), opnd(W->cls1.w, H), H);
-    HIP_TRY(launch_gemm(&j2, 1, MODE_RK, MODE_KR, 0.f, rng, st));
+    STAGE_TRY("bwd.cls_dfused_gemm", launch_gemm(&j2, 1, MODE_RK, MODE_KR, 0.f, rng, st));
     plan_wgrad(wp, bw, C, H, B, opnd(dlogits, C), opnd(s.h1, H), G->cls2.w, G->cls2.b);
     plan_wgrad(wp, bw, H, H, B, opnd(w.dz1, H), opnd(s.fused, H), G->cls1.w, G->cls1.b);
   }
@@ -440,13 +518,12 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
   for (int m = 0; m < M; ++m) ha.inv_cnt[m] = 1.0f / ((float)cnt[m] * (float)Lm(d, m));
   ha.pooled = s.pooled; ha.scores = s.scores; ha.weights = s.weights;
   ha.dfused = w.dfused; ha.cvec = w.cvec; ha.dscore = w.dscore;
-  HIP_TRY(launch_head_bwd(ha, st));
-  {
-    float* dgw[MMF_MAX_MODALITIES];
-    float* dgb[MMF_MAX_MODALITIES];
-    for (int m = 0; m < M; ++m) { dgw[m] = G->gate[m].w; dgb[m] = G->gate[m].b; }
-    HIP_TRY(launch_gate_wgrad(B, M, H, w.dscore, s.pooled, dgw, dgb, st));
-  }
+  STAGE_TRY("bwd.head", launch_head_bwd(ha, st));
+  // gating_layers[m] grads = dscore[:, m]^T pooled[:, m, :] (+ row sums for the bias):
+  // a 1 x H weight-gradient GEMM riding in the split-K batch below.
+  for (int m = 0; m < M; ++m)
+    plan_wgrad(wp, bw, 1, H, B, opnd(w.dscore + m, M), opnd(s.pooled + (size_t)m * H, M * H),
+               G->gate[m].w, G->gate[m].b);
   const float scale = 1.0f / std::sqrt((float)hd);
   if (d->num_pairs) {
     // (3) out_proj backward: dA_g rows are c_{q(g)} broadcast over L_q
@@ -459,7 +536,7 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
       plan_wgrad(wp, bw, H, H, B * lq, opnd(w.cvec + (size_t)q * H, M * H, lq), opnd(s.O[g], H),
                  G->o[g].w, G->o[g].b);
     }
-    HIP_TRY(launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, 0.f, rng, st));
+    STAGE_TRY("bwd.out_dO_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, 0.f, rng, st));
     // (4) attention backward
     std::vector<AttnPair> pairs(d->num_pairs);
     for (int g = 0; g < d->num_pairs; ++g) {
@@ -473,7 +550,9 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
       a.drop_site = SITE_ATTN + g;
       a.dout = w.dO[g]; a.dsum = w.dsum[g]; a.dq = w.dQ[g]; a.dk = w.dK[g]; a.dv = w.dV[g];
     }
-    HIP_TRY(launch_attn_bwd(pairs.data(), d->num_pairs, B, d->num_heads, hd, scale, p, rng, st));
+    STAGE_TRY("bwd.attn_prep", launch_attn_bwd_stage(0, pairs.data(), d->num_pairs, B, d->num_heads, hd, scale, p, rng, st));
+    STAGE_TRY("bwd.attn_dkv", launch_attn_bwd_stage(1, pairs.data(), d->num_pairs, B, d->num_heads, hd, scale, p, rng, st));
+    STAGE_TRY("bwd.attn_dq", launch_attn_bwd_stage(2, pairs.data(), d->num_pairs, B, d->num_heads, hd, scale, p, rng, st));
     // (5) Q/K/V weight grads
     for (int g = 0; g < d->num_pairs; ++g) {
       const int q = d->pair_q[g], k = d->pair_k[g];
@@ -505,7 +584,7 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
       if (j.nsrc > GEMM_MAX_SRCS) return fail(MMF_ELIMIT, "too many gradient sources");
       jobs.push_back(j);
     }
-    HIP_TRY(launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, 0.f, rng, st));
+    STAGE_TRY("bwd.dZ_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, 0.f, rng, st));
   }
   // (7) projection weight grads (X~ recomputed: mask * input dropout) and dX
   {
@@ -527,14 +606,14 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
         jobs.push_back(j);
       }
     }
-    if (!jobs.empty()) HIP_TRY(launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, p, rng, st));
+    if (!jobs.empty()) STAGE_TRY("bwd.dx_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, p, rng, st));
   }
   // (8) all weight gradients: split-K slabs (only written here), then one
   // deterministic reduce.
   if (bw.off > mmf_hybrid_workspace_bytes(d))
     return fail(MMF_EINVAL, "internal: workspace overflow");
-  HIP_TRY(launch_gemm(wp.jobs.data(), (int)wp.jobs.size(), MODE_KR, MODE_KR, p, rng, st));
-  HIP_TRY(launch_reduce(wp.reds.data(), (int)wp.reds.size(), st));
+  STAGE_TRY("bwd.wgrad_gemm", launch_gemm(wp.jobs.data(), (int)wp.jobs.size(), MODE_KR, MODE_KR, p, rng, st));
+  STAGE_TRY("bwd.wgrad_reduce", launch_reduce(wp.reds.data(), (int)wp.reds.size(), st));
   return MMF_OK;
 }
 
@@ -653,7 +732,7 @@ int mmf_cma_forward(const mmf_cma_desc* d, const mmf_cma_params* W, const float*
   Bump bp(saved);
   CmaSaved s;
   layout_cma(d, bp, s);
-  if (rng_state) HIP_TRY(launch_rng_snapshot(rng_state, s.rng, st));
+  if (rng_state) STAGE_TRY("cma.fwd.rng", launch_rng_snapshot(rng_state, s.rng, st));
   const RngSnap* rng = rng_state ? s.rng : nullptr;
   GemmJob jobs[3];
   jobs[0] = make_job(B * d->lq, H, s.Q, H, EPI_BIAS);
@@ -665,7 +744,7 @@ int mmf_cma_forward(const mmf_cma_desc* d, const mmf_cma_params* W, const float*
   jobs[2] = make_job(B * d->lk, H, s.V, H, EPI_BIAS);
   jobs[2].g.bias = W->v.b;
   add_src(jobs[2], opnd(value, d->key_dim), opnd(W->v.w, d->key_dim), d->key_dim);
-  HIP_TRY(launch_gemm(jobs, 3, MODE_RK, MODE_RK, 0.f, rng, st));
+  STAGE_TRY("cma.fwd.qkv_gemm", launch_gemm(jobs, 3, MODE_RK, MODE_RK, 0.f, rng, st));
   AttnPair a;
   memset(&a, 0, sizeof(a));
   a.q = s.Q; a.k = s.K; a.v = s.V; a.o = s.O; a.lse = s.lse;
@@ -675,12 +754,12 @@ int mmf_cma_forward(const mmf_cma_desc* d, const mmf_cma_params* W, const float*
   a.drop_site = SITE_ATTN;
   a.probs = attn_weights;
   const float scale = 1.0f / std::sqrt((float)hd);
-  HIP_TRY(launch_attn_fwd(&a, 1, B, d->num_heads, hd, scale, p, rng, st));
-  if (attn_weights) HIP_TRY(launch_attn_probs(&a, 1, B, d->num_heads, hd, scale, p, rng, st));
+  STAGE_TRY("cma.fwd.attn", launch_attn_fwd(&a, 1, B, d->num_heads, hd, scale, p, rng, st));
+  if (attn_weights) STAGE_TRY("cma.fwd.attn_probs", launch_attn_probs(&a, 1, B, d->num_heads, hd, scale, p, rng, st));
   GemmJob jo = make_job(B * d->lq, H, attended, H, EPI_BIAS);
   jo.g.bias = W->o.b;
   add_src(jo, opnd(s.O, H), opnd(W->o.w, H), H);
-  HIP_TRY(launch_gemm(&jo, 1, MODE_RK, MODE_RK, 0.f, rng, st));
+  STAGE_TRY("cma.fwd.out_gemm", launch_gemm(&jo, 1, MODE_RK, MODE_RK, 0.f, rng, st));
   return MMF_OK;
 }
 
@@ -707,7 +786,7 @@ int mmf_cma_backward(const mmf_cma_desc* d, const mmf_cma_params* W, const float
   {
     GemmJob j = make_job(B * d->lq, H, w.dO, H, 0);
     add_src(j, opnd(dA, H), opnd(W->o.w, H), H);
-    HIP_TRY(launch_gemm(&j, 1, MODE_RK, MODE_KR, 0.f, rng, st));
+    STAGE_TRY("cma.bwd.dO_gemm", launch_gemm(&j, 1, MODE_RK, MODE_KR, 0.f, rng, st));
     plan_wgrad(wp, bw, H, H, B * d->lq, opnd(dA, H), opnd(s.O, H), G->o.w, G->o.b);
   }
   AttnPair a;
@@ -719,7 +798,7 @@ int mmf_cma_backward(const mmf_cma_desc* d, const mmf_cma_params* W, const float
   a.drop_site = SITE_ATTN;
   a.dout = w.dO; a.dsum = w.dsum; a.dq = w.dQ; a.dk = w.dK; a.dv = w.dV;
   const float scale = 1.0f / std::sqrt((float)hd);
-  HIP_TRY(launch_attn_bwd(&a, 1, B, d->num_heads, hd, scale, p, rng, st));
+  STAGE_TRY("cma.bwd.attn", launch_attn_bwd(&a, 1, B, d->num_heads, hd, scale, p, rng, st));
   plan_wgrad(wp, bw, H, d->query_dim, B * d->lq, opnd(w.dQ, H), opnd(query, d->query_dim), G->q.w, G->q.b);
   plan_wgrad(wp, bw, H, d->key_dim, B * d->lk, opnd(w.dK, H), opnd(key, d->key_dim), G->k.w, G->k.b);
   plan_wgrad(wp, bw, H, d->key_dim, B * d->lk, opnd(w.dV, H), opnd(value, d->key_dim), G->v.w, G->v.b);
@@ -739,10 +818,10 @@ int mmf_cma_backward(const mmf_cma_desc* d, const mmf_cma_params* W, const float
     add_src(j, opnd(w.dV, H), opnd(W->v.w, d->key_dim), H);
     jobs.push_back(j);
   }
-  if (!jobs.empty()) HIP_TRY(launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, 0.f, rng, st));
+  if (!jobs.empty()) STAGE_TRY("cma.bwd.dx_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, 0.f, rng, st));
   if (bw.off > mmf_cma_workspace_bytes(d)) return fail(MMF_EINVAL, "internal: workspace overflow");
-  HIP_TRY(launch_gemm(wp.jobs.data(), (int)wp.jobs.size(), MODE_KR, MODE_KR, 0.f, rng, st));
-  HIP_TRY(launch_reduce(wp.reds.data(), (int)wp.reds.size(), st));
+  STAGE_TRY("cma.bwd.wgrad_gemm", launch_gemm(wp.jobs.data(), (int)wp.jobs.size(), MODE_KR, MODE_KR, 0.f, rng, st));
+  STAGE_TRY("cma.bwd.wgrad_reduce", launch_reduce(wp.reds.data(), (int)wp.reds.size(), st));
   return MMF_OK;
 }
 

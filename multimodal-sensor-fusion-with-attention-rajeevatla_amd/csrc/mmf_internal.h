@@ -147,6 +147,9 @@ hipError_t launch_attn_probs(const AttnPair* pairs, int npairs, int B, int heads
                              float scale, float drop_p, const RngSnap* rng, hipStream_t st);
 hipError_t launch_attn_bwd(const AttnPair* pairs, int npairs, int B, int heads, int hd, float scale,
                            float drop_p, const RngSnap* rng, hipStream_t st);
+// stage 0: D = rowsum(dO*O); 1: dK/dV; 2: dQ
+hipError_t launch_attn_bwd_stage(int stage, const AttnPair* pairs, int npairs, int B, int heads, int hd,
+                                 float scale, float drop_p, const RngSnap* rng, hipStream_t st);
 
 // ---------------------------------------------------------------------------
 // Fusion head: pooling + gating + adaptive weights + weighted sum, and backward.

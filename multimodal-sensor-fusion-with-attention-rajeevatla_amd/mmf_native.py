@@ -25,7 +25,8 @@ EXPORTED_SYMBOLS = (
     "mmf_hybrid_saved_bytes", "mmf_hybrid_workspace_bytes", "mmf_hybrid_forward",
     "mmf_hybrid_backward", "mmf_adaptive_weights_workspace_bytes", "mmf_adaptive_weights",
     "mmf_cma_saved_bytes", "mmf_cma_workspace_bytes", "mmf_cma_forward", "mmf_cma_backward",
-    "mmf_cross_entropy_ls", "mmf_adamw_step", "mmf_last_error", "mmf_version",
+    "mmf_cross_entropy_ls", "mmf_adamw_step", "mmf_profile_begin", "mmf_profile_end",
+    "mmf_last_error", "mmf_version",
 )
 
 
@@ -115,12 +116,32 @@ def lib() -> ctypes.CDLL:
     L.mmf_adamw_step.argtypes = [c_int64, vp, vp, vp, vp, vp, c_float, c_float, c_float, c_float,
                                  c_float, c_float, vp]
     L.mmf_adamw_step.restype = c_int32
+    L.mmf_profile_begin.argtypes = []
+    L.mmf_profile_begin.restype = None
+    L.mmf_profile_end.argtypes = [ctypes.c_char_p, c_size_t]
+    L.mmf_profile_end.restype = c_size_t
     L.mmf_last_error.argtypes = []
     L.mmf_last_error.restype = ctypes.c_char_p
     L.mmf_version.argtypes = []
     L.mmf_version.restype = ctypes.c_char_p
     _LIB = L
     return L
+
+
+def profile_begin() -> None:
+    lib().mmf_profile_begin()
+
+
+def profile_end() -> list:
+    """[(stage_name, ms), ...] for every launch group since profile_begin()."""
+    L = lib()
+    buf = ctypes.create_string_buffer(1 << 20)
+    L.mmf_profile_end(buf, len(buf))
+    out = []
+    for line in buf.value.decode().splitlines():
+        name, ms = line.rsplit(" ", 1)
+        out.append((name, float(ms)))
+    return out
 
 
 def check(rc: int, what: str) -> None:
