@@ -503,7 +503,358 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(const AttnArgs A) {
     }
 }
 
-enum class Kind { Fwd, Probs, Prep, Dkv, Dq };
+// ===========================================================================
+// Pooled-output attention (HybridFusion).  HybridFusion consumes the attended
+// features only through their mean over the query axis (agg -> mean-pool,
+// src/fusion.py:406-408 + sequence-mode pooling) and out_proj / value_proj are
+// affine, so
+//     mean_q (P' V) W_o^T + b_o = (pbar V) W_o^T + b_o,   pbar = mean_q P'[q, :]
+// and the (Lq x Lk) attention only has to deliver the column means pbar (and
+// LSE for the backward).  In the backward every query row of dP' equals
+// dpbar / Lq, so dP needs no MFMA: dS = P' * dpbar / Lq - P * D,
+// D = rowsum(P' * dpbar) / Lq.  Limits: Lk <= 128 (one LDS chunk).
+// ===========================================================================
+constexpr int PKC = 128;
+
+// Column-sum of a 32x32 S^T tile over its 32 query lanes (reduce-scatter
+// butterfly, 16 shuffles).  Returns, in lane c, the sum for tile row
+// r = (c >> 1) & 15 (lanes c and c^1 hold the same value).
+__device__ __forceinline__ float colsum_tile(const float (&v)[16], int c) {
+  float a8[8], a4[4], a2[2];
+  const bool b4 = c & 16, b3 = c & 8, b2 = c & 4, b1 = c & 2;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float recv = __shfl_xor(b4 ? v[i] : v[i + 8], 16);
+    a8[i] = (b4 ? v[i + 8] : v[i]) + recv;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float recv = __shfl_xor(b3 ? a8[i] : a8[i + 4], 8);
+    a4[i] = (b3 ? a8[i + 4] : a8[i]) + recv;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float recv = __shfl_xor(b2 ? a4[i] : a4[i + 2], 4);
+    a2[i] = (b2 ? a4[i + 2] : a4[i]) + recv;
+  }
+  float a1 = (b1 ? a2[1] : a2[0]) + __shfl_xor(b1 ? a2[0] : a2[1], 2);
+  a1 += __shfl_xor(a1, 1);
+  return a1;
+}
+
+template <int HDP>
+__global__ __launch_bounds__(NT) void attn_pool_fwd_kernel(const AttnArgs A) {
+  constexpr int LS = HDP + 4;
+  constexpr int HALF = HDP / 2;
+  constexpr int NKT = PKC / 32;
+  __shared__ __attribute__((aligned(16))) float Ks[PKC * LS];
+  __shared__ float cs[4][PKC];
+
+  const AttnPair& P = A.p[blockIdx.y];
+  int bid = blockIdx.x;
+  if (bid >= A.B * A.heads) return;
+  const int head = bid % A.heads, b = bid / A.heads;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, c = lane & 31;
+  const int hd = A.hd, col0 = head * hd;
+  const int Lq = P.Lq, Lk = P.Lk;
+  const float scale = A.scale, pdrop = A.drop_p;
+  const float inv_keep = pdrop < 1.f ? 1.f / (1.f - pdrop) : 0.f;
+  RngSnap rs{0, 0};
+  if (pdrop > 0.f && A.rng) rs = *A.rng;
+  const int64_t bh = (int64_t)b * A.heads + head;
+  float* pbar = P.pbar + bh * Lk;
+
+  if (P.kmask_mode == 1 && P.kmask[(int64_t)b * P.kmask_ld] == 0.f) {
+    // masked key modality: softmax over all -inf -> NaN -> 0 (src/attention.py:127-129)
+    for (int k = t; k < Lk; k += NT) pbar[k] = 0.f;
+    for (int q = t; q < Lq; q += NT) P.lse[bh * Lq + q] = -INFINITY;
+    if (P.keep_bits)
+      for (int q = t; q < Lq; q += NT)
+        *reinterpret_cast<uint4*>(P.keep_bits + (bh * Lq + q) * 4) = make_uint4(0, 0, 0, 0);
+    return;
+  }
+  const bool vk = (P.ldk % 4 == 0) && (hd % 4 == 0);
+  load_rows<PKC, HDP, LS>(Ks, P.k + (int64_t)b * Lk * P.ldk + col0, Lk, P.ldk, 0, hd, vk);
+  for (int i = t; i < 4 * PKC; i += NT) (&cs[0][0])[i] = 0.f;
+  __syncthreads();
+  const int nkt = (Lk + 31) / 32;
+
+  for (int q0 = 0; q0 < Lq; q0 += 128) {
+    const int q = q0 + w * 32 + c;
+    if (q0 + w * 32 >= Lq) continue;   // whole wave idle (no barrier below)
+    const bool qvalid = q < Lq;
+    float qf[HALF];
+    load_frag<HALF>(qf, P.q + ((int64_t)b * Lq + (qvalid ? q : 0)) * P.ldq + col0, h * HALF, hd, qvalid);
+    float sv[NKT][16];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      if (kt < nkt) {
+        f32x16 s = dot_rows<HALF>(Ks + (kt * 32 + c) * LS + h * HALF, qf, zero16());
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kt * 32 + acc_row(r, h);
+          const bool valid = key < Lk && (P.kmask_mode != 2 || kmask_val(P, b, key) != 0.f);
+          sv[kt][r] = valid ? s[r] * scale : -INFINITY;
+          mx = fmaxf(mx, sv[kt][r]);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sv[kt][r] = -INFINITY;
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    float l = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        sv[kt][r] = (sv[kt][r] == -INFINITY) ? 0.f : __expf(sv[kt][r] - mx);
+        l += sv[kt][r];
+      }
+    l += __shfl_xor(l, 32);
+    const float inv_l = (l > 0.f && qvalid) ? 1.f / l : 0.f;
+    const int64_t rowidx = bh * Lq + q;
+    uint32_t words[NKT];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      uint32_t bits = 0;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint32_t kb = 0xFu;
+        if (pdrop > 0.f && qvalid && kt < nkt)
+          kb = keep4(rs, P.drop_site, (uint64_t)rowidx * Lk + kt * 32 + 8 * g + 4 * h, pdrop);
+        bits |= kb << (8 * g + 4 * h);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float pv = sv[kt][4 * g + j] * inv_l;
+          sv[kt][4 * g + j] = (pdrop > 0.f) ? (((kb >> j) & 1u) ? pv * inv_keep : 0.f) : pv;
+        }
+      }
+      words[kt] = bits | __shfl_xor(bits, 32);
+      if (kt < nkt) {
+        const float colsum = colsum_tile(sv[kt], c);
+        if ((c & 1) == 0) cs[w][kt * 32 + acc_row((c >> 1) & 15, h)] += colsum;
+      }
+    }
+    if (qvalid && h == 0) {
+      P.lse[rowidx] = l > 0.f ? mx + __logf(l) : -INFINITY;
+      if (P.keep_bits) {
+        uint32_t wv[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt) wv[kt] = words[kt];
+        *reinterpret_cast<uint4*>(P.keep_bits + rowidx * 4) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+      }
+    }
+  }
+  __syncthreads();
+  const float inv_lq = 1.f / (float)Lq;
+  for (int k = t; k < Lk; k += NT) pbar[k] = (cs[0][k] + cs[1][k] + cs[2][k] + cs[3][k]) * inv_lq;
+}
+
+// Pooled backward, query on the lane: D = rowsum(P' dpbar)/Lq, dS, dQ.
+template <int HDP>
+__global__ __launch_bounds__(NT) void attn_pool_bwd_dq_kernel(const AttnArgs A) {
+  constexpr int LS = HDP + 4;
+  constexpr int HALF = HDP / 2;
+  constexpr int NDT = HDP / 32;
+  constexpr int NKT = PKC / 32;
+  __shared__ __attribute__((aligned(16))) float Ks[PKC * LS];
+  __shared__ float dpb[PKC];
+
+  const AttnPair& P = A.p[blockIdx.y];
+  const int qblocks = (P.Lq + 127) / 128;
+  int bid = blockIdx.x;
+  if (bid >= A.B * A.heads * qblocks) return;
+  const int qb = bid % qblocks;
+  bid /= qblocks;
+  const int head = bid % A.heads, b = bid / A.heads;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, c = lane & 31;
+  const int hd = A.hd, col0 = head * hd;
+  const int Lq = P.Lq, Lk = P.Lk;
+  const int q = qb * 128 + w * 32 + c;
+  const bool qvalid = q < Lq;
+  const int64_t bh = (int64_t)b * A.heads + head;
+  const int64_t rowidx = bh * Lq + q;
+  const float scale = A.scale, pdrop = A.drop_p;
+  const float inv_keep = pdrop < 1.f ? 1.f / (1.f - pdrop) : 0.f;
+  const float inv_lq = 1.f / (float)Lq;
+  float* qrow = P.dq + ((int64_t)b * Lq + (qvalid ? q : 0)) * P.ldq + col0;
+
+  if (P.kmask_mode == 1 && P.kmask[(int64_t)b * P.kmask_ld] == 0.f) {
+    if (qvalid) {
+      for (int d = h; d < hd; d += 2) qrow[d] = 0.f;
+      if (h == 0) P.dsum[rowidx] = 0.f;
+    }
+    return;
+  }
+  const bool vk = (P.ldk % 4 == 0) && (hd % 4 == 0);
+  load_rows<PKC, HDP, LS>(Ks, P.k + (int64_t)b * Lk * P.ldk + col0, Lk, P.ldk, 0, hd, vk);
+  for (int k = t; k < PKC; k += NT) dpb[k] = k < Lk ? P.dpbar[bh * Lk + k] : 0.f;
+  __syncthreads();
+  if (qb * 128 + w * 32 >= Lq) return;
+  const int nkt = (Lk + 31) / 32;
+  float qf[HALF];
+  load_frag<HALF>(qf, P.q + ((int64_t)b * Lq + (qvalid ? q : 0)) * P.ldq + col0, h * HALF, hd, qvalid);
+  const float lse = qvalid ? P.lse[rowidx] : -INFINITY;
+  uint4 kw = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+  if (P.keep_bits && pdrop > 0.f && qvalid) kw = *reinterpret_cast<const uint4*>(P.keep_bits + rowidx * 4);
+  const uint32_t kwa[4] = {kw.x, kw.y, kw.z, kw.w};
+  float pr[NKT][16];
+  float D = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    if (kt < nkt) {
+      f32x16 s = dot_rows<HALF>(Ks + (kt * 32 + c) * LS + h * HALF, qf, zero16());
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kt * 32 + acc_row(r, h);
+        const bool valid = qvalid && key < Lk && lse != -INFINITY &&
+                           (P.kmask_mode != 2 || kmask_val(P, b, key) != 0.f);
+        const float p = valid ? __expf(s[r] * scale - lse) : 0.f;
+        pr[kt][r] = p;
+        const bool keep = pdrop <= 0.f || ((kwa[kt] >> (key & 31)) & 1u);
+        D += keep ? p * inv_keep * dpb[key] : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) pr[kt][r] = 0.f;
+    }
+  }
+  D = (D + __shfl_xor(D, 32)) * inv_lq;
+  if (qvalid && h == 0) P.dsum[rowidx] = D;
+  f32x16 dq[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) dq[dt] = zero16();
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    if (kt >= nkt) break;
+    float ds[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = kt * 32 + acc_row(r, h);
+      const bool keep = pdrop <= 0.f || ((kwa[kt] >> (key & 31)) & 1u);
+      const float pd = keep ? pr[kt][r] * inv_keep : 0.f;
+      ds[r] = pd * dpb[key] * inv_lq - pr[kt][r] * D;
+    }
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        dq[dt] = mfma32(Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], ds[r], dq[dt]);
+  }
+  if (!qvalid) return;
+  const bool vo = (P.ldq % 4 == 0) && (hd % 4 == 0);
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d0 = dt * 32 + 8 * g + 4 * h;
+      if (vo && d0 + 3 < hd) {
+        *reinterpret_cast<float4*>(qrow + d0) =
+            make_float4(dq[dt][4 * g] * scale, dq[dt][4 * g + 1] * scale, dq[dt][4 * g + 2] * scale,
+                        dq[dt][4 * g + 3] * scale);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (d0 + j < hd) qrow[d0 + j] = dq[dt][4 * g + j] * scale;
+      }
+    }
+}
+
+// Pooled backward, key on the lane: dK = scale * dS^T Q (needs D from the dq kernel).
+template <int HDP>
+__global__ __launch_bounds__(NT) void attn_pool_bwd_dk_kernel(const AttnArgs A) {
+  constexpr int QC = 128;
+  constexpr int LS = HDP + 4;
+  constexpr int HALF = HDP / 2;
+  constexpr int NDT = HDP / 32;
+  __shared__ __attribute__((aligned(16))) float Qs[QC * LS];
+  __shared__ float lse_s[QC], dsum_s[QC];
+  __shared__ uint32_t kw_s[QC * 4];
+
+  const AttnPair& P = A.p[blockIdx.y];
+  const int kblocks = (P.Lk + 127) / 128;
+  int bid = blockIdx.x;
+  if (bid >= A.B * A.heads * kblocks) return;
+  const int kb = bid % kblocks;
+  bid /= kblocks;
+  const int head = bid % A.heads, b = bid / A.heads;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, c = lane & 31;
+  const int hd = A.hd, col0 = head * hd;
+  const int Lq = P.Lq, Lk = P.Lk;
+  const int key = kb * 128 + w * 32 + c;
+  const bool wave_active = kb * 128 + w * 32 < Lk;
+  bool kvalid = key < Lk;
+  if (kvalid && P.kmask_mode == 2) kvalid = kmask_val(P, b, key) != 0.f;
+  const int64_t bh = (int64_t)b * A.heads + head;
+  const float scale = A.scale, pdrop = A.drop_p;
+  const float inv_keep = pdrop < 1.f ? 1.f / (1.f - pdrop) : 0.f;
+  const float inv_lq = 1.f / (float)Lq;
+  const bool use_bits = P.keep_bits && pdrop > 0.f;
+
+  f32x16 dk[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) dk[dt] = zero16();
+  const bool sample_masked = (P.kmask_mode == 1 && P.kmask[(int64_t)b * P.kmask_ld] == 0.f);
+  if (!sample_masked) {
+    float kf[HALF];
+    load_frag<HALF>(kf, P.k + ((int64_t)b * Lk + (key < Lk ? key : 0)) * P.ldk + col0, h * HALF, hd,
+                    key < Lk);
+    const float dpk = key < Lk ? P.dpbar[bh * Lk + key] * inv_lq : 0.f;
+    const bool vq = (P.ldq % 4 == 0) && (hd % 4 == 0);
+    for (int qbase = 0; qbase < Lq; qbase += QC) {
+      __syncthreads();
+      load_rows<QC, HDP, LS>(Qs, P.q + (int64_t)b * Lq * P.ldq + col0, Lq, P.ldq, qbase, hd, vq);
+      for (int i = t; i < QC; i += NT) {
+        const int qq = qbase + i;
+        lse_s[i] = qq < Lq ? P.lse[bh * Lq + qq] : -INFINITY;
+        dsum_s[i] = qq < Lq ? P.dsum[bh * Lq + qq] : 0.f;
+      }
+      if (use_bits)
+        for (int i = t; i < QC * 4; i += NT) {
+          const int qq = qbase + i / 4;
+          kw_s[i] = qq < Lq ? P.keep_bits[(bh * Lq + qbase) * 4 + i] : 0u;
+        }
+      __syncthreads();
+      if (!wave_active) continue;
+      const int nqt = (min(QC, Lq - qbase) + 31) / 32;
+      for (int qt = 0; qt < nqt; ++qt) {
+        f32x16 s = dot_rows<HALF>(Qs + (qt * 32 + c) * LS + h * HALF, kf, zero16());
+        float ds[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ql = qt * 32 + acc_row(r, h);
+          const float lq = lse_s[ql];
+          const bool valid = kvalid && lq != -INFINITY && (qbase + ql < Lq);
+          const float p = valid ? __expf(s[r] * scale - lq) : 0.f;
+          bool keep = true;
+          if (use_bits) keep = (kw_s[ql * 4 + (key >> 5)] >> (key & 31)) & 1u;
+          const float pd = keep ? p * inv_keep : 0.f;
+          ds[r] = pd * dpk - p * dsum_s[ql];
+        }
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            dk[dt] = mfma32(ds[r], Qs[(qt * 32 + acc_row(r, h)) * LS + dt * 32 + c], dk[dt]);
+      }
+    }
+  }
+  if (!wave_active) return;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) {
+    const int d = dt * 32 + c;
+    if (d >= hd) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int kr = kb * 128 + w * 32 + acc_row(r, h);
+      if (kr < Lk) P.dk[((int64_t)b * Lk + kr) * P.ldk + col0 + d] = dk[dt][r] * scale;
+    }
+  }
+}
+
+enum class Kind { Fwd, Probs, Prep, Dkv, Dq, PoolFwd, PoolDq, PoolDk };
 
 hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, int heads, int hd,
                           float scale, float drop_p, const RngSnap* rng, hipStream_t st) {
@@ -526,8 +877,11 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
       if (kind == Kind::Prep)
         nb = prep_vec ? ((int64_t)B * P.Lq * (heads * hd / 4) + NT - 1) / NT
                       : ((int64_t)B * P.Lq * heads + NT - 1) / NT;
-      else if (kind == Kind::Dkv) nb = (int64_t)B * heads * ((P.Lk + 127) / 128);
+      else if (kind == Kind::Dkv || kind == Kind::PoolDk) nb = (int64_t)B * heads * ((P.Lk + 127) / 128);
+      else if (kind == Kind::PoolFwd) nb = (int64_t)B * heads;
       else nb = (int64_t)B * heads * ((P.Lq + 127) / 128);
+      if ((kind == Kind::PoolFwd || kind == Kind::PoolDq || kind == Kind::PoolDk) && P.Lk > PKC)
+        return hipErrorInvalidValue;
       if (nb > maxblk) maxblk = nb;
       ++n;
     }
@@ -562,6 +916,18 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
         if (small) hipLaunchKernelGGL((attn_bwd_dq_kernel<32>), grid, dim3(NT), 0, st, a);
         else hipLaunchKernelGGL((attn_bwd_dq_kernel<64>), grid, dim3(NT), 0, st, a);
         break;
+      case Kind::PoolFwd:
+        if (small) hipLaunchKernelGGL((attn_pool_fwd_kernel<32>), grid, dim3(NT), 0, st, a);
+        else hipLaunchKernelGGL((attn_pool_fwd_kernel<64>), grid, dim3(NT), 0, st, a);
+        break;
+      case Kind::PoolDq:
+        if (small) hipLaunchKernelGGL((attn_pool_bwd_dq_kernel<32>), grid, dim3(NT), 0, st, a);
+        else hipLaunchKernelGGL((attn_pool_bwd_dq_kernel<64>), grid, dim3(NT), 0, st, a);
+        break;
+      case Kind::PoolDk:
+        if (small) hipLaunchKernelGGL((attn_pool_bwd_dk_kernel<32>), grid, dim3(NT), 0, st, a);
+        else hipLaunchKernelGGL((attn_pool_bwd_dk_kernel<64>), grid, dim3(NT), 0, st, a);
+        break;
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -579,6 +945,17 @@ hipError_t launch_attn_fwd(const AttnPair* pairs, int npairs, int B, int heads, 
 hipError_t launch_attn_probs(const AttnPair* pairs, int npairs, int B, int heads, int hd,
                              float scale, float drop_p, const RngSnap* rng, hipStream_t st) {
   return launch_generic(Kind::Probs, pairs, npairs, B, heads, hd, scale, drop_p, rng, st);
+}
+
+hipError_t launch_attn_pool_fwd(const AttnPair* pairs, int npairs, int B, int heads, int hd, float scale,
+                                float drop_p, const RngSnap* rng, hipStream_t st) {
+  return launch_generic(Kind::PoolFwd, pairs, npairs, B, heads, hd, scale, drop_p, rng, st);
+}
+
+hipError_t launch_attn_pool_bwd(int stage, const AttnPair* pairs, int npairs, int B, int heads, int hd,
+                                float scale, float drop_p, const RngSnap* rng, hipStream_t st) {
+  return launch_generic(stage == 0 ? Kind::PoolDq : Kind::PoolDk, pairs, npairs, B, heads, hd, scale,
+                        drop_p, rng, st);
 }
 
 hipError_t launch_attn_bwd_stage(int stage, const AttnPair* pairs, int npairs, int B, int heads, int hd,

@@ -198,10 +198,10 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const GemmArgs args) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int i = i0 + wm * 64 + a * 32 + acc_row(r, h);
-          if (i < G.M) out[(int64_t)i * G.N + j] = acc[a][b][r];
+          if (i < G.M) out[(int64_t)i * G.N + j] = acc[a][b][r] * G.alpha;
         }
       }
-    if (want_db && t < BM && i0 + t < G.M) G.part_db[(int64_t)split * G.M + i0 + t] = dbsum;
+    if (want_db && t < BM && i0 + t < G.M) G.part_db[(int64_t)split * G.M + i0 + t] = dbsum * G.alpha;
     return;
   }
   const int epi = G.epi;
@@ -216,8 +216,12 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const GemmArgs args) {
       for (int r = 0; r < 16; ++r) {
         const int i = i0 + wm * 64 + a * 32 + acc_row(r, h);
         if (i >= G.M) continue;
-        float v = acc[a][b][r] + bj;
-        if (epi & EPI_ROWADD) v += G.rowadd[(int64_t)(i / G.rowadd_div) * G.ld_rowadd + j];
+        float v = acc[a][b][r] * G.alpha;
+        if (epi & EPI_BIAS_RS) v += bj * G.bias_rs[(int64_t)i * G.bias_rs_ld + G.bias_rs_off];
+        else v += bj;
+        if (epi & EPI_ROWADD)
+          v += G.rowadd_scale * G.rowadd[(int64_t)(i / G.rowadd_div) * G.ld_rowadd + j];
+        if (epi & EPI_ADDMAT) v += G.addm[(int64_t)i * G.ld_addm + j];
         if (epi & EPI_RELU) v = fmaxf(v, 0.f);
         if (epi & EPI_GATE) v = G.gate[(int64_t)i * G.ld_gate + j] > 0.f ? v * G.gate_scale : 0.f;
         if (epi & EPI_ROWSCALE) v *= G.rowscale[(int64_t)(i / G.rs_div) * G.rs_stride + G.rs_off];

@@ -70,14 +70,17 @@ __global__ __launch_bounds__(NT) void head_fwd_kernel(const HeadArgs a) {
   for (int m = 0; m < M; ++m) {
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     if (active) {
-      const int L = a.L[m];
       for (int si = 0; si < a.nsrc; ++si) {
         if (a.src_mod[si] != m) continue;
+        const int L = a.src_L[si];
+        const float sc = a.src_scale[si];
         const float* base = a.src[si] + (int64_t)b * L * H + 4 * cg;
+        float4 part = make_float4(0.f, 0.f, 0.f, 0.f);
         for (int r = rg; r < L; r += RG) {
           const float4 v = *reinterpret_cast<const float4*>(base + (int64_t)r * H);
-          acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+          part.x += v.x; part.y += v.y; part.z += v.z; part.w += v.w;
         }
+        acc.x += part.x * sc; acc.y += part.y * sc; acc.z += part.z * sc; acc.w += part.w * sc;
       }
     }
     red4[t] = acc;

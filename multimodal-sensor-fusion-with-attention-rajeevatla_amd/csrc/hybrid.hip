@@ -1,0 +1,570 @@
+// HybridFusion C-ABI entry points (include/mmfusion.h): native orchestration of
+// the forward and backward of src/fusion.py::HybridFusion (forward :331-427,
+// compute_adaptive_weights :429-479) on the libmmfusion kernels.
+//
+// Two execution plans compute the same function:
+//  * pooled (default; every key modality has L <= 128 and heads <= 8): the
+//    attended features are consumed only through their mean over L, so
+//    mean_q(P' V) W_o^T + b_o is evaluated as (pbar P_k) W_v^T ... on B rows
+//    (attention.hip "Pooled-output attention", pool.hip).  No V / O / attended
+//    (B, L, H) tensors exist and the backward needs no dO V^T / dV products.
+//  * general (fallback): per-pair Q/K/V projections, flash attention
+//    (O = softmax(QK^T) V), out_proj on every row, L-mean in the head.
+// Both are exact reformulations (fp32 reassociation only) of the reference.
+#include <cmath>
+
+#include "capi_util.h"
+
+using namespace mmf;
+
+namespace {
+
+inline int Lm(const mmf_hybrid_desc* d, int m) { return d->seq_len[m] > 0 ? d->seq_len[m] : 1; }
+inline bool dropping(const mmf_hybrid_desc* d) { return d->training && d->dropout > 0.f; }
+
+bool use_pool(const mmf_hybrid_desc* d) {
+  if (d->num_heads > 8) return false;
+  for (int g = 0; g < d->num_pairs; ++g)
+    if (Lm(d, d->pair_k[g]) > 128) return false;
+  return true;
+}
+
+struct Saved {
+  RngSnap* rng;
+  float* P[MMF_MAX_MODALITIES];
+  float *Q[MMF_MAX_PAIRS], *K[MMF_MAX_PAIRS], *lse[MMF_MAX_PAIRS];
+  // general plan
+  float *V[MMF_MAX_PAIRS], *O[MMF_MAX_PAIRS], *A[MMF_MAX_PAIRS];
+  // pooled plan
+  float *pbar[MMF_MAX_PAIRS], *U[MMF_MAX_PAIRS], *r[MMF_MAX_PAIRS], *Ob[MMF_MAX_PAIRS], *Ab[MMF_MAX_PAIRS];
+  uint32_t* bits[MMF_MAX_PAIRS];
+  float *pooled, *scores, *weights, *fused, *h1;
+};
+
+void layout_saved(const mmf_hybrid_desc* d, Bump& bp, Saved& s) {
+  memset(&s, 0, sizeof(s));
+  const size_t B = d->batch, H = d->hidden, M = d->num_modalities, nh = d->num_heads;
+  const bool pool = use_pool(d);
+  s.rng = bp.take<RngSnap>(1);
+  for (int m = 0; m < d->num_modalities; ++m) s.P[m] = bp.take<float>(B * Lm(d, m) * H);
+  for (int g = 0; g < d->num_pairs; ++g) {
+    const size_t lq = Lm(d, d->pair_q[g]), lk = Lm(d, d->pair_k[g]);
+    s.Q[g] = bp.take<float>(B * lq * H);
+    s.K[g] = bp.take<float>(B * lk * H);
+    s.lse[g] = bp.take<float>(B * nh * lq);
+    if (pool) {
+      s.pbar[g] = bp.take<float>(B * nh * lk);
+      s.U[g] = bp.take<float>(B * nh * H);
+      s.r[g] = bp.take<float>(B * nh);
+      s.Ob[g] = bp.take<float>(B * H);
+      s.Ab[g] = bp.take<float>(B * H);
+      if (dropping(d)) s.bits[g] = bp.take<uint32_t>(B * nh * lq * 4);
+    } else {
+      s.V[g] = bp.take<float>(B * lk * H);
+      s.O[g] = bp.take<float>(B * lq * H);
+      s.A[g] = bp.take<float>(B * lq * H);
+    }
+  }
+  s.pooled = bp.take<float>(B * M * H);
+  s.scores = bp.take<float>(B * M);
+  s.weights = bp.take<float>(B * M);
+  s.fused = bp.take<float>(B * H);
+  s.h1 = bp.take<float>(B * H);
+}
+
+struct Ws {
+  float *dz1, *dfused, *cvec, *dscore;
+  float *dQ[MMF_MAX_PAIRS], *dK[MMF_MAX_PAIRS], *dsum[MMF_MAX_PAIRS];
+  float *dO[MMF_MAX_PAIRS], *dV[MMF_MAX_PAIRS];                              // general
+  float *dOb[MMF_MAX_PAIRS], *dU[MMF_MAX_PAIRS], *dpbar[MMF_MAX_PAIRS];      // pooled
+  float* E[MMF_MAX_MODALITIES];                                              // pooled
+  float* dZ[MMF_MAX_MODALITIES];
+};
+
+void layout_ws(const mmf_hybrid_desc* d, Bump& bp, Ws& w) {
+  memset(&w, 0, sizeof(w));
+  const size_t B = d->batch, H = d->hidden, M = d->num_modalities, nh = d->num_heads;
+  const bool pool = use_pool(d);
+  w.dz1 = bp.take<float>(B * H);
+  w.dfused = bp.take<float>(B * H);
+  w.cvec = bp.take<float>(B * M * H);
+  w.dscore = bp.take<float>(B * M);
+  for (int g = 0; g < d->num_pairs; ++g) {
+    const size_t lq = Lm(d, d->pair_q[g]), lk = Lm(d, d->pair_k[g]);
+    w.dQ[g] = bp.take<float>(B * lq * H);
+    w.dK[g] = bp.take<float>(B * lk * H);
+    w.dsum[g] = bp.take<float>(B * nh * lq);
+    if (pool) {
+      w.dOb[g] = bp.take<float>(B * H);
+      w.dU[g] = bp.take<float>(B * nh * H);
+      w.dpbar[g] = bp.take<float>(B * nh * lk);
+    } else {
+      w.dO[g] = bp.take<float>(B * lq * H);
+      w.dV[g] = bp.take<float>(B * lk * H);
+    }
+  }
+  for (int m = 0; m < d->num_modalities; ++m) {
+    if (pool) w.E[m] = bp.take<float>(B * Lm(d, m) * H);
+    w.dZ[m] = bp.take<float>(B * Lm(d, m) * H);
+  }
+}
+
+int check_hybrid(const mmf_hybrid_desc* d) {
+  if (!d) return fail(MMF_EINVAL, "null descriptor");
+  if (d->batch < 1) return fail(MMF_EINVAL, "batch must be >= 1 (got %d)", d->batch);
+  if (d->num_modalities < 1 || d->num_modalities > MMF_MAX_MODALITIES)
+    return fail(MMF_ELIMIT, "num_modalities must be in [1, %d] (got %d)", MMF_MAX_MODALITIES,
+                d->num_modalities);
+  if (d->num_heads < 1 || d->hidden % d->num_heads != 0)
+    return fail(MMF_EINVAL, "hidden_dim (%d) must be divisible by num_heads (%d)", d->hidden,
+                d->num_heads);
+  if (d->hidden / d->num_heads > MMF_MAX_HEAD_DIM)
+    return fail(MMF_ELIMIT, "head_dim %d > %d is not supported by the HIP kernels",
+                d->hidden / d->num_heads, MMF_MAX_HEAD_DIM);
+  if (d->hidden % 4 != 0 || d->hidden > 1024)
+    return fail(MMF_ELIMIT, "hidden_dim must be a multiple of 4 and <= 1024 (got %d)", d->hidden);
+  if (d->num_classes < 1) return fail(MMF_EINVAL, "num_classes must be >= 1");
+  if (d->num_pairs < 0 || d->num_pairs > d->num_modalities * (d->num_modalities - 1))
+    return fail(MMF_EINVAL, "bad num_pairs %d", d->num_pairs);
+  for (int m = 0; m < d->num_modalities; ++m) {
+    if (d->in_dim[m] < 1) return fail(MMF_EINVAL, "in_dim[%d] must be >= 1", m);
+    if (d->seq_len[m] < 0) return fail(MMF_EINVAL, "seq_len[%d] must be >= 0", m);
+  }
+  for (int g = 0; g < d->num_pairs; ++g) {
+    const int q = d->pair_q[g], k = d->pair_k[g];
+    if (q < 0 || k < 0 || q >= d->num_modalities || k >= d->num_modalities || q == k)
+      return fail(MMF_EINVAL, "bad pair %d: (%d, %d)", g, q, k);
+  }
+  if (!(d->dropout >= 0.f && d->dropout < 1.f))
+    return fail(MMF_EINVAL, "dropout must be in [0, 1) (got %g)", (double)d->dropout);
+  return MMF_OK;
+}
+
+// Every weight gradient as a split-K job; the same code sizes the workspace
+// (called with null bases) and plans the real launch.
+void plan_wgrads(const mmf_hybrid_desc* d, const float* const* x, const float* mask,
+                 const float* dlogits, const Saved& s, const Ws& w, const mmf_hybrid_grads* G,
+                 Bump& bw, WgradPlan& wp) {
+  const int B = d->batch, M = d->num_modalities, H = d->hidden, C = d->num_classes;
+  const int nh = d->num_heads, hd = H / nh;
+  const bool pool = use_pool(d);
+  static const mmf_hybrid_grads kNull = {};
+  const mmf_hybrid_grads* g = G ? G : &kNull;
+  plan_wgrad(wp, bw, C, H, B, opnd(dlogits, C), opnd(s.h1, H), g->cls2.w, g->cls2.b);
+  plan_wgrad(wp, bw, H, H, B, opnd(w.dz1, H), opnd(s.fused, H), g->cls1.w, g->cls1.b);
+  // gating_layers[m]: dscore[:, m]^T pooled[:, m, :]
+  for (int m = 0; m < M; ++m)
+    plan_wgrad(wp, bw, 1, H, B, opnd(w.dscore ? w.dscore + m : nullptr, M),
+               opnd(s.pooled ? s.pooled + (size_t)m * H : nullptr, M * H), g->gate[m].w, g->gate[m].b);
+  for (int p = 0; p < d->num_pairs; ++p) {
+    const int q = d->pair_q[p], k = d->pair_k[p];
+    const int lq = Lm(d, q), lk = Lm(d, k);
+    const float* cq = w.cvec ? w.cvec + (size_t)q * H : nullptr;
+    if (pool) {
+      plan_wgrad(wp, bw, H, H, B, opnd(cq, M * H), opnd(s.Ob[p], H), g->o[p].w, g->o[p].b);
+      for (int hh = 0; hh < nh; ++hh) {
+        const float* dob = w.dOb[p] ? w.dOb[p] + hh * hd : nullptr;
+        plan_wgrad(wp, bw, hd, H, B, opnd(dob, H), opnd(s.U[p] ? s.U[p] + (size_t)hh * H : nullptr, nh * H),
+                   g->v[p].w ? g->v[p].w + (size_t)hh * hd * H : nullptr, nullptr, false);
+        // value_proj.bias slice = sum_b r_h[b] dObar_h[b]  (Obar_h = U_h W_v,h^T + r_h b_v,h)
+        plan_wgrad(wp, bw, hd, 1, B, opnd(dob, H), opnd(s.r[p] ? s.r[p] + hh : nullptr, nh),
+                   g->v[p].b ? g->v[p].b + hh * hd : nullptr, nullptr, false);
+      }
+    } else {
+      plan_wgrad(wp, bw, H, H, B * lq, opnd(cq, M * H, lq), opnd(s.O[p], H), g->o[p].w, g->o[p].b,
+                 1.f / (float)lq);
+      plan_wgrad(wp, bw, H, H, B * lk, opnd(w.dV[p], H), opnd(s.P[k], H), g->v[p].w, g->v[p].b);
+    }
+    plan_wgrad(wp, bw, H, H, B * lq, opnd(w.dQ[p], H), opnd(s.P[q], H), g->q[p].w, g->q[p].b);
+    plan_wgrad(wp, bw, H, H, B * lk, opnd(w.dK[p], H), opnd(s.P[k], H), g->k[p].w, g->k[p].b);
+  }
+  for (int m = 0; m < M; ++m) {
+    const int L = Lm(d, m), D = d->in_dim[m];
+    Xform xf;
+    memset(&xf, 0, sizeof(xf));
+    xf.rowscale = mask; xf.rs_div = L; xf.rs_stride = M; xf.rs_off = m;
+    xf.drop_site = dropping(d) ? SITE_IN + m : 0;
+    xf.ncols = D;
+    plan_wgrad(wp, bw, H, D, B * L, opnd(w.dZ[m], H), opnd(x ? x[m] : nullptr, D), g->proj[m].w,
+               g->proj[m].b, 1.f, &xf);
+  }
+}
+
+size_t saved_bytes(const mmf_hybrid_desc* d) {
+  Bump bp(nullptr);
+  Saved s;
+  layout_saved(d, bp, s);
+  return bp.off + 256;
+}
+
+size_t workspace_bytes(const mmf_hybrid_desc* d) {
+  Bump bs(nullptr);
+  Saved s;
+  layout_saved(d, bs, s);
+  Bump bw(nullptr);
+  Ws w;
+  layout_ws(d, bw, w);
+  WgradPlan wp;
+  plan_wgrads(d, nullptr, nullptr, nullptr, s, w, nullptr, bw, wp);
+  return bw.off + 256;
+}
+
+void fill_head(HeadArgs& ha, const mmf_hybrid_desc* d, const mmf_hybrid_params* W, const float* mask,
+               const Saved& s) {
+  const bool pool = use_pool(d);
+  memset(&ha, 0, sizeof(ha));
+  ha.B = d->batch; ha.M = d->num_modalities; ha.H = d->hidden; ha.mask = mask;
+  ha.scale_by_mask = 1;
+  int cnt[MMF_MAX_MODALITIES];
+  for (int m = 0; m < d->num_modalities; ++m) {
+    ha.src[ha.nsrc] = s.P[m];
+    ha.src_mod[ha.nsrc] = m;
+    ha.src_L[ha.nsrc] = Lm(d, m);
+    ha.src_scale[ha.nsrc++] = 1.f / (float)Lm(d, m);
+    cnt[m] = 1;
+    ha.gate_w[m] = W->gate[m].w;
+    ha.gate_b[m] = W->gate[m].b;
+  }
+  for (int g = 0; g < d->num_pairs; ++g) {
+    const int q = d->pair_q[g];
+    ha.src[ha.nsrc] = pool ? s.Ab[g] : s.A[g];
+    ha.src_mod[ha.nsrc] = q;
+    ha.src_L[ha.nsrc] = pool ? 1 : Lm(d, q);
+    ha.src_scale[ha.nsrc++] = pool ? 1.f : 1.f / (float)Lm(d, q);
+    cnt[q]++;
+  }
+  for (int m = 0; m < d->num_modalities; ++m) ha.inv_cnt[m] = 1.0f / (float)cnt[m];
+  ha.pooled = s.pooled; ha.scores = s.scores; ha.weights = s.weights; ha.fused = s.fused;
+}
+
+AttnPair make_pair(const mmf_hybrid_desc* d, const Saved& s, const float* mask, int g) {
+  AttnPair a;
+  memset(&a, 0, sizeof(a));
+  const int q = d->pair_q[g], k = d->pair_k[g];
+  a.q = s.Q[g]; a.k = s.K[g]; a.v = s.V[g]; a.o = s.O[g]; a.lse = s.lse[g];
+  a.kmask = mask + k; a.kmask_mode = 1; a.kmask_ld = d->num_modalities;
+  a.Lq = Lm(d, q); a.Lk = Lm(d, k);
+  a.ldq = a.ldk = a.ldv = a.ldo = d->hidden;
+  a.drop_site = SITE_ATTN + g;
+  a.pbar = s.pbar[g];
+  a.keep_bits = s.bits[g];
+  return a;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t mmf_hybrid_saved_bytes(const mmf_hybrid_desc* d) {
+  if (check_hybrid(d) != MMF_OK) return 0;
+  return saved_bytes(d);
+}
+
+size_t mmf_hybrid_workspace_bytes(const mmf_hybrid_desc* d) {
+  if (check_hybrid(d) != MMF_OK) return 0;
+  return workspace_bytes(d);
+}
+
+int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, const float* const* x,
+                       const float* mask, const uint64_t* rng_state, void* saved, float* logits,
+                       float* fusion_weights, float* const* attn_maps, void* stream) {
+  int rc = check_hybrid(d);
+  if (rc) return rc;
+  if (!W || !x || !mask || !saved || !logits) return fail(MMF_EINVAL, "null argument");
+  hipStream_t st = (hipStream_t)stream;
+  const int B = d->batch, M = d->num_modalities, H = d->hidden, C = d->num_classes;
+  const int nh = d->num_heads, hd = H / nh;
+  const bool drop = dropping(d);
+  const float p = drop ? d->dropout : 0.f;
+  const bool pool = use_pool(d);
+  if (drop && !rng_state) return fail(MMF_EINVAL, "training with dropout needs rng_state");
+
+  Bump bp(saved);
+  Saved s;
+  layout_saved(d, bp, s);
+  if (rng_state) STAGE_TRY("fwd.rng", launch_rng_snapshot(rng_state, s.rng, st));
+  const RngSnap* rng = rng_state ? s.rng : nullptr;
+
+  // (1) per-modality projection: P_m = Drop(ReLU(Drop(X_m * mask_m) W_m^T + b_m))  (fusion.py:364-374)
+  {
+    std::vector<GemmJob> jobs;
+    for (int m = 0; m < M; ++m) {
+      const int L = Lm(d, m), D = d->in_dim[m];
+      GemmJob j = make_job(B * L, H, s.P[m], H, EPI_BIAS | EPI_RELU | (drop ? EPI_DROP : 0));
+      j.g.bias = W->proj[m].b;
+      j.g.drop_site = SITE_PROJ + m;
+      add_src(j, opnd(x[m], D), opnd(W->proj[m].w, D), D);
+      j.has_xf_a[0] = 1;
+      Xform& xf = j.xf_a[0];
+      xf.rowscale = mask; xf.rs_div = L; xf.rs_stride = M; xf.rs_off = m;
+      xf.drop_site = drop ? SITE_IN + m : 0;
+      xf.ncols = D;
+      jobs.push_back(j);
+    }
+    STAGE_TRY("fwd.proj_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, p, rng, st));
+  }
+  // (2) Q/K (and V for the general plan) projections of every present pair (attention.py:104-106)
+  if (d->num_pairs) {
+    std::vector<GemmJob> jobs;
+    for (int g = 0; g < d->num_pairs; ++g) {
+      const int q = d->pair_q[g], k = d->pair_k[g];
+      const int lq = Lm(d, q), lk = Lm(d, k);
+      GemmJob jq = make_job(B * lq, H, s.Q[g], H, EPI_BIAS);
+      jq.g.bias = W->q[g].b;
+      add_src(jq, opnd(s.P[q], H), opnd(W->q[g].w, H), H);
+      jobs.push_back(jq);
+      GemmJob jk = make_job(B * lk, H, s.K[g], H, EPI_BIAS);
+      jk.g.bias = W->k[g].b;
+      add_src(jk, opnd(s.P[k], H), opnd(W->k[g].w, H), H);
+      jobs.push_back(jk);
+      if (!pool) {
+        GemmJob jv = make_job(B * lk, H, s.V[g], H, EPI_BIAS);
+        jv.g.bias = W->v[g].b;
+        add_src(jv, opnd(s.P[k], H), opnd(W->v[g].w, H), H);
+        jobs.push_back(jv);
+      }
+    }
+    STAGE_TRY("fwd.qkv_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, 0.f, rng, st));
+  }
+  std::vector<AttnPair> pairs(d->num_pairs);
+  for (int g = 0; g < d->num_pairs; ++g) pairs[g] = make_pair(d, s, mask, g);
+  const float scale = 1.0f / std::sqrt((float)hd);
+  if (d->num_pairs && pool) {
+    // (3p) attention -> LSE, pbar = mean_q P'; U = pbar P_k; Obar = U W_v^T + r b_v; Abar = out_proj
+    STAGE_TRY("fwd.attn", launch_attn_pool_fwd(pairs.data(), d->num_pairs, B, nh, hd, scale, p, rng, st));
+    std::vector<PoolPair> pp(d->num_pairs);
+    for (int g = 0; g < d->num_pairs; ++g) {
+      memset(&pp[g], 0, sizeof(PoolPair));
+      pp[g].pk = s.P[d->pair_k[g]];
+      pp[g].Lk = Lm(d, d->pair_k[g]);
+      pp[g].pbar = s.pbar[g];
+      pp[g].u = s.U[g];
+      pp[g].r = s.r[g];
+    }
+    STAGE_TRY("fwd.pool_u", launch_pool_u(pp.data(), d->num_pairs, B, nh, hd, H, st));
+    std::vector<GemmJob> jobs;
+    for (int g = 0; g < d->num_pairs; ++g)
+      for (int hh = 0; hh < nh; ++hh) {
+        GemmJob j = make_job(B, hd, s.Ob[g] + hh * hd, H, EPI_BIAS | EPI_BIAS_RS);
+        j.g.bias = W->v[g].b + hh * hd;
+        j.g.bias_rs = s.r[g];
+        j.g.bias_rs_ld = nh;
+        j.g.bias_rs_off = hh;
+        add_src(j, opnd(s.U[g] + (size_t)hh * H, nh * H), opnd(W->v[g].w + (size_t)hh * hd * H, H), H);
+        jobs.push_back(j);
+      }
+    STAGE_TRY("fwd.vbar_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, 0.f, rng, st));
+    jobs.clear();
+    for (int g = 0; g < d->num_pairs; ++g) {
+      GemmJob j = make_job(B, H, s.Ab[g], H, EPI_BIAS);
+      j.g.bias = W->o[g].b;
+      add_src(j, opnd(s.Ob[g], H), opnd(W->o[g].w, H), H);
+      jobs.push_back(j);
+    }
+    STAGE_TRY("fwd.out_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, 0.f, rng, st));
+  } else if (d->num_pairs) {
+    // (3g) flash attention per pair (key mask = modality mask column k, fusion.py:391-401) + out_proj
+    STAGE_TRY("fwd.attn", launch_attn_fwd(pairs.data(), d->num_pairs, B, nh, hd, scale, p, rng, st));
+    std::vector<GemmJob> jobs;
+    for (int g = 0; g < d->num_pairs; ++g) {
+      const int lq = Lm(d, d->pair_q[g]);
+      GemmJob j = make_job(B * lq, H, s.A[g], H, EPI_BIAS);
+      j.g.bias = W->o[g].b;
+      add_src(j, opnd(s.O[g], H), opnd(W->o[g].w, H), H);
+      jobs.push_back(j);
+    }
+    STAGE_TRY("fwd.out_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, 0.f, rng, st));
+  }
+  // (4) aggregation + pooling + gating + adaptive weights + weighted sum (fusion.py:406-418)
+  HeadArgs ha;
+  fill_head(ha, d, W, mask, s);
+  ha.weights_out = fusion_weights;
+  STAGE_TRY("fwd.head", launch_head_fwd(ha, st));
+  // (5) classifier: Linear -> ReLU -> Dropout -> Linear (fusion.py:323-328)
+  {
+    GemmJob j = make_job(B, H, s.h1, H, EPI_BIAS | EPI_RELU | (drop ? EPI_DROP : 0));
+    j.g.bias = W->cls1.b;
+    j.g.drop_site = SITE_CLS;
+    add_src(j, opnd(s.fused, H), opnd(W->cls1.w, H), H);
+    STAGE_TRY("fwd.cls1_gemm", launch_gemm(&j, 1, MODE_RK, MODE_RK, p, rng, st));
+    GemmJob j2 = make_job(B, C, logits, C, EPI_BIAS);
+    j2.g.bias = W->cls2.b;
+    add_src(j2, opnd(s.h1, H), opnd(W->cls2.w, H), H);
+    STAGE_TRY("fwd.cls2_gemm", launch_gemm(&j2, 1, MODE_RK, MODE_RK, 0.f, rng, st));
+  }
+  // (6) optional attention maps (post-dropout, attention.py:130,144-146)
+  if (d->return_attention && attn_maps && d->num_pairs) {
+    std::vector<AttnPair> pp;
+    for (int g = 0; g < d->num_pairs; ++g)
+      if (attn_maps[g]) {
+        pp.push_back(pairs[g]);
+        pp.back().probs = attn_maps[g];
+      }
+    if (!pp.empty())
+      STAGE_TRY("fwd.attn_probs", launch_attn_probs(pp.data(), (int)pp.size(), B, nh, hd, scale, p, rng, st));
+  }
+  return MMF_OK;
+}
+
+int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, const float* const* x,
+                        const float* mask, const void* saved, const float* dlogits, void* workspace,
+                        const mmf_hybrid_grads* G, float* const* dx, void* stream) {
+  int rc = check_hybrid(d);
+  if (rc) return rc;
+  if (!W || !x || !mask || !saved || !dlogits || !workspace || !G)
+    return fail(MMF_EINVAL, "null argument");
+  hipStream_t st = (hipStream_t)stream;
+  const int B = d->batch, M = d->num_modalities, H = d->hidden, C = d->num_classes;
+  const int nh = d->num_heads, hd = H / nh;
+  const bool drop = dropping(d);
+  const float p = drop ? d->dropout : 0.f;
+  const float gscale = drop ? 1.f / (1.f - p) : 1.f;
+  const bool pool = use_pool(d);
+
+  Bump bs(const_cast<void*>(saved));
+  Saved s;
+  layout_saved(d, bs, s);
+  const RngSnap* rng = s.rng;
+  Bump bw(workspace);
+  Ws w;
+  layout_ws(d, bw, w);
+  WgradPlan wp;
+  plan_wgrads(d, x, mask, dlogits, s, w, G, bw, wp);
+  if (bw.off > workspace_bytes(d)) return fail(MMF_EINVAL, "internal: workspace overflow");
+
+  // (1) classifier backward: dz1 = ReLU'/Dropout' (dlogits W2), dfused = dz1 W1
+  {
+    GemmJob j = make_job(B, H, w.dz1, H, EPI_GATE);
+    j.g.gate = s.h1; j.g.ld_gate = H; j.g.gate_scale = gscale;
+    add_src(j, opnd(dlogits, C), opnd(W->cls2.w, H), C);
+    STAGE_TRY("bwd.cls_dz1_gemm", launch_gemm(&j, 1, MODE_RK, MODE_KR, 0.f, rng, st));
+    GemmJob j2 = make_job(B, H, w.dfused, H, 0);
+    add_src(j2, opnd(w.dz1, H), opnd(W->cls1.w, H), H);
+    STAGE_TRY("bwd.cls_dfused_gemm", launch_gemm(&j2, 1, MODE_RK, MODE_KR, 0.f, rng, st));
+  }
+  // (2) head backward: dscore and c_m = dpooled_m * mask_m / n_m
+  {
+    HeadArgs ha;
+    fill_head(ha, d, W, mask, s);
+    ha.dfused = w.dfused; ha.cvec = w.cvec; ha.dscore = w.dscore;
+    STAGE_TRY("bwd.head", launch_head_bwd(ha, st));
+  }
+  const float scale = 1.0f / std::sqrt((float)hd);
+  std::vector<AttnPair> pairs(d->num_pairs);
+  for (int g = 0; g < d->num_pairs; ++g) {
+    pairs[g] = make_pair(d, s, mask, g);
+    pairs[g].dsum = w.dsum[g]; pairs[g].dq = w.dQ[g]; pairs[g].dk = w.dK[g];
+    pairs[g].dout = w.dO[g]; pairs[g].dv = w.dV[g]; pairs[g].dpbar = w.dpbar[g];
+  }
+  if (d->num_pairs && pool) {
+    // (3p) dObar = dAbar W_o (dAbar = c_q); dU_h = dObar_h W_v,h; dpbar; attention dQ/dK; E_m
+    std::vector<GemmJob> jobs;
+    for (int g = 0; g < d->num_pairs; ++g) {
+      GemmJob j = make_job(B, H, w.dOb[g], H, 0);
+      add_src(j, opnd(w.cvec + (size_t)d->pair_q[g] * H, M * H), opnd(W->o[g].w, H), H);
+      jobs.push_back(j);
+    }
+    STAGE_TRY("bwd.out_dO_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, 0.f, rng, st));
+    jobs.clear();
+    for (int g = 0; g < d->num_pairs; ++g)
+      for (int hh = 0; hh < nh; ++hh) {
+        GemmJob j = make_job(B, H, w.dU[g] + (size_t)hh * H, nh * H, 0);
+        add_src(j, opnd(w.dOb[g] + hh * hd, H), opnd(W->v[g].w + (size_t)hh * hd * H, H), hd);
+        jobs.push_back(j);
+      }
+    STAGE_TRY("bwd.du_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, 0.f, rng, st));
+    std::vector<PoolPair> pp(d->num_pairs);
+    for (int g = 0; g < d->num_pairs; ++g) {
+      memset(&pp[g], 0, sizeof(PoolPair));
+      pp[g].pk = s.P[d->pair_k[g]];
+      pp[g].Lk = Lm(d, d->pair_k[g]);
+      pp[g].du = w.dU[g];
+      pp[g].dob = w.dOb[g];
+      pp[g].bv = W->v[g].b;
+      pp[g].dpbar = w.dpbar[g];
+    }
+    STAGE_TRY("bwd.pool_dpbar", launch_pool_dpbar(pp.data(), d->num_pairs, B, nh, hd, H, st));
+    STAGE_TRY("bwd.attn_dq", launch_attn_pool_bwd(0, pairs.data(), d->num_pairs, B, nh, hd, scale, p, rng, st));
+    STAGE_TRY("bwd.attn_dk", launch_attn_pool_bwd(1, pairs.data(), d->num_pairs, B, nh, hd, scale, p, rng, st));
+    std::vector<PoolEMod> em(M);
+    for (int m = 0; m < M; ++m) {
+      memset(&em[m], 0, sizeof(PoolEMod));
+      em[m].out = w.E[m];
+      em[m].L = Lm(d, m);
+      em[m].c = w.cvec + (size_t)m * H;
+      em[m].ldc = M * H;
+      em[m].cscale = 1.f / (float)Lm(d, m);
+      for (int g = 0; g < d->num_pairs; ++g)
+        if (d->pair_k[g] == m) {
+          em[m].pbar[em[m].nsrc] = s.pbar[g];
+          em[m].du[em[m].nsrc++] = w.dU[g];
+        }
+    }
+    STAGE_TRY("bwd.pool_e", launch_pool_e(em.data(), M, B, nh, H, st));
+  } else if (d->num_pairs) {
+    // (3g) dA_g rows = c_q / L_q broadcast: dO = dA W_o; flash attention backward
+    std::vector<GemmJob> jobs;
+    for (int g = 0; g < d->num_pairs; ++g) {
+      const int q = d->pair_q[g], lq = Lm(d, q);
+      GemmJob j = make_job(B * lq, H, w.dO[g], H, 0);
+      j.g.alpha = 1.f / (float)lq;
+      add_src(j, opnd(w.cvec + (size_t)q * H, M * H, lq), opnd(W->o[g].w, H), H);
+      jobs.push_back(j);
+    }
+    STAGE_TRY("bwd.out_dO_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, 0.f, rng, st));
+    STAGE_TRY("bwd.attn_prep", launch_attn_bwd_stage(0, pairs.data(), d->num_pairs, B, nh, hd, scale, p, rng, st));
+    STAGE_TRY("bwd.attn_dkv", launch_attn_bwd_stage(1, pairs.data(), d->num_pairs, B, nh, hd, scale, p, rng, st));
+    STAGE_TRY("bwd.attn_dq", launch_attn_bwd_stage(2, pairs.data(), d->num_pairs, B, nh, hd, scale, p, rng, st));
+  }
+  // (4) dZ_m = gate(P_m) * [direct + sum_q dQ W_q + sum_k dK W_k (+ dV W_v)]
+  {
+    std::vector<GemmJob> jobs;
+    for (int m = 0; m < M; ++m) {
+      const int L = Lm(d, m);
+      GemmJob j = make_job(B * L, H, w.dZ[m], H, EPI_GATE | (pool ? EPI_ADDMAT : EPI_ROWADD));
+      if (pool) {
+        j.g.addm = w.E[m];
+        j.g.ld_addm = H;
+      } else {
+        j.g.rowadd = w.cvec + (size_t)m * H;
+        j.g.ld_rowadd = M * H;
+        j.g.rowadd_div = L;
+        j.g.rowadd_scale = 1.f / (float)L;
+      }
+      j.g.gate = s.P[m];
+      j.g.ld_gate = H;
+      j.g.gate_scale = gscale;
+      for (int g = 0; g < d->num_pairs; ++g) {
+        if (d->pair_q[g] == m) add_src(j, opnd(w.dQ[g], H), opnd(W->q[g].w, H), H);
+        if (d->pair_k[g] == m) {
+          add_src(j, opnd(w.dK[g], H), opnd(W->k[g].w, H), H);
+          if (!pool) add_src(j, opnd(w.dV[g], H), opnd(W->v[g].w, H), H);
+        }
+      }
+      if (j.nsrc > GEMM_MAX_SRCS) return fail(MMF_ELIMIT, "too many gradient sources");
+      jobs.push_back(j);
+    }
+    STAGE_TRY("bwd.dZ_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, 0.f, rng, st));
+  }
+  // (5) dX_m = (dZ_m W_m) * mask * input-dropout'
+  {
+    std::vector<GemmJob> jobs;
+    for (int m = 0; m < M; ++m) {
+      if (!dx || !dx[m]) continue;
+      const int L = Lm(d, m), D = d->in_dim[m];
+      GemmJob j = make_job(B * L, D, dx[m], D, EPI_ROWSCALE | (drop ? EPI_DROP : 0));
+      j.g.rowscale = mask; j.g.rs_div = L; j.g.rs_stride = M; j.g.rs_off = m;
+      j.g.drop_site = SITE_IN + m;
+      add_src(j, opnd(w.dZ[m], H), opnd(W->proj[m].w, D), H);
+      jobs.push_back(j);
+    }
+    if (!jobs.empty())
+      STAGE_TRY("bwd.dx_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, p, rng, st));
+  }
+  // (6) every weight gradient: split-K slabs, then one deterministic reduce
+  STAGE_TRY("bwd.wgrad_gemm", launch_gemm(wp.jobs.data(), (int)wp.jobs.size(), MODE_KR, MODE_KR, p, rng, st));
+  STAGE_TRY("bwd.wgrad_reduce", launch_reduce(wp.reds.data(), (int)wp.reds.size(), st));
+  return MMF_OK;
+}
+
+}  // extern "C"

@@ -54,16 +54,22 @@ struct GemmSrc {
 
 enum : int32_t {
   EPI_BIAS = 1, EPI_RELU = 2, EPI_DROP = 4, EPI_ROWADD = 8, EPI_GATE = 16,
-  EPI_ROWSCALE = 32, EPI_PARTIAL = 64
+  EPI_ROWSCALE = 32, EPI_PARTIAL = 64, EPI_BIAS_RS = 128, EPI_ADDMAT = 256
 };
 
+// Epilogue order: v = alpha*acc; +bias[j] (x bias_rs[i*ld+off] with EPI_BIAS_RS);
+// +rowadd_scale*rowadd; +addm[i][j]; relu; gate; rowscale; dropout.
 struct GemmGroup {
   int32_t M, N;
   int32_t src_begin, src_count;
   float* C; int32_t ldc;
   int32_t epi;
+  float alpha;                                         // scales the accumulator (and part_db)
   const float* bias;                                   // EPI_BIAS
-  const float* rowadd; int32_t ld_rowadd, rowadd_div;  // EPI_ROWADD: += rowadd[(i/div)*ld + j]
+  const float* bias_rs; int32_t bias_rs_ld, bias_rs_off;  // EPI_BIAS_RS: bias[j] * bias_rs[i*ld + off]
+  const float* addm; int32_t ld_addm;                  // EPI_ADDMAT: += addm[i*ld + j]
+  float rowadd_scale;
+  const float* rowadd; int32_t ld_rowadd, rowadd_div;  // EPI_ROWADD: += scale*rowadd[(i/div)*ld + j]
   const float* gate; int32_t ld_gate; float gate_scale;// EPI_GATE: gate[i][j] > 0 ? v*scale : 0
   const float* rowscale; int32_t rs_div, rs_stride;    // EPI_ROWSCALE: v *= rowscale[(i/div)*stride + off]
   int32_t rs_off;
@@ -128,6 +134,11 @@ struct AttnPair {
   float* dsum;         // D = rowsum(dO*O) (B, heads, Lq)
   float* dq; float* dk; float* dv;   // (B, L, ld*)
   float* probs;        // (B, heads, Lq, Lk) output of attn_probs
+  // pooled-output formulation (HybridFusion): only column means of P' are needed
+  float* pbar;         // (B, heads, Lk) fwd output: mean over queries of the post-dropout probs
+  const float* dpbar;  // (B, heads, Lk) bwd input: d loss / d pbar
+  uint32_t* keep_bits; // (B, heads, Lq, 4) dropout keep mask written by the pooled forward
+                       // (Lk <= 128: bit k%32 of word k/32), read by its backward
 };
 
 constexpr int ATTN_MAX_PAIRS = 12;
@@ -150,6 +161,48 @@ hipError_t launch_attn_bwd(const AttnPair* pairs, int npairs, int B, int heads, 
 // stage 0: D = rowsum(dO*O); 1: dK/dV; 2: dQ
 hipError_t launch_attn_bwd_stage(int stage, const AttnPair* pairs, int npairs, int B, int heads, int hd,
                                  float scale, float drop_p, const RngSnap* rng, hipStream_t st);
+// Pooled formulation: forward writes LSE and pbar = mean_q P'[q, :];
+// backward (stage 0: dQ and D = rowsum(P . dP); stage 1: dK) from dpbar.
+hipError_t launch_attn_pool_fwd(const AttnPair* pairs, int npairs, int B, int heads, int hd, float scale,
+                                float drop_p, const RngSnap* rng, hipStream_t st);
+hipError_t launch_attn_pool_bwd(int stage, const AttnPair* pairs, int npairs, int B, int heads, int hd,
+                                float scale, float drop_p, const RngSnap* rng, hipStream_t st);
+
+// ---------------------------------------------------------------------------
+// Pooled-output helpers (pool.hip), per (pair, sample):
+//   U[h] = pbar_h P_k      r[h] = sum_j pbar_h[j]            (forward)
+//   dpbar_h[j] = P_k[j] . dU[h] + dObar_h . bv_h             (backward)
+//   E_m = cscale * c_m (row-broadcast) + sum_{pairs g with key m} pbar_g^T dU_g
+// ---------------------------------------------------------------------------
+struct PoolPair {
+  const float* pk;     // P_k (B, Lk, H)
+  int32_t Lk;
+  const float* pbar;   // (B, heads, Lk)
+  float* u;            // (B, heads, H)
+  float* r;            // (B, heads)
+  const float* du;     // (B, heads, H)
+  const float* dob;    // dObar (B, H)
+  const float* bv;     // value_proj.bias (H)
+  float* dpbar;        // (B, heads, Lk)
+};
+constexpr int POOL_MAX_PAIRS = 12;
+struct PoolArgs {
+  PoolPair p[POOL_MAX_PAIRS];
+  int32_t npairs, B, heads, hd, H;
+};
+hipError_t launch_pool_u(const PoolPair* pairs, int npairs, int B, int heads, int hd, int H, hipStream_t st);
+hipError_t launch_pool_dpbar(const PoolPair* pairs, int npairs, int B, int heads, int hd, int H,
+                             hipStream_t st);
+constexpr int POOLE_MAX_SRC = 7;
+struct PoolEMod {
+  float* out;          // (B, L, H)
+  int32_t L;
+  const float* c; int32_t ldc; float cscale;   // row-broadcast term c[b*ldc + col] * cscale
+  int32_t nsrc;
+  const float* pbar[POOLE_MAX_SRC];            // (B, heads, L)
+  const float* du[POOLE_MAX_SRC];              // (B, heads, H)
+};
+hipError_t launch_pool_e(const PoolEMod* mods, int nmods, int B, int heads, int H, hipStream_t st);
 
 // ---------------------------------------------------------------------------
 // Fusion head: pooling + gating + adaptive weights + weighted sum, and backward.
@@ -159,12 +212,14 @@ struct HeadArgs {
   int32_t B, M, H;
   const float* mask;                     // (B, M)
   int32_t scale_by_mask;                 // agg *= mask (src/fusion.py:408); 0 for compute_adaptive_weights
-  // per modality: list of (B, L_m, H) tensors whose L-mean is summed
+  // pooled_m = mask_m * inv_cnt[m] * sum_{sources s of m} src_scale[s] * sum_{rows} src_s
+  // (each source is (B, src_L[s], H); src_scale = 1/L for an L-mean)
   const float* src[HEAD_MAX_SRC];
   int32_t src_mod[HEAD_MAX_SRC];
+  int32_t src_L[HEAD_MAX_SRC];
+  float src_scale[HEAD_MAX_SRC];
   int32_t nsrc;
-  int32_t L[8];
-  float inv_cnt[8];                      // 1 / (n_entries_m * L_m)
+  float inv_cnt[8];                      // 1 / n_entries_m (the list length, src/fusion.py:406-408)
   const float* gate_w[8]; const float* gate_b[8];
   float* pooled;                         // (B, M, H)
   float* scores;                         // (B, M)
@@ -173,7 +228,8 @@ struct HeadArgs {
   float* weights_out;                    // optional copy (B, M)
   // backward
   const float* dfused;                   // (B, H)
-  float* cvec;                           // (B, M, H) per-row grad of every list entry of m
+  float* cvec;                           // (B, M, H) = dpooled_m * mask_m * inv_cnt[m]; a source
+                                         // row's grad is cvec * src_scale
   float* dscore;                         // (B, M)
 };
 hipError_t launch_head_fwd(const HeadArgs& a, hipStream_t st);

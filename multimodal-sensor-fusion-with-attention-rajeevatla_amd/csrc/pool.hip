@@ -1,0 +1,200 @@
+// Pooled-output helpers for HybridFusion (see attention.hip, "Pooled-output
+// attention").  Per (pair g = q->k, sample b), with P_k the key modality's
+// projected features (Lk x H):
+//   forward   U_h = pbar_h P_k,  r_h = sum_j pbar_h[j]
+//             (then Obar_h = U_h W_v,h^T + r_h b_v,h, an ordinary small GEMM)
+//   backward  dpbar_h[j] = P_k[j] . dU_h + dObar_h . b_v,h
+//             E_m = c_m/L_m (row broadcast) + sum_{g: key(g)=m} sum_h pbar_{g,h}^T dU_{g,h}
+// E_m is the part of dP_m that flows through value_proj (and the direct
+// aggregation term); the Q/K parts come from the dZ GEMM that adds E_m.
+#include <cstring>
+
+#include "mmf_device.h"
+
+namespace mmf {
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int MAXH = 8;           // heads supported by the pooled helpers
+constexpr int MAXLK = 128;
+
+__global__ __launch_bounds__(NT) void pool_u_kernel(const PoolArgs a) {
+  __shared__ float pb[MAXH * MAXLK];
+  __shared__ float4 red[NT];
+  const PoolPair& P = a.p[blockIdx.y];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int H = a.H, heads = a.heads, Lk = P.Lk;
+  const float* pbar = P.pbar + (int64_t)b * heads * Lk;
+  for (int i = t; i < heads * Lk; i += NT) pb[i] = pbar[i];
+  __syncthreads();
+  if (t < heads) {
+    float s = 0.f;
+    for (int j = 0; j < Lk; ++j) s += pb[t * Lk + j];
+    P.r[(int64_t)b * heads + t] = s;
+  }
+  const int H4 = H / 4;
+  const int ncol = heads * H4;
+  const float* pk = P.pk + (int64_t)b * Lk * H;
+  for (int task0 = 0; task0 < ncol; task0 += NT) {
+    const int nact = min(NT, ncol - task0);
+    const int RG = NT / nact;
+    const int task = task0 + t % nact, rg = t / nact;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (rg < RG) {
+      const int hh = task / H4, c4 = task % H4;
+      for (int j = rg; j < Lk; j += RG) {
+        const float4 v = *reinterpret_cast<const float4*>(pk + (int64_t)j * H + 4 * c4);
+        const float w = pb[hh * Lk + j];
+        acc.x += w * v.x; acc.y += w * v.y; acc.z += w * v.z; acc.w += w * v.w;
+      }
+    }
+    __syncthreads();
+    red[t] = acc;
+    __syncthreads();
+    if (t < nact) {
+      float4 s = red[t];
+      for (int g = 1; g < RG; ++g) {
+        const float4 v = red[g * nact + t];
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      }
+      const int task_t = task0 + t;
+      const int hh = task_t / H4, c4 = task_t % H4;
+      *reinterpret_cast<float4*>(P.u + ((int64_t)b * heads + hh) * H + 4 * c4) = s;
+    }
+  }
+}
+
+__global__ __launch_bounds__(NT) void pool_dpbar_kernel(const PoolArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float du_s[];   // heads * H
+  __shared__ float dr_s[MAXH];
+  const PoolPair& P = a.p[blockIdx.y];
+  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int H = a.H, heads = a.heads, hd = a.hd, Lk = P.Lk;
+  const float* du = P.du + (int64_t)b * heads * H;
+  for (int i = t; i < heads * H; i += NT) du_s[i] = du[i];
+  // dr_h = dObar_h . b_v,h  (d/d r_h of r_h * b_v,h)
+  for (int hh = wave; hh < heads; hh += 4) {
+    float s = 0.f;
+    for (int d = lane; d < hd; d += 64) s += P.dob[(int64_t)b * H + hh * hd + d] * P.bv[hh * hd + d];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) dr_s[hh] = s;
+  }
+  __syncthreads();
+  const float* pk = P.pk + (int64_t)b * Lk * H;
+  const int half = lane >> 5, l32 = lane & 31;
+  for (int j0 = 2 * wave; j0 < Lk; j0 += 8) {
+    const int j = j0 + half;
+    float acc[MAXH];
+#pragma unroll
+    for (int hh = 0; hh < MAXH; ++hh) acc[hh] = 0.f;
+    if (j < Lk) {
+      for (int c4 = l32; c4 < H / 4; c4 += 32) {
+        const float4 v = *reinterpret_cast<const float4*>(pk + (int64_t)j * H + 4 * c4);
+#pragma unroll
+        for (int hh = 0; hh < MAXH; ++hh) {
+          if (hh < heads) {
+            const float4 u = *reinterpret_cast<const float4*>(&du_s[hh * H + 4 * c4]);
+            acc[hh] += v.x * u.x + v.y * u.y + v.z * u.z + v.w * u.w;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int hh = 0; hh < MAXH; ++hh) {
+      if (hh < heads) {
+        float s = acc[hh];
+#pragma unroll
+        for (int o = 16; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+        if (l32 == 0 && j < Lk) P.dpbar[((int64_t)b * heads + hh) * Lk + j] = s + dr_s[hh];
+      }
+    }
+  }
+}
+
+struct PoolEArgs {
+  PoolEMod m[8];
+  int32_t B, heads, H;
+  int32_t blocks_per_b[8];
+};
+
+__global__ __launch_bounds__(NT) void pool_e_kernel(const PoolEArgs a) {
+  const PoolEMod& E = a.m[blockIdx.y];
+  const int H = a.H, H4 = H / 4, heads = a.heads, L = E.L;
+  const int bpb = a.blocks_per_b[blockIdx.y];
+  const int b = blockIdx.x / bpb;
+  if (b >= a.B) return;
+  const int64_t e = (int64_t)(blockIdx.x % bpb) * NT + threadIdx.x;   // (j, c4) inside sample b
+  if (e >= (int64_t)L * H4) return;
+  const int j = (int)(e / H4), c4 = (int)(e % H4);
+  const float4 cv = *reinterpret_cast<const float4*>(E.c + (int64_t)b * E.ldc + 4 * c4);
+  float4 acc = make_float4(cv.x * E.cscale, cv.y * E.cscale, cv.z * E.cscale, cv.w * E.cscale);
+  for (int s = 0; s < E.nsrc; ++s) {
+    const float* pb = E.pbar[s] + (int64_t)b * heads * L;
+    const float* du = E.du[s] + (int64_t)b * heads * H;
+    for (int hh = 0; hh < heads; ++hh) {
+      const float w = pb[hh * L + j];
+      const float4 u = *reinterpret_cast<const float4*>(du + hh * H + 4 * c4);
+      acc.x += w * u.x; acc.y += w * u.y; acc.z += w * u.z; acc.w += w * u.w;
+    }
+  }
+  *reinterpret_cast<float4*>(E.out + ((int64_t)b * L + j) * H + 4 * c4) = acc;
+}
+
+hipError_t launch_pool(bool fwd, const PoolPair* pairs, int npairs, int B, int heads, int hd, int H,
+                       hipStream_t st) {
+  if (heads > MAXH || H % 4 != 0) return hipErrorInvalidValue;
+  int done = 0;
+  while (done < npairs) {
+    PoolArgs a;
+    memset(&a, 0, sizeof(a));
+    int n = 0;
+    while (done < npairs && n < POOL_MAX_PAIRS) {
+      if (pairs[done].Lk > MAXLK) return hipErrorInvalidValue;
+      a.p[n++] = pairs[done++];
+    }
+    a.npairs = n;
+    a.B = B; a.heads = heads; a.hd = hd; a.H = H;
+    if (fwd) {
+      hipLaunchKernelGGL(pool_u_kernel, dim3(B, n), dim3(NT), 0, st, a);
+    } else {
+      const size_t shm = (size_t)heads * H * sizeof(float);
+      hipLaunchKernelGGL(pool_dpbar_kernel, dim3(B, n), dim3(NT), shm, st, a);
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace
+
+hipError_t launch_pool_u(const PoolPair* pairs, int npairs, int B, int heads, int hd, int H, hipStream_t st) {
+  return launch_pool(true, pairs, npairs, B, heads, hd, H, st);
+}
+
+hipError_t launch_pool_dpbar(const PoolPair* pairs, int npairs, int B, int heads, int hd, int H,
+                             hipStream_t st) {
+  return launch_pool(false, pairs, npairs, B, heads, hd, H, st);
+}
+
+hipError_t launch_pool_e(const PoolEMod* mods, int nmods, int B, int heads, int H, hipStream_t st) {
+  if (nmods > 8 || H % 4 != 0) return hipErrorInvalidValue;
+  PoolEArgs a;
+  memset(&a, 0, sizeof(a));
+  a.B = B; a.heads = heads; a.H = H;
+  int maxb = 0;
+  for (int i = 0; i < nmods; ++i) {
+    if (mods[i].nsrc > POOLE_MAX_SRC) return hipErrorInvalidValue;
+    a.m[i] = mods[i];
+    const int64_t per_b = (int64_t)mods[i].L * (H / 4);
+    a.blocks_per_b[i] = (int)((per_b + NT - 1) / NT);
+    const int nb = a.blocks_per_b[i] * B;
+    if (nb > maxb) maxb = nb;
+  }
+  hipLaunchKernelGGL(pool_e_kernel, dim3(maxb, nmods), dim3(NT), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace mmf

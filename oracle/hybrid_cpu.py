@@ -40,11 +40,21 @@ import torch
 import torch.nn.functional as F
 
 
-def _dropout(x: torch.Tensor, p: float, train: bool, gen: Optional[torch.Generator]) -> torch.Tensor:
+def _dropout(x: torch.Tensor, p: float, train: bool, gen, site: int = 0) -> torch.Tensor:
+    """nn.Dropout(p).  `gen` is a torch.Generator (CPU RNG) or a callable
+    (site, tensor) -> keep mask, used by the tests to replay the device's
+    Philox masks so train-mode outputs can be compared exactly."""
     if not train or p <= 0.0:
         return x
-    keep = (torch.rand(x.shape, generator=gen, dtype=x.dtype) >= p).to(x.dtype)
+    if callable(gen):
+        keep = gen(site, x).to(x.dtype)
+    else:
+        keep = (torch.rand(x.shape, generator=gen, dtype=x.dtype) >= p).to(x.dtype)
     return x * keep / (1.0 - p)
+
+
+# dropout site ids (mirror of the device's Philox streams, csrc/mmf_internal.h)
+SITE_IN, SITE_PROJ, SITE_ATTN, SITE_CLS = 0x100, 0x200, 0x300, 0x400
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
@@ -54,7 +64,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 def cma_forward(params: Mapping[str, torch.Tensor], prefix: str, query: torch.Tensor,
                 key: torch.Tensor, value: torch.Tensor, num_heads: int,
                 mask: Optional[torch.Tensor] = None, p: float = 0.0, train: bool = False,
-                gen: Optional[torch.Generator] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+                gen=None, site: int = SITE_ATTN) -> Tuple[torch.Tensor, torch.Tensor]:
     """src/attention.py:68-146."""
     B = query.shape[0]
     sq = query.dim() == 2
@@ -81,7 +91,7 @@ def cma_forward(params: Mapping[str, torch.Tensor], prefix: str, query: torch.Te
         s = s.masked_fill((mk == 0).reshape(B, 1, 1, -1), float("-inf"))
     a = torch.softmax(s, dim=-1)
     a = torch.nan_to_num(a, nan=0.0, posinf=0.0, neginf=0.0)
-    a = _dropout(a, p, train, gen)
+    a = _dropout(a, p, train, gen, site)
     o = a.matmul(v).permute(0, 2, 1, 3).reshape(B, Lq, H)
     o = linear(o, *W("out_proj"))
     if sq:
@@ -116,8 +126,7 @@ def pairs_present(names: Sequence[str], params: Mapping[str, torch.Tensor]) -> L
 
 def hybrid_forward(params: Mapping[str, torch.Tensor], names: Sequence[str],
                    feats: Mapping[str, torch.Tensor], mask: Optional[torch.Tensor],
-                   num_heads: int, p: float = 0.0, train: bool = False,
-                   gen: Optional[torch.Generator] = None):
+                   num_heads: int, p: float = 0.0, train: bool = False, gen=None):
     """HybridFusion forward (src/fusion.py:331-427) + sequence-mode pooling.
 
     Returns (logits, info) with info = {attention_maps, fusion_weights, pooled}.
@@ -131,15 +140,15 @@ def hybrid_forward(params: Mapping[str, torch.Tensor], names: Sequence[str],
     for i, m in enumerate(names):
         x = feats[m]
         mk = mask[:, i].reshape(-1, *([1] * (x.dim() - 1)))
-        z = linear(_dropout(x * mk, p, train, gen), params[f"projections.{m}.0.weight"],
+        z = linear(_dropout(x * mk, p, train, gen, SITE_IN + i), params[f"projections.{m}.0.weight"],
                    params[f"projections.{m}.0.bias"])
-        P[m] = _dropout(torch.relu(z), p, train, gen)
+        P[m] = _dropout(torch.relu(z), p, train, gen, SITE_PROJ + i)
     lists = {m: [P[m]] for m in names}
     maps: Dict[str, torch.Tensor] = {}
-    for q, k in pairs_present(names, params):
+    for g, (q, k) in enumerate(pairs_present(names, params)):
         ki = names.index(k)
         att, a = cma_forward(params, f"attention_modules.{q}_to_{k}.", P[q], P[k], P[k],
-                             num_heads, mask=mask[:, ki], p=p, train=train, gen=gen)
+                             num_heads, mask=mask[:, ki], p=p, train=train, gen=gen, site=SITE_ATTN + g)
         lists[q].append(att)
         maps[f"{q}_to_{k}"] = a
     pooled = []
@@ -151,7 +160,7 @@ def hybrid_forward(params: Mapping[str, torch.Tensor], names: Sequence[str],
     w = adaptive_weights(params, names, {m: pooled[i] for i, m in enumerate(names)}, mask)
     fused = (pooled_t * w.unsqueeze(-1)).sum(1)
     h = _dropout(torch.relu(linear(fused, params["classifier.0.weight"], params["classifier.0.bias"])),
-                 p, train, gen)
+                 p, train, gen, SITE_CLS)
     logits = linear(h, params["classifier.3.weight"], params["classifier.3.bias"])
     return logits, {"attention_maps": maps, "fusion_weights": w, "pooled": pooled_t}
 

@@ -1,0 +1,49 @@
+"""numpy Philox4x32-10 replay of the device dropout streams (test infrastructure).
+
+The HIP kernels draw keep decisions as (csrc/mmf_device.h):
+    counter = (idx>>2 lo32, idx>>2 hi32, site, offset lo32), key = (seed lo32, seed hi32)
+    word    = philox10(counter, key)[idx & 3]
+    keep    = float(word >> 8) * 2^-24 >= p
+so a test can rebuild the exact masks and run the CPU oracle in train mode.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+_M0, _M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+_W0, _W1 = np.uint64(0x9E3779B9), np.uint64(0xBB67AE85)
+_MASK = np.uint64(0xFFFFFFFF)
+
+
+def philox10(c0, c1, c2, c3, k0, k1):
+    c0, c1, c2, c3 = (np.asarray(v, dtype=np.uint64) for v in (c0, c1, c2, c3))
+    k0, k1 = np.uint64(k0), np.uint64(k1)
+    for _ in range(10):
+        p0 = _M0 * c0
+        p1 = _M1 * c2
+        hi0, lo0 = p0 >> np.uint64(32), p0 & _MASK
+        hi1, lo1 = p1 >> np.uint64(32), p1 & _MASK
+        c0, c1, c2, c3 = (hi1 ^ c1 ^ k0) & _MASK, lo1, (hi0 ^ c3 ^ k1) & _MASK, lo0
+        k0 = (k0 + _W0) & _MASK
+        k1 = (k1 + _W1) & _MASK
+    return c0, c1, c2, c3
+
+
+def keep_mask(shape, site: int, seed: int, offset: int, p: float) -> np.ndarray:
+    n = int(np.prod(shape))
+    idx = np.arange(n, dtype=np.uint64)
+    blk = idx >> np.uint64(2)
+    words = philox10(blk & _MASK, blk >> np.uint64(32), np.full(n, site, np.uint64),
+                     np.full(n, offset & 0xFFFFFFFF, np.uint64), seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
+    sel = (idx & np.uint64(3)).astype(np.int64)
+    w = np.choose(sel, words)
+    u = (w >> np.uint64(8)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    return (u >= np.float32(p)).reshape(shape)
+
+
+def mask_provider(seed: int, offset: int, p: float):
+    """Callable (site, tensor) -> keep mask for oracle.hybrid_cpu._dropout."""
+    def fn(site, x):
+        return torch.from_numpy(keep_mask(tuple(x.shape), site, seed, offset, p))
+    return fn

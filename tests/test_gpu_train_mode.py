@@ -1,0 +1,109 @@
+"""GPU parity in TRAIN mode (dropout active), exact up to fp32 rounding.
+
+The device draws its dropout masks from Philox4x32-10 (csrc/mmf_device.h);
+tests/_philox.py replays the same streams in numpy and feeds them to the CPU
+oracle, so forward outputs and every gradient can be compared at the same
+1e-3 tolerance as eval mode.  Covers both HybridFusion execution plans
+(pooled: every key length <= 128; general: a key modality longer than 128)
+and the standalone CrossModalAttention.
+"""
+import numpy as np
+import pytest
+import torch
+
+from _philox import keep_mask, mask_provider
+from _util import close
+from cases import HybridCase, hybrid_inputs, hybrid_state
+
+pytestmark = pytest.mark.gpu
+RTOL, ATOL = 1e-3, 1e-5
+SEED, OFFSET, P = 0x1234_5678_9ABC, 7, 0.3
+
+
+@pytest.fixture(scope="module")
+def mods(pkg_on_path):
+    if not torch.cuda.is_available():
+        pytest.fail("no ROCm device visible")
+    import attention
+    import fusion
+    return fusion, attention
+
+
+TRAIN_CASES = [
+    HybridCase("train_pooled", ["m0", "m1", "m2"], {"m0": 24, "m1": 32, "m2": 16},
+               {"m0": 16, "m1": 24, "m2": 8}, batch=4, hidden=32, heads=4, classes=5, seed=51,
+               mask=[[1, 1, 1], [1, 0, 1], [0, 0, 0], [0.5, 1, 0]]),
+    HybridCase("train_l1", ["a", "b", "c"], {"a": 12, "b": 20, "c": 16},
+               {"a": 0, "b": 0, "c": 0}, batch=8, hidden=32, heads=4, classes=5, seed=52,
+               mask=[[1, 1, 1], [1, 0, 1], [0, 0, 1], [0, 0, 0], [1, 1, 0.5]]),
+    HybridCase("train_general_long", ["x", "y"], {"x": 16, "y": 8},
+               {"x": 20, "y": 140}, batch=2, hidden=64, heads=2, classes=3, seed=53,
+               mask=[[1, 1], [1, 0]]),
+]
+
+
+@pytest.mark.parametrize("case", TRAIN_CASES, ids=lambda c: c.name)
+def test_hybrid_train_mode_matches_oracle(mods, case):
+    fusion, _ = mods
+    from oracle.hybrid_cpu import hybrid_forward
+    sd = hybrid_state(case.names, case.dims, case.hidden, case.classes, case.seed)
+    model = fusion.HybridFusion({m: case.dims[m] for m in case.names}, hidden_dim=case.hidden,
+                                num_classes=case.classes, num_heads=case.heads, dropout=P)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    model = model.cuda().train()
+    model._rng_state.copy_(torch.tensor([SEED, OFFSET], dtype=torch.int64))
+    feats_np, mask_np, grad_np = hybrid_inputs(case)
+    feats = {m: torch.from_numpy(v).cuda().requires_grad_(True) for m, v in feats_np.items()}
+    logits, info = model(feats, torch.from_numpy(mask_np).cuda(), return_attention=True)
+    (logits * torch.from_numpy(grad_np).cuda()).sum().backward()
+    torch.cuda.synchronize()
+    assert int(model._rng_state[1].item()) == OFFSET + 1   # the device advanced its stream
+
+    params = {k: torch.from_numpy(v).requires_grad_(True) for k, v in sd.items()}
+    xs = {m: torch.from_numpy(v).requires_grad_(True) for m, v in feats_np.items()}
+    ref, rinfo = hybrid_forward(params, case.names, xs, torch.from_numpy(mask_np), case.heads, p=P,
+                                train=True, gen=mask_provider(SEED, OFFSET, P))
+    (ref * torch.from_numpy(grad_np)).sum().backward()
+    assert close(logits.detach().cpu(), ref.detach(), RTOL, ATOL)
+    assert close(info["fusion_weights"].cpu(), rinfo["fusion_weights"].detach(), RTOL, ATOL)
+    for key, amap in info["attention_maps"].items():
+        assert close(amap.cpu(), rinfo["attention_maps"][key].detach(), RTOL, ATOL), key
+    for m in case.names:
+        assert close(feats[m].grad.cpu(), xs[m].grad, RTOL, ATOL), m
+    for name, p in model.named_parameters():
+        assert close(p.grad.cpu(), params[name].grad, RTOL, ATOL), name
+
+
+def test_cma_train_mode_matches_oracle(mods):
+    _, attention = mods
+    from oracle.hybrid_cpu import cma_forward
+    torch.manual_seed(3)
+    m = attention.CrossModalAttention(24, 40, hidden_dim=64, num_heads=4, dropout=P)
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.cuda().train()
+    m._rng_state.copy_(torch.tensor([SEED, OFFSET], dtype=torch.int64))
+    q, k, v = torch.randn(3, 30, 24), torch.randn(3, 50, 40), torch.randn(3, 50, 40)
+    mask = (torch.rand(3, 50) < 0.8).float()
+    g = torch.randn(3, 30, 64)
+    qt, kt, vt = (t.cuda().requires_grad_(True) for t in (q, k, v))
+    att, w = m(qt, kt, vt, mask.cuda())
+    (att * g.cuda()).sum().backward()
+    params = {k2: t.requires_grad_(True) for k2, t in sd.items()}
+    qc, kc, vc = (t.clone().requires_grad_(True) for t in (q, k, v))
+    ra, rw = cma_forward(params, "", qc, kc, vc, 4, mask=mask, p=P, train=True,
+                         gen=mask_provider(SEED, OFFSET, P))
+    (ra * g).sum().backward()
+    assert close(att.detach().cpu(), ra.detach(), RTOL, ATOL)
+    assert close(w.cpu(), rw.detach(), RTOL, ATOL)
+    for a, b in ((qt, qc), (kt, kc), (vt, vc)):
+        assert close(a.grad.cpu(), b.grad, RTOL, ATOL)
+    for name, p in m.named_parameters():
+        assert close(p.grad.cpu(), params[name].grad, RTOL, ATOL), name
+
+
+def test_philox_replay_statistics():
+    """CPU-side sanity of the replayed masks (keep rate, independence across sites)."""
+    a = keep_mask((64, 1000), 0x300, SEED, OFFSET, 0.3)
+    b = keep_mask((64, 1000), 0x301, SEED, OFFSET, 0.3)
+    assert 0.68 < a.mean() < 0.72
+    assert 0.45 < (a == b).mean() < 0.65
