@@ -616,14 +616,16 @@ __global__ __launch_bounds__(NT) void attn_pool_fwd_kernel(const AttnArgs A) {
     const float inv_l = (l > 0.f && qvalid) ? 1.f / l : 0.f;
     const int64_t rowidx = bh * Lq + q;
     uint32_t words[NKT];
+    const bool aligned8 = (Lk & 7) == 0;
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
+      uint32_t kb16 = 0xFFFFu;   // bit r: reg r kept
+      if (pdrop > 0.f && kt < nkt)
+        kb16 = keep_tile16(rs, P.drop_site, (uint64_t)rowidx * Lk + kt * 32, pdrop, h, qvalid, aligned8);
       uint32_t bits = 0;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        uint32_t kb = 0xFu;
-        if (pdrop > 0.f && qvalid && kt < nkt)
-          kb = keep4(rs, P.drop_site, (uint64_t)rowidx * Lk + kt * 32 + 8 * g + 4 * h, pdrop);
+        const uint32_t kb = (kb16 >> (4 * g)) & 0xFu;
         bits |= kb << (8 * g + 4 * h);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {

@@ -119,11 +119,13 @@ inline void add_src(GemmJob& j, Operand a, Operand b, int K) {
   s.K = K;
 }
 
-// Split of a weight-gradient contraction over `rows`: ~1024 rows per slab.
+// Split of a weight-gradient contraction over `rows`: ~256 rows per slab, so a
+// launch of 8 (128x128-output) jobs at B*L = 32768 rows fills the chip with
+// 1024 workgroups (4 per CU).
 inline void split_rows(int rows, int& nsplit, int& kchunk) {
-  nsplit = rows / 1024;
+  nsplit = rows / 256;
   if (nsplit < 1) nsplit = 1;
-  if (nsplit > 64) nsplit = 64;
+  if (nsplit > 128) nsplit = 128;
   kchunk = (rows + nsplit - 1) / nsplit;
   kchunk = (kchunk + 31) & ~31;
   nsplit = (rows + kchunk - 1) / kchunk;
@@ -166,6 +168,8 @@ inline void plan_wgrad(WgradPlan& wp, Bump& ws, int M, int N, int rows, Operand 
   }
   wp.jobs.push_back(j);
   ReduceJob r;
+  memset(&r, 0, sizeof(r));
+  r.nbatch = 1;
   r.part = part;
   r.part_db = part_db;
   r.out = out_w;
@@ -173,6 +177,34 @@ inline void plan_wgrad(WgradPlan& wp, Bump& ws, int M, int N, int rows, Operand 
   r.nsplit = nsplit;
   r.M = M;
   r.N = N;
+  wp.reds.push_back(r);
+}
+
+// Strided batch of `nbatch` weight-gradient problems without bias: problem i
+// reads A + i*bs_a, B + i*bs_b and writes out_w + i*bs_out (e.g. the per-head
+// row blocks of value_proj.weight in the pooled plan).
+inline void plan_wgrad_batched(WgradPlan& wp, Bump& ws, int M, int N, int rows, Operand a, Operand b,
+                               float* out_w, int nbatch, int bs_a, int bs_b, int bs_out) {
+  int nsplit, kchunk;
+  split_rows(rows, nsplit, kchunk);
+  float* part = ws.take<float>((size_t)nbatch * nsplit * M * N);
+  GemmJob j = make_job(M, N, part, N, EPI_PARTIAL);
+  j.g.nsplit = nsplit;
+  j.g.kchunk = kchunk;
+  j.g.nbatch = nbatch;
+  j.g.bs_a = bs_a;
+  j.g.bs_b = bs_b;
+  add_src(j, a, b, rows);
+  wp.jobs.push_back(j);
+  ReduceJob r;
+  memset(&r, 0, sizeof(r));
+  r.part = part;
+  r.out = out_w;
+  r.nsplit = nsplit;
+  r.M = M;
+  r.N = N;
+  r.nbatch = nbatch;
+  r.bs_out = bs_out;
   wp.reds.push_back(r);
 }
 

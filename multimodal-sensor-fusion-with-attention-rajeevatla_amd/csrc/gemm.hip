@@ -41,7 +41,7 @@ __device__ __forceinline__ float apply_xf(float v, const Xform& xf, int64_t srow
 //  MODE_RK: stored [e][kk] (kk contiguous): thread t covers e = t/8 + 32u, kk = 4*(t%8)..+3
 //  MODE_KR: stored [kk][e] (e contiguous):  thread t covers kk = t/32 + 8u, e = 4*(t%32)..+3
 template <int MODE>
-__device__ __forceinline__ void load_tile(TileRegs& R, const Operand& op, const Xform* xft, int e0,
+__device__ __forceinline__ void load_tile(TileRegs& R, const Operand& op, int64_t boff, const Xform* xft, int e0,
                                           int eext, int k0, int kend, const RngSnap& rs, float p,
                                           float inv_keep) {
   const int t = threadIdx.x;
@@ -55,7 +55,7 @@ __device__ __forceinline__ void load_tile(TileRegs& R, const Operand& op, const 
     if (MODE == MODE_RK) {
       if (e < eext) {
         const int64_t srow = e / op.row_div;
-        const float* rowp = op.ptr + srow * (int64_t)op.ld;
+        const float* rowp = op.ptr + boff + srow * (int64_t)op.ld;
         if (op.vec && kk + 3 < kend) {
           const float4 f = *reinterpret_cast<const float4*>(rowp + kk);
           x[0] = f.x; x[1] = f.y; x[2] = f.z; x[3] = f.w;
@@ -71,7 +71,7 @@ __device__ __forceinline__ void load_tile(TileRegs& R, const Operand& op, const 
     } else {
       if (kk < kend) {
         const int64_t srow = kk / op.row_div;
-        const float* rowp = op.ptr + srow * (int64_t)op.ld;
+        const float* rowp = op.ptr + boff + srow * (int64_t)op.ld;
         if (op.vec && e + 3 < eext) {
           const float4 f = *reinterpret_cast<const float4*>(rowp + e);
           x[0] = f.x; x[1] = f.y; x[2] = f.z; x[3] = f.w;
@@ -113,12 +113,21 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const GemmArgs args) {
   const int tiles_n = (G.N + BN - 1) / BN;
   const int tiles_m = (G.M + BM - 1) / BM;
   const int nsplit = (G.epi & EPI_PARTIAL) ? G.nsplit : 1;
-  int tile = blockIdx.x;
+  const int per_batch = tiles_m * tiles_n * nsplit;
+  const int batch = blockIdx.x / per_batch;
+  if (batch >= G.nbatch) return;
+  int tile = blockIdx.x - batch * per_batch;
   const int split = tile % nsplit;
   tile /= nsplit;
-  if (tile >= tiles_m * tiles_n) return;
   const int tm = tile / tiles_n, tn = tile % tiles_n;
   const int i0 = tm * BM, j0 = tn * BN;
+  // strided-batch element: shift every pointer of this problem
+  const int64_t offA = (int64_t)batch * G.bs_a, offB = (int64_t)batch * G.bs_b;
+  float* const Cb = (G.epi & EPI_PARTIAL) ? G.C + (int64_t)batch * nsplit * G.M * G.N
+                                          : G.C + (int64_t)batch * G.bs_c;
+  float* const part_db = G.part_db ? G.part_db + (int64_t)batch * nsplit * G.M : nullptr;
+  const float* const biasb = G.bias ? G.bias + (int64_t)batch * G.bs_bias : nullptr;
+  const int brs_off = G.bias_rs_off + batch * G.bs_brs;
 
   __shared__ __attribute__((aligned(16))) float As[BK * LDS_STRIDE];
   __shared__ __attribute__((aligned(16))) float Bs[BK * LDS_STRIDE];
@@ -143,7 +152,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const GemmArgs args) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
-  const bool want_db = (G.epi & EPI_PARTIAL) && G.part_db != nullptr && tn == 0;
+  const bool want_db = (G.epi & EPI_PARTIAL) && part_db != nullptr && tn == 0;
   float dbsum = 0.f;
 
   for (int si = 0; si < G.src_count; ++si) {
@@ -156,8 +165,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const GemmArgs args) {
     if (kbeg >= kend) continue;
     const int ntk = (kend - kbeg + BK - 1) / BK;
     TileRegs ra, rb;
-    load_tile<AMODE>(ra, S.a, args.xf, i0, G.M, kbeg, kend, rs, p, inv_keep);
-    load_tile<BMODE>(rb, S.b, args.xf, j0, G.N, kbeg, kend, rs, p, inv_keep);
+    load_tile<AMODE>(ra, S.a, offA, args.xf, i0, G.M, kbeg, kend, rs, p, inv_keep);
+    load_tile<BMODE>(rb, S.b, offB, args.xf, j0, G.N, kbeg, kend, rs, p, inv_keep);
     for (int kt = 0; kt < ntk; ++kt) {
       __syncthreads();
       store_tile<AMODE>(ra, As);
@@ -165,8 +174,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const GemmArgs args) {
       __syncthreads();
       if (kt + 1 < ntk) {
         const int kn = kbeg + (kt + 1) * BK;
-        load_tile<AMODE>(ra, S.a, args.xf, i0, G.M, kn, kend, rs, p, inv_keep);
-        load_tile<BMODE>(rb, S.b, args.xf, j0, G.N, kn, kend, rs, p, inv_keep);
+        load_tile<AMODE>(ra, S.a, offA, args.xf, i0, G.M, kn, kend, rs, p, inv_keep);
+        load_tile<BMODE>(rb, S.b, offB, args.xf, j0, G.N, kn, kend, rs, p, inv_keep);
       }
       if (want_db && t < BM) {
 #pragma unroll 8
@@ -188,7 +197,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const GemmArgs args) {
 
   // ------------------------------------------------------------- epilogue
   if (G.epi & EPI_PARTIAL) {
-    float* out = G.C + (int64_t)split * G.M * G.N;
+    float* out = Cb + (int64_t)split * G.M * G.N;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -201,7 +210,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const GemmArgs args) {
           if (i < G.M) out[(int64_t)i * G.N + j] = acc[a][b][r] * G.alpha;
         }
       }
-    if (want_db && t < BM && i0 + t < G.M) G.part_db[(int64_t)split * G.M + i0 + t] = dbsum * G.alpha;
+    if (want_db && t < BM && i0 + t < G.M) part_db[(int64_t)split * G.M + i0 + t] = dbsum * G.alpha;
     return;
   }
   const int epi = G.epi;
@@ -211,13 +220,13 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const GemmArgs args) {
     for (int b = 0; b < 2; ++b) {
       const int j = j0 + wn * 64 + b * 32 + c;
       if (j >= G.N) continue;
-      const float bj = (epi & EPI_BIAS) ? G.bias[j] : 0.f;
+      const float bj = (epi & EPI_BIAS) ? biasb[j] : 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int i = i0 + wm * 64 + a * 32 + acc_row(r, h);
         if (i >= G.M) continue;
         float v = acc[a][b][r] * G.alpha;
-        if (epi & EPI_BIAS_RS) v += bj * G.bias_rs[(int64_t)i * G.bias_rs_ld + G.bias_rs_off];
+        if (epi & EPI_BIAS_RS) v += bj * G.bias_rs[(int64_t)i * G.bias_rs_ld + brs_off];
         else v += bj;
         if (epi & EPI_ROWADD)
           v += G.rowadd_scale * G.rowadd[(int64_t)(i / G.rowadd_div) * G.ld_rowadd + j];
@@ -227,7 +236,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const GemmArgs args) {
         if (epi & EPI_ROWSCALE) v *= G.rowscale[(int64_t)(i / G.rs_div) * G.rs_stride + G.rs_off];
         if ((epi & EPI_DROP) && p > 0.f)
           v = keep1(rs, G.drop_site, (uint64_t)i * (uint64_t)G.N + (uint64_t)j, p) ? v * inv_keep : 0.f;
-        G.C[(int64_t)i * G.ldc + j] = v;
+        Cb[(int64_t)i * G.ldc + j] = v;
       }
     }
 }
@@ -238,16 +247,37 @@ struct ReduceArgs {
 };
 
 __global__ __launch_bounds__(256) void partial_reduce_kernel(const ReduceArgs a) {
-  const ReduceJob& J = a.j[blockIdx.y];
+  ReduceJob J = a.j[blockIdx.y];
   const int64_t MN = (int64_t)J.M * J.N;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < MN; e += stride) {
-    float s = 0.f;
-    for (int k = 0; k < J.nsplit; ++k) s += J.part[(int64_t)k * MN + e];
-    J.out[e] = s;
+  const int batch = blockIdx.z;
+  if (batch >= J.nbatch) return;
+  J.part += (int64_t)batch * J.nsplit * MN;
+  if (J.part_db) J.part_db += (int64_t)batch * J.nsplit * J.M;
+  J.out += (int64_t)batch * J.bs_out;
+  if (J.db) J.db += (int64_t)batch * J.bs_db;
+  // 64 outputs x 4 split-groups per block; the 4 partial sums are combined in a
+  // fixed order, so the result is deterministic.
+  __shared__ float red[4][64];
+  const int el = threadIdx.x & 63, sg = threadIdx.x >> 6;
+  const int64_t gstride = (int64_t)gridDim.x * 64;
+  for (int64_t e0 = (int64_t)blockIdx.x * 64; e0 < MN; e0 += gstride) {
+    const int64_t e = e0 + el;
+    float s0 = 0.f, s1 = 0.f;
+    if (e < MN) {
+      int k = sg;
+      for (; k + 4 < J.nsplit; k += 8) {
+        s0 += J.part[(int64_t)k * MN + e];
+        s1 += J.part[(int64_t)(k + 4) * MN + e];
+      }
+      for (; k < J.nsplit; k += 4) s0 += J.part[(int64_t)k * MN + e];
+    }
+    __syncthreads();
+    red[sg][el] = s0 + s1;
+    __syncthreads();
+    if (sg == 0 && e < MN) J.out[e] = (red[0][el] + red[1][el]) + (red[2][el] + red[3][el]);
   }
-  if (J.db && J.part_db) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < J.M; i += stride) {
+  if (J.db && J.part_db && blockIdx.x == 0) {
+    for (int i = threadIdx.x; i < J.M; i += blockDim.x) {
       float s = 0.f;
       for (int k = 0; k < J.nsplit; ++k) s += J.part_db[(int64_t)k * J.M + i];
       J.db[i] = s;
@@ -275,6 +305,7 @@ hipError_t launch_gemm(const GemmJob* jobs, int njobs, int amode, int bmode, flo
       if (J.nsrc > GEMM_MAX_SRCS) return hipErrorInvalidValue;
       if (ns + J.nsrc > GEMM_MAX_SRCS || nx + need_x > GEMM_MAX_XF) break;
       GemmGroup g = J.g;
+      if (g.nbatch < 1) g.nbatch = 1;
       g.src_begin = ns;
       g.src_count = J.nsrc;
       for (int s = 0; s < J.nsrc; ++s) {
@@ -287,7 +318,7 @@ hipError_t launch_gemm(const GemmJob* jobs, int njobs, int amode, int bmode, flo
       }
       args.g[ng++] = g;
       const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN) *
-                        ((g.epi & EPI_PARTIAL) ? g.nsplit : 1);
+                        ((g.epi & EPI_PARTIAL) ? g.nsplit : 1) * g.nbatch;
       if (tiles > max_blocks) max_blocks = tiles;
       ++done;
     }
@@ -317,17 +348,20 @@ hipError_t launch_reduce(const ReduceJob* jobs, int njobs, hipStream_t st) {
     memset(&a, 0, sizeof(a));
     int n = 0;
     int64_t maxmn = 0;
+    int maxbatch = 1;
     while (done < njobs && n < 16) {
       a.j[n] = jobs[done++];
+      if (a.j[n].nbatch < 1) a.j[n].nbatch = 1;
+      if (a.j[n].nbatch > maxbatch) maxbatch = a.j[n].nbatch;
       const int64_t mn = (int64_t)a.j[n].M * a.j[n].N;
       if (mn > maxmn) maxmn = mn;
       ++n;
     }
     a.njobs = n;
-    int blocks = (int)((maxmn + 255) / 256);
+    int blocks = (int)((maxmn + 63) / 64);
     if (blocks < 1) blocks = 1;
-    if (blocks > 1024) blocks = 1024;
-    hipLaunchKernelGGL(partial_reduce_kernel, dim3(blocks, n), dim3(256), 0, st, a);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(partial_reduce_kernel, dim3(blocks, n, maxbatch), dim3(256), 0, st, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

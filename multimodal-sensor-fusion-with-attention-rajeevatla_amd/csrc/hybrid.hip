@@ -11,6 +11,7 @@
 //  * general (fallback): per-pair Q/K/V projections, flash attention
 //    (O = softmax(QK^T) V), out_proj on every row, L-mean in the head.
 // Both are exact reformulations (fp32 reassociation only) of the reference.
+#include <algorithm>
 #include <cmath>
 
 #include "capi_util.h"
@@ -162,14 +163,13 @@ void plan_wgrads(const mmf_hybrid_desc* d, const float* const* x, const float* m
     const float* cq = w.cvec ? w.cvec + (size_t)q * H : nullptr;
     if (pool) {
       plan_wgrad(wp, bw, H, H, B, opnd(cq, M * H), opnd(s.Ob[p], H), g->o[p].w, g->o[p].b);
-      for (int hh = 0; hh < nh; ++hh) {
-        const float* dob = w.dOb[p] ? w.dOb[p] + hh * hd : nullptr;
-        plan_wgrad(wp, bw, hd, H, B, opnd(dob, H), opnd(s.U[p] ? s.U[p] + (size_t)hh * H : nullptr, nh * H),
-                   g->v[p].w ? g->v[p].w + (size_t)hh * hd * H : nullptr, nullptr, false);
-        // value_proj.bias slice = sum_b r_h[b] dObar_h[b]  (Obar_h = U_h W_v,h^T + r_h b_v,h)
-        plan_wgrad(wp, bw, hd, 1, B, opnd(dob, H), opnd(s.r[p] ? s.r[p] + hh : nullptr, nh),
-                   g->v[p].b ? g->v[p].b + hh * hd : nullptr, nullptr, false);
-      }
+      // value_proj.weight rows of head h = dObar_h^T U_h; bias slice = sum_b r_h[b] dObar_h[b]
+      // (Obar_h = U_h W_v,h^T + r_h b_v,h): strided batches over the heads
+      Operand dob = opnd(w.dOb[p], H), u = opnd(s.U[p], nh * H), rr = opnd(s.r[p], nh);
+      dob.vec = u.vec = (hd % 4 == 0) && (H % 4 == 0);
+      rr.vec = 0;
+      plan_wgrad_batched(wp, bw, hd, H, B, dob, u, g->v[p].w, nh, hd, H, hd * H);
+      plan_wgrad_batched(wp, bw, hd, 1, B, dob, rr, g->v[p].b, nh, hd, 1, hd);
     } else {
       plan_wgrad(wp, bw, H, H, B * lq, opnd(cq, M * H, lq), opnd(s.O[p], H), g->o[p].w, g->o[p].b,
                  1.f / (float)lq);
@@ -343,16 +343,17 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
     }
     STAGE_TRY("fwd.pool_u", launch_pool_u(pp.data(), d->num_pairs, B, nh, hd, H, st));
     std::vector<GemmJob> jobs;
-    for (int g = 0; g < d->num_pairs; ++g)
-      for (int hh = 0; hh < nh; ++hh) {
-        GemmJob j = make_job(B, hd, s.Ob[g] + hh * hd, H, EPI_BIAS | EPI_BIAS_RS);
-        j.g.bias = W->v[g].b + hh * hd;
-        j.g.bias_rs = s.r[g];
-        j.g.bias_rs_ld = nh;
-        j.g.bias_rs_off = hh;
-        add_src(j, opnd(s.U[g] + (size_t)hh * H, nh * H), opnd(W->v[g].w + (size_t)hh * hd * H, H), H);
-        jobs.push_back(j);
-      }
+    for (int g = 0; g < d->num_pairs; ++g) {
+      // Obar[:, h*hd:(h+1)*hd] = U_h W_v[h*hd:(h+1)*hd, :]^T + r_h b_v,h  (batch over heads)
+      GemmJob j = make_job(B, hd, s.Ob[g], H, EPI_BIAS | EPI_BIAS_RS);
+      j.g.bias = W->v[g].b;
+      j.g.bias_rs = s.r[g];
+      j.g.bias_rs_ld = nh;
+      j.g.nbatch = nh;
+      j.g.bs_a = H; j.g.bs_b = hd * H; j.g.bs_c = hd; j.g.bs_bias = hd; j.g.bs_brs = 1;
+      add_src(j, opnd(s.U[g], nh * H), opnd(W->v[g].w, H), H);
+      jobs.push_back(j);
+    }
     STAGE_TRY("fwd.vbar_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, 0.f, rng, st));
     jobs.clear();
     for (int g = 0; g < d->num_pairs; ++g) {
@@ -466,12 +467,16 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
     }
     STAGE_TRY("bwd.out_dO_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, 0.f, rng, st));
     jobs.clear();
-    for (int g = 0; g < d->num_pairs; ++g)
-      for (int hh = 0; hh < nh; ++hh) {
-        GemmJob j = make_job(B, H, w.dU[g] + (size_t)hh * H, nh * H, 0);
-        add_src(j, opnd(w.dOb[g] + hh * hd, H), opnd(W->v[g].w + (size_t)hh * hd * H, H), hd);
-        jobs.push_back(j);
-      }
+    for (int g = 0; g < d->num_pairs; ++g) {
+      // dU_h = dObar_h W_v[h*hd:(h+1)*hd, :]  (batch over heads)
+      GemmJob j = make_job(B, H, w.dU[g], nh * H, 0);
+      j.g.nbatch = nh;
+      j.g.bs_a = hd; j.g.bs_b = hd * H; j.g.bs_c = H;
+      Operand a = opnd(w.dOb[g], H);
+      a.vec = (hd % 4 == 0) && (H % 4 == 0);
+      add_src(j, a, opnd(W->v[g].w, H), hd);
+      jobs.push_back(j);
+    }
     STAGE_TRY("bwd.du_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, 0.f, rng, st));
     std::vector<PoolPair> pp(d->num_pairs);
     for (int g = 0; g < d->num_pairs; ++g) {
@@ -562,6 +567,12 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
       STAGE_TRY("bwd.dx_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, p, rng, st));
   }
   // (6) every weight gradient: split-K slabs, then one deterministic reduce
+  // biggest jobs first so every launch (<= 8 jobs) is a full grid
+  std::stable_sort(wp.jobs.begin(), wp.jobs.end(), [](const GemmJob& a, const GemmJob& b) {
+    const int64_t wa = (int64_t)a.g.nsplit * std::max(1, a.g.nbatch) * a.g.M * a.g.N;
+    const int64_t wb = (int64_t)b.g.nsplit * std::max(1, b.g.nbatch) * b.g.M * b.g.N;
+    return wa > wb;
+  });
   STAGE_TRY("bwd.wgrad_gemm", launch_gemm(wp.jobs.data(), (int)wp.jobs.size(), MODE_KR, MODE_KR, p, rng, st));
   STAGE_TRY("bwd.wgrad_reduce", launch_reduce(wp.reds.data(), (int)wp.reds.size(), st));
   return MMF_OK;

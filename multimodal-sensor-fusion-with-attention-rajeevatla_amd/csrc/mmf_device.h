@@ -36,39 +36,78 @@ __device__ __forceinline__ uint4 philox_block(const RngSnap& s, uint32_t site, u
                   (uint32_t)s.seed, (uint32_t)(s.seed >> 32));
 }
 
-__device__ __forceinline__ float u01(uint32_t w) { return (float)(w >> 8) * (1.0f / 16777216.0f); }
-
+// One Philox call = 128 random bits = 8 keep decisions of 16 bits each:
+// element idx uses block idx>>3, word (idx>>1)&3, half idx&1, and is kept iff
+// u16 * 2^-16 >= p (p is quantised to 2^-16, |error| < 1.6e-5).
 __device__ __forceinline__ uint32_t pick(const uint4& r, int j) {
   return j == 0 ? r.x : (j == 1 ? r.y : (j == 2 ? r.z : r.w));
+}
+__device__ __forceinline__ uint32_t p16(float p) {
+  return (uint32_t)ceilf(p * 65536.0f);   // keep iff u16 >= p16
+}
+__device__ __forceinline__ bool keep_from(const uint4& r, int e, uint32_t thr) {
+  const uint32_t w = pick(r, (e >> 1) & 3);
+  return ((w >> (16 * (e & 1))) & 0xFFFFu) >= thr;
 }
 
 // keep decision for element idx of tensor `site` (drop with probability p)
 __device__ __forceinline__ bool keep1(const RngSnap& s, uint32_t site, uint64_t idx, float p) {
-  const uint4 r = philox_block(s, site, idx >> 2);
-  return u01(pick(r, (int)(idx & 3))) >= p;
+  const uint4 r = philox_block(s, site, idx >> 3);
+  return keep_from(r, (int)(idx & 7), p16(p));
 }
 
 // keep decisions for idx .. idx+3 (bit j set => element idx+j kept)
 __device__ __forceinline__ uint32_t keep4(const RngSnap& s, uint32_t site, uint64_t idx, float p) {
-  const uint64_t b0 = idx >> 2;
-  const int o = (int)(idx & 3);
+  const uint64_t b0 = idx >> 3;
+  const int o = (int)(idx & 7);
+  const uint32_t thr = p16(p);
   const uint4 r0 = philox_block(s, site, b0);
   uint32_t bits = 0;
-  if (o == 0) {
-    bits |= (u01(r0.x) >= p) ? 1u : 0u;
-    bits |= (u01(r0.y) >= p) ? 2u : 0u;
-    bits |= (u01(r0.z) >= p) ? 4u : 0u;
-    bits |= (u01(r0.w) >= p) ? 8u : 0u;
+  if (o <= 4) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bits |= keep_from(r0, o + j, thr) ? (1u << j) : 0u;
     return bits;
   }
   const uint4 r1 = philox_block(s, site, b0 + 1);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int t = o + j;
-    const uint32_t w = t < 4 ? pick(r0, t) : pick(r1, t - 4);
-    bits |= (u01(w) >= p) ? (1u << j) : 0u;
+    bits |= (t < 8 ? keep_from(r0, t, thr) : keep_from(r1, t - 8, thr)) ? (1u << j) : 0u;
   }
   return bits;
+}
+
+// Keep mask for one lane's 16 accumulator registers of a 32-key MFMA tile whose
+// first element index is `base` (a row of a (.., Lk) probability tensor): reg r
+// holds key 8*(r>>2) + 4*half + (r&3).  The two lane halves split the four
+// 8-key Philox blocks (2 calls per lane instead of 4) and swap the decisions
+// that belong to the other half with one xor-32 shuffle.  Bit r set => kept.
+// Every lane of the wave must call it (it shuffles); `aligned` (base % 8 == 0 in
+// every lane, e.g. Lk % 8 == 0) must be wave-uniform.
+__device__ __forceinline__ uint32_t keep_tile16(const RngSnap& s, uint32_t site, uint64_t base, float p,
+                                                int half, bool active, bool aligned) {
+  uint32_t mine = 0, other = 0;
+  if (aligned) {
+    const uint32_t thr = p16(p);
+    if (active) {
+#pragma unroll
+      for (int gi = 0; gi < 2; ++gi) {
+        const int g = 2 * half + gi;
+        const uint4 r = philox_block(s, site, (base >> 3) + g);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          mine |= keep_from(r, 4 * half + j, thr) ? (1u << (4 * g + j)) : 0u;
+          other |= keep_from(r, 4 * (1 - half) + j, thr) ? (1u << (4 * g + j)) : 0u;
+        }
+      }
+    }
+    return mine | __shfl_xor(other, 32);
+  }
+  if (active) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) mine |= keep4(s, site, base + 8 * g + 4 * half, p) << (4 * g);
+  }
+  return mine;
 }
 
 }  // namespace mmf

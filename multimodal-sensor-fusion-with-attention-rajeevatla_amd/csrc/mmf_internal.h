@@ -78,6 +78,11 @@ struct GemmGroup {
   // part_db[split][M] = row sums of A over the split (bias grad of a TN dW).
   int32_t nsplit, kchunk;
   float* part_db;
+  // strided batch: nbatch identical problems, element i offsets every source's A/B
+  // by i*bs_a / i*bs_b, C by i*bs_c (partial: i*nsplit*M*N, part_db i*nsplit*M),
+  // bias by i*bs_bias and bias_rs_off by i*bs_brs.
+  int32_t nbatch;
+  int32_t bs_a, bs_b, bs_c, bs_bias, bs_brs;
 };
 
 constexpr int GEMM_MAX_GROUPS = 8;
@@ -114,6 +119,7 @@ struct ReduceJob {
   const float* part; const float* part_db;
   float* out; float* db;
   int32_t nsplit, M, N;
+  int32_t nbatch, bs_out, bs_db;   // batch i: part += i*nsplit*M*N, out += i*bs_out, db += i*bs_db
 };
 hipError_t launch_reduce(const ReduceJob* jobs, int njobs, hipStream_t st);
 

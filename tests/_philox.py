@@ -1,9 +1,9 @@
 """numpy Philox4x32-10 replay of the device dropout streams (test infrastructure).
 
 The HIP kernels draw keep decisions as (csrc/mmf_device.h):
-    counter = (idx>>2 lo32, idx>>2 hi32, site, offset lo32), key = (seed lo32, seed hi32)
-    word    = philox10(counter, key)[idx & 3]
-    keep    = float(word >> 8) * 2^-24 >= p
+    counter = (idx>>3 lo32, idx>>3 hi32, site, offset lo32), key = (seed lo32, seed hi32)
+    word    = philox10(counter, key)[(idx >> 1) & 3]
+    keep    = ((word >> 16*(idx & 1)) & 0xFFFF) >= ceil(p * 65536)
 so a test can rebuild the exact masks and run the CPU oracle in train mode.
 """
 from __future__ import annotations
@@ -31,15 +31,19 @@ def philox10(c0, c1, c2, c3, k0, k1):
 
 
 def keep_mask(shape, site: int, seed: int, offset: int, p: float) -> np.ndarray:
+    """8 decisions per Philox call: block idx>>3, word (idx>>1)&3, 16-bit half idx&1;
+    keep iff u16 >= ceil(p * 65536) (csrc/mmf_device.h keep1/keep4)."""
     n = int(np.prod(shape))
     idx = np.arange(n, dtype=np.uint64)
-    blk = idx >> np.uint64(2)
+    blk = idx >> np.uint64(3)
     words = philox10(blk & _MASK, blk >> np.uint64(32), np.full(n, site, np.uint64),
                      np.full(n, offset & 0xFFFFFFFF, np.uint64), seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
-    sel = (idx & np.uint64(3)).astype(np.int64)
+    sel = ((idx >> np.uint64(1)) & np.uint64(3)).astype(np.int64)
     w = np.choose(sel, words)
-    u = (w >> np.uint64(8)).astype(np.float32) * np.float32(1.0 / 16777216.0)
-    return (u >= np.float32(p)).reshape(shape)
+    half = (idx & np.uint64(1)) * np.uint64(16)
+    u16 = (w >> half) & np.uint64(0xFFFF)
+    thr = np.uint64(int(np.ceil(np.float32(p) * np.float32(65536.0))))
+    return (u16 >= thr).reshape(shape)
 
 
 def mask_provider(seed: int, offset: int, p: float):
