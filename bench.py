@@ -39,11 +39,40 @@ WORKLOADS = {
 }
 
 
+def pooled_plan(L, heads):
+    """csrc/hybrid.hip use_pool(): key lengths <= 128 and <= 8 heads."""
+    return max(L, 1) <= 128 and heads <= 8
+
+
 def stage_flops(M, B, L, D, H, heads, C):
     """Algorithmic FLOPs of each launch group (no recompute counted)."""
     Le = max(L, 1)
     P = M * (M - 1)
     rows = B * Le
+    if pooled_plan(L, heads):
+        # pooled-output plan (DESIGN.md): no V / O / attended (B, L, H) tensors
+        return {
+            "fwd.proj_gemm": 2 * rows * D * H * M,
+            "fwd.qkv_gemm": 2 * 2 * rows * H * H * P,
+            "fwd.attn": 2 * B * Le * Le * H * P,             # S = Q K^T (+ softmax, column mean)
+            "fwd.pool_u": 2 * B * heads * Le * H * P,         # U_h = pbar_h P_k
+            "fwd.vbar_gemm": 2 * B * H * H * P,
+            "fwd.out_gemm": 2 * B * H * H * P,
+            "fwd.cls1_gemm": 2 * B * H * H,
+            "fwd.cls2_gemm": 2 * B * H * C,
+            "bwd.cls_dz1_gemm": 2 * B * C * H,
+            "bwd.cls_dfused_gemm": 2 * B * H * H,
+            "bwd.out_dO_gemm": 2 * B * H * H * P,
+            "bwd.du_gemm": 2 * B * H * H * P,
+            "bwd.pool_dpbar": 2 * B * heads * Le * H * P,
+            "bwd.attn_dq": 2 * B * Le * Le * H * P,          # dQ = dS K (S recompute not counted)
+            "bwd.attn_dk": 2 * B * Le * Le * H * P,          # dK = dS^T Q
+            "bwd.pool_e": 2 * B * heads * Le * H * P,
+            "bwd.dZ_gemm": 2 * rows * H * H * 2 * P,         # dQ W_q + dK W_k into every modality
+            "bwd.dx_gemm": 2 * rows * H * D * M,
+            "bwd.wgrad_gemm": 2 * rows * H * D * M + 2 * 2 * rows * H * H * P + 2 * 2 * B * H * H * P
+                              + 2 * B * H * (H + C),
+        }
     f = {
         "fwd.proj_gemm": 2 * rows * D * H * M,
         "fwd.qkv_gemm": 3 * 2 * rows * H * H * P,

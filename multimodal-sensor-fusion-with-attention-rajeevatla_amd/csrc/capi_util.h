@@ -91,7 +91,7 @@ inline Operand opnd(const float* p, int ld, int row_div = 1) {
   o.ld = ld;
   o.row_div = row_div;
   o.vec = (ld % 4 == 0) && aligned16(p);
-  o.xf = -1;
+  o.pad_ = 0;
   return o;
 }
 
@@ -119,13 +119,13 @@ inline void add_src(GemmJob& j, Operand a, Operand b, int K) {
   s.K = K;
 }
 
-// Split of a weight-gradient contraction over `rows`: ~256 rows per slab, so a
-// launch of 8 (128x128-output) jobs at B*L = 32768 rows fills the chip with
-// 1024 workgroups (4 per CU).
+// Split of a weight-gradient contraction over `rows`: ~512 rows per slab, so a
+// launch of 8 (128x128-output) jobs at B*L = 32768 rows is 512 workgroups
+// (2 per CU) and the slabs of all 15 such jobs are 63 MB.
 inline void split_rows(int rows, int& nsplit, int& kchunk) {
-  nsplit = rows / 256;
+  nsplit = rows / 512;
   if (nsplit < 1) nsplit = 1;
-  if (nsplit > 128) nsplit = 128;
+  if (nsplit > 64) nsplit = 64;
   kchunk = (rows + nsplit - 1) / nsplit;
   kchunk = (kchunk + 31) & ~31;
   nsplit = (rows + kchunk - 1) / kchunk;
@@ -150,8 +150,7 @@ struct WgradPlan {
 // explicit (not out_b != nullptr) so a sizing pass with null grads reserves the
 // same workspace as the real call.
 inline void plan_wgrad(WgradPlan& wp, Bump& ws, int M, int N, int rows, Operand a, Operand b,
-                       float* out_w, float* out_b, bool has_db, float alpha = 1.f,
-                       const Xform* xfb = nullptr) {
+                       float* out_w, float* out_b, bool has_db, float alpha = 1.f) {
   int nsplit, kchunk;
   split_rows(rows, nsplit, kchunk);
   float* part = ws.take<float>((size_t)nsplit * M * N);
@@ -162,10 +161,6 @@ inline void plan_wgrad(WgradPlan& wp, Bump& ws, int M, int N, int rows, Operand 
   j.g.kchunk = kchunk;
   j.g.part_db = part_db;
   add_src(j, a, b, rows);
-  if (xfb) {
-    j.has_xf_b[0] = 1;
-    j.xf_b[0] = *xfb;
-  }
   wp.jobs.push_back(j);
   ReduceJob r;
   memset(&r, 0, sizeof(r));
@@ -210,8 +205,8 @@ inline void plan_wgrad_batched(WgradPlan& wp, Bump& ws, int M, int N, int rows, 
 
 // Linear layer with bias (the common case).
 inline void plan_wgrad(WgradPlan& wp, Bump& ws, int M, int N, int rows, Operand a, Operand b,
-                       float* out_w, float* out_b, float alpha = 1.f, const Xform* xfb = nullptr) {
-  plan_wgrad(wp, ws, M, N, rows, a, b, out_w, out_b, true, alpha, xfb);
+                       float* out_w, float* out_b, float alpha = 1.f) {
+  plan_wgrad(wp, ws, M, N, rows, a, b, out_w, out_b, true, alpha);
 }
 
 }  // namespace mmf

@@ -1,18 +1,29 @@
 // Grouped, multi-source fp32 GEMM on CDNA4 matrix cores (v_mfma_f32_32x32x2_f32).
 //
-// One launch covers several independent outputs ("groups": e.g. the Q/K/V
+// One launch covers several independent outputs ("groups": e.g. the Q/K
 // projections of every modality pair, src/attention.py:104-106, or the
 // per-modality projections, src/fusion.py:291-298).  A group may sum several
 // (A, B) sources into one output tile (the backward of a tensor that feeds
-// several Linears, e.g. dP_m = sum over pairs of dQ W_q + dK W_k + dV W_v),
-// and may split its contraction into slabs (dW = dY^T X over B*L rows) that a
+// several Linears, e.g. dP_m = sum over pairs of dQ W_q + dK W_k), and may
+// split its contraction into slabs (dW = dY^T X over B*L rows) that a
 // deterministic reduce kernel sums.
 //
-// Tile: 128x128x32, 256 threads = 4 waves as 2x2, each wave 64x64 = 2x2
-// MFMA 32x32 accumulators (64 acc VGPRs).  Tiles are staged global -> regs ->
-// LDS with the next tile's global loads in flight during the MFMAs.  The LDS
-// image is contraction-major ([kk][i]) so every MFMA operand is one
-// conflict-free ds_read_b32 (lanes 0-31 read 32 consecutive dwords).
+// Tile: 128x128 outputs per 256-thread workgroup = 4 waves as 2x2, each wave
+// 64x64 = 2x2 MFMA 32x32 accumulators.  Two kernels share that tiling and the
+// epilogue:
+//  * gemm_lds_kernel (the fast path): operand tiles (128 x 32 fp32) go
+//    global -> LDS by LDS-DMA (global_load_lds_dwordx4, no VGPR round trip),
+//    double-buffered so tile t+1 streams in while tile t feeds the MFMAs; one
+//    barrier per k-tile.  k-contiguous tiles are stored [e][k] with an XOR
+//    swizzle on the 16-B slot (applied on the global source address, the LDS
+//    image stays lane-linear) so each ds_read_b128 fragment read (4 k-steps of
+//    one lane) is bank-conflict free; k-strided tiles are stored [k][e] and
+//    read with conflict-free ds_read_b32.
+//  * gemm_generic_kernel: register-staged, element-guarded; for operands that
+//    are not float4-able (odd leading dims, K % 4 != 0).
+// MFMA k-order: within each 8-deep k chunk j, lane half h feeds k = 8j+4h+s at
+// step s (the same permutation on A and B, so the contraction is unchanged).
+#include <algorithm>
 #include <cstring>
 
 #include "mmf_device.h"
@@ -22,30 +33,329 @@ namespace mmf {
 namespace {
 
 constexpr int BM = 128, BN = 128, BK = 32, NT = 256;
-constexpr int LDS_STRIDE = BM + 4;      // KR image (float4 writes need 16-B rows)
-constexpr int LDS_STRIDE_T = BM + 1;    // RK image (transposing scalar writes, conflict-free)
+constexpr int LDS_STRIDE = BM + 4;      // generic kernel, KR image
+constexpr int LDS_STRIDE_T = BM + 1;    // generic kernel, RK image (transposing writes)
 
-struct TileRegs { float4 v[4]; };
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ float apply_xf(float v, const Xform& xf, int64_t srow, int64_t col,
-                                          const RngSnap& rs, float p, float inv_keep) {
-  if (xf.rowscale) v *= xf.rowscale[(srow / xf.rs_div) * xf.rs_stride + xf.rs_off];
-  if (xf.drop_site && p > 0.f) {
-    v = keep1(rs, xf.drop_site, (uint64_t)srow * (uint64_t)xf.ncols + (uint64_t)col, p) ? v * inv_keep
-                                                                                           : 0.f;
-  }
-  return v;
+struct TileCtx {
+  int i0, j0, batch, split, nsplit;
+  float* Cb;
+  float* part_db;
+  const float* biasb;
+  int brs_off;
+};
+
+__device__ __forceinline__ bool tile_ctx(const GemmGroup& G, TileCtx& t) {
+  const int tiles_n = (G.N + BN - 1) / BN;
+  const int tiles_m = (G.M + BM - 1) / BM;
+  t.nsplit = (G.epi & EPI_PARTIAL) ? G.nsplit : 1;
+  const int per_batch = tiles_m * tiles_n * t.nsplit;
+  t.batch = blockIdx.x / per_batch;
+  if (t.batch >= G.nbatch) return false;
+  int tile = blockIdx.x - t.batch * per_batch;
+  t.split = tile % t.nsplit;
+  tile /= t.nsplit;
+  t.i0 = (tile / tiles_n) * BM;
+  t.j0 = (tile % tiles_n) * BN;
+  t.Cb = (G.epi & EPI_PARTIAL) ? G.C + (int64_t)t.batch * t.nsplit * G.M * G.N
+                               : G.C + (int64_t)t.batch * G.bs_c;
+  t.part_db = G.part_db ? G.part_db + (int64_t)t.batch * t.nsplit * G.M : nullptr;
+  t.biasb = G.bias ? G.bias + (int64_t)t.batch * G.bs_bias : nullptr;
+  t.brs_off = G.bias_rs_off + t.batch * G.bs_brs;
+  return true;
 }
 
-// Load one 128 x 32 tile of an operand into registers.
+// ------------------------------------------------------------------ epilogue
+// The accumulators go through LDS (two passes of 64 rows, [64][BN+4] image)
+// so the epilogue runs row-major: each thread finishes 8 consecutive columns
+// of a row at a time (float4 loads/stores, one Philox call per 8 dropout
+// decisions), and the code stays small (the kernels are I-cache sensitive at
+// small grids).  Order: v = alpha*acc; +bias[j] (x bias_rs[i]); +rowadd;
+// +addm; relu; gate; rowscale; dropout (keep(site, i*N + j)).
+constexpr int CS = BN + 4;
+
+__device__ __forceinline__ void epilogue(const GemmGroup& G, const TileCtx& T, f32x16 (&acc)[2][2], float* cs,
+                                         const RngSnap& rs, float p, float inv_keep, int wm, int wn, int h,
+                                         int c) {
+  const int t = threadIdx.x;
+  const int epi = G.epi;
+  const bool partial = (epi & EPI_PARTIAL) != 0;
+  const bool drop = !partial && (epi & EPI_DROP) && p > 0.f;
+  const bool coop = drop && (G.N % 8) == 0;
+  const uint32_t thr = p16(p);
+  float* const out = partial ? T.Cb + (int64_t)T.split * G.M * G.N : T.Cb;
+  const int ldc = partial ? G.N : G.ldc;
+  const bool vst = (ldc % 4) == 0 && ((uintptr_t)out & 15) == 0;
+  for (int pass = 0; pass < 2; ++pass) {
+    __syncthreads();
+    if (wm == pass) {
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) cs[(a * 32 + acc_row(r, h)) * CS + wn * 64 + b * 32 + c] = acc[a][b][r];
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int g = t; g < 64 * (BN / 8); g += NT) {
+      const int lr = g >> 4, cg = (g & 15) * 8;
+      const int i = T.i0 + pass * 64 + lr, j0 = T.j0 + cg;
+      if (i >= G.M || j0 >= G.N) continue;
+      const int nv = min(8, G.N - j0);
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(cs + lr * CS + cg);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(cs + lr * CS + cg + 4);
+      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      if (partial) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] *= G.alpha;
+      } else {
+        uint4 rr = make_uint4(0, 0, 0, 0);
+        if (coop) rr = philox_block(rs, G.drop_site, ((uint64_t)i * (uint64_t)G.N + (uint64_t)j0) >> 3);
+        const float brs = (epi & EPI_BIAS_RS) ? G.bias_rs[(int64_t)i * G.bias_rs_ld + T.brs_off] : 1.f;
+        const float rsc = (epi & EPI_ROWSCALE) ? G.rowscale[(int64_t)(i / G.rs_div) * G.rs_stride + G.rs_off] : 1.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          if (e >= nv) break;
+          const int j = j0 + e;
+          float x = v[e] * G.alpha;
+          if (epi & EPI_BIAS) x += T.biasb[j] * brs;
+          if (epi & EPI_ROWADD) x += G.rowadd_scale * G.rowadd[(int64_t)(i / G.rowadd_div) * G.ld_rowadd + j];
+          if (epi & EPI_ADDMAT) x += G.addm[(int64_t)i * G.ld_addm + j];
+          if (epi & EPI_RELU) x = fmaxf(x, 0.f);
+          if (epi & EPI_GATE) x = G.gate[(int64_t)i * G.ld_gate + j] > 0.f ? x * G.gate_scale : 0.f;
+          x *= rsc;
+          if (drop) {
+            const bool keep = coop ? keep_from(rr, e, thr)
+                                   : keep1(rs, G.drop_site, (uint64_t)i * (uint64_t)G.N + (uint64_t)j, p);
+            x = keep ? x * inv_keep : 0.f;
+          }
+          v[e] = x;
+        }
+      }
+      float* o = out + (int64_t)i * ldc + j0;
+      if (vst && nv == 8) {
+        *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};
+        *reinterpret_cast<f32x4*>(o + 4) = f32x4{v[4], v[5], v[6], v[7]};
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (e < nv) o[e] = v[e];
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ LDS-DMA kernel
+// k-tiles of DK = 16 in a 3-deep LDS ring: tile t+2 is issued while tile t
+// feeds the MFMAs and tile t+1 is in flight (2 tiles = 32 KB in flight per
+// workgroup, 3 workgroups per CU).  A 128 x 16 operand tile is 8 KB = 8
+// wave-instructions of 1 KB (wave w issues 2).  Rows past `eext` and k past
+// `kend` are clamped to valid addresses; the k tail is zeroed afterwards
+// (zero_tail), the row tail only feeds outputs that are never stored.
+constexpr int DK = 16, NSTAGE = 3;
+constexpr int DTILE = BM * DK;           // floats per operand tile (8 KB)
+constexpr int DMA_PER_TILE = 4;          // glds instructions per wave per (A, B) tile pair
+
+template <int MODE>
+__device__ __forceinline__ void stage_tile(float* lds, const Operand& op, int64_t boff, int e0, int eext, int k0,
+                                           int kend, int wave, int lane) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int ins = wave * 2 + u;
+    const float* src;
+    if (MODE == MODE_RK) {
+      // [e][16] image, 64-B rows; 16-B slot XOR-swizzled by (row >> 2) & 3
+      const int row = ins * 16 + (lane >> 2);
+      const int slot = (lane & 3) ^ ((row >> 2) & 3);
+      const int e = min(e0 + row, eext - 1);
+      const int k = min(k0 + 4 * slot, kend - 4);
+      src = op.ptr + boff + (int64_t)(e / op.row_div) * op.ld + k;
+    } else {
+      // [16][128] image, 512-B k-rows
+      const int kr = min(k0 + ins * 2 + (lane >> 5), kend - 1);
+      const int e = min(e0 + 4 * (lane & 31), eext - 4);
+      src = op.ptr + boff + (int64_t)(kr / op.row_div) * op.ld + e;
+    }
+    __builtin_amdgcn_global_load_lds((const void*)src,
+                                     (__attribute__((address_space(3))) void*)(lds + ins * 256), 16, 0, 0);
+  }
+}
+
+// Zero the k >= kv part of a staged tile (last tile of a contraction; kv % 4 == 0 for RK).
+template <int MODE>
+__device__ __forceinline__ void zero_tail(float* lds, int kv) {
+  const int t = threadIdx.x;
+  if (MODE == MODE_RK) {
+    const int row = t >> 1;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int slot = 2 * (t & 1) + q;
+      if (4 * slot >= kv)
+        *reinterpret_cast<f32x4*>(lds + row * DK + ((slot ^ ((row >> 2) & 3)) << 2)) = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int idx = t + q * NT;                 // float4 index in the [16][128] image
+      if (idx / (BM / 4) >= kv) *reinterpret_cast<f32x4*>(lds + idx * 4) = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+}
+
+// Fragment of 4 consecutive MFMA k-steps (chunk j) for tile row/col e.
+template <int MODE>
+__device__ __forceinline__ f32x4 frag(const float* lds, int e, int j, int h) {
+  if (MODE == MODE_RK) {
+    const int slot = (2 * j + h) ^ ((e >> 2) & 3);
+    return *reinterpret_cast<const f32x4*>(lds + e * DK + (slot << 2));
+  } else {
+    const float* p = lds + (8 * j + 4 * h) * BM + e;
+    return f32x4{p[0], p[BM], p[2 * BM], p[3 * BM]};
+  }
+}
+
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// (source, k0) cursor over one tile's contraction
+struct KCursor { int si, k0, kend; };
+
+template <int AMODE, int BMODE>
+__global__ __launch_bounds__(NT, 3) void gemm_lds_kernel(const GemmArgs args) {
+  const GemmGroup& G = args.g[blockIdx.y];
+  TileCtx T;
+  if (!tile_ctx(G, T)) return;
+  const int64_t offA = (int64_t)T.batch * G.bs_a, offB = (int64_t)T.batch * G.bs_b;
+
+  // one LDS object: NSTAGE x [A | B] tiles (also the epilogue image) + 128 floats for the row-sum combine
+  __shared__ __attribute__((aligned(16))) float lds[NSTAGE * 2 * DTILE + BM];
+  static_assert(NSTAGE * 2 * DTILE >= 64 * CS, "epilogue image does not fit");
+
+  const int t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  RngSnap rs{0, 0};
+  const float p = args.drop_p;
+  const float inv_keep = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  if (p > 0.f && args.rng) rs = *args.rng;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  const bool partial = (G.epi & EPI_PARTIAL) != 0;
+  const bool want_db = partial && T.part_db != nullptr && T.j0 == 0;
+  float dbsum = 0.f;
+
+  auto first_from = [&](int si) {
+    KCursor k;
+    for (k.si = si; k.si < G.src_count; ++k.si) {
+      const GemmSrc& S = args.s[G.src_begin + k.si];
+      k.k0 = partial ? T.split * G.kchunk : 0;
+      k.kend = partial ? min(S.K, k.k0 + G.kchunk) : S.K;
+      if (k.k0 < k.kend) break;
+    }
+    return k;
+  };
+  auto advance = [&](KCursor k) {
+    if (k.si >= G.src_count) return k;
+    k.k0 += DK;
+    if (k.k0 < k.kend) return k;
+    return first_from(k.si + 1);
+  };
+  auto stage = [&](int buf, const KCursor& k) {
+    const GemmSrc& S = args.s[G.src_begin + k.si];
+    float* At = lds + buf * 2 * DTILE;
+    stage_tile<AMODE>(At, S.a, offA, T.i0, G.M, k.k0, k.kend, wave, lane);
+    stage_tile<BMODE>(At + DTILE, S.b, offB, T.j0, G.N, k.k0, k.kend, wave, lane);
+  };
+
+  KCursor cur = first_from(0);
+  if (cur.si < G.src_count) {
+    KCursor nx1 = advance(cur);
+    stage(0, cur);
+    if (nx1.si < G.src_count) stage(1, nx1);
+    int buf = 0;
+    for (;;) {
+      // tile `cur` has landed (only nx1's DMAs may still be outstanding) and
+      // every wave is done reading the buffer that nx2 overwrites
+      if (nx1.si < G.src_count) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      static_assert(DMA_PER_TILE == 4, "vmcnt literal above");
+      lds_barrier();
+      float* At = lds + buf * 2 * DTILE;
+      float* Bt = At + DTILE;
+      const int kv = cur.kend - cur.k0;
+      if (kv < DK) {
+        zero_tail<AMODE>(At, kv);
+        zero_tail<BMODE>(Bt, kv);
+        lds_barrier();
+      }
+      const KCursor nx2 = advance(nx1);
+      if (nx2.si < G.src_count) stage(buf == 0 ? 2 : buf - 1, nx2);
+      if (want_db) {
+        // bias grad of a TN dW: row sums of A over this k-tile (thread: row t&127, k half t>>7)
+        const int row = t & (BM - 1), kh = t >> 7;
+#pragma unroll
+        for (int q = 0; q < DK / 2; ++q) {
+          const int kk = kh * (DK / 2) + q;
+          dbsum += AMODE == MODE_KR ? At[kk * BM + row]
+                                    : At[row * DK + ((((kk >> 2) ^ ((row >> 2) & 3))) << 2) + (kk & 3)];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < DK / 8; ++j) {
+        f32x4 af[2], bf[2];
+#pragma unroll
+        for (int a = 0; a < 2; ++a) af[a] = frag<AMODE>(At, wm * 64 + a * 32 + c, j, h);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) bf[b] = frag<BMODE>(Bt, wn * 64 + b * 32 + c, j, h);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) acc[a][b] = mfma32(af[a][s], bf[b][s], acc[a][b]);
+      }
+      if (nx1.si >= G.src_count) break;
+      cur = nx1;
+      nx1 = nx2;
+      buf = buf == NSTAGE - 1 ? 0 : buf + 1;
+    }
+  }
+
+  if (want_db) {
+    float* red = lds + NSTAGE * 2 * DTILE;
+    __syncthreads();
+    if (t >= BM) red[t - BM] = dbsum;
+    __syncthreads();
+    if (t < BM && T.i0 + t < G.M)
+      T.part_db[(int64_t)T.split * G.M + T.i0 + t] = (dbsum + red[t]) * G.alpha;
+  }
+  epilogue(G, T, acc, lds, rs, p, inv_keep, wm, wn, h, c);
+}
+
+// ------------------------------------------------------------------ generic kernel
+struct TileRegs { float4 v[4]; };
+
+// Load one 128 x 32 tile of an operand into registers (element-guarded).
 //  MODE_RK: stored [e][kk] (kk contiguous): thread t covers e = t/8 + 32u, kk = 4*(t%8)..+3
 //  MODE_KR: stored [kk][e] (e contiguous):  thread t covers kk = t/32 + 8u, e = 4*(t%32)..+3
 template <int MODE>
-__device__ __forceinline__ void load_tile(TileRegs& R, const Operand& op, int64_t boff, const Xform* xft, int e0,
-                                          int eext, int k0, int kend, const RngSnap& rs, float p,
-                                          float inv_keep) {
+__device__ __forceinline__ void load_tile(TileRegs& R, const Operand& op, int64_t boff, int e0, int eext, int k0,
+                                          int kend) {
   const int t = threadIdx.x;
-  const bool has_xf = op.xf >= 0;
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     int e, kk;
@@ -54,34 +364,24 @@ __device__ __forceinline__ void load_tile(TileRegs& R, const Operand& op, int64_
     float x[4] = {0.f, 0.f, 0.f, 0.f};
     if (MODE == MODE_RK) {
       if (e < eext) {
-        const int64_t srow = e / op.row_div;
-        const float* rowp = op.ptr + boff + srow * (int64_t)op.ld;
+        const float* rowp = op.ptr + boff + (int64_t)(e / op.row_div) * op.ld;
         if (op.vec && kk + 3 < kend) {
           const float4 f = *reinterpret_cast<const float4*>(rowp + kk);
           x[0] = f.x; x[1] = f.y; x[2] = f.z; x[3] = f.w;
         } else {
 #pragma unroll
-          for (int c = 0; c < 4; ++c) if (kk + c < kend) x[c] = rowp[kk + c];
-        }
-        if (has_xf) {
-#pragma unroll
-          for (int c = 0; c < 4; ++c) x[c] = apply_xf(x[c], xft[op.xf], srow, kk + c, rs, p, inv_keep);
+          for (int q = 0; q < 4; ++q) if (kk + q < kend) x[q] = rowp[kk + q];
         }
       }
     } else {
       if (kk < kend) {
-        const int64_t srow = kk / op.row_div;
-        const float* rowp = op.ptr + boff + srow * (int64_t)op.ld;
+        const float* rowp = op.ptr + boff + (int64_t)(kk / op.row_div) * op.ld;
         if (op.vec && e + 3 < eext) {
           const float4 f = *reinterpret_cast<const float4*>(rowp + e);
           x[0] = f.x; x[1] = f.y; x[2] = f.z; x[3] = f.w;
         } else {
 #pragma unroll
-          for (int c = 0; c < 4; ++c) if (e + c < eext) x[c] = rowp[e + c];
-        }
-        if (has_xf) {
-#pragma unroll
-          for (int c = 0; c < 4; ++c) x[c] = apply_xf(x[c], xft[op.xf], srow, e + c, rs, p, inv_keep);
+          for (int q = 0; q < 4; ++q) if (e + q < eext) x[q] = rowp[e + q];
         }
       }
     }
@@ -108,29 +408,17 @@ __device__ __forceinline__ void store_tile(const TileRegs& R, float* S) {
 }
 
 template <int AMODE, int BMODE>
-__global__ __launch_bounds__(NT) void gemm_kernel(const GemmArgs args) {
+__global__ __launch_bounds__(NT) void gemm_generic_kernel(const GemmArgs args) {
   const GemmGroup& G = args.g[blockIdx.y];
-  const int tiles_n = (G.N + BN - 1) / BN;
-  const int tiles_m = (G.M + BM - 1) / BM;
-  const int nsplit = (G.epi & EPI_PARTIAL) ? G.nsplit : 1;
-  const int per_batch = tiles_m * tiles_n * nsplit;
-  const int batch = blockIdx.x / per_batch;
-  if (batch >= G.nbatch) return;
-  int tile = blockIdx.x - batch * per_batch;
-  const int split = tile % nsplit;
-  tile /= nsplit;
-  const int tm = tile / tiles_n, tn = tile % tiles_n;
-  const int i0 = tm * BM, j0 = tn * BN;
-  // strided-batch element: shift every pointer of this problem
-  const int64_t offA = (int64_t)batch * G.bs_a, offB = (int64_t)batch * G.bs_b;
-  float* const Cb = (G.epi & EPI_PARTIAL) ? G.C + (int64_t)batch * nsplit * G.M * G.N
-                                          : G.C + (int64_t)batch * G.bs_c;
-  float* const part_db = G.part_db ? G.part_db + (int64_t)batch * nsplit * G.M : nullptr;
-  const float* const biasb = G.bias ? G.bias + (int64_t)batch * G.bs_bias : nullptr;
-  const int brs_off = G.bias_rs_off + batch * G.bs_brs;
+  TileCtx T;
+  if (!tile_ctx(G, T)) return;
+  const int64_t offA = (int64_t)T.batch * G.bs_a, offB = (int64_t)T.batch * G.bs_b;
 
-  __shared__ __attribute__((aligned(16))) float As[BK * LDS_STRIDE];
-  __shared__ __attribute__((aligned(16))) float Bs[BK * LDS_STRIDE];
+  // one LDS object: A and B tiles, reused as the [64][CS] epilogue image
+  __shared__ __attribute__((aligned(16))) float sm[2 * BK * LDS_STRIDE];
+  static_assert(2 * BK * LDS_STRIDE >= 64 * CS, "epilogue image does not fit");
+  float* const As = sm;
+  float* const Bs = sm + BK * LDS_STRIDE;
   constexpr int SA = AMODE == MODE_RK ? LDS_STRIDE_T : LDS_STRIDE;
   constexpr int SB = BMODE == MODE_RK ? LDS_STRIDE_T : LDS_STRIDE;
 
@@ -152,21 +440,21 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const GemmArgs args) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
-  const bool want_db = (G.epi & EPI_PARTIAL) && part_db != nullptr && tn == 0;
+  const bool want_db = (G.epi & EPI_PARTIAL) && T.part_db != nullptr && T.j0 == 0;
   float dbsum = 0.f;
 
   for (int si = 0; si < G.src_count; ++si) {
     const GemmSrc& S = args.s[G.src_begin + si];
     int kbeg = 0, kend = S.K;
     if (G.epi & EPI_PARTIAL) {
-      kbeg = split * G.kchunk;
+      kbeg = T.split * G.kchunk;
       kend = min(S.K, kbeg + G.kchunk);
     }
     if (kbeg >= kend) continue;
     const int ntk = (kend - kbeg + BK - 1) / BK;
     TileRegs ra, rb;
-    load_tile<AMODE>(ra, S.a, offA, args.xf, i0, G.M, kbeg, kend, rs, p, inv_keep);
-    load_tile<BMODE>(rb, S.b, offB, args.xf, j0, G.N, kbeg, kend, rs, p, inv_keep);
+    load_tile<AMODE>(ra, S.a, offA, T.i0, G.M, kbeg, kend);
+    load_tile<BMODE>(rb, S.b, offB, T.j0, G.N, kbeg, kend);
     for (int kt = 0; kt < ntk; ++kt) {
       __syncthreads();
       store_tile<AMODE>(ra, As);
@@ -174,8 +462,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const GemmArgs args) {
       __syncthreads();
       if (kt + 1 < ntk) {
         const int kn = kbeg + (kt + 1) * BK;
-        load_tile<AMODE>(ra, S.a, offA, args.xf, i0, G.M, kn, kend, rs, p, inv_keep);
-        load_tile<BMODE>(rb, S.b, offB, args.xf, j0, G.N, kn, kend, rs, p, inv_keep);
+        load_tile<AMODE>(ra, S.a, offA, T.i0, G.M, kn, kend);
+        load_tile<BMODE>(rb, S.b, offB, T.j0, G.N, kn, kend);
       }
       if (want_db && t < BM) {
 #pragma unroll 8
@@ -194,58 +482,19 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const GemmArgs args) {
       }
     }
   }
-
-  // ------------------------------------------------------------- epilogue
-  if (G.epi & EPI_PARTIAL) {
-    float* out = Cb + (int64_t)split * G.M * G.N;
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const int j = j0 + wn * 64 + b * 32 + c;
-        if (j >= G.N) continue;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int i = i0 + wm * 64 + a * 32 + acc_row(r, h);
-          if (i < G.M) out[(int64_t)i * G.N + j] = acc[a][b][r] * G.alpha;
-        }
-      }
-    if (want_db && t < BM && i0 + t < G.M) part_db[(int64_t)split * G.M + i0 + t] = dbsum * G.alpha;
-    return;
-  }
-  const int epi = G.epi;
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int j = j0 + wn * 64 + b * 32 + c;
-      if (j >= G.N) continue;
-      const float bj = (epi & EPI_BIAS) ? biasb[j] : 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int i = i0 + wm * 64 + a * 32 + acc_row(r, h);
-        if (i >= G.M) continue;
-        float v = acc[a][b][r] * G.alpha;
-        if (epi & EPI_BIAS_RS) v += bj * G.bias_rs[(int64_t)i * G.bias_rs_ld + brs_off];
-        else v += bj;
-        if (epi & EPI_ROWADD)
-          v += G.rowadd_scale * G.rowadd[(int64_t)(i / G.rowadd_div) * G.ld_rowadd + j];
-        if (epi & EPI_ADDMAT) v += G.addm[(int64_t)i * G.ld_addm + j];
-        if (epi & EPI_RELU) v = fmaxf(v, 0.f);
-        if (epi & EPI_GATE) v = G.gate[(int64_t)i * G.ld_gate + j] > 0.f ? v * G.gate_scale : 0.f;
-        if (epi & EPI_ROWSCALE) v *= G.rowscale[(int64_t)(i / G.rs_div) * G.rs_stride + G.rs_off];
-        if ((epi & EPI_DROP) && p > 0.f)
-          v = keep1(rs, G.drop_site, (uint64_t)i * (uint64_t)G.N + (uint64_t)j, p) ? v * inv_keep : 0.f;
-        Cb[(int64_t)i * G.ldc + j] = v;
-      }
-    }
+  if (want_db && t < BM && T.i0 + t < G.M) T.part_db[(int64_t)T.split * G.M + T.i0 + t] = dbsum * G.alpha;
+  epilogue(G, T, acc, sm, rs, p, inv_keep, wm, wn, h, c);
 }
 
+// ------------------------------------------------------------------ split-K reduce
 struct ReduceArgs {
   ReduceJob j[16];
   int32_t njobs;
 };
 
+// Block: 64 float4 columns (256 outputs) x 4 split-groups; a thread sums the
+// splits sg, sg+4, ... with 4 loads in flight, then the 4 group sums are
+// combined in a fixed order (deterministic).
 __global__ __launch_bounds__(256) void partial_reduce_kernel(const ReduceArgs a) {
   ReduceJob J = a.j[blockIdx.y];
   const int64_t MN = (int64_t)J.M * J.N;
@@ -255,26 +504,42 @@ __global__ __launch_bounds__(256) void partial_reduce_kernel(const ReduceArgs a)
   if (J.part_db) J.part_db += (int64_t)batch * J.nsplit * J.M;
   J.out += (int64_t)batch * J.bs_out;
   if (J.db) J.db += (int64_t)batch * J.bs_db;
-  // 64 outputs x 4 split-groups per block; the 4 partial sums are combined in a
-  // fixed order, so the result is deterministic.
-  __shared__ float red[4][64];
+  __shared__ f32x4 red[4][64];
   const int el = threadIdx.x & 63, sg = threadIdx.x >> 6;
-  const int64_t gstride = (int64_t)gridDim.x * 64;
-  for (int64_t e0 = (int64_t)blockIdx.x * 64; e0 < MN; e0 += gstride) {
-    const int64_t e = e0 + el;
-    float s0 = 0.f, s1 = 0.f;
-    if (e < MN) {
-      int k = sg;
-      for (; k + 4 < J.nsplit; k += 8) {
-        s0 += J.part[(int64_t)k * MN + e];
-        s1 += J.part[(int64_t)(k + 4) * MN + e];
+  const bool v4 = (MN % 4) == 0 && ((uintptr_t)J.part & 15) == 0;
+  const int64_t n4 = v4 ? MN / 4 : MN;        // vector (or scalar) columns
+  const bool out_al = ((uintptr_t)J.out & 15) == 0;
+  for (int64_t c0 = (int64_t)blockIdx.x * 64; c0 < n4; c0 += (int64_t)gridDim.x * 64) {
+    const int64_t col = c0 + el;
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, s2 = s0, s3 = s0;
+    if (col < n4) {
+      if (v4) {
+        const f32x4* base = reinterpret_cast<const f32x4*>(J.part) + col;
+        const int64_t st = MN / 4;
+        int k = sg;
+        for (; k + 12 < J.nsplit; k += 16) {
+          s0 += base[(int64_t)k * st];
+          s1 += base[(int64_t)(k + 4) * st];
+          s2 += base[(int64_t)(k + 8) * st];
+          s3 += base[(int64_t)(k + 12) * st];
+        }
+        for (; k < J.nsplit; k += 4) s0 += base[(int64_t)k * st];
+      } else {
+        for (int k = sg; k < J.nsplit; k += 4) s0[0] += J.part[(int64_t)k * MN + col];
       }
-      for (; k < J.nsplit; k += 4) s0 += J.part[(int64_t)k * MN + e];
     }
     __syncthreads();
-    red[sg][el] = s0 + s1;
+    red[sg][el] = (s0 + s1) + (s2 + s3);
     __syncthreads();
-    if (sg == 0 && e < MN) J.out[e] = (red[0][el] + red[1][el]) + (red[2][el] + red[3][el]);
+    if (sg == 0 && col < n4) {
+      const f32x4 r = (red[0][el] + red[1][el]) + (red[2][el] + red[3][el]);
+      if (!v4) J.out[col] = r[0];
+      else if (out_al) reinterpret_cast<f32x4*>(J.out)[col] = r;
+      else {
+        float* o = J.out + col * 4;
+        o[0] = r[0]; o[1] = r[1]; o[2] = r[2]; o[3] = r[3];
+      }
+    }
   }
   if (J.db && J.part_db && blockIdx.x == 0) {
     for (int i = threadIdx.x; i < J.M; i += blockDim.x) {
@@ -283,6 +548,68 @@ __global__ __launch_bounds__(256) void partial_reduce_kernel(const ReduceArgs a)
       J.db[i] = s;
     }
   }
+}
+
+// ------------------------------------------------------------------ input mask + dropout
+__global__ __launch_bounds__(256) void mask_dropout_rows_kernel(int64_t n, int D, const float* __restrict__ x,
+                                                                float* __restrict__ out,
+                                                                const float* __restrict__ mask, int L, int M,
+                                                                int m, uint32_t site, float p,
+                                                                const RngSnap* rng, int vec) {
+  const bool drop = p > 0.f && rng != nullptr;
+  RngSnap rs{0, 0};
+  if (drop) rs = *rng;
+  const uint32_t thr = p16(p);
+  const float inv_keep = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  // thread handles the 8 elements of one Philox block
+  for (int64_t blk = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; blk * 8 < n;
+       blk += (int64_t)gridDim.x * blockDim.x) {
+    uint4 r = make_uint4(0, 0, 0, 0);
+    if (drop) r = philox_block(rs, site, (uint64_t)blk);
+    const int64_t base = blk * 8;
+    if (vec && base + 8 <= n) {
+      const float s = mask[(base / D / L) * M + m];
+      float4 v0 = *reinterpret_cast<const float4*>(x + base);
+      float4 v1 = *reinterpret_cast<const float4*>(x + base + 4);
+      float o[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float v = o[e] * s;
+        if (drop) v = keep_from(r, e, thr) ? v * inv_keep : 0.f;
+        o[e] = v;
+      }
+      *reinterpret_cast<float4*>(out + base) = make_float4(o[0], o[1], o[2], o[3]);
+      *reinterpret_cast<float4*>(out + base + 4) = make_float4(o[4], o[5], o[6], o[7]);
+    } else {
+      for (int e = 0; e < 8 && base + e < n; ++e) {
+        const int64_t idx = base + e;
+        float v = x[idx] * mask[(idx / D / L) * M + m];
+        if (drop) v = keep_from(r, e, thr) ? v * inv_keep : 0.f;
+        out[idx] = v;
+      }
+    }
+  }
+}
+
+// LDS-DMA eligibility of one operand: 16-B aligned rows (and batch strides),
+// plus an extent % 4 == 0 along the contiguous axis for KR operands.
+bool dma_ok(const Operand& op, int mode, int eext, int bstride, int nbatch) {
+  if (!op.vec || op.row_div < 1) return false;
+  if (nbatch > 1 && (bstride % 4) != 0) return false;
+  if (mode == MODE_KR && (eext % 4) != 0) return false;
+  return true;
+}
+
+bool job_fast(const GemmJob& J, int amode, int bmode) {
+  const GemmGroup& g = J.g;
+  const int nb = g.nbatch < 1 ? 1 : g.nbatch;
+  if ((g.epi & EPI_PARTIAL) && (g.kchunk % DK) != 0) return false;
+  for (int s = 0; s < J.nsrc; ++s) {
+    const GemmSrc& src = J.src[s];
+    if ((src.K % 4) != 0 || !dma_ok(src.a, amode, g.M, g.bs_a, nb) || !dma_ok(src.b, bmode, g.N, g.bs_b, nb))
+      return false;
+  }
+  return true;
 }
 
 }  // namespace
@@ -297,28 +624,22 @@ hipError_t launch_gemm(const GemmJob* jobs, int njobs, int amode, int bmode, flo
     args.bmode = bmode;
     args.drop_p = drop_p;
     args.rng = rng;
-    int ng = 0, ns = 0, nx = 0, max_blocks = 0;
+    int ng = 0, ns = 0, max_blocks = 0;
+    // one launch = consecutive jobs of the same kernel flavour
+    const bool fast = job_fast(jobs[done], amode, bmode);
     while (done < njobs && ng < GEMM_MAX_GROUPS) {
       const GemmJob& J = jobs[done];
-      int need_x = 0;
-      for (int s = 0; s < J.nsrc; ++s) need_x += J.has_xf_a[s] + J.has_xf_b[s];
       if (J.nsrc > GEMM_MAX_SRCS) return hipErrorInvalidValue;
-      if (ns + J.nsrc > GEMM_MAX_SRCS || nx + need_x > GEMM_MAX_XF) break;
+      if (ns + J.nsrc > GEMM_MAX_SRCS) break;
+      if (job_fast(J, amode, bmode) != fast) break;
       GemmGroup g = J.g;
       if (g.nbatch < 1) g.nbatch = 1;
       g.src_begin = ns;
       g.src_count = J.nsrc;
-      for (int s = 0; s < J.nsrc; ++s) {
-        GemmSrc src = J.src[s];
-        src.a.xf = J.has_xf_a[s] ? nx : -1;
-        if (J.has_xf_a[s]) args.xf[nx++] = J.xf_a[s];
-        src.b.xf = J.has_xf_b[s] ? nx : -1;
-        if (J.has_xf_b[s]) args.xf[nx++] = J.xf_b[s];
-        args.s[ns++] = src;
-      }
+      const bool partial = (g.epi & EPI_PARTIAL) != 0;
+      for (int s = 0; s < J.nsrc; ++s) args.s[ns++] = J.src[s];
       args.g[ng++] = g;
-      const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN) *
-                        ((g.epi & EPI_PARTIAL) ? g.nsplit : 1) * g.nbatch;
+      const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN) * (partial ? g.nsplit : 1) * g.nbatch;
       if (tiles > max_blocks) max_blocks = tiles;
       ++done;
     }
@@ -326,14 +647,21 @@ hipError_t launch_gemm(const GemmJob* jobs, int njobs, int amode, int bmode, flo
     args.ngroups = ng;
     if (max_blocks > 0) {
       dim3 grid(max_blocks, ng);
-      if (amode == MODE_RK && bmode == MODE_RK)
-        hipLaunchKernelGGL((gemm_kernel<MODE_RK, MODE_RK>), grid, dim3(NT), 0, st, args);
-      else if (amode == MODE_RK && bmode == MODE_KR)
-        hipLaunchKernelGGL((gemm_kernel<MODE_RK, MODE_KR>), grid, dim3(NT), 0, st, args);
-      else if (amode == MODE_KR && bmode == MODE_KR)
-        hipLaunchKernelGGL((gemm_kernel<MODE_KR, MODE_KR>), grid, dim3(NT), 0, st, args);
-      else
-        hipLaunchKernelGGL((gemm_kernel<MODE_KR, MODE_RK>), grid, dim3(NT), 0, st, args);
+#define MMF_LAUNCH(KERNEL)                                                                 \
+      if (amode == MODE_RK && bmode == MODE_RK)                                            \
+        hipLaunchKernelGGL((KERNEL<MODE_RK, MODE_RK>), grid, dim3(NT), 0, st, args);       \
+      else if (amode == MODE_RK && bmode == MODE_KR)                                       \
+        hipLaunchKernelGGL((KERNEL<MODE_RK, MODE_KR>), grid, dim3(NT), 0, st, args);       \
+      else if (amode == MODE_KR && bmode == MODE_KR)                                       \
+        hipLaunchKernelGGL((KERNEL<MODE_KR, MODE_KR>), grid, dim3(NT), 0, st, args);       \
+      else                                                                                 \
+        hipLaunchKernelGGL((KERNEL<MODE_KR, MODE_RK>), grid, dim3(NT), 0, st, args);
+      if (fast) {
+        MMF_LAUNCH(gemm_lds_kernel)
+      } else {
+        MMF_LAUNCH(gemm_generic_kernel)
+      }
+#undef MMF_LAUNCH
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
@@ -358,7 +686,7 @@ hipError_t launch_reduce(const ReduceJob* jobs, int njobs, hipStream_t st) {
       ++n;
     }
     a.njobs = n;
-    int blocks = (int)((maxmn + 63) / 64);
+    int blocks = (int)((maxmn / 4 + 63) / 64);
     if (blocks < 1) blocks = 1;
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(partial_reduce_kernel, dim3(blocks, n, maxbatch), dim3(256), 0, st, a);
@@ -366,6 +694,18 @@ hipError_t launch_reduce(const ReduceJob* jobs, int njobs, hipStream_t st) {
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+
+hipError_t launch_mask_dropout_rows(int64_t rows, int D, const float* x, float* out, const float* mask, int L,
+                                    int M, int m, uint32_t site, float p, const RngSnap* rng, hipStream_t st) {
+  const int64_t n = rows * D;
+  if (n == 0) return hipSuccess;
+  const int64_t blks = (n + 7) / 8;
+  int grid = (int)std::min<int64_t>((blks + 255) / 256, 4096);
+  const int vec = (D % 8) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)out & 15) == 0;
+  hipLaunchKernelGGL(mask_dropout_rows_kernel, dim3(grid), dim3(256), 0, st, n, D, x, out, mask, L, M, m, site,
+                     p, rng, vec);
+  return hipGetLastError();
 }
 
 }  // namespace mmf

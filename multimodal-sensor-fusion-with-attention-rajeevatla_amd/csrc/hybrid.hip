@@ -32,6 +32,7 @@ bool use_pool(const mmf_hybrid_desc* d) {
 
 struct Saved {
   RngSnap* rng;
+  float* Xd[MMF_MAX_MODALITIES];   // X_m * mask_m with input dropout (fusion.py:364-373)
   float* P[MMF_MAX_MODALITIES];
   float *Q[MMF_MAX_PAIRS], *K[MMF_MAX_PAIRS], *lse[MMF_MAX_PAIRS];
   // general plan
@@ -47,6 +48,7 @@ void layout_saved(const mmf_hybrid_desc* d, Bump& bp, Saved& s) {
   const size_t B = d->batch, H = d->hidden, M = d->num_modalities, nh = d->num_heads;
   const bool pool = use_pool(d);
   s.rng = bp.take<RngSnap>(1);
+  for (int m = 0; m < d->num_modalities; ++m) s.Xd[m] = bp.take<float>(B * Lm(d, m) * d->in_dim[m]);
   for (int m = 0; m < d->num_modalities; ++m) s.P[m] = bp.take<float>(B * Lm(d, m) * H);
   for (int g = 0; g < d->num_pairs; ++g) {
     const size_t lq = Lm(d, d->pair_q[g]), lk = Lm(d, d->pair_k[g]);
@@ -180,13 +182,7 @@ void plan_wgrads(const mmf_hybrid_desc* d, const float* const* x, const float* m
   }
   for (int m = 0; m < M; ++m) {
     const int L = Lm(d, m), D = d->in_dim[m];
-    Xform xf;
-    memset(&xf, 0, sizeof(xf));
-    xf.rowscale = mask; xf.rs_div = L; xf.rs_stride = M; xf.rs_off = m;
-    xf.drop_site = dropping(d) ? SITE_IN + m : 0;
-    xf.ncols = D;
-    plan_wgrad(wp, bw, H, D, B * L, opnd(w.dZ[m], H), opnd(x ? x[m] : nullptr, D), g->proj[m].w,
-               g->proj[m].b, 1.f, &xf);
+    plan_wgrad(wp, bw, H, D, B * L, opnd(w.dZ[m], H), opnd(s.Xd[m], D), g->proj[m].w, g->proj[m].b);
   }
 }
 
@@ -285,20 +281,18 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
   if (rng_state) STAGE_TRY("fwd.rng", launch_rng_snapshot(rng_state, s.rng, st));
   const RngSnap* rng = rng_state ? s.rng : nullptr;
 
-  // (1) per-modality projection: P_m = Drop(ReLU(Drop(X_m * mask_m) W_m^T + b_m))  (fusion.py:364-374)
+  // (1) per-modality projection: P_m = Drop(ReLU(X'_m W_m^T + b_m)), X'_m = Drop(X_m * mask_m)
+  //     (fusion.py:364-374); X' is kept for the weight gradient
   {
     std::vector<GemmJob> jobs;
     for (int m = 0; m < M; ++m) {
       const int L = Lm(d, m), D = d->in_dim[m];
+      STAGE_TRY("fwd.input_mask", launch_mask_dropout_rows((int64_t)B * L, D, x[m], s.Xd[m], mask, L, M, m,
+                                                           SITE_IN + m, p, rng, st));
       GemmJob j = make_job(B * L, H, s.P[m], H, EPI_BIAS | EPI_RELU | (drop ? EPI_DROP : 0));
       j.g.bias = W->proj[m].b;
       j.g.drop_site = SITE_PROJ + m;
-      add_src(j, opnd(x[m], D), opnd(W->proj[m].w, D), D);
-      j.has_xf_a[0] = 1;
-      Xform& xf = j.xf_a[0];
-      xf.rowscale = mask; xf.rs_div = L; xf.rs_stride = M; xf.rs_off = m;
-      xf.drop_site = drop ? SITE_IN + m : 0;
-      xf.ncols = D;
+      add_src(j, opnd(s.Xd[m], D), opnd(W->proj[m].w, D), D);
       jobs.push_back(j);
     }
     STAGE_TRY("fwd.proj_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, p, rng, st));

@@ -9,8 +9,8 @@ namespace mmf {
 
 // ---------------------------------------------------------------------------
 // Dropout RNG: Philox4x32-10 keyed by the per-call snapshot {seed, offset};
-// counter = (idx>>2 lo, idx>>2 hi, site, offset).  One call yields the keep
-// decisions of 4 consecutive elements of one tensor ("site").
+// counter = (idx>>3 lo, idx>>3 hi, site, offset).  One call yields the keep
+// decisions of 8 consecutive elements of one tensor ("site"), 16 bits each.
 // ---------------------------------------------------------------------------
 struct RngSnap { uint64_t seed; uint64_t offset; };
 
@@ -30,20 +30,12 @@ enum : uint32_t {
 // ---------------------------------------------------------------------------
 enum { MODE_RK = 0, MODE_KR = 1 };  // for B: RK == NK (stored [j][kk]), KR == KN
 
-struct Xform {               // optional prologue on a stored element (row r, col c)
-  const float* rowscale;     // v *= rowscale[(r / rs_div) * rs_stride + rs_off]
-  int32_t rs_div, rs_stride, rs_off;
-  uint32_t drop_site;        // 0 = none; keep(site, r * ncols + c) ? v/(1-p) : 0
-  int32_t ncols;
-  int32_t pad_;
-};
-
 struct Operand {
   const float* ptr;
   int32_t ld;                // stored row stride (elements)
   int32_t row_div;           // >= 1
   int32_t vec;               // 1 => 16-byte aligned rows, float4 loads allowed
-  int32_t xf;                // -1 none, else index into GemmArgs::xf
+  int32_t pad_;
 };
 
 struct GemmSrc {
@@ -87,12 +79,10 @@ struct GemmGroup {
 
 constexpr int GEMM_MAX_GROUPS = 8;
 constexpr int GEMM_MAX_SRCS = 24;
-constexpr int GEMM_MAX_XF = 8;
 
 struct GemmArgs {
   GemmGroup g[GEMM_MAX_GROUPS];
   GemmSrc s[GEMM_MAX_SRCS];
-  Xform xf[GEMM_MAX_XF];
   int32_t ngroups;
   int32_t amode, bmode;
   float drop_p;              // p of every dropout site in this launch
@@ -104,15 +94,22 @@ struct GemmArgs {
 struct GemmJob {
   GemmGroup g;
   GemmSrc src[GEMM_MAX_SRCS];
-  int has_xf_a[GEMM_MAX_SRCS];
-  int has_xf_b[GEMM_MAX_SRCS];
-  Xform xf_a[GEMM_MAX_SRCS];
-  Xform xf_b[GEMM_MAX_SRCS];
   int nsrc;
 };
 
+// Launches every job (grouped <= GEMM_MAX_GROUPS per launch).  A launch whose
+// operands are all float4-able (16-B aligned, ld % 4 == 0, K % 4 == 0, KR
+// extents % 4 == 0) runs the LDS-DMA pipelined kernel; anything else runs the
+// register-staged generic kernel.
 hipError_t launch_gemm(const GemmJob* jobs, int njobs, int amode, int bmode, float drop_p,
                        const RngSnap* rng, hipStream_t st);
+
+// X'[r][c] = X[r][c] * mask[(r / L) * M + m] * (keep(site, r*D + c) ? 1/(1-p) : 0)
+// (the masked, input-dropped modality features of src/fusion.py:364-373,
+// materialised once for the projection GEMM and its weight gradient).
+hipError_t launch_mask_dropout_rows(int64_t rows, int D, const float* x, float* out, const float* mask,
+                                    int L, int M, int m, uint32_t site, float p, const RngSnap* rng,
+                                    hipStream_t st);
 
 // Split-K partial-slab reduction: out[e] = sum_s part[s][e]; db[i] = sum_s part_db[s][i].
 struct ReduceJob {

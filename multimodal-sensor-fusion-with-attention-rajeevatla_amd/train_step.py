@@ -33,6 +33,35 @@ import mmf_native as _nat  # noqa: E402
 from fusion import HybridFusion  # noqa: E402
 
 
+def shard_batch(feats: List[torch.Tensor], mask: torch.Tensor, labels: torch.Tensor, rank: int,
+                world: int):
+    """Rank `rank`'s contiguous slice of a global batch (equal shards: B % world == 0).
+
+    Equal shards keep the DP gradient exact: each rank's CE is a mean over its
+    B/world samples, so the sum of the ranks' gradients divided by world is the
+    mean-CE gradient of the whole batch.
+    """
+    B = mask.size(0)
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} for world size {world}")
+    if B % world:
+        raise ValueError(f"global batch {B} is not divisible by world size {world}")
+    n = B // world
+    sl = slice(rank * n, (rank + 1) * n)
+    return [f[sl] for f in feats], mask[sl], labels[sl]
+
+
+def allreduce_flat(grad: torch.Tensor, process_group=None, world: int = 1) -> None:
+    """The one data-path exchange of DP training: sum the flat gradient over ranks.
+
+    A single collective over one contiguous buffer (1.77 MiB at C2): RCCL
+    (backend "nccl") on MI355X, gloo in the CPU tests.  The 1/world average is
+    folded into AdamW's gradient scale (mmf_adamw_step gscale), so no extra pass.
+    """
+    if world > 1:
+        torch.distributed.all_reduce(grad, group=process_group)
+
+
 class HybridTrainStep:
     def __init__(self, model: HybridFusion, feats: List[torch.Tensor], mask: torch.Tensor,
                  labels: torch.Tensor, lr: float = 1e-3, weight_decay: float = 0.01,
@@ -102,8 +131,7 @@ class HybridTrainStep:
         _nat.check(rc, "train backward")
 
     def allreduce(self) -> None:
-        if self.world > 1:
-            torch.distributed.all_reduce(self.grad, group=self.pg)
+        allreduce_flat(self.grad, self.pg, self.world)
 
     def optimizer_step(self) -> None:
         rc = _nat.lib().mmf_adamw_step(self.flat.numel(), self.flat.data_ptr(), self.grad.data_ptr(),
