@@ -856,6 +856,342 @@ __global__ __launch_bounds__(NT) void attn_pool_bwd_dk_kernel(const AttnArgs A) 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Lean pooled kernels: the same three passes for the common HybridFusion case
+// (every key valid: Lk % 32 == 0, Lk <= 128, no per-key mask; float4-able
+// rows), with the per-score work cut to a handful of VALU ops: scores stay in
+// the exp2 domain (one FMA + v_exp per score), no per-element validity
+// tests (invalid query lanes get a zero weight / +inf LSE), and per-key /
+// per-query side data are read from LDS as broadcast float4s.
+// ---------------------------------------------------------------------------
+constexpr float LOG2E = 1.4426950408889634f;
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+template <int HALF>
+__device__ __forceinline__ void load_frag_vec(float* f, const float* row) {
+#pragma unroll
+  for (int s = 0; s < HALF; s += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(row + s);
+    f[s] = v.x; f[s + 1] = v.y; f[s + 2] = v.z; f[s + 3] = v.w;
+  }
+}
+
+template <int HDP>
+__global__ __launch_bounds__(NT) void attn_pool_fwd_lean(const AttnArgs A) {
+  constexpr int LS = HDP + 4;
+  constexpr int HALF = HDP / 2;
+  constexpr int NKT = PKC / 32;
+  __shared__ __attribute__((aligned(16))) float Ks[PKC * LS];
+  __shared__ float cs[4][PKC];
+
+  const AttnPair& P = A.p[blockIdx.y];
+  const int bid = blockIdx.x;
+  if (bid >= A.B * A.heads) return;
+  const int head = bid % A.heads, b = bid / A.heads;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, c = lane & 31;
+  const int hd = A.hd, col0 = head * hd;
+  const int Lq = P.Lq, Lk = P.Lk, nkt = Lk >> 5;
+  const float pdrop = A.drop_p;
+  const float inv_keep = pdrop < 1.f ? 1.f / (1.f - pdrop) : 0.f;
+  RngSnap rs{0, 0};
+  if (pdrop > 0.f && A.rng) rs = *A.rng;
+  const int64_t bh = (int64_t)b * A.heads + head;
+  float* pbar = P.pbar + bh * Lk;
+
+  if (P.kmask_mode == 1 && P.kmask[(int64_t)b * P.kmask_ld] == 0.f) {
+    for (int k = t; k < Lk; k += NT) pbar[k] = 0.f;
+    for (int q = t; q < Lq; q += NT) P.lse[bh * Lq + q] = -INFINITY;
+    if (P.keep_bits)
+      for (int q = t; q < Lq; q += NT)
+        *reinterpret_cast<uint4*>(P.keep_bits + (bh * Lq + q) * 4) = make_uint4(0, 0, 0, 0);
+    return;
+  }
+  load_rows<PKC, HDP, LS>(Ks, P.k + (int64_t)b * Lk * P.ldk + col0, Lk, P.ldk, 0, hd, true);
+  __syncthreads();
+
+  const float c2 = A.scale * LOG2E;
+  float colacc[NKT];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) colacc[kt] = 0.f;
+
+  for (int qt = w; qt * 32 < Lq; qt += 4) {
+    const int q = qt * 32 + c;
+    const bool qvalid = q < Lq;
+    const int qq = qvalid ? q : Lq - 1;
+    float qf[HALF];
+    load_frag_vec<HALF>(qf, P.q + ((int64_t)b * Lq + qq) * P.ldq + col0 + h * HALF);
+    float sv[NKT][16];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      if (kt < nkt) {
+        const f32x16 s = dot_rows<HALF>(Ks + (kt * 32 + c) * LS + h * HALF, qf, zero16());
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          sv[kt][r] = s[r];
+          mx = fmaxf(mx, s[r]);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sv[kt][r] = 0.f;
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float mc = mx * c2;
+    float l = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      if (kt < nkt) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float e = fast_exp2(fmaf(sv[kt][r], c2, -mc));
+          sv[kt][r] = e;
+          l += e;
+        }
+      }
+    }
+    l += __shfl_xor(l, 32);
+    const float f = qvalid ? (pdrop > 0.f ? inv_keep : 1.f) / l : 0.f;
+    const int64_t rowidx = bh * Lq + qq;
+    uint32_t words[NKT];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      words[kt] = 0u;
+      if (kt < nkt) {
+        uint32_t kb16 = 0xFFFFu;
+        if (pdrop > 0.f) kb16 = keep_tile16(rs, P.drop_site, (uint64_t)rowidx * Lk + kt * 32, pdrop, h, qvalid, true);
+        uint32_t bits = 0;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) bits |= ((kb16 >> (4 * g)) & 0xFu) << (8 * g + 4 * h);
+        words[kt] = bits | __shfl_xor(bits, 32);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sv[kt][r] = ((kb16 >> r) & 1u) ? sv[kt][r] * f : 0.f;
+        colacc[kt] += colsum_tile(sv[kt], c);
+      }
+    }
+    if (qvalid && h == 0) {
+      P.lse[rowidx] = mx * A.scale + __logf(l);
+      if (P.keep_bits && pdrop > 0.f)
+        *reinterpret_cast<uint4*>(P.keep_bits + rowidx * 4) =
+            make_uint4(words[0], NKT > 1 ? words[1] : 0u, NKT > 2 ? words[2] : 0u, NKT > 3 ? words[3] : 0u);
+    }
+  }
+  if ((c & 1) == 0) {
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+      if (kt < nkt) cs[w][kt * 32 + acc_row((c >> 1) & 15, h)] = colacc[kt];
+  }
+  __syncthreads();
+  const float inv_lq = 1.f / (float)Lq;
+  for (int k = t; k < Lk; k += NT) pbar[k] = ((cs[0][k] + cs[1][k]) + (cs[2][k] + cs[3][k])) * inv_lq;
+}
+
+// dq pass, query on the lane: G[k] = keep ? dpbar[k] / ((1-p) Lq) : 0;
+// D = rowsum(P . G) (saved for the dk pass); dS = P . (G - D); dQ = scale dS K.
+template <int HDP>
+__global__ __launch_bounds__(NT) void attn_pool_bwd_dq_lean(const AttnArgs A) {
+  constexpr int LS = HDP + 4;
+  constexpr int HALF = HDP / 2;
+  constexpr int NDT = HDP / 32;
+  constexpr int NKT = PKC / 32;
+  __shared__ __attribute__((aligned(16))) float Ks[PKC * LS];
+  __shared__ __attribute__((aligned(16))) float gk[PKC];
+
+  const AttnPair& P = A.p[blockIdx.y];
+  const int qblocks = (P.Lq + 127) / 128;
+  int bid = blockIdx.x;
+  if (bid >= A.B * A.heads * qblocks) return;
+  const int qb = bid % qblocks;
+  bid /= qblocks;
+  const int head = bid % A.heads, b = bid / A.heads;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, c = lane & 31;
+  const int hd = A.hd, col0 = head * hd;
+  const int Lq = P.Lq, Lk = P.Lk, nkt = Lk >> 5;
+  const int q = qb * 128 + w * 32 + c;
+  const bool qvalid = q < Lq;
+  const int qq = qvalid ? q : Lq - 1;
+  const int64_t bh = (int64_t)b * A.heads + head;
+  const int64_t rowidx = bh * Lq + qq;
+  const float pdrop = A.drop_p;
+  const float inv_keep = pdrop > 0.f && pdrop < 1.f ? 1.f / (1.f - pdrop) : 1.f;
+  const float inv_lq = 1.f / (float)Lq;
+  float* qrow = P.dq + ((int64_t)b * Lq + qq) * P.ldq + col0;
+
+  if (P.kmask_mode == 1 && P.kmask[(int64_t)b * P.kmask_ld] == 0.f) {
+    if (qvalid) {
+      for (int d = h; d < hd; d += 2) qrow[d] = 0.f;
+      if (h == 0) P.dsum[rowidx] = 0.f;
+    }
+    return;
+  }
+  load_rows<PKC, HDP, LS>(Ks, P.k + (int64_t)b * Lk * P.ldk + col0, Lk, P.ldk, 0, hd, true);
+  for (int k = t; k < PKC; k += NT) gk[k] = k < Lk ? P.dpbar[bh * Lk + k] * inv_keep * inv_lq : 0.f;
+  __syncthreads();
+  if (qb * 128 + w * 32 >= Lq) return;
+  float qf[HALF];
+  load_frag_vec<HALF>(qf, P.q + ((int64_t)b * Lq + qq) * P.ldq + col0 + h * HALF);
+  const float lse = P.lse[rowidx];
+  const float lse2 = (!qvalid || lse == -INFINITY) ? INFINITY : lse * LOG2E;
+  const float c2 = A.scale * LOG2E;
+  uint4 kw = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+  if (P.keep_bits && pdrop > 0.f) kw = *reinterpret_cast<const uint4*>(P.keep_bits + rowidx * 4);
+  const uint32_t kwa[4] = {kw.x, kw.y, kw.z, kw.w};
+  float pr[NKT][16];
+  float D = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    if (kt < nkt) {
+      const f32x16 s = dot_rows<HALF>(Ks + (kt * 32 + c) * LS + h * HALF, qf, zero16());
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 gv = *reinterpret_cast<const float4*>(gk + kt * 32 + 8 * g + 4 * h);
+        const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 4 * g + j;
+          const float p = fast_exp2(fmaf(s[r], c2, -lse2));
+          pr[kt][r] = p;
+          const bool keep = (kwa[kt] >> (8 * g + 4 * h + j)) & 1u;
+          D += keep ? p * gg[j] : 0.f;
+        }
+      }
+    }
+  }
+  D += __shfl_xor(D, 32);
+  if (qvalid && h == 0) P.dsum[rowidx] = D;
+  f32x16 dq[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) dq[dt] = zero16();
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    if (kt >= nkt) break;
+    float ds[16];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4 gv = *reinterpret_cast<const float4*>(gk + kt * 32 + 8 * g + 4 * h);
+      const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = 4 * g + j;
+        const bool keep = (kwa[kt] >> (8 * g + 4 * h + j)) & 1u;
+        ds[r] = pr[kt][r] * ((keep ? gg[j] : 0.f) - D);
+      }
+    }
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        dq[dt] = mfma32(Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], ds[r], dq[dt]);
+  }
+  if (!qvalid) return;
+  const float scale = A.scale;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d0 = dt * 32 + 8 * g + 4 * h;
+      if (d0 + 3 < hd)
+        *reinterpret_cast<float4*>(qrow + d0) = make_float4(dq[dt][4 * g] * scale, dq[dt][4 * g + 1] * scale,
+                                                            dq[dt][4 * g + 2] * scale, dq[dt][4 * g + 3] * scale);
+    }
+}
+
+// dk pass, key on the lane: dK = scale * dS^T Q, dS = P . (G - D).
+template <int HDP>
+__global__ __launch_bounds__(NT) void attn_pool_bwd_dk_lean(const AttnArgs A) {
+  constexpr int QC = 128;
+  constexpr int LS = HDP + 4;
+  constexpr int HALF = HDP / 2;
+  constexpr int NDT = HDP / 32;
+  __shared__ __attribute__((aligned(16))) float Qs[QC * LS];
+  __shared__ __attribute__((aligned(16))) float lse_s[QC];
+  __shared__ __attribute__((aligned(16))) float dsum_s[QC];
+  __shared__ __attribute__((aligned(16))) uint32_t kw_t[4 * QC];   // [key word][query]
+
+  const AttnPair& P = A.p[blockIdx.y];
+  const int bid = blockIdx.x;
+  if (bid >= A.B * A.heads) return;
+  const int head = bid % A.heads, b = bid / A.heads;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, c = lane & 31;
+  const int hd = A.hd, col0 = head * hd;
+  const int Lq = P.Lq, Lk = P.Lk;
+  const int key = w * 32 + c;
+  const bool wave_active = w * 32 < Lk;
+  const int kk = wave_active ? key : 0;
+  const int64_t bh = (int64_t)b * A.heads + head;
+  const float pdrop = A.drop_p;
+  const bool use_bits = P.keep_bits && pdrop > 0.f;
+  const float inv_keep = pdrop > 0.f && pdrop < 1.f ? 1.f / (1.f - pdrop) : 1.f;
+  const float inv_lq = 1.f / (float)Lq;
+  const float c2 = A.scale * LOG2E;
+
+  f32x16 dk[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) dk[dt] = zero16();
+  const bool sample_masked = (P.kmask_mode == 1 && P.kmask[(int64_t)b * P.kmask_ld] == 0.f);
+  if (!sample_masked) {
+    float kf[HALF];
+    load_frag_vec<HALF>(kf, P.k + ((int64_t)b * Lk + kk) * P.ldk + col0 + h * HALF);
+    const float gkey = P.dpbar[bh * Lk + kk] * inv_keep * inv_lq;
+    for (int qbase = 0; qbase < Lq; qbase += QC) {
+      __syncthreads();
+      load_rows<QC, HDP, LS>(Qs, P.q + (int64_t)b * Lq * P.ldq + col0, Lq, P.ldq, qbase, hd, true);
+      for (int i = t; i < QC; i += NT) {
+        const int qq = qbase + i;
+        const float lse = qq < Lq ? P.lse[bh * Lq + qq] : -INFINITY;
+        lse_s[i] = lse == -INFINITY ? INFINITY : lse * LOG2E;
+        dsum_s[i] = qq < Lq ? P.dsum[bh * Lq + qq] : 0.f;
+      }
+      for (int i = t; i < QC * 4; i += NT) {
+        const int qi = i >> 2, wd = i & 3;
+        kw_t[wd * QC + qi] = (use_bits && qbase + qi < Lq) ? P.keep_bits[(bh * Lq + qbase + qi) * 4 + wd] : 0xFFFFFFFFu;
+      }
+      __syncthreads();
+      if (!wave_active) continue;
+      const int nqt = (min(QC, Lq - qbase) + 31) / 32;
+      for (int qt = 0; qt < nqt; ++qt) {
+        const f32x16 s = dot_rows<HALF>(Qs + (qt * 32 + c) * LS + h * HALF, kf, zero16());
+        float ds[16];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int q0 = qt * 32 + 8 * g + 4 * h;
+          const float4 l4 = *reinterpret_cast<const float4*>(lse_s + q0);
+          const float4 d4 = *reinterpret_cast<const float4*>(dsum_s + q0);
+          const uint4 w4 = *reinterpret_cast<const uint4*>(kw_t + w * QC + q0);
+          const float ll[4] = {l4.x, l4.y, l4.z, l4.w};
+          const float dd[4] = {d4.x, d4.y, d4.z, d4.w};
+          const uint32_t ww[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int r = 4 * g + j;
+            const float p = fast_exp2(fmaf(s[r], c2, -ll[j]));
+            const bool keep = (ww[j] >> c) & 1u;
+            ds[r] = p * ((keep ? gkey : 0.f) - dd[j]);
+          }
+        }
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            dk[dt] = mfma32(ds[r], Qs[(qt * 32 + acc_row(r, h)) * LS + dt * 32 + c], dk[dt]);
+      }
+    }
+  }
+  if (!wave_active) return;
+  const float scale = A.scale;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) {
+    const int d = dt * 32 + c;
+    if (d >= hd) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int kr = w * 32 + acc_row(r, h);
+      if (kr < Lk) P.dk[((int64_t)b * Lk + kr) * P.ldk + col0 + d] = dk[dt][r] * scale;
+    }
+  }
+}
+
 enum class Kind { Fwd, Probs, Prep, Dkv, Dq, PoolFwd, PoolDq, PoolDk };
 
 hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, int heads, int hd,
@@ -866,6 +1202,14 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
   for (int i = 0; i < npairs && prep_vec; ++i)
     prep_vec = (pairs[i].ldo % 4 == 0) && (((uintptr_t)pairs[i].dout & 15) == 0) &&
                (((uintptr_t)pairs[i].o & 15) == 0) && pairs[i].ldo == heads * hd;
+  // lean pooled kernels: every pair has all keys valid and float4-able rows
+  bool lean = (kind == Kind::PoolFwd || kind == Kind::PoolDq || kind == Kind::PoolDk) && (hd % 4 == 0);
+  for (int i = 0; i < npairs && lean; ++i) {
+    const AttnPair& P = pairs[i];
+    lean = (P.Lk % 32 == 0) && P.Lk <= PKC && P.kmask_mode != 2 && (P.ldq % 4 == 0) && (P.ldk % 4 == 0) &&
+           (((uintptr_t)P.q & 15) == 0) && (((uintptr_t)P.k & 15) == 0) &&
+           (kind != Kind::PoolDq || (((uintptr_t)P.dq & 15) == 0));
+  }
   int done = 0;
   while (done < npairs) {
     AttnArgs a;
@@ -919,15 +1263,21 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
         else hipLaunchKernelGGL((attn_bwd_dq_kernel<64>), grid, dim3(NT), 0, st, a);
         break;
       case Kind::PoolFwd:
-        if (small) hipLaunchKernelGGL((attn_pool_fwd_kernel<32>), grid, dim3(NT), 0, st, a);
+        if (lean && small) hipLaunchKernelGGL((attn_pool_fwd_lean<32>), grid, dim3(NT), 0, st, a);
+        else if (lean) hipLaunchKernelGGL((attn_pool_fwd_lean<64>), grid, dim3(NT), 0, st, a);
+        else if (small) hipLaunchKernelGGL((attn_pool_fwd_kernel<32>), grid, dim3(NT), 0, st, a);
         else hipLaunchKernelGGL((attn_pool_fwd_kernel<64>), grid, dim3(NT), 0, st, a);
         break;
       case Kind::PoolDq:
-        if (small) hipLaunchKernelGGL((attn_pool_bwd_dq_kernel<32>), grid, dim3(NT), 0, st, a);
+        if (lean && small) hipLaunchKernelGGL((attn_pool_bwd_dq_lean<32>), grid, dim3(NT), 0, st, a);
+        else if (lean) hipLaunchKernelGGL((attn_pool_bwd_dq_lean<64>), grid, dim3(NT), 0, st, a);
+        else if (small) hipLaunchKernelGGL((attn_pool_bwd_dq_kernel<32>), grid, dim3(NT), 0, st, a);
         else hipLaunchKernelGGL((attn_pool_bwd_dq_kernel<64>), grid, dim3(NT), 0, st, a);
         break;
       case Kind::PoolDk:
-        if (small) hipLaunchKernelGGL((attn_pool_bwd_dk_kernel<32>), grid, dim3(NT), 0, st, a);
+        if (lean && small) hipLaunchKernelGGL((attn_pool_bwd_dk_lean<32>), grid, dim3(NT), 0, st, a);
+        else if (lean) hipLaunchKernelGGL((attn_pool_bwd_dk_lean<64>), grid, dim3(NT), 0, st, a);
+        else if (small) hipLaunchKernelGGL((attn_pool_bwd_dk_kernel<32>), grid, dim3(NT), 0, st, a);
         else hipLaunchKernelGGL((attn_pool_bwd_dk_kernel<64>), grid, dim3(NT), 0, st, a);
         break;
     }

@@ -119,11 +119,15 @@ inline void add_src(GemmJob& j, Operand a, Operand b, int K) {
   s.K = K;
 }
 
-// Split of a weight-gradient contraction over `rows`: ~512 rows per slab, so a
-// launch of 8 (128x128-output) jobs at B*L = 32768 rows is 512 workgroups
-// (2 per CU) and the slabs of all 15 such jobs are 63 MB.
+// Split of a weight-gradient contraction over `rows`: slabs of 512 rows for
+// long contractions (a launch of 8 128x128-output jobs at B*L = 32768 rows is
+// 512 workgroups, 2 per CU; the slabs of all 15 such jobs are 63 MB) and of
+// >= 64 rows for short ones (B = 256 rows -> 4 slabs: a short serial chain).
 inline void split_rows(int rows, int& nsplit, int& kchunk) {
-  nsplit = rows / 512;
+  int chunk = rows / 4;
+  if (chunk > 512) chunk = 512;
+  if (chunk < 64) chunk = 64;
+  nsplit = (rows + chunk - 1) / chunk;
   if (nsplit < 1) nsplit = 1;
   if (nsplit > 64) nsplit = 64;
   kchunk = (rows + nsplit - 1) / nsplit;

@@ -87,6 +87,12 @@ __device__ __forceinline__ void epilogue(const GemmGroup& G, const TileCtx& T, f
   float* const out = partial ? T.Cb + (int64_t)T.split * G.M * G.N : T.Cb;
   const int ldc = partial ? G.N : G.ldc;
   const bool vst = (ldc % 4) == 0 && ((uintptr_t)out & 15) == 0;
+  // a thread always finishes the same 8 columns (rows t>>4 + 16*it of each 64-row pass)
+  const int cg = (t & 15) * 8, j0 = T.j0 + cg;
+  const int nv = min(8, G.N - j0);
+  float bias[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bias[e] = (!partial && (epi & EPI_BIAS) && e < nv) ? T.biasb[j0 + e] : 0.f;
   for (int pass = 0; pass < 2; ++pass) {
     __syncthreads();
     if (wm == pass) {
@@ -98,12 +104,12 @@ __device__ __forceinline__ void epilogue(const GemmGroup& G, const TileCtx& T, f
           for (int r = 0; r < 16; ++r) cs[(a * 32 + acc_row(r, h)) * CS + wn * 64 + b * 32 + c] = acc[a][b][r];
     }
     __syncthreads();
-#pragma unroll 1
-    for (int g = t; g < 64 * (BN / 8); g += NT) {
-      const int lr = g >> 4, cg = (g & 15) * 8;
-      const int i = T.i0 + pass * 64 + lr, j0 = T.j0 + cg;
-      if (i >= G.M || j0 >= G.N) continue;
-      const int nv = min(8, G.N - j0);
+    if (nv <= 0) continue;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int lr = (t >> 4) + 16 * it;
+      const int i = T.i0 + pass * 64 + lr;
+      if (i >= G.M) continue;
       const f32x4 lo = *reinterpret_cast<const f32x4*>(cs + lr * CS + cg);
       const f32x4 hi = *reinterpret_cast<const f32x4*>(cs + lr * CS + cg + 4);
       float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -119,8 +125,7 @@ __device__ __forceinline__ void epilogue(const GemmGroup& G, const TileCtx& T, f
         for (int e = 0; e < 8; ++e) {
           if (e >= nv) break;
           const int j = j0 + e;
-          float x = v[e] * G.alpha;
-          if (epi & EPI_BIAS) x += T.biasb[j] * brs;
+          float x = v[e] * G.alpha + bias[e] * brs;
           if (epi & EPI_ROWADD) x += G.rowadd_scale * G.rowadd[(int64_t)(i / G.rowadd_div) * G.ld_rowadd + j];
           if (epi & EPI_ADDMAT) x += G.addm[(int64_t)i * G.ld_addm + j];
           if (epi & EPI_RELU) x = fmaxf(x, 0.f);

@@ -175,7 +175,7 @@ class _HybridFunction(torch.autograd.Function):
         dev = mask.device
         dlogits = _nat.f32c(dlogits)
         ws = torch.empty(L.mmf_hybrid_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
-        flat = torch.empty(plan.num_param_elems, dtype=torch.float32, device=dev)
+        flat = torch.zeros(plan.num_param_elems, dtype=torch.float32, device=dev)
         gviews = plan.grad_views(flat, params)
         gstruct = plan.param_struct(gviews)
         pstruct = plan.param_struct(params)
@@ -229,18 +229,23 @@ class _Plan:
                        "classifier.3.bias"]
         self.num_param_elems = 0
 
+    # every tensor of a flat parameter / gradient buffer starts on a 256-byte
+    # boundary, so the kernels' 16-byte vector paths apply to all of them
+    ALIGN = 64
+
     def params(self, model: "HybridFusion") -> List[torch.Tensor]:
         named = dict(model.named_parameters())
         out = [named[n] for n in self.names]
-        self.num_param_elems = sum(p.numel() for p in out)
+        self.offsets = []
+        off = 0
+        for p in out:
+            self.offsets.append(off)
+            off += -(-p.numel() // self.ALIGN) * self.ALIGN
+        self.num_param_elems = off
         return out
 
     def grad_views(self, flat: torch.Tensor, params) -> List[torch.Tensor]:
-        views, off = [], 0
-        for p in params:
-            views.append(flat[off:off + p.numel()].view_as(p))
-            off += p.numel()
-        return views
+        return [flat[o:o + p.numel()].view_as(p) for o, p in zip(self.offsets, params)]
 
     def param_struct(self, ts) -> "_nat.HybridParams":
         s = _nat.HybridParams()

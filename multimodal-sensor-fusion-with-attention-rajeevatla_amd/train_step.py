@@ -83,14 +83,13 @@ class HybridTrainStep:
         d = self.plan.desc
         params = self.plan.params(model)
         n = self.plan.num_param_elems
-        self.flat = torch.empty(n, dtype=torch.float32, device=dev)
+        # flat buffers (zero padding between tensors stays zero under AdamW)
+        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(n, dtype=torch.float32, device=dev)
-        off = 0
-        for p in params:
+        for off, p in zip(self.plan.offsets, params):
             k = p.numel()
             self.flat[off:off + k].copy_(p.detach().reshape(-1))
             p.data = self.flat[off:off + k].view_as(p)
-            off += k
         self.params = params
         self.gviews = self.plan.grad_views(self.grad, params)
         self.exp_avg = torch.zeros_like(self.flat)

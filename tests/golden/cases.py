@@ -98,6 +98,7 @@ class HybridCase:
     mask_keep: float = 1.0                       # seeded Bernoulli keep-rate when mask is None
     deleted: List[str] = field(default_factory=list)
     full: bool = True            # store full gradient tensors (small cases)
+    attn_slice: int = 0          # > 0: store attention maps as flat[::attn_slice] (large maps)
 
     @property
     def seq_mode(self) -> bool:
@@ -191,6 +192,16 @@ HYBRID_CASES: List[HybridCase] = [
     HybridCase("seq_hd64", ["m0", "m1"], {"m0": 32, "m1": 48},
                {"m0": 40, "m1": 72}, batch=2, hidden=128, heads=2, classes=4,
                seed=33, mask=[[1, 1], [1, 0]]),
+    # The benchmark's per-sample shape (C2 seq mode: L=128, D=H=128, 4 heads) at
+    # B=3: every key length a multiple of 32 (the lean pooled-attention kernels)
+    # and float4-able GEMM operands (the LDS-DMA GEMM).
+    HybridCase("seq_c2_b3", ["m0", "m1", "m2"], {"m0": 128, "m1": 128, "m2": 128},
+               {"m0": 128, "m1": 128, "m2": 128}, batch=3, hidden=128, heads=4, classes=5,
+               seed=34, mask=[[1, 1, 1], [1, 0, 1], [0.5, 1, 1]], full=False, attn_slice=29),
+    # Mixed multiples of 32 with head_dim 64 (lean kernels, HDP = 64).
+    HybridCase("seq_lean_hd64", ["a", "b"], {"a": 64, "b": 32},
+               {"a": 64, "b": 96}, batch=2, hidden=128, heads=2, classes=4,
+               seed=35, mask=[[1, 1], [1, 0]], full=False, attn_slice=7),
 ]
 
 CMA_CASES: List[CMACase] = [

@@ -16,7 +16,7 @@ What is recorded (eval mode, ``torch.set_float32_matmul_precision("highest")``):
   * standalone CrossModalAttention (src/attention.py:68-146).
   * for a fixed upstream gradient G: d(sum(out * G)) w.r.t. inputs and params.
 
-Run:  python tests/golden/gen_golden.py
+Run:  python tests/golden/gen_golden.py [case1,case2,...]
 """
 
 from __future__ import annotations
@@ -118,7 +118,11 @@ def gen_hybrid(ref_fusion, case):
         "mask": mask_np,
     }
     for key in pair_names(case.names, case.deleted):
-        out[f"attn/{key}"] = info["attention_maps"][key].detach().numpy()
+        amap = info["attention_maps"][key].detach().numpy()
+        if case.attn_slice:
+            out[f"attnslice/{key}"] = amap.reshape(-1)[::case.attn_slice].copy()
+        else:
+            out[f"attn/{key}"] = amap
     for m in case.names:
         g = feats[m].grad.numpy()
         out[f"dx/{m}"] = g
@@ -154,14 +158,19 @@ def gen_cma(ref_attention, case):
 
 
 def main():
+    only = set(sys.argv[1].split(",")) if len(sys.argv) > 1 else None   # e.g. seq_c2_b3,seq_lean_hd64
     torch.set_float32_matmul_precision("highest")
     torch.set_num_threads(4)
     ref_fusion, ref_attention = _load_reference()
     for case in HYBRID_CASES:
+        if only and case.name not in only:
+            continue
         out = gen_hybrid(ref_fusion, case)
         np.savez_compressed(HERE / f"{case.name}.npz", **out)
         print(f"wrote {case.name}.npz ({sum(a.nbytes for a in out.values())} B raw)")
     for case in CMA_CASES:
+        if only and case.name not in only:
+            continue
         out = gen_cma(ref_attention, case)
         np.savez_compressed(HERE / f"{case.name}.npz", **out)
         print(f"wrote {case.name}.npz ({sum(a.nbytes for a in out.values())} B raw)")

@@ -70,8 +70,12 @@ def _oracle_flat_grad(model, feats, mask, labels) -> torch.Tensor:
     fd = {n: f.clone() for n, f in zip(names, feats)}
     hybrid_train_step(params, names, fd, mask, labels, HEADS, 0.0)
     plan = model._plan(feats, False)
-    return torch.cat([(params[n].grad if params[n].grad is not None else torch.zeros_like(params[n])).reshape(-1)
-                      for n in plan.names])
+    plan.params(model)
+    flat = torch.zeros(plan.num_param_elems)
+    for n, o in zip(plan.names, plan.offsets):
+        g = params[n].grad if params[n].grad is not None else torch.zeros_like(params[n])
+        flat[o:o + g.numel()] = g.reshape(-1)
+    return flat
 
 
 def _cpu_rank(rank: int, world: int, port: int, out: str) -> None:

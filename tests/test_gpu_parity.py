@@ -52,8 +52,12 @@ def test_hybrid_matches_reference(mods, case):
     assert close(logits.detach().cpu(), fx["logits"], RTOL, ATOL)
     assert close(info["fusion_weights"].cpu(), fx["fusion_weights"], RTOL, ATOL)
     for key, amap in info["attention_maps"].items():
-        assert close(amap.cpu(), fx[f"attn/{key}"], RTOL, ATOL), key
-    assert set(info["attention_maps"]) == {k[5:] for k in fx if k.startswith("attn/")}
+        if case.attn_slice:
+            assert close(amap.cpu().reshape(-1)[::case.attn_slice], fx[f"attnslice/{key}"], RTOL, ATOL), key
+        else:
+            assert close(amap.cpu(), fx[f"attn/{key}"], RTOL, ATOL), key
+    pref = "attnslice/" if case.attn_slice else "attn/"
+    assert set(info["attention_maps"]) == {k[len(pref):] for k in fx if k.startswith(pref)}
     for m in case.names:
         assert close(feats[m].grad.cpu(), fx[f"dx/{m}"], RTOL, ATOL), m
     for name, p in model.named_parameters():

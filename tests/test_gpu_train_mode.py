@@ -36,6 +36,10 @@ TRAIN_CASES = [
     HybridCase("train_l1", ["a", "b", "c"], {"a": 12, "b": 20, "c": 16},
                {"a": 0, "b": 0, "c": 0}, batch=8, hidden=32, heads=4, classes=5, seed=52,
                mask=[[1, 1, 1], [1, 0, 1], [0, 0, 1], [0, 0, 0], [1, 1, 0.5]]),
+    # key lengths multiples of 32: the lean pooled-attention kernels in train mode
+    HybridCase("train_lean", ["a", "b", "c"], {"a": 32, "b": 32, "c": 64},
+               {"a": 32, "b": 64, "c": 96}, batch=3, hidden=64, heads=2, classes=5, seed=54,
+               mask=[[1, 1, 1], [1, 0, 1], [0.5, 1, 0]]),
     HybridCase("train_general_long", ["x", "y"], {"x": 16, "y": 8},
                {"x": 20, "y": 140}, batch=2, hidden=64, heads=2, classes=3, seed=53,
                mask=[[1, 1], [1, 0]]),

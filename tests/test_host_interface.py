@@ -150,5 +150,10 @@ def test_deepcopy_and_plan_descriptor(mods):
     assert list(d.seq_len)[:2] == [5, 7] and list(d.in_dim)[:2] == [6, 10]
     assert d.num_pairs == 2 and (d.pair_q[0], d.pair_k[0], d.pair_q[1], d.pair_k[1]) == (0, 1, 1, 0)
     params = plan.params(model)
-    assert plan.num_param_elems == sum(p.numel() for p in model.parameters())
     assert len(params) == len(list(model.parameters()))
+    # flat buffers: every tensor on a 256-byte boundary, no overlap
+    assert all(o % 64 == 0 for o in plan.offsets)
+    ends = [o + p.numel() for o, p in zip(plan.offsets, params)]
+    assert all(e <= o2 for e, o2 in zip(ends, plan.offsets[1:])) and ends[-1] <= plan.num_param_elems
+    views = plan.grad_views(torch.zeros(plan.num_param_elems), params)
+    assert [v.shape for v in views] == [p.shape for p in params]

@@ -25,6 +25,9 @@ def test_oracle_hybrid_matches_reference(case):
     for k in fx:
         if k.startswith("attn/"):
             assert rel_err(out[k], fx[k]) <= TOL, k
+        elif k.startswith("attnslice/"):
+            got = out["attn/" + k[len("attnslice/"):]].reshape(-1)[::case.attn_slice]
+            assert rel_err(got, fx[k]) <= TOL, k
     for m in case.names:
         assert rel_err(dx[m], fx[f"dx/{m}"]) <= TOL, m
     for k, g in grads.items():
