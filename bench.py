@@ -60,6 +60,8 @@ def stage_flops(M, B, L, D, H, heads, C):
             "fwd.out_gemm": 2 * B * H * H * P,
             "fwd.cls1_gemm": 2 * B * H * H,
             "fwd.cls2_gemm": 2 * B * H * C,
+            "fwd.tail": 2 * 2 * B * H * H * P + 2 * B * H * H + 2 * B * H * C,   # fused V/O/head/classifier
+            "bwd.tail": 2 * B * C * H + 2 * B * H * H + 2 * 2 * B * H * H * P,
             "bwd.cls_dz1_gemm": 2 * B * C * H,
             "bwd.cls_dfused_gemm": 2 * B * H * H,
             "bwd.out_dO_gemm": 2 * B * H * H * P,

@@ -522,6 +522,7 @@ __global__ __launch_bounds__(256) void partial_reduce_kernel(const ReduceArgs a)
         const f32x4* base = reinterpret_cast<const f32x4*>(J.part) + col;
         const int64_t st = MN / 4;
         int k = sg;
+#pragma unroll 4
         for (; k + 12 < J.nsplit; k += 16) {
           s0 += base[(int64_t)k * st];
           s1 += base[(int64_t)(k + 4) * st];
@@ -546,51 +547,62 @@ __global__ __launch_bounds__(256) void partial_reduce_kernel(const ReduceArgs a)
       }
     }
   }
-  if (J.db && J.part_db && blockIdx.x == 0) {
+  // bias gradient: row sums of the slabs' part_db (4 independent partial sums
+  // per thread so the loads overlap; fixed order => deterministic)
+  if (J.db && J.part_db && blockIdx.x == gridDim.x - 1) {
     for (int i = threadIdx.x; i < J.M; i += blockDim.x) {
-      float s = 0.f;
-      for (int k = 0; k < J.nsplit; ++k) s += J.part_db[(int64_t)k * J.M + i];
-      J.db[i] = s;
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+      int k = 0;
+#pragma unroll 4
+      for (; k + 3 < J.nsplit; k += 4) {
+        s0 += J.part_db[(int64_t)k * J.M + i];
+        s1 += J.part_db[(int64_t)(k + 1) * J.M + i];
+        s2 += J.part_db[(int64_t)(k + 2) * J.M + i];
+        s3 += J.part_db[(int64_t)(k + 3) * J.M + i];
+      }
+      for (; k < J.nsplit; ++k) s0 += J.part_db[(int64_t)k * J.M + i];
+      J.db[i] = (s0 + s1) + (s2 + s3);
     }
   }
 }
 
 // ------------------------------------------------------------------ input mask + dropout
-__global__ __launch_bounds__(256) void mask_dropout_rows_kernel(int64_t n, int D, const float* __restrict__ x,
-                                                                float* __restrict__ out,
-                                                                const float* __restrict__ mask, int L, int M,
-                                                                int m, uint32_t site, float p,
-                                                                const RngSnap* rng, int vec) {
-  const bool drop = p > 0.f && rng != nullptr;
+// X'_m = X_m * mask[:, m] * keep / (1-p) for every modality in one launch
+// (blockIdx.y = modality); a thread handles the 8 elements of one Philox block.
+__global__ __launch_bounds__(256) void mask_dropout_rows_kernel(const MaskDropArgs a) {
+  const int m = blockIdx.y;
+  const MaskDropJob& J = a.j[m];
+  const int64_t n = J.rows * J.D;
+  const bool drop = a.p > 0.f && a.rng != nullptr;
   RngSnap rs{0, 0};
-  if (drop) rs = *rng;
-  const uint32_t thr = p16(p);
-  const float inv_keep = p < 1.f ? 1.f / (1.f - p) : 0.f;
-  // thread handles the 8 elements of one Philox block
+  if (drop) rs = *a.rng;
+  const uint32_t thr = p16(a.p);
+  const float inv_keep = a.p < 1.f ? 1.f / (1.f - a.p) : 0.f;
+  const int D = J.D, L = J.L, M = a.M;
   for (int64_t blk = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; blk * 8 < n;
        blk += (int64_t)gridDim.x * blockDim.x) {
     uint4 r = make_uint4(0, 0, 0, 0);
-    if (drop) r = philox_block(rs, site, (uint64_t)blk);
+    if (drop) r = philox_block(rs, J.site, (uint64_t)blk);
     const int64_t base = blk * 8;
-    if (vec && base + 8 <= n) {
-      const float s = mask[(base / D / L) * M + m];
-      float4 v0 = *reinterpret_cast<const float4*>(x + base);
-      float4 v1 = *reinterpret_cast<const float4*>(x + base + 4);
+    if (J.vec && base + 8 <= n) {
+      const float sc = a.mask[(base / D / L) * M + m];
+      const float4 v0 = *reinterpret_cast<const float4*>(J.x + base);
+      const float4 v1 = *reinterpret_cast<const float4*>(J.x + base + 4);
       float o[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        float v = o[e] * s;
+        float v = o[e] * sc;
         if (drop) v = keep_from(r, e, thr) ? v * inv_keep : 0.f;
         o[e] = v;
       }
-      *reinterpret_cast<float4*>(out + base) = make_float4(o[0], o[1], o[2], o[3]);
-      *reinterpret_cast<float4*>(out + base + 4) = make_float4(o[4], o[5], o[6], o[7]);
+      *reinterpret_cast<float4*>(J.out + base) = make_float4(o[0], o[1], o[2], o[3]);
+      *reinterpret_cast<float4*>(J.out + base + 4) = make_float4(o[4], o[5], o[6], o[7]);
     } else {
       for (int e = 0; e < 8 && base + e < n; ++e) {
         const int64_t idx = base + e;
-        float v = x[idx] * mask[(idx / D / L) * M + m];
+        float v = J.x[idx] * a.mask[(idx / D / L) * M + m];
         if (drop) v = keep_from(r, e, thr) ? v * inv_keep : 0.f;
-        out[idx] = v;
+        J.out[idx] = v;
       }
     }
   }
@@ -701,15 +713,16 @@ hipError_t launch_reduce(const ReduceJob* jobs, int njobs, hipStream_t st) {
   return hipSuccess;
 }
 
-hipError_t launch_mask_dropout_rows(int64_t rows, int D, const float* x, float* out, const float* mask, int L,
-                                    int M, int m, uint32_t site, float p, const RngSnap* rng, hipStream_t st) {
-  const int64_t n = rows * D;
-  if (n == 0) return hipSuccess;
-  const int64_t blks = (n + 7) / 8;
-  int grid = (int)std::min<int64_t>((blks + 255) / 256, 4096);
-  const int vec = (D % 8) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)out & 15) == 0;
-  hipLaunchKernelGGL(mask_dropout_rows_kernel, dim3(grid), dim3(256), 0, st, n, D, x, out, mask, L, M, m, site,
-                     p, rng, vec);
+hipError_t launch_mask_dropout(MaskDropArgs a, hipStream_t st) {
+  if (a.n < 1 || a.n > 8) return hipErrorInvalidValue;
+  int64_t maxblk = 1;
+  for (int m = 0; m < a.n; ++m) {
+    MaskDropJob& J = a.j[m];
+    J.vec = (J.D % 8) == 0 && ((uintptr_t)J.x & 15) == 0 && ((uintptr_t)J.out & 15) == 0;
+    maxblk = std::max<int64_t>(maxblk, (J.rows * J.D + 7) / 8);
+  }
+  const int grid = (int)std::min<int64_t>((maxblk + 255) / 256, 2048);
+  hipLaunchKernelGGL(mask_dropout_rows_kernel, dim3(grid, a.n), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

@@ -233,6 +233,43 @@ void fill_head(HeadArgs& ha, const mmf_hybrid_desc* d, const mmf_hybrid_params* 
   ha.pooled = s.pooled; ha.scores = s.scores; ha.weights = s.weights; ha.fused = s.fused;
 }
 
+bool use_tail(const mmf_hybrid_desc* d) {
+  return use_pool(d) && tail_supported(d->num_modalities, d->hidden, d->num_classes, d->num_heads,
+                                       d->hidden / d->num_heads, d->num_pairs);
+}
+
+void fill_tail(TailArgs& ta, const mmf_hybrid_desc* d, const mmf_hybrid_params* W, const float* mask,
+               const Saved& s) {
+  memset(&ta, 0, sizeof(ta));
+  const int M = d->num_modalities;
+  ta.B = d->batch; ta.M = M; ta.H = d->hidden; ta.C = d->num_classes;
+  ta.heads = d->num_heads; ta.hd = d->hidden / d->num_heads; ta.npairs = d->num_pairs;
+  ta.mask = mask;
+  int cnt[MMF_MAX_MODALITIES];
+  for (int m = 0; m < M; ++m) {
+    ta.P[m] = s.P[m];
+    ta.L[m] = Lm(d, m);
+    ta.gate_w[m] = W->gate[m].w;
+    ta.gate_b[m] = W->gate[m].b;
+    cnt[m] = 1;
+  }
+  for (int g = 0; g < d->num_pairs; ++g) {
+    TailPair& P = ta.p[g];
+    P.U = s.U[g]; P.r = s.r[g];
+    P.Wv = W->v[g].w; P.bv = W->v[g].b; P.Wo = W->o[g].w; P.bo = W->o[g].b;
+    P.Ob = s.Ob[g];
+    P.q = d->pair_q[g];
+    cnt[d->pair_q[g]]++;
+  }
+  for (int m = 0; m < M; ++m) ta.inv_cnt[m] = 1.0f / (float)cnt[m];
+  ta.W1 = W->cls1.w; ta.b1 = W->cls1.b; ta.W2 = W->cls2.w; ta.b2 = W->cls2.b;
+  ta.pooled = s.pooled; ta.scores = s.scores; ta.weights = s.weights; ta.fused = s.fused; ta.h1 = s.h1;
+  ta.drop_p = dropping(d) ? d->dropout : 0.f;
+  ta.drop_site = SITE_CLS;
+  ta.rng = s.rng;
+  ta.gscale = dropping(d) ? 1.f / (1.f - d->dropout) : 1.f;
+}
+
 AttnPair make_pair(const mmf_hybrid_desc* d, const Saved& s, const float* mask, int g) {
   AttnPair a;
   memset(&a, 0, sizeof(a));
@@ -284,17 +321,21 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
   // (1) per-modality projection: P_m = Drop(ReLU(X'_m W_m^T + b_m)), X'_m = Drop(X_m * mask_m)
   //     (fusion.py:364-374); X' is kept for the weight gradient
   {
+    MaskDropArgs ma;
+    memset(&ma, 0, sizeof(ma));
+    ma.n = M; ma.M = M; ma.mask = mask; ma.p = p; ma.rng = rng;
     std::vector<GemmJob> jobs;
     for (int m = 0; m < M; ++m) {
       const int L = Lm(d, m), D = d->in_dim[m];
-      STAGE_TRY("fwd.input_mask", launch_mask_dropout_rows((int64_t)B * L, D, x[m], s.Xd[m], mask, L, M, m,
-                                                           SITE_IN + m, p, rng, st));
+      ma.j[m].x = x[m]; ma.j[m].out = s.Xd[m]; ma.j[m].rows = (int64_t)B * L; ma.j[m].D = D; ma.j[m].L = L;
+      ma.j[m].site = SITE_IN + m;
       GemmJob j = make_job(B * L, H, s.P[m], H, EPI_BIAS | EPI_RELU | (drop ? EPI_DROP : 0));
       j.g.bias = W->proj[m].b;
       j.g.drop_site = SITE_PROJ + m;
       add_src(j, opnd(s.Xd[m], D), opnd(W->proj[m].w, D), D);
       jobs.push_back(j);
     }
+    STAGE_TRY("fwd.input_mask", launch_mask_dropout(ma, st));
     STAGE_TRY("fwd.proj_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, p, rng, st));
   }
   // (2) Q/K (and V for the general plan) projections of every present pair (attention.py:104-106)
@@ -336,27 +377,36 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
       pp[g].r = s.r[g];
     }
     STAGE_TRY("fwd.pool_u", launch_pool_u(pp.data(), d->num_pairs, B, nh, hd, H, st));
-    std::vector<GemmJob> jobs;
-    for (int g = 0; g < d->num_pairs; ++g) {
-      // Obar[:, h*hd:(h+1)*hd] = U_h W_v[h*hd:(h+1)*hd, :]^T + r_h b_v,h  (batch over heads)
-      GemmJob j = make_job(B, hd, s.Ob[g], H, EPI_BIAS | EPI_BIAS_RS);
-      j.g.bias = W->v[g].b;
-      j.g.bias_rs = s.r[g];
-      j.g.bias_rs_ld = nh;
-      j.g.nbatch = nh;
-      j.g.bs_a = H; j.g.bs_b = hd * H; j.g.bs_c = hd; j.g.bs_bias = hd; j.g.bs_brs = 1;
-      add_src(j, opnd(s.U[g], nh * H), opnd(W->v[g].w, H), H);
-      jobs.push_back(j);
+    if (use_tail(d)) {
+      // (4p) fused per-sample tail: Obar, Abar, aggregation, weighting, classifier
+      TailArgs ta;
+      fill_tail(ta, d, W, mask, s);
+      ta.weights_out = fusion_weights;
+      ta.logits = logits;
+      STAGE_TRY("fwd.tail", launch_tail_fwd(ta, st));
+    } else {
+      std::vector<GemmJob> jobs;
+      for (int g = 0; g < d->num_pairs; ++g) {
+        // Obar[:, h*hd:(h+1)*hd] = U_h W_v[h*hd:(h+1)*hd, :]^T + r_h b_v,h  (batch over heads)
+        GemmJob j = make_job(B, hd, s.Ob[g], H, EPI_BIAS | EPI_BIAS_RS);
+        j.g.bias = W->v[g].b;
+        j.g.bias_rs = s.r[g];
+        j.g.bias_rs_ld = nh;
+        j.g.nbatch = nh;
+        j.g.bs_a = H; j.g.bs_b = hd * H; j.g.bs_c = hd; j.g.bs_bias = hd; j.g.bs_brs = 1;
+        add_src(j, opnd(s.U[g], nh * H), opnd(W->v[g].w, H), H);
+        jobs.push_back(j);
+      }
+      STAGE_TRY("fwd.vbar_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, 0.f, rng, st));
+      jobs.clear();
+      for (int g = 0; g < d->num_pairs; ++g) {
+        GemmJob j = make_job(B, H, s.Ab[g], H, EPI_BIAS);
+        j.g.bias = W->o[g].b;
+        add_src(j, opnd(s.Ob[g], H), opnd(W->o[g].w, H), H);
+        jobs.push_back(j);
+      }
+      STAGE_TRY("fwd.out_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, 0.f, rng, st));
     }
-    STAGE_TRY("fwd.vbar_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, 0.f, rng, st));
-    jobs.clear();
-    for (int g = 0; g < d->num_pairs; ++g) {
-      GemmJob j = make_job(B, H, s.Ab[g], H, EPI_BIAS);
-      j.g.bias = W->o[g].b;
-      add_src(j, opnd(s.Ob[g], H), opnd(W->o[g].w, H), H);
-      jobs.push_back(j);
-    }
-    STAGE_TRY("fwd.out_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, 0.f, rng, st));
   } else if (d->num_pairs) {
     // (3g) flash attention per pair (key mask = modality mask column k, fusion.py:391-401) + out_proj
     STAGE_TRY("fwd.attn", launch_attn_fwd(pairs.data(), d->num_pairs, B, nh, hd, scale, p, rng, st));
@@ -371,12 +421,12 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
     STAGE_TRY("fwd.out_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, 0.f, rng, st));
   }
   // (4) aggregation + pooling + gating + adaptive weights + weighted sum (fusion.py:406-418)
-  HeadArgs ha;
-  fill_head(ha, d, W, mask, s);
-  ha.weights_out = fusion_weights;
-  STAGE_TRY("fwd.head", launch_head_fwd(ha, st));
   // (5) classifier: Linear -> ReLU -> Dropout -> Linear (fusion.py:323-328)
-  {
+  if (!(d->num_pairs && use_tail(d))) {
+    HeadArgs ha;
+    fill_head(ha, d, W, mask, s);
+    ha.weights_out = fusion_weights;
+    STAGE_TRY("fwd.head", launch_head_fwd(ha, st));
     GemmJob j = make_job(B, H, s.h1, H, EPI_BIAS | EPI_RELU | (drop ? EPI_DROP : 0));
     j.g.bias = W->cls1.b;
     j.g.drop_site = SITE_CLS;
@@ -427,22 +477,35 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
   plan_wgrads(d, x, mask, dlogits, s, w, G, bw, wp);
   if (bw.off > workspace_bytes(d)) return fail(MMF_EINVAL, "internal: workspace overflow");
 
-  // (1) classifier backward: dz1 = ReLU'/Dropout' (dlogits W2), dfused = dz1 W1
-  {
-    GemmJob j = make_job(B, H, w.dz1, H, EPI_GATE);
-    j.g.gate = s.h1; j.g.ld_gate = H; j.g.gate_scale = gscale;
-    add_src(j, opnd(dlogits, C), opnd(W->cls2.w, H), C);
-    STAGE_TRY("bwd.cls_dz1_gemm", launch_gemm(&j, 1, MODE_RK, MODE_KR, 0.f, rng, st));
-    GemmJob j2 = make_job(B, H, w.dfused, H, 0);
-    add_src(j2, opnd(w.dz1, H), opnd(W->cls1.w, H), H);
-    STAGE_TRY("bwd.cls_dfused_gemm", launch_gemm(&j2, 1, MODE_RK, MODE_KR, 0.f, rng, st));
-  }
-  // (2) head backward: dscore and c_m = dpooled_m * mask_m / n_m
-  {
-    HeadArgs ha;
-    fill_head(ha, d, W, mask, s);
-    ha.dfused = w.dfused; ha.cvec = w.cvec; ha.dscore = w.dscore;
-    STAGE_TRY("bwd.head", launch_head_bwd(ha, st));
+  const bool tail = d->num_pairs && use_tail(d);
+  if (tail) {
+    // (1-3p) fused per-sample tail backward: classifier, head, dObar, dU
+    TailArgs ta;
+    fill_tail(ta, d, W, mask, s);
+    ta.dlogits = dlogits; ta.dz1 = w.dz1; ta.cvec = w.cvec; ta.dscore = w.dscore;
+    for (int g = 0; g < d->num_pairs; ++g) {
+      ta.p[g].dOb = w.dOb[g];
+      ta.p[g].dU = w.dU[g];
+    }
+    STAGE_TRY("bwd.tail", launch_tail_bwd(ta, st));
+  } else {
+    // (1) classifier backward: dz1 = ReLU'/Dropout' (dlogits W2), dfused = dz1 W1
+    {
+      GemmJob j = make_job(B, H, w.dz1, H, EPI_GATE);
+      j.g.gate = s.h1; j.g.ld_gate = H; j.g.gate_scale = gscale;
+      add_src(j, opnd(dlogits, C), opnd(W->cls2.w, H), C);
+      STAGE_TRY("bwd.cls_dz1_gemm", launch_gemm(&j, 1, MODE_RK, MODE_KR, 0.f, rng, st));
+      GemmJob j2 = make_job(B, H, w.dfused, H, 0);
+      add_src(j2, opnd(w.dz1, H), opnd(W->cls1.w, H), H);
+      STAGE_TRY("bwd.cls_dfused_gemm", launch_gemm(&j2, 1, MODE_RK, MODE_KR, 0.f, rng, st));
+    }
+    // (2) head backward: dscore and c_m = dpooled_m * mask_m / n_m
+    {
+      HeadArgs ha;
+      fill_head(ha, d, W, mask, s);
+      ha.dfused = w.dfused; ha.cvec = w.cvec; ha.dscore = w.dscore;
+      STAGE_TRY("bwd.head", launch_head_bwd(ha, st));
+    }
   }
   const float scale = 1.0f / std::sqrt((float)hd);
   std::vector<AttnPair> pairs(d->num_pairs);
@@ -453,25 +516,27 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
   }
   if (d->num_pairs && pool) {
     // (3p) dObar = dAbar W_o (dAbar = c_q); dU_h = dObar_h W_v,h; dpbar; attention dQ/dK; E_m
-    std::vector<GemmJob> jobs;
-    for (int g = 0; g < d->num_pairs; ++g) {
-      GemmJob j = make_job(B, H, w.dOb[g], H, 0);
-      add_src(j, opnd(w.cvec + (size_t)d->pair_q[g] * H, M * H), opnd(W->o[g].w, H), H);
-      jobs.push_back(j);
+    if (!tail) {
+      std::vector<GemmJob> jobs;
+      for (int g = 0; g < d->num_pairs; ++g) {
+        GemmJob j = make_job(B, H, w.dOb[g], H, 0);
+        add_src(j, opnd(w.cvec + (size_t)d->pair_q[g] * H, M * H), opnd(W->o[g].w, H), H);
+        jobs.push_back(j);
+      }
+      STAGE_TRY("bwd.out_dO_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, 0.f, rng, st));
+      jobs.clear();
+      for (int g = 0; g < d->num_pairs; ++g) {
+        // dU_h = dObar_h W_v[h*hd:(h+1)*hd, :]  (batch over heads)
+        GemmJob j = make_job(B, H, w.dU[g], nh * H, 0);
+        j.g.nbatch = nh;
+        j.g.bs_a = hd; j.g.bs_b = hd * H; j.g.bs_c = H;
+        Operand a = opnd(w.dOb[g], H);
+        a.vec = (hd % 4 == 0) && (H % 4 == 0);
+        add_src(j, a, opnd(W->v[g].w, H), hd);
+        jobs.push_back(j);
+      }
+      STAGE_TRY("bwd.du_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, 0.f, rng, st));
     }
-    STAGE_TRY("bwd.out_dO_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, 0.f, rng, st));
-    jobs.clear();
-    for (int g = 0; g < d->num_pairs; ++g) {
-      // dU_h = dObar_h W_v[h*hd:(h+1)*hd, :]  (batch over heads)
-      GemmJob j = make_job(B, H, w.dU[g], nh * H, 0);
-      j.g.nbatch = nh;
-      j.g.bs_a = hd; j.g.bs_b = hd * H; j.g.bs_c = H;
-      Operand a = opnd(w.dOb[g], H);
-      a.vec = (hd % 4 == 0) && (H % 4 == 0);
-      add_src(j, a, opnd(W->v[g].w, H), hd);
-      jobs.push_back(j);
-    }
-    STAGE_TRY("bwd.du_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, 0.f, rng, st));
     std::vector<PoolPair> pp(d->num_pairs);
     for (int g = 0; g < d->num_pairs; ++g) {
       memset(&pp[g], 0, sizeof(PoolPair));

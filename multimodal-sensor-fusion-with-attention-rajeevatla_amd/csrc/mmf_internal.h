@@ -104,12 +104,22 @@ struct GemmJob {
 hipError_t launch_gemm(const GemmJob* jobs, int njobs, int amode, int bmode, float drop_p,
                        const RngSnap* rng, hipStream_t st);
 
-// X'[r][c] = X[r][c] * mask[(r / L) * M + m] * (keep(site, r*D + c) ? 1/(1-p) : 0)
+// X'_m[r][c] = X_m[r][c] * mask[(r / L_m) * M + m] * (keep(site_m, r*D_m + c) ? 1/(1-p) : 0)
 // (the masked, input-dropped modality features of src/fusion.py:364-373,
 // materialised once for the projection GEMM and its weight gradient).
-hipError_t launch_mask_dropout_rows(int64_t rows, int D, const float* x, float* out, const float* mask,
-                                    int L, int M, int m, uint32_t site, float p, const RngSnap* rng,
-                                    hipStream_t st);
+struct MaskDropJob {
+  const float* x; float* out;
+  int64_t rows; int32_t D, L;
+  uint32_t site; int32_t vec;
+};
+struct MaskDropArgs {
+  MaskDropJob j[8];
+  int32_t n, M;
+  const float* mask;
+  float p;
+  const RngSnap* rng;
+};
+hipError_t launch_mask_dropout(MaskDropArgs a, hipStream_t st);
 
 // Split-K partial-slab reduction: out[e] = sum_s part[s][e]; db[i] = sum_s part_db[s][i].
 struct ReduceJob {
@@ -248,5 +258,46 @@ hipError_t launch_cross_entropy(int B, int C, const float* logits, const int64_t
 hipError_t launch_adamw(int64_t n, float* p, const float* g, float* m, float* v, int64_t* step,
                         float lr, float b1, float b2, float eps, float wd, float gscale,
                         hipStream_t st);
+
+}  // namespace mmf
+
+namespace mmf {
+
+// ---------------------------------------------------------------------------
+// Fused per-sample tail of the pooled plan (tail.hip): one workgroup per sample
+// runs the B-row work that is otherwise a chain of tiny latency-bound launches.
+//   forward : Obar_g = U_g W_v^T (per head) + r_g b_v;  Abar_g = Obar_g W_o^T + b_o;
+//             pooled_m = mask_m / n_m * (mean_L P_m + sum_{g: q(g)=m} Abar_g);
+//             gating scores, adaptive weights, fused; h1 = Drop(ReLU(fused W1^T + b1));
+//             logits = h1 W2^T + b2                                 (src/fusion.py:383-427)
+//   backward: dz1 = ReLU'/Drop'(dlogits W2); dfused = dz1 W1; head backward
+//             (dscore, cvec); dObar_g = cvec_q(g) W_o; dU_g,h = dObar_g,h W_v,h
+// ---------------------------------------------------------------------------
+struct TailPair {
+  const float* U; const float* r;      // (B, h, H), (B, h)
+  const float* Wv; const float* bv; const float* Wo; const float* bo;
+  float* Ob;                           // (B, H) saved Obar
+  float* dOb;                          // (B, H)
+  float* dU;                           // (B, h, H)
+  int32_t q; int32_t pad_;
+};
+constexpr int TAIL_MAX_PAIRS = 12;
+constexpr int TAIL_MAX_H = 256;
+struct TailArgs {
+  int32_t B, M, H, C, heads, hd, npairs;
+  const float* mask;                   // (B, M)
+  const float* P[8]; int32_t L[8];     // projected features (B, L_m, H)
+  float inv_cnt[8];
+  const float* gate_w[8]; const float* gate_b[8];
+  const float* W1; const float* b1; const float* W2; const float* b2;
+  float* pooled; float* scores; float* weights; float* weights_out; float* fused; float* h1; float* logits;
+  float drop_p; uint32_t drop_site; const RngSnap* rng;
+  // backward
+  const float* dlogits; float* dz1; float* cvec; float* dscore; float gscale;
+  TailPair p[TAIL_MAX_PAIRS];
+};
+bool tail_supported(int M, int H, int C, int heads, int hd, int npairs);
+hipError_t launch_tail_fwd(const TailArgs& a, hipStream_t st);
+hipError_t launch_tail_bwd(const TailArgs& a, hipStream_t st);
 
 }  // namespace mmf

@@ -43,11 +43,22 @@ __global__ __launch_bounds__(NT) void pool_u_kernel(const PoolArgs a) {
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     if (rg < RG) {
       const int hh = task / H4, c4 = task % H4;
-      for (int j = rg; j < Lk; j += RG) {
+      float4 acc2 = acc;
+      int j = rg;
+#pragma unroll 4
+      for (; j + RG < Lk; j += 2 * RG) {
+        const float4 v = *reinterpret_cast<const float4*>(pk + (int64_t)j * H + 4 * c4);
+        const float4 u = *reinterpret_cast<const float4*>(pk + (int64_t)(j + RG) * H + 4 * c4);
+        const float w = pb[hh * Lk + j], w2 = pb[hh * Lk + j + RG];
+        acc.x += w * v.x; acc.y += w * v.y; acc.z += w * v.z; acc.w += w * v.w;
+        acc2.x += w2 * u.x; acc2.y += w2 * u.y; acc2.z += w2 * u.z; acc2.w += w2 * u.w;
+      }
+      if (j < Lk) {
         const float4 v = *reinterpret_cast<const float4*>(pk + (int64_t)j * H + 4 * c4);
         const float w = pb[hh * Lk + j];
         acc.x += w * v.x; acc.y += w * v.y; acc.z += w * v.z; acc.w += w * v.w;
       }
+      acc.x += acc2.x; acc.y += acc2.y; acc.z += acc2.z; acc.w += acc2.w;
     }
     __syncthreads();
     red[t] = acc;
@@ -84,6 +95,7 @@ __global__ __launch_bounds__(NT) void pool_dpbar_kernel(const PoolArgs a) {
   __syncthreads();
   const float* pk = P.pk + (int64_t)b * Lk * H;
   const int half = lane >> 5, l32 = lane & 31;
+#pragma unroll 2
   for (int j0 = 2 * wave; j0 < Lk; j0 += 8) {
     const int j = j0 + half;
     float acc[MAXH];
@@ -130,9 +142,11 @@ __global__ __launch_bounds__(NT) void pool_e_kernel(const PoolEArgs a) {
   const int j = (int)(e / H4), c4 = (int)(e % H4);
   const float4 cv = *reinterpret_cast<const float4*>(E.c + (int64_t)b * E.ldc + 4 * c4);
   float4 acc = make_float4(cv.x * E.cscale, cv.y * E.cscale, cv.z * E.cscale, cv.w * E.cscale);
+#pragma unroll 2
   for (int s = 0; s < E.nsrc; ++s) {
     const float* pb = E.pbar[s] + (int64_t)b * heads * L;
     const float* du = E.du[s] + (int64_t)b * heads * H;
+#pragma unroll 4
     for (int hh = 0; hh < heads; ++hh) {
       const float w = pb[hh * L + j];
       const float4 u = *reinterpret_cast<const float4*>(du + hh * H + 4 * c4);

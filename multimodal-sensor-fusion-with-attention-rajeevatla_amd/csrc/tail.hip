@@ -1,0 +1,360 @@
+// Fused per-sample tail of the pooled HybridFusion plan (forward and backward).
+//
+// After the attention kernels, everything left in a HybridFusion step works on
+// B rows: value/out projections of the query-mean (pooled plan, see
+// attention.hip), the aggregation + gating + adaptive weighting
+// (src/fusion.py:406-418, compute_adaptive_weights :429-479) and the
+// classifier (src/fusion.py:323-328, 419).  As separate GEMM launches these
+// are a dozen latency-bound kernels of 2-12 workgroups each.  Here ONE
+// workgroup per sample runs the whole chain as GEMVs against L2-resident
+// weights (a weight row is read with float4 loads by adjacent lanes), keeping
+// every intermediate in LDS.  Nothing mixes samples, so the launch is B
+// independent workgroups.
+#include <cstring>
+
+#include "mmf_device.h"
+
+namespace mmf {
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int MAXM = 8;
+constexpr int MAXHEADS = 8;
+
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// y[n] = sum_k x(n)[k] * W[n][k] for n < N; x(n) = xs + (n / xdiv) * xstride
+// (a per-head input when xdiv = head_dim).  Two adjacent lanes share an output
+// (k halves, K % 16 == 0) and keep all their float4 loads of the W row in
+// flight at once: these chains are latency-bound, so memory-level
+// parallelism per lane beats wider coalescing (measured: 8 lanes per row
+// with 4 passes was 1.5x slower).
+__device__ __forceinline__ void gemv_nt(const float* xs, int xdiv, int xstride, const float* __restrict__ W,
+                                        int N, int K, float* y) {
+  const int t = threadIdx.x, half = t & 1;
+  const int kh = K >> 1;
+  for (int n = t >> 1; n < N; n += NT / 2) {
+    const float* x = xs + (n / xdiv) * xstride + half * kh;
+    const float* w = W + (int64_t)n * K + half * kh;
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < kh; k += 8) {
+      const float4 a = *reinterpret_cast<const float4*>(w + k);
+      const float4 b = *reinterpret_cast<const float4*>(w + k + 4);
+      s0 += a.x * x[k] + a.y * x[k + 1] + a.z * x[k + 2] + a.w * x[k + 3];
+      s1 += b.x * x[k + 4] + b.y * x[k + 5] + b.z * x[k + 6] + b.w * x[k + 7];
+    }
+    float s = s0 + s1;
+    s += __shfl_xor(s, 1);
+    if (half == 0) y[n] = s;
+  }
+}
+
+// y[k] = sum_{n in [n0, n1)} x[n] * W[n][k] for k < K (W row-major, ld = K):
+// threads split as 128 columns x 2 row halves, combined through `red` (NT floats).
+__device__ __forceinline__ void gemv_nn(const float* x, const float* __restrict__ W, int n0, int n1, int K,
+                                        float* y, float* red) {
+  const int t = threadIdx.x, rh = t >> 7, kc = t & 127;
+  const int nm = n0 + ((n1 - n0) >> 1);
+  for (int k0 = 0; k0 < K; k0 += 128) {
+    const int k = k0 + kc;
+    float s = 0.f;
+    if (k < K) {
+      const int a = rh ? nm : n0, e = rh ? n1 : nm;
+      float s1 = 0.f;
+      int n = a;
+#pragma unroll 8
+      for (; n + 1 < e; n += 2) {
+        s += x[n] * W[(int64_t)n * K + k];
+        s1 += x[n + 1] * W[(int64_t)(n + 1) * K + k];
+      }
+      if (n < e) s += x[n] * W[(int64_t)n * K + k];
+      s += s1;
+    }
+    __syncthreads();
+    red[t] = s;
+    __syncthreads();
+    if (rh == 0 && k < K) y[k] = red[t] + red[t + 128];
+  }
+}
+
+// y[s][k] = sum_{n in segment s} x[n] * W[n][k] for nseg segments of `seg` rows
+// (the per-head row blocks of value_proj.weight): thread (k = t & 127, group
+// t >> 7) owns whole segments, so no cross-thread reduction is needed.
+__device__ __forceinline__ void gemv_nn_seg(const float* x, const float* __restrict__ W, int nseg, int seg, int K,
+                                            float* y) {
+  const int t = threadIdx.x, sg = t >> 7, kc = t & 127;
+  for (int k0 = 0; k0 < K; k0 += 128) {
+    const int k = k0 + kc;
+    if (k >= K) continue;
+    for (int sgi = sg; sgi < nseg; sgi += NT / 128) {
+      const int n0 = sgi * seg;
+      float s0 = 0.f, s1 = 0.f;
+      int n = 0;
+#pragma unroll 8
+      for (; n + 1 < seg; n += 2) {
+        s0 += x[n0 + n] * W[(int64_t)(n0 + n) * K + k];
+        s1 += x[n0 + n + 1] * W[(int64_t)(n0 + n + 1) * K + k];
+      }
+      if (n < seg) s0 += x[n0 + n] * W[(int64_t)(n0 + n) * K + k];
+      y[sgi * K + k] = s0 + s1;
+    }
+  }
+}
+
+// Masked softmax over modalities + renormalisation / fallback (src/fusion.py:462-478);
+// see head.hip adaptive_fwd (identical arithmetic).
+__device__ float adaptive_w(int M, const float* score, const float* mask, float* sm, float* w) {
+  float mx = -INFINITY;
+  for (int m = 0; m < M; ++m)
+    if (mask[m] > 0.f) mx = fmaxf(mx, score[m]);
+  float z = 0.f;
+  for (int m = 0; m < M; ++m) {
+    sm[m] = (mask[m] > 0.f) ? __expf(score[m] - mx) : 0.f;
+    z += sm[m];
+  }
+  float sw = 0.f, ms = 0.f;
+  for (int m = 0; m < M; ++m) {
+    sm[m] = (mx == -INFINITY) ? 0.f : sm[m] / z;
+    w[m] = sm[m] * mask[m];
+    sw += w[m];
+    ms += mask[m];
+  }
+  if (sw > 0.f) {
+    const float den = sw + 1e-8f;
+    for (int m = 0; m < M; ++m) w[m] = w[m] / den;
+  } else {
+    for (int m = 0; m < M; ++m) w[m] = ms > 0.f ? mask[m] / (ms + 1e-8f) : 1.f / (float)M;
+  }
+  return sw;
+}
+
+__global__ __launch_bounds__(NT) void tail_fwd_kernel(const TailArgs a) {
+  __shared__ __attribute__((aligned(16))) float pooled_s[MAXM * TAIL_MAX_H];
+  __shared__ __attribute__((aligned(16))) float u_s[MAXHEADS * TAIL_MAX_H];
+  __shared__ __attribute__((aligned(16))) float v1[TAIL_MAX_H], v2[TAIL_MAX_H];
+  __shared__ __attribute__((aligned(16))) float4 red4[NT];
+  __shared__ float score_s[MAXM], w_s[MAXM], r_s[MAXHEADS];
+  const int b = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int M = a.M, H = a.H, nh = a.heads, hd = a.hd;
+  const int H4 = H >> 2;
+
+  // (1) mean over L of P_m (the modality's own entry of the aggregation list)
+  for (int m = 0; m < M; ++m) {
+    const int L = a.L[m];
+    const float* base = a.P[m] + (int64_t)b * L * H;
+    const int RG = NT / H4;
+    const int c4 = t % H4, rg = t / H4;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f), acc2 = acc;
+    if (rg < RG) {
+      int r = rg;
+#pragma unroll 4
+      for (; r + RG < L; r += 2 * RG) {
+        const float4 v = *reinterpret_cast<const float4*>(base + (int64_t)r * H + 4 * c4);
+        const float4 u = *reinterpret_cast<const float4*>(base + (int64_t)(r + RG) * H + 4 * c4);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        acc2.x += u.x; acc2.y += u.y; acc2.z += u.z; acc2.w += u.w;
+      }
+      if (r < L) {
+        const float4 v = *reinterpret_cast<const float4*>(base + (int64_t)r * H + 4 * c4);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+    }
+    red4[t] = make_float4(acc.x + acc2.x, acc.y + acc2.y, acc.z + acc2.z, acc.w + acc2.w);
+    __syncthreads();
+    if (t < H4) {
+      float4 s = red4[t];
+      for (int g = 1; g < RG; ++g) {
+        const float4 v = red4[g * H4 + t];
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      }
+      const float f = 1.f / (float)L;
+      *reinterpret_cast<float4*>(&pooled_s[m * H + 4 * t]) = make_float4(s.x * f, s.y * f, s.z * f, s.w * f);
+    }
+    __syncthreads();
+  }
+  // (2) per pair: Obar = U W_v^T (per head) + r b_v;  Abar = Obar W_o^T + b_o -> pooled[q]
+  for (int g = 0; g < a.npairs; ++g) {
+    const TailPair& P = a.p[g];
+    for (int i = t; i < nh * H4; i += NT)
+      *reinterpret_cast<float4*>(&u_s[4 * i]) =
+          *reinterpret_cast<const float4*>(P.U + (int64_t)b * nh * H + 4 * i);
+    if (t < nh) r_s[t] = P.r[(int64_t)b * nh + t];
+    __syncthreads();
+    gemv_nt(u_s, hd, H, P.Wv, H, H, v1);
+    __syncthreads();
+    for (int n = t; n < H; n += NT) {
+      const float o = v1[n] + r_s[n / hd] * P.bv[n];
+      v1[n] = o;
+      P.Ob[(int64_t)b * H + n] = o;
+    }
+    __syncthreads();
+    gemv_nt(v1, 1 << 30, 0, P.Wo, H, H, v2);
+    __syncthreads();
+    for (int n = t; n < H; n += NT) pooled_s[P.q * H + n] += v2[n] + P.bo[n];
+    __syncthreads();
+  }
+  // (3) agg * mask / n_m; gating scores (nn.Linear(H, 1), src/fusion.py:316-321,452-461)
+  for (int i = t; i < M * H; i += NT) {
+    const int m = i / H;
+    pooled_s[i] *= a.inv_cnt[m] * a.mask[(int64_t)b * M + m];
+    a.pooled[(int64_t)b * M * H + i] = pooled_s[i];
+  }
+  __syncthreads();
+  for (int m = wave; m < M; m += NT / 64) {
+    float s = 0.f;
+    for (int j = lane; j < H; j += 64) s += pooled_s[m * H + j] * a.gate_w[m][j];
+    s = wsum(s);
+    if (lane == 0) score_s[m] = s + a.gate_b[m][0];
+  }
+  __syncthreads();
+  if (t == 0) {
+    float msk[MAXM], sm[MAXM], w[MAXM];
+    for (int m = 0; m < M; ++m) msk[m] = a.mask[(int64_t)b * M + m];
+    adaptive_w(M, score_s, msk, sm, w);
+    for (int m = 0; m < M; ++m) {
+      w_s[m] = w[m];
+      a.scores[(int64_t)b * M + m] = score_s[m];
+      a.weights[(int64_t)b * M + m] = w[m];
+      if (a.weights_out) a.weights_out[(int64_t)b * M + m] = w[m];
+    }
+  }
+  __syncthreads();
+  // (4) fused = sum_m w_m pooled_m; classifier Linear -> ReLU -> Dropout -> Linear
+  for (int j = t; j < H; j += NT) {
+    float f = 0.f;
+    for (int m = 0; m < M; ++m) f += pooled_s[m * H + j] * w_s[m];
+    v1[j] = f;
+    a.fused[(int64_t)b * H + j] = f;
+  }
+  __syncthreads();
+  gemv_nt(v1, 1 << 30, 0, a.W1, H, H, v2);
+  __syncthreads();
+  const float p = a.drop_p;
+  const bool drop = p > 0.f && a.rng != nullptr;
+  RngSnap rs{0, 0};
+  if (drop) rs = *a.rng;
+  const float inv_keep = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  for (int n = t; n < H; n += NT) {
+    float x = fmaxf(v2[n] + a.b1[n], 0.f);
+    if (drop) x = keep1(rs, a.drop_site, (uint64_t)b * H + n, p) ? x * inv_keep : 0.f;
+    v2[n] = x;
+    a.h1[(int64_t)b * H + n] = x;
+  }
+  __syncthreads();
+  for (int c = wave; c < a.C; c += NT / 64) {
+    float s = 0.f;
+    for (int j = lane; j < H; j += 64) s += v2[j] * a.W2[(int64_t)c * H + j];
+    s = wsum(s);
+    if (lane == 0) a.logits[(int64_t)b * a.C + c] = s + a.b2[c];
+  }
+}
+
+__global__ __launch_bounds__(NT) void tail_bwd_kernel(const TailArgs a) {
+  __shared__ __attribute__((aligned(16))) float pooled_s[MAXM * TAIL_MAX_H];
+  __shared__ __attribute__((aligned(16))) float cvec_s[MAXM * TAIL_MAX_H];
+  __shared__ __attribute__((aligned(16))) float du_s[MAXHEADS * TAIL_MAX_H];
+  __shared__ __attribute__((aligned(16))) float v1[TAIL_MAX_H], v2[TAIL_MAX_H], dl_s[256];
+  __shared__ float red[NT];
+  __shared__ float dw_s[MAXM], dscore_s[MAXM];
+  const int b = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int M = a.M, H = a.H, C = a.C, nh = a.heads, hd = a.hd;
+
+  for (int c = t; c < C; c += NT) dl_s[c] = a.dlogits[(int64_t)b * C + c];
+  for (int i = t; i < M * H; i += NT) pooled_s[i] = a.pooled[(int64_t)b * M * H + i];
+  __syncthreads();
+  // (1) dz1 = ReLU'/Dropout'(dlogits W2): the saved h1 is post-dropout, so h1 > 0
+  //     marks kept, active units (gscale = 1/(1-p))
+  gemv_nn(dl_s, a.W2, 0, C, H, v1, red);
+  __syncthreads();
+  for (int n = t; n < H; n += NT) {
+    const float z = a.h1[(int64_t)b * H + n] > 0.f ? v1[n] * a.gscale : 0.f;
+    v1[n] = z;
+    a.dz1[(int64_t)b * H + n] = z;
+  }
+  __syncthreads();
+  // dfused = dz1 W1
+  gemv_nn(v1, a.W1, 0, H, H, v2, red);
+  __syncthreads();
+  // (2) head backward (head.hip head_bwd_kernel): dw_m = dfused . pooled_m
+  for (int m = wave; m < M; m += NT / 64) {
+    float s = 0.f;
+    for (int j = lane; j < H; j += 64) s += v2[j] * pooled_s[m * H + j];
+    s = wsum(s);
+    if (lane == 0) dw_s[m] = s;
+  }
+  __syncthreads();
+  if (t == 0) {
+    float msk[MAXM], sc[MAXM], sm[MAXM], w[MAXM], ds[MAXM];
+    for (int m = 0; m < M; ++m) {
+      msk[m] = a.mask[(int64_t)b * M + m];
+      sc[m] = a.scores[(int64_t)b * M + m];
+      ds[m] = 0.f;
+    }
+    const float sw = adaptive_w(M, sc, msk, sm, w);
+    if (sw > 0.f) {
+      const float S = sw + 1e-8f;
+      float dot = 0.f;
+      for (int m = 0; m < M; ++m) dot += dw_s[m] * sm[m] * msk[m];
+      float dsm[MAXM], sdot = 0.f;
+      for (int m = 0; m < M; ++m) {
+        dsm[m] = (dw_s[m] / S - dot / (S * S)) * msk[m];
+        sdot += sm[m] * dsm[m];
+      }
+      for (int m = 0; m < M; ++m) ds[m] = msk[m] > 0.f ? sm[m] * (dsm[m] - sdot) : 0.f;
+    }
+    for (int m = 0; m < M; ++m) {
+      dscore_s[m] = ds[m];
+      a.dscore[(int64_t)b * M + m] = ds[m];
+    }
+  }
+  __syncthreads();
+  for (int i = t; i < M * H; i += NT) {
+    const int m = i / H, j = i - m * H;
+    const float wm = a.weights[(int64_t)b * M + m];
+    const float f = a.mask[(int64_t)b * M + m] * a.inv_cnt[m];
+    const float c = (wm * v2[j] + dscore_s[m] * a.gate_w[m][j]) * f;
+    cvec_s[i] = c;
+    a.cvec[(int64_t)b * M * H + i] = c;
+  }
+  __syncthreads();
+  // (3) per pair: dObar = cvec_q W_o;  dU_h = dObar_h W_v[h rows]
+  for (int g = 0; g < a.npairs; ++g) {
+    const TailPair& P = a.p[g];
+    gemv_nn(cvec_s + P.q * H, P.Wo, 0, H, H, v1, red);
+    __syncthreads();
+    for (int n = t; n < H; n += NT) P.dOb[(int64_t)b * H + n] = v1[n];
+    gemv_nn_seg(v1, P.Wv, nh, hd, H, du_s);
+    __syncthreads();
+    for (int i = t; i < nh * H; i += NT) P.dU[(int64_t)b * nh * H + i] = du_s[i];
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+bool tail_supported(int M, int H, int C, int heads, int hd, int npairs) {
+  return M <= MAXM && heads <= MAXHEADS && H % 32 == 0 && H <= TAIL_MAX_H && C <= 256 &&
+         npairs <= TAIL_MAX_PAIRS && hd % 8 == 0 && (NT % (H / 4)) == 0;
+}
+
+hipError_t launch_tail_fwd(const TailArgs& a, hipStream_t st) {
+  if (!tail_supported(a.M, a.H, a.C, a.heads, a.hd, a.npairs)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(tail_fwd_kernel, dim3(a.B), dim3(NT), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_tail_bwd(const TailArgs& a, hipStream_t st) {
+  if (!tail_supported(a.M, a.H, a.C, a.heads, a.hd, a.npairs)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(tail_bwd_kernel, dim3(a.B), dim3(NT), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace mmf
