@@ -255,9 +255,10 @@ void fill_tail(TailArgs& ta, const mmf_hybrid_desc* d, const mmf_hybrid_params* 
   }
   for (int g = 0; g < d->num_pairs; ++g) {
     TailPair& P = ta.p[g];
+    P.pbar = s.pbar[g]; P.Pk = s.P[d->pair_k[g]]; P.Lk = Lm(d, d->pair_k[g]);
     P.U = s.U[g]; P.r = s.r[g];
     P.Wv = W->v[g].w; P.bv = W->v[g].b; P.Wo = W->o[g].w; P.bo = W->o[g].b;
-    P.Ob = s.Ob[g];
+    P.Ob = s.Ob[g]; P.Ab = s.Ab[g];
     P.q = d->pair_q[g];
     cnt[d->pair_q[g]]++;
   }
@@ -376,7 +377,6 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
       pp[g].u = s.U[g];
       pp[g].r = s.r[g];
     }
-    STAGE_TRY("fwd.pool_u", launch_pool_u(pp.data(), d->num_pairs, B, nh, hd, H, st));
     if (use_tail(d)) {
       // (4p) fused per-sample tail: Obar, Abar, aggregation, weighting, classifier
       TailArgs ta;
@@ -385,6 +385,7 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
       ta.logits = logits;
       STAGE_TRY("fwd.tail", launch_tail_fwd(ta, st));
     } else {
+      STAGE_TRY("fwd.pool_u", launch_pool_u(pp.data(), d->num_pairs, B, nh, hd, H, st));
       std::vector<GemmJob> jobs;
       for (int g = 0; g < d->num_pairs; ++g) {
         // Obar[:, h*hd:(h+1)*hd] = U_h W_v[h*hd:(h+1)*hd, :]^T + r_h b_v,h  (batch over heads)
@@ -486,6 +487,7 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
     for (int g = 0; g < d->num_pairs; ++g) {
       ta.p[g].dOb = w.dOb[g];
       ta.p[g].dU = w.dU[g];
+      ta.p[g].dpbar = w.dpbar[g];
     }
     STAGE_TRY("bwd.tail", launch_tail_bwd(ta, st));
   } else {
@@ -547,7 +549,7 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
       pp[g].bv = W->v[g].b;
       pp[g].dpbar = w.dpbar[g];
     }
-    STAGE_TRY("bwd.pool_dpbar", launch_pool_dpbar(pp.data(), d->num_pairs, B, nh, hd, H, st));
+    if (!tail) STAGE_TRY("bwd.pool_dpbar", launch_pool_dpbar(pp.data(), d->num_pairs, B, nh, hd, H, st));
     STAGE_TRY("bwd.attn_dq", launch_attn_pool_bwd(0, pairs.data(), d->num_pairs, B, nh, hd, scale, p, rng, st));
     STAGE_TRY("bwd.attn_dk", launch_attn_pool_bwd(1, pairs.data(), d->num_pairs, B, nh, hd, scale, p, rng, st));
     std::vector<PoolEMod> em(M);

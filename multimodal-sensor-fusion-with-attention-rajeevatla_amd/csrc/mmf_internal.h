@@ -264,22 +264,26 @@ hipError_t launch_adamw(int64_t n, float* p, const float* g, float* m, float* v,
 namespace mmf {
 
 // ---------------------------------------------------------------------------
-// Fused per-sample tail of the pooled plan (tail.hip): one workgroup per sample
-// runs the B-row work that is otherwise a chain of tiny latency-bound launches.
-//   forward : Obar_g = U_g W_v^T (per head) + r_g b_v;  Abar_g = Obar_g W_o^T + b_o;
+// Fused tail of the pooled plan (tail.hip): the B-row work that is otherwise a
+// chain of tiny latency-bound launches, as one launch per (pair, sample) and one
+// per sample in each direction.
+//   forward : U_g = pbar_g P_k; Obar_g = U_g W_v^T (per head) + r_g b_v;  Abar_g = Obar_g W_o^T + b_o;
 //             pooled_m = mask_m / n_m * (mean_L P_m + sum_{g: q(g)=m} Abar_g);
 //             gating scores, adaptive weights, fused; h1 = Drop(ReLU(fused W1^T + b1));
 //             logits = h1 W2^T + b2                                 (src/fusion.py:383-427)
 //   backward: dz1 = ReLU'/Drop'(dlogits W2); dfused = dz1 W1; head backward
-//             (dscore, cvec); dObar_g = cvec_q(g) W_o; dU_g,h = dObar_g,h W_v,h
+//             (dscore, cvec); dObar_g = cvec_q(g) W_o; dU_g,h = dObar_g,h W_v,h;
+//             dpbar_g,h = P_k dU_g,h + dObar_g,h . b_v,h
 // ---------------------------------------------------------------------------
 struct TailPair {
-  const float* U; const float* r;      // (B, h, H), (B, h)
+  const float* pbar; const float* Pk; int32_t Lk;   // (B, h, Lk) query-mean probs; key features (B, Lk, H)
+  int32_t q;                                         // query modality of the pair
+  float* U; float* r;                  // (B, h, H), (B, h) written by the forward
   const float* Wv; const float* bv; const float* Wo; const float* bo;
-  float* Ob;                           // (B, H) saved Obar
+  float* Ob; float* Ab;                // (B, H) Obar (saved) and Abar
   float* dOb;                          // (B, H)
   float* dU;                           // (B, h, H)
-  int32_t q; int32_t pad_;
+  float* dpbar;                        // (B, h, Lk)
 };
 constexpr int TAIL_MAX_PAIRS = 12;
 constexpr int TAIL_MAX_H = 256;

@@ -134,15 +134,149 @@ __device__ float adaptive_w(int M, const float* score, const float* mask, float*
   return sw;
 }
 
-__global__ __launch_bounds__(NT) void tail_fwd_kernel(const TailArgs a) {
-  __shared__ __attribute__((aligned(16))) float pooled_s[MAXM * TAIL_MAX_H];
+// ---------------------------------------------------------------- per (pair, sample)
+// Forward: U_h = pbar_h P_k (+ r_h = sum pbar_h), Obar = U W_v^T (per head) + r b_v,
+// Abar = Obar W_o^T + b_o.  grid (B, npairs).
+__global__ __launch_bounds__(NT) void tail_pair_fwd_kernel(const TailArgs a) {
+  __shared__ float pb_s[MAXHEADS * 128];
   __shared__ __attribute__((aligned(16))) float u_s[MAXHEADS * TAIL_MAX_H];
+  __shared__ __attribute__((aligned(16))) float4 red4[NT];
+  __shared__ __attribute__((aligned(16))) float v1[TAIL_MAX_H], v2[TAIL_MAX_H];
+  __shared__ float r_s[MAXHEADS];
+  const int b = blockIdx.x;
+  const TailPair& P = a.p[blockIdx.y];
+  const int t = threadIdx.x;
+  const int H = a.H, nh = a.heads, hd = a.hd, Lk = P.Lk, H4 = H >> 2;
+  for (int i = t; i < nh * Lk; i += NT) pb_s[i] = P.pbar[(int64_t)b * nh * Lk + i];
+  __syncthreads();
+  if (t < nh) {
+    float s = 0.f;
+    for (int j = 0; j < Lk; ++j) s += pb_s[t * Lk + j];
+    r_s[t] = s;
+    P.r[(int64_t)b * nh + t] = s;
+  }
+  // U: tasks = (head, float4 column); RG row groups split the Lk keys
+  const float* pk = P.Pk + (int64_t)b * Lk * H;
+  const int ncol = nh * H4;
+  for (int task0 = 0; task0 < ncol; task0 += NT) {
+    const int nact = min(NT, ncol - task0);
+    const int RG = NT / nact;
+    const int task = task0 + t % nact, rg = t / nact;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f), acc2 = acc;
+    if (rg < RG) {
+      const int hh = task / H4, c4 = task % H4;
+      int j = rg;
+#pragma unroll 4
+      for (; j + RG < Lk; j += 2 * RG) {
+        const float4 v = *reinterpret_cast<const float4*>(pk + (int64_t)j * H + 4 * c4);
+        const float4 u = *reinterpret_cast<const float4*>(pk + (int64_t)(j + RG) * H + 4 * c4);
+        const float w = pb_s[hh * Lk + j], w2 = pb_s[hh * Lk + j + RG];
+        acc.x += w * v.x; acc.y += w * v.y; acc.z += w * v.z; acc.w += w * v.w;
+        acc2.x += w2 * u.x; acc2.y += w2 * u.y; acc2.z += w2 * u.z; acc2.w += w2 * u.w;
+      }
+      if (j < Lk) {
+        const float4 v = *reinterpret_cast<const float4*>(pk + (int64_t)j * H + 4 * c4);
+        const float w = pb_s[hh * Lk + j];
+        acc.x += w * v.x; acc.y += w * v.y; acc.z += w * v.z; acc.w += w * v.w;
+      }
+    }
+    __syncthreads();
+    red4[t] = make_float4(acc.x + acc2.x, acc.y + acc2.y, acc.z + acc2.z, acc.w + acc2.w);
+    __syncthreads();
+    if (t < nact) {
+      float4 sum = red4[t];
+      for (int g = 1; g < RG; ++g) {
+        const float4 v = red4[g * nact + t];
+        sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
+      }
+      const int tt = task0 + t;
+      *reinterpret_cast<float4*>(&u_s[4 * tt]) = sum;
+      *reinterpret_cast<float4*>(P.U + (int64_t)b * nh * H + 4 * tt) = sum;
+    }
+  }
+  __syncthreads();
+  gemv_nt(u_s, hd, H, P.Wv, H, H, v1);
+  __syncthreads();
+  for (int n = t; n < H; n += NT) {
+    const float o = v1[n] + r_s[n / hd] * P.bv[n];
+    v1[n] = o;
+    P.Ob[(int64_t)b * H + n] = o;
+  }
+  __syncthreads();
+  gemv_nt(v1, 1 << 30, 0, P.Wo, H, H, v2);
+  __syncthreads();
+  for (int n = t; n < H; n += NT) P.Ab[(int64_t)b * H + n] = v2[n] + P.bo[n];
+}
+
+// Backward: dObar = cvec_q W_o; dU_h = dObar_h W_v[h rows];
+// dpbar_h[j] = P_k[j] . dU_h + dObar_h . b_v,h.  grid (B, npairs).
+__global__ __launch_bounds__(NT) void tail_pair_bwd_kernel(const TailArgs a) {
+  __shared__ __attribute__((aligned(16))) float c_s[TAIL_MAX_H], v1[TAIL_MAX_H];
+  __shared__ __attribute__((aligned(16))) float du_s[MAXHEADS * TAIL_MAX_H];
+  __shared__ float red[NT];
+  __shared__ float dr_s[MAXHEADS];
+  const int b = blockIdx.x;
+  const TailPair& P = a.p[blockIdx.y];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int H = a.H, nh = a.heads, hd = a.hd, Lk = P.Lk, M = a.M;
+  for (int i = t; i < H; i += NT) c_s[i] = a.cvec[((int64_t)b * M + P.q) * H + i];
+  __syncthreads();
+  gemv_nn(c_s, P.Wo, 0, H, H, v1, red);
+  __syncthreads();
+  for (int n = t; n < H; n += NT) P.dOb[(int64_t)b * H + n] = v1[n];
+  gemv_nn_seg(v1, P.Wv, nh, hd, H, du_s);
+  for (int hh = wave; hh < nh; hh += NT / 64) {
+    float s = 0.f;
+    for (int d = lane; d < hd; d += 64) s += v1[hh * hd + d] * P.bv[hh * hd + d];
+    s = wsum(s);
+    if (lane == 0) dr_s[hh] = s;
+  }
+  __syncthreads();
+  for (int i = t; i < nh * H; i += NT) P.dU[(int64_t)b * nh * H + i] = du_s[i];
+  // dpbar: a wave takes two keys per step (lane halves), lanes stride the H/4 float4 columns
+  const float* pk = P.Pk + (int64_t)b * Lk * H;
+  const int half = lane >> 5, l32 = lane & 31;
+#pragma unroll 2
+  for (int j0 = 2 * wave; j0 < Lk; j0 += 2 * (NT / 64)) {
+    const int j = j0 + half;
+    float acc[MAXHEADS];
+#pragma unroll
+    for (int hh = 0; hh < MAXHEADS; ++hh) acc[hh] = 0.f;
+    if (j < Lk) {
+      for (int c4 = l32; c4 < H / 4; c4 += 32) {
+        const float4 v = *reinterpret_cast<const float4*>(pk + (int64_t)j * H + 4 * c4);
+#pragma unroll
+        for (int hh = 0; hh < MAXHEADS; ++hh) {
+          if (hh < nh) {
+            const float4 u = *reinterpret_cast<const float4*>(&du_s[hh * H + 4 * c4]);
+            acc[hh] += v.x * u.x + v.y * u.y + v.z * u.z + v.w * u.w;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int hh = 0; hh < MAXHEADS; ++hh) {
+      if (hh < nh) {
+        float sv = acc[hh];
+#pragma unroll
+        for (int o = 16; o >= 1; o >>= 1) sv += __shfl_xor(sv, o);
+        if (l32 == 0 && j < Lk) P.dpbar[((int64_t)b * nh + hh) * Lk + j] = sv + dr_s[hh];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- per sample
+// Forward head: pooled_m = mask_m / n_m (mean_L P_m + sum_{g: q(g)=m} Abar_g), gating
+// scores, adaptive weights, fused, classifier.  grid (B).
+__global__ __launch_bounds__(NT) void tail_head_fwd_kernel(const TailArgs a) {
+  __shared__ __attribute__((aligned(16))) float pooled_s[MAXM * TAIL_MAX_H];
   __shared__ __attribute__((aligned(16))) float v1[TAIL_MAX_H], v2[TAIL_MAX_H];
   __shared__ __attribute__((aligned(16))) float4 red4[NT];
-  __shared__ float score_s[MAXM], w_s[MAXM], r_s[MAXHEADS];
+  __shared__ float score_s[MAXM], w_s[MAXM];
   const int b = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int M = a.M, H = a.H, nh = a.heads, hd = a.hd;
+  const int M = a.M, H = a.H;
   const int H4 = H >> 2;
 
   // (1) mean over L of P_m (the modality's own entry of the aggregation list)
@@ -179,34 +313,18 @@ __global__ __launch_bounds__(NT) void tail_fwd_kernel(const TailArgs a) {
     }
     __syncthreads();
   }
-  // (2) per pair: Obar = U W_v^T (per head) + r b_v;  Abar = Obar W_o^T + b_o -> pooled[q]
-  for (int g = 0; g < a.npairs; ++g) {
-    const TailPair& P = a.p[g];
-    for (int i = t; i < nh * H4; i += NT)
-      *reinterpret_cast<float4*>(&u_s[4 * i]) =
-          *reinterpret_cast<const float4*>(P.U + (int64_t)b * nh * H + 4 * i);
-    if (t < nh) r_s[t] = P.r[(int64_t)b * nh + t];
-    __syncthreads();
-    gemv_nt(u_s, hd, H, P.Wv, H, H, v1);
-    __syncthreads();
-    for (int n = t; n < H; n += NT) {
-      const float o = v1[n] + r_s[n / hd] * P.bv[n];
-      v1[n] = o;
-      P.Ob[(int64_t)b * H + n] = o;
-    }
-    __syncthreads();
-    gemv_nt(v1, 1 << 30, 0, P.Wo, H, H, v2);
-    __syncthreads();
-    for (int n = t; n < H; n += NT) pooled_s[P.q * H + n] += v2[n] + P.bo[n];
-    __syncthreads();
-  }
-  // (3) agg * mask / n_m; gating scores (nn.Linear(H, 1), src/fusion.py:316-321,452-461)
+  // (2) + the attended means of every pair whose query is m, then agg * mask / n_m
   for (int i = t; i < M * H; i += NT) {
-    const int m = i / H;
-    pooled_s[i] *= a.inv_cnt[m] * a.mask[(int64_t)b * M + m];
-    a.pooled[(int64_t)b * M * H + i] = pooled_s[i];
+    const int m = i / H, n = i - m * H;
+    float v = pooled_s[i];
+    for (int g = 0; g < a.npairs; ++g)
+      if (a.p[g].q == m) v += a.p[g].Ab[(int64_t)b * H + n];
+    v *= a.inv_cnt[m] * a.mask[(int64_t)b * M + m];
+    pooled_s[i] = v;
+    a.pooled[(int64_t)b * M * H + i] = v;
   }
   __syncthreads();
+  // (3) gating scores (nn.Linear(H, 1), src/fusion.py:316-321,452-461), adaptive weights
   for (int m = wave; m < M; m += NT / 64) {
     float s = 0.f;
     for (int j = lane; j < H; j += 64) s += pooled_s[m * H + j] * a.gate_w[m][j];
@@ -256,22 +374,21 @@ __global__ __launch_bounds__(NT) void tail_fwd_kernel(const TailArgs a) {
   }
 }
 
-__global__ __launch_bounds__(NT) void tail_bwd_kernel(const TailArgs a) {
+// Backward head: dz1 = ReLU'/Dropout'(dlogits W2), dfused = dz1 W1, head backward
+// (dscore, cvec = dpooled * mask / n).  grid (B).
+__global__ __launch_bounds__(NT) void tail_head_bwd_kernel(const TailArgs a) {
   __shared__ __attribute__((aligned(16))) float pooled_s[MAXM * TAIL_MAX_H];
-  __shared__ __attribute__((aligned(16))) float cvec_s[MAXM * TAIL_MAX_H];
-  __shared__ __attribute__((aligned(16))) float du_s[MAXHEADS * TAIL_MAX_H];
   __shared__ __attribute__((aligned(16))) float v1[TAIL_MAX_H], v2[TAIL_MAX_H], dl_s[256];
   __shared__ float red[NT];
   __shared__ float dw_s[MAXM], dscore_s[MAXM];
   const int b = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int M = a.M, H = a.H, C = a.C, nh = a.heads, hd = a.hd;
+  const int M = a.M, H = a.H, C = a.C;
 
   for (int c = t; c < C; c += NT) dl_s[c] = a.dlogits[(int64_t)b * C + c];
   for (int i = t; i < M * H; i += NT) pooled_s[i] = a.pooled[(int64_t)b * M * H + i];
   __syncthreads();
-  // (1) dz1 = ReLU'/Dropout'(dlogits W2): the saved h1 is post-dropout, so h1 > 0
-  //     marks kept, active units (gscale = 1/(1-p))
+  // the saved h1 is post-dropout, so h1 > 0 marks kept, active units (gscale = 1/(1-p))
   gemv_nn(dl_s, a.W2, 0, C, H, v1, red);
   __syncthreads();
   for (int n = t; n < H; n += NT) {
@@ -280,10 +397,9 @@ __global__ __launch_bounds__(NT) void tail_bwd_kernel(const TailArgs a) {
     a.dz1[(int64_t)b * H + n] = z;
   }
   __syncthreads();
-  // dfused = dz1 W1
   gemv_nn(v1, a.W1, 0, H, H, v2, red);
   __syncthreads();
-  // (2) head backward (head.hip head_bwd_kernel): dw_m = dfused . pooled_m
+  // head backward (head.hip head_bwd_kernel): dw_m = dfused . pooled_m
   for (int m = wave; m < M; m += NT / 64) {
     float s = 0.f;
     for (int j = lane; j < H; j += 64) s += v2[j] * pooled_s[m * H + j];
@@ -320,40 +436,36 @@ __global__ __launch_bounds__(NT) void tail_bwd_kernel(const TailArgs a) {
     const int m = i / H, j = i - m * H;
     const float wm = a.weights[(int64_t)b * M + m];
     const float f = a.mask[(int64_t)b * M + m] * a.inv_cnt[m];
-    const float c = (wm * v2[j] + dscore_s[m] * a.gate_w[m][j]) * f;
-    cvec_s[i] = c;
-    a.cvec[(int64_t)b * M * H + i] = c;
-  }
-  __syncthreads();
-  // (3) per pair: dObar = cvec_q W_o;  dU_h = dObar_h W_v[h rows]
-  for (int g = 0; g < a.npairs; ++g) {
-    const TailPair& P = a.p[g];
-    gemv_nn(cvec_s + P.q * H, P.Wo, 0, H, H, v1, red);
-    __syncthreads();
-    for (int n = t; n < H; n += NT) P.dOb[(int64_t)b * H + n] = v1[n];
-    gemv_nn_seg(v1, P.Wv, nh, hd, H, du_s);
-    __syncthreads();
-    for (int i = t; i < nh * H; i += NT) P.dU[(int64_t)b * nh * H + i] = du_s[i];
-    __syncthreads();
+    a.cvec[(int64_t)b * M * H + i] = (wm * v2[j] + dscore_s[m] * a.gate_w[m][j]) * f;
   }
 }
 
 }  // namespace
 
 bool tail_supported(int M, int H, int C, int heads, int hd, int npairs) {
-  return M <= MAXM && heads <= MAXHEADS && H % 32 == 0 && H <= TAIL_MAX_H && C <= 256 &&
+  return M <= MAXM && heads <= MAXHEADS && H % 16 == 0 && H <= TAIL_MAX_H && C <= 256 &&
          npairs <= TAIL_MAX_PAIRS && hd % 8 == 0 && (NT % (H / 4)) == 0;
 }
 
 hipError_t launch_tail_fwd(const TailArgs& a, hipStream_t st) {
   if (!tail_supported(a.M, a.H, a.C, a.heads, a.hd, a.npairs)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(tail_fwd_kernel, dim3(a.B), dim3(NT), 0, st, a);
+  for (int g = 0; g < a.npairs; ++g)
+    if (a.p[g].Lk > 128) return hipErrorInvalidValue;
+  if (a.npairs) {
+    hipLaunchKernelGGL(tail_pair_fwd_kernel, dim3(a.B, a.npairs), dim3(NT), 0, st, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(tail_head_fwd_kernel, dim3(a.B), dim3(NT), 0, st, a);
   return hipGetLastError();
 }
 
 hipError_t launch_tail_bwd(const TailArgs& a, hipStream_t st) {
   if (!tail_supported(a.M, a.H, a.C, a.heads, a.hd, a.npairs)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(tail_bwd_kernel, dim3(a.B), dim3(NT), 0, st, a);
+  hipLaunchKernelGGL(tail_head_bwd_kernel, dim3(a.B), dim3(NT), 0, st, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !a.npairs) return e;
+  hipLaunchKernelGGL(tail_pair_bwd_kernel, dim3(a.B, a.npairs), dim3(NT), 0, st, a);
   return hipGetLastError();
 }
 
