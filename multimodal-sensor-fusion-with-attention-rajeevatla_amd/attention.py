@@ -1,6 +1,11 @@
 """Drop-in `attention` module: CrossModalAttention on MI355X HIP kernels.
 
-Mirrors src/attention.py::CrossModalAttention (src/attention.py:16-146): same
+Import surface of src/attention.py (tests/test_attention.py:22-27):
+CrossModalAttention (the hot path), TemporalAttention and
+PairwiseModalityAttention (compositions over the same HIP attention kernels)
+and visualize_attention (matplotlib).
+
+CrossModalAttention mirrors src/attention.py:16-146: same
 constructor arguments, attributes (hidden_dim, num_heads, head_dim,
 query_proj, key_proj, value_proj, out_proj, dropout, scale), state_dict keys
 and forward(query, key, value, mask=None) -> (attended, attn_weights).
@@ -189,3 +194,139 @@ class CrossModalAttention(nn.Module):
         if squeeze_k:
             attn = attn[:, :, :, :1]
         return attended, attn
+
+
+class TemporalAttention(CrossModalAttention):
+    """Self-attention over the time steps of one sequence (src/attention.py:149-281).
+
+    Same parameters as the reference (query/key/value/out_proj, feature_dim ->
+    hidden_dim) and the same forward(sequence, mask=None) -> (attended,
+    weights).  The attention itself runs on the CrossModalAttention HIP kernels
+    with query = key = value = sequence and a per-key mask; the reference's
+    post-mask multiply (src/attention.py:245-248) keeps its exact broadcasting,
+    including the extra leading dims it produces for a 2-D mask.
+    """
+
+    feature_dim: int
+
+    def __init__(self, feature_dim: int, hidden_dim: int = 256, num_heads: int = 4, dropout: float = 0.1):
+        super().__init__(feature_dim, feature_dim, hidden_dim=hidden_dim, num_heads=num_heads, dropout=dropout)
+        cast(Any, self).feature_dim = feature_dim
+
+    def forward(self, sequence: torch.Tensor,  # type: ignore[override]
+                mask: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        if sequence.dim() != 3:
+            raise RuntimeError(f"TemporalAttention expects (batch, seq_len, feature_dim), got {tuple(sequence.shape)}")
+        B, L = sequence.size(0), sequence.size(1)
+        key_mask = None
+        if mask is not None:
+            m = mask.to(sequence.device)
+            if m.dim() == 1:          # one mask over the time axis, shared by the batch (:239-240)
+                m = m.unsqueeze(0)
+            key_mask = m.expand(B, L).to(torch.float32).contiguous()
+        attended, weights = super().forward(sequence, sequence, sequence, mask=key_mask)
+        if mask is not None:
+            m = mask.to(sequence.device)
+            if m.dim() == 1:
+                m = m.unsqueeze(0)
+            attended = attended * m.unsqueeze(1).unsqueeze(2).unsqueeze(-1)
+        return attended, weights
+
+    def pool_sequence(self, sequence: torch.Tensor, attention_weights: torch.Tensor) -> torch.Tensor:
+        """Attention-weighted pooling over time (src/attention.py:253-281): the mean
+        over heads and queries of the weights, renormalised, applied to the sequence."""
+        if attention_weights.dim() != 4:
+            raise ValueError(f"Expected attention weights with 4 dims, got {attention_weights.shape}")
+        w = attention_weights.mean(dim=(1, 2))                         # (B, L)
+        w = w / (w.sum(dim=1, keepdim=True) + 1e-8)
+        return torch.bmm(w.unsqueeze(1), sequence).squeeze(1)
+
+
+class PairwiseModalityAttention(nn.Module):
+    """Attention between every ordered pair of modalities (src/attention.py:284-424).
+
+    Per-modality Linear -> ReLU -> Dropout projections, a CrossModalAttention
+    (HIP kernels) for each present "{q}_to_{k}" pair keyed by the key
+    modality's mask column, then the mean of each modality's list scaled by its
+    mask.  Returns (attended_features, attention_maps) like the reference.
+    """
+
+    modality_names: list
+    num_modalities: int
+    hidden_dim: int
+
+    def __init__(self, modality_dims, hidden_dim: int = 256, num_heads: int = 4, dropout: float = 0.1):
+        super().__init__()
+        dims = dict(modality_dims)
+        cast_self = cast(Any, self)
+        cast_self.modality_names = list(dims)
+        cast_self.num_modalities = len(dims)
+        cast_self.hidden_dim = hidden_dim
+        self.projections = nn.ModuleDict({
+            m: nn.Sequential(nn.Linear(d, hidden_dim), nn.ReLU(), nn.Dropout(dropout)) for m, d in dims.items()})
+        self.attention_layers = nn.ModuleDict({
+            f"{q}_to_{k}": CrossModalAttention(hidden_dim, hidden_dim, hidden_dim=hidden_dim, num_heads=num_heads,
+                                               dropout=dropout)
+            for q in dims for k in dims if q != k})
+
+    def forward(self, modality_features, modality_mask: Optional[torch.Tensor] = None):
+        if not self.modality_names:
+            raise ValueError("No modalities provided for PairwiseModalityAttention.")
+        first = modality_features[self.modality_names[0]]
+        B, dev, dt = first.size(0), first.device, first.dtype
+        if modality_mask is None:
+            mask = torch.ones(B, self.num_modalities, device=dev, dtype=dt)
+        else:
+            mask = modality_mask.to(device=dev, dtype=dt)
+        proj = {m: self.projections[m](modality_features[m].to(dev)) for m in self.modality_names}
+        lists = {m: [proj[m]] for m in self.modality_names}
+        maps = {}
+        for q in self.modality_names:
+            for k in self.modality_names:
+                key = f"{q}_to_{k}"
+                if q == k or key not in self.attention_layers:
+                    continue
+                att, w = self.attention_layers[key](proj[q], proj[k], proj[k],
+                                                    mask=mask[:, self.modality_names.index(k)])
+                lists[q].append(att)
+                maps[key] = w
+        out = {}
+        for i, m in enumerate(self.modality_names):
+            out[m] = torch.stack(lists[m], dim=0).mean(dim=0) * mask[:, i].unsqueeze(-1)
+        return out, maps
+
+
+def visualize_attention(attention_weights, modality_names, save_path=None) -> None:
+    """Heat map of attention weights (src/attention.py:427-480): leading dims are
+    averaged down to a (queries, keys) matrix; saved to `save_path` or shown."""
+    from pathlib import Path
+
+    import matplotlib.pyplot as plt
+    import numpy as np
+
+    t = attention_weights.detach().float().cpu() if torch.is_tensor(attention_weights) \
+        else torch.as_tensor(attention_weights, dtype=torch.float32)
+    while t.dim() < 2:
+        t = t.unsqueeze(0)
+    while t.dim() > 2:
+        t = t.mean(dim=0)
+    grid = t.numpy()
+    nq, nk = grid.shape
+    fig, ax = plt.subplots(figsize=(4 + 0.5 * nk, 4))
+    im = ax.imshow(grid, cmap="viridis", aspect="auto")
+    ax.set_xticks(np.arange(nk))
+    ax.set_yticks(np.arange(nq))
+    ax.set_xticklabels(list(modality_names)[:nk], rotation=45, ha="right")
+    ax.set_yticklabels(list(modality_names)[:nq])
+    ax.set_xlabel("Key Modality")
+    ax.set_ylabel("Query Modality")
+    ax.set_title("Cross-Modal Attention Weights")
+    plt.colorbar(im, ax=ax, fraction=0.046, pad=0.04)
+    plt.tight_layout()
+    if save_path is not None:
+        out = Path(save_path)
+        out.parent.mkdir(parents=True, exist_ok=True)
+        fig.savefig(out, dpi=300, bbox_inches="tight")
+        plt.close(fig)
+    else:
+        plt.show()

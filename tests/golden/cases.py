@@ -221,3 +221,84 @@ def case_by_name(name: str):
         if c.name == name:
             return c
     raise KeyError(name)
+
+
+# ----------------------------------------------------------------------------
+# TemporalAttention (src/attention.py:149-281) and PairwiseModalityAttention
+# (src/attention.py:284-424): the rest of the attention module's import surface.
+# ----------------------------------------------------------------------------
+@dataclass
+class TemporalCase:
+    name: str
+    batch: int
+    seq: int
+    feature_dim: int
+    hidden: int
+    heads: int
+    seed: int
+    mask_kind: str = "none"     # none | 1d (per time step, shared) | 2d (B, L)
+
+
+TEMPORAL_CASES: List[TemporalCase] = [
+    TemporalCase("temporal_nomask", batch=3, seq=40, feature_dim=32, hidden=64, heads=4, seed=61),
+    TemporalCase("temporal_mask2d", batch=2, seq=10, feature_dim=24, hidden=32, heads=4, seed=62, mask_kind="2d"),
+    TemporalCase("temporal_mask1d", batch=2, seq=6, feature_dim=16, hidden=32, heads=2, seed=63, mask_kind="1d"),
+]
+
+
+def temporal_inputs(case: TemporalCase):
+    """(sequence, mask or None, upstream grad with the output's shape)."""
+    rng = np.random.default_rng(case.seed + 15485863)
+    seq = rng.standard_normal((case.batch, case.seq, case.feature_dim)).astype(np.float32)
+    mask = None
+    out_shape = (case.batch, case.seq, case.hidden)
+    if case.mask_kind == "2d":
+        mask = np.zeros((case.batch, case.seq), dtype=np.float32)
+        for b in range(case.batch):
+            mask[b, : max(1, case.seq - 3 - 2 * b)] = 1.0
+        out_shape = (case.batch, 1, case.batch, case.seq, case.hidden)   # the reference's broadcast
+    elif case.mask_kind == "1d":
+        mask = np.asarray([1, 0, 1, 0, 1, 1][: case.seq], dtype=np.float32)
+        out_shape = (1, 1, case.batch, case.seq, case.hidden)
+    grad = rng.standard_normal(out_shape).astype(np.float32)
+    return seq, mask, grad
+
+
+@dataclass
+class PairwiseCase:
+    name: str
+    names: List[str]
+    dims: Dict[str, int]
+    batch: int
+    hidden: int
+    heads: int
+    seed: int
+    mask: Optional[List[List[float]]] = None
+    deleted: List[str] = field(default_factory=list)
+
+
+PAIRWISE_CASES: List[PairwiseCase] = [
+    PairwiseCase("pairwise_3mod", ["video", "audio", "imu"], {"video": 24, "audio": 16, "imu": 8},
+                 batch=4, hidden=32, heads=4, seed=71,
+                 mask=[[1, 0, 1], [1, 1, 1], [0, 1, 1], [1, 1, 0]], deleted=["video_to_audio"]),
+]
+
+
+def pairwise_state(case: PairwiseCase) -> "OrderedDict[str, np.ndarray]":
+    """Keys of the reference PairwiseModalityAttention (projections + attention_layers)."""
+    full = hybrid_state(case.names, case.dims, case.hidden, 2, case.seed, case.deleted)
+    sd: "OrderedDict[str, np.ndarray]" = OrderedDict()
+    for k, v in full.items():
+        if k.startswith("projections."):
+            sd[k] = v
+        elif k.startswith("attention_modules."):
+            sd["attention_layers." + k[len("attention_modules."):]] = v
+    return sd
+
+
+def pairwise_inputs(case: PairwiseCase):
+    rng = np.random.default_rng(case.seed + 32452843)
+    feats = {m: rng.standard_normal((case.batch, case.dims[m])).astype(np.float32) for m in case.names}
+    mask = np.asarray(case.mask, dtype=np.float32)
+    grads = {m: rng.standard_normal((case.batch, case.hidden)).astype(np.float32) for m in case.names}
+    return feats, mask, grads

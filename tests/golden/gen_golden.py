@@ -13,7 +13,8 @@ What is recorded (eval mode, ``torch.set_float32_matmul_precision("highest")``):
     ``attention_modules`` called on 3-D tensors (src/attention.py:92-146),
     mean over the per-modality list, x mask, mean-pool over L,
     ``compute_adaptive_weights`` (src/fusion.py:429-479), ``classifier``.
-  * standalone CrossModalAttention (src/attention.py:68-146).
+  * standalone CrossModalAttention (src/attention.py:68-146), TemporalAttention
+    (src/attention.py:149-281) and PairwiseModalityAttention (:284-424).
   * for a fixed upstream gradient G: d(sum(out * G)) w.r.t. inputs and params.
 
 Run:  python tests/golden/gen_golden.py [case1,case2,...]
@@ -31,8 +32,9 @@ HERE = Path(__file__).resolve().parent
 sys.path.insert(0, str(HERE))
 REF_SRC = Path("/root/reference/src")
 
-from cases import (CMA_CASES, HYBRID_CASES, cma_inputs, cma_state,  # noqa: E402
-                   hybrid_inputs, hybrid_state, pair_names)
+from cases import (CMA_CASES, HYBRID_CASES, PAIRWISE_CASES, TEMPORAL_CASES,  # noqa: E402
+                   cma_inputs, cma_state, hybrid_inputs, hybrid_state, pair_names,
+                   pairwise_inputs, pairwise_state, temporal_inputs)
 
 
 def _load_reference():
@@ -157,6 +159,46 @@ def gen_cma(ref_attention, case):
     return out
 
 
+def gen_temporal(ref_attention, case):
+    model = ref_attention.TemporalAttention(case.feature_dim, hidden_dim=case.hidden, num_heads=case.heads,
+                                            dropout=0.1)
+    sd = cma_state(case.feature_dim, case.feature_dim, case.hidden, case.seed)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    model.eval()
+    seq, mask, grad = temporal_inputs(case)
+    st = torch.from_numpy(seq).requires_grad_(True)
+    mt = torch.from_numpy(mask) if mask is not None else None
+    att, w = model(st, mt)
+    assert tuple(att.shape) == grad.shape, (tuple(att.shape), grad.shape)
+    (att * torch.from_numpy(grad)).sum().backward()
+    out = {"attended": att.detach().numpy(), "weights": w.detach().numpy(), "dsequence": st.grad.numpy()}
+    for name, p in model.named_parameters():
+        out[f"grad/{name}"] = p.grad.numpy()
+    return out
+
+
+def gen_pairwise(ref_attention, case):
+    model = ref_attention.PairwiseModalityAttention({m: case.dims[m] for m in case.names},
+                                                    hidden_dim=case.hidden, num_heads=case.heads, dropout=0.1)
+    for key in case.deleted:
+        del model.attention_layers[key]
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in pairwise_state(case).items()}, strict=True)
+    model.eval()
+    feats_np, mask_np, grads_np = pairwise_inputs(case)
+    feats = {m: torch.from_numpy(v).requires_grad_(True) for m, v in feats_np.items()}
+    attended, maps = model(feats, torch.from_numpy(mask_np))
+    sum(((attended[m] * torch.from_numpy(grads_np[m])).sum() for m in case.names)).backward()
+    out = {}
+    for m in case.names:
+        out[f"attended/{m}"] = attended[m].detach().numpy()
+        out[f"dx/{m}"] = feats[m].grad.numpy()
+    for k, w in maps.items():
+        out[f"attn/{k}"] = w.detach().numpy()
+    for name, p in model.named_parameters():
+        out[f"grad/{name}"] = p.grad.numpy() if p.grad is not None else np.zeros_like(p.detach().numpy())
+    return out
+
+
 def main():
     only = set(sys.argv[1].split(",")) if len(sys.argv) > 1 else None   # e.g. seq_c2_b3,seq_lean_hd64
     torch.set_float32_matmul_precision("highest")
@@ -168,12 +210,13 @@ def main():
         out = gen_hybrid(ref_fusion, case)
         np.savez_compressed(HERE / f"{case.name}.npz", **out)
         print(f"wrote {case.name}.npz ({sum(a.nbytes for a in out.values())} B raw)")
-    for case in CMA_CASES:
-        if only and case.name not in only:
-            continue
-        out = gen_cma(ref_attention, case)
-        np.savez_compressed(HERE / f"{case.name}.npz", **out)
-        print(f"wrote {case.name}.npz ({sum(a.nbytes for a in out.values())} B raw)")
+    for cases, gen in ((CMA_CASES, gen_cma), (TEMPORAL_CASES, gen_temporal), (PAIRWISE_CASES, gen_pairwise)):
+        for case in cases:
+            if only and case.name not in only:
+                continue
+            out = gen(ref_attention, case)
+            np.savez_compressed(HERE / f"{case.name}.npz", **out)
+            print(f"wrote {case.name}.npz ({sum(a.nbytes for a in out.values())} B raw)")
 
 
 if __name__ == "__main__":

@@ -10,7 +10,7 @@ import pytest
 import torch
 
 from _util import close, load_fixture, oracle_cma, oracle_hybrid, rel_err
-from cases import CMA_CASES, HYBRID_CASES
+from cases import CMA_CASES, HYBRID_CASES, TEMPORAL_CASES, cma_state, temporal_inputs
 
 TOL = 1e-5
 
@@ -62,3 +62,25 @@ def test_l1_zero_qk_grads():
     for k, v in fx.items():
         if k.startswith("grad/attention_modules") and ("query_proj" in k or "key_proj" in k):
             assert np.all(v == 0.0), k
+
+
+@pytest.mark.parametrize("case", TEMPORAL_CASES, ids=lambda c: c.name)
+def test_oracle_temporal_matches_reference(case):
+    """TemporalAttention = the CMA restatement with q = k = v and a per-key mask,
+    then the reference's post-mask broadcast (src/attention.py:233-248)."""
+    from oracle.hybrid_cpu import cma_forward
+    fx = load_fixture(case.name)
+    sd = cma_state(case.feature_dim, case.feature_dim, case.hidden, case.seed)
+    params = {k: torch.from_numpy(v) for k, v in sd.items()}
+    seq, mask, _ = temporal_inputs(case)
+    st = torch.from_numpy(seq)
+    km = None
+    if mask is not None:
+        m = torch.from_numpy(mask)
+        m = m.unsqueeze(0) if m.dim() == 1 else m
+        km = m.expand(case.batch, case.seq).contiguous()
+    att, w = cma_forward(params, "", st, st, st, case.heads, mask=km)
+    if mask is not None:
+        att = att * m.unsqueeze(1).unsqueeze(2).unsqueeze(-1)
+    assert rel_err(att, fx["attended"]) <= TOL
+    assert rel_err(w, fx["weights"]) <= TOL
