@@ -1039,10 +1039,13 @@ __global__ __launch_bounds__(NT) void attn_pool_bwd_dq_lean(const AttnArgs A) {
   const uint32_t kwa[4] = {kw.x, kw.y, kw.z, kw.w};
   float pr[NKT][16];
   float D = 0.f;
+  // software pipeline: the next key tile's S chain is issued before this tile's VALU work
+  f32x16 s_nx = dot_rows<HALF>(Ks + c * LS + h * HALF, qf, zero16());
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) {
     if (kt < nkt) {
-      const f32x16 s = dot_rows<HALF>(Ks + (kt * 32 + c) * LS + h * HALF, qf, zero16());
+      const f32x16 s = s_nx;
+      if (kt + 1 < nkt) s_nx = dot_rows<HALF>(Ks + ((kt + 1) * 32 + c) * LS + h * HALF, qf, zero16());
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const float4 gv = *reinterpret_cast<const float4*>(gk + kt * 32 + 8 * g + 4 * h);
@@ -1150,8 +1153,11 @@ __global__ __launch_bounds__(NT) void attn_pool_bwd_dk_lean(const AttnArgs A) {
       __syncthreads();
       if (!wave_active) continue;
       const int nqt = (min(QC, Lq - qbase) + 31) / 32;
+      // software pipeline: the next tile's S chain is issued before this tile's VALU work
+      f32x16 s_nx = dot_rows<HALF>(Qs + c * LS + h * HALF, kf, zero16());
       for (int qt = 0; qt < nqt; ++qt) {
-        const f32x16 s = dot_rows<HALF>(Qs + (qt * 32 + c) * LS + h * HALF, kf, zero16());
+        const f32x16 s = s_nx;
+        if (qt + 1 < nqt) s_nx = dot_rows<HALF>(Qs + ((qt + 1) * 32 + c) * LS + h * HALF, kf, zero16());
         float ds[16];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {

@@ -24,6 +24,7 @@
 // MFMA k-order: within each 8-deep k chunk j, lane half h feeds k = 8j+4h+s at
 // step s (the same permutation on A and B, so the contraction is unchanged).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "mmf_device.h"
@@ -75,6 +76,7 @@ __device__ __forceinline__ bool tile_ctx(const GemmGroup& G, TileCtx& t) {
 // +addm; relu; gate; rowscale; dropout (keep(site, i*N + j)).
 constexpr int CS = BN + 4;
 
+template <int PR = 64>   // rows per LDS pass (64 or 32)
 __device__ __forceinline__ void epilogue(const GemmGroup& G, const TileCtx& T, f32x16 (&acc)[2][2], float* cs,
                                          const RngSnap& rs, float p, float inv_keep, int wm, int wn, int h,
                                          int c) {
@@ -93,22 +95,24 @@ __device__ __forceinline__ void epilogue(const GemmGroup& G, const TileCtx& T, f
   float bias[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) bias[e] = (!partial && (epi & EPI_BIAS) && e < nv) ? T.biasb[j0 + e] : 0.f;
-  for (int pass = 0; pass < 2; ++pass) {
+  for (int pass = 0; pass < BM / PR; ++pass) {
     __syncthreads();
-    if (wm == pass) {
 #pragma unroll
-      for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < 2; ++a) {
+      const int rb = wm * 64 + a * 32 - pass * PR;    // this accumulator's first row in the pass
+      if (rb >= 0 && rb < PR) {
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) cs[(a * 32 + acc_row(r, h)) * CS + wn * 64 + b * 32 + c] = acc[a][b][r];
+          for (int r = 0; r < 16; ++r) cs[(rb + acc_row(r, h)) * CS + wn * 64 + b * 32 + c] = acc[a][b][r];
+      }
     }
     __syncthreads();
     if (nv <= 0) continue;
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
+    for (int it = 0; it < PR / 16; ++it) {
       const int lr = (t >> 4) + 16 * it;
-      const int i = T.i0 + pass * 64 + lr;
+      const int i = T.i0 + pass * PR + lr;
       if (i >= G.M) continue;
       const f32x4 lo = *reinterpret_cast<const f32x4*>(cs + lr * CS + cg);
       const f32x4 hi = *reinterpret_cast<const f32x4*>(cs + lr * CS + cg + 4);
@@ -159,26 +163,32 @@ __device__ __forceinline__ void epilogue(const GemmGroup& G, const TileCtx& T, f
 // wave-instructions of 1 KB (wave w issues 2).  Rows past `eext` and k past
 // `kend` are clamped to valid addresses; the k tail is zeroed afterwards
 // (zero_tail), the row tail only feeds outputs that are never stored.
-constexpr int DK = 16, NSTAGE = 3;
-constexpr int DTILE = BM * DK;           // floats per operand tile (8 KB)
-constexpr int DMA_PER_TILE = 4;          // glds instructions per wave per (A, B) tile pair
+// RK image [e][DK], 4*DK-byte rows; 16-B slots XOR-swizzled by the row's
+// position in its 256-B bank row so ds_read_b128 fragment reads are conflict
+// free.  KR image [DK][128], 512-B k-rows.  A wave-instruction moves 1 KB.
+template <int DK>
+__device__ __forceinline__ int swz(int row) {
+  constexpr int S = DK / 4;              // slots per row
+  constexpr int RB = 64 / DK;            // rows per 256-B bank row
+  return (row / RB) & (S - 1);
+}
 
-template <int MODE>
+template <int MODE, int DK>
 __device__ __forceinline__ void stage_tile(float* lds, const Operand& op, int64_t boff, int e0, int eext, int k0,
                                            int kend, int wave, int lane) {
+  constexpr int PER_WAVE = BM * DK / 256 / 4;   // 1-KB instructions per wave
+  constexpr int S = DK / 4;
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int ins = wave * 2 + u;
+  for (int u = 0; u < PER_WAVE; ++u) {
+    const int ins = wave * PER_WAVE + u;
     const float* src;
     if (MODE == MODE_RK) {
-      // [e][16] image, 64-B rows; 16-B slot XOR-swizzled by (row >> 2) & 3
-      const int row = ins * 16 + (lane >> 2);
-      const int slot = (lane & 3) ^ ((row >> 2) & 3);
+      const int row = ins * (64 / S) + lane / S;
+      const int slot = (lane % S) ^ swz<DK>(row);
       const int e = min(e0 + row, eext - 1);
       const int k = min(k0 + 4 * slot, kend - 4);
       src = op.ptr + boff + (int64_t)(e / op.row_div) * op.ld + k;
     } else {
-      // [16][128] image, 512-B k-rows
       const int kr = min(k0 + ins * 2 + (lane >> 5), kend - 1);
       const int e = min(e0 + 4 * (lane & 31), eext - 4);
       src = op.ptr + boff + (int64_t)(kr / op.row_div) * op.ld + e;
@@ -189,31 +199,28 @@ __device__ __forceinline__ void stage_tile(float* lds, const Operand& op, int64_
 }
 
 // Zero the k >= kv part of a staged tile (last tile of a contraction; kv % 4 == 0 for RK).
-template <int MODE>
+template <int MODE, int DK>
 __device__ __forceinline__ void zero_tail(float* lds, int kv) {
   const int t = threadIdx.x;
   if (MODE == MODE_RK) {
-    const int row = t >> 1;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int slot = 2 * (t & 1) + q;
+    constexpr int S = DK / 4;
+    for (int idx = t; idx < BM * S; idx += NT) {
+      const int row = idx / S, slot = idx % S;
       if (4 * slot >= kv)
-        *reinterpret_cast<f32x4*>(lds + row * DK + ((slot ^ ((row >> 2) & 3)) << 2)) = f32x4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f32x4*>(lds + row * DK + ((slot ^ swz<DK>(row)) << 2)) = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   } else {
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int idx = t + q * NT;                 // float4 index in the [16][128] image
+    for (int idx = t; idx < DK * BM / 4; idx += NT) {
       if (idx / (BM / 4) >= kv) *reinterpret_cast<f32x4*>(lds + idx * 4) = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
 }
 
 // Fragment of 4 consecutive MFMA k-steps (chunk j) for tile row/col e.
-template <int MODE>
+template <int MODE, int DK>
 __device__ __forceinline__ f32x4 frag(const float* lds, int e, int j, int h) {
   if (MODE == MODE_RK) {
-    const int slot = (2 * j + h) ^ ((e >> 2) & 3);
+    const int slot = (2 * j + h) ^ swz<DK>(e);
     return *reinterpret_cast<const f32x4*>(lds + e * DK + (slot << 2));
   } else {
     const float* p = lds + (8 * j + 4 * h) * BM + e;
@@ -230,8 +237,10 @@ __device__ __forceinline__ void lds_barrier() {
 // (source, k0) cursor over one tile's contraction
 struct KCursor { int si, k0, kend; };
 
-template <int AMODE, int BMODE>
-__global__ __launch_bounds__(NT, 3) void gemm_lds_kernel(const GemmArgs args) {
+template <int AMODE, int BMODE, int DK, int NSTAGE>
+__global__ __launch_bounds__(NT, (NSTAGE * DK <= 32 ? 4 : 2)) void gemm_lds_kernel(const GemmArgs args) {
+  constexpr int DTILE = BM * DK;                  // floats per operand tile
+  constexpr int DMA_PER_TILE = 2 * (BM * DK / 1024);  // glds per wave per (A, B) tile pair
   const GemmGroup& G = args.g[blockIdx.y];
   TileCtx T;
   if (!tile_ctx(G, T)) return;
@@ -239,7 +248,8 @@ __global__ __launch_bounds__(NT, 3) void gemm_lds_kernel(const GemmArgs args) {
 
   // one LDS object: NSTAGE x [A | B] tiles (also the epilogue image) + 128 floats for the row-sum combine
   __shared__ __attribute__((aligned(16))) float lds[NSTAGE * 2 * DTILE + BM];
-  static_assert(NSTAGE * 2 * DTILE >= 64 * CS, "epilogue image does not fit");
+  constexpr int PR = NSTAGE * 2 * DTILE >= 64 * CS ? 64 : 32;   // epilogue rows per LDS pass
+  static_assert(NSTAGE * 2 * DTILE >= PR * CS, "epilogue image does not fit");
 
   const int t = threadIdx.x;
   const int lane = t & 63, wave = t >> 6;
@@ -282,33 +292,47 @@ __global__ __launch_bounds__(NT, 3) void gemm_lds_kernel(const GemmArgs args) {
   auto stage = [&](int buf, const KCursor& k) {
     const GemmSrc& S = args.s[G.src_begin + k.si];
     float* At = lds + buf * 2 * DTILE;
-    stage_tile<AMODE>(At, S.a, offA, T.i0, G.M, k.k0, k.kend, wave, lane);
-    stage_tile<BMODE>(At + DTILE, S.b, offB, T.j0, G.N, k.k0, k.kend, wave, lane);
+    stage_tile<AMODE, DK>(At, S.a, offA, T.i0, G.M, k.k0, k.kend, wave, lane);
+    stage_tile<BMODE, DK>(At + DTILE, S.b, offB, T.j0, G.N, k.k0, k.kend, wave, lane);
   };
+  // wait until at most `ahead` tiles' DMAs are outstanding (vmcnt needs an immediate)
+  auto wait_tiles = [&](int ahead) {
+    if (ahead <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA_PER_TILE) : "memory");
+    else if (ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DMA_PER_TILE) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * DMA_PER_TILE) : "memory");
+  };
+  static_assert(NSTAGE >= 2 && NSTAGE <= 5, "ring depth");
 
   KCursor cur = first_from(0);
   if (cur.si < G.src_count) {
-    KCursor nx1 = advance(cur);
-    stage(0, cur);
-    if (nx1.si < G.src_count) stage(1, nx1);
-    int buf = 0;
+    // prologue: NSTAGE-1 tiles in flight; tile n always lives in buffer n % NSTAGE
+    KCursor iss = cur;
+    int nissued = 0;
+    for (int q = 0; q < NSTAGE - 1 && iss.si < G.src_count; ++q) {
+      stage(q, iss);
+      iss = advance(iss);
+      ++nissued;
+    }
+    int tile = 0, buf = 0;
     for (;;) {
-      // tile `cur` has landed (only nx1's DMAs may still be outstanding) and
-      // every wave is done reading the buffer that nx2 overwrites
-      if (nx1.si < G.src_count) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      static_assert(DMA_PER_TILE == 4, "vmcnt literal above");
+      // tile `tile` has landed once only the later tiles' DMAs are outstanding;
+      // the barrier also means every wave is done with the buffer restaged below
+      wait_tiles(nissued - tile - 1);
       lds_barrier();
       float* At = lds + buf * 2 * DTILE;
       float* Bt = At + DTILE;
       const int kv = cur.kend - cur.k0;
       if (kv < DK) {
-        zero_tail<AMODE>(At, kv);
-        zero_tail<BMODE>(Bt, kv);
+        zero_tail<AMODE, DK>(At, kv);
+        zero_tail<BMODE, DK>(Bt, kv);
         lds_barrier();
       }
-      const KCursor nx2 = advance(nx1);
-      if (nx2.si < G.src_count) stage(buf == 0 ? 2 : buf - 1, nx2);
+      if (iss.si < G.src_count) {
+        stage(nissued % NSTAGE, iss);
+        iss = advance(iss);
+        ++nissued;
+      }
       if (want_db) {
         // bias grad of a TN dW: row sums of A over this k-tile (thread: row t&127, k half t>>7)
         const int row = t & (BM - 1), kh = t >> 7;
@@ -316,16 +340,16 @@ __global__ __launch_bounds__(NT, 3) void gemm_lds_kernel(const GemmArgs args) {
         for (int q = 0; q < DK / 2; ++q) {
           const int kk = kh * (DK / 2) + q;
           dbsum += AMODE == MODE_KR ? At[kk * BM + row]
-                                    : At[row * DK + ((((kk >> 2) ^ ((row >> 2) & 3))) << 2) + (kk & 3)];
+                                    : At[row * DK + ((((kk >> 2) ^ swz<DK>(row))) << 2) + (kk & 3)];
         }
       }
 #pragma unroll
       for (int j = 0; j < DK / 8; ++j) {
         f32x4 af[2], bf[2];
 #pragma unroll
-        for (int a = 0; a < 2; ++a) af[a] = frag<AMODE>(At, wm * 64 + a * 32 + c, j, h);
+        for (int a = 0; a < 2; ++a) af[a] = frag<AMODE, DK>(At, wm * 64 + a * 32 + c, j, h);
 #pragma unroll
-        for (int b = 0; b < 2; ++b) bf[b] = frag<BMODE>(Bt, wn * 64 + b * 32 + c, j, h);
+        for (int b = 0; b < 2; ++b) bf[b] = frag<BMODE, DK>(Bt, wn * 64 + b * 32 + c, j, h);
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -333,9 +357,10 @@ __global__ __launch_bounds__(NT, 3) void gemm_lds_kernel(const GemmArgs args) {
 #pragma unroll
             for (int b = 0; b < 2; ++b) acc[a][b] = mfma32(af[a][s], bf[b][s], acc[a][b]);
       }
-      if (nx1.si >= G.src_count) break;
-      cur = nx1;
-      nx1 = nx2;
+      const KCursor nx = advance(cur);
+      if (nx.si >= G.src_count) break;
+      cur = nx;
+      ++tile;
       buf = buf == NSTAGE - 1 ? 0 : buf + 1;
     }
   }
@@ -348,7 +373,7 @@ __global__ __launch_bounds__(NT, 3) void gemm_lds_kernel(const GemmArgs args) {
     if (t < BM && T.i0 + t < G.M)
       T.part_db[(int64_t)T.split * G.M + T.i0 + t] = (dbsum + red[t]) * G.alpha;
   }
-  epilogue(G, T, acc, lds, rs, p, inv_keep, wm, wn, h, c);
+  epilogue<PR>(G, T, acc, lds, rs, p, inv_keep, wm, wn, h, c);
 }
 
 // ------------------------------------------------------------------ generic kernel
@@ -620,7 +645,7 @@ bool dma_ok(const Operand& op, int mode, int eext, int bstride, int nbatch) {
 bool job_fast(const GemmJob& J, int amode, int bmode) {
   const GemmGroup& g = J.g;
   const int nb = g.nbatch < 1 ? 1 : g.nbatch;
-  if ((g.epi & EPI_PARTIAL) && (g.kchunk % DK) != 0) return false;
+  if ((g.epi & EPI_PARTIAL) && (g.kchunk % 32) != 0) return false;
   for (int s = 0; s < J.nsrc; ++s) {
     const GemmSrc& src = J.src[s];
     if ((src.K % 4) != 0 || !dma_ok(src.a, amode, g.M, g.bs_a, nb) || !dma_ok(src.b, bmode, g.N, g.bs_b, nb))
@@ -664,6 +689,15 @@ hipError_t launch_gemm(const GemmJob* jobs, int njobs, int amode, int bmode, flo
     args.ngroups = ng;
     if (max_blocks > 0) {
       dim3 grid(max_blocks, ng);
+#define MMF_LAUNCH_CFG(DKV, NSV)                                                                  \
+      if (amode == MODE_RK && bmode == MODE_RK)                                                     \
+        hipLaunchKernelGGL((gemm_lds_kernel<MODE_RK, MODE_RK, DKV, NSV>), grid, dim3(NT), 0, st, args); \
+      else if (amode == MODE_RK && bmode == MODE_KR)                                                \
+        hipLaunchKernelGGL((gemm_lds_kernel<MODE_RK, MODE_KR, DKV, NSV>), grid, dim3(NT), 0, st, args); \
+      else if (amode == MODE_KR && bmode == MODE_KR)                                                \
+        hipLaunchKernelGGL((gemm_lds_kernel<MODE_KR, MODE_KR, DKV, NSV>), grid, dim3(NT), 0, st, args); \
+      else                                                                                          \
+        hipLaunchKernelGGL((gemm_lds_kernel<MODE_KR, MODE_RK, DKV, NSV>), grid, dim3(NT), 0, st, args);
 #define MMF_LAUNCH(KERNEL)                                                                 \
       if (amode == MODE_RK && bmode == MODE_RK)                                            \
         hipLaunchKernelGGL((KERNEL<MODE_RK, MODE_RK>), grid, dim3(NT), 0, st, args);       \
@@ -674,11 +708,14 @@ hipError_t launch_gemm(const GemmJob* jobs, int njobs, int amode, int bmode, flo
       else                                                                                 \
         hipLaunchKernelGGL((KERNEL<MODE_KR, MODE_RK>), grid, dim3(NT), 0, st, args);
       if (fast) {
-        MMF_LAUNCH(gemm_lds_kernel)
+        // (DK, ring depth) = (16, 3): measured best of (16|32) x (2|3|4) at C2
+        // (profiles/tune_gemm_cfg.sh)
+        MMF_LAUNCH_CFG(16, 3)
       } else {
         MMF_LAUNCH(gemm_generic_kernel)
       }
 #undef MMF_LAUNCH
+#undef MMF_LAUNCH_CFG
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
