@@ -216,6 +216,18 @@ CMA_CASES: List[CMACase] = [
 ]
 
 
+# PAMAP2 logits / ECE parity (tests/golden/gen_pamap2.py): the config/base.yaml
+# model on the four PAMAP2 modalities (dataset.modalities, model.output_dim 128,
+# model.hidden_dim 256, model.num_heads 4, dataset.num_classes 25, chunk 1024).
+PAMAP2_MODALITIES = ["imu_hand", "imu_chest", "imu_ankle", "heart_rate"]
+PAMAP2_OUT_DIM = 128
+PAMAP2_HIDDEN = 256
+PAMAP2_HEADS = 4
+PAMAP2_CLASSES = 25
+PAMAP2_CHUNK = 1024
+PAMAP2_SEED = 81
+
+
 def case_by_name(name: str):
     for c in HYBRID_CASES + CMA_CASES:
         if c.name == name:
