@@ -31,68 +31,13 @@ sys.path.insert(0, ROOT)
 
 METRIC = "HybridFusion fwd+bwd samples/sec at 1/2/4/8 MI355X; CPU-ref parity"
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 
 WORKLOADS = {
     # name: (M, B per GPU, L (0 => 2-D reference semantics), D, H, heads, C)
     "c2": (3, 256, 128, 128, 128, 4, 5),
     "c2_l1": (3, 256, 0, 128, 128, 4, 5),
 }
-
-
-def pooled_plan(L, heads):
-    """csrc/hybrid.hip use_pool(): key lengths <= 128 and <= 8 heads."""
-    return max(L, 1) <= 128 and heads <= 8
-
-
-def stage_flops(M, B, L, D, H, heads, C):
-    """Algorithmic FLOPs of each launch group (no recompute counted)."""
-    Le = max(L, 1)
-    P = M * (M - 1)
-    rows = B * Le
-    if pooled_plan(L, heads):
-        # pooled-output plan (DESIGN.md): no V / O / attended (B, L, H) tensors
-        return {
-            "fwd.proj_gemm": 2 * rows * D * H * M,
-            "fwd.qkv_gemm": 2 * 2 * rows * H * H * P,
-            "fwd.attn": 2 * B * Le * Le * H * P,             # S = Q K^T (+ softmax, column mean)
-            "fwd.pool_u": 2 * B * heads * Le * H * P,         # U_h = pbar_h P_k
-            "fwd.vbar_gemm": 2 * B * H * H * P,
-            "fwd.out_gemm": 2 * B * H * H * P,
-            "fwd.cls1_gemm": 2 * B * H * H,
-            "fwd.cls2_gemm": 2 * B * H * C,
-            "fwd.tail": 2 * 2 * B * H * H * P + 2 * B * H * H + 2 * B * H * C,   # fused V/O/head/classifier
-            "bwd.tail": 2 * B * C * H + 2 * B * H * H + 2 * 2 * B * H * H * P,
-            "bwd.cls_dz1_gemm": 2 * B * C * H,
-            "bwd.cls_dfused_gemm": 2 * B * H * H,
-            "bwd.out_dO_gemm": 2 * B * H * H * P,
-            "bwd.du_gemm": 2 * B * H * H * P,
-            "bwd.pool_dpbar": 2 * B * heads * Le * H * P,
-            "bwd.attn_dq": 2 * B * Le * Le * H * P,          # dQ = dS K (S recompute not counted)
-            "bwd.attn_dk": 2 * B * Le * Le * H * P,          # dK = dS^T Q
-            "bwd.pool_e": 2 * B * heads * Le * H * P,
-            "bwd.dZ_gemm": 2 * rows * H * H * 2 * P,         # dQ W_q + dK W_k into every modality
-            "bwd.dx_gemm": 2 * rows * H * D * M,
-            "bwd.wgrad_gemm": 2 * rows * H * D * M + 2 * 2 * rows * H * H * P + 2 * 2 * B * H * H * P
-                              + 2 * B * H * (H + C),
-        }
-    f = {
-        "fwd.proj_gemm": 2 * rows * D * H * M,
-        "fwd.qkv_gemm": 3 * 2 * rows * H * H * P,
-        "fwd.attn": 4 * B * Le * Le * H * P,
-        "fwd.out_gemm": 2 * rows * H * H * P,
-        "fwd.cls1_gemm": 2 * B * H * H,
-        "fwd.cls2_gemm": 2 * B * H * C,
-        "bwd.cls_dz1_gemm": 2 * B * C * H,
-        "bwd.cls_dfused_gemm": 2 * B * H * H,
-        "bwd.out_dO_gemm": 2 * rows * H * H * P,
-        "bwd.attn_dkv": 6 * B * Le * Le * H * P,     # dP, dV, dK
-        "bwd.attn_dq": 2 * B * Le * Le * H * P,      # dQ
-        "bwd.dZ_gemm": 3 * 2 * rows * H * H * P,     # dP_m from dQ, dK, dV
-        "bwd.dx_gemm": 2 * rows * H * D * M,
-        # dW for proj (M), q/k/v/out (4P), classifier (2)
-        "bwd.wgrad_gemm": 2 * rows * H * D * M + 4 * 2 * rows * H * H * P + 2 * B * H * (H + C),
-    }
-    return f
 
 
 def total_step_flops(M, B, L, D, H, heads, C):
@@ -106,6 +51,64 @@ def total_step_flops(M, B, L, D, H, heads, C):
         fwd += P * 4 * B * H * H      # reference semantics: Q/K dead at L=1
     fwd += 2 * B * H * H + 2 * B * H * C + 4 * M * B * H + B * Le * H * M
     return 3 * fwd
+
+
+def kernel_table(launches, steps):
+    """Per kernel name: time per step, average launch duration and the roofline
+    of its launches (algorithmic FLOPs / bytes from the library's per-launch
+    records over the measured durations), sorted by time per step."""
+    acc = {}
+    for _stage, kname, ms, flops, nbytes in launches:
+        a = acc.setdefault(kname, [0.0, 0, 0.0, 0.0])
+        a[0] += ms
+        a[1] += 1
+        a[2] += flops
+        a[3] += nbytes
+    out = {}
+    for kname, (ms, n, flops, nbytes) in sorted(acc.items(), key=lambda kv: -kv[1][0]):
+        sec = ms * 1e-3
+        t_f = flops / (FP32_MFMA_PEAK_TFLOPS * 1e12)
+        t_b = nbytes / (HBM_PEAK_GBS * 1e9)
+        if t_f >= t_b:
+            bound, ach, peak, unit = "mfma", flops / sec / 1e12 if sec else 0.0, FP32_MFMA_PEAK_TFLOPS, "TFLOP/s"
+        else:
+            bound, ach, peak, unit = "hbm", nbytes / sec / 1e9 if sec else 0.0, HBM_PEAK_GBS, "GB/s"
+        out[kname] = {
+            "ms_per_step": round(ms / steps, 4), "launches_per_step": round(n / steps, 2),
+            "avg_launch_ms": round(ms / n, 5), "bound": bound, "achieved": round(ach, 2), "peak": peak,
+            "unit": unit, "frac": round(ach / peak, 4),
+            "flops_per_launch": flops / n, "bytes_per_launch": nbytes / n,
+        }
+    return out
+
+
+def pmc_traffic():
+    """HBM bytes per launch by kernel name from the committed PMC summary
+    (profiles/pmc_traffic.py output: FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE,
+    KiB -> bytes, averaged over the dispatches of an eager run of this bench)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return {}, None
+    with open(path) as f:
+        d = json.load(f)
+    return d.get("kernels", {}), d.get("source")
+
+
+def dominant_roofline(kernels):
+    """Roofline of the kernel with the most time per step."""
+    kname = next(iter(kernels))
+    k = kernels[kname]
+    traffic, src = pmc_traffic()
+    t = traffic.get(kname, {}).get("hbm_bytes_per_launch")
+    per_launch = k["flops_per_launch"] if k["bound"] == "mfma" else k["bytes_per_launch"]
+    return {
+        "bound": k["bound"], "achieved": k["achieved"], "peak": k["peak"], "unit": k["unit"],
+        "frac": k["frac"], "traffic": round(t) if t is not None else None,
+        "kernel": kname, "avg_launch_ms": k["avg_launch_ms"], "launches_per_step": k["launches_per_step"],
+        "algorithmic_per_launch": round(per_launch),
+        "algorithmic_bytes_per_launch": round(k["bytes_per_launch"]),
+        "traffic_source": src if t is not None else None,
+    }
 
 
 def make_inputs(M, B, L, D, C, seed, device):
@@ -179,18 +182,20 @@ def main():
     feats, mask, labels = make_inputs(M, B, L, D, C, 42 + rank, dev)
     trainer = HybridTrainStep(model, feats, mask, labels, process_group=pg)
 
-    # kernel-level timing (eager, hipEvents around each launch group on the launch stream)
+    # kernel-level timing (eager): hipEvents around each launch group and each
+    # kernel launch, on the launch stream (mmf_profile_begin/end)
     trainer.forward_backward()
     torch.cuda.synchronize(dev)
     mmf_native.profile_begin()
     for _ in range(args.profile_steps):
         trainer.forward_backward()
-    stages = mmf_native.profile_end()
+    stages, launches = mmf_native.profile_end()
     per_stage = {}
     for name, ms in stages:
         t, n = per_stage.get(name, (0.0, 0))
         per_stage[name] = (t + ms, n + 1)
     avg_ms = {k: t / n for k, (t, n) in per_stage.items()}
+    kernels = kernel_table(launches, args.profile_steps)
 
     if not args.no_graph:
         trainer.capture()
@@ -216,17 +221,7 @@ def main():
     loss = float(trainer.loss.item())
 
     if rank == 0:
-        fl = stage_flops(M, B, L, D, H, heads, C)
-        dom = max(avg_ms, key=lambda k: avg_ms[k])
-        dom_flops = fl.get(dom, 0)
-        achieved = dom_flops / (avg_ms[dom] * 1e-3) / 1e12 if dom_flops else None
-        roofline = {
-            "bound": "mfma", "kernel": dom, "achieved": round(achieved, 2) if achieved else None,
-            "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4) if achieved else None,
-            "traffic": None, "avg_launch_ms": round(avg_ms[dom], 4),
-            "algorithmic_gflop_per_launch": round(dom_flops / 1e9, 3),
-        }
+        roofline = dominant_roofline(kernels)
         step_fl = total_step_flops(M, B, L, D, H, heads, C)
         cpu = None
         if world == 1 and not args.skip_cpu:
@@ -245,7 +240,12 @@ def main():
             "cpu_baseline": cpu,
             "step_tflops_algorithmic": round(step_fl / (ms_per_step * 1e-3) / 1e12, 3),
             "step_gflop_algorithmic": round(step_fl / 1e9, 2),
+            "step_gflop_executed_plan": round(sum(v["flops_per_launch"] * v["launches_per_step"]
+                                                  for v in kernels.values()) / 1e9, 2),
             "stage_ms": {k: round(v, 4) for k, v in sorted(avg_ms.items(), key=lambda kv: -kv[1])},
+            "kernels": {k: {kk: v[kk] for kk in ("ms_per_step", "launches_per_step", "avg_launch_ms",
+                                                 "bound", "achieved", "unit", "frac")}
+                        for k, v in list(kernels.items())[:12]},
             "loss": round(loss, 5),
         }
         print(json.dumps(out), flush=True)

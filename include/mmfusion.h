@@ -175,11 +175,16 @@ int mmf_adamw_step(int64_t n, float* param, const float* grad, float* exp_avg, f
                    int64_t* step_dev, float lr, float beta1, float beta2, float eps,
                    float weight_decay, float grad_scale, void* stream);
 
-/* Per-launch-group timing for the benchmark: between begin and end every
- * launch group of the entry points above is bracketed by hipEvents on its
- * stream; end() synchronises those events and writes "stage_name ms\n" lines
- * into out (truncated to cap) and returns the bytes needed.  Eager use only
- * (not under graph capture). */
+/* Timing for the benchmark: between begin and end every launch group AND
+ * every kernel launch of the entry points above is bracketed by hipEvents on
+ * its stream.  end() synchronises those events and writes tab-separated lines
+ * into out (truncated to cap), returning the bytes needed:
+ *   "S <stage> <ms>"                            per launch group
+ *   "L <stage> <kernel> <ms> <flops> <bytes>"   per kernel launch, with the
+ *                                               launch's algorithmic FLOPs and
+ *                                               HBM bytes (no recompute).
+ * Kernel names are rocprofv3's minus the "mmf::(anonymous namespace)::" prefix.
+ * Eager use only (not under graph capture). */
 void mmf_profile_begin(void);
 size_t mmf_profile_end(char* out, size_t cap);
 

@@ -1247,6 +1247,36 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
     a.nblk = (int)maxblk;
     if (maxblk <= 0) continue;
     dim3 grid((unsigned)maxblk, n);
+    // algorithmic work of this launch (no S recompute counted)
+    double fl = 0.0, by = 0.0;
+    const double H = (double)heads * hd;
+    for (int i = 0; i < n; ++i) {
+      const double lq = a.p[i].Lq, lk = a.p[i].Lk, bq = (double)B * lq * H, bk = (double)B * lk * H;
+      const double qk = 2.0 * B * lq * lk * H;   // one (B, h, Lq, Lk, hd) contraction
+      switch (kind) {
+        case Kind::Fwd: fl += 2 * qk; by += 4 * (2 * bq + 2 * bk); break;               // Q K V -> O
+        case Kind::Probs: fl += 2 * qk; by += 4 * (2 * bq + 2 * bk + B * heads * lq * lk); break;
+        case Kind::Prep: fl += 2.0 * bq; by += 4 * 2 * bq; break;                         // dO, O -> D
+        case Kind::Dkv: fl += 3 * qk; by += 4 * (3 * bq + 4 * bk); break;               // Q K V dO -> dK dV
+        case Kind::Dq: fl += qk; by += 4 * (3 * bq + 2 * bk); break;                    // Q K V dO -> dQ
+        case Kind::PoolFwd: fl += qk; by += 4 * (bq + bk); break;                         // Q K -> lse, pbar
+        case Kind::PoolDq: fl += qk; by += 4 * (2 * bq + bk); break;                      // Q K -> dQ
+        case Kind::PoolDk: fl += qk; by += 4 * (bq + 2 * bk); break;                      // Q K -> dK
+      }
+    }
+    static const char* const kNames[8][4] = {
+        {"attn_fwd_kernel<32, 0>", "attn_fwd_kernel<64, 0>", "attn_fwd_kernel<32, 0>", "attn_fwd_kernel<64, 0>"},
+        {"attn_fwd_kernel<32, 1>", "attn_fwd_kernel<64, 1>", "attn_fwd_kernel<32, 1>", "attn_fwd_kernel<64, 1>"},
+        {"attn_bwd_prep_kernel", "attn_bwd_prep_kernel", "attn_bwd_prep_vec_kernel", "attn_bwd_prep_vec_kernel"},
+        {"attn_bwd_dkv_kernel<32>", "attn_bwd_dkv_kernel<64>", "attn_bwd_dkv_kernel<32>", "attn_bwd_dkv_kernel<64>"},
+        {"attn_bwd_dq_kernel<32>", "attn_bwd_dq_kernel<64>", "attn_bwd_dq_kernel<32>", "attn_bwd_dq_kernel<64>"},
+        {"attn_pool_fwd_kernel<32>", "attn_pool_fwd_kernel<64>", "attn_pool_fwd_lean<32>", "attn_pool_fwd_lean<64>"},
+        {"attn_pool_bwd_dq_kernel<32>", "attn_pool_bwd_dq_kernel<64>", "attn_pool_bwd_dq_lean<32>",
+         "attn_pool_bwd_dq_lean<64>"},
+        {"attn_pool_bwd_dk_kernel<32>", "attn_pool_bwd_dk_kernel<64>", "attn_pool_bwd_dk_lean<32>",
+         "attn_pool_bwd_dk_lean<64>"}};
+    const bool alt = kind == Kind::Prep ? prep_vec : lean;
+    ProfLaunch prof_(st, kNames[(int)kind][(alt ? 2 : 0) + (small ? 0 : 1)], fl, by);
     switch (kind) {
       case Kind::Fwd:
         if (small) hipLaunchKernelGGL((attn_fwd_kernel<32, 0>), grid, dim3(NT), 0, st, a);

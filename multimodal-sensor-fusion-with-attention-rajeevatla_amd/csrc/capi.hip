@@ -85,6 +85,24 @@ AttnPair cma_pair(const mmf_cma_desc* d, const CmaSaved& s, const float* mask) {
 
 }  // namespace
 
+namespace mmf {
+
+void* prof_launch_begin(hipStream_t st) {
+  if (!g_prof.on) return nullptr;
+  hipEvent_t a = g_prof.ev();
+  if (!a || hipEventRecord(a, st) != hipSuccess) return nullptr;
+  return (void*)a;
+}
+
+void prof_launch_end(void* tok, hipStream_t st, const char* kernel, double flops, double bytes) {
+  if (!tok || !g_prof.on) return;
+  hipEvent_t b = g_prof.ev();
+  if (!b || hipEventRecord(b, st) != hipSuccess) return;
+  g_prof.launches.push_back({g_prof.cur_stage, kernel, flops, bytes, (hipEvent_t)tok, b});
+}
+
+}  // namespace mmf
+
 extern "C" {
 
 const char* mmf_last_error(void) { return g_err.c_str(); }
@@ -92,23 +110,38 @@ const char* mmf_version(void) { return "mmfusion 0.2 (gfx950, fp32 MFMA, pooled 
 
 void mmf_profile_begin(void) {
   g_prof.on = true;
+  g_prof.cur_stage = "";
   g_prof.recs.clear();
+  g_prof.launches.clear();
   g_prof.next = 0;
 }
 
-// Ends profiling: waits for the recorded events and writes "name ms\n" lines
-// (one per launch group, in launch order) into out.  Returns the bytes needed.
+// Ends profiling: waits for the recorded events and writes tab-separated lines
+// into out, in launch order:
+//   "S <stage> <ms>"                              one per launch group
+//   "L <stage> <kernel> <ms> <flops> <bytes>"     one per kernel launch
+// (flops / bytes: the launch's algorithmic work, mmf_internal.h ProfLaunch).
+// Returns the bytes needed.
 size_t mmf_profile_end(char* out, size_t cap) {
   std::string s;
+  char line[320];
   for (const ProfRec& r : g_prof.recs) {
     float ms = 0.f;
     if (hipEventSynchronize(r.b) == hipSuccess) (void)hipEventElapsedTime(&ms, r.a, r.b);
-    char line[160];
-    snprintf(line, sizeof(line), "%s %.6f\n", r.name, (double)ms);
+    snprintf(line, sizeof(line), "S\t%s\t%.6f\n", r.name, (double)ms);
+    s += line;
+  }
+  for (const LaunchRec& r : g_prof.launches) {
+    float ms = 0.f;
+    if (hipEventSynchronize(r.b) == hipSuccess) (void)hipEventElapsedTime(&ms, r.a, r.b);
+    snprintf(line, sizeof(line), "L\t%s\t%s\t%.6f\t%.6e\t%.6e\n", r.stage, r.kernel, (double)ms, r.flops,
+             r.bytes);
     s += line;
   }
   g_prof.on = false;
+  g_prof.cur_stage = "";
   g_prof.recs.clear();
+  g_prof.launches.clear();
   g_prof.next = 0;
   if (out && cap) {
     const size_t n = s.size() < cap - 1 ? s.size() : cap - 1;

@@ -18,9 +18,12 @@ int fail(int code, const char* fmt, ...);
 
 // ---------------------------------------------------------------- profiling
 struct ProfRec { const char* name; hipEvent_t a, b; };
+struct LaunchRec { const char* stage; const char* kernel; double flops, bytes; hipEvent_t a, b; };
 struct Prof {
   bool on = false;
+  const char* cur_stage = "";
   std::vector<ProfRec> recs;
+  std::vector<LaunchRec> launches;
   std::vector<hipEvent_t> pool;
   size_t next = 0;
   hipEvent_t ev() {
@@ -39,13 +42,17 @@ struct Stage {
   const char* name;
   hipStream_t st;
   hipEvent_t a = nullptr;
+  const char* outer = nullptr;
   Stage(const char* n, hipStream_t s) : name(n), st(s) {
     if (g_prof.on) {
+      outer = g_prof.cur_stage;
+      g_prof.cur_stage = n;
       a = g_prof.ev();
       if (a) (void)hipEventRecord(a, st);
     }
   }
   ~Stage() {
+    if (outer) g_prof.cur_stage = outer;
     if (g_prof.on && a) {
       hipEvent_t b = g_prof.ev();
       if (b) {

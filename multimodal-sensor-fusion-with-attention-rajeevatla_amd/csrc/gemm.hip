@@ -689,6 +689,21 @@ hipError_t launch_gemm(const GemmJob* jobs, int njobs, int amode, int bmode, flo
     args.ngroups = ng;
     if (max_blocks > 0) {
       dim3 grid(max_blocks, ng);
+      double fl = 0.0, by = 0.0;
+      for (int gi = 0; gi < ng; ++gi) {
+        const GemmGroup& g = args.g[gi];
+        for (int si = g.src_begin; si < g.src_begin + g.src_count; ++si) {
+          fl += 2.0 * g.M * g.N * args.s[si].K * g.nbatch;
+          by += 4.0 * ((double)g.M + g.N) * args.s[si].K * g.nbatch;
+        }
+        by += 4.0 * g.M * g.N * g.nbatch;
+      }
+      static const char* const kLdsName[4] = {"gemm_lds_kernel<0, 0, 16, 3>", "gemm_lds_kernel<0, 1, 16, 3>",
+                                              "gemm_lds_kernel<1, 0, 16, 3>", "gemm_lds_kernel<1, 1, 16, 3>"};
+      static const char* const kGenName[4] = {"gemm_generic_kernel<0, 0>", "gemm_generic_kernel<0, 1>",
+                                              "gemm_generic_kernel<1, 0>", "gemm_generic_kernel<1, 1>"};
+      const int flavour = (amode == MODE_KR ? 2 : 0) + (bmode == MODE_KR ? 1 : 0);
+      ProfLaunch prof_(st, fast ? kLdsName[flavour] : kGenName[flavour], fl, by);
 #define MMF_LAUNCH_CFG(DKV, NSV)                                                                  \
       if (amode == MODE_RK && bmode == MODE_RK)                                                     \
         hipLaunchKernelGGL((gemm_lds_kernel<MODE_RK, MODE_RK, DKV, NSV>), grid, dim3(NT), 0, st, args); \
@@ -743,6 +758,12 @@ hipError_t launch_reduce(const ReduceJob* jobs, int njobs, hipStream_t st) {
     int blocks = (int)((maxmn / 4 + 63) / 64);
     if (blocks < 1) blocks = 1;
     if (blocks > 4096) blocks = 4096;
+    double by = 0.0;   // slabs (+ bias-row slabs) read once, sums written once
+    for (int i = 0; i < n; ++i) {
+      const ReduceJob& r = a.j[i];
+      by += 4.0 * r.nbatch * ((double)r.nsplit + 1) * r.M * ((double)r.N + (r.part_db ? 1 : 0));
+    }
+    ProfLaunch prof_(st, "partial_reduce_kernel", 0.0, by);
     hipLaunchKernelGGL(partial_reduce_kernel, dim3(blocks, n, maxbatch), dim3(256), 0, st, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -759,6 +780,9 @@ hipError_t launch_mask_dropout(MaskDropArgs a, hipStream_t st) {
     maxblk = std::max<int64_t>(maxblk, (J.rows * J.D + 7) / 8);
   }
   const int grid = (int)std::min<int64_t>((maxblk + 255) / 256, 2048);
+  double by = 0.0;
+  for (int m = 0; m < a.n; ++m) by += 8.0 * a.j[m].rows * a.j[m].D;   // read x, write x'
+  ProfLaunch prof_(st, "mask_dropout_rows_kernel", 0.0, by);
   hipLaunchKernelGGL(mask_dropout_rows_kernel, dim3(grid, a.n), dim3(256), 0, st, a);
   return hipGetLastError();
 }

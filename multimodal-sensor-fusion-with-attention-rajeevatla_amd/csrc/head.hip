@@ -275,12 +275,14 @@ __global__ void step_incr_kernel(int64_t* step) {
 
 hipError_t launch_head_fwd(const HeadArgs& a, hipStream_t st) {
   if (a.H % 4 != 0 || a.H > HEAD_MAX_H || a.H < 4 || a.M > 8) return hipErrorInvalidValue;
+  ProfLaunch prof_(st, "head_fwd_kernel", 0.0, 0.0);
   hipLaunchKernelGGL(head_fwd_kernel, dim3(a.B), dim3(NT), 0, st, a);
   return hipGetLastError();
 }
 
 hipError_t launch_head_bwd(const HeadArgs& a, hipStream_t st) {
   if (a.M > 8) return hipErrorInvalidValue;
+  ProfLaunch prof_(st, "head_bwd_kernel", 0.0, 0.0);
   hipLaunchKernelGGL(head_bwd_kernel, dim3(a.B), dim3(NT), 0, st, a);
   return hipGetLastError();
 }
@@ -292,11 +294,13 @@ hipError_t launch_gate_wgrad(int B, int M, int H, const float* dscore, const flo
   a.B = B; a.M = M; a.H = H; a.dscore = dscore; a.pooled = pooled;
   for (int m = 0; m < M; ++m) { a.dgw[m] = dgw[m]; a.dgb[m] = dgb[m]; }
   const int n = M * (H + 1);
+  ProfLaunch prof_(st, "gate_wgrad_kernel", 2.0 * B * M * H, 4.0 * B * M * (H + 1));
   hipLaunchKernelGGL(gate_wgrad_kernel, dim3((n + NT - 1) / NT), dim3(NT), 0, st, a);
   return hipGetLastError();
 }
 
 hipError_t launch_rng_snapshot(const uint64_t* state, RngSnap* snap, hipStream_t st) {
+  ProfLaunch prof_(st, "rng_snapshot_kernel", 0.0, 32.0);
   hipLaunchKernelGGL(rng_snapshot_kernel, dim3(1), dim3(64), 0, st, const_cast<uint64_t*>(state), snap);
   return hipGetLastError();
 }
@@ -304,6 +308,7 @@ hipError_t launch_rng_snapshot(const uint64_t* state, RngSnap* snap, hipStream_t
 hipError_t launch_cross_entropy(int B, int C, const float* logits, const int64_t* labels,
                                 float smoothing, float grad_scale, float* loss, float* dlogits,
                                 hipStream_t st) {
+  ProfLaunch prof_(st, "cross_entropy_kernel", 0.0, 8.0 * B * C + 8.0 * B);
   hipLaunchKernelGGL(cross_entropy_kernel, dim3(1), dim3(NT), 0, st, B, C, logits, labels, smoothing,
                      grad_scale, loss, dlogits);
   return hipGetLastError();
@@ -315,6 +320,7 @@ hipError_t launch_adamw(int64_t n, float* p, const float* g, float* m, float* v,
   int64_t blocks = (n + NT - 1) / NT;
   if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
+  ProfLaunch prof_(st, "adamw_kernel", 0.0, 28.0 * n);   // p m v read+write, g read
   hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(NT), 0, st, n, p, g, m, v, step, lr, b1,
                      b2, eps, wd, gscale);
   hipError_t e = hipGetLastError();

@@ -14,6 +14,29 @@ namespace mmf {
 // ---------------------------------------------------------------------------
 struct RngSnap { uint64_t seed; uint64_t offset; };
 
+// ---------------------------------------------------------------------------
+// Per-launch profiling (capi.hip).  While mmf_profile_begin() is active, every
+// kernel launch of the library is bracketed by two hipEvents on its stream and
+// tagged with the kernel's name (as rocprofv3 prints it, minus the namespace)
+// and its ALGORITHMIC work: FLOPs of the math it implements (no recompute) and
+// the bytes a perfect-reuse kernel would move to/from HBM.  Inactive, a launch
+// pays one branch.  `kernel` must point to static storage.
+// ---------------------------------------------------------------------------
+void* prof_launch_begin(hipStream_t st);
+void prof_launch_end(void* tok, hipStream_t st, const char* kernel, double flops, double bytes);
+struct ProfLaunch {
+  hipStream_t st;
+  const char* kernel;
+  double flops, bytes;
+  void* tok;
+  ProfLaunch(hipStream_t s, const char* k, double f, double b) : st(s), kernel(k), flops(f), bytes(b) {
+    tok = prof_launch_begin(s);
+  }
+  ~ProfLaunch() { prof_launch_end(tok, st, kernel, flops, bytes); }
+  ProfLaunch(const ProfLaunch&) = delete;
+  ProfLaunch& operator=(const ProfLaunch&) = delete;
+};
+
 enum : uint32_t {
   SITE_IN = 0x100,     // + m : input dropout on X_m*mask  (src/fusion.py:373)
   SITE_PROJ = 0x200,   // + m : projections[m] Dropout     (src/fusion.py:291-298)

@@ -170,6 +170,12 @@ hipError_t launch_pool(bool fwd, const PoolPair* pairs, int npairs, int B, int h
     }
     a.npairs = n;
     a.B = B; a.heads = heads; a.hd = hd; a.H = H;
+    double fl = 0.0, by = 0.0;   // U_h = pbar_h P_k  /  dpbar = P_k . dU_h: one pass over P_k
+    for (int i = 0; i < n; ++i) {
+      fl += 2.0 * B * heads * a.p[i].Lk * H;
+      by += 4.0 * B * ((double)a.p[i].Lk * H + heads * (a.p[i].Lk + H));
+    }
+    ProfLaunch prof_(st, fwd ? "pool_u_kernel" : "pool_dpbar_kernel", fl, by);
     if (fwd) {
       hipLaunchKernelGGL(pool_u_kernel, dim3(B, n), dim3(NT), 0, st, a);
     } else {
@@ -207,6 +213,12 @@ hipError_t launch_pool_e(const PoolEMod* mods, int nmods, int B, int heads, int 
     const int nb = a.blocks_per_b[i] * B;
     if (nb > maxb) maxb = nb;
   }
+  double fl = 0.0, by = 0.0;   // E_m = c/L + sum_s pbar_s^T dU_s, written once
+  for (int i = 0; i < nmods; ++i) {
+    fl += 2.0 * B * mods[i].nsrc * heads * mods[i].L * H;
+    by += 4.0 * B * ((double)mods[i].L * H + mods[i].nsrc * heads * (mods[i].L + H) + H);
+  }
+  ProfLaunch prof_(st, "pool_e_kernel", fl, by);
   hipLaunchKernelGGL(pool_e_kernel, dim3(maxb, nmods), dim3(NT), 0, st, a);
   return hipGetLastError();
 }

@@ -451,21 +451,37 @@ hipError_t launch_tail_fwd(const TailArgs& a, hipStream_t st) {
   if (!tail_supported(a.M, a.H, a.C, a.heads, a.hd, a.npairs)) return hipErrorInvalidValue;
   for (int g = 0; g < a.npairs; ++g)
     if (a.p[g].Lk > 128) return hipErrorInvalidValue;
+  const double B = a.B, H = a.H;
   if (a.npairs) {
+    // per pair: Vbar = U W_v^T (+ r b_v), Obar = Vbar W_o^T + b_o; weights read once
+    ProfLaunch prof_(st, "tail_pair_fwd_kernel", 4.0 * B * H * H * a.npairs,
+                     4.0 * a.npairs * (2 * H * H + B * (a.heads * H + 2 * H)));
     hipLaunchKernelGGL(tail_pair_fwd_kernel, dim3(a.B, a.npairs), dim3(NT), 0, st, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
+  // pooling, gating, adaptive weights, weighted sum, classifier
+  ProfLaunch prof_(st, "tail_head_fwd_kernel", 2.0 * B * H * (H + a.C) + 4.0 * a.M * B * H,
+                   4.0 * (H * (H + a.C) + B * (a.M * H + a.C)));
   hipLaunchKernelGGL(tail_head_fwd_kernel, dim3(a.B), dim3(NT), 0, st, a);
   return hipGetLastError();
 }
 
 hipError_t launch_tail_bwd(const TailArgs& a, hipStream_t st) {
   if (!tail_supported(a.M, a.H, a.C, a.heads, a.hd, a.npairs)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(tail_head_bwd_kernel, dim3(a.B), dim3(NT), 0, st, a);
+  const double B = a.B, H = a.H;
+  {
+    ProfLaunch prof_(st, "tail_head_bwd_kernel", 2.0 * B * H * (H + a.C) + 4.0 * a.M * B * H,
+                     4.0 * (H * (H + a.C) + B * (a.M * H + a.C)));
+    hipLaunchKernelGGL(tail_head_bwd_kernel, dim3(a.B), dim3(NT), 0, st, a);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !a.npairs) return e;
-  hipLaunchKernelGGL(tail_pair_bwd_kernel, dim3(a.B, a.npairs), dim3(NT), 0, st, a);
+  {
+    ProfLaunch prof_(st, "tail_pair_bwd_kernel", 4.0 * B * H * H * a.npairs,
+                     4.0 * a.npairs * (2 * H * H + B * (a.heads * H + 2 * H)));
+    hipLaunchKernelGGL(tail_pair_bwd_kernel, dim3(a.B, a.npairs), dim3(NT), 0, st, a);
+  }
   return hipGetLastError();
 }
 

@@ -132,16 +132,24 @@ def profile_begin() -> None:
     lib().mmf_profile_begin()
 
 
-def profile_end() -> list:
-    """[(stage_name, ms), ...] for every launch group since profile_begin()."""
+def profile_end() -> tuple:
+    """(stages, launches) recorded since profile_begin(), in launch order.
+
+    stages:   [(stage_name, ms), ...], one per launch group;
+    launches: [(stage_name, kernel_name, ms, flops, bytes), ...], one per kernel
+              launch, with the launch's algorithmic FLOPs and HBM bytes.
+    """
     L = lib()
-    buf = ctypes.create_string_buffer(1 << 20)
+    buf = ctypes.create_string_buffer(1 << 22)
     L.mmf_profile_end(buf, len(buf))
-    out = []
+    stages, launches = [], []
     for line in buf.value.decode().splitlines():
-        name, ms = line.rsplit(" ", 1)
-        out.append((name, float(ms)))
-    return out
+        f = line.split("\t")
+        if f[0] == "S":
+            stages.append((f[1], float(f[2])))
+        elif f[0] == "L":
+            launches.append((f[1], f[2], float(f[3]), float(f[4]), float(f[5])))
+    return stages, launches
 
 
 def check(rc: int, what: str) -> None:
