@@ -1198,7 +1198,185 @@ __global__ __launch_bounds__(NT) void attn_pool_bwd_dk_lean(const AttnArgs A) {
   }
 }
 
-enum class Kind { Fwd, Probs, Prep, Dkv, Dq, PoolFwd, PoolDq, PoolDk };
+// Fused lean backward (Lq <= 128, every key valid, Lk % 32 == 0, Lk <= 128): one
+// workgroup per (pair, sample, head) computes P and dS ONCE, query on the lane
+// (as the dq pass), and produces both gradients from them:
+//   dQ = scale dS K   straight from the registers (dS is the MFMA B operand);
+//   dK = scale dS^T Q through a transposed dS image in LDS, built in two
+//        64-query halves ([key][64 + 4] floats, ds_write_b32 from the
+//        accumulator layout, ds_read_b128 as the A operand of the key-on-lane
+//        contraction).
+// Against the two passes it saves one S = Q K^T recompute (MFMA), one exp /
+// keep-bit pass (VALU), one read of Q, K, LSE and the keep words, and the D
+// round trip.  LDS at hd <= 32: K, Q images 2 x 18 KB + dS^T half 34 KB -> 2
+// workgroups per CU.
+template <int HDP>
+__global__ __launch_bounds__(NT, 2) void attn_pool_bwd_fused_lean(const AttnArgs A) {
+  constexpr int LS = HDP + 4;
+  constexpr int HALF = HDP / 2;
+  constexpr int NDT = HDP / 32;
+  constexpr int NKT = PKC / 32;
+  constexpr int TS = 64 + 4;   // dS^T image row pitch (floats): one 64-query half
+  __shared__ __attribute__((aligned(16))) float Ks[PKC * LS];
+  __shared__ __attribute__((aligned(16))) float Qs[PKC * LS];
+  __shared__ __attribute__((aligned(16))) float dsT[PKC * TS];
+  __shared__ __attribute__((aligned(16))) float gk[PKC];
+
+  const AttnPair& P = A.p[blockIdx.y];
+  const int bid = blockIdx.x;
+  if (bid >= A.B * A.heads) return;
+  const int head = bid % A.heads, b = bid / A.heads;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, c = lane & 31;
+  const int hd = A.hd, col0 = head * hd;
+  const int Lq = P.Lq, Lk = P.Lk, nkt = Lk >> 5;
+  const int q = w * 32 + c;
+  const bool qvalid = q < Lq;
+  const int qq = qvalid ? q : Lq - 1;
+  const int64_t bh = (int64_t)b * A.heads + head;
+  const int64_t rowidx = bh * Lq + qq;
+  const float pdrop = A.drop_p;
+  const float inv_keep = pdrop > 0.f && pdrop < 1.f ? 1.f / (1.f - pdrop) : 1.f;
+  const float inv_lq = 1.f / (float)Lq;
+  const float scale = A.scale;
+  float* qrow = P.dq + ((int64_t)b * Lq + qq) * P.ldq + col0;
+  const int key = w * 32 + c;                 // dK phase: this wave's keys
+  const bool kwave = w * 32 < Lk;
+
+  if (P.kmask_mode == 1 && P.kmask[(int64_t)b * P.kmask_ld] == 0.f) {
+    // fully masked sample: P = 0 -> dQ = dK = 0
+    if (qvalid)
+      for (int d = h; d < hd; d += 2) qrow[d] = 0.f;
+    if (kwave)
+      for (int d = h; d < hd; d += 2) P.dk[((int64_t)b * Lk + key) * P.ldk + col0 + d] = 0.f;
+    return;
+  }
+  load_rows<PKC, HDP, LS>(Ks, P.k + (int64_t)b * Lk * P.ldk + col0, Lk, P.ldk, 0, hd, true);
+  load_rows<PKC, HDP, LS>(Qs, P.q + (int64_t)b * Lq * P.ldq + col0, Lq, P.ldq, 0, hd, true);
+  for (int k = t; k < PKC; k += NT) gk[k] = k < Lk ? P.dpbar[bh * Lk + k] * inv_keep * inv_lq : 0.f;
+  const float lse = P.lse[rowidx];
+  const float lse2 = (!qvalid || lse == -INFINITY) ? INFINITY : lse * LOG2E;
+  uint4 kw = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+  if (P.keep_bits && pdrop > 0.f) kw = *reinterpret_cast<const uint4*>(P.keep_bits + rowidx * 4);
+  const uint32_t kwa[4] = {kw.x, kw.y, kw.z, kw.w};
+  __syncthreads();
+
+  float qf[HALF];
+  load_frag_vec<HALF>(qf, Qs + q * LS + h * HALF);
+  const float c2 = scale * LOG2E;
+  float pr[NKT][16];
+  float D = 0.f;
+  f32x16 s_nx = dot_rows<HALF>(Ks + c * LS + h * HALF, qf, zero16());
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    if (kt < nkt) {
+      const f32x16 s = s_nx;
+      if (kt + 1 < nkt) s_nx = dot_rows<HALF>(Ks + ((kt + 1) * 32 + c) * LS + h * HALF, qf, zero16());
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 gv = *reinterpret_cast<const float4*>(gk + kt * 32 + 8 * g + 4 * h);
+        const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 4 * g + j;
+          const float p = fast_exp2(fmaf(s[r], c2, -lse2));
+          pr[kt][r] = p;
+          const bool keep = (kwa[kt] >> (8 * g + 4 * h + j)) & 1u;
+          D += keep ? p * gg[j] : 0.f;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) pr[kt][r] = 0.f;
+    }
+  }
+  D += __shfl_xor(D, 32);
+  // dS = P . (G - D), in place
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    if (kt < nkt) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 gv = *reinterpret_cast<const float4*>(gk + kt * 32 + 8 * g + 4 * h);
+        const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 4 * g + j;
+          const bool keep = (kwa[kt] >> (8 * g + 4 * h + j)) & 1u;
+          pr[kt][r] = pr[kt][r] * ((keep ? gg[j] : 0.f) - D);
+        }
+      }
+    }
+  }
+  // dQ = scale dS K (query on the lane; dS is the B operand)
+  {
+    f32x16 dq[NDT];
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) dq[dt] = zero16();
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      if (kt < nkt) {
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            dq[dt] = mfma32(Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], pr[kt][r], dq[dt]);
+      }
+    }
+    if (qvalid) {
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d0 = dt * 32 + 8 * g + 4 * h;
+          if (d0 + 3 < hd)
+            *reinterpret_cast<float4*>(qrow + d0) = make_float4(dq[dt][4 * g] * scale, dq[dt][4 * g + 1] * scale,
+                                                                dq[dt][4 * g + 2] * scale, dq[dt][4 * g + 3] * scale);
+        }
+    }
+  }
+  // dK = scale dS^T Q (key on the lane), over two 64-query halves of dS^T in LDS
+  f32x16 dk[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) dk[dt] = zero16();
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    if (hf) __syncthreads();   // every wave is done reading the first half
+    if ((w >> 1) == hf) {
+      const int ql = (w & 1) * 32 + c;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dsT[(kt * 32 + acc_row(r, h)) * TS + ql] = pr[kt][r];
+    }
+    __syncthreads();
+    if (kwave && hf * 64 < Lq) {
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 a4 = *reinterpret_cast<const float4*>(dsT + key * TS + qt * 32 + 8 * g + 4 * h);
+          const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int qg = hf * 64 + qt * 32 + 8 * g + 4 * h + j;
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt) dk[dt] = mfma32(av[j], Qs[qg * LS + dt * 32 + c], dk[dt]);
+          }
+        }
+    }
+  }
+  if (!kwave) return;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) {
+    const int d = dt * 32 + c;
+    if (d >= hd) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      P.dk[((int64_t)b * Lk + w * 32 + acc_row(r, h)) * P.ldk + col0 + d] = dk[dt][r] * scale;
+  }
+}
+
+enum class Kind { Fwd, Probs, Prep, Dkv, Dq, PoolFwd, PoolDq, PoolDk, PoolFused };
 
 hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, int heads, int hd,
                           float scale, float drop_p, const RngSnap* rng, hipStream_t st) {
@@ -1209,12 +1387,19 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
     prep_vec = (pairs[i].ldo % 4 == 0) && (((uintptr_t)pairs[i].dout & 15) == 0) &&
                (((uintptr_t)pairs[i].o & 15) == 0) && pairs[i].ldo == heads * hd;
   // lean pooled kernels: every pair has all keys valid and float4-able rows
-  bool lean = (kind == Kind::PoolFwd || kind == Kind::PoolDq || kind == Kind::PoolDk) && (hd % 4 == 0);
+  const bool pooled = kind == Kind::PoolFwd || kind == Kind::PoolDq || kind == Kind::PoolDk || kind == Kind::PoolFused;
+  bool lean = pooled && (hd % 4 == 0);
   for (int i = 0; i < npairs && lean; ++i) {
     const AttnPair& P = pairs[i];
     lean = (P.Lk % 32 == 0) && P.Lk <= PKC && P.kmask_mode != 2 && (P.ldq % 4 == 0) && (P.ldk % 4 == 0) &&
            (((uintptr_t)P.q & 15) == 0) && (((uintptr_t)P.k & 15) == 0) &&
            (kind != Kind::PoolDq || (((uintptr_t)P.dq & 15) == 0));
+  }
+  if (kind == Kind::PoolFused) {
+    // lean conditions plus a single query block and float4-able dQ rows
+    for (int i = 0; i < npairs && lean; ++i)
+      lean = pairs[i].Lq <= 128 && (pairs[i].ldq % 4 == 0) && (((uintptr_t)pairs[i].dq & 15) == 0);
+    if (!lean) return hipErrorNotSupported;
   }
   int done = 0;
   while (done < npairs) {
@@ -1230,9 +1415,9 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
         nb = prep_vec ? ((int64_t)B * P.Lq * (heads * hd / 4) + NT - 1) / NT
                       : ((int64_t)B * P.Lq * heads + NT - 1) / NT;
       else if (kind == Kind::Dkv || kind == Kind::PoolDk) nb = (int64_t)B * heads * ((P.Lk + 127) / 128);
-      else if (kind == Kind::PoolFwd) nb = (int64_t)B * heads;
+      else if (kind == Kind::PoolFwd || kind == Kind::PoolFused) nb = (int64_t)B * heads;
       else nb = (int64_t)B * heads * ((P.Lq + 127) / 128);
-      if ((kind == Kind::PoolFwd || kind == Kind::PoolDq || kind == Kind::PoolDk) && P.Lk > PKC)
+      if (pooled && P.Lk > PKC)
         return hipErrorInvalidValue;
       if (nb > maxblk) maxblk = nb;
       ++n;
@@ -1262,9 +1447,10 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
         case Kind::PoolFwd: fl += qk; by += 4 * (bq + bk); break;                         // Q K -> lse, pbar
         case Kind::PoolDq: fl += qk; by += 4 * (2 * bq + bk); break;                      // Q K -> dQ
         case Kind::PoolDk: fl += qk; by += 4 * (bq + 2 * bk); break;                      // Q K -> dK
+        case Kind::PoolFused: fl += 2 * qk; by += 4 * (2 * bq + 2 * bk); break;           // Q K -> dQ dK
       }
     }
-    static const char* const kNames[8][4] = {
+    static const char* const kNames[9][4] = {
         {"attn_fwd_kernel<32, 0>", "attn_fwd_kernel<64, 0>", "attn_fwd_kernel<32, 0>", "attn_fwd_kernel<64, 0>"},
         {"attn_fwd_kernel<32, 1>", "attn_fwd_kernel<64, 1>", "attn_fwd_kernel<32, 1>", "attn_fwd_kernel<64, 1>"},
         {"attn_bwd_prep_kernel", "attn_bwd_prep_kernel", "attn_bwd_prep_vec_kernel", "attn_bwd_prep_vec_kernel"},
@@ -1274,7 +1460,8 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
         {"attn_pool_bwd_dq_kernel<32>", "attn_pool_bwd_dq_kernel<64>", "attn_pool_bwd_dq_lean<32>",
          "attn_pool_bwd_dq_lean<64>"},
         {"attn_pool_bwd_dk_kernel<32>", "attn_pool_bwd_dk_kernel<64>", "attn_pool_bwd_dk_lean<32>",
-         "attn_pool_bwd_dk_lean<64>"}};
+         "attn_pool_bwd_dk_lean<64>"},
+        {"", "", "attn_pool_bwd_fused_lean<32>", "attn_pool_bwd_fused_lean<64>"}};
     const bool alt = kind == Kind::Prep ? prep_vec : lean;
     ProfLaunch prof_(st, kNames[(int)kind][(alt ? 2 : 0) + (small ? 0 : 1)], fl, by);
     switch (kind) {
@@ -1310,6 +1497,10 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
         else if (small) hipLaunchKernelGGL((attn_pool_bwd_dq_kernel<32>), grid, dim3(NT), 0, st, a);
         else hipLaunchKernelGGL((attn_pool_bwd_dq_kernel<64>), grid, dim3(NT), 0, st, a);
         break;
+      case Kind::PoolFused:
+        if (small) hipLaunchKernelGGL((attn_pool_bwd_fused_lean<32>), grid, dim3(NT), 0, st, a);
+        else hipLaunchKernelGGL((attn_pool_bwd_fused_lean<64>), grid, dim3(NT), 0, st, a);
+        break;
       case Kind::PoolDk:
         if (lean && small) hipLaunchKernelGGL((attn_pool_bwd_dk_lean<32>), grid, dim3(NT), 0, st, a);
         else if (lean) hipLaunchKernelGGL((attn_pool_bwd_dk_lean<64>), grid, dim3(NT), 0, st, a);
@@ -1342,7 +1533,10 @@ hipError_t launch_attn_pool_fwd(const AttnPair* pairs, int npairs, int B, int he
 
 hipError_t launch_attn_pool_bwd(int stage, const AttnPair* pairs, int npairs, int B, int heads, int hd,
                                 float scale, float drop_p, const RngSnap* rng, hipStream_t st) {
-  return launch_generic(stage == 0 ? Kind::PoolDq : Kind::PoolDk, pairs, npairs, B, heads, hd, scale,
+  // stage 2: both gradients in one pass when the fused lean kernel applies
+  // (hipErrorNotSupported otherwise: run stages 0 and 1)
+  return launch_generic(stage == 0 ? Kind::PoolDq : (stage == 1 ? Kind::PoolDk : Kind::PoolFused), pairs, npairs,
+                        B, heads, hd, scale,
                         drop_p, rng, st);
 }
 

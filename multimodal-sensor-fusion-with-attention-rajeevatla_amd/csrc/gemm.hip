@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "mmf_device.h"
 
@@ -34,6 +35,12 @@ namespace mmf {
 namespace {
 
 constexpr int BM = 128, BN = 128, BK = 32, NT = 256;
+#ifndef MMF_GEMM_DK
+#define MMF_GEMM_DK 16   // k-tile depth of the LDS-DMA kernel
+#endif
+#ifndef MMF_GEMM_NS
+#define MMF_GEMM_NS 3    // LDS ring stages
+#endif
 constexpr int LDS_STRIDE = BM + 4;      // generic kernel, KR image
 constexpr int LDS_STRIDE_T = BM + 1;    // generic kernel, RK image (transposing writes)
 
@@ -47,14 +54,26 @@ struct TileCtx {
   int brs_off;
 };
 
-__device__ __forceinline__ bool tile_ctx(const GemmGroup& G, TileCtx& t) {
+// The grid is 1-D over the tiles of every group of the launch, in group order
+// (launch_gemm puts the longest contractions first).
+__device__ __forceinline__ int group_of_block(const GemmArgs& args, int& local) {
+  const int b = blockIdx.x;
+  int g = 0;
+#pragma unroll
+  for (int i = 1; i < GEMM_MAX_GROUPS; ++i)
+    if (i < args.ngroups && b >= args.tile_off[i]) g = i;
+  local = b - args.tile_off[g];
+  return g;
+}
+
+__device__ __forceinline__ bool tile_ctx(const GemmGroup& G, int local, TileCtx& t) {
   const int tiles_n = (G.N + BN - 1) / BN;
   const int tiles_m = (G.M + BM - 1) / BM;
   t.nsplit = (G.epi & EPI_PARTIAL) ? G.nsplit : 1;
   const int per_batch = tiles_m * tiles_n * t.nsplit;
-  t.batch = blockIdx.x / per_batch;
+  t.batch = local / per_batch;
   if (t.batch >= G.nbatch) return false;
-  int tile = blockIdx.x - t.batch * per_batch;
+  int tile = local - t.batch * per_batch;
   t.split = tile % t.nsplit;
   tile /= t.nsplit;
   t.i0 = (tile / tiles_n) * BM;
@@ -241,9 +260,10 @@ template <int AMODE, int BMODE, int DK, int NSTAGE>
 __global__ __launch_bounds__(NT, (NSTAGE * DK <= 32 ? 4 : 2)) void gemm_lds_kernel(const GemmArgs args) {
   constexpr int DTILE = BM * DK;                  // floats per operand tile
   constexpr int DMA_PER_TILE = 2 * (BM * DK / 1024);  // glds per wave per (A, B) tile pair
-  const GemmGroup& G = args.g[blockIdx.y];
+  int local;
+  const GemmGroup& G = args.g[group_of_block(args, local)];
   TileCtx T;
-  if (!tile_ctx(G, T)) return;
+  if (!tile_ctx(G, local, T)) return;
   const int64_t offA = (int64_t)T.batch * G.bs_a, offB = (int64_t)T.batch * G.bs_b;
 
   // one LDS object: NSTAGE x [A | B] tiles (also the epilogue image) + 128 floats for the row-sum combine
@@ -376,6 +396,181 @@ __global__ __launch_bounds__(NT, (NSTAGE * DK <= 32 ? 4 : 2)) void gemm_lds_kern
   epilogue<PR>(G, T, acc, lds, rs, p, inv_keep, wm, wn, h, c);
 }
 
+// ------------------------------------------------------------------ weight-stationary kernel
+// Y (rows x N) = X (rows x K) W^T (+bias, relu) for N <= 128, K <= 128 (16 | K):
+// the projection shape of the fused modalities (Q/K projections of every pair,
+// src/attention.py:104-105).  At K = 128 a 128 x 128 tile is 4.2 MFLOP against
+// 128 KB of operands, so staging BOTH operands through LDS per tile makes the
+// LDS-DMA fill (~6 TB/s chip-wide) the co-bottleneck with the fp32 MFMA.  Here
+// each wave loads its 64 columns of W^T once into registers (128 VGPRs at K =
+// 128, in the MFMA k-order of the A fragments) and keeps them while the
+// workgroup walks a contiguous run of row tiles; only X streams through a
+// 6-deep LDS-DMA ring of 128 x 16 k-tiles, which runs ahead across tile
+// boundaries.  The epilogue stores straight from the accumulators (each store
+// instruction writes two 128-B row segments), so the ring keeps filling while
+// a tile is written out.  Persistent grid: 2 workgroups per CU.
+constexpr int WSR_DK = 16, WSR_NS = 6, WSR_NKC = 16;   // k-tile, ring depth, max 8-deep k chunks (K <= 128)
+
+__global__ __launch_bounds__(NT, 2) void gemm_wsr_kernel(const GemmArgs args, int total_items, int K) {
+  constexpr int DTILE = BM * WSR_DK;
+  __shared__ __attribute__((aligned(16))) float ring[WSR_NS * DTILE];
+  const int t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nkt = K / WSR_DK, nkc = K / 8;
+
+  const int nwg = gridDim.x;
+  const int item0 = (int)(((int64_t)blockIdx.x * total_items) / nwg);
+  const int item1 = (int)(((int64_t)(blockIdx.x + 1) * total_items) / nwg);
+  if (item0 >= item1) return;
+
+  // flat DMA cursor over (item, k-tile)
+  const int nflat = (item1 - item0) * nkt;
+  auto item_group = [&](int item, int& rowtile) {
+    int g = 0;
+#pragma unroll
+    for (int i = 1; i < GEMM_MAX_GROUPS; ++i)
+      if (i < args.ngroups && item >= args.tile_off[i]) g = i;
+    rowtile = item - args.tile_off[g];
+    return g;
+  };
+  auto issue = [&](int f) {
+    int rt;
+    const int g = item_group(item0 + f / nkt, rt);
+    const GemmSrc& S = args.s[args.g[g].src_begin];
+    stage_tile<MODE_RK, WSR_DK>(ring + (f % WSR_NS) * DTILE, S.a, 0, rt * BM, args.g[g].M, (f % nkt) * WSR_DK, K,
+                                wave, lane);
+  };
+  // Wait for k-tile f: every later k-tile (2 LDS-DMAs per wave each) and the
+  // epilogue stores issued after it (16 per wave per tile, exact: WSR tiles are
+  // never partial) may stay in flight -- vmcnt counts loads, stores and DMAs
+  // together, in issue order.
+  auto wait_ahead = [&](int ahead, bool stores_younger) {
+    if (stores_younger) {
+      switch (ahead) {
+        case 0: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(22)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+      }
+    } else {
+      switch (ahead) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+      }
+    }
+  };
+  static_assert(WSR_NS - 2 <= 4, "wait_ahead covers 4 tiles ahead");
+
+  int nissued = 0;
+  for (; nissued < WSR_NS - 1 && nissued < nflat; ++nissued) issue(nissued);
+
+  f32x4 breg[2][WSR_NKC];
+  float bias[2];
+  int cur_g = -1;
+  int f = 0;
+  int epi_mark = 0;   // k-tiles issued before the latest epilogue's stores
+  for (int item = item0; item < item1; ++item) {
+    int rt;
+    const int g = item_group(item, rt);
+    const GemmGroup& G = args.g[g];
+    if (g != cur_g) {
+      // this group's W^T slice for the wave's 64 columns, in the A fragments' k-order:
+      // breg[b][m] = W[col][8m + 4h .. 8m + 4h + 3], col = wn*64 + b*32 + c
+      cur_g = g;
+      const GemmSrc& S = args.s[G.src_begin];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int col = wn * 64 + b * 32 + c;
+        const bool ok = col < G.N;
+        const float* wrow = S.b.ptr + (int64_t)(ok ? col : 0) * S.b.ld + 4 * h;
+#pragma unroll
+        for (int m = 0; m < WSR_NKC; ++m)
+          breg[b][m] = (ok && m < nkc) ? *reinterpret_cast<const f32x4*>(wrow + 8 * m) : f32x4{0.f, 0.f, 0.f, 0.f};
+        bias[b] = (ok && (G.epi & EPI_BIAS)) ? G.bias[col] : 0.f;
+      }
+      // Retire these loads here with a wait the compiler can see (the builtin,
+      // not inline asm: vmcnt(0), lgkmcnt/expcnt untouched).  Otherwise it
+      // cannot tell them apart from the LDS-DMAs issued after them and drains
+      // the whole ring (vmcnt(0)) before every k-tile that uses them.
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+    }
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+#pragma unroll
+    for (int kt = 0; kt < WSR_NKC / 2; ++kt) {
+      if (kt < nkt) {
+        wait_ahead(nissued - f - 1, f < epi_mark);
+        lds_barrier();   // tile f landed for every wave; every wave is done with slot (f-1) % NS
+        if (nissued < nflat) issue(nissued++);
+        const float* At = ring + (f % WSR_NS) * DTILE;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x4 af[2];
+#pragma unroll
+          for (int a = 0; a < 2; ++a) af[a] = frag<MODE_RK, WSR_DK>(At, wm * 64 + a * 32 + c, j, h);
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+              for (int b = 0; b < 2; ++b) acc[a][b] = mfma32(af[a][s], breg[b][2 * kt + j][s], acc[a][b]);
+        }
+        ++f;
+      }
+    }
+    // Epilogue straight from the accumulators: v = alpha*acc + bias[j]; relu.
+    // Lane (c, h) holds rows 8q+4h+{0..3} of column c; a 4x4 transpose across
+    // the lane quad (xor 2, then xor 1) leaves it 4 consecutive columns of one
+    // row, stored as one 16-B store (8 rows x 128 B per wave instruction).
+    const int x = c & 3;
+    const int i0 = rt * BM + wm * 64;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = acc[a][b][4 * q + e] * G.alpha + bias[b];
+            if (G.epi & EPI_RELU) v[e] = fmaxf(v[e], 0.f);
+          }
+          // v[r] = M[r][x]; step 1 swaps the off-diagonal 2x2 blocks (partner x^2)
+          {
+            const bool up = (x & 2) != 0;
+            const float s0 = __shfl_xor(up ? v[0] : v[2], 2);
+            const float s1 = __shfl_xor(up ? v[1] : v[3], 2);
+            if (up) { v[0] = s0; v[1] = s1; } else { v[2] = s0; v[3] = s1; }
+          }
+          // now lane x holds M[x&2 .. +1][x&1 + (0|2)]; step 2 swaps within 2x2 (partner x^1)
+          {
+            const bool odd = (x & 1) != 0;
+            const float s0 = __shfl_xor(odd ? v[0] : v[1], 1);
+            const float s1 = __shfl_xor(odd ? v[2] : v[3], 1);
+            if (odd) { v[0] = s0; v[2] = s1; } else { v[1] = s0; v[3] = s1; }
+          }
+          const int row = i0 + a * 32 + 8 * q + 4 * h + x;
+          const int col = wn * 64 + b * 32 + (c & ~3);
+          *reinterpret_cast<f32x4*>(G.C + (int64_t)row * G.ldc + col) = f32x4{v[0], v[1], v[2], v[3]};
+        }
+      }
+    epi_mark = nissued;
+  }
+}
+
 // ------------------------------------------------------------------ generic kernel
 struct TileRegs { float4 v[4]; };
 
@@ -439,9 +634,10 @@ __device__ __forceinline__ void store_tile(const TileRegs& R, float* S) {
 
 template <int AMODE, int BMODE>
 __global__ __launch_bounds__(NT) void gemm_generic_kernel(const GemmArgs args) {
-  const GemmGroup& G = args.g[blockIdx.y];
+  int local;
+  const GemmGroup& G = args.g[group_of_block(args, local)];
   TileCtx T;
-  if (!tile_ctx(G, T)) return;
+  if (!tile_ctx(G, local, T)) return;
   const int64_t offA = (int64_t)T.batch * G.bs_a, offB = (int64_t)T.batch * G.bs_b;
 
   // one LDS object: A and B tiles, reused as the [64][CS] epilogue image
@@ -656,8 +852,93 @@ bool job_fast(const GemmJob& J, int amode, int bmode) {
 
 }  // namespace
 
-hipError_t launch_gemm(const GemmJob* jobs, int njobs, int amode, int bmode, float drop_p,
+namespace {
+
+inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+bool job_wsr(const GemmJob& J, int amode, int bmode) {
+  const GemmGroup& g = J.g;
+  if (amode != MODE_RK || bmode != MODE_RK || J.nsrc != 1 || g.nbatch > 1) return false;
+  if (g.epi & ~(EPI_BIAS | EPI_RELU)) return false;
+  const GemmSrc& s = J.src[0];
+  return g.N == BN && g.M % BM == 0 && s.K % WSR_DK == 0 && s.K >= WSR_DK && s.K <= 8 * WSR_NKC &&
+         s.a.row_div == 1 && s.b.row_div == 1 && s.a.ld % 4 == 0 && s.b.ld % 4 == 0 && aligned16(s.a.ptr) &&
+         aligned16(s.b.ptr) && g.ldc % 4 == 0 && aligned16(g.C);
+}
+
+int cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+// Every job weight-stationary-eligible with one common K: persistent launches
+// of up to GEMM_MAX_GROUPS groups.
+hipError_t launch_wsr(const GemmJob* jobs, int njobs, hipStream_t st) {
+  for (int done = 0; done < njobs;) {
+    GemmArgs args;
+    memset(&args, 0, sizeof(args));
+    args.amode = MODE_RK;
+    args.bmode = MODE_RK;
+    int ng = 0, items = 0;
+    double fl = 0.0, by = 0.0;
+    while (done < njobs && ng < GEMM_MAX_GROUPS) {
+      GemmGroup g = jobs[done].g;
+      g.nbatch = 1;
+      g.src_begin = ng;
+      g.src_count = 1;
+      args.s[ng] = jobs[done].src[0];
+      args.tile_off[ng] = items;
+      args.g[ng++] = g;
+      items += g.M / BM;
+      fl += 2.0 * g.M * g.N * jobs[done].src[0].K;
+      by += 4.0 * ((double)g.M + g.N) * jobs[done].src[0].K + 4.0 * g.M * g.N;
+      ++done;
+    }
+    args.ngroups = ng;
+    const int K = args.s[0].K;
+    const int grid = std::min(items, 2 * cu_count());
+    ProfLaunch prof_(st, "gemm_wsr_kernel", fl, by);
+    hipLaunchKernelGGL(gemm_wsr_kernel, dim3(grid), dim3(NT), 0, st, args, items, K);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace
+
+hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, float drop_p,
                        const RngSnap* rng, hipStream_t st) {
+  {
+    bool wsr = njobs > 0;
+    for (int i = 0; i < njobs && wsr; ++i)
+      wsr = job_wsr(jobs_in[i], amode, bmode) && jobs_in[i].src[0].K == jobs_in[0].src[0].K;
+    if (wsr && getenv("MMF_NO_WSR") == nullptr) return launch_wsr(jobs_in, njobs, st);
+  }
+  // The jobs of one call are independent outputs, so they may be launched in
+  // any order: longest contraction per tile first (the first-dispatched blocks
+  // carry the most work), fast-path jobs packed together.
+  std::vector<int> order(njobs);
+  std::vector<double> work(njobs);
+  for (int i = 0; i < njobs; ++i) {
+    order[i] = i;
+    const GemmGroup& g = jobs_in[i].g;
+    const bool partial = (g.epi & EPI_PARTIAL) != 0;
+    double kk = 0.0;
+    for (int s = 0; s < jobs_in[i].nsrc; ++s) kk += jobs_in[i].src[s].K;
+    work[i] = partial ? (double)g.kchunk : kk;
+  }
+  std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
+    const bool fx = job_fast(jobs_in[x], amode, bmode), fy = job_fast(jobs_in[y], amode, bmode);
+    if (fx != fy) return fx;
+    return work[x] > work[y];
+  });
   int done = 0;
   while (done < njobs) {
     GemmArgs args;
@@ -668,9 +949,9 @@ hipError_t launch_gemm(const GemmJob* jobs, int njobs, int amode, int bmode, flo
     args.rng = rng;
     int ng = 0, ns = 0, max_blocks = 0;
     // one launch = consecutive jobs of the same kernel flavour
-    const bool fast = job_fast(jobs[done], amode, bmode);
+    const bool fast = job_fast(jobs_in[order[done]], amode, bmode);
     while (done < njobs && ng < GEMM_MAX_GROUPS) {
-      const GemmJob& J = jobs[done];
+      const GemmJob& J = jobs_in[order[done]];
       if (J.nsrc > GEMM_MAX_SRCS) return hipErrorInvalidValue;
       if (ns + J.nsrc > GEMM_MAX_SRCS) break;
       if (job_fast(J, amode, bmode) != fast) break;
@@ -680,15 +961,16 @@ hipError_t launch_gemm(const GemmJob* jobs, int njobs, int amode, int bmode, flo
       g.src_count = J.nsrc;
       const bool partial = (g.epi & EPI_PARTIAL) != 0;
       for (int s = 0; s < J.nsrc; ++s) args.s[ns++] = J.src[s];
-      args.g[ng++] = g;
       const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN) * (partial ? g.nsplit : 1) * g.nbatch;
-      if (tiles > max_blocks) max_blocks = tiles;
+      args.tile_off[ng] = max_blocks;
+      args.g[ng++] = g;
+      max_blocks += tiles;
       ++done;
     }
     if (ng == 0) return hipErrorInvalidValue;
     args.ngroups = ng;
     if (max_blocks > 0) {
-      dim3 grid(max_blocks, ng);
+      dim3 grid(max_blocks, 1);
       double fl = 0.0, by = 0.0;
       for (int gi = 0; gi < ng; ++gi) {
         const GemmGroup& g = args.g[gi];
@@ -725,7 +1007,7 @@ hipError_t launch_gemm(const GemmJob* jobs, int njobs, int amode, int bmode, flo
       if (fast) {
         // (DK, ring depth) = (16, 3): measured best of (16|32) x (2|3|4) at C2
         // (profiles/tune_gemm_cfg.sh)
-        MMF_LAUNCH_CFG(16, 3)
+        MMF_LAUNCH_CFG(MMF_GEMM_DK, MMF_GEMM_NS)
       } else {
         MMF_LAUNCH(gemm_generic_kernel)
       }

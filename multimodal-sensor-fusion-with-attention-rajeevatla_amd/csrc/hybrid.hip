@@ -13,6 +13,7 @@
 // Both are exact reformulations (fp32 reassociation only) of the reference.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "capi_util.h"
 
@@ -550,8 +551,19 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
       pp[g].dpbar = w.dpbar[g];
     }
     if (!tail) STAGE_TRY("bwd.pool_dpbar", launch_pool_dpbar(pp.data(), d->num_pairs, B, nh, hd, H, st));
-    STAGE_TRY("bwd.attn_dq", launch_attn_pool_bwd(0, pairs.data(), d->num_pairs, B, nh, hd, scale, p, rng, st));
-    STAGE_TRY("bwd.attn_dk", launch_attn_pool_bwd(1, pairs.data(), d->num_pairs, B, nh, hd, scale, p, rng, st));
+    hipError_t fe;
+    {
+      Stage stage_("bwd.attn", st);
+      fe = getenv("MMF_NO_FUSED_BWD") ? hipErrorNotSupported
+                                      : launch_attn_pool_bwd(2, pairs.data(), d->num_pairs, B, nh, hd, scale, p, rng, st);
+    }
+    if (fe == hipErrorNotSupported) {
+      (void)hipGetLastError();
+      STAGE_TRY("bwd.attn_dq", launch_attn_pool_bwd(0, pairs.data(), d->num_pairs, B, nh, hd, scale, p, rng, st));
+      STAGE_TRY("bwd.attn_dk", launch_attn_pool_bwd(1, pairs.data(), d->num_pairs, B, nh, hd, scale, p, rng, st));
+    } else {
+      HIP_TRY(fe);
+    }
     std::vector<PoolEMod> em(M);
     for (int m = 0; m < M; ++m) {
       memset(&em[m], 0, sizeof(PoolEMod));

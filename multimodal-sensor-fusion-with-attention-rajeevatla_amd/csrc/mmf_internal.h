@@ -100,12 +100,13 @@ struct GemmGroup {
   int32_t bs_a, bs_b, bs_c, bs_bias, bs_brs;
 };
 
-constexpr int GEMM_MAX_GROUPS = 8;
+constexpr int GEMM_MAX_GROUPS = 12;
 constexpr int GEMM_MAX_SRCS = 24;
 
 struct GemmArgs {
   GemmGroup g[GEMM_MAX_GROUPS];
   GemmSrc s[GEMM_MAX_SRCS];
+  int32_t tile_off[GEMM_MAX_GROUPS];   // first block of each group (1-D grid over all groups' tiles)
   int32_t ngroups;
   int32_t amode, bmode;
   float drop_p;              // p of every dropout site in this launch

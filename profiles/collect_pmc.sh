@@ -9,13 +9,13 @@ mkdir -p "$OUT"
 B="python3 bench.py --steps 2 --warmup 1 --skip-cpu --no-graph --profile-steps 1"
 pass() {
   local name=$1; shift
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc "$@" --output-format csv -d "$OUT/$name" -o run -- $B \
+  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc "$@" --output-format csv -d "$OUT/$name" -o run -- $B \
     > "$OUT/$name.log" 2>&1
 }
 pass p1 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU \
         SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE &&
 pass p2 SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_SALU \
-        SQ_INSTS_VALU_INT32 SQ_ACTIVE_INST_VMEM FETCH_SIZE &&
-pass p3 WRITE_SIZE SQ_INSTS_VALU_TRANS_F32 SQ_LEVEL_WAVES SQ_IFETCH SQ_INSTS_SMEM SQ_INST_LEVEL_VMEM \
-        SQ_WAIT_INST_LDS SQ_INSTS_BRANCH
+        SQ_INSTS_VALU_INT32 SQ_ACTIVE_INST_VMEM &&
+pass p3 SQ_INSTS_VALU_TRANS_F32 SQ_LEVEL_WAVES SQ_IFETCH SQ_INSTS_SMEM SQ_INST_LEVEL_VMEM \
+        SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_INSTS_VMEM_WR
 echo "pmc rc=$?"
