@@ -159,6 +159,42 @@ int mmf_cma_backward(const mmf_cma_desc* d, const mmf_cma_params* params, const 
                      float* dquery, float* dkey, float* dvalue, void* stream);
 
 /* ---------------------------------------------------------------------
+ * FrameEncoder.attention_pool (src/encoders.py:313-336): learned-score
+ * softmax pooling over frames.  x (B, T, D); score_w (D) / score_b (1) are
+ * FrameEncoder.attention (nn.Linear(D, 1)); mask (B, T) or NULL (frames with
+ * mask == 0 are excluded; an all-masked row gives weights 0 and pooled 0, the
+ * reference's nan_to_num).  Outputs pooled (B, D) and weights (B, T), which
+ * the backward reads.  T <= 8192.
+ * ------------------------------------------------------------------- */
+size_t mmf_attention_pool_workspace_bytes(int32_t batch, int32_t dim);
+int mmf_attention_pool_forward(int32_t batch, int32_t frames, int32_t dim, const float* x,
+                               const float* score_w, const float* score_b, const float* mask,
+                               float* pooled, float* weights, void* stream);
+/* Backward of sum(pooled * dpooled): dx (B, T, D), dscore_w (D), dscore_b (1)
+ * (overwritten, batch-reduced in a fixed order). */
+int mmf_attention_pool_backward(int32_t batch, int32_t frames, int32_t dim, const float* x,
+                                const float* score_w, const float* weights, const float* dpooled,
+                                float* dx, float* dscore_w, float* dscore_b, void* workspace,
+                                void* stream);
+
+/* ---------------------------------------------------------------------
+ * LateFusion weighting (src/fusion.py:228-245): logits (B, M, C) stacked
+ * per-modality classifier outputs, weight_logits (M), mask (B, M) or NULL.
+ * fused (B, C) = sum_m w[b, m] logits[b, m, :] with w = softmax(weight_logits)
+ * * mask renormalised by (sum + 1e-8), or 1/M where the masked sum is 0.
+ * weights (B, M) is written for the backward.  M <= 64.
+ * ------------------------------------------------------------------- */
+size_t mmf_late_fusion_workspace_bytes(int32_t batch, int32_t num_modalities);
+int mmf_late_fusion_forward(int32_t batch, int32_t num_modalities, int32_t num_classes,
+                            const float* logits, const float* weight_logits, const float* mask,
+                            float* fused, float* weights, void* stream);
+/* Backward of sum(fused * dfused): dlogits (B, M, C), dweight_logits (M). */
+int mmf_late_fusion_backward(int32_t batch, int32_t num_modalities, int32_t num_classes,
+                             const float* logits, const float* weight_logits, const float* mask,
+                             const float* weights, const float* dfused, float* dlogits,
+                             float* dweight_logits, void* workspace, void* stream);
+
+/* ---------------------------------------------------------------------
  * Training-step helpers used by the data-parallel step (not part of the
  * reference interface; the reference uses torch.optim.AdamW via Lightning,
  * src/train.py:374-414).

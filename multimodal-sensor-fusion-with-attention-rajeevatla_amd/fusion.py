@@ -19,8 +19,9 @@ kernels through include/mmfusion.h (mmf_hybrid_forward / mmf_hybrid_backward);
 inputs may be 2-D (B, D_m) (reference semantics) or 3-D (B, L_m, D_m)
 (sequence mode: each modality's aggregate is mean-pooled over L_m before the
 weighting; identical to the reference at L = 1).  No CPU path exists: CPU
-tensors raise.  EarlyFusion / LateFusion are plain-PyTorch plumbing kept only
-so the import surface matches (they are not on the accelerated path).
+tensors raise.  EarlyFusion is plain-PyTorch plumbing kept only so the import
+surface matches; LateFusion's per-modality classifiers are nn.Linear layers
+and its masked softmax weighting (src/fusion.py:228-245) runs on HIP.
 """
 
 from __future__ import annotations
@@ -42,7 +43,7 @@ from attention import CrossModalAttention, _new_rng_state  # noqa: E402
 
 
 # --------------------------------------------------------------------------
-# Out-of-scope plumbing (not accelerated): Early / Late fusion restated in torch.
+# Early fusion (plumbing, torch) and Late fusion (torch classifiers + HIP weighting).
 # --------------------------------------------------------------------------
 def _mask_or_ones(features, names, mask):
     first = features[names[0]]
@@ -87,8 +88,44 @@ class EarlyFusion(nn.Module):
         return self.fusion(torch.cat(parts, dim=1))
 
 
+class _LateWeightFunction(torch.autograd.Function):
+    """LateFusion's masked softmax weighting (src/fusion.py:228-245) on HIP
+    (mmf_late_fusion_forward / _backward, csrc/softmax_pool.hip)."""
+
+    @staticmethod
+    def forward(ctx, stacked, weight_logits, mask):
+        L = _nat.lib()
+        _nat.require_device(stacked, "LateFusion logits")
+        dev = stacked.device
+        B, M, C = stacked.shape
+        fused = torch.empty(B, C, dtype=torch.float32, device=dev)
+        weights = torch.empty(B, M, dtype=torch.float32, device=dev)
+        rc = L.mmf_late_fusion_forward(B, M, C, stacked.data_ptr(), weight_logits.data_ptr(), mask.data_ptr(),
+                                       fused.data_ptr(), weights.data_ptr(), _nat.stream_ptr(dev))
+        _nat.check(rc, "LateFusion weighting forward")
+        ctx.save_for_backward(stacked, weight_logits, mask, weights)
+        return fused
+
+    @staticmethod
+    def backward(ctx, dfused):
+        L = _nat.lib()
+        stacked, weight_logits, mask, weights = ctx.saved_tensors
+        dev = stacked.device
+        B, M, C = stacked.shape
+        dfused = _nat.f32c(dfused)
+        dstacked = torch.empty_like(stacked)
+        dwl = torch.empty(M, dtype=torch.float32, device=dev)
+        ws = torch.empty(L.mmf_late_fusion_workspace_bytes(B, M), dtype=torch.uint8, device=dev)
+        rc = L.mmf_late_fusion_backward(B, M, C, stacked.data_ptr(), weight_logits.data_ptr(), mask.data_ptr(),
+                                        weights.data_ptr(), dfused.data_ptr(), dstacked.data_ptr(), dwl.data_ptr(),
+                                        ws.data_ptr(), _nat.stream_ptr(dev))
+        _nat.check(rc, "LateFusion weighting backward")
+        return dstacked, dwl, None
+
+
 class LateFusion(nn.Module):
-    """Per-modality classifiers, softmax(learned logits) x mask weighting (src/fusion.py:126-245)."""
+    """Per-modality classifiers (nn.Linear on PyTorch-ROCm), then the masked
+    softmax(weight_logits) weighting on HIP (src/fusion.py:126-245)."""
 
     def __init__(self, modality_dims: Dict[str, int], hidden_dim: int = 256, num_classes: int = 11,
                  dropout: float = 0.1):
@@ -116,10 +153,7 @@ class LateFusion(nn.Module):
             x = modality_features[name].to(mask.device) * mask[:, i:i + 1]
             per[name] = self.classifiers[name](self.dropout(x))
         stacked = torch.stack([per[n] for n in self.modality_names], dim=1)
-        w = torch.softmax(self.weight_logits, dim=0).unsqueeze(0) * mask
-        s = w.sum(dim=1, keepdim=True)
-        w = torch.where(s > 0, w / (s + 1e-8), torch.full_like(w, 1.0 / self.num_modalities))
-        return (stacked * w.unsqueeze(-1)).sum(dim=1), per
+        return _LateWeightFunction.apply(_nat.f32c(stacked), self.weight_logits, mask.float().contiguous()), per
 
 
 # --------------------------------------------------------------------------

@@ -27,6 +27,8 @@ EXPORTED_SYMBOLS = (
     "mmf_cma_saved_bytes", "mmf_cma_workspace_bytes", "mmf_cma_forward", "mmf_cma_backward",
     "mmf_cross_entropy_ls", "mmf_adamw_step", "mmf_profile_begin", "mmf_profile_end",
     "mmf_last_error", "mmf_version",
+    "mmf_attention_pool_workspace_bytes", "mmf_attention_pool_forward", "mmf_attention_pool_backward",
+    "mmf_late_fusion_workspace_bytes", "mmf_late_fusion_forward", "mmf_late_fusion_backward",
 )
 
 
@@ -120,6 +122,18 @@ def lib() -> ctypes.CDLL:
     L.mmf_profile_begin.restype = None
     L.mmf_profile_end.argtypes = [ctypes.c_char_p, c_size_t]
     L.mmf_profile_end.restype = c_size_t
+    L.mmf_attention_pool_workspace_bytes.argtypes = [c_int32, c_int32]
+    L.mmf_attention_pool_workspace_bytes.restype = sz
+    L.mmf_attention_pool_forward.argtypes = [c_int32, c_int32, c_int32, vp, vp, vp, vp, vp, vp, vp]
+    L.mmf_attention_pool_forward.restype = c_int32
+    L.mmf_attention_pool_backward.argtypes = [c_int32, c_int32, c_int32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.mmf_attention_pool_backward.restype = c_int32
+    L.mmf_late_fusion_workspace_bytes.argtypes = [c_int32, c_int32]
+    L.mmf_late_fusion_workspace_bytes.restype = sz
+    L.mmf_late_fusion_forward.argtypes = [c_int32, c_int32, c_int32, vp, vp, vp, vp, vp, vp]
+    L.mmf_late_fusion_forward.restype = c_int32
+    L.mmf_late_fusion_backward.argtypes = [c_int32, c_int32, c_int32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.mmf_late_fusion_backward.restype = c_int32
     L.mmf_last_error.argtypes = []
     L.mmf_last_error.restype = ctypes.c_char_p
     L.mmf_version.argtypes = []

@@ -314,3 +314,90 @@ def pairwise_inputs(case: PairwiseCase):
     mask = np.asarray(case.mask, dtype=np.float32)
     grads = {m: rng.standard_normal((case.batch, case.hidden)).astype(np.float32) for m in case.names}
     return feats, mask, grads
+
+
+# ----------------------------------------------------------------------------
+# FrameEncoder attention pooling (src/encoders.py:210-336) and the LateFusion
+# weighting (src/fusion.py:126-245): the §8(f) masked-softmax weighting ops.
+# ----------------------------------------------------------------------------
+@dataclass
+class FramePoolCase:
+    name: str
+    batch: int
+    frames: int
+    frame_dim: int
+    hidden: int
+    out_dim: int
+    seed: int
+    masked: bool = False
+
+
+FRAMEPOOL_CASES: List[FramePoolCase] = [
+    FramePoolCase("framepool_nomask", batch=4, frames=30, frame_dim=48, hidden=32, out_dim=16, seed=81),
+    FramePoolCase("framepool_mask", batch=4, frames=13, frame_dim=24, hidden=40, out_dim=8, seed=82, masked=True),
+]
+
+
+def framepool_state(case: FramePoolCase) -> "OrderedDict[str, np.ndarray]":
+    rng = np.random.default_rng(case.seed)
+    sd: "OrderedDict[str, np.ndarray]" = OrderedDict()
+    for key, (o, i) in (("frame_processor.0", (case.hidden, case.frame_dim)), ("attention", (1, case.hidden)),
+                        ("projection.0", (case.hidden, case.hidden)), ("projection.3", (case.out_dim, case.hidden))):
+        w, b = _linear(rng, o, i)
+        if key == "attention":
+            w = w * 4.0   # sharper frame weights than the default init
+        sd[f"{key}.weight"], sd[f"{key}.bias"] = w, b
+    return sd
+
+
+def framepool_inputs(case: FramePoolCase):
+    """(frames, mask or None, upstream grad of the pooled (B, hidden) and of the encoding (B, out))."""
+    rng = np.random.default_rng(case.seed + 982451653)
+    frames = rng.standard_normal((case.batch, case.frames, case.frame_dim)).astype(np.float32)
+    mask = None
+    if case.masked:
+        mask = np.zeros((case.batch, case.frames), dtype=np.float32)
+        lengths = [case.frames, 5, 0, 1][: case.batch]      # full, ragged, all masked, single frame
+        for b, n in enumerate(lengths):
+            mask[b, :n] = 1.0
+    g_pool = rng.standard_normal((case.batch, case.hidden)).astype(np.float32)
+    g_out = rng.standard_normal((case.batch, case.out_dim)).astype(np.float32)
+    return frames, mask, g_pool, g_out
+
+
+@dataclass
+class LateCase:
+    name: str
+    names: List[str]
+    dims: Dict[str, int]
+    batch: int
+    hidden: int
+    classes: int
+    seed: int
+    mask: List[List[float]]
+
+
+LATE_CASES: List[LateCase] = [
+    LateCase("late_3mod", ["video", "audio", "imu"], {"video": 12, "audio": 8, "imu": 6}, batch=5, hidden=16,
+             classes=4, seed=91, mask=[[1, 1, 1], [1, 0, 1], [0, 0, 0], [0, 0, 1], [0.5, 1, 0]]),
+]
+
+
+def late_state(case: LateCase) -> "OrderedDict[str, np.ndarray]":
+    rng = np.random.default_rng(case.seed)
+    sd: "OrderedDict[str, np.ndarray]" = OrderedDict()
+    for m in case.names:
+        w, b = _linear(rng, case.hidden, case.dims[m])
+        sd[f"classifiers.{m}.0.weight"], sd[f"classifiers.{m}.0.bias"] = w, b
+        w, b = _linear(rng, case.classes, case.hidden)
+        sd[f"classifiers.{m}.3.weight"], sd[f"classifiers.{m}.3.bias"] = w, b
+    sd["weight_logits"] = rng.standard_normal(len(case.names)).astype(np.float32)
+    return sd
+
+
+def late_inputs(case: LateCase):
+    rng = np.random.default_rng(case.seed + 49979687)
+    feats = {m: rng.standard_normal((case.batch, case.dims[m])).astype(np.float32) for m in case.names}
+    mask = np.asarray(case.mask, dtype=np.float32)
+    grad = rng.standard_normal((case.batch, case.classes)).astype(np.float32)
+    return feats, mask, grad

