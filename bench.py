@@ -33,23 +33,36 @@ METRIC = "HybridFusion fwd+bwd samples/sec at 1/2/4/8 MI355X; CPU-ref parity"
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 
+# Per-GPU workloads (BASELINE.json configs; the headline is configs[1] = "c2").
+#   L: per-modality sequence lengths (0 => 2-D (B, D) inputs, reference semantics)
+#   keep: per-(sample, modality) keep probability of the modality mask (>= 1 kept
+#         per row) plus 1 % all-masked rows when < 1
 WORKLOADS = {
-    # name: (M, B per GPU, L (0 => 2-D reference semantics), D, H, heads, C)
-    "c2": (3, 256, 128, 128, 128, 4, 5),
-    "c2_l1": (3, 256, 0, 128, 128, 4, 5),
+    "c2": dict(M=3, B=256, L=[128] * 3, D=128, H=128, heads=4, C=5, keep=1.0),
+    "c2_l1": dict(M=3, B=256, L=[0] * 3, D=128, H=128, heads=4, C=5, keep=1.0),
+    # C4 shape: video (30 frame embeddings) + IMU (50 steps), Lq != Lk, H = 256, 11 classes
+    "c4": dict(M=2, B=256, L=[30, 50], D=256, H=256, heads=4, C=11, keep=1.0),
+    # C5: 6 modalities, global B = 1024 over 8 GPUs, T = 512, d_model = 256, missing-modality masks
+    "c5": dict(M=6, B=128, L=[512] * 6, D=256, H=256, heads=4, C=5, keep=0.9),
 }
 
 
-def total_step_flops(M, B, L, D, H, heads, C):
-    """SURVEY §8d formula: 3 x forward (projections + P*(8BLH^2 + 4BL^2H) + head)."""
-    Le = max(L, 1)
-    P = M * (M - 1)
-    fwd = 2 * B * Le * D * H * M
-    if L > 0:
-        fwd += P * (8 * B * Le * H * H + 4 * B * Le * Le * H)
-    else:
-        fwd += P * 4 * B * H * H      # reference semantics: Q/K dead at L=1
-    fwd += 2 * B * H * H + 2 * B * H * C + 4 * M * B * H + B * Le * H * M
+def total_step_flops(w):
+    """SURVEY §8d formula: 3 x forward (projections + per pair Q,K,V,out + QK^T + AV + head)."""
+    B, D, H, C, M = w["B"], w["D"], w["H"], w["C"], w["M"]
+    Ls = w["L"]
+    fwd = sum(2 * B * max(l, 1) * D * H for l in Ls)
+    for q in range(M):
+        for k in range(M):
+            if q == k:
+                continue
+            lq, lk = Ls[q], Ls[k]
+            if lq == 0 and lk == 0:
+                fwd += 4 * B * H * H          # reference semantics: Q/K dead at L=1
+            else:
+                lq, lk = max(lq, 1), max(lk, 1)
+                fwd += 4 * B * lq * H * H + 4 * B * lk * H * H + 4 * B * lq * lk * H
+    fwd += 2 * B * H * H + 2 * B * H * C + 4 * M * B * H + sum(B * max(l, 1) * H for l in Ls)
     return 3 * fwd
 
 
@@ -111,40 +124,47 @@ def dominant_roofline(kernels):
     }
 
 
-def make_inputs(M, B, L, D, C, seed, device):
+def make_inputs(w, B, seed, device):
     g = torch.Generator().manual_seed(seed)
-    shape = (B, L, D) if L > 0 else (B, D)
-    feats = [torch.randn(shape, generator=g) for _ in range(M)]
-    mask = torch.ones(B, M)
-    labels = torch.randint(0, C, (B,), generator=g)
+    feats = [torch.randn((B, l, w["D"]) if l > 0 else (B, w["D"]), generator=g) for l in w["L"]]
+    mask = torch.ones(B, w["M"])
+    if w["keep"] < 1.0:
+        mask = (torch.rand(B, w["M"], generator=g) < w["keep"]).float()
+        first = torch.randint(0, w["M"], (B,), generator=g)
+        mask[torch.arange(B), first] = 1.0            # >= 1 modality kept per row ...
+        mask[torch.randperm(B, generator=g)[: max(1, B // 100)]] = 0.0   # ... except 1 % all-masked rows
+    labels = torch.randint(0, w["C"], (B,), generator=g)
     return [f.to(device) for f in feats], mask.to(device), labels.to(device)
 
 
-def cpu_baseline(M, L, D, H, heads, C, budget_s=15.0, max_steps=20):
+def cpu_baseline(w, budget_s=15.0, max_steps=20):
     """Time the oracle (torch-CPU restatement, oracle/hybrid_cpu.py) on a bounded sample."""
     from oracle.hybrid_cpu import hybrid_train_step
     from fusion import HybridFusion
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
     torch.set_num_threads(threads)
-    bs = 16 if L > 0 else 256
+    lmax = max(w["L"])
+    bs = 256 if lmax == 0 else (16 if lmax <= 128 else 2)
     torch.manual_seed(0)
-    names = [f"m{i}" for i in range(M)]
-    model = HybridFusion({n: D for n in names}, hidden_dim=H, num_classes=C, num_heads=heads, dropout=0.1)
+    names = [f"m{i}" for i in range(w["M"])]
+    model = HybridFusion({n: w["D"] for n in names}, hidden_dim=w["H"], num_classes=w["C"], num_heads=w["heads"],
+                         dropout=0.1)
     params = {k: v.detach().clone().requires_grad_(True) for k, v in model.state_dict().items()}
-    feats_l, mask, labels = make_inputs(M, bs, L, D, C, 1234, "cpu")
+    feats_l, mask, labels = make_inputs(w, bs, 1234, "cpu")
     feats = {n: f.requires_grad_(True) for n, f in zip(names, feats_l)}
     gen = torch.Generator().manual_seed(5)
-    hybrid_train_step(params, names, feats, mask, labels, heads, 0.1, gen)   # warm-up
+    hybrid_train_step(params, names, feats, mask, labels, w["heads"], 0.1, gen)   # warm-up
     n, t0 = 0, time.perf_counter()
     while n < max_steps and (time.perf_counter() - t0) < budget_s:
         for p in list(params.values()) + list(feats.values()):
             p.grad = None
-        hybrid_train_step(params, names, feats, mask, labels, heads, 0.1, gen)
+        hybrid_train_step(params, names, feats, mask, labels, w["heads"], 0.1, gen)
         n += 1
     dt = time.perf_counter() - t0
     return {"value": round(bs * n / dt, 2), "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": f"{n} oracle steps of B={bs} (same per-sample work: M={M}, L={max(L, 1)}, "
-                      f"D=H={H}, h={heads}, fwd+CE+bwd, fp32, torch {torch.__version__} CPU), {dt:.1f}s"}
+            "sample": f"{n} oracle steps of B={bs} (same per-sample work: M={w['M']}, L={w['L']}, "
+                      f"D={w['D']}, H={w['H']}, h={w['heads']}, fwd+CE+bwd, fp32, torch {torch.__version__} CPU), "
+                      f"{dt:.1f}s"}
 
 
 def main():
@@ -173,13 +193,14 @@ def main():
     from fusion import HybridFusion
     from train_step import HybridTrainStep
 
-    M, B, L, D, H, heads, C = WORKLOADS[args.workload]
+    w = WORKLOADS[args.workload]
+    M, B, D, H, heads, C = w["M"], w["B"], w["D"], w["H"], w["heads"], w["C"]
     torch.manual_seed(0)                      # identical initial weights on every rank
     names = [f"m{i}" for i in range(M)]
     model = HybridFusion({n: D for n in names}, hidden_dim=H, num_classes=C, num_heads=heads,
                          dropout=0.1).to(dev)
     model._rng_state[0] ^= rank * 0x9E3779B1  # distinct dropout streams per rank
-    feats, mask, labels = make_inputs(M, B, L, D, C, 42 + rank, dev)
+    feats, mask, labels = make_inputs(w, B, 42 + rank, dev)
     trainer = HybridTrainStep(model, feats, mask, labels, process_group=pg)
 
     # kernel-level timing (eager): hipEvents around each launch group and each
@@ -222,19 +243,24 @@ def main():
 
     if rank == 0:
         roofline = dominant_roofline(kernels)
-        step_fl = total_step_flops(M, B, L, D, H, heads, C)
+        step_fl = total_step_flops(w)
         cpu = None
         if world == 1 and not args.skip_cpu:
-            cpu = cpu_baseline(M, L, D, H, heads, C)
+            cpu = cpu_baseline(w)
+        Ls = w["L"]
+        lens = Ls[0] if len(set(Ls)) == 1 else Ls
+        mask_note = "" if w["keep"] >= 1 else f", modality masks keep={w['keep']} (+1% all-masked rows)"
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
             "data": "synthetic (N(0,1) encoder outputs, random-init weights, seeded)",
-            "config": {"workload": f"{args.workload}: HybridFusion M={M} B={B}/gpu L={L or 1}"
-                                   f"{'' if L else ' (2-D reference semantics)'} D=H={H} heads={heads} "
-                                   f"C={C} dropout=0.1 train, fwd+CE(ls=0.05)+bwd+AdamW",
-                       "global_batch": B * world, "seq_len": L or 1, "parallelism": f"dp{world}",
+            "config": {"workload": f"{args.workload}: HybridFusion M={M} B={B}/gpu L={lens or 1}"
+                                   f"{'' if max(Ls) else ' (2-D reference semantics)'} D={D} H={H} heads={heads} "
+                                   f"C={C} dropout=0.1 train"
+                                   f"{mask_note}"
+                                   f", fwd+CE(ls=0.05)+bwd+AdamW",
+                       "global_batch": B * world, "seq_len": lens or 1, "parallelism": f"dp{world}",
                        "graph": not args.no_graph},
             "roofline": roofline,
             "cpu_baseline": cpu,
