@@ -1202,25 +1202,26 @@ __global__ __launch_bounds__(NT) void attn_pool_bwd_dk_lean(const AttnArgs A) {
 // workgroup per (pair, sample, head) computes P and dS ONCE, query on the lane
 // (as the dq pass), and produces both gradients from them:
 //   dQ = scale dS K   straight from the registers (dS is the MFMA B operand);
-//   dK = scale dS^T Q through a transposed dS image in LDS, built in two
-//        64-query halves ([key][64 + 4] floats, ds_write_b32 from the
+//   dK = scale dS^T Q through a transposed dS image in LDS, built in four
+//        32-query quarters ([key][32 + 4] floats, ds_write_b32 from the
 //        accumulator layout, ds_read_b128 as the A operand of the key-on-lane
 //        contraction).
 // Against the two passes it saves one S = Q K^T recompute (MFMA), one exp /
 // keep-bit pass (VALU), one read of Q, K, LSE and the keep words, and the D
-// round trip.  LDS at hd <= 32: K, Q images 2 x 18 KB + dS^T half 34 KB -> 2
-// workgroups per CU.
+// round trip.  LDS at hd <= 32: K and Q images, 2 x 18 KB (the dS^T quarters
+// reuse the K image) -> 4 workgroups per CU, whose load phases hide each other.
 template <int HDP>
-__global__ __launch_bounds__(NT, 2) void attn_pool_bwd_fused_lean(const AttnArgs A) {
+__global__ __launch_bounds__(NT, 4) void attn_pool_bwd_fused_lean(const AttnArgs A) {
   constexpr int LS = HDP + 4;
   constexpr int HALF = HDP / 2;
   constexpr int NDT = HDP / 32;
   constexpr int NKT = PKC / 32;
-  constexpr int TS = 64 + 4;   // dS^T image row pitch (floats): one 64-query half
-  __shared__ __attribute__((aligned(16))) float Ks[PKC * LS];
+  constexpr int TS = 32 + 4;   // dS^T image row pitch (floats): one wave's 32 queries
+  static_assert(PKC * TS <= PKC * LS, "the dS^T quarter image reuses the K image");
+  __shared__ __attribute__((aligned(16))) float Ks[PKC * LS];   // K, then the dS^T quarters
   __shared__ __attribute__((aligned(16))) float Qs[PKC * LS];
-  __shared__ __attribute__((aligned(16))) float dsT[PKC * TS];
   __shared__ __attribute__((aligned(16))) float gk[PKC];
+  float* const dsT = Ks;
 
   const AttnPair& P = A.p[blockIdx.y];
   const int bid = blockIdx.x;
@@ -1334,35 +1335,33 @@ __global__ __launch_bounds__(NT, 2) void attn_pool_bwd_fused_lean(const AttnArgs
         }
     }
   }
-  // dK = scale dS^T Q (key on the lane), over two 64-query halves of dS^T in LDS
+  // dK = scale dS^T Q (key on the lane), over four 32-query quarters of dS^T
+  // staged in the K image (K is dead once every wave is past the dQ phase)
   f32x16 dk[NDT];
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) dk[dt] = zero16();
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf) {
-    if (hf) __syncthreads();   // every wave is done reading the first half
-    if ((w >> 1) == hf) {
-      const int ql = (w & 1) * 32 + c;
+  for (int qw = 0; qw < 4; ++qw) {
+    if (qw * 32 >= Lq) break;   // uniform: no queries left
+    __syncthreads();            // K image (qw = 0) / previous quarter no longer read
+    if (w == qw) {
 #pragma unroll
       for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) dsT[(kt * 32 + acc_row(r, h)) * TS + ql] = pr[kt][r];
+        for (int r = 0; r < 16; ++r) dsT[(kt * 32 + acc_row(r, h)) * TS + c] = pr[kt][r];
     }
     __syncthreads();
-    if (kwave && hf * 64 < Lq) {
+    if (kwave) {
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
+      for (int g = 0; g < 4; ++g) {
+        const float4 a4 = *reinterpret_cast<const float4*>(dsT + key * TS + 8 * g + 4 * h);
+        const float av[4] = {a4.x, a4.y, a4.z, a4.w};
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float4 a4 = *reinterpret_cast<const float4*>(dsT + key * TS + qt * 32 + 8 * g + 4 * h);
-          const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+        for (int j = 0; j < 4; ++j) {
+          const int qg = qw * 32 + 8 * g + 4 * h + j;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int qg = hf * 64 + qt * 32 + 8 * g + 4 * h + j;
-#pragma unroll
-            for (int dt = 0; dt < NDT; ++dt) dk[dt] = mfma32(av[j], Qs[qg * LS + dt * 32 + c], dk[dt]);
-          }
+          for (int dt = 0; dt < NDT; ++dt) dk[dt] = mfma32(av[j], Qs[qg * LS + dt * 32 + c], dk[dt]);
         }
+      }
     }
   }
   if (!kwave) return;
