@@ -201,16 +201,19 @@ __device__ __forceinline__ void stage_tile(float* lds, const Operand& op, int64_
   for (int u = 0; u < PER_WAVE; ++u) {
     const int ins = wave * PER_WAVE + u;
     const float* src;
+    // (row_div is wave-uniform and 1 on every hot launch: the division stays off that path)
     if (MODE == MODE_RK) {
       const int row = ins * (64 / S) + lane / S;
       const int slot = (lane % S) ^ swz<DK>(row);
       const int e = min(e0 + row, eext - 1);
       const int k = min(k0 + 4 * slot, kend - 4);
-      src = op.ptr + boff + (int64_t)(e / op.row_div) * op.ld + k;
+      const int er = op.row_div == 1 ? e : e / op.row_div;
+      src = op.ptr + boff + (int64_t)er * op.ld + k;
     } else {
       const int kr = min(k0 + ins * 2 + (lane >> 5), kend - 1);
       const int e = min(e0 + 4 * (lane & 31), eext - 4);
-      src = op.ptr + boff + (int64_t)(kr / op.row_div) * op.ld + e;
+      const int krr = op.row_div == 1 ? kr : kr / op.row_div;
+      src = op.ptr + boff + (int64_t)krr * op.ld + e;
     }
     __builtin_amdgcn_global_load_lds((const void*)src,
                                      (__attribute__((address_space(3))) void*)(lds + ins * 256), 16, 0, 0);
@@ -309,11 +312,19 @@ __global__ __launch_bounds__(NT, (NSTAGE * DK <= 32 ? 4 : 2)) void gemm_lds_kern
     if (k.k0 < k.kend) return k;
     return first_from(k.si + 1);
   };
+  // the staged source's operands, re-read from the kernel arguments only when
+  // the cursor moves to another source
+  Operand opA = args.s[G.src_begin].a, opB = args.s[G.src_begin].b;
+  int op_si = 0;
   auto stage = [&](int buf, const KCursor& k) {
-    const GemmSrc& S = args.s[G.src_begin + k.si];
+    if (k.si != op_si) {
+      opA = args.s[G.src_begin + k.si].a;
+      opB = args.s[G.src_begin + k.si].b;
+      op_si = k.si;
+    }
     float* At = lds + buf * 2 * DTILE;
-    stage_tile<AMODE, DK>(At, S.a, offA, T.i0, G.M, k.k0, k.kend, wave, lane);
-    stage_tile<BMODE, DK>(At + DTILE, S.b, offB, T.j0, G.N, k.k0, k.kend, wave, lane);
+    stage_tile<AMODE, DK>(At, opA, offA, T.i0, G.M, k.k0, k.kend, wave, lane);
+    stage_tile<BMODE, DK>(At + DTILE, opB, offB, T.j0, G.N, k.k0, k.kend, wave, lane);
   };
   // wait until at most `ahead` tiles' DMAs are outstanding (vmcnt needs an immediate)
   auto wait_tiles = [&](int ahead) {
