@@ -567,6 +567,8 @@ __global__ __launch_bounds__(NT) void attn_pool_fwd_kernel(const AttnArgs A) {
   if (P.kmask_mode == 1 && P.kmask[(int64_t)b * P.kmask_ld] == 0.f) {
     // masked key modality: softmax over all -inf -> NaN -> 0 (src/attention.py:127-129)
     for (int k = t; k < Lk; k += NT) pbar[k] = 0.f;
+    if (P.pbarT)
+      for (int k = t; k < Lk; k += NT) P.pbarT[((int64_t)b * Lk + k) * A.heads + head] = 0.f;
     for (int q = t; q < Lq; q += NT) P.lse[bh * Lq + q] = -INFINITY;
     if (P.keep_bits)
       for (int q = t; q < Lq; q += NT)
@@ -651,7 +653,11 @@ __global__ __launch_bounds__(NT) void attn_pool_fwd_kernel(const AttnArgs A) {
   }
   __syncthreads();
   const float inv_lq = 1.f / (float)Lq;
-  for (int k = t; k < Lk; k += NT) pbar[k] = (cs[0][k] + cs[1][k] + cs[2][k] + cs[3][k]) * inv_lq;
+  for (int k = t; k < Lk; k += NT) {
+    const float v = (cs[0][k] + cs[1][k] + cs[2][k] + cs[3][k]) * inv_lq;
+    pbar[k] = v;
+    if (P.pbarT) P.pbarT[((int64_t)b * Lk + k) * A.heads + head] = v;
+  }
 }
 
 // Pooled backward, query on the lane: D = rowsum(P' dpbar)/Lq, dS, dQ.
@@ -901,6 +907,8 @@ __global__ __launch_bounds__(NT) void attn_pool_fwd_lean(const AttnArgs A) {
 
   if (P.kmask_mode == 1 && P.kmask[(int64_t)b * P.kmask_ld] == 0.f) {
     for (int k = t; k < Lk; k += NT) pbar[k] = 0.f;
+    if (P.pbarT)
+      for (int k = t; k < Lk; k += NT) P.pbarT[((int64_t)b * Lk + k) * A.heads + head] = 0.f;
     for (int q = t; q < Lq; q += NT) P.lse[bh * Lq + q] = -INFINITY;
     if (P.keep_bits)
       for (int q = t; q < Lq; q += NT)
@@ -984,7 +992,11 @@ __global__ __launch_bounds__(NT) void attn_pool_fwd_lean(const AttnArgs A) {
   }
   __syncthreads();
   const float inv_lq = 1.f / (float)Lq;
-  for (int k = t; k < Lk; k += NT) pbar[k] = ((cs[0][k] + cs[1][k]) + (cs[2][k] + cs[3][k])) * inv_lq;
+  for (int k = t; k < Lk; k += NT) {
+    const float v = ((cs[0][k] + cs[1][k]) + (cs[2][k] + cs[3][k])) * inv_lq;
+    pbar[k] = v;
+    if (P.pbarT) P.pbarT[((int64_t)b * Lk + k) * A.heads + head] = v;
+  }
 }
 
 // dq pass, query on the lane: G[k] = keep ? dpbar[k] / ((1-p) Lq) : 0;

@@ -98,7 +98,7 @@ inline Operand opnd(const float* p, int ld, int row_div = 1) {
   o.ld = ld;
   o.row_div = row_div;
   o.vec = (ld % 4 == 0) && aligned16(p);
-  o.pad_ = 0;
+  o.seg_stride = 0;
   return o;
 }
 

@@ -316,6 +316,8 @@ __global__ __launch_bounds__(NT, (NSTAGE * DK <= 32 ? 4 : 2)) void gemm_lds_kern
   // the cursor moves to another source
   Operand opA = args.s[G.src_begin].a, opB = args.s[G.src_begin].b;
   int op_si = 0;
+  // per-segment operands (seg_stride != 0): offset by the segment of the tile's first row
+  const int64_t seg = G.seg_rows > 0 ? T.i0 / G.seg_rows : 0;
   auto stage = [&](int buf, const KCursor& k) {
     if (k.si != op_si) {
       opA = args.s[G.src_begin + k.si].a;
@@ -323,8 +325,8 @@ __global__ __launch_bounds__(NT, (NSTAGE * DK <= 32 ? 4 : 2)) void gemm_lds_kern
       op_si = k.si;
     }
     float* At = lds + buf * 2 * DTILE;
-    stage_tile<AMODE, DK>(At, opA, offA, T.i0, G.M, k.k0, k.kend, wave, lane);
-    stage_tile<BMODE, DK>(At + DTILE, opB, offB, T.j0, G.N, k.k0, k.kend, wave, lane);
+    stage_tile<AMODE, DK>(At, opA, offA + seg * opA.seg_stride, T.i0, G.M, k.k0, k.kend, wave, lane);
+    stage_tile<BMODE, DK>(At + DTILE, opB, offB + seg * opB.seg_stride, T.j0, G.N, k.k0, k.kend, wave, lane);
   };
   // wait until at most `ahead` tiles' DMAs are outstanding (vmcnt needs an immediate)
   auto wait_tiles = [&](int ahead) {
@@ -650,6 +652,7 @@ __global__ __launch_bounds__(NT) void gemm_generic_kernel(const GemmArgs args) {
   TileCtx T;
   if (!tile_ctx(G, local, T)) return;
   const int64_t offA = (int64_t)T.batch * G.bs_a, offB = (int64_t)T.batch * G.bs_b;
+  const int64_t seg = G.seg_rows > 0 ? T.i0 / G.seg_rows : 0;
 
   // one LDS object: A and B tiles, reused as the [64][CS] epilogue image
   __shared__ __attribute__((aligned(16))) float sm[2 * BK * LDS_STRIDE];
@@ -690,8 +693,8 @@ __global__ __launch_bounds__(NT) void gemm_generic_kernel(const GemmArgs args) {
     if (kbeg >= kend) continue;
     const int ntk = (kend - kbeg + BK - 1) / BK;
     TileRegs ra, rb;
-    load_tile<AMODE>(ra, S.a, offA, T.i0, G.M, kbeg, kend);
-    load_tile<BMODE>(rb, S.b, offB, T.j0, G.N, kbeg, kend);
+    load_tile<AMODE>(ra, S.a, offA + seg * S.a.seg_stride, T.i0, G.M, kbeg, kend);
+    load_tile<BMODE>(rb, S.b, offB + seg * S.b.seg_stride, T.j0, G.N, kbeg, kend);
     for (int kt = 0; kt < ntk; ++kt) {
       __syncthreads();
       store_tile<AMODE>(ra, As);
@@ -699,8 +702,8 @@ __global__ __launch_bounds__(NT) void gemm_generic_kernel(const GemmArgs args) {
       __syncthreads();
       if (kt + 1 < ntk) {
         const int kn = kbeg + (kt + 1) * BK;
-        load_tile<AMODE>(ra, S.a, offA, T.i0, G.M, kn, kend);
-        load_tile<BMODE>(rb, S.b, offB, T.j0, G.N, kn, kend);
+        load_tile<AMODE>(ra, S.a, offA + seg * S.a.seg_stride, T.i0, G.M, kn, kend);
+        load_tile<BMODE>(rb, S.b, offB + seg * S.b.seg_stride, T.j0, G.N, kn, kend);
       }
       if (want_db && t < BM) {
 #pragma unroll 8

@@ -40,6 +40,7 @@ struct Saved {
   float *V[MMF_MAX_PAIRS], *O[MMF_MAX_PAIRS], *A[MMF_MAX_PAIRS];
   // pooled plan
   float *pbar[MMF_MAX_PAIRS], *U[MMF_MAX_PAIRS], *r[MMF_MAX_PAIRS], *Ob[MMF_MAX_PAIRS], *Ab[MMF_MAX_PAIRS];
+  float* pbarT[MMF_MAX_PAIRS];   // (B, Lk, heads): pbar as the RK operand of the dZ GEMM's E_m term
   uint32_t* bits[MMF_MAX_PAIRS];
   float *pooled, *scores, *weights, *fused, *h1;
 };
@@ -58,6 +59,7 @@ void layout_saved(const mmf_hybrid_desc* d, Bump& bp, Saved& s) {
     s.lse[g] = bp.take<float>(B * nh * lq);
     if (pool) {
       s.pbar[g] = bp.take<float>(B * nh * lk);
+      s.pbarT[g] = bp.take<float>(B * nh * lk);
       s.U[g] = bp.take<float>(B * nh * H);
       s.r[g] = bp.take<float>(B * nh);
       s.Ob[g] = bp.take<float>(B * H);
@@ -189,14 +191,14 @@ void plan_wgrads(const mmf_hybrid_desc* d, const float* const* x, const float* m
 
 size_t saved_bytes(const mmf_hybrid_desc* d) {
   Bump bp(nullptr);
-  Saved s;
+  Saved s{};
   layout_saved(d, bp, s);
   return bp.off + 256;
 }
 
 size_t workspace_bytes(const mmf_hybrid_desc* d) {
   Bump bs(nullptr);
-  Saved s;
+  Saved s{};
   layout_saved(d, bs, s);
   Bump bw(nullptr);
   Ws w;
@@ -282,6 +284,7 @@ AttnPair make_pair(const mmf_hybrid_desc* d, const Saved& s, const float* mask, 
   a.ldq = a.ldk = a.ldv = a.ldo = d->hidden;
   a.drop_site = SITE_ATTN + g;
   a.pbar = s.pbar[g];
+  a.pbarT = s.pbarT[g];
   a.keep_bits = s.bits[g];
   return a;
 }
@@ -300,6 +303,18 @@ size_t mmf_hybrid_workspace_bytes(const mmf_hybrid_desc* d) {
   return workspace_bytes(d);
 }
 
+namespace {
+
+// dZ_m takes its value-path term E_m as extra K = heads sources of the dZ GEMM
+// (pbarT against the per-sample dU) when a 128-row tile never straddles two
+// samples and the pbarT rows are float4-able; otherwise pool_e materialises E_m.
+bool poole_in_dz(const mmf_hybrid_desc* d, int m) {
+  if (getenv("MMF_NO_POOLE")) return false;
+  return Lm(d, m) % 128 == 0 && d->hidden % 4 == 0 && d->num_heads % 4 == 0;
+}
+
+}  // namespace
+
 int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, const float* const* x,
                        const float* mask, const uint64_t* rng_state, void* saved, float* logits,
                        float* fusion_weights, float* const* attn_maps, void* stream) {
@@ -315,7 +330,7 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
   if (drop && !rng_state) return fail(MMF_EINVAL, "training with dropout needs rng_state");
 
   Bump bp(saved);
-  Saved s;
+  Saved s{};
   layout_saved(d, bp, s);
   if (rng_state) STAGE_TRY("fwd.rng", launch_rng_snapshot(rng_state, s.rng, st));
   const RngSnap* rng = rng_state ? s.rng : nullptr;
@@ -469,7 +484,7 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
   const bool pool = use_pool(d);
 
   Bump bs(const_cast<void*>(saved));
-  Saved s;
+  Saved s{};
   layout_saved(d, bs, s);
   const RngSnap* rng = s.rng;
   Bump bw(workspace);
@@ -564,21 +579,24 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
     } else {
       HIP_TRY(fe);
     }
-    std::vector<PoolEMod> em(M);
+    std::vector<PoolEMod> em;
     for (int m = 0; m < M; ++m) {
-      memset(&em[m], 0, sizeof(PoolEMod));
-      em[m].out = w.E[m];
-      em[m].L = Lm(d, m);
-      em[m].c = w.cvec + (size_t)m * H;
-      em[m].ldc = M * H;
-      em[m].cscale = 1.f / (float)Lm(d, m);
+      if (poole_in_dz(d, m)) continue;   // E_m is formed in the dZ GEMM's epilogue instead
+      em.emplace_back();
+      PoolEMod& e = em.back();
+      memset(&e, 0, sizeof(PoolEMod));
+      e.out = w.E[m];
+      e.L = Lm(d, m);
+      e.c = w.cvec + (size_t)m * H;
+      e.ldc = M * H;
+      e.cscale = 1.f / (float)Lm(d, m);
       for (int g = 0; g < d->num_pairs; ++g)
         if (d->pair_k[g] == m) {
-          em[m].pbar[em[m].nsrc] = s.pbar[g];
-          em[m].du[em[m].nsrc++] = w.dU[g];
+          e.pbar[e.nsrc] = s.pbar[g];
+          e.du[e.nsrc++] = w.dU[g];
         }
     }
-    STAGE_TRY("bwd.pool_e", launch_pool_e(em.data(), M, B, nh, H, st));
+    if (!em.empty()) STAGE_TRY("bwd.pool_e", launch_pool_e(em.data(), (int)em.size(), B, nh, H, st));
   } else if (d->num_pairs) {
     // (3g) dA_g rows = c_q / L_q broadcast: dO = dA W_o; flash attention backward
     std::vector<GemmJob> jobs;
@@ -599,8 +617,9 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
     std::vector<GemmJob> jobs;
     for (int m = 0; m < M; ++m) {
       const int L = Lm(d, m);
-      GemmJob j = make_job(B * L, H, w.dZ[m], H, EPI_GATE | (pool ? EPI_ADDMAT : EPI_ROWADD));
-      if (pool) {
+      const bool pe = pool && poole_in_dz(d, m);
+      GemmJob j = make_job(B * L, H, w.dZ[m], H, EPI_GATE | (pool && !pe ? EPI_ADDMAT : EPI_ROWADD));
+      if (pool && !pe) {
         j.g.addm = w.E[m];
         j.g.ld_addm = H;
       } else {
@@ -618,6 +637,17 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
           add_src(j, opnd(w.dK[g], H), opnd(W->k[g].w, H), H);
           if (!pool) add_src(j, opnd(w.dV[g], H), opnd(W->v[g].w, H), H);
         }
+      }
+      if (pe) {
+        // E_m = c_m / L (the ROWADD above) + sum over pairs keyed by m of pbar^T dU: per sample a
+        // K = heads contraction, rows b*L + l of pbarT (B, L, heads) against dU_b (heads, H)
+        j.g.seg_rows = L;
+        for (int g = 0; g < d->num_pairs; ++g)
+          if (d->pair_k[g] == m && j.nsrc < GEMM_MAX_SRCS) {
+            Operand du = opnd(w.dU[g], H);
+            du.seg_stride = nh * H;
+            add_src(j, opnd(s.pbarT[g], nh), du, nh);
+          }
       }
       if (j.nsrc > GEMM_MAX_SRCS) return fail(MMF_ELIMIT, "too many gradient sources");
       jobs.push_back(j);

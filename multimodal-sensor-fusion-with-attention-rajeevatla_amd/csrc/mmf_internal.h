@@ -58,7 +58,8 @@ struct Operand {
   int32_t ld;                // stored row stride (elements)
   int32_t row_div;           // >= 1
   int32_t vec;               // 1 => 16-byte aligned rows, float4 loads allowed
-  int32_t pad_;
+  int32_t seg_stride;        // != 0: + (tile's first row / group seg_rows) * seg_stride elements
+                             // (a per-sample operand, e.g. dU (B, heads, H) against rows b*L + l)
 };
 
 struct GemmSrc {
@@ -98,6 +99,7 @@ struct GemmGroup {
   // bias by i*bs_bias and bias_rs_off by i*bs_brs.
   int32_t nbatch;
   int32_t bs_a, bs_b, bs_c, bs_bias, bs_brs;
+  int32_t seg_rows;        // rows per segment for operands with seg_stride (a tile never straddles two)
 };
 
 constexpr int GEMM_MAX_GROUPS = 12;
@@ -173,6 +175,7 @@ struct AttnPair {
   float* probs;        // (B, heads, Lq, Lk) output of attn_probs
   // pooled-output formulation (HybridFusion): only column means of P' are needed
   float* pbar;         // (B, heads, Lk) fwd output: mean over queries of the post-dropout probs
+  float* pbarT;        // optional (B, Lk, heads) copy of pbar (an RK GEMM operand for E_m)
   const float* dpbar;  // (B, heads, Lk) bwd input: d loss / d pbar
   uint32_t* keep_bits; // (B, heads, Lq, 4) dropout keep mask written by the pooled forward
                        // (Lk <= 128: bit k%32 of word k/32), read by its backward
