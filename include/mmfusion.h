@@ -195,6 +195,25 @@ int mmf_late_fusion_backward(int32_t batch, int32_t num_modalities, int32_t num_
                              float* dweight_logits, void* workspace, void* stream);
 
 /* ---------------------------------------------------------------------
+ * Manifest data path (src/data.py:110-343, MultimodalDataset over .pt shards
+ * {columns, data (rows, ncols)}): gather a batch of chunk windows from the
+ * HBM-resident shard table into per-modality tensors.
+ *   table (rows, ncols) fp32 device; chunk_row0 (B) int64 / chunk_len (B)
+ *   int32 device (first table row and length <= T of each chunk); cols: device
+ *   int32, the selected columns of every modality concatenated; col_offsets:
+ *   HOST int32[num_modalities + 1] (modality m = cols[off[m] .. off[m+1]));
+ *   out: HOST array of num_modalities device pointers, out[m] (B, T, c_m).
+ * Values are nan_to_num'd (NaN / +-inf -> 0, src/data.py:289-291); rows t >=
+ * chunk_len[b] are zero.  With labels != NULL: labels[b] = activity_id of the
+ * chunk's first row, and *mismatch (device int32, caller-zeroed) counts rows
+ * whose activity_id differs (the reference raises, src/data.py:283-284).
+ * ------------------------------------------------------------------- */
+int mmf_gather_chunks(const float* table, int64_t rows, int32_t ncols, const int64_t* chunk_row0,
+                      const int32_t* chunk_len, int32_t batch, int32_t T, int32_t num_modalities,
+                      const int32_t* cols, const int32_t* col_offsets, float* const* out,
+                      int32_t label_col, int64_t* labels, int32_t* mismatch, void* stream);
+
+/* ---------------------------------------------------------------------
  * Training-step helpers used by the data-parallel step (not part of the
  * reference interface; the reference uses torch.optim.AdamW via Lightning,
  * src/train.py:374-414).
