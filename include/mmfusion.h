@@ -214,6 +214,35 @@ int mmf_gather_chunks(const float* table, int64_t rows, int32_t ncols, const int
                       int32_t label_col, int64_t* labels, int32_t* mismatch, void* stream);
 
 /* ---------------------------------------------------------------------
+ * LSTM recurrence (SequenceEncoder's nn.LSTM, src/encoders.py:67-75 / 135-166;
+ * torch.nn.LSTM semantics, gate order i, f, g, o, zero initial state).
+ * One persistent launch runs all `steps` time steps of up to 4 independent
+ * LSTMs (one per modality); the input projection xproj = x W_ih^T + b_ih +
+ * b_hh and the weight gradients are time-parallel GEMMs left to the caller.
+ * Each LSTM's batch is split into instances of <= 4 rows that run side by
+ * side (G = hidden / 64 workgroups of 1024 threads each, all co-resident).
+ * Limits: hidden a multiple of 64 up to 256, num_lstm <= 8,
+ * num_lstm * ceil(batch / 4) <= 32.
+ * Arrays are HOST arrays of num_lstm device pointers:
+ *   xproj (B, T, 4H), w_hh (4H, H), h / c (B, T, H), gates (B, T, 4H) =
+ *   activated (i, f, g, o) saved for the backward;
+ *   dh (B, T, H) upstream gradient of every h_t (entries may be NULL = 0),
+ *   dgates (B, T, 4H) = gradient of the pre-activation gates (= d xproj;
+ *   dW_hh = sum_t dgates_t^T h_{t-1}).
+ * sync[i]: device scratch of mmf_lstm_sync_bytes(batch, hidden) bytes per
+ * LSTM (re-zeroed on the stream by every call).  timeout: device uint32 the
+ * kernel ORs 1 into if an inter-workgroup wait gives up (results invalid).
+ * ------------------------------------------------------------------- */
+size_t mmf_lstm_sync_bytes(int32_t batch, int32_t hidden);
+int mmf_lstm_forward(int32_t num_lstm, int32_t batch, int32_t steps, int32_t hidden, const float* const* xproj,
+                     const float* const* w_hh, float* const* h, float* const* c, float* const* gates,
+                     void* const* sync, uint32_t* timeout, void* stream);
+int mmf_lstm_backward(int32_t num_lstm, int32_t batch, int32_t steps, int32_t hidden,
+                      const float* const* w_hh, const float* const* c, const float* const* gates,
+                      const float* const* dh, float* const* dgates, void* const* sync, uint32_t* timeout,
+                      void* stream);
+
+/* ---------------------------------------------------------------------
  * Training-step helpers used by the data-parallel step (not part of the
  * reference interface; the reference uses torch.optim.AdamW via Lightning,
  * src/train.py:374-414).

@@ -16,15 +16,23 @@ softmax over frames, nan_to_num, weighted sum -- runs forward and backward as
 the HIP kernels behind mmf_attention_pool_forward / _backward
 (csrc/softmax_pool.hip).  The frame MLP and the projection are nn.Linear
 layers on PyTorch-ROCm (encoders are outside the fused path), and the
-'average' / 'max' pooling branches stay plain torch (:288-305).  Only
-FrameEncoder lives here: the reference's other encoders are not on the path.
+'average' / 'max' pooling branches stay plain torch (:288-305).  
+SequenceEncoder (src/encoders.py:34-166) mirrors the
+reference's 'lstm' branch: the same constructor, parameter names
+(rnn.weight_ih_l{k}, rnn.weight_hh_l{k}, rnn.bias_*, projection.*), forward
+(sequence, lengths=None) and errors.  The recurrence runs as one persistent
+HIP launch per layer (csrc/lstm.hip, mmf_lstm_forward / _backward); the
+time-parallel input projection and weight gradients are rocBLAS GEMMs.
+``encode_sequences`` batches the LSTMs of several modalities into the same
+launches.  The 'gru' / 'cnn' / 'transformer' encoder types are not on the
+path and raise NotImplementedError.
 """
 
 from __future__ import annotations
 
 import os
 import sys
-from typing import Any, Optional, cast
+from typing import Any, Dict, List, Optional, Sequence, cast
 
 import torch
 import torch.nn as nn
@@ -130,3 +138,195 @@ class FrameEncoder(nn.Module):
         if self.attention is None:
             raise RuntimeError("Attention layer not initialized.")
         return attention_pool(frames, self.attention, mask)
+
+
+# ---------------------------------------------------------------------------
+# SequenceEncoder (LSTM) on the persistent HIP recurrence
+# ---------------------------------------------------------------------------
+
+_LSTM_TIMEOUT: Dict[int, torch.Tensor] = {}
+
+
+def _timeout_flag(dev: torch.device) -> torch.Tensor:
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    t = _LSTM_TIMEOUT.get(idx)
+    if t is None:
+        t = torch.zeros(1, dtype=torch.int32, device=dev)
+        _LSTM_TIMEOUT[idx] = t
+    return t
+
+
+def lstm_timed_out(device=None) -> bool:
+    """True if any LSTM launch on `device` gave up an inter-workgroup wait (results invalid)."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    return bool(int(_timeout_flag(dev).item()))
+
+
+class _LstmLayersFunction(torch.autograd.Function):
+    """One LSTM layer of n independent LSTMs (same B, T, H): h_l = LSTM(x_l) for each l.
+
+    inputs: n, then n x (x, w_ih, w_hh, b_ih, b_hh); outputs: n x h (B, T, H)."""
+
+    @staticmethod
+    def forward(ctx, n, *flat):
+        L = _nat.lib()
+        xs = [_nat.f32c(flat[5 * i]) for i in range(n)]
+        w_ih = [flat[5 * i + 1] for i in range(n)]
+        w_hh = [_nat.f32c(flat[5 * i + 2]) for i in range(n)]
+        b_ih = [flat[5 * i + 3] for i in range(n)]
+        b_hh = [flat[5 * i + 4] for i in range(n)]
+        dev = xs[0].device
+        B, T, _ = xs[0].shape
+        H = w_hh[0].shape[1]
+        xproj = [torch.addmm(b_ih[i] + b_hh[i], xs[i].reshape(B * T, -1), w_ih[i].t()).view(B, T, 4 * H)
+                 for i in range(n)]
+        hs = [torch.empty(B, T, H, dtype=torch.float32, device=dev) for _ in range(n)]
+        cs = [torch.empty(B, T, H, dtype=torch.float32, device=dev) for _ in range(n)]
+        gates = [torch.empty(B, T, 4 * H, dtype=torch.float32, device=dev) for _ in range(n)]
+        sb = L.mmf_lstm_sync_bytes(B, H)
+        sync = torch.empty(n, sb, dtype=torch.uint8, device=dev)
+        rc = L.mmf_lstm_forward(
+            n, B, T, H, _nat.ptr_array([t.data_ptr() for t in xproj]), _nat.ptr_array([w.data_ptr() for w in w_hh]),
+            _nat.ptr_array([t.data_ptr() for t in hs]), _nat.ptr_array([t.data_ptr() for t in cs]),
+            _nat.ptr_array([t.data_ptr() for t in gates]), _nat.ptr_array([sync[i].data_ptr() for i in range(n)]),
+            _timeout_flag(dev).data_ptr(), _nat.stream_ptr(dev))
+        _nat.check(rc, "LSTM forward")
+        ctx.n = n
+        ctx.save_for_backward(*xs, *w_ih, *w_hh, *hs, *cs, *gates)
+        return tuple(hs)
+
+    @staticmethod
+    def backward(ctx, *dhs):
+        L = _nat.lib()
+        n = ctx.n
+        sv = ctx.saved_tensors
+        xs, w_ih, w_hh, hs, cs, gates = (sv[k * n:(k + 1) * n] for k in range(6))
+        dev = xs[0].device
+        B, T, _ = xs[0].shape
+        H = w_hh[0].shape[1]
+        dh = [None if d is None else _nat.f32c(d) for d in dhs]
+        dgates = [torch.empty(B, T, 4 * H, dtype=torch.float32, device=dev) for _ in range(n)]
+        sync = torch.empty(n, L.mmf_lstm_sync_bytes(B, H), dtype=torch.uint8, device=dev)
+        rc = L.mmf_lstm_backward(
+            n, B, T, H, _nat.ptr_array([w.data_ptr() for w in w_hh]), _nat.ptr_array([t.data_ptr() for t in cs]),
+            _nat.ptr_array([t.data_ptr() for t in gates]), _nat.ptr_array([0 if d is None else d.data_ptr() for d in dh]),
+            _nat.ptr_array([t.data_ptr() for t in dgates]), _nat.ptr_array([sync[i].data_ptr() for i in range(n)]),
+            _timeout_flag(dev).data_ptr(), _nat.stream_ptr(dev))
+        _nat.check(rc, "LSTM backward")
+        grads: List[Optional[torch.Tensor]] = [None]
+        for i in range(n):
+            dg = dgates[i].view(B * T, 4 * H)
+            x2 = xs[i].reshape(B * T, -1)
+            dx = (dg @ w_ih[i]).view_as(xs[i]) if ctx.needs_input_grad[1 + 5 * i] else None
+            dw_ih = dg.t() @ x2
+            dw_hh = dgates[i][:, 1:].reshape(-1, 4 * H).t() @ hs[i][:, :-1].reshape(-1, H)
+            db = dg.sum(0)
+            grads += [dx, dw_ih, dw_hh, db, db]
+        return tuple(grads)
+
+
+def lstm_layers(rnns: Sequence[nn.LSTM], inputs: Sequence[torch.Tensor]) -> List[torch.Tensor]:
+    """Run several nn.LSTM parameter sets (batch_first, zero initial state) over their inputs on the
+    HIP recurrence, every layer of all of them in one launch; returns each LSTM's top-layer output
+    sequence (B, T, H).  Inter-layer dropout follows nn.LSTM (training only)."""
+    n = len(rnns)
+    if n == 0:
+        return []
+    H = rnns[0].hidden_size
+    layers = rnns[0].num_layers
+    for r in rnns:
+        if not r.batch_first or r.bidirectional or r.proj_size or not r.bias:
+            raise NotImplementedError("LSTM path: batch_first, unidirectional, biased, no projection")
+        if r.hidden_size != H or r.num_layers != layers:
+            raise ValueError("lstm_layers: all LSTMs need the same hidden_size and num_layers")
+    B, T = inputs[0].shape[:2]
+    for x in inputs:
+        _nat.require_device(x, "SequenceEncoder input")
+        if x.shape[:2] != (B, T):
+            raise ValueError("lstm_layers: all sequences need the same (batch, seq_len)")
+    cur = list(inputs)
+    for k in range(layers):
+        flat: List[torch.Tensor] = []
+        for r, x in zip(rnns, cur):
+            flat += [x, getattr(r, f"weight_ih_l{k}"), getattr(r, f"weight_hh_l{k}"),
+                     getattr(r, f"bias_ih_l{k}"), getattr(r, f"bias_hh_l{k}")]
+        outs = _LstmLayersFunction.apply(n, *flat)
+        cur = list(outs)
+        if k + 1 < layers:
+            cur = [torch.nn.functional.dropout(o, rnns[i].dropout, rnns[i].training) for i, o in enumerate(cur)]
+    return cur
+
+
+def _final_state(out: torch.Tensor, lengths: Optional[torch.Tensor]) -> torch.Tensor:
+    if lengths is None:
+        return out[:, -1]
+    idx = lengths.to(device=out.device, dtype=torch.int64) - 1
+    if bool((idx < 0).any()) or bool((idx >= out.shape[1]).any()):
+        raise RuntimeError("lengths must be in [1, seq_len]")
+    return out[torch.arange(out.shape[0], device=out.device), idx]
+
+
+class SequenceEncoder(nn.Module):
+    """Time-series sequence -> fixed embedding (src/encoders.py:22-166), 'lstm' on the HIP path."""
+
+    encoder_type: str
+    hidden_dim: int
+    output_dim: int
+    rnn: Optional[nn.LSTM]
+    conv_net: Optional[nn.Module]
+    pool: Optional[nn.Module]
+    input_projection: Optional[nn.Linear]
+    transformer: Optional[nn.TransformerEncoder]
+    projection: nn.Module
+
+    def __init__(self, input_dim: int, hidden_dim: int = 256, output_dim: int = 128, num_layers: int = 2,
+                 encoder_type: str = "lstm", dropout: float = 0.1):
+        super().__init__()
+        cast_self = cast(Any, self)
+        cast_self.encoder_type = encoder_type
+        cast_self.hidden_dim = hidden_dim
+        cast_self.output_dim = output_dim
+        self.dropout_layer = nn.Dropout(dropout)
+        cast_self.rnn = None
+        cast_self.conv_net = None
+        cast_self.pool = None
+        cast_self.input_projection = None
+        cast_self.transformer = None
+        self.projection = nn.Identity()
+        if encoder_type == "lstm":
+            cast_self.rnn = nn.LSTM(input_dim, hidden_dim, num_layers=num_layers, batch_first=True,
+                                    dropout=dropout if num_layers > 1 else 0.0)
+            self.projection = nn.Linear(hidden_dim, output_dim)
+        elif encoder_type in ("gru", "cnn", "transformer"):
+            raise NotImplementedError(f"encoder_type '{encoder_type}' is not on the MI355X path (only 'lstm')")
+        else:
+            raise ValueError(f"Unknown encoder type: {encoder_type}")
+
+    def encode_final_state(self, final_state: torch.Tensor) -> torch.Tensor:
+        return self.projection(self.dropout_layer(final_state))
+
+    def forward(self, sequence: torch.Tensor, lengths: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if sequence.dim() != 3:
+            raise ValueError(f"Expected 3D input sequence, got shape {sequence.shape}")
+        if self.rnn is None:
+            raise RuntimeError("RNN module not initialized.")
+        out = lstm_layers([self.rnn], [sequence])[0]
+        return self.encode_final_state(_final_state(out, lengths))
+
+
+def encode_sequences(encoders: Dict[str, SequenceEncoder], sequences: Dict[str, torch.Tensor],
+                     lengths: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+    """{m: encoders[m](sequences[m], lengths)} with every modality's LSTM layers sharing launches
+    (the modalities of one chunk have the same (B, T))."""
+    names = list(sequences)
+    for m in names:
+        if sequences[m].dim() != 3:
+            raise ValueError(f"Expected 3D input sequence, got shape {sequences[m].shape}")
+    rnns = []
+    for m in names:
+        r = encoders[m].rnn
+        if r is None:
+            raise RuntimeError("RNN module not initialized.")
+        rnns.append(r)
+    outs = lstm_layers(rnns, [sequences[m] for m in names])
+    return {m: encoders[m].encode_final_state(_final_state(o, lengths)) for m, o in zip(names, outs)}

@@ -30,6 +30,7 @@ EXPORTED_SYMBOLS = (
     "mmf_attention_pool_workspace_bytes", "mmf_attention_pool_forward", "mmf_attention_pool_backward",
     "mmf_late_fusion_workspace_bytes", "mmf_late_fusion_forward", "mmf_late_fusion_backward",
     "mmf_gather_chunks",
+    "mmf_lstm_sync_bytes", "mmf_lstm_forward", "mmf_lstm_backward",
 )
 
 
@@ -138,6 +139,12 @@ def lib() -> ctypes.CDLL:
     L.mmf_gather_chunks.argtypes = [vp, c_int64, c_int32, vp, vp, c_int32, c_int32, c_int32, vp, vp, vp, c_int32,
                                      vp, vp, vp]
     L.mmf_gather_chunks.restype = c_int32
+    L.mmf_lstm_sync_bytes.argtypes = [c_int32, c_int32]
+    L.mmf_lstm_sync_bytes.restype = c_size_t
+    L.mmf_lstm_forward.argtypes = [c_int32, c_int32, c_int32, c_int32, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.mmf_lstm_forward.restype = c_int32
+    L.mmf_lstm_backward.argtypes = [c_int32, c_int32, c_int32, c_int32, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.mmf_lstm_backward.restype = c_int32
     L.mmf_last_error.argtypes = []
     L.mmf_last_error.restype = ctypes.c_char_p
     L.mmf_version.argtypes = []

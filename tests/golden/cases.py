@@ -401,3 +401,51 @@ def late_inputs(case: LateCase):
     mask = np.asarray(case.mask, dtype=np.float32)
     grad = rng.standard_normal((case.batch, case.classes)).astype(np.float32)
     return feats, mask, grad
+
+
+@dataclass
+class SeqEncCase:
+    """SequenceEncoder(encoder_type="lstm") (src/encoders.py:34-166)."""
+    name: str
+    batch: int
+    steps: int
+    input_dim: int
+    hidden: int
+    out_dim: int
+    layers: int
+    seed: int
+    lengths: Optional[List[int]] = None
+
+
+SEQENC_CASES: List[SeqEncCase] = [
+    SeqEncCase("seqenc_1layer", batch=3, steps=40, input_dim=17, hidden=64, out_dim=16, layers=1, seed=91),
+    # batch 6 -> instances of 4 + 2 rows; packed-sequence lengths incl. 1 and full
+    SeqEncCase("seqenc_2layer_len", batch=6, steps=25, input_dim=9, hidden=128, out_dim=8, layers=2, seed=92,
+               lengths=[25, 10, 1, 25, 7, 3]),
+    # the C3 encoder shape (imu 17 features, hidden 256 -> 128)
+    SeqEncCase("seqenc_h256", batch=2, steps=48, input_dim=17, hidden=256, out_dim=128, layers=1, seed=93),
+]
+
+
+def seqenc_state(case: SeqEncCase) -> "OrderedDict[str, np.ndarray]":
+    rng = np.random.default_rng(case.seed)
+    sd: "OrderedDict[str, np.ndarray]" = OrderedDict()
+    H = case.hidden
+    bound = 1.0 / np.sqrt(H)
+    for k in range(case.layers):
+        in_f = case.input_dim if k == 0 else H
+        sd[f"rnn.weight_ih_l{k}"] = rng.uniform(-bound, bound, size=(4 * H, in_f)).astype(np.float32)
+        sd[f"rnn.weight_hh_l{k}"] = rng.uniform(-bound, bound, size=(4 * H, H)).astype(np.float32)
+        sd[f"rnn.bias_ih_l{k}"] = rng.uniform(-bound, bound, size=(4 * H,)).astype(np.float32)
+        sd[f"rnn.bias_hh_l{k}"] = rng.uniform(-bound, bound, size=(4 * H,)).astype(np.float32)
+    sd["projection.weight"], sd["projection.bias"] = _linear(rng, case.out_dim, H)
+    return sd
+
+
+def seqenc_inputs(case: SeqEncCase):
+    """(sequence (B, T, D), lengths or None, upstream grad of the encoding (B, out))."""
+    rng = np.random.default_rng(case.seed + 15485863)
+    seq = rng.standard_normal((case.batch, case.steps, case.input_dim)).astype(np.float32)
+    lengths = np.array(case.lengths, dtype=np.int64) if case.lengths is not None else None
+    g_out = rng.standard_normal((case.batch, case.out_dim)).astype(np.float32)
+    return seq, lengths, g_out

@@ -34,10 +34,10 @@ HERE = Path(__file__).resolve().parent
 sys.path.insert(0, str(HERE))
 REF_SRC = Path("/root/reference/src")
 
-from cases import (CMA_CASES, FRAMEPOOL_CASES, HYBRID_CASES, LATE_CASES, PAIRWISE_CASES,  # noqa: E402
+from cases import (CMA_CASES, FRAMEPOOL_CASES, HYBRID_CASES, LATE_CASES, PAIRWISE_CASES, SEQENC_CASES,  # noqa: E402
                    TEMPORAL_CASES, cma_inputs, cma_state, framepool_inputs, framepool_state,
                    hybrid_inputs, hybrid_state, late_inputs, late_state, pair_names,
-                   pairwise_inputs, pairwise_state, temporal_inputs)
+                   pairwise_inputs, pairwise_state, temporal_inputs, seqenc_inputs, seqenc_state)
 
 
 def _load_reference():
@@ -250,6 +250,26 @@ def gen_late(ref_fusion, case):
     return out
 
 
+def gen_seqenc(ref_encoders, case):
+    """SequenceEncoder(encoder_type="lstm") (src/encoders.py:34-166): encoding, top-layer output
+    sequence, and gradients of sum(encoding * g) w.r.t. the sequence and every parameter."""
+    model = ref_encoders.SequenceEncoder(case.input_dim, hidden_dim=case.hidden, output_dim=case.out_dim,
+                                         num_layers=case.layers, encoder_type="lstm", dropout=0.1)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in seqenc_state(case).items()}, strict=True)
+    model.eval()
+    seq_np, len_np, g_out = seqenc_inputs(case)
+    seq = torch.from_numpy(seq_np).requires_grad_(True)
+    lengths = torch.from_numpy(len_np) if len_np is not None else None
+    enc = model(seq, lengths)
+    (enc * torch.from_numpy(g_out)).sum().backward()
+    with torch.no_grad():
+        outputs, _ = model.rnn(torch.from_numpy(seq_np))
+    out = {"encoding": enc.detach().numpy(), "dsequence": seq.grad.numpy(), "outputs": outputs.numpy()}
+    for name, p in model.named_parameters():
+        out[f"grad/{name}"] = p.grad.numpy()
+    return out
+
+
 def main():
     only = set(sys.argv[1].split(",")) if len(sys.argv) > 1 else None   # e.g. seq_c2_b3,seq_lean_hd64
     torch.set_float32_matmul_precision("highest")
@@ -263,7 +283,8 @@ def main():
         print(f"wrote {case.name}.npz ({sum(a.nbytes for a in out.values())} B raw)")
     for cases, gen, mod in ((CMA_CASES, gen_cma, ref_attention), (TEMPORAL_CASES, gen_temporal, ref_attention),
                             (PAIRWISE_CASES, gen_pairwise, ref_attention),
-                            (FRAMEPOOL_CASES, gen_framepool, ref_encoders), (LATE_CASES, gen_late, ref_fusion)):
+                            (FRAMEPOOL_CASES, gen_framepool, ref_encoders), (LATE_CASES, gen_late, ref_fusion),
+                            (SEQENC_CASES, gen_seqenc, ref_encoders)):
         for case in cases:
             if only and case.name not in only:
                 continue

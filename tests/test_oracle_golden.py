@@ -134,3 +134,23 @@ def test_oracle_late_matches_reference(case):
         assert rel_err(feats[m].grad, fx[f"dx/{m}"]) <= TOL
     for k, p in params.items():
         assert close(p.grad, fx[f"grad/{k}"], TOL, 1e-7), k
+
+
+# --------------------------------------------------------------------------
+# §8(f) SequenceEncoder (LSTM)
+# --------------------------------------------------------------------------
+from cases import SEQENC_CASES, seqenc_inputs, seqenc_state  # noqa: E402
+
+
+@pytest.mark.parametrize("case", SEQENC_CASES, ids=lambda c: c.name)
+def test_oracle_seqenc_matches_reference(case):
+    from oracle.lstm_cpu import sequence_encoder
+    fx = load_fixture(case.name)
+    params = seqenc_state(case)
+    seq, lengths, g_out = seqenc_inputs(case)
+    enc, outputs, dseq, grads = sequence_encoder(params, case.layers, seq, lengths, g_out)
+    assert rel_err(torch.from_numpy(enc), fx["encoding"]) <= TOL
+    assert rel_err(torch.from_numpy(outputs), fx["outputs"]) <= TOL
+    assert rel_err(torch.from_numpy(dseq), fx["dsequence"]) <= TOL
+    for k, g in grads.items():
+        assert close(torch.from_numpy(g), fx[f"grad/{k}"], TOL, 1e-7), k
