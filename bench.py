@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import re
 import os
 import sys
 import time
@@ -31,6 +32,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "HybridFusion fwd+bwd samples/sec at 1/2/4/8 MI355X; CPU-ref parity"
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+BF16_MFMA_PEAK_TFLOPS = 16 * FP32_MFMA_PEAK_TFLOPS   # ~2.5 PF dense: v_mfma_f32_32x32x16_bf16 (16x the f32 rate)
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 
 # Per-GPU workloads (BASELINE.json configs; the headline is configs[1] = "c2").
@@ -80,10 +82,12 @@ def kernel_table(launches, steps):
     out = {}
     for kname, (ms, n, flops, nbytes) in sorted(acc.items(), key=lambda kv: -kv[1][0]):
         sec = ms * 1e-3
-        t_f = flops / (FP32_MFMA_PEAK_TFLOPS * 1e12)
+        # bf16-operand instantiations (matmul precision "medium") end in ", true>"
+        fpeak = BF16_MFMA_PEAK_TFLOPS if re.search(r"[<, ]true>$", kname) else FP32_MFMA_PEAK_TFLOPS
+        t_f = flops / (fpeak * 1e12)
         t_b = nbytes / (HBM_PEAK_GBS * 1e9)
         if t_f >= t_b:
-            bound, ach, peak, unit = "mfma", flops / sec / 1e12 if sec else 0.0, FP32_MFMA_PEAK_TFLOPS, "TFLOP/s"
+            bound, ach, peak, unit = "mfma", flops / sec / 1e12 if sec else 0.0, fpeak, "TFLOP/s"
         else:
             bound, ach, peak, unit = "hbm", nbytes / sec / 1e9 if sec else 0.0, HBM_PEAK_GBS, "GB/s"
         out[kname] = {
@@ -176,7 +180,12 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=5)
+    ap.add_argument("--precision", default="highest", choices=["highest", "medium"],
+                    help="torch.set_float32_matmul_precision for the run: 'highest' = fp32 MFMA (the "
+                         "fp32-parity headline), 'medium' = bf16 MFMA operands, fp32 accumulate "
+                         "(config/base.yaml:80)")
     args = ap.parse_args()
+    torch.set_float32_matmul_precision(args.precision)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -253,7 +262,8 @@ def main():
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp32" if args.precision == "highest" else "bf16 (fp32 accumulate)",
             "data": "synthetic (N(0,1) encoder outputs, random-init weights, seeded)",
             "config": {"workload": f"{args.workload}: HybridFusion M={M} B={B}/gpu L={lens or 1}"
                                    f"{'' if max(Ls) else ' (2-D reference semantics)'} D={D} H={H} heads={heads} "
@@ -261,7 +271,7 @@ def main():
                                    f"{mask_note}"
                                    f", fwd+CE(ls=0.05)+bwd+AdamW",
                        "global_batch": B * world, "seq_len": lens or 1, "parallelism": f"dp{world}",
-                       "graph": not args.no_graph},
+                       "graph": not args.no_graph, "matmul_precision": args.precision},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "step_tflops_algorithmic": round(step_fl / (ms_per_step * 1e-3) / 1e12, 3),

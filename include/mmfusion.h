@@ -42,6 +42,11 @@ extern "C" {
 #define MMF_MAX_HEAD_DIM 64
 
 enum {
+  MMF_PRECISION_HIGHEST = 0, /* "highest": fp32 operands */
+  MMF_PRECISION_MEDIUM = 1   /* "medium": bf16 operands, fp32 accumulate ("high" = TF32 is absent on gfx950: use HIGHEST) */
+};
+
+enum {
   MMF_OK = 0,
   MMF_EINVAL = 1,   /* bad shape / argument (reference would raise) */
   MMF_ELIMIT = 2,   /* outside the kernel limits (e.g. head_dim > 64) */
@@ -75,6 +80,11 @@ typedef struct mmf_hybrid_desc {
   float dropout;            /* nn.Dropout p shared by every dropout site */
   int32_t training;         /* module.training */
   int32_t return_attention; /* write attention maps */
+  /* torch.get_float32_matmul_precision() of the caller (config/base.yaml:80
+   * training.matmul_precision, applied at src/train.py:53-68,448):
+   * MMF_PRECISION_HIGHEST = fp32 MFMA; MMF_PRECISION_MEDIUM = bf16 MFMA operands
+   * with fp32 accumulation (storage, softmax and reductions stay fp32). */
+  int32_t matmul_precision;
 } mmf_hybrid_desc;
 
 typedef struct mmf_hybrid_params {
@@ -138,6 +148,7 @@ typedef struct mmf_cma_desc {
   int32_t mask_mode;
   float dropout;
   int32_t training;
+  int32_t matmul_precision; /* as mmf_hybrid_desc.matmul_precision */
 } mmf_cma_desc;
 
 typedef struct mmf_cma_params { mmf_linear q, k, v, o; } mmf_cma_params;

@@ -184,7 +184,7 @@ class CrossModalAttention(nn.Module):
             m = m.contiguous()
         desc = _nat.CmaDesc(B, lq, lk, self.query_proj.in_features, self.key_proj.in_features,
                             self.hidden_dim, self.num_heads, mask_mode, float(self.dropout.p),
-                            int(self.training))
+                            int(self.training), _nat.matmul_precision())
         attended, attn = _CMAFunction.apply(
             desc, m, self._rng_state, _nat.f32c(q3), _nat.f32c(k3), _nat.f32c(v3),
             self.query_proj.weight, self.query_proj.bias, self.key_proj.weight, self.key_proj.bias,

@@ -20,6 +20,9 @@
 // order over d is permuted (lane half h owns d in [h*HDP/2, (h+1)*HDP/2)) so
 // each lane's operand is contiguous.
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
 
 #include "mmf_device.h"
 
@@ -70,18 +73,35 @@ __device__ __forceinline__ void load_frag(float* f, const float* row, int dbase,
 }
 
 // acc += A_lds_row(lane) . f   over the HALF-long contraction (row-wise LDS operand)
-template <int HALF>
+// (BF: bf16 MFMA operands, see mfma_k16 in mmf_device.h; eight k-steps per chain)
+template <int HALF, bool BF = false>
 __device__ __forceinline__ f32x16 dot_rows(const float* lds_row, const float* f, f32x16 acc) {
+  static_assert(HALF % 8 == 0, "k chains of 8");
 #pragma unroll
-  for (int s4 = 0; s4 < HALF; s4 += 4) {
-    const float4 a = *reinterpret_cast<const float4*>(lds_row + s4);
-    acc = mfma32(a.x, f[s4 + 0], acc);
-    acc = mfma32(a.y, f[s4 + 1], acc);
-    acc = mfma32(a.z, f[s4 + 2], acc);
-    acc = mfma32(a.w, f[s4 + 3], acc);
+  for (int s8 = 0; s8 < HALF; s8 += 8) {
+    const float4 a0 = *reinterpret_cast<const float4*>(lds_row + s8);
+    const float4 a1 = *reinterpret_cast<const float4*>(lds_row + s8 + 4);
+    const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    float bv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bv[j] = f[s8 + j];
+    acc = mfma_k16<BF>(av, bv, acc);
   }
   return acc;
 }
+
+// ACC += sum over the 16 accumulator-register steps r of AEXPR(r) x BEXPR(r)
+// (one fp32 k-step per r), issued as two chains of eight (mfma_k16<BF>).
+#define MMF_CHAIN16(ACC, AEXPR, BEXPR)                                  \
+  _Pragma("unroll") for (int g_ = 0; g_ < 2; ++g_) {                    \
+    float av_[8], bv_[8];                                               \
+    _Pragma("unroll") for (int j_ = 0; j_ < 8; ++j_) {                  \
+      const int r = 8 * g_ + j_;                                        \
+      av_[j_] = (AEXPR);                                                \
+      bv_[j_] = (BEXPR);                                                \
+    }                                                                   \
+    ACC = mfma_k16<BF>(av_, bv_, ACC);                                  \
+  }
 
 __device__ __forceinline__ f32x16 zero16() {
   f32x16 z;
@@ -93,7 +113,7 @@ __device__ __forceinline__ f32x16 zero16() {
 // ---------------------------------------------------------------------------
 // Forward (MODE 0) and attention-probability output (MODE 1, needs LSE).
 // ---------------------------------------------------------------------------
-template <int HDP, int MODE>
+template <int HDP, int MODE, bool BF>
 __global__ __launch_bounds__(NT) void attn_fwd_kernel(const AttnArgs A) {
   constexpr int KC = HDP == 32 ? 128 : 64;
   constexpr int LS = HDP + 4;
@@ -164,7 +184,7 @@ __global__ __launch_bounds__(NT) void attn_fwd_kernel(const AttnArgs A) {
     if (!wave_active) continue;
     const int nkt = (min(KC, Lk - kbase) + 31) / 32;
     for (int kt = 0; kt < nkt; ++kt) {
-      f32x16 s = dot_rows<HALF>(Ks + (kt * 32 + c) * LS + h * HALF, qf, zero16());
+      f32x16 s = dot_rows<HALF, BF>(Ks + (kt * 32 + c) * LS + h * HALF, qf, zero16());
       float sv[16];
       float mx = -INFINITY;
 #pragma unroll
@@ -208,9 +228,7 @@ __global__ __launch_bounds__(NT) void attn_fwd_kernel(const AttnArgs A) {
       if (MODE == 0) {
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            o[dt] = mfma32(Vs[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], sv[r], o[dt]);
+MMF_CHAIN16(o[dt], Vs[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], sv[r])
         }
       } else if (qvalid) {
         float* prow = P.probs + rowidx * Lk;
@@ -289,7 +307,7 @@ __global__ __launch_bounds__(NT) void attn_bwd_prep_kernel(const AttnArgs A) {
 // ---------------------------------------------------------------------------
 // dK / dV: one workgroup = 128 keys (4 waves x 32, key on the lane).
 // ---------------------------------------------------------------------------
-template <int HDP>
+template <int HDP, bool BF>
 __global__ __launch_bounds__(NT) void attn_bwd_dkv_kernel(const AttnArgs A) {
   constexpr int QC = HDP == 32 ? 128 : 64;
   constexpr int LS = HDP + 4;
@@ -351,8 +369,8 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkv_kernel(const AttnArgs A) {
       if (!wave_active) continue;
       const int nqt = (min(QC, Lq - qbase) + 31) / 32;
       for (int qt = 0; qt < nqt; ++qt) {
-        f32x16 s = dot_rows<HALF>(Qs + (qt * 32 + c) * LS + h * HALF, kf, zero16());
-        f32x16 dp = dot_rows<HALF>(Ds + (qt * 32 + c) * LS + h * HALF, vf, zero16());
+        f32x16 s = dot_rows<HALF, BF>(Qs + (qt * 32 + c) * LS + h * HALF, kf, zero16());
+        f32x16 dp = dot_rows<HALF, BF>(Ds + (qt * 32 + c) * LS + h * HALF, vf, zero16());
         float pd[16], dsr[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -373,12 +391,8 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkv_kernel(const AttnArgs A) {
         }
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int row = (qt * 32 + acc_row(r, h)) * LS + dt * 32 + c;
-            dv[dt] = mfma32(pd[r], Ds[row], dv[dt]);
-            dk[dt] = mfma32(dsr[r], Qs[row], dk[dt]);
-          }
+MMF_CHAIN16(dv[dt], pd[r], Ds[(qt * 32 + acc_row(r, h)) * LS + dt * 32 + c])
+          MMF_CHAIN16(dk[dt], dsr[r], Qs[(qt * 32 + acc_row(r, h)) * LS + dt * 32 + c])
         }
       }
     }
@@ -402,7 +416,7 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkv_kernel(const AttnArgs A) {
 // ---------------------------------------------------------------------------
 // dQ: one workgroup = 128 queries (query on the lane, like the forward).
 // ---------------------------------------------------------------------------
-template <int HDP>
+template <int HDP, bool BF>
 __global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(const AttnArgs A) {
   constexpr int KC = HDP == 32 ? 128 : 64;
   constexpr int LS = HDP + 4;
@@ -455,8 +469,8 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(const AttnArgs A) {
       if (!wave_active) continue;
       const int nkt = (min(KC, Lk - kbase) + 31) / 32;
       for (int kt = 0; kt < nkt; ++kt) {
-        f32x16 s = dot_rows<HALF>(Ks + (kt * 32 + c) * LS + h * HALF, qf, zero16());
-        f32x16 dp = dot_rows<HALF>(Vs + (kt * 32 + c) * LS + h * HALF, df, zero16());
+        f32x16 s = dot_rows<HALF, BF>(Ks + (kt * 32 + c) * LS + h * HALF, qf, zero16());
+        f32x16 dp = dot_rows<HALF, BF>(Vs + (kt * 32 + c) * LS + h * HALF, df, zero16());
         float dsr[16];
         uint32_t bits[4] = {0xFu, 0xFu, 0xFu, 0xFu};
         if (pdrop > 0.f && qvalid) {
@@ -476,9 +490,7 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(const AttnArgs A) {
         }
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            dq[dt] = mfma32(Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], dsr[r], dq[dt]);
+MMF_CHAIN16(dq[dt], Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], dsr[r])
         }
       }
     }
@@ -542,7 +554,7 @@ __device__ __forceinline__ float colsum_tile(const float (&v)[16], int c) {
   return a1;
 }
 
-template <int HDP>
+template <int HDP, bool BF>
 __global__ __launch_bounds__(NT) void attn_pool_fwd_kernel(const AttnArgs A) {
   constexpr int LS = HDP + 4;
   constexpr int HALF = HDP / 2;
@@ -592,7 +604,7 @@ __global__ __launch_bounds__(NT) void attn_pool_fwd_kernel(const AttnArgs A) {
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
       if (kt < nkt) {
-        f32x16 s = dot_rows<HALF>(Ks + (kt * 32 + c) * LS + h * HALF, qf, zero16());
+        f32x16 s = dot_rows<HALF, BF>(Ks + (kt * 32 + c) * LS + h * HALF, qf, zero16());
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int key = kt * 32 + acc_row(r, h);
@@ -661,7 +673,7 @@ __global__ __launch_bounds__(NT) void attn_pool_fwd_kernel(const AttnArgs A) {
 }
 
 // Pooled backward, query on the lane: D = rowsum(P' dpbar)/Lq, dS, dQ.
-template <int HDP>
+template <int HDP, bool BF>
 __global__ __launch_bounds__(NT) void attn_pool_bwd_dq_kernel(const AttnArgs A) {
   constexpr int LS = HDP + 4;
   constexpr int HALF = HDP / 2;
@@ -713,7 +725,7 @@ __global__ __launch_bounds__(NT) void attn_pool_bwd_dq_kernel(const AttnArgs A) 
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) {
     if (kt < nkt) {
-      f32x16 s = dot_rows<HALF>(Ks + (kt * 32 + c) * LS + h * HALF, qf, zero16());
+      f32x16 s = dot_rows<HALF, BF>(Ks + (kt * 32 + c) * LS + h * HALF, qf, zero16());
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int key = kt * 32 + acc_row(r, h);
@@ -747,9 +759,7 @@ __global__ __launch_bounds__(NT) void attn_pool_bwd_dq_kernel(const AttnArgs A) 
     }
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        dq[dt] = mfma32(Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], ds[r], dq[dt]);
+MMF_CHAIN16(dq[dt], Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], ds[r])
   }
   if (!qvalid) return;
   const bool vo = (P.ldq % 4 == 0) && (hd % 4 == 0);
@@ -771,7 +781,7 @@ __global__ __launch_bounds__(NT) void attn_pool_bwd_dq_kernel(const AttnArgs A) 
 }
 
 // Pooled backward, key on the lane: dK = scale * dS^T Q (needs D from the dq kernel).
-template <int HDP>
+template <int HDP, bool BF>
 __global__ __launch_bounds__(NT) void attn_pool_bwd_dk_kernel(const AttnArgs A) {
   constexpr int QC = 128;
   constexpr int LS = HDP + 4;
@@ -828,7 +838,7 @@ __global__ __launch_bounds__(NT) void attn_pool_bwd_dk_kernel(const AttnArgs A) 
       if (!wave_active) continue;
       const int nqt = (min(QC, Lq - qbase) + 31) / 32;
       for (int qt = 0; qt < nqt; ++qt) {
-        f32x16 s = dot_rows<HALF>(Qs + (qt * 32 + c) * LS + h * HALF, kf, zero16());
+        f32x16 s = dot_rows<HALF, BF>(Qs + (qt * 32 + c) * LS + h * HALF, kf, zero16());
         float ds[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -843,9 +853,7 @@ __global__ __launch_bounds__(NT) void attn_pool_bwd_dk_kernel(const AttnArgs A) 
         }
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            dk[dt] = mfma32(ds[r], Qs[(qt * 32 + acc_row(r, h)) * LS + dt * 32 + c], dk[dt]);
+MMF_CHAIN16(dk[dt], ds[r], Qs[(qt * 32 + acc_row(r, h)) * LS + dt * 32 + c])
       }
     }
   }
@@ -883,7 +891,7 @@ __device__ __forceinline__ void load_frag_vec(float* f, const float* row) {
   }
 }
 
-template <int HDP>
+template <int HDP, bool BF>
 __global__ __launch_bounds__(NT) void attn_pool_fwd_lean(const AttnArgs A) {
   constexpr int LS = HDP + 4;
   constexpr int HALF = HDP / 2;
@@ -934,7 +942,7 @@ __global__ __launch_bounds__(NT) void attn_pool_fwd_lean(const AttnArgs A) {
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
       if (kt < nkt) {
-        const f32x16 s = dot_rows<HALF>(Ks + (kt * 32 + c) * LS + h * HALF, qf, zero16());
+        const f32x16 s = dot_rows<HALF, BF>(Ks + (kt * 32 + c) * LS + h * HALF, qf, zero16());
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           sv[kt][r] = s[r];
@@ -1001,7 +1009,7 @@ __global__ __launch_bounds__(NT) void attn_pool_fwd_lean(const AttnArgs A) {
 
 // dq pass, query on the lane: G[k] = keep ? dpbar[k] / ((1-p) Lq) : 0;
 // D = rowsum(P . G) (saved for the dk pass); dS = P . (G - D); dQ = scale dS K.
-template <int HDP>
+template <int HDP, bool BF>
 __global__ __launch_bounds__(NT) void attn_pool_bwd_dq_lean(const AttnArgs A) {
   constexpr int LS = HDP + 4;
   constexpr int HALF = HDP / 2;
@@ -1052,12 +1060,12 @@ __global__ __launch_bounds__(NT) void attn_pool_bwd_dq_lean(const AttnArgs A) {
   float pr[NKT][16];
   float D = 0.f;
   // software pipeline: the next key tile's S chain is issued before this tile's VALU work
-  f32x16 s_nx = dot_rows<HALF>(Ks + c * LS + h * HALF, qf, zero16());
+  f32x16 s_nx = dot_rows<HALF, BF>(Ks + c * LS + h * HALF, qf, zero16());
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) {
     if (kt < nkt) {
       const f32x16 s = s_nx;
-      if (kt + 1 < nkt) s_nx = dot_rows<HALF>(Ks + ((kt + 1) * 32 + c) * LS + h * HALF, qf, zero16());
+      if (kt + 1 < nkt) s_nx = dot_rows<HALF, BF>(Ks + ((kt + 1) * 32 + c) * LS + h * HALF, qf, zero16());
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const float4 gv = *reinterpret_cast<const float4*>(gk + kt * 32 + 8 * g + 4 * h);
@@ -1095,9 +1103,7 @@ __global__ __launch_bounds__(NT) void attn_pool_bwd_dq_lean(const AttnArgs A) {
     }
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        dq[dt] = mfma32(Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], ds[r], dq[dt]);
+MMF_CHAIN16(dq[dt], Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], ds[r])
   }
   if (!qvalid) return;
   const float scale = A.scale;
@@ -1113,7 +1119,7 @@ __global__ __launch_bounds__(NT) void attn_pool_bwd_dq_lean(const AttnArgs A) {
 }
 
 // dk pass, key on the lane: dK = scale * dS^T Q, dS = P . (G - D).
-template <int HDP>
+template <int HDP, bool BF>
 __global__ __launch_bounds__(NT) void attn_pool_bwd_dk_lean(const AttnArgs A) {
   constexpr int QC = 128;
   constexpr int LS = HDP + 4;
@@ -1166,10 +1172,10 @@ __global__ __launch_bounds__(NT) void attn_pool_bwd_dk_lean(const AttnArgs A) {
       if (!wave_active) continue;
       const int nqt = (min(QC, Lq - qbase) + 31) / 32;
       // software pipeline: the next tile's S chain is issued before this tile's VALU work
-      f32x16 s_nx = dot_rows<HALF>(Qs + c * LS + h * HALF, kf, zero16());
+      f32x16 s_nx = dot_rows<HALF, BF>(Qs + c * LS + h * HALF, kf, zero16());
       for (int qt = 0; qt < nqt; ++qt) {
         const f32x16 s = s_nx;
-        if (qt + 1 < nqt) s_nx = dot_rows<HALF>(Qs + ((qt + 1) * 32 + c) * LS + h * HALF, kf, zero16());
+        if (qt + 1 < nqt) s_nx = dot_rows<HALF, BF>(Qs + ((qt + 1) * 32 + c) * LS + h * HALF, kf, zero16());
         float ds[16];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -1190,9 +1196,7 @@ __global__ __launch_bounds__(NT) void attn_pool_bwd_dk_lean(const AttnArgs A) {
         }
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            dk[dt] = mfma32(ds[r], Qs[(qt * 32 + acc_row(r, h)) * LS + dt * 32 + c], dk[dt]);
+MMF_CHAIN16(dk[dt], ds[r], Qs[(qt * 32 + acc_row(r, h)) * LS + dt * 32 + c])
       }
     }
   }
@@ -1222,7 +1226,7 @@ __global__ __launch_bounds__(NT) void attn_pool_bwd_dk_lean(const AttnArgs A) {
 // keep-bit pass (VALU), one read of Q, K, LSE and the keep words, and the D
 // round trip.  LDS at hd <= 32: K and Q images, 2 x 18 KB (the dS^T quarters
 // reuse the K image) -> 4 workgroups per CU, whose load phases hide each other.
-template <int HDP>
+template <int HDP, bool BF>
 __global__ __launch_bounds__(NT, 4) void attn_pool_bwd_fused_lean(const AttnArgs A) {
   constexpr int LS = HDP + 4;
   constexpr int HALF = HDP / 2;
@@ -1278,12 +1282,12 @@ __global__ __launch_bounds__(NT, 4) void attn_pool_bwd_fused_lean(const AttnArgs
   const float c2 = scale * LOG2E;
   float pr[NKT][16];
   float D = 0.f;
-  f32x16 s_nx = dot_rows<HALF>(Ks + c * LS + h * HALF, qf, zero16());
+  f32x16 s_nx = dot_rows<HALF, BF>(Ks + c * LS + h * HALF, qf, zero16());
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) {
     if (kt < nkt) {
       const f32x16 s = s_nx;
-      if (kt + 1 < nkt) s_nx = dot_rows<HALF>(Ks + ((kt + 1) * 32 + c) * LS + h * HALF, qf, zero16());
+      if (kt + 1 < nkt) s_nx = dot_rows<HALF, BF>(Ks + ((kt + 1) * 32 + c) * LS + h * HALF, qf, zero16());
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const float4 gv = *reinterpret_cast<const float4*>(gk + kt * 32 + 8 * g + 4 * h);
@@ -1330,9 +1334,7 @@ __global__ __launch_bounds__(NT, 4) void attn_pool_bwd_fused_lean(const AttnArgs
       if (kt < nkt) {
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            dq[dt] = mfma32(Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], pr[kt][r], dq[dt]);
+MMF_CHAIN16(dq[dt], Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], pr[kt][r])
       }
     }
     if (qvalid) {
@@ -1363,16 +1365,24 @@ __global__ __launch_bounds__(NT, 4) void attn_pool_bwd_fused_lean(const AttnArgs
     }
     __syncthreads();
     if (kwave) {
+// k-steps (g, j) = query 8g + 4h + j of the quarter; chains of eight over g pairs
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 a4 = *reinterpret_cast<const float4*>(dsT + key * TS + 8 * g + 4 * h);
-        const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+      for (int gp = 0; gp < 2; ++gp) {
+        float av[8], qv[NDT][8];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int qg = qw * 32 + 8 * g + 4 * h + j;
+        for (int u = 0; u < 2; ++u) {
+          const int g = 2 * gp + u;
+          const float4 a4 = *reinterpret_cast<const float4*>(dsT + key * TS + 8 * g + 4 * h);
+          av[4 * u + 0] = a4.x; av[4 * u + 1] = a4.y; av[4 * u + 2] = a4.z; av[4 * u + 3] = a4.w;
 #pragma unroll
-          for (int dt = 0; dt < NDT; ++dt) dk[dt] = mfma32(av[j], Qs[qg * LS + dt * 32 + c], dk[dt]);
+          for (int j = 0; j < 4; ++j) {
+            const int qg = qw * 32 + 8 * g + 4 * h + j;
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt) qv[dt][4 * u + j] = Qs[qg * LS + dt * 32 + c];
+          }
         }
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) dk[dt] = mfma_k16<BF>(av, qv[dt], dk[dt]);
       }
     }
   }
@@ -1385,6 +1395,21 @@ __global__ __launch_bounds__(NT, 4) void attn_pool_bwd_fused_lean(const AttnArgs
     for (int r = 0; r < 16; ++r)
       P.dk[((int64_t)b * Lk + w * 32 + acc_row(r, h)) * P.ldk + col0 + d] = dk[dt][r] * scale;
   }
+}
+
+// "name<a, b>" -> "name<a, b, false|true>" (the rocprof name of the BF instantiation);
+// stable storage for the profiler tags.
+const char* with_bf(const char* base, bool bf) {
+  static std::mutex mu;
+  static std::map<std::string, std::string> names[2];
+  std::lock_guard<std::mutex> lk(mu);
+  auto& slot = names[bf ? 1 : 0][base];
+  if (slot.empty()) {
+    std::string b(base);
+    const size_t gt = b.rfind('>');
+    slot = gt == std::string::npos ? b : b.substr(0, gt) + (bf ? ", true>" : ", false>");
+  }
+  return slot.c_str();
 }
 
 enum class Kind { Fwd, Probs, Prep, Dkv, Dq, PoolFwd, PoolDq, PoolDk, PoolFused };
@@ -1474,49 +1499,50 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
          "attn_pool_bwd_dk_lean<64>"},
         {"", "", "attn_pool_bwd_fused_lean<32>", "attn_pool_bwd_fused_lean<64>"}};
     const bool alt = kind == Kind::Prep ? prep_vec : lean;
-    ProfLaunch prof_(st, kNames[(int)kind][(alt ? 2 : 0) + (small ? 0 : 1)], fl, by);
+    const bool bf = math_bf16();
+    ProfLaunch prof_(st, with_bf(kNames[(int)kind][(alt ? 2 : 0) + (small ? 0 : 1)], bf), fl, by);
     switch (kind) {
       case Kind::Fwd:
-        if (small) hipLaunchKernelGGL((attn_fwd_kernel<32, 0>), grid, dim3(NT), 0, st, a);
-        else hipLaunchKernelGGL((attn_fwd_kernel<64, 0>), grid, dim3(NT), 0, st, a);
+        if (small) { if (bf) hipLaunchKernelGGL((attn_fwd_kernel<32, 0, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_fwd_kernel<32, 0, false>), grid, dim3(NT), 0, st, a); }
+        else { if (bf) hipLaunchKernelGGL((attn_fwd_kernel<64, 0, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_fwd_kernel<64, 0, false>), grid, dim3(NT), 0, st, a); }
         break;
       case Kind::Probs:
-        if (small) hipLaunchKernelGGL((attn_fwd_kernel<32, 1>), grid, dim3(NT), 0, st, a);
-        else hipLaunchKernelGGL((attn_fwd_kernel<64, 1>), grid, dim3(NT), 0, st, a);
+        if (small) { if (bf) hipLaunchKernelGGL((attn_fwd_kernel<32, 1, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_fwd_kernel<32, 1, false>), grid, dim3(NT), 0, st, a); }
+        else { if (bf) hipLaunchKernelGGL((attn_fwd_kernel<64, 1, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_fwd_kernel<64, 1, false>), grid, dim3(NT), 0, st, a); }
         break;
       case Kind::Prep:
         if (prep_vec) hipLaunchKernelGGL(attn_bwd_prep_vec_kernel, grid, dim3(NT), 0, st, a);
         else hipLaunchKernelGGL(attn_bwd_prep_kernel, grid, dim3(NT), 0, st, a);
         break;
       case Kind::Dkv:
-        if (small) hipLaunchKernelGGL((attn_bwd_dkv_kernel<32>), grid, dim3(NT), 0, st, a);
-        else hipLaunchKernelGGL((attn_bwd_dkv_kernel<64>), grid, dim3(NT), 0, st, a);
+        if (small) { if (bf) hipLaunchKernelGGL((attn_bwd_dkv_kernel<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_bwd_dkv_kernel<32, false>), grid, dim3(NT), 0, st, a); }
+        else { if (bf) hipLaunchKernelGGL((attn_bwd_dkv_kernel<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_bwd_dkv_kernel<64, false>), grid, dim3(NT), 0, st, a); }
         break;
       case Kind::Dq:
-        if (small) hipLaunchKernelGGL((attn_bwd_dq_kernel<32>), grid, dim3(NT), 0, st, a);
-        else hipLaunchKernelGGL((attn_bwd_dq_kernel<64>), grid, dim3(NT), 0, st, a);
+        if (small) { if (bf) hipLaunchKernelGGL((attn_bwd_dq_kernel<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_bwd_dq_kernel<32, false>), grid, dim3(NT), 0, st, a); }
+        else { if (bf) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_bwd_dq_kernel<64, false>), grid, dim3(NT), 0, st, a); }
         break;
       case Kind::PoolFwd:
-        if (lean && small) hipLaunchKernelGGL((attn_pool_fwd_lean<32>), grid, dim3(NT), 0, st, a);
-        else if (lean) hipLaunchKernelGGL((attn_pool_fwd_lean<64>), grid, dim3(NT), 0, st, a);
-        else if (small) hipLaunchKernelGGL((attn_pool_fwd_kernel<32>), grid, dim3(NT), 0, st, a);
-        else hipLaunchKernelGGL((attn_pool_fwd_kernel<64>), grid, dim3(NT), 0, st, a);
+        if (lean && small) { if (bf) hipLaunchKernelGGL((attn_pool_fwd_lean<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_fwd_lean<32, false>), grid, dim3(NT), 0, st, a); }
+        else if (lean) { if (bf) hipLaunchKernelGGL((attn_pool_fwd_lean<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_fwd_lean<64, false>), grid, dim3(NT), 0, st, a); }
+        else if (small) { if (bf) hipLaunchKernelGGL((attn_pool_fwd_kernel<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_fwd_kernel<32, false>), grid, dim3(NT), 0, st, a); }
+        else { if (bf) hipLaunchKernelGGL((attn_pool_fwd_kernel<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_fwd_kernel<64, false>), grid, dim3(NT), 0, st, a); }
         break;
       case Kind::PoolDq:
-        if (lean && small) hipLaunchKernelGGL((attn_pool_bwd_dq_lean<32>), grid, dim3(NT), 0, st, a);
-        else if (lean) hipLaunchKernelGGL((attn_pool_bwd_dq_lean<64>), grid, dim3(NT), 0, st, a);
-        else if (small) hipLaunchKernelGGL((attn_pool_bwd_dq_kernel<32>), grid, dim3(NT), 0, st, a);
-        else hipLaunchKernelGGL((attn_pool_bwd_dq_kernel<64>), grid, dim3(NT), 0, st, a);
+        if (lean && small) { if (bf) hipLaunchKernelGGL((attn_pool_bwd_dq_lean<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_bwd_dq_lean<32, false>), grid, dim3(NT), 0, st, a); }
+        else if (lean) { if (bf) hipLaunchKernelGGL((attn_pool_bwd_dq_lean<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_bwd_dq_lean<64, false>), grid, dim3(NT), 0, st, a); }
+        else if (small) { if (bf) hipLaunchKernelGGL((attn_pool_bwd_dq_kernel<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_bwd_dq_kernel<32, false>), grid, dim3(NT), 0, st, a); }
+        else { if (bf) hipLaunchKernelGGL((attn_pool_bwd_dq_kernel<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_bwd_dq_kernel<64, false>), grid, dim3(NT), 0, st, a); }
         break;
       case Kind::PoolFused:
-        if (small) hipLaunchKernelGGL((attn_pool_bwd_fused_lean<32>), grid, dim3(NT), 0, st, a);
-        else hipLaunchKernelGGL((attn_pool_bwd_fused_lean<64>), grid, dim3(NT), 0, st, a);
+        if (small) { if (bf) hipLaunchKernelGGL((attn_pool_bwd_fused_lean<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_bwd_fused_lean<32, false>), grid, dim3(NT), 0, st, a); }
+        else { if (bf) hipLaunchKernelGGL((attn_pool_bwd_fused_lean<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_bwd_fused_lean<64, false>), grid, dim3(NT), 0, st, a); }
         break;
       case Kind::PoolDk:
-        if (lean && small) hipLaunchKernelGGL((attn_pool_bwd_dk_lean<32>), grid, dim3(NT), 0, st, a);
-        else if (lean) hipLaunchKernelGGL((attn_pool_bwd_dk_lean<64>), grid, dim3(NT), 0, st, a);
-        else if (small) hipLaunchKernelGGL((attn_pool_bwd_dk_kernel<32>), grid, dim3(NT), 0, st, a);
-        else hipLaunchKernelGGL((attn_pool_bwd_dk_kernel<64>), grid, dim3(NT), 0, st, a);
+        if (lean && small) { if (bf) hipLaunchKernelGGL((attn_pool_bwd_dk_lean<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_bwd_dk_lean<32, false>), grid, dim3(NT), 0, st, a); }
+        else if (lean) { if (bf) hipLaunchKernelGGL((attn_pool_bwd_dk_lean<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_bwd_dk_lean<64, false>), grid, dim3(NT), 0, st, a); }
+        else if (small) { if (bf) hipLaunchKernelGGL((attn_pool_bwd_dk_kernel<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_bwd_dk_kernel<32, false>), grid, dim3(NT), 0, st, a); }
+        else { if (bf) hipLaunchKernelGGL((attn_pool_bwd_dk_kernel<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_bwd_dk_kernel<64, false>), grid, dim3(NT), 0, st, a); }
         break;
     }
     hipError_t e = hipGetLastError();

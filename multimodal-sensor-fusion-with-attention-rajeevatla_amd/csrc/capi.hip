@@ -53,6 +53,8 @@ void layout_cma_ws(const mmf_cma_desc* d, Bump& bp, CmaWs& w) {
 
 int check_cma(const mmf_cma_desc* d) {
   if (!d) return fail(MMF_EINVAL, "null descriptor");
+  if (d->matmul_precision != MMF_PRECISION_HIGHEST && d->matmul_precision != MMF_PRECISION_MEDIUM)
+    return fail(MMF_EINVAL, "bad matmul_precision %d", d->matmul_precision);
   if (d->batch < 1 || d->lq < 1 || d->lk < 1 || d->query_dim < 1 || d->key_dim < 1)
     return fail(MMF_EINVAL, "bad CrossModalAttention shape");
   if (d->num_heads < 1 || d->hidden % d->num_heads != 0)
@@ -101,12 +103,14 @@ void prof_launch_end(void* tok, hipStream_t st, const char* kernel, double flops
   g_prof.launches.push_back({g_prof.cur_stage, kernel, flops, bytes, (hipEvent_t)tok, b});
 }
 
+thread_local int g_math_bf16 = 0;
+
 }  // namespace mmf
 
 extern "C" {
 
 const char* mmf_last_error(void) { return g_err.c_str(); }
-const char* mmf_version(void) { return "mmfusion 0.2 (gfx950, fp32 MFMA, pooled HybridFusion)"; }
+const char* mmf_version(void) { return "mmfusion 0.3 (gfx950, fp32 / bf16 MFMA, pooled HybridFusion)"; }
 
 void mmf_profile_begin(void) {
   g_prof.on = true;
@@ -212,6 +216,7 @@ int mmf_cma_forward(const mmf_cma_desc* d, const mmf_cma_params* W, const float*
                     void* stream) {
   int rc = check_cma(d);
   if (rc) return rc;
+  mmf::MathScope math_(d->matmul_precision == MMF_PRECISION_MEDIUM);
   if (!W || !query || !key || !value || !saved || !attended) return fail(MMF_EINVAL, "null argument");
   if (d->mask_mode && !mask) return fail(MMF_EINVAL, "mask_mode set but mask is null");
   hipStream_t st = (hipStream_t)stream;
@@ -254,6 +259,7 @@ int mmf_cma_backward(const mmf_cma_desc* d, const mmf_cma_params* W, const float
                      float* dkey, float* dvalue, void* stream) {
   int rc = check_cma(d);
   if (rc) return rc;
+  mmf::MathScope math_(d->matmul_precision == MMF_PRECISION_MEDIUM);
   if (!W || !query || !key || !value || !saved || !dA || !workspace || !G)
     return fail(MMF_EINVAL, "null argument");
   hipStream_t st = (hipStream_t)stream;

@@ -259,7 +259,7 @@ __device__ __forceinline__ void lds_barrier() {
 // (source, k0) cursor over one tile's contraction
 struct KCursor { int si, k0, kend; };
 
-template <int AMODE, int BMODE, int DK, int NSTAGE>
+template <int AMODE, int BMODE, int DK, int NSTAGE, bool BF = false>
 __global__ __launch_bounds__(NT, (NSTAGE * DK <= 32 ? 4 : 2)) void gemm_lds_kernel(const GemmArgs args) {
   constexpr int DTILE = BM * DK;                  // floats per operand tile
   constexpr int DMA_PER_TILE = 2 * (BM * DK / 1024);  // glds per wave per (A, B) tile pair
@@ -376,6 +376,32 @@ __global__ __launch_bounds__(NT, (NSTAGE * DK <= 32 ? 4 : 2)) void gemm_lds_kern
                                     : At[row * DK + ((((kk >> 2) ^ swz<DK>(row))) << 2) + (kk & 3)];
         }
       }
+if constexpr (BF) {
+        // chunks 2u, 2u+1 (16 k) -> one bf16 MFMA per accumulator
+#pragma unroll
+        for (int u = 0; u < DK / 16; ++u) {
+          float av[2][8], bv[2][8];
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) {
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+              const f32x4 f = frag<AMODE, DK>(At, wm * 64 + a * 32 + c, 2 * u + jj, h);
+#pragma unroll
+              for (int s = 0; s < 4; ++s) av[a][4 * jj + s] = f[s];
+            }
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+              const f32x4 f = frag<BMODE, DK>(Bt, wn * 64 + b * 32 + c, 2 * u + jj, h);
+#pragma unroll
+              for (int s = 0; s < 4; ++s) bv[b][4 * jj + s] = f[s];
+            }
+          }
+#pragma unroll
+          for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) acc[a][b] = mfma_k16<true>(av[a], bv[b], acc[a][b]);
+        }
+      } else {
 #pragma unroll
       for (int j = 0; j < DK / 8; ++j) {
         f32x4 af[2], bf[2];
@@ -389,6 +415,7 @@ __global__ __launch_bounds__(NT, (NSTAGE * DK <= 32 ? 4 : 2)) void gemm_lds_kern
           for (int a = 0; a < 2; ++a)
 #pragma unroll
             for (int b = 0; b < 2; ++b) acc[a][b] = mfma32(af[a][s], bf[b][s], acc[a][b]);
+      }
       }
       const KCursor nx = advance(cur);
       if (nx.si >= G.src_count) break;
@@ -424,6 +451,7 @@ __global__ __launch_bounds__(NT, (NSTAGE * DK <= 32 ? 4 : 2)) void gemm_lds_kern
 // a tile is written out.  Persistent grid: 2 workgroups per CU.
 constexpr int WSR_DK = 16, WSR_NS = 6, WSR_NKC = 16;   // k-tile, ring depth, max 8-deep k chunks (K <= 128)
 
+template <bool BF>
 __global__ __launch_bounds__(NT, 2) void gemm_wsr_kernel(const GemmArgs args, int total_items, int K) {
   constexpr int DTILE = BM * WSR_DK;
   __shared__ __attribute__((aligned(16))) float ring[WSR_NS * DTILE];
@@ -528,6 +556,26 @@ __global__ __launch_bounds__(NT, 2) void gemm_wsr_kernel(const GemmArgs args, in
         lds_barrier();   // tile f landed for every wave; every wave is done with slot (f-1) % NS
         if (nissued < nflat) issue(nissued++);
         const float* At = ring + (f % WSR_NS) * DTILE;
+if constexpr (BF) {
+          float av[2][8], bv[2][8];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+              const f32x4 fa = frag<MODE_RK, WSR_DK>(At, wm * 64 + a * 32 + c, j, h);
+#pragma unroll
+              for (int s = 0; s < 4; ++s) av[a][4 * j + s] = fa[s];
+            }
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+              for (int s = 0; s < 4; ++s) bv[b][4 * j + s] = breg[b][2 * kt + j][s];
+          }
+#pragma unroll
+          for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) acc[a][b] = mfma_k16<true>(av[a], bv[b], acc[a][b]);
+        } else {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           f32x4 af[2];
@@ -539,6 +587,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_wsr_kernel(const GemmArgs args, in
             for (int a = 0; a < 2; ++a)
 #pragma unroll
               for (int b = 0; b < 2; ++b) acc[a][b] = mfma32(af[a][s], breg[b][2 * kt + j][s], acc[a][b]);
+        }
         }
         ++f;
       }
@@ -917,8 +966,13 @@ hipError_t launch_wsr(const GemmJob* jobs, int njobs, hipStream_t st) {
     args.ngroups = ng;
     const int K = args.s[0].K;
     const int grid = std::min(items, 2 * cu_count());
-    ProfLaunch prof_(st, "gemm_wsr_kernel", fl, by);
-    hipLaunchKernelGGL(gemm_wsr_kernel, dim3(grid), dim3(NT), 0, st, args, items, K);
+    if (math_bf16()) {
+      ProfLaunch prof_(st, "gemm_wsr_kernel<true>", fl, by);
+      hipLaunchKernelGGL(gemm_wsr_kernel<true>, dim3(grid), dim3(NT), 0, st, args, items, K);
+    } else {
+      ProfLaunch prof_(st, "gemm_wsr_kernel<false>", fl, by);
+      hipLaunchKernelGGL(gemm_wsr_kernel<false>, dim3(grid), dim3(NT), 0, st, args, items, K);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
@@ -994,21 +1048,27 @@ hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, 
         }
         by += 4.0 * g.M * g.N * g.nbatch;
       }
-      static const char* const kLdsName[4] = {"gemm_lds_kernel<0, 0, 16, 3>", "gemm_lds_kernel<0, 1, 16, 3>",
-                                              "gemm_lds_kernel<1, 0, 16, 3>", "gemm_lds_kernel<1, 1, 16, 3>"};
+      static const char* const kLdsName[8] = {
+          "gemm_lds_kernel<0, 0, 16, 3, false>", "gemm_lds_kernel<0, 1, 16, 3, false>",
+          "gemm_lds_kernel<1, 0, 16, 3, false>", "gemm_lds_kernel<1, 1, 16, 3, false>",
+          "gemm_lds_kernel<0, 0, 16, 3, true>",  "gemm_lds_kernel<0, 1, 16, 3, true>",
+          "gemm_lds_kernel<1, 0, 16, 3, true>",  "gemm_lds_kernel<1, 1, 16, 3, true>"};
+      const bool bf = math_bf16();
       static const char* const kGenName[4] = {"gemm_generic_kernel<0, 0>", "gemm_generic_kernel<0, 1>",
                                               "gemm_generic_kernel<1, 0>", "gemm_generic_kernel<1, 1>"};
       const int flavour = (amode == MODE_KR ? 2 : 0) + (bmode == MODE_KR ? 1 : 0);
-      ProfLaunch prof_(st, fast ? kLdsName[flavour] : kGenName[flavour], fl, by);
-#define MMF_LAUNCH_CFG(DKV, NSV)                                                                  \
+      ProfLaunch prof_(st, fast ? kLdsName[flavour + (bf ? 4 : 0)] : kGenName[flavour], fl, by);
+#define MMF_LAUNCH_CFG2(DKV, NSV, BFV)                                                              \
       if (amode == MODE_RK && bmode == MODE_RK)                                                     \
-        hipLaunchKernelGGL((gemm_lds_kernel<MODE_RK, MODE_RK, DKV, NSV>), grid, dim3(NT), 0, st, args); \
+        hipLaunchKernelGGL((gemm_lds_kernel<MODE_RK, MODE_RK, DKV, NSV, BFV>), grid, dim3(NT), 0, st, args); \
       else if (amode == MODE_RK && bmode == MODE_KR)                                                \
-        hipLaunchKernelGGL((gemm_lds_kernel<MODE_RK, MODE_KR, DKV, NSV>), grid, dim3(NT), 0, st, args); \
+        hipLaunchKernelGGL((gemm_lds_kernel<MODE_RK, MODE_KR, DKV, NSV, BFV>), grid, dim3(NT), 0, st, args); \
       else if (amode == MODE_KR && bmode == MODE_KR)                                                \
-        hipLaunchKernelGGL((gemm_lds_kernel<MODE_KR, MODE_KR, DKV, NSV>), grid, dim3(NT), 0, st, args); \
+        hipLaunchKernelGGL((gemm_lds_kernel<MODE_KR, MODE_KR, DKV, NSV, BFV>), grid, dim3(NT), 0, st, args); \
       else                                                                                          \
-        hipLaunchKernelGGL((gemm_lds_kernel<MODE_KR, MODE_RK, DKV, NSV>), grid, dim3(NT), 0, st, args);
+        hipLaunchKernelGGL((gemm_lds_kernel<MODE_KR, MODE_RK, DKV, NSV, BFV>), grid, dim3(NT), 0, st, args);
+#define MMF_LAUNCH_CFG(DKV, NSV)                                                                    \
+      if (bf) { MMF_LAUNCH_CFG2(DKV, NSV, true) } else { MMF_LAUNCH_CFG2(DKV, NSV, false) }
 #define MMF_LAUNCH(KERNEL)                                                                 \
       if (amode == MODE_RK && bmode == MODE_RK)                                            \
         hipLaunchKernelGGL((KERNEL<MODE_RK, MODE_RK>), grid, dim3(NT), 0, st, args);       \
@@ -1027,6 +1087,7 @@ hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, 
       }
 #undef MMF_LAUNCH
 #undef MMF_LAUNCH_CFG
+#undef MMF_LAUNCH_CFG2
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }

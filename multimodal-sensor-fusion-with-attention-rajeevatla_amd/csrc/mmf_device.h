@@ -18,6 +18,35 @@ __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
 
 __device__ __forceinline__ int acc_row(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
 
+// ---------------------------------------------------------------- bf16 math mode
+// torch.set_float32_matmul_precision("medium") (config/base.yaml:80 via
+// src/train.py:53-68,448) lets fp32 matmuls run with bf16 operands and fp32
+// accumulation.  Operands stay fp32 in HBM and LDS; a kernel's MFMA issue
+// switches from eight v_mfma_f32_32x32x2_f32 k-steps to one
+// v_mfma_f32_32x32x16_bf16 over the same 16 products.  Lane half h of the
+// fp32 form feeds k-pair element h at step j (j = 0..7); the bf16 form takes
+// element j of lane half h as k = 8h + j.  Applied to A and B alike this is a
+// permutation of the contraction, so a chain of eight fp32 k-steps into one
+// accumulator maps 1:1 onto one bf16 MFMA with a[j], b[j] = step j's operands.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+template <bool BF>
+__device__ __forceinline__ f32x16 mfma_k16(const float (&a)[8], const float (&b)[8], f32x16 c) {
+  if constexpr (BF) {
+    bf16x8 av, bv;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      av[j] = (__bf16)a[j];   // v_cvt_pk_bf16_f32: round to nearest even, NaN kept
+      bv[j] = (__bf16)b[j];
+    }
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, c, 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) c = mfma32(a[j], b[j], c);
+    return c;
+  }
+}
+
 // ---------------------------------------------------------------- Philox4x32-10
 __device__ __forceinline__ uint4 philox10(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll

@@ -37,6 +37,22 @@ struct ProfLaunch {
   ProfLaunch& operator=(const ProfLaunch&) = delete;
 };
 
+// ---------------------------------------------------------------------------
+// Matmul precision of the current C-ABI call (torch.get_float32_matmul_precision
+// at the caller): 0 = "highest" (fp32 MFMA), 1 = "medium" (bf16 MFMA operands,
+// fp32 accumulate).  Set for the duration of one entry point by MathScope; the
+// launchers pick the kernel instantiation from it (a graph captures that choice).
+// ---------------------------------------------------------------------------
+extern thread_local int g_math_bf16;
+inline bool math_bf16() { return g_math_bf16 != 0; }
+struct MathScope {
+  int prev;
+  explicit MathScope(int bf16) : prev(g_math_bf16) { g_math_bf16 = bf16 ? 1 : 0; }
+  ~MathScope() { g_math_bf16 = prev; }
+  MathScope(const MathScope&) = delete;
+  MathScope& operator=(const MathScope&) = delete;
+};
+
 enum : uint32_t {
   SITE_IN = 0x100,     // + m : input dropout on X_m*mask  (src/fusion.py:373)
   SITE_PROJ = 0x200,   // + m : projections[m] Dropout     (src/fusion.py:291-298)

@@ -246,6 +246,7 @@ class _Plan:
         d.dropout = float(model.dropout.p)
         d.training = int(model.training)
         d.return_attention = int(return_attention)
+        d.matmul_precision = _nat.matmul_precision()
         self.desc = d
         self.seq = [max(s, 1) for s in seq]
         self.pairs = pairs

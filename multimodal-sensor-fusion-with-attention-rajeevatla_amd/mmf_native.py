@@ -17,6 +17,20 @@ import torch
 MAX_MODALITIES = 8
 MAX_PAIRS = MAX_MODALITIES * (MAX_MODALITIES - 1)
 MAX_HEAD_DIM = 64
+PRECISION_HIGHEST = 0   # MMF_PRECISION_HIGHEST: fp32 MFMA
+PRECISION_MEDIUM = 1    # MMF_PRECISION_MEDIUM: bf16 MFMA operands, fp32 accumulate
+
+
+def matmul_precision() -> int:
+    """The caller's torch.get_float32_matmul_precision() as the C-ABI enum.
+
+    The reference sets it from ``training.matmul_precision`` (config/base.yaml:80,
+    "medium") through ``_configure_matmul_precision`` (src/train.py:53-68,448).
+    "medium" lets fp32 matmuls use bf16 operands with fp32 accumulation; "high"
+    asks for TF32, which gfx950 does not have, so it runs like "highest" (fp32),
+    as PyTorch does on hardware without TF32.
+    """
+    return PRECISION_MEDIUM if torch.get_float32_matmul_precision() == "medium" else PRECISION_HIGHEST
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "csrc", "libmmfusion.so")
@@ -46,6 +60,7 @@ class HybridDesc(ctypes.Structure):
         ("num_pairs", c_int32),
         ("pair_q", c_int32 * MAX_PAIRS), ("pair_k", c_int32 * MAX_PAIRS),
         ("dropout", c_float), ("training", c_int32), ("return_attention", c_int32),
+        ("matmul_precision", c_int32),
     ]
 
 
@@ -67,6 +82,7 @@ class CmaDesc(ctypes.Structure):
         ("batch", c_int32), ("lq", c_int32), ("lk", c_int32), ("query_dim", c_int32),
         ("key_dim", c_int32), ("hidden", c_int32), ("num_heads", c_int32),
         ("mask_mode", c_int32), ("dropout", c_float), ("training", c_int32),
+        ("matmul_precision", c_int32),
     ]
 
 

@@ -18,8 +18,49 @@ def load_fixture(name: str) -> Dict[str, np.ndarray]:
         return {k: z[k] for k in z.files}
 
 
-def oracle_hybrid(case: HybridCase, dtype=torch.float32):
-    """Run the CPU oracle on the case; returns (outputs dict, param grads, input grads)."""
+def _bf16(x: torch.Tensor) -> torch.Tensor:
+    return x.to(torch.bfloat16).to(torch.float32)
+
+
+class _Bf16MatMul(torch.autograd.Function):
+    """matmul with bf16-rounded operands and fp32 accumulation, forward AND backward:
+    what torch.set_float32_matmul_precision("medium") permits for every fp32
+    matmul (config/base.yaml:80).  Used to size the error a bf16 path must show."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        ctx.save_for_backward(a, b)
+        return torch.matmul(_bf16(a), _bf16(b))
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        ga = torch.matmul(_bf16(g), _bf16(b).transpose(-1, -2))
+        gb = torch.matmul(_bf16(a).transpose(-1, -2), _bf16(g))
+        while ga.dim() > a.dim():
+            ga = ga.sum(0)
+        while gb.dim() > b.dim():
+            gb = gb.sum(0)
+        return ga, gb
+
+
+class bf16_matmul_mode(torch.overrides.TorchFunctionMode):
+    """Routes every Tensor.matmul / torch.matmul of the oracle through _Bf16MatMul."""
+
+    def __torch_function__(self, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        if func in (torch.Tensor.matmul, torch.matmul) and not kwargs:
+            with torch._C.DisableTorchFunction():
+                return _Bf16MatMul.apply(*args)
+        return func(*args, **kwargs)
+
+
+def oracle_hybrid(case: HybridCase, dtype=torch.float32, bf16_matmul: bool = False):
+    """Run the CPU oracle on the case; returns (outputs dict, param grads, input grads).
+    bf16_matmul: every matmul with bf16 operands (bf16_matmul_mode)."""
+    if bf16_matmul:
+        with bf16_matmul_mode():
+            return oracle_hybrid(case, dtype)
     from oracle.hybrid_cpu import hybrid_forward
     sd = hybrid_state(case.names, case.dims, case.hidden, case.classes, case.seed, case.deleted)
     params = {k: torch.from_numpy(v).to(dtype).requires_grad_(True) for k, v in sd.items()}
@@ -38,7 +79,10 @@ def oracle_hybrid(case: HybridCase, dtype=torch.float32):
     return out, grads, dx
 
 
-def oracle_cma(case: CMACase, dtype=torch.float32):
+def oracle_cma(case: CMACase, dtype=torch.float32, bf16_matmul: bool = False):
+    if bf16_matmul:
+        with bf16_matmul_mode():
+            return oracle_cma(case, dtype)
     from oracle.hybrid_cpu import cma_forward
     sd = cma_state(case.query_dim, case.key_dim, case.hidden, case.seed)
     params = {k: torch.from_numpy(v).to(dtype).requires_grad_(True) for k, v in sd.items()}
