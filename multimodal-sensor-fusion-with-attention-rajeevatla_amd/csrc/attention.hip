@@ -23,6 +23,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "mmf_device.h"
 
@@ -528,6 +529,10 @@ MMF_CHAIN16(dq[dt], Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], dsr[r])
 // ===========================================================================
 constexpr int PKC = 128;
 
+constexpr float LOG2E = 1.4426950408889634f;
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 // Column-sum of a 32x32 S^T tile over its 32 query lanes (reduce-scatter
 // butterfly, 16 shuffles).  Returns, in lane c, the sum for tile row
 // r = (c >> 1) & 15 (lanes c and c^1 hold the same value).
@@ -831,8 +836,9 @@ __global__ __launch_bounds__(NT) void attn_pool_bwd_dk_kernel(const AttnArgs A) 
       }
       if (use_bits)
         for (int i = t; i < QC * 4; i += NT) {
-          const int qq = qbase + i / 4;
-          kw_s[i] = qq < Lq ? P.keep_bits[(bh * Lq + qbase) * 4 + i] : 0u;
+          // this workgroup's four 32-key words of query qq (kw_ld words per query row)
+          const int qq = qbase + i / 4, wd = kb * 4 + (i & 3);
+          kw_s[i] = (qq < Lq && wd < P.kw_ld) ? P.keep_bits[(bh * Lq + qq) * P.kw_ld + wd] : 0u;
         }
       __syncthreads();
       if (!wave_active) continue;
@@ -847,7 +853,7 @@ __global__ __launch_bounds__(NT) void attn_pool_bwd_dk_kernel(const AttnArgs A) 
           const bool valid = kvalid && lq != -INFINITY && (qbase + ql < Lq);
           const float p = valid ? __expf(s[r] * scale - lq) : 0.f;
           bool keep = true;
-          if (use_bits) keep = (kw_s[ql * 4 + (key >> 5)] >> (key & 31)) & 1u;
+          if (use_bits) keep = (kw_s[ql * 4 + w] >> c) & 1u;   // key = kb*128 + 32w + c
           const float pd = keep ? p * inv_keep : 0.f;
           ds[r] = pd * dpk - p * dsum_s[ql];
         }
@@ -871,6 +877,288 @@ MMF_CHAIN16(dk[dt], ds[r], Qs[(qt * 32 + acc_row(r, h)) * LS + dt * 32 + c])
 }
 
 // ---------------------------------------------------------------------------
+// Long-key pooled kernels (Lk > 128, e.g. C5's T = 512): the same pooled
+// formulation, with keys streamed through LDS in chunks instead of held whole.
+//   fwd pass 1 (query on the lane): LSE by an online max / sum over key chunks,
+//       and the dropout keep words (B, heads, Lq, kw_ld), bit k%32 of word k/32;
+//   fwd pass 2 (key on the lane, queries streamed): pbar = colsum(P') / Lq;
+//   bwd dQ (query on the lane, two passes over key chunks): D, then dS and dQ;
+//   bwd dK: attn_pool_bwd_dk_kernel (key on the lane; any Lk).
+// ---------------------------------------------------------------------------
+template <int HDP, bool BF>
+__global__ __launch_bounds__(NT) void attn_poolL_lse_kernel(const AttnArgs A) {
+  constexpr int KC = HDP == 32 ? 128 : 64;
+  constexpr int LS = HDP + 4;
+  constexpr int HALF = HDP / 2;
+  __shared__ __attribute__((aligned(16))) float Ks[KC * LS];
+
+  const AttnPair& P = A.p[blockIdx.y];
+  const int qblocks = (P.Lq + 127) / 128;
+  int bid = blockIdx.x;
+  if (bid >= A.B * A.heads * qblocks) return;
+  const int qb = bid % qblocks;
+  bid /= qblocks;
+  const int head = bid % A.heads, b = bid / A.heads;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, c = lane & 31;
+  const int hd = A.hd, col0 = head * hd;
+  const int Lq = P.Lq, Lk = P.Lk, kwl = P.kw_ld;
+  const int q = qb * 128 + w * 32 + c;
+  const bool qvalid = q < Lq;
+  const bool wave_active = qb * 128 + w * 32 < Lq;
+  const int64_t bh = (int64_t)b * A.heads + head;
+  const int64_t rowidx = bh * Lq + q;
+  const float pdrop = A.drop_p;
+  RngSnap rs{0, 0};
+  if (pdrop > 0.f && A.rng) rs = *A.rng;
+  const bool bits_out = P.keep_bits != nullptr && pdrop > 0.f;
+
+  // masked key modality: every probability is 0 (src/attention.py:127-129); the
+  // keep words are never read when LSE = -inf
+  if (P.kmask_mode == 1 && P.kmask[(int64_t)b * P.kmask_ld] == 0.f) {
+    if (qvalid && h == 0) P.lse[rowidx] = -INFINITY;
+    return;
+  }
+  const bool vk = (P.ldk % 4 == 0) && (hd % 4 == 0);
+  float qf[HALF];
+  load_frag<HALF>(qf, P.q + ((int64_t)b * Lq + (qvalid ? q : 0)) * P.ldq + col0, h * HALF, hd, qvalid);
+  const float sl2 = A.scale * LOG2E;
+  const bool aligned8 = (Lk & 7) == 0;
+  float m = -INFINITY, l = 0.f;   // running max / sum, log2 domain
+  for (int kbase = 0; kbase < Lk; kbase += KC) {
+    __syncthreads();
+    load_rows<KC, HDP, LS>(Ks, P.k + (int64_t)b * Lk * P.ldk + col0, Lk, P.ldk, kbase, hd, vk);
+    __syncthreads();
+    if (!wave_active) continue;
+    const int nkt = (min(KC, Lk - kbase) + 31) / 32;
+    for (int kt = 0; kt < nkt; ++kt) {
+      const f32x16 s = dot_rows<HALF, BF>(Ks + (kt * 32 + c) * LS + h * HALF, qf, zero16());
+      float sv[16];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kbase + kt * 32 + acc_row(r, h);
+        const bool valid = key < Lk && (P.kmask_mode != 2 || kmask_val(P, b, key) != 0.f);
+        sv[r] = valid ? s[r] * sl2 : -INFINITY;
+        mx = fmaxf(mx, sv[r]);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      const float mnew = fmaxf(m, mx);
+      const float mref = mnew == -INFINITY ? 0.f : mnew;   // exp2(-inf - mref) = 0, no NaN
+      float ls = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ls += fast_exp2(sv[r] - mref);
+      ls += __shfl_xor(ls, 32);
+      l = l * fast_exp2(m - mref) + ls;
+      m = mnew;
+      if (bits_out) {
+        const uint32_t kb16 =
+            keep_tile16(rs, P.drop_site, (uint64_t)rowidx * Lk + kbase + kt * 32, pdrop, h, qvalid, aligned8);
+        uint32_t bits = 0;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) bits |= ((kb16 >> (4 * g)) & 0xFu) << (8 * g + 4 * h);
+        bits |= __shfl_xor(bits, 32);
+        if (qvalid && h == 0) P.keep_bits[rowidx * kwl + ((kbase >> 5) + kt)] = bits;
+      }
+    }
+  }
+  if (qvalid && h == 0) P.lse[rowidx] = l > 0.f ? (m + __log2f(l)) * (1.f / LOG2E) : -INFINITY;
+}
+
+template <int HDP, bool BF>
+__global__ __launch_bounds__(NT) void attn_poolL_colsum_kernel(const AttnArgs A) {
+  constexpr int QC = 128;
+  constexpr int LS = HDP + 4;
+  constexpr int HALF = HDP / 2;
+  __shared__ __attribute__((aligned(16))) float Qs[QC * LS];
+  __shared__ float lse_s[QC];
+  __shared__ uint32_t kw_s[QC * 4];
+
+  const AttnPair& P = A.p[blockIdx.y];
+  const int kblocks = (P.Lk + 127) / 128;
+  int bid = blockIdx.x;
+  if (bid >= A.B * A.heads * kblocks) return;
+  const int kb = bid % kblocks;
+  bid /= kblocks;
+  const int head = bid % A.heads, b = bid / A.heads;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, c = lane & 31;
+  const int hd = A.hd, col0 = head * hd;
+  const int Lq = P.Lq, Lk = P.Lk;
+  const int key = kb * 128 + w * 32 + c;
+  const bool wave_active = kb * 128 + w * 32 < Lk;
+  bool kvalid = key < Lk;
+  if (kvalid && P.kmask_mode == 2) kvalid = kmask_val(P, b, key) != 0.f;
+  const int64_t bh = (int64_t)b * A.heads + head;
+  const float pdrop = A.drop_p;
+  const float inv_keep = pdrop > 0.f ? (pdrop < 1.f ? 1.f / (1.f - pdrop) : 0.f) : 1.f;
+  const bool use_bits = P.keep_bits != nullptr && pdrop > 0.f;
+  const float sl2 = A.scale * LOG2E;
+
+  float cs = 0.f;
+  const bool sample_masked = (P.kmask_mode == 1 && P.kmask[(int64_t)b * P.kmask_ld] == 0.f);
+  if (!sample_masked) {
+    float kf[HALF];
+    load_frag<HALF>(kf, P.k + ((int64_t)b * Lk + (key < Lk ? key : 0)) * P.ldk + col0, h * HALF, hd, key < Lk);
+    const bool vq = (P.ldq % 4 == 0) && (hd % 4 == 0);
+    for (int qbase = 0; qbase < Lq; qbase += QC) {
+      __syncthreads();
+      load_rows<QC, HDP, LS>(Qs, P.q + (int64_t)b * Lq * P.ldq + col0, Lq, P.ldq, qbase, hd, vq);
+      for (int i = t; i < QC; i += NT) {
+        const int qq = qbase + i;
+        lse_s[i] = qq < Lq ? P.lse[bh * Lq + qq] * LOG2E : -INFINITY;
+      }
+      if (use_bits)
+        for (int i = t; i < QC * 4; i += NT) {
+          const int qq = qbase + i / 4, wd = kb * 4 + (i & 3);
+          kw_s[i] = (qq < Lq && wd < P.kw_ld) ? P.keep_bits[(bh * Lq + qq) * P.kw_ld + wd] : 0u;
+        }
+      __syncthreads();
+      if (!wave_active) continue;
+      const int nqt = (min(QC, Lq - qbase) + 31) / 32;
+      for (int qt = 0; qt < nqt; ++qt) {
+        const f32x16 s = dot_rows<HALF, BF>(Qs + (qt * 32 + c) * LS + h * HALF, kf, zero16());
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ql = qt * 32 + acc_row(r, h);
+          const float lq = lse_s[ql];
+          const bool valid = kvalid && lq != -INFINITY && (qbase + ql < Lq);
+          const bool keep = !use_bits || ((kw_s[ql * 4 + w] >> c) & 1u);
+          cs += (valid && keep) ? fast_exp2(s[r] * sl2 - lq) : 0.f;
+        }
+      }
+    }
+  }
+  cs = (cs + __shfl_xor(cs, 32)) * inv_keep * (1.f / (float)Lq);
+  if (wave_active && h == 0 && key < Lk) {
+    P.pbar[bh * Lk + key] = cs;
+    if (P.pbarT) P.pbarT[((int64_t)b * Lk + key) * A.heads + head] = cs;
+  }
+}
+
+template <int HDP, bool BF>
+__global__ __launch_bounds__(NT) void attn_poolL_dq_kernel(const AttnArgs A) {
+  constexpr int KC = HDP == 32 ? 128 : 64;
+  constexpr int LS = HDP + 4;
+  constexpr int HALF = HDP / 2;
+  constexpr int NDT = HDP / 32;
+  __shared__ __attribute__((aligned(16))) float Ks[KC * LS];
+  __shared__ float dpb[KC];
+
+  const AttnPair& P = A.p[blockIdx.y];
+  const int qblocks = (P.Lq + 127) / 128;
+  int bid = blockIdx.x;
+  if (bid >= A.B * A.heads * qblocks) return;
+  const int qb = bid % qblocks;
+  bid /= qblocks;
+  const int head = bid % A.heads, b = bid / A.heads;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, c = lane & 31;
+  const int hd = A.hd, col0 = head * hd;
+  const int Lq = P.Lq, Lk = P.Lk, kwl = P.kw_ld;
+  const int q = qb * 128 + w * 32 + c;
+  const bool qvalid = q < Lq;
+  const bool wave_active = qb * 128 + w * 32 < Lq;
+  const int64_t bh = (int64_t)b * A.heads + head;
+  const int64_t rowidx = bh * Lq + q;
+  const float scale = A.scale, pdrop = A.drop_p;
+  const float inv_keep = pdrop > 0.f ? (pdrop < 1.f ? 1.f / (1.f - pdrop) : 0.f) : 1.f;
+  const bool use_bits = P.keep_bits != nullptr && pdrop > 0.f;
+  const float gscale = inv_keep / (float)Lq;   // dP'[q, k] = dpbar[k] / Lq, through the dropout scale
+  float* qrow = P.dq + ((int64_t)b * Lq + (qvalid ? q : 0)) * P.ldq + col0;
+
+  if (P.kmask_mode == 1 && P.kmask[(int64_t)b * P.kmask_ld] == 0.f) {
+    if (qvalid) {
+      for (int d = h; d < hd; d += 2) qrow[d] = 0.f;
+      if (h == 0) P.dsum[rowidx] = 0.f;
+    }
+    return;
+  }
+  const bool vk = (P.ldk % 4 == 0) && (hd % 4 == 0);
+  float qf[HALF];
+  load_frag<HALF>(qf, P.q + ((int64_t)b * Lq + (qvalid ? q : 0)) * P.ldq + col0, h * HALF, hd, qvalid);
+  const float sl2 = scale * LOG2E;
+  const float lse2 = qvalid ? P.lse[rowidx] * LOG2E : -INFINITY;
+  const bool rowlive = qvalid && lse2 != -INFINITY;
+  const float* kbase_ptr = P.k + (int64_t)b * Lk * P.ldk + col0;
+
+  // probabilities (pre-dropout) and keep bits of one 32-key tile
+  auto tile = [&](int kbase, int kt, float (&pr)[16], uint32_t& word) {
+    const f32x16 s = dot_rows<HALF, BF>(Ks + (kt * 32 + c) * LS + h * HALF, qf, zero16());
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = kbase + kt * 32 + acc_row(r, h);
+      const bool valid = rowlive && key < Lk && (P.kmask_mode != 2 || kmask_val(P, b, key) != 0.f);
+      pr[r] = valid ? fast_exp2(s[r] * sl2 - lse2) : 0.f;
+    }
+    word = (use_bits && qvalid) ? P.keep_bits[rowidx * kwl + ((kbase >> 5) + kt)] : 0xFFFFFFFFu;
+  };
+  auto stage = [&](int kbase) {
+    __syncthreads();
+    load_rows<KC, HDP, LS>(Ks, kbase_ptr, Lk, P.ldk, kbase, hd, vk);
+    for (int i = t; i < KC; i += NT) dpb[i] = kbase + i < Lk ? P.dpbar[bh * Lk + kbase + i] * gscale : 0.f;
+    __syncthreads();
+  };
+
+  // pass A: D = sum_k P'[q, k] dP'[q, k]
+  float D = 0.f;
+  for (int kbase = 0; kbase < Lk; kbase += KC) {
+    stage(kbase);
+    if (!wave_active) continue;
+    const int nkt = (min(KC, Lk - kbase) + 31) / 32;
+    for (int kt = 0; kt < nkt; ++kt) {
+      float pr[16];
+      uint32_t word;
+      tile(kbase, kt, pr, word);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kl = kt * 32 + acc_row(r, h);
+        D += ((word >> (kl & 31)) & 1u) ? pr[r] * dpb[kl] : 0.f;
+      }
+    }
+  }
+  D += __shfl_xor(D, 32);
+  if (qvalid && h == 0) P.dsum[rowidx] = D;
+
+  // pass B: dS = P (dP - D), dQ = scale dS K
+  f32x16 dq[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) dq[dt] = zero16();
+  for (int kbase = 0; kbase < Lk; kbase += KC) {
+    stage(kbase);
+    if (!wave_active) continue;
+    const int nkt = (min(KC, Lk - kbase) + 31) / 32;
+    for (int kt = 0; kt < nkt; ++kt) {
+      float pr[16], ds[16];
+      uint32_t word;
+      tile(kbase, kt, pr, word);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kl = kt * 32 + acc_row(r, h);
+        ds[r] = pr[r] * ((((word >> (kl & 31)) & 1u) ? dpb[kl] : 0.f) - D);
+      }
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+MMF_CHAIN16(dq[dt], Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], ds[r])
+    }
+  }
+  if (!qvalid) return;
+  const bool vo = (P.ldq % 4 == 0) && (hd % 4 == 0);
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d0 = dt * 32 + 8 * g + 4 * h;
+      if (vo && d0 + 3 < hd) {
+        *reinterpret_cast<float4*>(qrow + d0) =
+            make_float4(dq[dt][4 * g] * scale, dq[dt][4 * g + 1] * scale, dq[dt][4 * g + 2] * scale,
+                        dq[dt][4 * g + 3] * scale);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (d0 + j < hd) qrow[d0 + j] = dq[dt][4 * g + j] * scale;
+      }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Lean pooled kernels: the same three passes for the common HybridFusion case
 // (every key valid: Lk % 32 == 0, Lk <= 128, no per-key mask; float4-able
 // rows), with the per-score work cut to a handful of VALU ops: scores stay in
@@ -878,9 +1166,6 @@ MMF_CHAIN16(dk[dt], ds[r], Qs[(qt * 32 + acc_row(r, h)) * LS + dt * 32 + c])
 // tests (invalid query lanes get a zero weight / +inf LSE), and per-key /
 // per-query side data are read from LDS as broadcast float4s.
 // ---------------------------------------------------------------------------
-constexpr float LOG2E = 1.4426950408889634f;
-
-__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 template <int HALF>
 __device__ __forceinline__ void load_frag_vec(float* f, const float* row) {
@@ -1412,7 +1697,7 @@ const char* with_bf(const char* base, bool bf) {
   return slot.c_str();
 }
 
-enum class Kind { Fwd, Probs, Prep, Dkv, Dq, PoolFwd, PoolDq, PoolDk, PoolFused };
+enum class Kind { Fwd, Probs, Prep, Dkv, Dq, PoolFwd, PoolDq, PoolDk, PoolFused, PoolLse, PoolColsum, PoolDqLong };
 
 hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, int heads, int hd,
                           float scale, float drop_p, const RngSnap* rng, hipStream_t st) {
@@ -1450,10 +1735,19 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
       if (kind == Kind::Prep)
         nb = prep_vec ? ((int64_t)B * P.Lq * (heads * hd / 4) + NT - 1) / NT
                       : ((int64_t)B * P.Lq * heads + NT - 1) / NT;
-      else if (kind == Kind::Dkv || kind == Kind::PoolDk) nb = (int64_t)B * heads * ((P.Lk + 127) / 128);
+      else if (kind == Kind::Dkv || kind == Kind::PoolDk || kind == Kind::PoolColsum)
+        nb = (int64_t)B * heads * ((P.Lk + 127) / 128);
       else if (kind == Kind::PoolFwd || kind == Kind::PoolFused) nb = (int64_t)B * heads;
       else nb = (int64_t)B * heads * ((P.Lq + 127) / 128);
-      if (pooled && P.Lk > PKC)
+      // one-chunk pooled kernels hold every key in LDS; the long-key kinds stream them
+      if ((kind == Kind::PoolFwd || kind == Kind::PoolDq || kind == Kind::PoolFused) && P.Lk > PKC)
+        return hipErrorInvalidValue;
+      // long-key keep words: kw_ld words of 32 keys per query row
+      if ((kind == Kind::PoolLse || kind == Kind::PoolColsum || kind == Kind::PoolDqLong || kind == Kind::PoolDk) &&
+          P.keep_bits != nullptr && P.kw_ld < (P.Lk + 31) / 32)
+        return hipErrorInvalidValue;
+      if ((kind == Kind::PoolLse || kind == Kind::PoolColsum || kind == Kind::PoolDqLong || kind == Kind::PoolDk) &&
+          drop_p > 0.f && P.keep_bits == nullptr)
         return hipErrorInvalidValue;
       if (nb > maxblk) maxblk = nb;
       ++n;
@@ -1484,9 +1778,12 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
         case Kind::PoolDq: fl += qk; by += 4 * (2 * bq + bk); break;                      // Q K -> dQ
         case Kind::PoolDk: fl += qk; by += 4 * (bq + 2 * bk); break;                      // Q K -> dK
         case Kind::PoolFused: fl += 2 * qk; by += 4 * (2 * bq + 2 * bk); break;           // Q K -> dQ dK
+        case Kind::PoolLse: fl += qk; by += 4 * (bq + bk); break;                         // Q K -> lse
+        case Kind::PoolColsum: by += 4 * (bq + bk); break;                                // (S recomputed) -> pbar
+        case Kind::PoolDqLong: fl += qk; by += 4 * (2 * bq + bk); break;                  // Q K -> dQ
       }
     }
-    static const char* const kNames[9][4] = {
+    static const char* const kNames[12][4] = {
         {"attn_fwd_kernel<32, 0>", "attn_fwd_kernel<64, 0>", "attn_fwd_kernel<32, 0>", "attn_fwd_kernel<64, 0>"},
         {"attn_fwd_kernel<32, 1>", "attn_fwd_kernel<64, 1>", "attn_fwd_kernel<32, 1>", "attn_fwd_kernel<64, 1>"},
         {"attn_bwd_prep_kernel", "attn_bwd_prep_kernel", "attn_bwd_prep_vec_kernel", "attn_bwd_prep_vec_kernel"},
@@ -1497,11 +1794,26 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
          "attn_pool_bwd_dq_lean<64>"},
         {"attn_pool_bwd_dk_kernel<32>", "attn_pool_bwd_dk_kernel<64>", "attn_pool_bwd_dk_lean<32>",
          "attn_pool_bwd_dk_lean<64>"},
-        {"", "", "attn_pool_bwd_fused_lean<32>", "attn_pool_bwd_fused_lean<64>"}};
-    const bool alt = kind == Kind::Prep ? prep_vec : lean;
+        {"", "", "attn_pool_bwd_fused_lean<32>", "attn_pool_bwd_fused_lean<64>"},
+        {"attn_poolL_lse_kernel<32>", "attn_poolL_lse_kernel<64>", "", ""},
+        {"attn_poolL_colsum_kernel<32>", "attn_poolL_colsum_kernel<64>", "", ""},
+        {"attn_poolL_dq_kernel<32>", "attn_poolL_dq_kernel<64>", "", ""}};
+    const bool alt = kind == Kind::Prep ? prep_vec : (lean && kind <= Kind::PoolFused);
     const bool bf = math_bf16();
     ProfLaunch prof_(st, with_bf(kNames[(int)kind][(alt ? 2 : 0) + (small ? 0 : 1)], bf), fl, by);
     switch (kind) {
+      case Kind::PoolLse:
+        if (small) { if (bf) hipLaunchKernelGGL((attn_poolL_lse_kernel<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_lse_kernel<32, false>), grid, dim3(NT), 0, st, a); }
+        else { if (bf) hipLaunchKernelGGL((attn_poolL_lse_kernel<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_lse_kernel<64, false>), grid, dim3(NT), 0, st, a); }
+        break;
+      case Kind::PoolColsum:
+        if (small) { if (bf) hipLaunchKernelGGL((attn_poolL_colsum_kernel<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_colsum_kernel<32, false>), grid, dim3(NT), 0, st, a); }
+        else { if (bf) hipLaunchKernelGGL((attn_poolL_colsum_kernel<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_colsum_kernel<64, false>), grid, dim3(NT), 0, st, a); }
+        break;
+      case Kind::PoolDqLong:
+        if (small) { if (bf) hipLaunchKernelGGL((attn_poolL_dq_kernel<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_dq_kernel<32, false>), grid, dim3(NT), 0, st, a); }
+        else { if (bf) hipLaunchKernelGGL((attn_poolL_dq_kernel<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_dq_kernel<64, false>), grid, dim3(NT), 0, st, a); }
+        break;
       case Kind::Fwd:
         if (small) { if (bf) hipLaunchKernelGGL((attn_fwd_kernel<32, 0, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_fwd_kernel<32, 0, false>), grid, dim3(NT), 0, st, a); }
         else { if (bf) hipLaunchKernelGGL((attn_fwd_kernel<64, 0, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_fwd_kernel<64, 0, false>), grid, dim3(NT), 0, st, a); }
@@ -1563,18 +1875,43 @@ hipError_t launch_attn_probs(const AttnPair* pairs, int npairs, int B, int heads
   return launch_generic(Kind::Probs, pairs, npairs, B, heads, hd, scale, drop_p, rng, st);
 }
 
+// pairs whose keys fit one LDS chunk (Lk <= PKC) vs the long-key kernels
+static void split_by_keys(const AttnPair* pairs, int npairs, std::vector<AttnPair>& shortp,
+                          std::vector<AttnPair>& longp) {
+  for (int i = 0; i < npairs; ++i) (pairs[i].Lk > PKC ? longp : shortp).push_back(pairs[i]);
+}
+
 hipError_t launch_attn_pool_fwd(const AttnPair* pairs, int npairs, int B, int heads, int hd, float scale,
                                 float drop_p, const RngSnap* rng, hipStream_t st) {
-  return launch_generic(Kind::PoolFwd, pairs, npairs, B, heads, hd, scale, drop_p, rng, st);
+  std::vector<AttnPair> sp, lp;
+  split_by_keys(pairs, npairs, sp, lp);
+  hipError_t e = hipSuccess;
+  if (!sp.empty()) e = launch_generic(Kind::PoolFwd, sp.data(), (int)sp.size(), B, heads, hd, scale, drop_p, rng, st);
+  if (e == hipSuccess && !lp.empty())
+    e = launch_generic(Kind::PoolLse, lp.data(), (int)lp.size(), B, heads, hd, scale, drop_p, rng, st);
+  if (e == hipSuccess && !lp.empty())
+    e = launch_generic(Kind::PoolColsum, lp.data(), (int)lp.size(), B, heads, hd, scale, drop_p, rng, st);
+  return e;
 }
 
 hipError_t launch_attn_pool_bwd(int stage, const AttnPair* pairs, int npairs, int B, int heads, int hd,
                                 float scale, float drop_p, const RngSnap* rng, hipStream_t st) {
   // stage 2: both gradients in one pass when the fused lean kernel applies
   // (hipErrorNotSupported otherwise: run stages 0 and 1)
-  return launch_generic(stage == 0 ? Kind::PoolDq : (stage == 1 ? Kind::PoolDk : Kind::PoolFused), pairs, npairs,
-                        B, heads, hd, scale,
-                        drop_p, rng, st);
+  std::vector<AttnPair> sp, lp;
+  split_by_keys(pairs, npairs, sp, lp);
+  if (stage == 2) {
+    if (!lp.empty()) return hipErrorNotSupported;
+    return launch_generic(Kind::PoolFused, pairs, npairs, B, heads, hd, scale, drop_p, rng, st);
+  }
+  hipError_t e = hipSuccess;
+  if (!sp.empty())
+    e = launch_generic(stage == 0 ? Kind::PoolDq : Kind::PoolDk, sp.data(), (int)sp.size(), B, heads, hd, scale,
+                       drop_p, rng, st);
+  if (e == hipSuccess && !lp.empty())
+    e = launch_generic(stage == 0 ? Kind::PoolDqLong : Kind::PoolDk, lp.data(), (int)lp.size(), B, heads, hd,
+                       scale, drop_p, rng, st);
+  return e;
 }
 
 hipError_t launch_attn_bwd_stage(int stage, const AttnPair* pairs, int npairs, int B, int heads, int hd,

@@ -24,11 +24,20 @@ namespace {
 inline int Lm(const mmf_hybrid_desc* d, int m) { return d->seq_len[m] > 0 ? d->seq_len[m] : 1; }
 inline bool dropping(const mmf_hybrid_desc* d) { return d->training && d->dropout > 0.f; }
 
+// Pooled plan (attention.hip "Pooled-output attention"): keys up to 128 run the
+// one-chunk kernels, longer keys the streamed long-key kernels; the pooled
+// helpers keep heads x Lk query-mean probabilities in LDS (pool.hip POOL_PB_CAP).
 bool use_pool(const mmf_hybrid_desc* d) {
   if (d->num_heads > 8) return false;
   for (int g = 0; g < d->num_pairs; ++g)
-    if (Lm(d, d->pair_k[g]) > 128) return false;
+    if (Lm(d, d->pair_k[g]) * d->num_heads > POOL_PB_CAP) return false;
   return true;
+}
+inline int kw_ld(int lk) { return lk <= 128 ? 4 : (lk + 31) / 32; }
+inline bool long_keys(const mmf_hybrid_desc* d) {
+  for (int g = 0; g < d->num_pairs; ++g)
+    if (Lm(d, d->pair_k[g]) > 128) return true;
+  return false;
 }
 
 struct Saved {
@@ -64,7 +73,7 @@ void layout_saved(const mmf_hybrid_desc* d, Bump& bp, Saved& s) {
       s.r[g] = bp.take<float>(B * nh);
       s.Ob[g] = bp.take<float>(B * H);
       s.Ab[g] = bp.take<float>(B * H);
-      if (dropping(d)) s.bits[g] = bp.take<uint32_t>(B * nh * lq * 4);
+      if (dropping(d)) s.bits[g] = bp.take<uint32_t>(B * nh * lq * kw_ld((int)lk));
     } else {
       s.V[g] = bp.take<float>(B * lk * H);
       s.O[g] = bp.take<float>(B * lq * H);
@@ -239,7 +248,7 @@ void fill_head(HeadArgs& ha, const mmf_hybrid_desc* d, const mmf_hybrid_params* 
 }
 
 bool use_tail(const mmf_hybrid_desc* d) {
-  return use_pool(d) && tail_supported(d->num_modalities, d->hidden, d->num_classes, d->num_heads,
+  return use_pool(d) && !long_keys(d) && tail_supported(d->num_modalities, d->hidden, d->num_classes, d->num_heads,
                                        d->hidden / d->num_heads, d->num_pairs);
 }
 
@@ -288,6 +297,7 @@ AttnPair make_pair(const mmf_hybrid_desc* d, const Saved& s, const float* mask, 
   a.pbar = s.pbar[g];
   a.pbarT = s.pbarT[g];
   a.keep_bits = s.bits[g];
+  a.kw_ld = kw_ld(a.Lk);
   return a;
 }
 

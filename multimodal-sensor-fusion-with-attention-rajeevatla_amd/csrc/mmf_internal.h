@@ -193,8 +193,9 @@ struct AttnPair {
   float* pbar;         // (B, heads, Lk) fwd output: mean over queries of the post-dropout probs
   float* pbarT;        // optional (B, Lk, heads) copy of pbar (an RK GEMM operand for E_m)
   const float* dpbar;  // (B, heads, Lk) bwd input: d loss / d pbar
-  uint32_t* keep_bits; // (B, heads, Lq, 4) dropout keep mask written by the pooled forward
-                       // (Lk <= 128: bit k%32 of word k/32), read by its backward
+  uint32_t* keep_bits; // (B, heads, Lq, kw_ld) dropout keep mask written by the pooled forward
+                       // (bit k%32 of word k/32), read by its backward
+  int32_t kw_ld;       // words per query row: 4 when Lk <= 128, ceil(Lk/32) otherwise
 };
 
 constexpr int ATTN_MAX_PAIRS = 12;
@@ -242,6 +243,7 @@ struct PoolPair {
   float* dpbar;        // (B, heads, Lk)
 };
 constexpr int POOL_MAX_PAIRS = 12;
+constexpr int POOL_PB_CAP = 4096;   // heads x Lk query-mean probabilities one pool_u workgroup stages in LDS
 struct PoolArgs {
   PoolPair p[POOL_MAX_PAIRS];
   int32_t npairs, B, heads, hd, H;

@@ -17,10 +17,8 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int MAXH = 8;           // heads supported by the pooled helpers
-constexpr int MAXLK = 128;
-
 __global__ __launch_bounds__(NT) void pool_u_kernel(const PoolArgs a) {
-  __shared__ float pb[MAXH * MAXLK];
+  __shared__ float pb[POOL_PB_CAP];
   __shared__ float4 red[NT];
   const PoolPair& P = a.p[blockIdx.y];
   const int b = blockIdx.x, t = threadIdx.x;
@@ -165,7 +163,7 @@ hipError_t launch_pool(bool fwd, const PoolPair* pairs, int npairs, int B, int h
     memset(&a, 0, sizeof(a));
     int n = 0;
     while (done < npairs && n < POOL_MAX_PAIRS) {
-      if (pairs[done].Lk > MAXLK) return hipErrorInvalidValue;
+      if (pairs[done].Lk * heads > POOL_PB_CAP || heads > MAXH) return hipErrorInvalidValue;
       a.p[n++] = pairs[done++];
     }
     a.npairs = n;

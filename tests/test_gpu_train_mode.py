@@ -3,9 +3,11 @@
 The device draws its dropout masks from Philox4x32-10 (csrc/mmf_device.h);
 tests/_philox.py replays the same streams in numpy and feeds them to the CPU
 oracle, so forward outputs and every gradient can be compared at the same
-1e-3 tolerance as eval mode.  Covers both HybridFusion execution plans
-(pooled: every key length <= 128; general: a key modality longer than 128)
-and the standalone CrossModalAttention.
+1e-3 tolerance as eval mode.  Covers both HybridFusion execution plans --
+pooled (one-chunk kernels for keys <= 128, the streamed long-key kernels
+beyond: several key chunks, several query blocks, unaligned key counts) and
+general (heads x Lk beyond the pooled helpers' LDS budget) -- and the
+standalone CrossModalAttention.
 """
 import numpy as np
 import pytest
@@ -42,6 +44,15 @@ TRAIN_CASES = [
                mask=[[1, 1, 1], [1, 0, 1], [0.5, 1, 0]]),
     HybridCase("train_general_long", ["x", "y"], {"x": 16, "y": 8},
                {"x": 20, "y": 140}, batch=2, hidden=64, heads=2, classes=3, seed=53,
+               mask=[[1, 1], [1, 0]]),
+    # long-key pooled kernels, head_dim 64: Lk = 300 (3 key chunks, 10 keep words,
+    # Lk % 8 != 0) and Lq = 300 (3 query blocks) against Lk = 160
+    HybridCase("train_long_hd64", ["a", "b"], {"a": 32, "b": 48},
+               {"a": 160, "b": 300}, batch=2, hidden=128, heads=2, classes=4, seed=55,
+               mask=[[1, 1], [0.5, 1]]),
+    # heads x Lk = 8 x 520 > POOL_PB_CAP: the general (flash) plan
+    HybridCase("train_general_wide", ["x", "y"], {"x": 16, "y": 8},
+               {"x": 20, "y": 520}, batch=2, hidden=64, heads=8, classes=3, seed=56,
                mask=[[1, 1], [1, 0]]),
 ]
 
@@ -111,3 +122,30 @@ def test_philox_replay_statistics():
     b = keep_mask((64, 1000), 0x301, SEED, OFFSET, 0.3)
     assert 0.68 < a.mean() < 0.72
     assert 0.45 < (a == b).mean() < 0.65
+
+
+def test_long_key_plan_selection(mods):
+    """Keys > 128 run the streamed pooled kernels; heads x Lk beyond the pooled
+    helpers' LDS budget runs the general flash plan (kernel names from the
+    library's per-launch profiler)."""
+    fusion, _ = mods
+    import mmf_native
+    expect = {"train_long_hd64": ("attn_poolL_lse_kernel", "attn_poolL_colsum_kernel", "attn_poolL_dq_kernel",
+                                  "attn_pool_bwd_dk_kernel"),
+              "train_general_wide": ("attn_fwd_kernel", "attn_bwd_dkv_kernel", "attn_bwd_dq_kernel")}
+    for case in TRAIN_CASES:
+        if case.name not in expect:
+            continue
+        sd = hybrid_state(case.names, case.dims, case.hidden, case.classes, case.seed)
+        model = fusion.HybridFusion({m: case.dims[m] for m in case.names}, hidden_dim=case.hidden,
+                                    num_classes=case.classes, num_heads=case.heads, dropout=P)
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+        model = model.cuda().train()
+        feats_np, mask_np, _ = hybrid_inputs(case)
+        feats = {m: torch.from_numpy(v).cuda().requires_grad_(True) for m, v in feats_np.items()}
+        mmf_native.profile_begin()
+        model(feats, torch.from_numpy(mask_np).cuda()).sum().backward()
+        _, launches = mmf_native.profile_end()
+        names = {k.split("<")[0] for _, k, *_ in launches}
+        for k in expect[case.name]:
+            assert k in names, (case.name, k, sorted(names))
