@@ -793,8 +793,9 @@ __global__ __launch_bounds__(NT) void attn_pool_bwd_dk_kernel(const AttnArgs A) 
   constexpr int HALF = HDP / 2;
   constexpr int NDT = HDP / 32;
   __shared__ __attribute__((aligned(16))) float Qs[QC * LS];
-  __shared__ float lse_s[QC], dsum_s[QC];
-  __shared__ uint32_t kw_s[QC * 4];
+  __shared__ __attribute__((aligned(16))) float lse_s[QC];        // log2 units; +inf: no probability
+  __shared__ __attribute__((aligned(16))) float dsum_s[QC];
+  __shared__ __attribute__((aligned(16))) uint32_t kw_s[4 * QC];   // [wave][query]: keep word of the wave's 32 keys
 
   const AttnPair& P = A.p[blockIdx.y];
   const int kblocks = (P.Lk + 127) / 128;
@@ -815,6 +816,7 @@ __global__ __launch_bounds__(NT) void attn_pool_bwd_dk_kernel(const AttnArgs A) 
   const float inv_keep = pdrop < 1.f ? 1.f / (1.f - pdrop) : 0.f;
   const float inv_lq = 1.f / (float)Lq;
   const bool use_bits = P.keep_bits && pdrop > 0.f;
+  const float sl2 = scale * LOG2E;
 
   f32x16 dk[NDT];
 #pragma unroll
@@ -824,20 +826,21 @@ __global__ __launch_bounds__(NT) void attn_pool_bwd_dk_kernel(const AttnArgs A) 
     float kf[HALF];
     load_frag<HALF>(kf, P.k + ((int64_t)b * Lk + (key < Lk ? key : 0)) * P.ldk + col0, h * HALF, hd,
                     key < Lk);
-    const float dpk = key < Lk ? P.dpbar[bh * Lk + key] * inv_lq : 0.f;
+    const float dpk = key < Lk ? P.dpbar[bh * Lk + key] * inv_lq * inv_keep : 0.f;
     const bool vq = (P.ldq % 4 == 0) && (hd % 4 == 0);
     for (int qbase = 0; qbase < Lq; qbase += QC) {
       __syncthreads();
       load_rows<QC, HDP, LS>(Qs, P.q + (int64_t)b * Lq * P.ldq + col0, Lq, P.ldq, qbase, hd, vq);
       for (int i = t; i < QC; i += NT) {
         const int qq = qbase + i;
-        lse_s[i] = qq < Lq ? P.lse[bh * Lq + qq] : -INFINITY;
+        const float l = qq < Lq ? P.lse[bh * Lq + qq] : -INFINITY;
+        lse_s[i] = l == -INFINITY ? INFINITY : l * LOG2E;
         dsum_s[i] = qq < Lq ? P.dsum[bh * Lq + qq] : 0.f;
       }
       if (use_bits)
         for (int i = t; i < QC * 4; i += NT) {
           // this workgroup's four 32-key words of query qq (kw_ld words per query row)
-          const int qq = qbase + i / 4, wd = kb * 4 + (i & 3);
+          const int wv = i / QC, qq = qbase + (i % QC), wd = kb * 4 + wv;
           kw_s[i] = (qq < Lq && wd < P.kw_ld) ? P.keep_bits[(bh * Lq + qq) * P.kw_ld + wd] : 0u;
         }
       __syncthreads();
@@ -847,15 +850,21 @@ __global__ __launch_bounds__(NT) void attn_pool_bwd_dk_kernel(const AttnArgs A) 
         f32x16 s = dot_rows<HALF, BF>(Qs + (qt * 32 + c) * LS + h * HALF, kf, zero16());
         float ds[16];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int ql = qt * 32 + acc_row(r, h);
-          const float lq = lse_s[ql];
-          const bool valid = kvalid && lq != -INFINITY && (qbase + ql < Lq);
-          const float p = valid ? __expf(s[r] * scale - lq) : 0.f;
-          bool keep = true;
-          if (use_bits) keep = (kw_s[ql * 4 + w] >> c) & 1u;   // key = kb*128 + 32w + c
-          const float pd = keep ? p * inv_keep : 0.f;
-          ds[r] = pd * dpk - p * dsum_s[ql];
+        for (int g = 0; g < 4; ++g) {
+          const int q0 = qt * 32 + 8 * g + 4 * h;   // regs 4g..4g+3: queries q0..q0+3
+          const float4 l4 = *reinterpret_cast<const float4*>(lse_s + q0);
+          const float4 d4 = *reinterpret_cast<const float4*>(dsum_s + q0);
+          const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv[4] = {d4.x, d4.y, d4.z, d4.w};
+          uint32_t kv[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+          if (use_bits) {
+            const uint4 k4 = *reinterpret_cast<const uint4*>(kw_s + w * QC + q0);
+            kv[0] = k4.x; kv[1] = k4.y; kv[2] = k4.z; kv[3] = k4.w;
+          }
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const float p = fast_exp2(s[4 * g + jj] * sl2 - lv[jj]);
+            ds[4 * g + jj] = kvalid ? p * ((((kv[jj] >> c) & 1u) ? dpk : 0.f) - dv[jj]) : 0.f;
+          }
         }
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt)
@@ -933,14 +942,18 @@ __global__ __launch_bounds__(NT) void attn_poolL_lse_kernel(const AttnArgs A) {
     for (int kt = 0; kt < nkt; ++kt) {
       const f32x16 s = dot_rows<HALF, BF>(Ks + (kt * 32 + c) * LS + h * HALF, qf, zero16());
       float sv[16];
-      float mx = -INFINITY;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kbase + kt * 32 + acc_row(r, h);
-        const bool valid = key < Lk && (P.kmask_mode != 2 || kmask_val(P, b, key) != 0.f);
-        sv[r] = valid ? s[r] * sl2 : -INFINITY;
-        mx = fmaxf(mx, sv[r]);
+      for (int r = 0; r < 16; ++r) sv[r] = s[r] * sl2;
+      if (kbase + kt * 32 + 32 > Lk || P.kmask_mode == 2) {   // partial tile / per-key mask only
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kbase + kt * 32 + acc_row(r, h);
+          if (!(key < Lk && (P.kmask_mode != 2 || kmask_val(P, b, key) != 0.f))) sv[r] = -INFINITY;
+        }
       }
+      float mx = sv[0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sv[r]);
       mx = fmaxf(mx, __shfl_xor(mx, 32));
       const float mnew = fmaxf(m, mx);
       const float mref = mnew == -INFINITY ? 0.f : mnew;   // exp2(-inf - mref) = 0, no NaN
@@ -970,8 +983,8 @@ __global__ __launch_bounds__(NT) void attn_poolL_colsum_kernel(const AttnArgs A)
   constexpr int LS = HDP + 4;
   constexpr int HALF = HDP / 2;
   __shared__ __attribute__((aligned(16))) float Qs[QC * LS];
-  __shared__ float lse_s[QC];
-  __shared__ uint32_t kw_s[QC * 4];
+  __shared__ __attribute__((aligned(16))) float lse_s[QC];        // log2 units; +inf: no probability
+  __shared__ __attribute__((aligned(16))) uint32_t kw_s[4 * QC];   // [wave][query]: keep word of the wave's 32 keys
 
   const AttnPair& P = A.p[blockIdx.y];
   const int kblocks = (P.Lk + 127) / 128;
@@ -1004,11 +1017,12 @@ __global__ __launch_bounds__(NT) void attn_poolL_colsum_kernel(const AttnArgs A)
       load_rows<QC, HDP, LS>(Qs, P.q + (int64_t)b * Lq * P.ldq + col0, Lq, P.ldq, qbase, hd, vq);
       for (int i = t; i < QC; i += NT) {
         const int qq = qbase + i;
-        lse_s[i] = qq < Lq ? P.lse[bh * Lq + qq] * LOG2E : -INFINITY;
+        const float l = qq < Lq ? P.lse[bh * Lq + qq] : -INFINITY;
+        lse_s[i] = l == -INFINITY ? INFINITY : l * LOG2E;
       }
       if (use_bits)
         for (int i = t; i < QC * 4; i += NT) {
-          const int qq = qbase + i / 4, wd = kb * 4 + (i & 3);
+          const int wv = i / QC, qq = qbase + (i % QC), wd = kb * 4 + wv;
           kw_s[i] = (qq < Lq && wd < P.kw_ld) ? P.keep_bits[(bh * Lq + qq) * P.kw_ld + wd] : 0u;
         }
       __syncthreads();
@@ -1017,16 +1031,23 @@ __global__ __launch_bounds__(NT) void attn_poolL_colsum_kernel(const AttnArgs A)
       for (int qt = 0; qt < nqt; ++qt) {
         const f32x16 s = dot_rows<HALF, BF>(Qs + (qt * 32 + c) * LS + h * HALF, kf, zero16());
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int ql = qt * 32 + acc_row(r, h);
-          const float lq = lse_s[ql];
-          const bool valid = kvalid && lq != -INFINITY && (qbase + ql < Lq);
-          const bool keep = !use_bits || ((kw_s[ql * 4 + w] >> c) & 1u);
-          cs += (valid && keep) ? fast_exp2(s[r] * sl2 - lq) : 0.f;
+        for (int g = 0; g < 4; ++g) {
+          const int q0 = qt * 32 + 8 * g + 4 * h;   // regs 4g..4g+3: queries q0..q0+3
+          const float4 l4 = *reinterpret_cast<const float4*>(lse_s + q0);
+          const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
+          uint32_t kv[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+          if (use_bits) {
+            const uint4 k4 = *reinterpret_cast<const uint4*>(kw_s + w * QC + q0);
+            kv[0] = k4.x; kv[1] = k4.y; kv[2] = k4.z; kv[3] = k4.w;
+          }
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj)
+            cs += ((kv[jj] >> c) & 1u) ? fast_exp2(s[4 * g + jj] * sl2 - lv[jj]) : 0.f;
         }
       }
     }
   }
+  if (!kvalid) cs = 0.f;
   cs = (cs + __shfl_xor(cs, 32)) * inv_keep * (1.f / (float)Lq);
   if (wave_active && h == 0 && key < Lk) {
     P.pbar[bh * Lk + key] = cs;
@@ -1041,7 +1062,7 @@ __global__ __launch_bounds__(NT) void attn_poolL_dq_kernel(const AttnArgs A) {
   constexpr int HALF = HDP / 2;
   constexpr int NDT = HDP / 32;
   __shared__ __attribute__((aligned(16))) float Ks[KC * LS];
-  __shared__ float dpb[KC];
+  __shared__ __attribute__((aligned(16))) float dpb[KC];
 
   const AttnPair& P = A.p[blockIdx.y];
   const int qblocks = (P.Lq + 127) / 128;
@@ -1075,21 +1096,28 @@ __global__ __launch_bounds__(NT) void attn_poolL_dq_kernel(const AttnArgs A) {
   float qf[HALF];
   load_frag<HALF>(qf, P.q + ((int64_t)b * Lq + (qvalid ? q : 0)) * P.ldq + col0, h * HALF, hd, qvalid);
   const float sl2 = scale * LOG2E;
-  const float lse2 = qvalid ? P.lse[rowidx] * LOG2E : -INFINITY;
-  const bool rowlive = qvalid && lse2 != -INFINITY;
+  // invalid query lanes (and fully masked rows) get LSE = +inf: every p = exp2(s - inf) = 0
+  const float lse_q = qvalid ? P.lse[rowidx] : -INFINITY;
+  const float lse2 = lse_q == -INFINITY ? INFINITY : lse_q * LOG2E;
   const float* kbase_ptr = P.k + (int64_t)b * Lk * P.ldk + col0;
 
-  // probabilities (pre-dropout) and keep bits of one 32-key tile
+  // pre-dropout probabilities of one 32-key tile and the lane's keep bits
+  // (shifted so reg r's key is bit (r & 3) + 8 (r >> 2)); per-key validity
+  // tests only on a partial last tile or with a per-key mask
   auto tile = [&](int kbase, int kt, float (&pr)[16], uint32_t& word) {
     const f32x16 s = dot_rows<HALF, BF>(Ks + (kt * 32 + c) * LS + h * HALF, qf, zero16());
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int key = kbase + kt * 32 + acc_row(r, h);
-      const bool valid = rowlive && key < Lk && (P.kmask_mode != 2 || kmask_val(P, b, key) != 0.f);
-      pr[r] = valid ? fast_exp2(s[r] * sl2 - lse2) : 0.f;
+    for (int r = 0; r < 16; ++r) pr[r] = fast_exp2(s[r] * sl2 - lse2);
+    if (kbase + kt * 32 + 32 > Lk || P.kmask_mode == 2) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kbase + kt * 32 + acc_row(r, h);
+        if (!(key < Lk && (P.kmask_mode != 2 || kmask_val(P, b, key) != 0.f))) pr[r] = 0.f;
+      }
     }
-    word = (use_bits && qvalid) ? P.keep_bits[rowidx * kwl + ((kbase >> 5) + kt)] : 0xFFFFFFFFu;
+    word = (use_bits && qvalid) ? P.keep_bits[rowidx * kwl + ((kbase >> 5) + kt)] >> (4 * h) : 0xFFFFFFFFu;
   };
+  auto keep_of = [](uint32_t word, int r) { return ((word >> ((r & 3) + 8 * (r >> 2))) & 1u) != 0u; };
   auto stage = [&](int kbase) {
     __syncthreads();
     load_rows<KC, HDP, LS>(Ks, kbase_ptr, Lk, P.ldk, kbase, hd, vk);
@@ -1108,9 +1136,11 @@ __global__ __launch_bounds__(NT) void attn_poolL_dq_kernel(const AttnArgs A) {
       uint32_t word;
       tile(kbase, kt, pr, word);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int kl = kt * 32 + acc_row(r, h);
-        D += ((word >> (kl & 31)) & 1u) ? pr[r] * dpb[kl] : 0.f;
+      for (int g = 0; g < 4; ++g) {
+        const float4 g4 = *reinterpret_cast<const float4*>(dpb + kt * 32 + 8 * g + 4 * h);
+        const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) D += keep_of(word, 4 * g + j) ? pr[4 * g + j] * gv[j] : 0.f;
       }
     }
   }
@@ -1130,9 +1160,11 @@ __global__ __launch_bounds__(NT) void attn_poolL_dq_kernel(const AttnArgs A) {
       uint32_t word;
       tile(kbase, kt, pr, word);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int kl = kt * 32 + acc_row(r, h);
-        ds[r] = pr[r] * ((((word >> (kl & 31)) & 1u) ? dpb[kl] : 0.f) - D);
+      for (int g = 0; g < 4; ++g) {
+        const float4 g4 = *reinterpret_cast<const float4*>(dpb + kt * 32 + 8 * g + 4 * h);
+        const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ds[4 * g + j] = pr[4 * g + j] * ((keep_of(word, 4 * g + j) ? gv[j] : 0.f) - D);
       }
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt)
