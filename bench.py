@@ -141,7 +141,7 @@ def make_inputs(w, B, seed, device):
     return [f.to(device) for f in feats], mask.to(device), labels.to(device)
 
 
-def cpu_baseline(w, budget_s=15.0, max_steps=20):
+def cpu_baseline(w, budget_s=12.0, max_steps=400):
     """Time the oracle (torch-CPU restatement, oracle/hybrid_cpu.py) on a bounded sample."""
     from oracle.hybrid_cpu import hybrid_train_step
     from fusion import HybridFusion
