@@ -10,6 +10,7 @@
 // weights (a weight row is read with float4 loads by adjacent lanes), keeping
 // every intermediate in LDS.  Nothing mixes samples, so the launch is B
 // independent workgroups.
+#include <cstdlib>
 #include <cstring>
 
 #include "mmf_device.h"
@@ -83,26 +84,92 @@ __device__ __forceinline__ void gemv_nn(const float* x, const float* __restrict_
   }
 }
 
-// y[s][k] = sum_{n in segment s} x[n] * W[n][k] for nseg segments of `seg` rows
-// (the per-head row blocks of value_proj.weight): thread (k = t & 127, group
-// t >> 7) owns whole segments, so no cross-thread reduction is needed.
-__device__ __forceinline__ void gemv_nn_seg(const float* x, const float* __restrict__ W, int nseg, int seg, int K,
-                                            float* y) {
+// Batched forms over S samples of one workgroup: each weight element is loaded
+// once and feeds S accumulators (the per-(pair, sample) tails read the same
+// L2-resident weights for every sample).  Sample s's input starts at
+// xs + s * xsamp, its output at y + s * ysamp.
+template <int S>
+__device__ __forceinline__ void gemv_nt_s(const float* xs, int xsamp, int xdiv, int xstride,
+                                          const float* __restrict__ W, int N, int K, float* y, int ysamp) {
+  const int t = threadIdx.x, half = t & 1;
+  const int kh = K >> 1;
+  for (int n = t >> 1; n < N; n += NT / 2) {
+    const float* x0 = xs + (n / xdiv) * xstride + half * kh;
+    const float* w = W + (int64_t)n * K + half * kh;
+    float acc[S];
+#pragma unroll
+    for (int q = 0; q < S; ++q) acc[q] = 0.f;
+#pragma unroll 4
+    for (int k = 0; k < kh; k += 8) {
+      const float4 a = *reinterpret_cast<const float4*>(w + k);
+      const float4 b = *reinterpret_cast<const float4*>(w + k + 4);
+#pragma unroll
+      for (int q = 0; q < S; ++q) {
+        const float4 xa = *reinterpret_cast<const float4*>(x0 + q * xsamp + k);
+        const float4 xb = *reinterpret_cast<const float4*>(x0 + q * xsamp + k + 4);
+        acc[q] += a.x * xa.x + a.y * xa.y + a.z * xa.z + a.w * xa.w + b.x * xb.x + b.y * xb.y + b.z * xb.z +
+                  b.w * xb.w;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < S; ++q) {
+      const float v = acc[q] + __shfl_xor(acc[q], 1);
+      if (half == 0) y[q * ysamp + n] = v;
+    }
+  }
+}
+
+// y_s[k] = sum_{n < N} x_s[n] W[n][k]; red: S * NT floats
+template <int S>
+__device__ __forceinline__ void gemv_nn_s(const float* x, int xsamp, const float* __restrict__ W, int N, int K,
+                                          float* y, int ysamp, float* red) {
+  const int t = threadIdx.x, rh = t >> 7, kc = t & 127;
+  const int nm = N >> 1;
+  for (int k0 = 0; k0 < K; k0 += 128) {
+    const int k = k0 + kc;
+    float acc[S];
+#pragma unroll
+    for (int q = 0; q < S; ++q) acc[q] = 0.f;
+    if (k < K) {
+      const int a = rh ? nm : 0, e = rh ? N : nm;
+#pragma unroll 4
+      for (int n = a; n < e; ++n) {
+        const float w = W[(int64_t)n * K + k];
+#pragma unroll
+        for (int q = 0; q < S; ++q) acc[q] += x[q * xsamp + n] * w;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < S; ++q) red[q * NT + t] = acc[q];
+    __syncthreads();
+    if (rh == 0 && k < K)
+#pragma unroll
+      for (int q = 0; q < S; ++q) y[q * ysamp + k] = red[q * NT + t] + red[q * NT + t + 128];
+  }
+}
+
+// y_s[g][k] = sum_{n in segment g} x_s[n] W[n][k] (per-head row blocks of value_proj.weight)
+template <int S>
+__device__ __forceinline__ void gemv_nn_seg_s(const float* x, int xsamp, const float* __restrict__ W, int nseg,
+                                              int seg, int K, float* y, int ysamp) {
   const int t = threadIdx.x, sg = t >> 7, kc = t & 127;
   for (int k0 = 0; k0 < K; k0 += 128) {
     const int k = k0 + kc;
     if (k >= K) continue;
     for (int sgi = sg; sgi < nseg; sgi += NT / 128) {
       const int n0 = sgi * seg;
-      float s0 = 0.f, s1 = 0.f;
-      int n = 0;
-#pragma unroll 8
-      for (; n + 1 < seg; n += 2) {
-        s0 += x[n0 + n] * W[(int64_t)(n0 + n) * K + k];
-        s1 += x[n0 + n + 1] * W[(int64_t)(n0 + n + 1) * K + k];
+      float acc[S];
+#pragma unroll
+      for (int q = 0; q < S; ++q) acc[q] = 0.f;
+#pragma unroll 4
+      for (int n = 0; n < seg; ++n) {
+        const float w = W[(int64_t)(n0 + n) * K + k];
+#pragma unroll
+        for (int q = 0; q < S; ++q) acc[q] += x[q * xsamp + n0 + n] * w;
       }
-      if (n < seg) s0 += x[n0 + n] * W[(int64_t)(n0 + n) * K + k];
-      y[sgi * K + k] = s0 + s1;
+#pragma unroll
+      for (int q = 0; q < S; ++q) y[q * ysamp + sgi * K + k] = acc[q];
     }
   }
 }
@@ -137,130 +204,164 @@ __device__ float adaptive_w(int M, const float* score, const float* mask, float*
 // ---------------------------------------------------------------- per (pair, sample)
 // Forward: U_h = pbar_h P_k (+ r_h = sum pbar_h), Obar = U W_v^T (per head) + r b_v,
 // Abar = Obar W_o^T + b_o.  grid (B, npairs).
+template <int S>
 __global__ __launch_bounds__(NT) void tail_pair_fwd_kernel(const TailArgs a) {
+  constexpr int TH = TAIL_MAX_H;
   __shared__ float pb_s[MAXHEADS * 128];
-  __shared__ __attribute__((aligned(16))) float u_s[MAXHEADS * TAIL_MAX_H];
+  __shared__ __attribute__((aligned(16))) float u_s[S * MAXHEADS * TH];
   __shared__ __attribute__((aligned(16))) float4 red4[NT];
-  __shared__ __attribute__((aligned(16))) float v1[TAIL_MAX_H], v2[TAIL_MAX_H];
-  __shared__ float r_s[MAXHEADS];
-  const int b = blockIdx.x;
+  __shared__ __attribute__((aligned(16))) float v1[S * TH], v2[S * TH];
+  __shared__ float r_s[S * MAXHEADS];
+  const int b0 = blockIdx.x * S, ns = min(S, a.B - b0);
   const TailPair& P = a.p[blockIdx.y];
   const int t = threadIdx.x;
   const int H = a.H, nh = a.heads, hd = a.hd, Lk = P.Lk, H4 = H >> 2;
-  for (int i = t; i < nh * Lk; i += NT) pb_s[i] = P.pbar[(int64_t)b * nh * Lk + i];
-  __syncthreads();
-  if (t < nh) {
-    float s = 0.f;
-    for (int j = 0; j < Lk; ++j) s += pb_s[t * Lk + j];
-    r_s[t] = s;
-    P.r[(int64_t)b * nh + t] = s;
-  }
-  // U: tasks = (head, float4 column); RG row groups split the Lk keys
-  const float* pk = P.Pk + (int64_t)b * Lk * H;
   const int ncol = nh * H4;
-  for (int task0 = 0; task0 < ncol; task0 += NT) {
-    const int nact = min(NT, ncol - task0);
-    const int RG = NT / nact;
-    const int task = task0 + t % nact, rg = t / nact;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f), acc2 = acc;
-    if (rg < RG) {
-      const int hh = task / H4, c4 = task % H4;
-      int j = rg;
+  for (int si = 0; si < S; ++si) {
+    float* us = u_s + si * nh * H;
+    if (si >= ns) {   // no sample: zero inputs keep the batched GEMVs finite
+      for (int i = t; i < nh * H; i += NT) us[i] = 0.f;
+      if (t < nh) r_s[si * MAXHEADS + t] = 0.f;
+      continue;
+    }
+    const int b = b0 + si;
+    __syncthreads();   // pb_s of the previous sample consumed
+    for (int i = t; i < nh * Lk; i += NT) pb_s[i] = P.pbar[(int64_t)b * nh * Lk + i];
+    __syncthreads();
+    if (t < nh) {
+      float s = 0.f;
+      for (int j = 0; j < Lk; ++j) s += pb_s[t * Lk + j];
+      r_s[si * MAXHEADS + t] = s;
+      P.r[(int64_t)b * nh + t] = s;
+    }
+    // U: tasks = (head, float4 column); RG row groups split the Lk keys
+    const float* pk = P.Pk + (int64_t)b * Lk * H;
+    for (int task0 = 0; task0 < ncol; task0 += NT) {
+      const int nact = min(NT, ncol - task0);
+      const int RG = NT / nact;
+      const int task = task0 + t % nact, rg = t / nact;
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f), acc2 = acc;
+      if (rg < RG) {
+        const int hh = task / H4, c4 = task % H4;
+        int j = rg;
 #pragma unroll 4
-      for (; j + RG < Lk; j += 2 * RG) {
-        const float4 v = *reinterpret_cast<const float4*>(pk + (int64_t)j * H + 4 * c4);
-        const float4 u = *reinterpret_cast<const float4*>(pk + (int64_t)(j + RG) * H + 4 * c4);
-        const float w = pb_s[hh * Lk + j], w2 = pb_s[hh * Lk + j + RG];
-        acc.x += w * v.x; acc.y += w * v.y; acc.z += w * v.z; acc.w += w * v.w;
-        acc2.x += w2 * u.x; acc2.y += w2 * u.y; acc2.z += w2 * u.z; acc2.w += w2 * u.w;
+        for (; j + RG < Lk; j += 2 * RG) {
+          const float4 v = *reinterpret_cast<const float4*>(pk + (int64_t)j * H + 4 * c4);
+          const float4 u = *reinterpret_cast<const float4*>(pk + (int64_t)(j + RG) * H + 4 * c4);
+          const float w = pb_s[hh * Lk + j], w2 = pb_s[hh * Lk + j + RG];
+          acc.x += w * v.x; acc.y += w * v.y; acc.z += w * v.z; acc.w += w * v.w;
+          acc2.x += w2 * u.x; acc2.y += w2 * u.y; acc2.z += w2 * u.z; acc2.w += w2 * u.w;
+        }
+        if (j < Lk) {
+          const float4 v = *reinterpret_cast<const float4*>(pk + (int64_t)j * H + 4 * c4);
+          const float w = pb_s[hh * Lk + j];
+          acc.x += w * v.x; acc.y += w * v.y; acc.z += w * v.z; acc.w += w * v.w;
+        }
       }
-      if (j < Lk) {
-        const float4 v = *reinterpret_cast<const float4*>(pk + (int64_t)j * H + 4 * c4);
-        const float w = pb_s[hh * Lk + j];
-        acc.x += w * v.x; acc.y += w * v.y; acc.z += w * v.z; acc.w += w * v.w;
+      __syncthreads();
+      red4[t] = make_float4(acc.x + acc2.x, acc.y + acc2.y, acc.z + acc2.z, acc.w + acc2.w);
+      __syncthreads();
+      if (t < nact) {
+        float4 sum = red4[t];
+        for (int g = 1; g < RG; ++g) {
+          const float4 v = red4[g * nact + t];
+          sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
+        }
+        const int tt = task0 + t;
+        *reinterpret_cast<float4*>(&us[4 * tt]) = sum;
+        *reinterpret_cast<float4*>(P.U + (int64_t)b * nh * H + 4 * tt) = sum;
       }
-    }
-    __syncthreads();
-    red4[t] = make_float4(acc.x + acc2.x, acc.y + acc2.y, acc.z + acc2.z, acc.w + acc2.w);
-    __syncthreads();
-    if (t < nact) {
-      float4 sum = red4[t];
-      for (int g = 1; g < RG; ++g) {
-        const float4 v = red4[g * nact + t];
-        sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
-      }
-      const int tt = task0 + t;
-      *reinterpret_cast<float4*>(&u_s[4 * tt]) = sum;
-      *reinterpret_cast<float4*>(P.U + (int64_t)b * nh * H + 4 * tt) = sum;
     }
   }
   __syncthreads();
-  gemv_nt(u_s, hd, H, P.Wv, H, H, v1);
+  // Obar = U W_v^T (per head) + r b_v;  Abar = Obar W_o^T + b_o
+  gemv_nt_s<S>(u_s, nh * H, hd, H, P.Wv, H, H, v1, TH);
   __syncthreads();
-  for (int n = t; n < H; n += NT) {
-    const float o = v1[n] + r_s[n / hd] * P.bv[n];
-    v1[n] = o;
-    P.Ob[(int64_t)b * H + n] = o;
+  for (int i = t; i < S * H; i += NT) {
+    const int si = i / H, n = i - si * H;
+    const float o = v1[si * TH + n] + r_s[si * MAXHEADS + n / hd] * P.bv[n];
+    v1[si * TH + n] = o;
+    if (si < ns) P.Ob[(int64_t)(b0 + si) * H + n] = o;
   }
   __syncthreads();
-  gemv_nt(v1, 1 << 30, 0, P.Wo, H, H, v2);
+  gemv_nt_s<S>(v1, TH, 1 << 30, 0, P.Wo, H, H, v2, TH);
   __syncthreads();
-  for (int n = t; n < H; n += NT) P.Ab[(int64_t)b * H + n] = v2[n] + P.bo[n];
+  for (int i = t; i < ns * H; i += NT) {
+    const int si = i / H, n = i - si * H;
+    P.Ab[(int64_t)(b0 + si) * H + n] = v2[si * TH + n] + P.bo[n];
+  }
 }
 
 // Backward: dObar = cvec_q W_o; dU_h = dObar_h W_v[h rows];
 // dpbar_h[j] = P_k[j] . dU_h + dObar_h . b_v,h.  grid (B, npairs).
+template <int S>
 __global__ __launch_bounds__(NT) void tail_pair_bwd_kernel(const TailArgs a) {
-  __shared__ __attribute__((aligned(16))) float c_s[TAIL_MAX_H], v1[TAIL_MAX_H];
-  __shared__ __attribute__((aligned(16))) float du_s[MAXHEADS * TAIL_MAX_H];
-  __shared__ float red[NT];
-  __shared__ float dr_s[MAXHEADS];
-  const int b = blockIdx.x;
+  constexpr int TH = TAIL_MAX_H;
+  __shared__ __attribute__((aligned(16))) float c_s[S * TH], v1[S * TH];
+  __shared__ __attribute__((aligned(16))) float du_s[S * MAXHEADS * TH];
+  __shared__ float red[S * NT];
+  __shared__ float dr_s[S * MAXHEADS];
+  const int b0 = blockIdx.x * S, ns = min(S, a.B - b0);
   const TailPair& P = a.p[blockIdx.y];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int H = a.H, nh = a.heads, hd = a.hd, Lk = P.Lk, M = a.M;
-  for (int i = t; i < H; i += NT) c_s[i] = a.cvec[((int64_t)b * M + P.q) * H + i];
-  __syncthreads();
-  gemv_nn(c_s, P.Wo, 0, H, H, v1, red);
-  __syncthreads();
-  for (int n = t; n < H; n += NT) P.dOb[(int64_t)b * H + n] = v1[n];
-  gemv_nn_seg(v1, P.Wv, nh, hd, H, du_s);
-  for (int hh = wave; hh < nh; hh += NT / 64) {
-    float s = 0.f;
-    for (int d = lane; d < hd; d += 64) s += v1[hh * hd + d] * P.bv[hh * hd + d];
-    s = wsum(s);
-    if (lane == 0) dr_s[hh] = s;
+  constexpr int DUS = MAXHEADS * TH;   // du_s stride per sample
+  for (int i = t; i < S * H; i += NT) {
+    const int si = i / H, n = i - si * H;
+    c_s[si * TH + n] = si < ns ? a.cvec[((int64_t)(b0 + si) * M + P.q) * H + n] : 0.f;
   }
   __syncthreads();
-  for (int i = t; i < nh * H; i += NT) P.dU[(int64_t)b * nh * H + i] = du_s[i];
+  gemv_nn_s<S>(c_s, TH, P.Wo, H, H, v1, TH, red);
+  __syncthreads();
+  for (int i = t; i < ns * H; i += NT) {
+    const int si = i / H, n = i - si * H;
+    P.dOb[(int64_t)(b0 + si) * H + n] = v1[si * TH + n];
+  }
+  gemv_nn_seg_s<S>(v1, TH, P.Wv, nh, hd, H, du_s, DUS);
+  for (int sh = wave; sh < S * nh; sh += NT / 64) {
+    const int si = sh / nh, hh = sh - si * nh;
+    float s = 0.f;
+    for (int d = lane; d < hd; d += 64) s += v1[si * TH + hh * hd + d] * P.bv[hh * hd + d];
+    s = wsum(s);
+    if (lane == 0) dr_s[si * MAXHEADS + hh] = s;
+  }
+  __syncthreads();
+  for (int i = t; i < ns * nh * H; i += NT) {
+    const int si = i / (nh * H), r = i - si * nh * H;
+    P.dU[(int64_t)(b0 + si) * nh * H + r] = du_s[si * DUS + r];
+  }
   // dpbar: a wave takes two keys per step (lane halves), lanes stride the H/4 float4 columns
-  const float* pk = P.Pk + (int64_t)b * Lk * H;
   const int half = lane >> 5, l32 = lane & 31;
+  for (int si = 0; si < ns; ++si) {
+    const int b = b0 + si;
+    const float* pk = P.Pk + (int64_t)b * Lk * H;
+    const float* du = du_s + si * DUS;
 #pragma unroll 2
-  for (int j0 = 2 * wave; j0 < Lk; j0 += 2 * (NT / 64)) {
-    const int j = j0 + half;
-    float acc[MAXHEADS];
+    for (int j0 = 2 * wave; j0 < Lk; j0 += 2 * (NT / 64)) {
+      const int j = j0 + half;
+      float acc[MAXHEADS];
 #pragma unroll
-    for (int hh = 0; hh < MAXHEADS; ++hh) acc[hh] = 0.f;
-    if (j < Lk) {
-      for (int c4 = l32; c4 < H / 4; c4 += 32) {
-        const float4 v = *reinterpret_cast<const float4*>(pk + (int64_t)j * H + 4 * c4);
+      for (int hh = 0; hh < MAXHEADS; ++hh) acc[hh] = 0.f;
+      if (j < Lk) {
+        for (int c4 = l32; c4 < H / 4; c4 += 32) {
+          const float4 v = *reinterpret_cast<const float4*>(pk + (int64_t)j * H + 4 * c4);
 #pragma unroll
-        for (int hh = 0; hh < MAXHEADS; ++hh) {
-          if (hh < nh) {
-            const float4 u = *reinterpret_cast<const float4*>(&du_s[hh * H + 4 * c4]);
-            acc[hh] += v.x * u.x + v.y * u.y + v.z * u.z + v.w * u.w;
+          for (int hh = 0; hh < MAXHEADS; ++hh) {
+            if (hh < nh) {
+              const float4 u = *reinterpret_cast<const float4*>(&du[hh * H + 4 * c4]);
+              acc[hh] += v.x * u.x + v.y * u.y + v.z * u.z + v.w * u.w;
+            }
           }
         }
       }
-    }
 #pragma unroll
-    for (int hh = 0; hh < MAXHEADS; ++hh) {
-      if (hh < nh) {
-        float sv = acc[hh];
+      for (int hh = 0; hh < MAXHEADS; ++hh) {
+        if (hh < nh) {
+          float sv = acc[hh];
 #pragma unroll
-        for (int o = 16; o >= 1; o >>= 1) sv += __shfl_xor(sv, o);
-        if (l32 == 0 && j < Lk) P.dpbar[((int64_t)b * nh + hh) * Lk + j] = sv + dr_s[hh];
+          for (int o = 16; o >= 1; o >>= 1) sv += __shfl_xor(sv, o);
+          if (l32 == 0 && j < Lk) P.dpbar[((int64_t)b * nh + hh) * Lk + j] = sv + dr_s[si * MAXHEADS + hh];
+        }
       }
     }
   }
@@ -442,6 +543,21 @@ __global__ __launch_bounds__(NT) void tail_head_bwd_kernel(const TailArgs a) {
 
 }  // namespace
 
+// Samples per workgroup of the per-(pair, sample) kernels (MMF_TAIL_S = 2 or 4
+// overrides, for tuning).  Measured at C2 (B = 256, 6 pairs): S = 1 / 2 / 4 ->
+// pair bwd 52.7 / 70.3 / 120.1 us, pair fwd 45.6 / 50.7 / 76.2 us.  The chains
+// are latency-bound, so the weight reuse of S > 1 loses to the parallelism it
+// removes; S = 1 it is.
+int tail_samples() {
+  static int s = 0;
+  if (s == 0) {
+    const char* e = getenv("MMF_TAIL_S");
+    s = e ? atoi(e) : 1;
+    if (s != 1 && s != 2 && s != 4) s = 1;
+  }
+  return s;
+}
+
 bool tail_supported(int M, int H, int C, int heads, int hd, int npairs) {
   return M <= MAXM && heads <= MAXHEADS && H % 16 == 0 && H <= TAIL_MAX_H && C <= 256 &&
          npairs <= TAIL_MAX_PAIRS && hd % 8 == 0 && (NT % (H / 4)) == 0;
@@ -456,7 +572,10 @@ hipError_t launch_tail_fwd(const TailArgs& a, hipStream_t st) {
     // per pair: Vbar = U W_v^T (+ r b_v), Obar = Vbar W_o^T + b_o; weights read once
     ProfLaunch prof_(st, "tail_pair_fwd_kernel", 4.0 * B * H * H * a.npairs,
                      4.0 * a.npairs * (2 * H * H + B * (a.heads * H + 2 * H)));
-    hipLaunchKernelGGL(tail_pair_fwd_kernel, dim3(a.B, a.npairs), dim3(NT), 0, st, a);
+    const int S = tail_samples();
+    if (S == 4) hipLaunchKernelGGL(tail_pair_fwd_kernel<4>, dim3((a.B + 3) / 4, a.npairs), dim3(NT), 0, st, a);
+    else if (S == 2) hipLaunchKernelGGL(tail_pair_fwd_kernel<2>, dim3((a.B + 1) / 2, a.npairs), dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL(tail_pair_fwd_kernel<1>, dim3(a.B, a.npairs), dim3(NT), 0, st, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
@@ -480,7 +599,10 @@ hipError_t launch_tail_bwd(const TailArgs& a, hipStream_t st) {
   {
     ProfLaunch prof_(st, "tail_pair_bwd_kernel", 4.0 * B * H * H * a.npairs,
                      4.0 * a.npairs * (2 * H * H + B * (a.heads * H + 2 * H)));
-    hipLaunchKernelGGL(tail_pair_bwd_kernel, dim3(a.B, a.npairs), dim3(NT), 0, st, a);
+    const int S = tail_samples();
+    if (S == 4) hipLaunchKernelGGL(tail_pair_bwd_kernel<4>, dim3((a.B + 3) / 4, a.npairs), dim3(NT), 0, st, a);
+    else if (S == 2) hipLaunchKernelGGL(tail_pair_bwd_kernel<2>, dim3((a.B + 1) / 2, a.npairs), dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL(tail_pair_bwd_kernel<1>, dim3(a.B, a.npairs), dim3(NT), 0, st, a);
   }
   return hipGetLastError();
 }
