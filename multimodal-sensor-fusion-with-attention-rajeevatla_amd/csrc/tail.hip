@@ -29,65 +29,12 @@ __device__ __forceinline__ float wsum(float v) {
   return v;
 }
 
-// y[n] = sum_k x(n)[k] * W[n][k] for n < N; x(n) = xs + (n / xdiv) * xstride
+// GEMVs against L2-resident weights, over S samples of one workgroup: each
+// weight element is loaded once and feeds S accumulators.  Sample s's input
+// starts at xs + s * xsamp, its output at y + s * ysamp.
+// gemv_nt_s: y[n] = sum_k x(n)[k] * W[n][k] for n < N; x(n) = xs + (n / xdiv) * xstride
 // (a per-head input when xdiv = head_dim).  Two adjacent lanes share an output
-// (k halves, K % 16 == 0) and keep all their float4 loads of the W row in
-// flight at once: these chains are latency-bound, so memory-level
-// parallelism per lane beats wider coalescing (measured: 8 lanes per row
-// with 4 passes was 1.5x slower).
-__device__ __forceinline__ void gemv_nt(const float* xs, int xdiv, int xstride, const float* __restrict__ W,
-                                        int N, int K, float* y) {
-  const int t = threadIdx.x, half = t & 1;
-  const int kh = K >> 1;
-  for (int n = t >> 1; n < N; n += NT / 2) {
-    const float* x = xs + (n / xdiv) * xstride + half * kh;
-    const float* w = W + (int64_t)n * K + half * kh;
-    float s0 = 0.f, s1 = 0.f;
-#pragma unroll 8
-    for (int k = 0; k < kh; k += 8) {
-      const float4 a = *reinterpret_cast<const float4*>(w + k);
-      const float4 b = *reinterpret_cast<const float4*>(w + k + 4);
-      s0 += a.x * x[k] + a.y * x[k + 1] + a.z * x[k + 2] + a.w * x[k + 3];
-      s1 += b.x * x[k + 4] + b.y * x[k + 5] + b.z * x[k + 6] + b.w * x[k + 7];
-    }
-    float s = s0 + s1;
-    s += __shfl_xor(s, 1);
-    if (half == 0) y[n] = s;
-  }
-}
-
-// y[k] = sum_{n in [n0, n1)} x[n] * W[n][k] for k < K (W row-major, ld = K):
-// threads split as 128 columns x 2 row halves, combined through `red` (NT floats).
-__device__ __forceinline__ void gemv_nn(const float* x, const float* __restrict__ W, int n0, int n1, int K,
-                                        float* y, float* red) {
-  const int t = threadIdx.x, rh = t >> 7, kc = t & 127;
-  const int nm = n0 + ((n1 - n0) >> 1);
-  for (int k0 = 0; k0 < K; k0 += 128) {
-    const int k = k0 + kc;
-    float s = 0.f;
-    if (k < K) {
-      const int a = rh ? nm : n0, e = rh ? n1 : nm;
-      float s1 = 0.f;
-      int n = a;
-#pragma unroll 8
-      for (; n + 1 < e; n += 2) {
-        s += x[n] * W[(int64_t)n * K + k];
-        s1 += x[n + 1] * W[(int64_t)(n + 1) * K + k];
-      }
-      if (n < e) s += x[n] * W[(int64_t)n * K + k];
-      s += s1;
-    }
-    __syncthreads();
-    red[t] = s;
-    __syncthreads();
-    if (rh == 0 && k < K) y[k] = red[t] + red[t + 128];
-  }
-}
-
-// Batched forms over S samples of one workgroup: each weight element is loaded
-// once and feeds S accumulators (the per-(pair, sample) tails read the same
-// L2-resident weights for every sample).  Sample s's input starts at
-// xs + s * xsamp, its output at y + s * ysamp.
+// (k halves, K % 16 == 0), their float4 loads of the W row all in flight.
 template <int S>
 __device__ __forceinline__ void gemv_nt_s(const float* xs, int xsamp, int xdiv, int xstride,
                                           const float* __restrict__ W, int N, int K, float* y, int ysamp) {
@@ -453,7 +400,7 @@ __global__ __launch_bounds__(NT) void tail_head_fwd_kernel(const TailArgs a) {
     a.fused[(int64_t)b * H + j] = f;
   }
   __syncthreads();
-  gemv_nt(v1, 1 << 30, 0, a.W1, H, H, v2);
+  gemv_nt_s<1>(v1, 0, 1 << 30, 0, a.W1, H, H, v2, 0);
   __syncthreads();
   const float p = a.drop_p;
   const bool drop = p > 0.f && a.rng != nullptr;
@@ -490,7 +437,7 @@ __global__ __launch_bounds__(NT) void tail_head_bwd_kernel(const TailArgs a) {
   for (int i = t; i < M * H; i += NT) pooled_s[i] = a.pooled[(int64_t)b * M * H + i];
   __syncthreads();
   // the saved h1 is post-dropout, so h1 > 0 marks kept, active units (gscale = 1/(1-p))
-  gemv_nn(dl_s, a.W2, 0, C, H, v1, red);
+  gemv_nn_s<1>(dl_s, 0, a.W2, C, H, v1, 0, red);
   __syncthreads();
   for (int n = t; n < H; n += NT) {
     const float z = a.h1[(int64_t)b * H + n] > 0.f ? v1[n] * a.gscale : 0.f;
@@ -498,7 +445,7 @@ __global__ __launch_bounds__(NT) void tail_head_bwd_kernel(const TailArgs a) {
     a.dz1[(int64_t)b * H + n] = z;
   }
   __syncthreads();
-  gemv_nn(v1, a.W1, 0, H, H, v2, red);
+  gemv_nn_s<1>(v1, 0, a.W1, H, H, v2, 0, red);
   __syncthreads();
   // head backward (head.hip head_bwd_kernel): dw_m = dfused . pooled_m
   for (int m = wave; m < M; m += NT / 64) {
