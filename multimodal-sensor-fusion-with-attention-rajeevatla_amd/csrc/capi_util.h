@@ -155,7 +155,6 @@ inline size_t slab_bytes(int M, int N, int rows) {
 struct WgradPlan {
   std::vector<GemmJob> jobs;
   std::vector<ReduceJob> reds;
-  size_t n_early = 0;   // jobs[0, n_early) do not read dZ: they may run beside the dZ / dX GEMMs
 };
 
 // has_db: the layer has a bias whose gradient (row sums) is produced too.  It is

@@ -194,39 +194,10 @@ void plan_wgrads(const mmf_hybrid_desc* d, const float* const* x, const float* m
     plan_wgrad(wp, bw, H, H, B * lq, opnd(w.dQ[p], H), opnd(s.P[q], H), g->q[p].w, g->q[p].b);
     plan_wgrad(wp, bw, H, H, B * lk, opnd(w.dK[p], H), opnd(s.P[k], H), g->k[p].w, g->k[p].b);
   }
-  wp.n_early = wp.jobs.size();
   for (int m = 0; m < M; ++m) {
     const int L = Lm(d, m), D = d->in_dim[m];
     plan_wgrad(wp, bw, H, D, B * L, opnd(w.dZ[m], H), opnd(s.Xd[m], D), g->proj[m].w, g->proj[m].b);
   }
-}
-
-// Side stream of the current device for the weight gradients that do not need
-// dZ (classifier, gating, value / out / query / key projections): forked from
-// the caller's stream after the attention backward and joined before the
-// split-K reduce, so they overlap the dZ and dX GEMMs (in a captured graph:
-// parallel branches).  Created on the first eager call; a call that is being
-// captured before that runs serially.
-struct SideStream {
-  hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-};
-SideStream* side_stream(hipStream_t st) {
-  static SideStream per_dev[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  SideStream& ss = per_dev[dev];
-  if (!ss.s) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-    if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess) { ss.s = nullptr; return nullptr; }
-    if (hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess) {
-      (void)hipGetLastError();
-      return nullptr;
-    }
-  }
-  return ss.join ? &ss : nullptr;
 }
 
 size_t saved_bytes(const mmf_hybrid_desc* d) {
@@ -656,25 +627,6 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
     STAGE_TRY("bwd.attn_dq", launch_attn_bwd_stage(2, pairs.data(), d->num_pairs, B, nh, hd, scale, p, rng, st));
   }
   // (4) dZ_m = gate(P_m) * [direct + sum_q dQ W_q + sum_k dK W_k (+ dV W_v)]
-  // (3.5) weight gradients that do not read dZ, on the side stream beside (4) and (5)
-  auto by_size = [](const GemmJob& a, const GemmJob& b) {
-    const int64_t wa = (int64_t)a.g.nsplit * std::max(1, a.g.nbatch) * a.g.M * a.g.N;
-    const int64_t wb = (int64_t)b.g.nsplit * std::max(1, b.g.nbatch) * b.g.M * b.g.N;
-    return wa > wb;
-  };
-  // biggest jobs first in each launch so every launch (<= 12 jobs) is a full grid
-  std::stable_sort(wp.jobs.begin(), wp.jobs.begin() + wp.n_early, by_size);
-  std::stable_sort(wp.jobs.begin() + wp.n_early, wp.jobs.end(), by_size);
-  SideStream* side = getenv("MMF_NO_FORK") ? nullptr : side_stream(st);
-  if (side && wp.n_early > 0) {
-    HIP_TRY(hipEventRecord(side->fork, st));
-    HIP_TRY(hipStreamWaitEvent(side->s, side->fork, 0));
-    {
-      Stage stage_("bwd.wgrad_gemm_early", side->s);
-      HIP_TRY(launch_gemm(wp.jobs.data(), (int)wp.n_early, MODE_KR, MODE_KR, p, rng, side->s));
-    }
-    HIP_TRY(hipEventRecord(side->join, side->s));
-  }
   {
     std::vector<GemmJob> jobs;
     for (int m = 0; m < M; ++m) {
@@ -731,12 +683,14 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
     if (!jobs.empty())
       STAGE_TRY("bwd.dx_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, p, rng, st));
   }
-  // (6) the remaining weight gradients (split-K slabs), join, then one deterministic reduce
-  const size_t first = (side && wp.n_early > 0) ? wp.n_early : 0;
-  if (first < wp.jobs.size())
-    STAGE_TRY("bwd.wgrad_gemm", launch_gemm(wp.jobs.data() + first, (int)(wp.jobs.size() - first), MODE_KR,
-                                            MODE_KR, p, rng, st));
-  if (side && wp.n_early > 0) HIP_TRY(hipStreamWaitEvent(st, side->join, 0));
+  // (6) every weight gradient: split-K slabs, then one deterministic reduce
+  // biggest jobs first so every launch (<= 8 jobs) is a full grid
+  std::stable_sort(wp.jobs.begin(), wp.jobs.end(), [](const GemmJob& a, const GemmJob& b) {
+    const int64_t wa = (int64_t)a.g.nsplit * std::max(1, a.g.nbatch) * a.g.M * a.g.N;
+    const int64_t wb = (int64_t)b.g.nsplit * std::max(1, b.g.nbatch) * b.g.M * b.g.N;
+    return wa > wb;
+  });
+  STAGE_TRY("bwd.wgrad_gemm", launch_gemm(wp.jobs.data(), (int)wp.jobs.size(), MODE_KR, MODE_KR, p, rng, st));
   STAGE_TRY("bwd.wgrad_reduce", launch_reduce(wp.reds.data(), (int)wp.reds.size(), st));
   return MMF_OK;
 }
