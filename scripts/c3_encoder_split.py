@@ -60,7 +60,10 @@ def main():
     ap.add_argument("--batches", default="1,32")
     ap.add_argument("--chunk", type=int, default=1024)
     ap.add_argument("--encoders", default="miopen,hip")
+    ap.add_argument("--precision", default="highest", choices=["highest", "medium"],
+                    help="torch.set_float32_matmul_precision (config/base.yaml:80 sets 'medium')")
     args = ap.parse_args()
+    torch.set_float32_matmul_precision(args.precision)
     from fusion import HybridFusion
     import encoders as hip_encoders
 
@@ -116,7 +119,9 @@ def main():
                 "fusion_fwd_bwd_samples_per_s": round(B / ((fus_f + fus_b) * 1e-3), 1),
             })
     print(json.dumps({"config": "c3: PAMAP2 3-IMU+HR, SequenceEncoder(LSTM 1x256 -> 128)+LayerNorm, "
-                                "HybridFusion(H=256, C=25, 4 heads), fp32, synthetic chunks",
+                                "HybridFusion(H=256, C=25, 4 heads), synthetic chunks, matmul precision "
+                                + args.precision + (" (fp32)" if args.precision == "highest" else
+                                                    " (bf16 MFMA operands in the fusion, fp32 LSTM recurrence)"),
                       "encoders": {"miopen": "torch nn.LSTM on ROCm (MIOpen)",
                                    "hip": "SequenceEncoder on the persistent HIP LSTM (csrc/lstm.hip)"},
                       "fusion": "mmfusion HIP",
