@@ -896,7 +896,7 @@ MMF_CHAIN16(dk[dt], ds[r], Qs[(qt * 32 + acc_row(r, h)) * LS + dt * 32 + c])
 // ---------------------------------------------------------------------------
 template <int HDP, bool BF>
 __global__ __launch_bounds__(NT) void attn_poolL_lse_kernel(const AttnArgs A) {
-  constexpr int KC = HDP == 32 ? 128 : 64;
+  constexpr int KC = 128;   // keys per LDS chunk (34 KB at HDP = 64: 4 workgroups / CU)
   constexpr int LS = HDP + 4;
   constexpr int HALF = HDP / 2;
   __shared__ __attribute__((aligned(16))) float Ks[KC * LS];
@@ -1057,7 +1057,7 @@ __global__ __launch_bounds__(NT) void attn_poolL_colsum_kernel(const AttnArgs A)
 
 template <int HDP, bool BF>
 __global__ __launch_bounds__(NT) void attn_poolL_dq_kernel(const AttnArgs A) {
-  constexpr int KC = HDP == 32 ? 128 : 64;
+  constexpr int KC = 128;   // keys per LDS chunk (34 KB at HDP = 64: 4 workgroups / CU)
   constexpr int LS = HDP + 4;
   constexpr int HALF = HDP / 2;
   constexpr int NDT = HDP / 32;
