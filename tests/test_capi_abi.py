@@ -45,9 +45,11 @@ def test_struct_layouts_match_header(nat, tmp_path):
 #include <stddef.h>
 #include "{HEADER}"
 int main(void) {{
-  printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(mmf_hybrid_desc), sizeof(mmf_hybrid_params),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %d\\n", sizeof(mmf_hybrid_desc), sizeof(mmf_hybrid_params),
          sizeof(mmf_hybrid_grads), sizeof(mmf_cma_desc), sizeof(mmf_cma_params),
-         offsetof(mmf_hybrid_desc, dropout), offsetof(mmf_hybrid_params, cls2));
+         offsetof(mmf_hybrid_desc, dropout), offsetof(mmf_hybrid_params, cls2),
+         offsetof(mmf_hybrid_desc, matmul_precision), offsetof(mmf_cma_desc, matmul_precision),
+         (int)MMF_PRECISION_MEDIUM);
   return 0;
 }}
 """)
@@ -57,7 +59,8 @@ int main(void) {{
                                           check=True).stdout.split()]
     py = [ctypes.sizeof(nat.HybridDesc), ctypes.sizeof(nat.HybridParams),
           ctypes.sizeof(nat.HybridGrads), ctypes.sizeof(nat.CmaDesc), ctypes.sizeof(nat.CmaParams),
-          nat.HybridDesc.dropout.offset, nat.HybridParams.cls2.offset]
+          nat.HybridDesc.dropout.offset, nat.HybridParams.cls2.offset,
+          nat.HybridDesc.matmul_precision.offset, nat.CmaDesc.matmul_precision.offset, nat.PRECISION_MEDIUM]
     assert out == py
 
 
@@ -91,7 +94,15 @@ def test_size_queries_and_validation(nat):
     # forward refuses a bad descriptor before touching the device
     rc = L.mmf_hybrid_forward(ctypes.byref(bad), None, None, None, None, None, None, None, None, None)
     assert rc != 0
+    odd = _desc(nat, matmul_precision=7)     # neither HIGHEST nor MEDIUM
+    assert L.mmf_hybrid_saved_bytes(ctypes.byref(odd)) == 0
+    assert b"matmul_precision" in L.mmf_last_error()
+    assert L.mmf_hybrid_saved_bytes(ctypes.byref(_desc(nat, matmul_precision=nat.PRECISION_MEDIUM))) > 0
     c = nat.CmaDesc(2, 5, 7, 8, 8, 16, 4, 2, 0.0, 0)
+    assert L.mmf_cma_saved_bytes(ctypes.byref(c)) > 0
+    c.matmul_precision = 3
+    assert L.mmf_cma_saved_bytes(ctypes.byref(c)) == 0
+    c.matmul_precision = nat.PRECISION_MEDIUM
     assert L.mmf_cma_saved_bytes(ctypes.byref(c)) > 0
     c.mask_mode = 5
     assert L.mmf_cma_saved_bytes(ctypes.byref(c)) == 0
@@ -106,3 +117,17 @@ def test_workspace_scales_with_sequence(nat):
         d2.seq_len[m] = 128
     assert L.mmf_hybrid_saved_bytes(ctypes.byref(d2)) > 10 * L.mmf_hybrid_saved_bytes(ctypes.byref(d1))
     assert L.mmf_hybrid_workspace_bytes(ctypes.byref(d2)) > 5 * L.mmf_hybrid_workspace_bytes(ctypes.byref(d1))
+
+
+def test_matmul_precision_follows_torch(nat):
+    """The modules read torch.get_float32_matmul_precision() (src/train.py:53-68
+    applies config/base.yaml:80 training.matmul_precision through it)."""
+    import torch
+    prev = torch.get_float32_matmul_precision()
+    try:
+        for mode, want in (("highest", nat.PRECISION_HIGHEST), ("high", nat.PRECISION_HIGHEST),
+                           ("medium", nat.PRECISION_MEDIUM)):
+            torch.set_float32_matmul_precision(mode)
+            assert nat.matmul_precision() == want, mode
+    finally:
+        torch.set_float32_matmul_precision(prev)
