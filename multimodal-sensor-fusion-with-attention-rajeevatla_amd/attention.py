@@ -150,6 +150,7 @@ class CrossModalAttention(nn.Module):
         cast_self.scale = head_dim ** -0.5
         self.register_buffer("_rng_state", _new_rng_state(), persistent=False)
 
+    @torch.compiler.disable  # HIP library calls: opaque to TorchDynamo (runs eagerly)
     def forward(self, query: torch.Tensor, key: torch.Tensor, value: torch.Tensor,
                 mask: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
         """src/attention.py:68-146: (B,Dq)/(B,Lq,Dq) x (B,Dk)/(B,Lk,Dk) -> (attended, weights)."""
@@ -213,6 +214,7 @@ class TemporalAttention(CrossModalAttention):
         super().__init__(feature_dim, feature_dim, hidden_dim=hidden_dim, num_heads=num_heads, dropout=dropout)
         cast(Any, self).feature_dim = feature_dim
 
+    @torch.compiler.disable  # HIP library calls: opaque to TorchDynamo (runs eagerly)
     def forward(self, sequence: torch.Tensor,  # type: ignore[override]
                 mask: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
         if sequence.dim() != 3:
@@ -269,6 +271,7 @@ class PairwiseModalityAttention(nn.Module):
                                                dropout=dropout)
             for q in dims for k in dims if q != k})
 
+    @torch.compiler.disable  # HIP library calls: opaque to TorchDynamo (runs eagerly)
     def forward(self, modality_features, modality_mask: Optional[torch.Tensor] = None):
         if not self.modality_names:
             raise ValueError("No modalities provided for PairwiseModalityAttention.")

@@ -78,6 +78,7 @@ class _AttentionPoolFunction(torch.autograd.Function):
         return dx, dw.view(1, D), db.view(ctx.bias_shape), None
 
 
+@torch.compiler.disable  # HIP library calls: opaque to TorchDynamo (runs eagerly)
 def attention_pool(frames: torch.Tensor, attention: nn.Linear, mask: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Learned-score softmax pooling over the frame axis (src/encoders.py:313-336) on HIP."""
     _nat.require_device(frames, "FrameEncoder input")
@@ -110,6 +111,7 @@ class FrameEncoder(nn.Module):
         self.projection = nn.Sequential(nn.Linear(hidden_dim, hidden_dim), nn.ReLU(), nn.Dropout(dropout),
                                         nn.Linear(hidden_dim, output_dim))
 
+    @torch.compiler.disable  # HIP library calls: opaque to TorchDynamo (runs eagerly)
     def forward(self, frames: torch.Tensor, mask: Optional[torch.Tensor] = None) -> torch.Tensor:
         if frames.dim() != 3:
             raise ValueError(f"Expected 3D frame tensor, got shape {frames.shape}")
@@ -134,6 +136,7 @@ class FrameEncoder(nn.Module):
             raise ValueError(f"Unknown pooling strategy: {self.temporal_pooling}")
         return self.projection(pooled)
 
+    @torch.compiler.disable  # HIP library calls: opaque to TorchDynamo (runs eagerly)
     def attention_pool(self, frames: torch.Tensor, mask: Optional[torch.Tensor] = None) -> torch.Tensor:
         if self.attention is None:
             raise RuntimeError("Attention layer not initialized.")
@@ -225,6 +228,7 @@ class _LstmLayersFunction(torch.autograd.Function):
         return tuple(grads)
 
 
+@torch.compiler.disable  # HIP library calls: opaque to TorchDynamo (runs eagerly)
 def lstm_layers(rnns: Sequence[nn.LSTM], inputs: Sequence[torch.Tensor]) -> List[torch.Tensor]:
     """Run several nn.LSTM parameter sets (batch_first, zero initial state) over their inputs on the
     HIP recurrence, every layer of all of them in one launch; returns each LSTM's top-layer output
@@ -305,6 +309,7 @@ class SequenceEncoder(nn.Module):
     def encode_final_state(self, final_state: torch.Tensor) -> torch.Tensor:
         return self.projection(self.dropout_layer(final_state))
 
+    @torch.compiler.disable  # HIP library calls: opaque to TorchDynamo (runs eagerly)
     def forward(self, sequence: torch.Tensor, lengths: Optional[torch.Tensor] = None) -> torch.Tensor:
         if sequence.dim() != 3:
             raise ValueError(f"Expected 3D input sequence, got shape {sequence.shape}")
@@ -314,6 +319,7 @@ class SequenceEncoder(nn.Module):
         return self.encode_final_state(_final_state(out, lengths))
 
 
+@torch.compiler.disable  # HIP library calls: opaque to TorchDynamo (runs eagerly)
 def encode_sequences(encoders: Dict[str, SequenceEncoder], sequences: Dict[str, torch.Tensor],
                      lengths: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
     """{m: encoders[m](sequences[m], lengths)} with every modality's LSTM layers sharing launches

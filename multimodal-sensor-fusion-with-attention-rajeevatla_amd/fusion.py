@@ -142,6 +142,7 @@ class LateFusion(nn.Module):
         self.weight_logits = nn.Parameter(torch.zeros(self.num_modalities))
         self.dropout = nn.Dropout(dropout)
 
+    @torch.compiler.disable  # HIP library calls: opaque to TorchDynamo (runs eagerly)
     def forward(self, modality_features, modality_mask=None):
         if not self.modality_names:
             raise ValueError("No modalities configured for LateFusion.")
@@ -367,6 +368,7 @@ class HybridFusion(nn.Module):
         return _Plan(self, seq, dims, B, self.present_pairs(), return_attention)
 
     # ------------------------------------------------------------------ forward
+    @torch.compiler.disable  # HIP library calls: opaque to TorchDynamo (runs eagerly)
     def forward(self, modality_features: Dict[str, torch.Tensor],
                 modality_mask: Optional[torch.Tensor] = None, return_attention: bool = False):
         if not self.modality_names:
@@ -399,6 +401,7 @@ class HybridFusion(nn.Module):
             return logits, {"attention_maps": attention_maps, "fusion_weights": fw}
         return logits
 
+    @torch.compiler.disable  # HIP library calls: opaque to TorchDynamo (runs eagerly)
     def compute_adaptive_weights(self, modality_features: Dict[str, torch.Tensor],
                                  modality_mask: torch.Tensor) -> torch.Tensor:
         """src/fusion.py:429-479 on the device (gating scores -> masked softmax -> renormalise)."""
