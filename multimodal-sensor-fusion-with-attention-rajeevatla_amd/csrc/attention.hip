@@ -1209,7 +1209,7 @@ __device__ __forceinline__ void load_frag_vec(float* f, const float* row) {
 }
 
 template <int HDP, bool BF>
-__global__ __launch_bounds__(NT) void attn_pool_fwd_lean(const AttnArgs A) {
+__global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(const AttnArgs A) {
   constexpr int LS = HDP + 4;
   constexpr int HALF = HDP / 2;
   constexpr int NKT = PKC / 32;
