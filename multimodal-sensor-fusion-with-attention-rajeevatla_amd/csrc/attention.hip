@@ -787,7 +787,7 @@ MMF_CHAIN16(dq[dt], Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], ds[r])
 
 // Pooled backward, key on the lane: dK = scale * dS^T Q (needs D from the dq kernel).
 template <int HDP, bool BF>
-__global__ __launch_bounds__(NT) void attn_pool_bwd_dk_kernel(const AttnArgs A) {
+__global__ __launch_bounds__(NT, 4) void attn_pool_bwd_dk_kernel(const AttnArgs A) {
   constexpr int QC = 128;
   constexpr int LS = HDP + 4;
   constexpr int HALF = HDP / 2;
@@ -1056,7 +1056,7 @@ __global__ __launch_bounds__(NT) void attn_poolL_colsum_kernel(const AttnArgs A)
 }
 
 template <int HDP, bool BF>
-__global__ __launch_bounds__(NT) void attn_poolL_dq_kernel(const AttnArgs A) {
+__global__ __launch_bounds__(NT, 4) void attn_poolL_dq_kernel(const AttnArgs A) {
   constexpr int KC = 128;   // keys per LDS chunk (34 KB at HDP = 64: 4 workgroups / CU)
   constexpr int LS = HDP + 4;
   constexpr int HALF = HDP / 2;
