@@ -95,6 +95,19 @@ __device__ __forceinline__ bool tile_ctx(const GemmGroup& G, int local, TileCtx&
 // +addm; relu; gate; rowscale; dropout (keep(site, i*N + j)).
 constexpr int CS = BN + 4;
 
+// 8 consecutive floats of a side operand row (vec: two 16-B loads)
+__device__ __forceinline__ void load8(float (&d)[8], const float* p, int nv, bool vec) {
+  if (vec) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(p);
+    const f32x4 b = *reinterpret_cast<const f32x4*>(p + 4);
+    d[0] = a[0]; d[1] = a[1]; d[2] = a[2]; d[3] = a[3];
+    d[4] = b[0]; d[5] = b[1]; d[6] = b[2]; d[7] = b[3];
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) d[e] = e < nv ? p[e] : 0.f;
+  }
+}
+
 template <int PR = 64>   // rows per LDS pass (64 or 32)
 __device__ __forceinline__ void epilogue(const GemmGroup& G, const TileCtx& T, f32x16 (&acc)[2][2], float* cs,
                                          const RngSnap& rs, float p, float inv_keep, int wm, int wn, int h,
@@ -111,6 +124,11 @@ __device__ __forceinline__ void epilogue(const GemmGroup& G, const TileCtx& T, f
   // a thread always finishes the same 8 columns (rows t>>4 + 16*it of each 64-row pass)
   const int cg = (t & 15) * 8, j0 = T.j0 + cg;
   const int nv = min(8, G.N - j0);
+  // side operands (rowadd / addm / gate) row-vectorisable: 16-B aligned rows, 8 columns present
+  const bool vside = nv == 8 && (j0 % 4) == 0 &&
+                     (!(epi & EPI_ROWADD) || ((G.ld_rowadd % 4) == 0 && ((uintptr_t)G.rowadd & 15) == 0)) &&
+                     (!(epi & EPI_ADDMAT) || ((G.ld_addm % 4) == 0 && ((uintptr_t)G.addm & 15) == 0)) &&
+                     (!(epi & EPI_GATE) || ((G.ld_gate % 4) == 0 && ((uintptr_t)G.gate & 15) == 0));
   float bias[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) bias[e] = (!partial && (epi & EPI_BIAS) && e < nv) ? T.biasb[j0 + e] : 0.f;
@@ -144,15 +162,29 @@ __device__ __forceinline__ void epilogue(const GemmGroup& G, const TileCtx& T, f
         if (coop) rr = philox_block(rs, G.drop_site, ((uint64_t)i * (uint64_t)G.N + (uint64_t)j0) >> 3);
         const float brs = (epi & EPI_BIAS_RS) ? G.bias_rs[(int64_t)i * G.bias_rs_ld + T.brs_off] : 1.f;
         const float rsc = (epi & EPI_ROWSCALE) ? G.rowscale[(int64_t)(i / G.rs_div) * G.rs_stride + G.rs_off] : 1.f;
+        // the row's side operands as two 16-B loads each (issued together, before the math)
+        float ad[8], gt[8];
+        if (epi & EPI_ROWADD) {
+          load8(ad, G.rowadd + (int64_t)(i / G.rowadd_div) * G.ld_rowadd + j0, nv, vside);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = v[e] * G.alpha + G.rowadd_scale * ad[e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] *= G.alpha;
+        }
+        if (epi & EPI_ADDMAT) {
+          load8(ad, G.addm + (int64_t)i * G.ld_addm + j0, nv, vside);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += ad[e];
+        }
+        if (epi & EPI_GATE) load8(gt, G.gate + (int64_t)i * G.ld_gate + j0, nv, vside);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           if (e >= nv) break;
           const int j = j0 + e;
-          float x = v[e] * G.alpha + bias[e] * brs;
-          if (epi & EPI_ROWADD) x += G.rowadd_scale * G.rowadd[(int64_t)(i / G.rowadd_div) * G.ld_rowadd + j];
-          if (epi & EPI_ADDMAT) x += G.addm[(int64_t)i * G.ld_addm + j];
+          float x = v[e] + bias[e] * brs;
           if (epi & EPI_RELU) x = fmaxf(x, 0.f);
-          if (epi & EPI_GATE) x = G.gate[(int64_t)i * G.ld_gate + j] > 0.f ? x * G.gate_scale : 0.f;
+          if (epi & EPI_GATE) x = gt[e] > 0.f ? x * G.gate_scale : 0.f;
           x *= rsc;
           if (drop) {
             const bool keep = coop ? keep_from(rr, e, thr)

@@ -67,6 +67,42 @@ int main() {
       jobs.push_back(j);
     }
     run("dZ", jobs, MODE_RK, MODE_KR, 3.0 * 4 * 2 * R * H * H);
+    // the same FLOPs as ONE source of K = 4H per output (source-switch cost)
+    std::vector<GemmJob> one;
+    float* a1 = dev((size_t)3 * R * 4 * H);
+    float* w1 = dev((size_t)3 * 4 * H * H);
+    for (int m = 0; m < 3; ++m) {
+      GemmJob j = make_job(R, H, out + (size_t)m * R * H, H, 0);
+      add_src(j, opnd(a1 + (size_t)m * R * 4 * H, 4 * H), opnd(w1 + (size_t)m * 4 * H * H, H), 4 * H);
+      one.push_back(j);
+    }
+    run("dZ_1src", one, MODE_RK, MODE_KR, 3.0 * 4 * 2 * R * H * H);
+    // RK B operand (W^T stored [j][kk]) instead of KR
+    run("dZ_1srcRK", one, MODE_RK, MODE_RK, 3.0 * 4 * 2 * R * H * H);
+    // the real epilogue: ReLU gate from P_m (EPI_GATE) + row-broadcast c_m / L (EPI_ROWADD)
+    float* gate = dev((size_t)3 * R * H);
+    float* cvec = dev((size_t)256 * 3 * H);
+    std::vector<GemmJob> g = jobs;
+    for (int m = 0; m < 3; ++m) {
+      g[m].g.epi = EPI_GATE | EPI_ROWADD;
+      g[m].g.gate = gate + (size_t)m * R * H; g[m].g.ld_gate = H; g[m].g.gate_scale = 1.f;
+      g[m].g.rowadd = cvec + (size_t)m * H; g[m].g.ld_rowadd = 3 * H; g[m].g.rowadd_div = 128;
+      g[m].g.rowadd_scale = 1.f / 128.f;
+    }
+    run("dZ_gate", g, MODE_RK, MODE_KR, 3.0 * 4 * 2 * R * H * H);
+    // + E_m: 2 per-sample K = heads sources (pbar^T rows against dU_b, segment offsets)
+    float* pbT = dev((size_t)2 * R * 4);
+    float* du = dev((size_t)2 * 256 * 4 * H);
+    std::vector<GemmJob> ge = g;
+    for (int m = 0; m < 3; ++m) {
+      ge[m].g.seg_rows = 128;
+      for (int e = 0; e < 2; ++e) {
+        Operand d = opnd(du + (size_t)e * 256 * 4 * H, H);
+        d.seg_stride = 4 * H;
+        add_src(ge[m], opnd(pbT + (size_t)e * R * 4, 4), d, 4);
+      }
+    }
+    run("dZ_gate_em", ge, MODE_RK, MODE_KR, 3.0 * 4 * 2 * R * H * H);
   }
   // bwd.wgrad: 15 x (H x H) = dY^T X over R rows, split-K slabs
   {
