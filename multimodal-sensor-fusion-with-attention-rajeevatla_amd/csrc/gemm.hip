@@ -863,21 +863,30 @@ __global__ __launch_bounds__(256) void partial_reduce_kernel(const ReduceArgs a)
       }
     }
   }
-  // bias gradient: row sums of the slabs' part_db (4 independent partial sums
-  // per thread so the loads overlap; fixed order => deterministic)
+  // bias gradient: row sums of the slabs' part_db, on the dedicated last block
+  // (launch_reduce adds it past the column blocks).  Same split-group layout as
+  // the columns: 64 rows x 4 groups, 4 partial sums per thread (16 loads in
+  // flight), combined in a fixed order => deterministic.
   if (J.db && J.part_db && blockIdx.x == gridDim.x - 1) {
-    for (int i = threadIdx.x; i < J.M; i += blockDim.x) {
+    __shared__ float redb[4][64];
+    for (int i0 = 0; i0 < J.M; i0 += 64) {
+      const int i = i0 + el;
       float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-      int k = 0;
+      if (i < J.M) {
+        int k = sg;
 #pragma unroll 4
-      for (; k + 3 < J.nsplit; k += 4) {
-        s0 += J.part_db[(int64_t)k * J.M + i];
-        s1 += J.part_db[(int64_t)(k + 1) * J.M + i];
-        s2 += J.part_db[(int64_t)(k + 2) * J.M + i];
-        s3 += J.part_db[(int64_t)(k + 3) * J.M + i];
+        for (; k + 12 < J.nsplit; k += 16) {
+          s0 += J.part_db[(int64_t)k * J.M + i];
+          s1 += J.part_db[(int64_t)(k + 4) * J.M + i];
+          s2 += J.part_db[(int64_t)(k + 8) * J.M + i];
+          s3 += J.part_db[(int64_t)(k + 12) * J.M + i];
+        }
+        for (; k < J.nsplit; k += 4) s0 += J.part_db[(int64_t)k * J.M + i];
       }
-      for (; k < J.nsplit; ++k) s0 += J.part_db[(int64_t)k * J.M + i];
-      J.db[i] = (s0 + s1) + (s2 + s3);
+      __syncthreads();
+      redb[sg][el] = (s0 + s1) + (s2 + s3);
+      __syncthreads();
+      if (sg == 0 && i < J.M) J.db[i] = (redb[0][el] + redb[1][el]) + (redb[2][el] + redb[3][el]);
     }
   }
 }
@@ -1147,6 +1156,8 @@ hipError_t launch_reduce(const ReduceJob* jobs, int njobs, hipStream_t st) {
     int blocks = (int)((maxmn / 4 + 63) / 64);
     if (blocks < 1) blocks = 1;
     if (blocks > 4096) blocks = 4096;
+    for (int i = 0; i < n; ++i)
+      if (a.j[i].db && a.j[i].part_db) { ++blocks; break; }   // dedicated bias-row block
     double by = 0.0;   // slabs (+ bias-row slabs) read once, sums written once
     for (int i = 0; i < n; ++i) {
       const ReduceJob& r = a.j[i];
