@@ -7,7 +7,8 @@ B=256 samples per GPU, T=L=128 tokens per modality, d_model=D=H=128, 4 heads,
 outputs of each modality (sequence mode), resident in HBM.
 One step = HybridFusion forward -> CrossEntropy(label_smoothing=0.05) ->
 backward (all parameter grads + input grads) -> [RCCL all-reduce of the flat
-gradient when N > 1] -> AdamW.  Weak scaling: every rank runs B=256.
+gradient when N > 1] -> global-norm gradient clipping (1.0) -> AdamW
+(lr 1e-3, weight decay 1e-4: config/base.yaml:69-74).  Weak scaling: every rank runs B=256.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c2_l1]
 N > 1 is launched by torch.distributed.run (one process per GPU, RCCL).
@@ -208,7 +209,6 @@ def main():
     names = [f"m{i}" for i in range(M)]
     model = HybridFusion({n: D for n in names}, hidden_dim=H, num_classes=C, num_heads=heads,
                          dropout=0.1).to(dev)
-    model._rng_state[0] ^= rank * 0x9E3779B1  # distinct dropout streams per rank
     feats, mask, labels = make_inputs(w, B, 42 + rank, dev)
     trainer = HybridTrainStep(model, feats, mask, labels, process_group=pg)
 
@@ -269,7 +269,7 @@ def main():
                                    f"{'' if max(Ls) else ' (2-D reference semantics)'} D={D} H={H} heads={heads} "
                                    f"C={C} dropout=0.1 train"
                                    f"{mask_note}"
-                                   f", fwd+CE(ls=0.05)+bwd+AdamW",
+                                   f", fwd+CE(ls=0.05)+bwd+clip(1.0)+AdamW",
                        "global_batch": B * world, "seq_len": lens or 1, "parallelism": f"dp{world}",
                        "graph": not args.no_graph, "matmul_precision": args.precision},
             "roofline": roofline,

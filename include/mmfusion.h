@@ -136,6 +136,17 @@ int mmf_adaptive_weights(int32_t batch, int32_t num_modalities, int32_t hidden,
                          const float* const* feats, const float* mask,
                          const mmf_linear* gate /* [M] */, float* weights, void* workspace,
                          void* stream);
+/* Backward of sum(weights * dweights) through compute_adaptive_weights (the
+ * reference's result is differentiable, src/fusion.py:452-479): dfeats (B, M, H)
+ * stacked per modality (may be NULL), dgate[m] = gradients of gating_layers.{m}
+ * (WRITTEN, batch-reduced in a fixed order; may be NULL).  The masked positions
+ * and the fallback branch get zero score gradients, as in autograd through
+ * masked_fill / torch.where.  Same workspace as the forward. */
+int mmf_adaptive_weights_backward(int32_t batch, int32_t num_modalities, int32_t hidden,
+                                  const float* const* feats, const float* mask,
+                                  const mmf_linear* gate /* [M] */, const float* dweights,
+                                  float* dfeats, const mmf_linear_grad* dgate /* [M] */,
+                                  void* workspace, void* stream);
 
 /* ---------------------------------------------------------------------
  * CrossModalAttention (src/attention.py:16-146), standalone.
@@ -241,8 +252,11 @@ int mmf_gather_chunks(const float* table, int64_t rows, int32_t ncols, const int
  *   dgates (B, T, 4H) = gradient of the pre-activation gates (= d xproj;
  *   dW_hh = sum_t dgates_t^T h_{t-1}).
  * sync[i]: device scratch of mmf_lstm_sync_bytes(batch, hidden) bytes per
- * LSTM (re-zeroed on the stream by every call).  timeout: device uint32 the
- * kernel ORs 1 into if an inter-workgroup wait gives up (results invalid).
+ * LSTM (re-zeroed on the stream by every call).  timeout: device uint32, zeroed
+ * on the stream by every call, that the kernel ORs 1 into if an inter-workgroup
+ * wait gives up; the values that never arrived are then NaN, so the call's
+ * outputs (h, c, gates / dgates) carry NaN rather than silently wrong numbers.
+ * A grid the device cannot hold co-resident returns MMF_ELIMIT before launch.
  * ------------------------------------------------------------------- */
 size_t mmf_lstm_sync_bytes(int32_t batch, int32_t hidden);
 int mmf_lstm_forward(int32_t num_lstm, int32_t batch, int32_t steps, int32_t hidden, const float* const* xproj,
@@ -269,6 +283,26 @@ int mmf_cross_entropy_ls(int32_t batch, int32_t classes, const float* logits,
 int mmf_adamw_step(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                    int64_t* step_dev, float lr, float beta1, float beta2, float eps,
                    float weight_decay, float grad_scale, void* stream);
+
+/* AdamW with the learning rate and an extra gradient factor read from device
+ * scalars (lr_dev[0]; grad_coef_dev[0], may be NULL = 1), so a captured hipGraph
+ * step follows an LR scheduler (CosineAnnealingLR, src/train.py:394-402) and
+ * gradient clipping without re-capture.  Effective gradient =
+ * grad * grad_scale * grad_coef_dev[0]. */
+int mmf_adamw_step_dev(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                       int64_t* step_dev, const float* lr_dev, const float* grad_coef_dev, float beta1,
+                       float beta2, float eps, float weight_decay, float grad_scale, void* stream);
+
+/* Global-norm gradient clipping (torch.nn.utils.clip_grad_norm_(max_norm,
+ * norm_type=2) as Lightning applies gradient_clip_val, src/train.py:416-430,
+ * config/base.yaml:74 gradient_clip_norm): over the flat gradient scaled by
+ * grad_scale, total_norm[0] (may be NULL) = ||grad * grad_scale||_2 and
+ * clip_coef[0] = min(1, max_norm / (total_norm + 1e-6)) (1 when max_norm <= 0),
+ * both device floats; feed clip_coef to mmf_adamw_step_dev.  Deterministic
+ * fixed-order reduction.  grad 16-byte aligned. */
+size_t mmf_grad_clip_workspace_bytes(void);
+int mmf_grad_clip_coef(int64_t n, const float* grad, float grad_scale, float max_norm, float* total_norm,
+                       float* clip_coef, void* workspace, void* stream);
 
 /* Timing for the benchmark: between begin and end every launch group AND
  * every kernel launch of the entry points above is bracketed by hipEvents on

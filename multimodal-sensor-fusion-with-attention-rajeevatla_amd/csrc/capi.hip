@@ -155,24 +155,28 @@ size_t mmf_profile_end(char* out, size_t cap) {
   return s.size() + 1;
 }
 
-size_t mmf_adaptive_weights_workspace_bytes(int32_t batch, int32_t M, int32_t H) {
-  Bump bp(nullptr);
-  bp.take<float>((size_t)batch * M * H);
-  bp.take<float>((size_t)batch * M);
-  bp.take<float>((size_t)batch * M);
-  bp.take<float>((size_t)batch * H);
-  return bp.off + 256;
+// compute_adaptive_weights workspace: the head-forward scratch (pooled, scores,
+// weights, fused) plus the backward's dscore and a cvec (B, M, H) scratch used
+// when the caller does not want the feature gradients.
+namespace {
+struct AdaptiveWs { float *pooled, *scores, *weights, *fused, *dscore, *cvec; };
+void layout_adaptive(Bump& bp, int32_t batch, int32_t M, int32_t H, AdaptiveWs& w) {
+  w.pooled = bp.take<float>((size_t)batch * M * H);
+  w.scores = bp.take<float>((size_t)batch * M);
+  w.weights = bp.take<float>((size_t)batch * M);
+  w.fused = bp.take<float>((size_t)batch * H);
+  w.dscore = bp.take<float>((size_t)batch * M);
+  w.cvec = bp.take<float>((size_t)batch * M * H);
 }
-
-int mmf_adaptive_weights(int32_t batch, int32_t M, int32_t H, const float* const* feats,
-                         const float* mask, const mmf_linear* gate, float* weights, void* workspace,
-                         void* stream) {
+int check_adaptive(int32_t batch, int32_t M, int32_t H) {
   if (batch < 1 || M < 1 || M > MMF_MAX_MODALITIES || H < 4 || H % 4 != 0 || H > 1024)
     return fail(MMF_ELIMIT, "adaptive weights: unsupported shape B=%d M=%d H=%d", batch, M, H);
-  if (!feats || !mask || !gate || !weights || !workspace) return fail(MMF_EINVAL, "null argument");
-  hipStream_t st = (hipStream_t)stream;
-  Bump bp(workspace);
-  HeadArgs ha;
+  return MMF_OK;
+}
+// head arguments of src/fusion.py:429-479 alone: one (B, H) source per modality,
+// no mask scaling of the features, no list-length divisor
+void fill_adaptive(HeadArgs& ha, int32_t batch, int32_t M, int32_t H, const float* const* feats,
+                   const float* mask, const mmf_linear* gate, const AdaptiveWs& w) {
   memset(&ha, 0, sizeof(ha));
   ha.B = batch; ha.M = M; ha.H = H; ha.mask = mask;
   ha.scale_by_mask = 0;
@@ -185,12 +189,63 @@ int mmf_adaptive_weights(int32_t batch, int32_t M, int32_t H, const float* const
     ha.gate_w[m] = gate[m].w;
     ha.gate_b[m] = gate[m].b;
   }
-  ha.pooled = bp.take<float>((size_t)batch * M * H);
-  ha.scores = bp.take<float>((size_t)batch * M);
-  ha.weights = bp.take<float>((size_t)batch * M);
-  ha.fused = bp.take<float>((size_t)batch * H);
+  ha.pooled = w.pooled; ha.scores = w.scores; ha.weights = w.weights; ha.fused = w.fused;
+}
+}  // namespace
+
+size_t mmf_adaptive_weights_workspace_bytes(int32_t batch, int32_t M, int32_t H) {
+  if (batch < 1 || M < 1 || H < 1) return 0;
+  Bump bp(nullptr);
+  AdaptiveWs w;
+  layout_adaptive(bp, batch, M, H, w);
+  return bp.off + 256;
+}
+
+int mmf_adaptive_weights(int32_t batch, int32_t M, int32_t H, const float* const* feats,
+                         const float* mask, const mmf_linear* gate, float* weights, void* workspace,
+                         void* stream) {
+  if (int rc = check_adaptive(batch, M, H)) return rc;
+  if (!feats || !mask || !gate || !weights || !workspace) return fail(MMF_EINVAL, "null argument");
+  hipStream_t st = (hipStream_t)stream;
+  Bump bp(workspace);
+  AdaptiveWs w;
+  layout_adaptive(bp, batch, M, H, w);
+  HeadArgs ha;
+  fill_adaptive(ha, batch, M, H, feats, mask, gate, w);
   ha.weights_out = weights;
   STAGE_TRY("adaptive_weights", launch_head_fwd(ha, st));
+  return MMF_OK;
+}
+
+int mmf_adaptive_weights_backward(int32_t batch, int32_t M, int32_t H, const float* const* feats,
+                                  const float* mask, const mmf_linear* gate, const float* dweights,
+                                  float* dfeats, const mmf_linear_grad* dgate, void* workspace,
+                                  void* stream) {
+  if (int rc = check_adaptive(batch, M, H)) return rc;
+  if (!feats || !mask || !gate || !dweights || !workspace) return fail(MMF_EINVAL, "null argument");
+  hipStream_t st = (hipStream_t)stream;
+  Bump bp(workspace);
+  AdaptiveWs w;
+  layout_adaptive(bp, batch, M, H, w);
+  HeadArgs ha;
+  fill_adaptive(ha, batch, M, H, feats, mask, gate, w);
+  // recompute the scores (the backward of the masked softmax re-derives its branch from them)
+  STAGE_TRY("adaptive_weights.bwd.recompute", launch_head_fwd(ha, st));
+  ha.dfused = nullptr;
+  ha.dweights = dweights;
+  ha.dscore = w.dscore;
+  ha.cvec = dfeats ? dfeats : w.cvec;   // d feat_m = dscore_m * gate_w[m]  (B, M, H)
+  STAGE_TRY("adaptive_weights.bwd.head", launch_head_bwd(ha, st));
+  if (dgate) {
+    float* dgw[MMF_MAX_MODALITIES];
+    float* dgb[MMF_MAX_MODALITIES];
+    for (int m = 0; m < M; ++m) {
+      if (!dgate[m].w || !dgate[m].b) return fail(MMF_EINVAL, "null gate gradient");
+      dgw[m] = dgate[m].w;
+      dgb[m] = dgate[m].b;
+    }
+    STAGE_TRY("adaptive_weights.bwd.gate_wgrad", launch_gate_wgrad(batch, M, H, w.dscore, w.pooled, dgw, dgb, st));
+  }
   return MMF_OK;
 }
 
@@ -330,6 +385,29 @@ int mmf_adamw_step(int64_t n, float* param, const float* grad, float* exp_avg, f
   hipStream_t st = (hipStream_t)stream;
   STAGE_TRY("optim.adamw", launch_adamw(n, param, grad, exp_avg, exp_avg_sq, step_dev, lr, beta1, beta2,
                                         eps, weight_decay, grad_scale, st));
+  return MMF_OK;
+}
+
+size_t mmf_grad_clip_workspace_bytes(void) { return grad_clip_workspace_bytes() + 256; }
+
+int mmf_grad_clip_coef(int64_t n, const float* grad, float grad_scale, float max_norm, float* total_norm,
+                       float* clip_coef, void* workspace, void* stream) {
+  if (n < 0 || !grad || !clip_coef || !workspace) return fail(MMF_EINVAL, "bad gradient-clip arguments");
+  if (reinterpret_cast<uintptr_t>(grad) & 15) return fail(MMF_EINVAL, "gradient-clip: grad must be 16-byte aligned");
+  hipStream_t st = (hipStream_t)stream;
+  STAGE_TRY("optim.clip_norm", launch_grad_clip_coef(n, grad, grad_scale, max_norm, total_norm, clip_coef,
+                                                     (float*)workspace, st));
+  return MMF_OK;
+}
+
+int mmf_adamw_step_dev(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                       int64_t* step_dev, const float* lr_dev, const float* grad_coef_dev, float beta1,
+                       float beta2, float eps, float weight_decay, float grad_scale, void* stream) {
+  if (n < 0 || !param || !grad || !exp_avg || !exp_avg_sq || !step_dev || !lr_dev)
+    return fail(MMF_EINVAL, "bad AdamW arguments");
+  hipStream_t st = (hipStream_t)stream;
+  STAGE_TRY("optim.adamw", launch_adamw(n, param, grad, exp_avg, exp_avg_sq, step_dev, 0.f, beta1, beta2, eps,
+                                        weight_decay, grad_scale, st, lr_dev, grad_coef_dev));
   return MMF_OK;
 }
 

@@ -133,13 +133,18 @@ __global__ __launch_bounds__(NT) void head_bwd_kernel(const HeadArgs a) {
   const int b = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int M = a.M, H = a.H;
-  const float* df = a.dfused + (int64_t)b * H;
+  const float* df = a.dfused ? a.dfused + (int64_t)b * H : nullptr;
   const float* pooled = a.pooled + (int64_t)b * M * H;
-  // dL/dw_m = dfused . pooled_m   (fused = sum_m w_m pooled_m)
+  // dL/dw_m = dfused . pooled_m   (fused = sum_m w_m pooled_m), or given directly
+  // (compute_adaptive_weights backward: dfused is null, dweights (B, M) the upstream grad)
   for (int m = wave; m < M; m += 4) {
     float s = 0.f;
-    for (int j = lane; j < H; j += 64) s += df[j] * pooled[m * H + j];
-    s = wave_sum(s);
+    if (df) {
+      for (int j = lane; j < H; j += 64) s += df[j] * pooled[m * H + j];
+      s = wave_sum(s);
+    } else {
+      s = a.dweights[(int64_t)b * M + m];
+    }
     if (lane == 0) dw_s[m] = s;
   }
   __syncthreads();
@@ -173,11 +178,11 @@ __global__ __launch_bounds__(NT) void head_bwd_kernel(const HeadArgs a) {
   __syncthreads();
   for (int m = 0; m < M; ++m) {
     const float wm = a.weights[(int64_t)b * M + m];
-    const float f = a.mask[(int64_t)b * M + m] * a.inv_cnt[m];
+    const float f = (a.scale_by_mask ? a.mask[(int64_t)b * M + m] : 1.f) * a.inv_cnt[m];
     const float dsm = dscore_s[m];
     const float* gw = a.gate_w[m];
     for (int j = t; j < H; j += NT) {
-      const float dp = wm * df[j] + dsm * gw[j];
+      const float dp = (df ? wm * df[j] : 0.f) + dsm * gw[j];
       a.cvec[((int64_t)b * M + m) * H + j] = dp * f;
     }
   }
@@ -246,11 +251,67 @@ __global__ __launch_bounds__(NT) void cross_entropy_kernel(int B, int C, const f
   if (t == 0) loss[0] = red[0] / (float)B;
 }
 
+// Global gradient norm for clipping (torch.nn.utils.clip_grad_norm_, norm_type 2, as
+// Lightning's gradient_clip_val applies it: src/train.py:416-430, config/base.yaml:74).
+// Pass 1: CLIP_BLOCKS fixed partial sums of squares (grid-stride, fixed order);
+// pass 2: one workgroup adds them in a fixed tree order -> deterministic.
+constexpr int CLIP_BLOCKS = 256;
+
+__global__ __launch_bounds__(NT) void grad_sumsq_kernel(int64_t n, const float* __restrict__ g,
+                                                        float* __restrict__ partial) {
+  __shared__ float red[NT];
+  const int t = threadIdx.x;
+  float acc = 0.f;
+  const int64_t n4 = n / 4;
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  for (int64_t i = (int64_t)blockIdx.x * NT + t; i < n4; i += (int64_t)CLIP_BLOCKS * NT) {
+    const float4 v = g4[i];
+    acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  if (blockIdx.x == 0)
+    for (int64_t i = 4 * n4 + t; i < n; i += NT) acc += g[i] * g[i];
+  red[t] = acc;
+  __syncthreads();
+  for (int s = NT / 2; s > 0; s >>= 1) {
+    if (t < s) red[t] += red[t + s];
+    __syncthreads();
+  }
+  if (t == 0) partial[blockIdx.x] = red[0];
+}
+
+// total_norm = gscale * sqrt(sum); coef = min(1, max_norm / (total_norm + 1e-6)) (1 when max_norm <= 0)
+__global__ __launch_bounds__(NT) void clip_coef_kernel(const float* __restrict__ partial, float gscale,
+                                                       float max_norm, float* norm_out, float* coef_out) {
+  __shared__ double red[NT];
+  const int t = threadIdx.x;
+  double acc = 0.0;
+  for (int i = t; i < CLIP_BLOCKS; i += NT) acc += (double)partial[i];
+  red[t] = acc;
+  __syncthreads();
+  for (int s = NT / 2; s > 0; s >>= 1) {
+    if (t < s) red[t] += red[t + s];
+    __syncthreads();
+  }
+  if (t == 0) {
+    const float norm = (float)(sqrt(red[0]) * (double)gscale);
+    float coef = 1.f;
+    if (max_norm > 0.f) coef = fminf(1.f, max_norm / (norm + 1e-6f));
+    if (norm_out) norm_out[0] = norm;
+    coef_out[0] = coef;
+  }
+}
+
 // torch.optim.AdamW (amsgrad=False, maximize=False): decoupled weight decay.
+// lr_dev (optional) replaces lr and coef_dev (optional) multiplies the gradient
+// scale, both read on the device so a captured step follows a scheduler / clipping.
 __global__ __launch_bounds__(NT) void adamw_kernel(int64_t n, float* __restrict__ p,
                                                    const float* __restrict__ g, float* __restrict__ m,
                                                    float* __restrict__ v, const int64_t* step, float lr,
-                                                   float b1, float b2, float eps, float wd, float gscale) {
+                                                   float b1, float b2, float eps, float wd, float gscale,
+                                                   const float* __restrict__ lr_dev,
+                                                   const float* __restrict__ coef_dev) {
+  if (lr_dev) lr = lr_dev[0];
+  if (coef_dev) gscale *= coef_dev[0];
   const double st = (double)(*step + 1);
   const float bc1 = (float)(1.0 - pow((double)b1, st));
   const float bc2s = (float)sqrt(1.0 - pow((double)b2, st));
@@ -314,15 +375,31 @@ hipError_t launch_cross_entropy(int B, int C, const float* logits, const int64_t
   return hipGetLastError();
 }
 
+size_t grad_clip_workspace_bytes() { return CLIP_BLOCKS * sizeof(float); }
+
+hipError_t launch_grad_clip_coef(int64_t n, const float* g, float gscale, float max_norm, float* norm_out,
+                                 float* coef_out, float* partial, hipStream_t st) {
+  {
+    ProfLaunch prof_(st, "grad_sumsq_kernel", 2.0 * n, 4.0 * n);
+    hipLaunchKernelGGL(grad_sumsq_kernel, dim3(CLIP_BLOCKS), dim3(NT), 0, st, n, g, partial);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  ProfLaunch prof_(st, "clip_coef_kernel", 0.0, 4.0 * CLIP_BLOCKS);
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(NT), 0, st, (const float*)partial, gscale, max_norm, norm_out,
+                     coef_out);
+  return hipGetLastError();
+}
+
 hipError_t launch_adamw(int64_t n, float* p, const float* g, float* m, float* v, int64_t* step,
                         float lr, float b1, float b2, float eps, float wd, float gscale,
-                        hipStream_t st) {
+                        hipStream_t st, const float* lr_dev, const float* coef_dev) {
   int64_t blocks = (n + NT - 1) / NT;
   if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
   ProfLaunch prof_(st, "adamw_kernel", 0.0, 28.0 * n);   // p m v read+write, g read
   hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(NT), 0, st, n, p, g, m, v, step, lr, b1,
-                     b2, eps, wd, gscale);
+                     b2, eps, wd, gscale, lr_dev, coef_dev);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(step_incr_kernel, dim3(1), dim3(64), 0, st, step);

@@ -10,7 +10,8 @@
 // 8-byte granules {epoch, value} (agent-scope relaxed atomic stores and polls,
 // double-buffered by step parity: the data is its own flag -- CDNA guide §6
 // Guideline 16, R2).  Nothing is ordered by dispatch or placement; every spin is
-// bounded and reports a timeout.  The backward runs the same way in reverse:
+// bounded: a wait that gives up sets the call's timeout word and poisons the
+// missing values with NaN, so the results can never be silently wrong.  The backward runs the same way in reverse:
 // each workgroup publishes its partial W_hh^T dgates for every hidden unit, each
 // unit's owner sums the G partials (fixed order).  The time-parallel GEMMs
 // (input projection, weight gradients) are left to the caller.
@@ -162,7 +163,8 @@ __global__ __launch_bounds__(LNT) void lstm_bwd_kernel(const LstmArgs a) {
           if (ready == all) break;
           if (timed_out(++spins, a.timeout)) {
             atomicOr(a.timeout, 1u);
-            for (int q = 0; q < LMAX_H / LU; ++q) if (!(ready >> q & 1)) v[q] = 0.f;
+            // poison what never arrived: the gradients become NaN, never silently wrong
+            for (int q = 0; q < LMAX_H / LU; ++q) if (!(ready >> q & 1)) v[q] = __builtin_nanf("");
             break;
           }
           __builtin_amdgcn_s_sleep(1);
@@ -305,7 +307,7 @@ __global__ __launch_bounds__(LNT) void lstm_fwd_kernel(const LstmArgs a) {
             atomicOr(a.timeout, 1u);
 #pragma unroll
             for (int p = 0; p < SWEEP_MAX; ++p)
-              if (pending >> p & 1) dst[l + 64 * p] = 0.f;
+              if (pending >> p & 1) dst[l + 64 * p] = __builtin_nanf("");   // poison: outputs become NaN
             break;
           }
           __builtin_amdgcn_s_sleep(1);
@@ -360,6 +362,23 @@ __global__ __launch_bounds__(LNT) void lstm_fwd_kernel(const LstmArgs a) {
   PROBE_END
 }
 
+// The recurrence needs every workgroup of the grid resident at once (they wait on
+// each other's granules).  Refuse a grid the device cannot hold even when idle;
+// residency under concurrent kernels (e.g. RCCL under DDP) is not guaranteed, which
+// the bounded spins + NaN poisoning + per-call timeout word make loud, not silent.
+template <typename K>
+int check_coresident(K kernel, int grid, const char* what) {
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, LNT, 0) != hipSuccess)
+    return fail(MMF_EHIP, "%s: occupancy query failed", what);
+  if ((int64_t)per_cu * cus < grid)
+    return fail(MMF_ELIMIT, "%s: %d workgroups of %d threads cannot be co-resident (%d per CU x %d CUs)", what,
+                grid, LNT, per_cu, cus);
+  return MMF_OK;
+}
+
 // split every LSTM's batch into instances of <= LMAX_B rows
 int lstm_plan(LstmArgs& a, int num_lstm, int batch, int steps, int hidden, unsigned* timeout) {
   if (num_lstm < 1 || num_lstm > LMAX_N || batch < 1 || steps < 1 || hidden < LU || hidden > LMAX_H ||
@@ -412,17 +431,16 @@ int mmf_lstm_forward(int32_t num_lstm, int32_t batch, int32_t steps, int32_t hid
     // every polled word is zeroed before the launch (epochs start at 1)
     HIP_TRY(hipMemsetAsync(sync[i], 0, mmf_lstm_sync_bytes(batch, hidden), st));
   }
+  const int grid = a.G * a.ninst;
+  void (*kern)(const LstmArgs) = hidden == 64    ? lstm_fwd_kernel<64>
+                                 : hidden == 128 ? lstm_fwd_kernel<128>
+                                 : hidden == 192 ? lstm_fwd_kernel<192>
+                                                 : lstm_fwd_kernel<256>;
+  if (int rc = check_coresident(kern, grid, "lstm forward")) return rc;
+  HIP_TRY(hipMemsetAsync(timeout, 0, sizeof(uint32_t), st));   // per call: a stale flag never aborts waits
   ProfLaunch prof_(st, "lstm_fwd_kernel", 8.0 * num_lstm * batch * steps * hidden * hidden,
                    4.0 * num_lstm * ((double)4 * hidden * hidden + (double)batch * steps * 10 * hidden));
-  const dim3 grid(a.G * a.ninst);
-  if (hidden == 64)
-    hipLaunchKernelGGL(lstm_fwd_kernel<64>, grid, dim3(LNT), 0, st, a);
-  else if (hidden == 128)
-    hipLaunchKernelGGL(lstm_fwd_kernel<128>, grid, dim3(LNT), 0, st, a);
-  else if (hidden == 192)
-    hipLaunchKernelGGL(lstm_fwd_kernel<192>, grid, dim3(LNT), 0, st, a);
-  else
-    hipLaunchKernelGGL(lstm_fwd_kernel<256>, grid, dim3(LNT), 0, st, a);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(LNT), 0, st, a);
   HIP_TRY(hipGetLastError());
   return MMF_OK;
 }
@@ -441,6 +459,8 @@ int mmf_lstm_backward(int32_t num_lstm, int32_t batch, int32_t steps, int32_t hi
     a.dgates[i] = dgates[i]; a.gran[i] = (gu64*)sync[i];
     HIP_TRY(hipMemsetAsync(sync[i], 0, mmf_lstm_sync_bytes(batch, hidden), st));
   }
+  if (int rc = check_coresident(lstm_bwd_kernel, a.G * a.ninst, "lstm backward")) return rc;
+  HIP_TRY(hipMemsetAsync(timeout, 0, sizeof(uint32_t), st));
   ProfLaunch prof_(st, "lstm_bwd_kernel", 8.0 * num_lstm * batch * steps * hidden * hidden,
                    4.0 * num_lstm * ((double)4 * hidden * hidden + (double)batch * steps * 14 * hidden));
   hipLaunchKernelGGL(lstm_bwd_kernel, dim3(a.G * a.ninst), dim3(LNT), 0, st, a);

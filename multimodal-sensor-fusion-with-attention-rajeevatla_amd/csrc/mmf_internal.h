@@ -285,7 +285,8 @@ struct HeadArgs {
   float* fused;                          // (B, H)
   float* weights_out;                    // optional copy (B, M)
   // backward
-  const float* dfused;                   // (B, H)
+  const float* dfused;                   // (B, H); null => dweights gives dL/dw directly
+  const float* dweights;                 // (B, M) upstream grad of the weights (when dfused is null)
   float* cvec;                           // (B, M, H) = dpooled_m * mask_m * inv_cnt[m]; a source
                                          // row's grad is cvec * src_scale
   float* dscore;                         // (B, M)
@@ -302,7 +303,10 @@ hipError_t launch_cross_entropy(int B, int C, const float* logits, const int64_t
                                 hipStream_t st);
 hipError_t launch_adamw(int64_t n, float* p, const float* g, float* m, float* v, int64_t* step,
                         float lr, float b1, float b2, float eps, float wd, float gscale,
-                        hipStream_t st);
+                        hipStream_t st, const float* lr_dev = nullptr, const float* coef_dev = nullptr);
+size_t grad_clip_workspace_bytes();
+hipError_t launch_grad_clip_coef(int64_t n, const float* g, float gscale, float max_norm, float* norm_out,
+                                 float* coef_out, float* partial, hipStream_t st);
 
 }  // namespace mmf
 

@@ -24,7 +24,10 @@ reference's 'lstm' branch: the same constructor, parameter names
 HIP launch per layer (csrc/lstm.hip, mmf_lstm_forward / _backward); the
 time-parallel input projection and weight gradients are rocBLAS GEMMs.
 ``encode_sequences`` batches the LSTMs of several modalities into the same
-launches.  The 'gru' / 'cnn' / 'transformer' encoder types are not on the
+launches.  The recurrence's workgroups wait on each other: the library refuses
+a grid that cannot be co-resident, every launch gets a fresh timeout word, and
+a wait that gives up poisons its outputs with NaN; ``lstm_timed_out()`` /
+``check_lstm_timeouts()`` report such launches (one stream sync per check).  The 'gru' / 'cnn' / 'transformer' encoder types are not on the
 path and raise NotImplementedError.
 """
 
@@ -151,6 +154,11 @@ _LSTM_TIMEOUT: Dict[int, torch.Tensor] = {}
 
 
 def _timeout_flag(dev: torch.device) -> torch.Tensor:
+    """A fresh timeout word for one LSTM launch (the library zeroes it on the stream)."""
+    return torch.zeros(1, dtype=torch.int32, device=dev)
+
+
+def _timeout_acc(dev: torch.device) -> torch.Tensor:
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     t = _LSTM_TIMEOUT.get(idx)
     if t is None:
@@ -159,10 +167,29 @@ def _timeout_flag(dev: torch.device) -> torch.Tensor:
     return t
 
 
-def lstm_timed_out(device=None) -> bool:
-    """True if any LSTM launch on `device` gave up an inter-workgroup wait (results invalid)."""
+def _record_timeout(flag: torch.Tensor) -> None:
+    # device-side OR into the per-device accumulator: no host sync, graph-capturable
+    _timeout_acc(flag.device).bitwise_or_(flag)
+
+
+def lstm_timed_out(device=None, reset: bool = True) -> bool:
+    """True if any LSTM launch on `device` since the last check gave up an inter-workgroup
+    wait.  Such a launch also writes NaN into the values it never received, so its
+    encodings / gradients are NaN, never silently wrong.  Reading syncs the stream;
+    call it once per step (or per epoch) rather than per launch."""
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-    return bool(int(_timeout_flag(dev).item()))
+    acc = _timeout_acc(dev)
+    hit = bool(int(acc.item()))
+    if reset:
+        acc.zero_()
+    return hit
+
+
+def check_lstm_timeouts(device=None) -> None:
+    """Raise RuntimeError if an LSTM launch timed out since the last check (see lstm_timed_out)."""
+    if lstm_timed_out(device):
+        raise RuntimeError("mmfusion LSTM recurrence: an inter-workgroup wait timed out (the grid was not "
+                           "fully co-resident); the affected encodings / gradients are NaN")
 
 
 class _LstmLayersFunction(torch.autograd.Function):
@@ -188,12 +215,14 @@ class _LstmLayersFunction(torch.autograd.Function):
         gates = [torch.empty(B, T, 4 * H, dtype=torch.float32, device=dev) for _ in range(n)]
         sb = L.mmf_lstm_sync_bytes(B, H)
         sync = torch.empty(n, sb, dtype=torch.uint8, device=dev)
+        flag = _timeout_flag(dev)
         rc = L.mmf_lstm_forward(
             n, B, T, H, _nat.ptr_array([t.data_ptr() for t in xproj]), _nat.ptr_array([w.data_ptr() for w in w_hh]),
             _nat.ptr_array([t.data_ptr() for t in hs]), _nat.ptr_array([t.data_ptr() for t in cs]),
             _nat.ptr_array([t.data_ptr() for t in gates]), _nat.ptr_array([sync[i].data_ptr() for i in range(n)]),
-            _timeout_flag(dev).data_ptr(), _nat.stream_ptr(dev))
+            flag.data_ptr(), _nat.stream_ptr(dev))
         _nat.check(rc, "LSTM forward")
+        _record_timeout(flag)
         ctx.n = n
         ctx.save_for_backward(*xs, *w_ih, *w_hh, *hs, *cs, *gates)
         return tuple(hs)
@@ -210,12 +239,14 @@ class _LstmLayersFunction(torch.autograd.Function):
         dh = [None if d is None else _nat.f32c(d) for d in dhs]
         dgates = [torch.empty(B, T, 4 * H, dtype=torch.float32, device=dev) for _ in range(n)]
         sync = torch.empty(n, L.mmf_lstm_sync_bytes(B, H), dtype=torch.uint8, device=dev)
+        flag = _timeout_flag(dev)
         rc = L.mmf_lstm_backward(
             n, B, T, H, _nat.ptr_array([w.data_ptr() for w in w_hh]), _nat.ptr_array([t.data_ptr() for t in cs]),
             _nat.ptr_array([t.data_ptr() for t in gates]), _nat.ptr_array([0 if d is None else d.data_ptr() for d in dh]),
             _nat.ptr_array([t.data_ptr() for t in dgates]), _nat.ptr_array([sync[i].data_ptr() for i in range(n)]),
-            _timeout_flag(dev).data_ptr(), _nat.stream_ptr(dev))
+            flag.data_ptr(), _nat.stream_ptr(dev))
         _nat.check(rc, "LSTM backward")
+        _record_timeout(flag)
         grads: List[Optional[torch.Tensor]] = [None]
         for i in range(n):
             dg = dgates[i].view(B * T, 4 * H)

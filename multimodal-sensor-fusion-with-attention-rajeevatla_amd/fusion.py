@@ -10,7 +10,10 @@ build_fusion_model` (src/train.py:25) resolves here unchanged:
   * forward(modality_features, modality_mask=None, return_attention=False)
     -> logits | (logits, {"attention_maps", "fusion_weights"}), src/fusion.py:331-427,
     with the reference's errors raised before any kernel launch;
-  * compute_adaptive_weights(features, mask), src/fusion.py:429-479;
+  * compute_adaptive_weights(features, mask), src/fusion.py:429-479, differentiable
+    (gradients reach the features and gating_layers, as in the reference);
+  * modality masks are validated on the host before any launch: (B, M), or (1, M)
+    broadcast over the batch as the reference's indexing allows; other shapes raise;
   * build_fusion_model(fusion_type, modality_dims, num_classes, **kw), src/fusion.py:485-515.
 
 The whole fused step (projections, pairwise Q/K/V, QK^T softmax attn.V,
@@ -45,11 +48,30 @@ from attention import CrossModalAttention, _new_rng_state  # noqa: E402
 # --------------------------------------------------------------------------
 # Early fusion (plumbing, torch) and Late fusion (torch classifiers + HIP weighting).
 # --------------------------------------------------------------------------
-def _mask_or_ones(features, names, mask):
+def _check_mask(mask: torch.Tensor, batch: int, num_modalities: int, what: str) -> torch.Tensor:
+    """Validate a modality mask before its pointer reaches a kernel (the C-ABI reads a
+    contiguous (B, M) array).
+
+    The reference indexes ``modality_mask[:, idx]`` and broadcasts it against (B, .)
+    tensors (src/fusion.py:371-373,408,462-467), so a (B, M) mask and a (1, M) mask
+    (broadcast over the batch) work there and every other shape raises (IndexError
+    or a broadcast RuntimeError).  Here a (1, M) mask is expanded to (B, M); any
+    other shape raises RuntimeError before a launch.
+    """
+    if mask.dim() != 2 or mask.size(1) != num_modalities or mask.size(0) not in (batch, 1):
+        raise RuntimeError(f"{what}: modality_mask must have shape ({batch}, {num_modalities}) "
+                           f"(or (1, {num_modalities})), got {tuple(mask.shape)}")
+    if mask.size(0) != batch:
+        mask = mask.expand(batch, num_modalities)
+    return mask
+
+
+def _mask_or_ones(features, names, mask, what="fusion"):
     first = features[names[0]]
     if mask is None:
         return torch.ones(first.size(0), len(names), device=first.device, dtype=first.dtype)
-    return mask.to(device=first.device, dtype=first.dtype)
+    mask = mask.to(device=first.device, dtype=first.dtype)
+    return _check_mask(mask, first.size(0), len(names), what)
 
 
 class EarlyFusion(nn.Module):
@@ -76,7 +98,7 @@ class EarlyFusion(nn.Module):
     def forward(self, modality_features, modality_mask=None):
         if not self.modality_names:
             raise ValueError("No modalities configured for EarlyFusion.")
-        mask = _mask_or_ones(modality_features, self.modality_names, modality_mask)
+        mask = _mask_or_ones(modality_features, self.modality_names, modality_mask, "EarlyFusion")
         parts = []
         for i, name in enumerate(self.modality_names):
             if name not in modality_features:
@@ -146,7 +168,7 @@ class LateFusion(nn.Module):
     def forward(self, modality_features, modality_mask=None):
         if not self.modality_names:
             raise ValueError("No modalities configured for LateFusion.")
-        mask = _mask_or_ones(modality_features, self.modality_names, modality_mask)
+        mask = _mask_or_ones(modality_features, self.modality_names, modality_mask, "LateFusion")
         per: Dict[str, torch.Tensor] = {}
         for i, name in enumerate(self.modality_names):
             if name not in modality_features:
@@ -378,7 +400,8 @@ class HybridFusion(nn.Module):
         if modality_mask is None:
             modality_mask = torch.ones(batch_size, self.num_modalities, device=device, dtype=dtype)
         else:
-            modality_mask = modality_mask.to(device=device, dtype=dtype)
+            modality_mask = _check_mask(modality_mask.to(device=device, dtype=dtype), batch_size,
+                                        self.num_modalities, "HybridFusion")
         feats = []
         for name in self.modality_names:
             if name not in modality_features:
@@ -404,7 +427,10 @@ class HybridFusion(nn.Module):
     @torch.compiler.disable  # HIP library calls: opaque to TorchDynamo (runs eagerly)
     def compute_adaptive_weights(self, modality_features: Dict[str, torch.Tensor],
                                  modality_mask: torch.Tensor) -> torch.Tensor:
-        """src/fusion.py:429-479 on the device (gating scores -> masked softmax -> renormalise)."""
+        """src/fusion.py:429-479 on the device (gating scores -> masked softmax -> renormalise).
+
+        Differentiable like the reference's: gradients reach the features and
+        gating_layers through mmf_adaptive_weights_backward."""
         if modality_mask is None:
             raise ValueError("modality_mask must be provided for adaptive weighting.")
         device = modality_mask.device
@@ -412,23 +438,83 @@ class HybridFusion(nn.Module):
         for name in self.modality_names:
             if name not in modality_features:
                 raise KeyError(f"Missing aggregated features for modality '{name}'.")
-            feats.append(_nat.f32c(modality_features[name].to(device)))
+            feats.append(modality_features[name].to(device))
+        B = feats[0].size(0) if feats[0].dim() > 0 else 0
+        M, H = self.num_modalities, self.hidden_dim
+        for name, f in zip(self.modality_names, feats):
+            # gating_layers[m](feat) then cat(dim=1) needs (B, H) per modality (src/fusion.py:452-461)
+            if f.dim() != 2 or f.size(0) != B or f.size(1) != H:
+                raise RuntimeError(f"compute_adaptive_weights: features of '{name}' must have shape "
+                                   f"({B}, {H}), got {tuple(f.shape)}")
+        mask = _check_mask(modality_mask.to(dtype=torch.float32), B, M, "compute_adaptive_weights")
         _nat.require_device(modality_mask, "modality_mask")
-        L = _nat.lib()
-        B, M, H = feats[0].size(0), self.num_modalities, self.hidden_dim
-        mask = _nat.f32c(modality_mask)
-        gates = (_nat.Linear * M)()
-        for m, name in enumerate(self.modality_names):
+        gparams = []
+        for name in self.modality_names:
             layer = self.gating_layers[name]
-            gates[m] = _nat.Linear(layer.weight.data_ptr(), layer.bias.data_ptr())
-        out = torch.empty(B, M, dtype=torch.float32, device=device)
-        ws = torch.empty(L.mmf_adaptive_weights_workspace_bytes(B, M, H), dtype=torch.uint8, device=device)
+            gparams += [layer.weight, layer.bias]
+        return _AdaptiveWeightsFunction.apply(M, H, _nat.f32c(mask), *[_nat.f32c(f) for f in feats], *gparams)
+
+
+class _AdaptiveWeightsFunction(torch.autograd.Function):
+    """compute_adaptive_weights (src/fusion.py:429-479) forward and backward on HIP
+    (mmf_adaptive_weights / mmf_adaptive_weights_backward, csrc/head.hip).
+    inputs: M, H, mask (B, M), feats x M (B, H), then (gate weight, gate bias) x M."""
+
+    @staticmethod
+    def forward(ctx, M, H, mask, *tensors):
+        L = _nat.lib()
+        feats, gparams = tensors[:M], tensors[M:]
+        dev = mask.device
+        B = mask.size(0)
+        gates = (_nat.Linear * M)()
+        for m in range(M):
+            gates[m] = _nat.Linear(gparams[2 * m].data_ptr(), gparams[2 * m + 1].data_ptr())
+        out = torch.empty(B, M, dtype=torch.float32, device=dev)
+        ws = torch.empty(L.mmf_adaptive_weights_workspace_bytes(B, M, H), dtype=torch.uint8, device=dev)
         farr = _nat.ptr_array([f.data_ptr() for f in feats])
         rc = L.mmf_adaptive_weights(B, M, H, ctypes.cast(farr, ctypes.c_void_p), mask.data_ptr(),
                                     ctypes.cast(gates, ctypes.c_void_p), out.data_ptr(), ws.data_ptr(),
-                                    _nat.stream_ptr(device))
+                                    _nat.stream_ptr(dev))
         _nat.check(rc, "compute_adaptive_weights")
+        ctx.M, ctx.H = M, H
+        ctx.save_for_backward(mask, *tensors)
+        ctx.mark_non_differentiable(mask)
         return out
+
+    @staticmethod
+    def backward(ctx, dweights):
+        L = _nat.lib()
+        M, H = ctx.M, ctx.H
+        mask, *tensors = ctx.saved_tensors
+        feats, gparams = tensors[:M], tensors[M:]
+        dev = mask.device
+        B = mask.size(0)
+        dweights = _nat.f32c(dweights)
+        need_x = any(ctx.needs_input_grad[3:3 + M])
+        need_g = any(ctx.needs_input_grad[3 + M:])
+        dfeats = torch.empty(B, M, H, dtype=torch.float32, device=dev) if need_x else None
+        gates = (_nat.Linear * M)()
+        dgates = (_nat.Linear * M)()
+        ggrads: List[Optional[torch.Tensor]] = []
+        for m in range(M):
+            w, b = gparams[2 * m], gparams[2 * m + 1]
+            gates[m] = _nat.Linear(w.data_ptr(), b.data_ptr())
+            if need_g:
+                gw = torch.empty_like(w, dtype=torch.float32)
+                gb = torch.empty_like(b, dtype=torch.float32)
+                dgates[m] = _nat.Linear(gw.data_ptr(), gb.data_ptr())
+                ggrads += [gw, gb]
+            else:
+                ggrads += [None, None]
+        ws = torch.empty(L.mmf_adaptive_weights_workspace_bytes(B, M, H), dtype=torch.uint8, device=dev)
+        farr = _nat.ptr_array([f.data_ptr() for f in feats])
+        rc = L.mmf_adaptive_weights_backward(B, M, H, ctypes.cast(farr, ctypes.c_void_p), mask.data_ptr(),
+                                             ctypes.cast(gates, ctypes.c_void_p), dweights.data_ptr(),
+                                             _nat.ptr(dfeats), ctypes.cast(dgates, ctypes.c_void_p) if need_g
+                                             else None, ws.data_ptr(), _nat.stream_ptr(dev))
+        _nat.check(rc, "compute_adaptive_weights backward")
+        dx = [dfeats[:, m] if dfeats is not None and ctx.needs_input_grad[3 + m] else None for m in range(M)]
+        return (None, None, None, *dx, *ggrads)
 
 
 def build_fusion_model(fusion_type: str, modality_dims: Dict[str, int], num_classes: int,

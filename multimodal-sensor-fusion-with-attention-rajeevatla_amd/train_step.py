@@ -4,19 +4,28 @@ The reference trains one process on CPU (src/train.py:511-524, devices=1);
 this is the MI355X-native equivalent of its per-step work for the fusion
 model: forward -> CrossEntropyLoss(label_smoothing=0.05)
 (src/train.py:185-186,310) -> backward (parameter AND input grads) ->
-one RCCL all-reduce of the gradients (world > 1) -> AdamW
-(src/train.py:374-414).  Nothing else crosses GPUs: samples are independent
+one RCCL all-reduce of the gradients (world > 1) -> global-norm gradient
+clipping (gradient_clip_norm 1.0: config/base.yaml:74, src/train.py:416-430)
+-> AdamW (src/train.py:374-414; lr / weight decay from config/base.yaml:69-70).  Nothing else crosses GPUs: samples are independent
 (no op mixes samples), so the batch is sharded and the weights replicated.
 
 Layout: every parameter of the model is re-pointed into ONE contiguous fp32
 buffer and its gradient into another, so the exchange is a single all-reduce
 of the flat gradient and AdamW is one kernel over flat buffers.  All buffers
 are allocated up front; the per-step work is pure kernel enqueues on the
-current stream (fwd / CE / bwd / AdamW through include/mmfusion.h), so the
-step is captured once into a hipGraph and replayed.
+current stream (fwd / CE / bwd / clip / AdamW through include/mmfusion.h), so
+the step is captured once into a hipGraph and replayed.  The learning rate and
+the clip factor live in device scalars that the replayed kernels read, so an LR
+scheduler (set_lr / cosine_annealing_lr) needs no re-capture, and load_batch()
+copies each new batch into the static input buffers the graph reads.
+
+Not mirrored: Lightning's accumulate_grad_batches (config/base.yaml:75) -- one
+step here is one optimizer step over its batch.
 """
 
 from __future__ import annotations
+
+import math
 
 import ctypes
 import os
@@ -62,19 +71,36 @@ def allreduce_flat(grad: torch.Tensor, process_group=None, world: int = 1) -> No
         torch.distributed.all_reduce(grad, group=process_group)
 
 
+def cosine_annealing_lr(epoch: int, base_lr: float, t_max: int, eta_min: Optional[float] = None) -> float:
+    """torch.optim.lr_scheduler.CosineAnnealingLR in closed form, as the reference configures it
+    (T_max = max_epochs, eta_min = learning_rate / 100, stepped per epoch; src/train.py:394-402)."""
+    if eta_min is None:
+        eta_min = base_lr / 100
+    return eta_min + (base_lr - eta_min) * (1 + math.cos(math.pi * epoch / t_max)) / 2
+
+
 class HybridTrainStep:
+    """One optimizer step of the fusion model on the HIP path: fwd -> CE -> bwd ->
+    [all-reduce] -> clip -> AdamW.  Defaults are config/base.yaml's training keys."""
+
     def __init__(self, model: HybridFusion, feats: List[torch.Tensor], mask: torch.Tensor,
-                 labels: torch.Tensor, lr: float = 1e-3, weight_decay: float = 0.01,
+                 labels: torch.Tensor, lr: float = 1e-3, weight_decay: float = 1e-4,
                  betas=(0.9, 0.999), eps: float = 1e-8, label_smoothing: float = 0.05,
-                 process_group=None, input_grads: bool = True):
+                 gradient_clip_norm: float = 1.0, process_group=None, input_grads: bool = True):
         dev = mask.device
         _nat.require_device(mask, "training inputs")
         self.model = model.train()
         self.dev = dev
-        self.lr, self.wd, self.betas, self.eps = lr, weight_decay, betas, eps
+        self.wd, self.betas, self.eps = weight_decay, betas, eps
         self.smoothing = label_smoothing
+        self.clip_norm = gradient_clip_norm
         self.pg = process_group
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
+        if self.world > 1:
+            # every rank starts from the same seed (identical weights), so the dropout
+            # streams would repeat across ranks: fold the rank into the Philox key
+            rank = torch.distributed.get_rank(process_group)
+            model._rng_state[0] ^= rank * 0x9E3779B1
         # static input buffers (graph replays read these addresses)
         self.x = [_nat.f32c(f.to(dev)).clone() for f in feats]
         self.mask = _nat.f32c(mask).clone()
@@ -95,7 +121,11 @@ class HybridTrainStep:
         self.exp_avg = torch.zeros_like(self.flat)
         self.exp_avg_sq = torch.zeros_like(self.flat)
         self.step_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.lr_dev = torch.full((1,), float(lr), dtype=torch.float32, device=dev)
+        self.grad_norm = torch.zeros(1, dtype=torch.float32, device=dev)   # pre-clip total norm
+        self.clip_coef = torch.ones(1, dtype=torch.float32, device=dev)
         L = _nat.lib()
+        self.clip_ws = torch.empty(L.mmf_grad_clip_workspace_bytes(), dtype=torch.uint8, device=dev)
         self.saved = torch.empty(L.mmf_hybrid_saved_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
         self.ws = torch.empty(L.mmf_hybrid_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
         self.logits = torch.empty(d.batch, d.num_classes, dtype=torch.float32, device=dev)
@@ -108,6 +138,31 @@ class HybridTrainStep:
         self.xarr = _nat.ptr_array([x.data_ptr() for x in self.x])
         self.dxarr = _nat.ptr_array([t.data_ptr() for t in self.dx]) if input_grads else None
         self.graph: Optional[torch.cuda.CUDAGraph] = None
+
+    # ---------------------------------------------------------------- host controls
+    def set_lr(self, lr: float) -> None:
+        """New learning rate for the next steps (a device write; no re-capture)."""
+        self.lr_dev.fill_(float(lr))
+
+    @property
+    def lr(self) -> float:
+        return float(self.lr_dev.item())
+
+    def load_batch(self, feats: List[torch.Tensor], mask: torch.Tensor, labels: torch.Tensor) -> None:
+        """Copy the next batch into the static input buffers the (captured) step reads.
+        Shapes must equal the construction batch's (the plan and the graph are fixed)."""
+        if len(feats) != len(self.x):
+            raise ValueError(f"load_batch: expected {len(self.x)} modalities, got {len(feats)}")
+        for i, (dst, src) in enumerate(zip(self.x, feats)):
+            if tuple(src.shape) != tuple(dst.shape):
+                raise ValueError(f"load_batch: modality {i} has shape {tuple(src.shape)}, expected {tuple(dst.shape)}")
+        if tuple(mask.shape) != tuple(self.mask.shape) or tuple(labels.shape) != tuple(self.labels.shape):
+            raise ValueError(f"load_batch: mask / labels shapes {tuple(mask.shape)} / {tuple(labels.shape)}, "
+                             f"expected {tuple(self.mask.shape)} / {tuple(self.labels.shape)}")
+        for dst, src in zip(self.x, feats):
+            dst.copy_(src, non_blocking=True)
+        self.mask.copy_(mask, non_blocking=True)
+        self.labels.copy_(labels, non_blocking=True)
 
     # ---------------------------------------------------------------- stages
     def forward_backward(self) -> None:
@@ -133,15 +188,23 @@ class HybridTrainStep:
         allreduce_flat(self.grad, self.pg, self.world)
 
     def optimizer_step(self) -> None:
-        rc = _nat.lib().mmf_adamw_step(self.flat.numel(), self.flat.data_ptr(), self.grad.data_ptr(),
-                                       self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
-                                       self.step_dev.data_ptr(), self.lr, self.betas[0], self.betas[1],
-                                       self.eps, self.wd, 1.0 / self.world, _nat.stream_ptr(self.dev))
+        """Clip the (rank-averaged) gradient to gradient_clip_norm, then AdamW; both read
+        their scalars on the device."""
+        L = _nat.lib()
+        st = _nat.stream_ptr(self.dev)
+        gscale = 1.0 / self.world
+        rc = L.mmf_grad_clip_coef(self.grad.numel(), self.grad.data_ptr(), gscale, float(self.clip_norm),
+                                  self.grad_norm.data_ptr(), self.clip_coef.data_ptr(), self.clip_ws.data_ptr(), st)
+        _nat.check(rc, "gradient clipping")
+        rc = L.mmf_adamw_step_dev(self.flat.numel(), self.flat.data_ptr(), self.grad.data_ptr(),
+                                  self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), self.step_dev.data_ptr(),
+                                  self.lr_dev.data_ptr(), self.clip_coef.data_ptr(), self.betas[0], self.betas[1],
+                                  self.eps, self.wd, gscale, st)
         _nat.check(rc, "AdamW")
 
     # ---------------------------------------------------------------- driver
     def capture(self) -> None:
-        """Capture fwd+CE+bwd (and AdamW when single-process) into one hipGraph."""
+        """Capture fwd+CE+bwd (and clip + AdamW when single-process) into one hipGraph."""
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(s):

@@ -103,6 +103,20 @@ def test_dp_gloo_cpu_matches_full_batch(tmp_path):
     assert err <= TOL, float(err)
 
 
+def test_cosine_annealing_lr_matches_torch():
+    """train_step.cosine_annealing_lr == CosineAnnealingLR(T_max=max_epochs, eta_min=lr/100),
+    the reference's scheduler (src/train.py:394-402), stepped per epoch."""
+    sys.path.insert(0, PKG)
+    from train_step import cosine_annealing_lr
+    p = torch.zeros(1, requires_grad=True)
+    opt = torch.optim.AdamW([p], lr=1e-3)
+    sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=100, eta_min=1e-5)
+    for epoch in range(0, 101):
+        assert abs(opt.param_groups[0]["lr"] - cosine_annealing_lr(epoch, 1e-3, 100)) <= 1e-12
+        opt.step()
+        sched.step()
+
+
 def test_shard_batch_rejects_uneven():
     sys.path.insert(0, PKG)
     from train_step import shard_batch
@@ -126,8 +140,11 @@ def _gpu_rank(rank: int, world: int, port: int, out: str) -> None:
         feats, mask, labels = _global_batch()
         lf, lm, ll = shard_batch(feats, mask, labels, rank, world)
         model = _model().to(dev)
+        seed0 = int(model._rng_state[0].item())
         step = HybridTrainStep(model, [f.to(dev) for f in lf], lm.to(dev), ll.to(dev),
                                process_group=dist.group.WORLD)
+        # every rank starts from the same seed; the step folds the rank into the Philox key
+        assert int(model._rng_state[0].item()) == seed0 ^ (rank * 0x9E3779B1)
         step.forward_backward()
         step.allreduce()
         torch.cuda.synchronize(dev)

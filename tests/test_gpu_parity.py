@@ -98,7 +98,50 @@ def test_compute_adaptive_weights_direct(mods):
     params = {k: v.detach() for k, v in model.state_dict().items()}
     ref = adaptive_weights(params, ["a", "b", "c"], feats, mask)
     got = model.cuda().compute_adaptive_weights({m: v.cuda() for m, v in feats.items()}, mask.cuda())
-    assert close(got.cpu(), ref, RTOL, 1e-6)
+    assert close(got.detach().cpu(), ref, RTOL, 1e-6)
+
+
+def test_compute_adaptive_weights_backward(mods):
+    """compute_adaptive_weights is differentiable as the reference's is (src/fusion.py:429-479):
+    feature and gating_layers gradients vs autograd through the oracle, with masked
+    positions, fractional masks, an all-masked row (fallback branch) and a
+    single-modality row."""
+    fusion, _ = mods
+    from oracle.hybrid_cpu import adaptive_weights
+    torch.manual_seed(2)
+    names = ["a", "b", "c"]
+    model = fusion.HybridFusion({m: 4 for m in names}, num_classes=3, hidden_dim=16, num_heads=2)
+    feats = {m: torch.randn(6, 16) for m in names}
+    mask = torch.tensor([[1, 1, 1], [1, 0, 1], [0, 0, 0], [0.5, 1, 0], [0, 0, 1], [1, 1, 0.]])
+    G = torch.randn(6, 3)
+    params = {k: v.detach().clone().requires_grad_(True) for k, v in model.state_dict().items()}
+    fref = {m: v.clone().requires_grad_(True) for m, v in feats.items()}
+    ref = adaptive_weights(params, names, fref, mask)
+    (ref * G).sum().backward()
+    model = model.cuda()
+    fgot = {m: v.cuda().requires_grad_(True) for m, v in feats.items()}
+    got = model.compute_adaptive_weights(fgot, mask.cuda())
+    (got * G.cuda()).sum().backward()
+    torch.cuda.synchronize()
+    assert close(got.detach().cpu(), ref.detach(), RTOL, 1e-6)
+    for m in names:
+        assert close(fgot[m].grad.cpu(), fref[m].grad, RTOL, ATOL), m
+        for suffix in ("weight", "bias"):
+            layer = model.gating_layers[m]
+            assert close(getattr(layer, suffix).grad.cpu(), params[f"gating_layers.{m}.{suffix}"].grad,
+                         RTOL, ATOL), (m, suffix)
+    # the all-masked row takes the uniform fallback: no gradient reaches its scores
+    assert torch.all(fgot["a"].grad[2] == 0)
+
+
+def test_broadcast_mask_row(mods):
+    """A (1, M) mask broadcasts over the batch as the reference's indexing does."""
+    fusion, _ = mods
+    torch.manual_seed(3)
+    model = fusion.HybridFusion({"a": 4, "b": 4}, num_classes=3, hidden_dim=8, num_heads=2).cuda().eval()
+    feats = {"a": torch.randn(5, 4).cuda(), "b": torch.randn(5, 4).cuda()}
+    row = torch.tensor([[1.0, 0.0]]).cuda()
+    torch.testing.assert_close(model(feats, row), model(feats, row.expand(5, 2).contiguous()), rtol=0, atol=0)
 
 
 @pytest.mark.parametrize("case", CMA_CASES, ids=lambda c: c.name)

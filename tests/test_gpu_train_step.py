@@ -1,0 +1,117 @@
+"""The optimizer side of HybridTrainStep on the device:
+
+* global-norm gradient clipping (torch.nn.utils.clip_grad_norm_, max_norm =
+  config/base.yaml:74 gradient_clip_norm; Lightning applies it every step,
+  src/train.py:416-430) and AdamW (src/train.py:374-381) against torch's own
+  clip_grad_norm_ + torch.optim.AdamW on the same gradient;
+* the flat gradient's norm against the oracle's gradients;
+* a captured hipGraph step follows set_lr() (scheduler) and load_batch() (new
+  data) without re-capture: bit-identical to the same sequence run eagerly.
+"""
+from __future__ import annotations
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+M, B, L, D, H, HEADS, C = 3, 8, 6, 16, 16, 2, 5
+
+
+@pytest.fixture(scope="module")
+def mods(pkg_on_path):
+    if not torch.cuda.is_available():
+        pytest.fail("no ROCm device visible")
+    import fusion
+    import train_step
+    return fusion, train_step
+
+
+def _batch(seed):
+    g = torch.Generator().manual_seed(seed)
+    feats = [torch.randn(B, L, D, generator=g) for _ in range(M)]
+    mask = torch.ones(B, M)
+    mask[1, 0] = 0.0
+    mask[5, 2] = 0.5
+    labels = torch.randint(0, C, (B,), generator=g)
+    return feats, mask, labels
+
+
+def _model(fusion, dropout):
+    torch.manual_seed(3)
+    return fusion.HybridFusion({f"m{i}": D for i in range(M)}, hidden_dim=H, num_classes=C, num_heads=HEADS,
+                               dropout=dropout)
+
+
+@pytest.mark.parametrize("max_norm", [0.05, 1.0, 0.0])
+def test_clip_and_adamw_match_torch(mods, max_norm):
+    fusion, train_step = mods
+    from oracle.hybrid_cpu import hybrid_train_step
+    feats, mask, labels = _batch(1)
+    model = _model(fusion, 0.0).cuda()
+    step = train_step.HybridTrainStep(model, [f.cuda() for f in feats], mask.cuda(), labels.cuda(), lr=3e-3,
+                                      weight_decay=1e-4, gradient_clip_norm=max_norm)
+    p0 = step.flat.clone().cpu()
+    step.forward_backward()
+    g = step.grad.clone().cpu()
+    step.optimizer_step()
+    torch.cuda.synchronize()
+    # torch on the same gradient: clip_grad_norm_ then AdamW
+    p = p0.clone().requires_grad_(True)
+    p.grad = g.clone()
+    norm = torch.nn.utils.clip_grad_norm_([p], max_norm if max_norm > 0 else float("inf"))
+    opt = torch.optim.AdamW([p], lr=3e-3, weight_decay=1e-4)
+    opt.step()
+    assert abs(float(step.grad_norm.item()) - float(norm)) <= 1e-5 * float(norm)
+    coef = float(step.clip_coef.item())
+    want = min(1.0, max_norm / (float(norm) + 1e-6)) if max_norm > 0 else 1.0
+    assert abs(coef - want) <= 1e-6 * want
+    if max_norm == 0.05:
+        assert coef < 1.0   # clipping is active in this case
+    torch.testing.assert_close(step.flat.cpu(), p.detach(), rtol=1e-6, atol=1e-7)
+    # and the gradient itself is the reference's (parity tolerance)
+    names = model.modality_names
+    params = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in model.state_dict().items()}
+    for n, o in zip(step.plan.names, step.plan.offsets):   # pre-update weights
+        params[n] = p0[o:o + params[n].numel()].view_as(params[n]).clone().requires_grad_(True)
+    hybrid_train_step(params, names, {n: f.clone() for n, f in zip(names, feats)}, mask, labels, HEADS, 0.0)
+    ref_norm = torch.sqrt(sum((params[n].grad.double() ** 2).sum() for n in step.plan.names
+                              if params[n].grad is not None))
+    assert abs(float(step.grad_norm.item()) - float(ref_norm)) <= 1e-3 * float(ref_norm)
+
+
+def test_graph_follows_lr_and_new_batches(mods):
+    fusion, train_step = mods
+    a, b = _batch(2), _batch(3)
+
+    def run(graph: bool):
+        model = _model(fusion, 0.1).cuda()
+        model._rng_state.copy_(torch.tensor([1234, 0], dtype=torch.int64))
+        st = train_step.HybridTrainStep(model, [f.cuda() for f in a[0]], a[1].cuda(), a[2].cuda(), lr=1e-3)
+        if graph:
+            st.capture()
+            # capture() ran one warm-up forward/backward: realign the RNG with the eager run
+            model._rng_state.copy_(torch.tensor([1234, 0], dtype=torch.int64))
+        st.step()
+        st.set_lr(train_step.cosine_annealing_lr(50, 1e-3, 100))
+        st.load_batch([f.cuda() for f in b[0]], b[1].cuda(), b[2].cuda())
+        st.step()
+        torch.cuda.synchronize()
+        return st.flat.cpu(), float(st.loss.item()), st.lr
+
+    pg, lg, lrg = run(True)
+    pe, le, lre = run(False)
+    assert lrg == lre == pytest.approx(train_step.cosine_annealing_lr(50, 1e-3, 100))
+    assert le == lg
+    assert torch.equal(pg, pe)
+
+
+def test_load_batch_rejects_new_shapes(mods):
+    fusion, train_step = mods
+    feats, mask, labels = _batch(4)
+    st = train_step.HybridTrainStep(_model(fusion, 0.0).cuda(), [f.cuda() for f in feats], mask.cuda(),
+                                    labels.cuda())
+    with pytest.raises(ValueError, match="load_batch"):
+        st.load_batch([f[:4].cuda() for f in feats], mask[:4].cuda(), labels[:4].cuda())
+    with pytest.raises(ValueError, match="load_batch"):
+        st.load_batch([f.cuda() for f in feats[:2]], mask.cuda(), labels.cuda())

@@ -96,6 +96,36 @@ def test_errors_before_launch(mods):
         fusion.CrossModalAttention(4, 4, hidden_dim=10, num_heads=4)
 
 
+def test_mask_and_feature_shapes_checked_before_launch(mods):
+    """A mask that is not (B, M) / (1, M) -- the shapes the reference's indexing and
+    broadcasting accept (src/fusion.py:371-373,462-467) -- raises on the host, before
+    its pointer could reach a kernel; so do wrongly shaped compute_adaptive_weights
+    features (gating_layers[m](feat) then cat(dim=1), src/fusion.py:452-461)."""
+    fusion, _ = mods
+    model = fusion.HybridFusion({"video": 4, "imu": 4}, num_classes=3, hidden_dim=8, num_heads=2)
+    feats = {"video": torch.randn(3, 4), "imu": torch.randn(3, 4)}
+    for bad in (torch.ones(2), torch.ones(3), torch.ones(3, 1), torch.ones(3, 3), torch.ones(2, 2),
+                torch.ones(4, 2), torch.ones(3, 2, 1)):
+        with pytest.raises(RuntimeError, match="modality_mask must have shape"):
+            model(feats, bad)
+    late = fusion.LateFusion({"video": 4, "imu": 4}, num_classes=3, hidden_dim=8)
+    for bad in (torch.ones(2), torch.ones(3, 1), torch.ones(5, 2)):
+        with pytest.raises(RuntimeError, match="modality_mask must have shape"):
+            late(feats, bad)
+    agg = {"video": torch.randn(3, 8), "imu": torch.randn(3, 8)}
+    with pytest.raises(RuntimeError, match="modality_mask must have shape"):
+        model.compute_adaptive_weights(agg, torch.ones(3, 3))
+    for bad_feats in ({"video": torch.randn(3, 8), "imu": torch.randn(2, 8)},
+                      {"video": torch.randn(3, 8), "imu": torch.randn(3, 7)},
+                      {"video": torch.randn(3, 1, 8), "imu": torch.randn(3, 8)}):
+        with pytest.raises(RuntimeError, match="must have shape"):
+            model.compute_adaptive_weights(bad_feats, torch.ones(3, 2))
+    # a (1, M) mask broadcasts over the batch as in the reference: passes the checks
+    # and reaches the device requirement
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        model(feats, torch.ones(1, 2))
+
+
 def test_cpu_tensors_raise_no_fallback(mods):
     fusion, attention = mods
     model = fusion.HybridFusion({"video": 4, "imu": 4}, num_classes=3, num_heads=1, hidden_dim=8)
