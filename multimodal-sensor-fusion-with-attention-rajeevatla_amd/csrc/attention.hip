@@ -19,6 +19,7 @@
 // The head dimension is zero-padded to HDP (32 or 64); the MFMA contraction
 // order over d is permuted (lane half h owns d in [h*HDP/2, (h+1)*HDP/2)) so
 // each lane's operand is contiguous.
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -33,6 +34,34 @@ namespace {
 
 constexpr int NT = 256;
 
+#ifdef MMF_STAMPS
+// Diagnostic build only (make stamps): s_memtime at phase boundaries of the fused
+// backward, wave 0 of each workgroup; read back with mmf_stamps_read().  Never in
+// the product library.
+constexpr int STAMP_WG = 8192;
+__device__ unsigned long long g_mmf_stamps[STAMP_WG][10];
+#define MMF_STAMP(i)                                                                       \
+  {                                                                                        \
+    unsigned long long t_;                                                                 \
+    __builtin_amdgcn_sched_barrier(0);                                                     \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");            \
+    __builtin_amdgcn_sched_barrier(0);                                                     \
+    const int sid_ = blockIdx.y * gridDim.x + blockIdx.x;                                  \
+    if ((threadIdx.x & 63) == 0 && (threadIdx.x >> 6) == 0 && sid_ < STAMP_WG) g_mmf_stamps[sid_][i] = t_; \
+  }
+#define MMF_STAMP_ID()                                                                     \
+  {                                                                                        \
+    const unsigned hw_ = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));             \
+    const unsigned xcc_ = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (31 << 11));           \
+    const int sid_ = blockIdx.y * gridDim.x + blockIdx.x;                                  \
+    if ((threadIdx.x & 63) == 0 && (threadIdx.x >> 6) == 0 && sid_ < STAMP_WG)             \
+      g_mmf_stamps[sid_][9] = ((unsigned long long)xcc_ << 32) | hw_;                      \
+  }
+#else
+#define MMF_STAMP(i)
+#define MMF_STAMP_ID()
+#endif
+
 __device__ __forceinline__ float kmask_val(const AttnPair& P, int b, int key) {
   if (P.kmask_mode == 1) return P.kmask[(int64_t)b * P.kmask_ld];
   if (P.kmask_mode == 2) return P.kmask[(int64_t)b * P.kmask_ld + key];
@@ -41,10 +70,39 @@ __device__ __forceinline__ float kmask_val(const AttnPair& P, int b, int key) {
 
 // Load rows [r0, r0+ROWS) of a (B, L, ld) tensor's head slice into LDS [ROWS][LS]
 // (cols >= hd and rows >= L are zero).
-template <int ROWS, int HDP, int LS>
+// With 16-B rows (vec) every global load of the image is issued before the
+// first LDS write: written as one loop, the compiler put an s_waitcnt vmcnt(0)
+// in front of each ds_write (a full HBM round trip per 4 KB, 8 in a row for the
+// K and Q images of the fused backward: a third of its workgroup lifetime).
+template <int ROWS, int HDP, int LS, bool BATCHED = true>
 __device__ __forceinline__ void load_rows(float* S, const float* base, int L, int ld, int r0, int hd,
                                           bool vec) {
   constexpr int C4 = HDP / 4;
+  if (BATCHED && vec) {
+    static_assert((ROWS * C4) % NT == 0, "whole float4 slots per thread");
+    constexpr int PER = ROWS * C4 / NT;
+    constexpr int BATCH = PER < 4 ? PER : 4;   // 16 VGPRs of loads in flight (the long-key kernels
+                                               // call this inside their chunk loops, beside live sums)
+    static_assert(PER % BATCH == 0, "whole batches");
+#pragma unroll
+    for (int i0 = 0; i0 < PER; i0 += BATCH) {
+      float4 v[BATCH];
+#pragma unroll
+      for (int i = 0; i < BATCH; ++i) {
+        const int idx = threadIdx.x + (i0 + i) * NT;
+        const int r = idx / C4, c4 = (idx % C4) * 4;
+        const int row = r0 + r;
+        v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (row < L && c4 < hd) v[i] = *reinterpret_cast<const float4*>(base + (int64_t)row * ld + c4);
+      }
+#pragma unroll
+      for (int i = 0; i < BATCH; ++i) {
+        const int idx = threadIdx.x + (i0 + i) * NT;
+        *reinterpret_cast<float4*>(&S[(idx / C4) * LS + (idx % C4) * 4]) = v[i];
+      }
+    }
+    return;
+  }
   for (int idx = threadIdx.x; idx < ROWS * C4; idx += NT) {
     const int r = idx / C4, c4 = (idx % C4) * 4;
     const int row = r0 + r;
@@ -830,7 +888,7 @@ __global__ __launch_bounds__(NT, 4) void attn_pool_bwd_dk_kernel(const AttnArgs 
     const bool vq = (P.ldq % 4 == 0) && (hd % 4 == 0);
     for (int qbase = 0; qbase < Lq; qbase += QC) {
       __syncthreads();
-      load_rows<QC, HDP, LS>(Qs, P.q + (int64_t)b * Lq * P.ldq + col0, Lq, P.ldq, qbase, hd, vq);
+      load_rows<QC, HDP, LS, HDP == 32>(Qs, P.q + (int64_t)b * Lq * P.ldq + col0, Lq, P.ldq, qbase, hd, vq);
       for (int i = t; i < QC; i += NT) {
         const int qq = qbase + i;
         const float l = qq < Lq ? P.lse[bh * Lq + qq] : -INFINITY;
@@ -1120,7 +1178,7 @@ __global__ __launch_bounds__(NT, 4) void attn_poolL_dq_kernel(const AttnArgs A) 
   auto keep_of = [](uint32_t word, int r) { return ((word >> ((r & 3) + 8 * (r >> 2))) & 1u) != 0u; };
   auto stage = [&](int kbase) {
     __syncthreads();
-    load_rows<KC, HDP, LS>(Ks, kbase_ptr, Lk, P.ldk, kbase, hd, vk);
+    load_rows<KC, HDP, LS, HDP == 32>(Ks, kbase_ptr, Lk, P.ldk, kbase, hd, vk);
     for (int i = t; i < KC; i += NT) dpb[i] = kbase + i < Lk ? P.dpbar[bh * Lk + kbase + i] * gscale : 0.f;
     __syncthreads();
   };
@@ -1543,40 +1601,78 @@ MMF_CHAIN16(dk[dt], ds[r], Qs[(qt * 32 + acc_row(r, h)) * LS + dt * 32 + c])
 // keep-bit pass (VALU), one read of Q, K, LSE and the keep words, and the D
 // round trip.  LDS at hd <= 32: K and Q images, 2 x 18 KB (the dS^T quarters
 // reuse the K image) -> 4 workgroups per CU, whose load phases hide each other.
+// Everything one (pair, sample, head) item of the fused lean backward reads from
+// memory, issued at once into registers (one round trip instead of one per
+// image / side array): the K and Q head slices, dpbar, LSE, the keep words and
+// the sample's modality mask.
+template <int HDP>
+struct FusedLoads {
+  static constexpr int PER = PKC * (HDP / 4) / NT;   // float4 slots per thread and image
+  float4 k[PER], q[PER];
+  float gk, lse, msk;
+  uint4 kw;
+};
+
+template <int HDP>
+__device__ __forceinline__ void fused_issue_loads(const AttnArgs& A, const AttnPair& P, int b, int head, int c,
+                                                  FusedLoads<HDP>& L) {
+  constexpr int C4 = HDP / 4;
+  const int t = threadIdx.x, w = t >> 6;
+  const int hd = A.hd, col0 = head * hd;
+  const int Lq = P.Lq, Lk = P.Lk;
+  const float* kb = P.k + (int64_t)b * Lk * P.ldk + col0;
+  const float* qb = P.q + (int64_t)b * Lq * P.ldq + col0;
+#pragma unroll
+  for (int i = 0; i < FusedLoads<HDP>::PER; ++i) {
+    const int idx = t + i * NT;
+    const int r = idx / C4, c4 = (idx % C4) * 4;
+    L.k[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    L.q[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r < Lk && c4 < hd) L.k[i] = *reinterpret_cast<const float4*>(kb + (int64_t)r * P.ldk + c4);
+    if (r < Lq && c4 < hd) L.q[i] = *reinterpret_cast<const float4*>(qb + (int64_t)r * P.ldq + c4);
+  }
+  const int q = w * 32 + c;
+  const int qq = q < Lq ? q : Lq - 1;
+  const int64_t bh = (int64_t)b * A.heads + head;
+  const int64_t rowidx = bh * Lq + qq;
+  const float pdrop = A.drop_p;
+  const float inv_keep = pdrop > 0.f && pdrop < 1.f ? 1.f / (1.f - pdrop) : 1.f;
+  L.gk = t < Lk ? P.dpbar[bh * Lk + t] * inv_keep / (float)Lq : 0.f;   // PKC <= NT
+  L.lse = P.lse[rowidx];
+  L.kw = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+  if (P.keep_bits && pdrop > 0.f) L.kw = *reinterpret_cast<const uint4*>(P.keep_bits + rowidx * 4);
+  L.msk = P.kmask_mode == 1 ? P.kmask[(int64_t)b * P.kmask_ld] : 1.f;
+}
+
+// One (pair, sample, head) item of the fused lean backward from its issued loads;
+// Ks / Qs are [PKC][HDP + 4] LDS images (Ks doubles as the dS^T quarter image),
+// gk [PKC].  Called by every thread of the workgroup (it holds barriers).
 template <int HDP, bool BF>
-__global__ __launch_bounds__(NT, 4) void attn_pool_bwd_fused_lean(const AttnArgs A) {
+__device__ __forceinline__ void fused_lean_item(const AttnArgs& A, const AttnPair& P, int b, int head, float* Ks,
+                                                float* Qs, float* gk, int h, int c, const FusedLoads<HDP>& LD) {
   constexpr int LS = HDP + 4;
   constexpr int HALF = HDP / 2;
   constexpr int NDT = HDP / 32;
   constexpr int NKT = PKC / 32;
   constexpr int TS = 32 + 4;   // dS^T image row pitch (floats): one wave's 32 queries
+  constexpr int C4 = HDP / 4;
   static_assert(PKC * TS <= PKC * LS, "the dS^T quarter image reuses the K image");
-  __shared__ __attribute__((aligned(16))) float Ks[PKC * LS];   // K, then the dS^T quarters
-  __shared__ __attribute__((aligned(16))) float Qs[PKC * LS];
-  __shared__ __attribute__((aligned(16))) float gk[PKC];
   float* const dsT = Ks;
-
-  const AttnPair& P = A.p[blockIdx.y];
-  const int bid = blockIdx.x;
-  if (bid >= A.B * A.heads) return;
-  const int head = bid % A.heads, b = bid / A.heads;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, c = lane & 31;
+  const int t = threadIdx.x, w = t >> 6;
   const int hd = A.hd, col0 = head * hd;
   const int Lq = P.Lq, Lk = P.Lk, nkt = Lk >> 5;
   const int q = w * 32 + c;
   const bool qvalid = q < Lq;
   const int qq = qvalid ? q : Lq - 1;
-  const int64_t bh = (int64_t)b * A.heads + head;
-  const int64_t rowidx = bh * Lq + qq;
   const float pdrop = A.drop_p;
-  const float inv_keep = pdrop > 0.f && pdrop < 1.f ? 1.f / (1.f - pdrop) : 1.f;
-  const float inv_lq = 1.f / (float)Lq;
   const float scale = A.scale;
   float* qrow = P.dq + ((int64_t)b * Lq + qq) * P.ldq + col0;
   const int key = w * 32 + c;                 // dK phase: this wave's keys
   const bool kwave = w * 32 < Lk;
 
-  if (P.kmask_mode == 1 && P.kmask[(int64_t)b * P.kmask_ld] == 0.f) {
+  MMF_STAMP(0)
+  MMF_STAMP_ID()
+  if (LD.msk == 0.f) {
     // fully masked sample: P = 0 -> dQ = dK = 0
     if (qvalid)
       for (int d = h; d < hd; d += 2) qrow[d] = 0.f;
@@ -1584,15 +1680,19 @@ __global__ __launch_bounds__(NT, 4) void attn_pool_bwd_fused_lean(const AttnArgs
       for (int d = h; d < hd; d += 2) P.dk[((int64_t)b * Lk + key) * P.ldk + col0 + d] = 0.f;
     return;
   }
-  load_rows<PKC, HDP, LS>(Ks, P.k + (int64_t)b * Lk * P.ldk + col0, Lk, P.ldk, 0, hd, true);
-  load_rows<PKC, HDP, LS>(Qs, P.q + (int64_t)b * Lq * P.ldq + col0, Lq, P.ldq, 0, hd, true);
-  for (int k = t; k < PKC; k += NT) gk[k] = k < Lk ? P.dpbar[bh * Lk + k] * inv_keep * inv_lq : 0.f;
-  const float lse = P.lse[rowidx];
-  const float lse2 = (!qvalid || lse == -INFINITY) ? INFINITY : lse * LOG2E;
-  uint4 kw = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-  if (P.keep_bits && pdrop > 0.f) kw = *reinterpret_cast<const uint4*>(P.keep_bits + rowidx * 4);
-  const uint32_t kwa[4] = {kw.x, kw.y, kw.z, kw.w};
+#pragma unroll
+  for (int i = 0; i < FusedLoads<HDP>::PER; ++i) {
+    const int idx = t + i * NT;
+    const int off = (idx / C4) * LS + (idx % C4) * 4;
+    *reinterpret_cast<float4*>(&Ks[off]) = LD.k[i];
+    *reinterpret_cast<float4*>(&Qs[off]) = LD.q[i];
+  }
+  if (t < PKC) gk[t] = LD.gk;
+  const float lse2 = (!qvalid || LD.lse == -INFINITY) ? INFINITY : LD.lse * LOG2E;
+  const uint32_t kwa[4] = {LD.kw.x, LD.kw.y, LD.kw.z, LD.kw.w};
+  (void)pdrop;
   __syncthreads();
+  MMF_STAMP(1)
 
   float qf[HALF];
   load_frag_vec<HALF>(qf, Qs + q * LS + h * HALF);
@@ -1624,6 +1724,7 @@ __global__ __launch_bounds__(NT, 4) void attn_pool_bwd_fused_lean(const AttnArgs
     }
   }
   D += __shfl_xor(D, 32);
+  MMF_STAMP(2)
   // dS = P . (G - D), in place
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) {
@@ -1641,6 +1742,7 @@ __global__ __launch_bounds__(NT, 4) void attn_pool_bwd_fused_lean(const AttnArgs
       }
     }
   }
+  MMF_STAMP(3)
   // dQ = scale dS K (query on the lane; dS is the B operand)
   {
     f32x16 dq[NDT];
@@ -1666,6 +1768,7 @@ MMF_CHAIN16(dq[dt], Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], pr[kt][r])
         }
     }
   }
+  MMF_STAMP(4)
   // dK = scale dS^T Q (key on the lane), over four 32-query quarters of dS^T
   // staged in the K image (K is dead once every wave is past the dQ phase)
   f32x16 dk[NDT];
@@ -1703,6 +1806,7 @@ MMF_CHAIN16(dq[dt], Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], pr[kt][r])
       }
     }
   }
+  MMF_STAMP(5)
   if (!kwave) return;
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) {
@@ -1712,6 +1816,21 @@ MMF_CHAIN16(dq[dt], Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], pr[kt][r])
     for (int r = 0; r < 16; ++r)
       P.dk[((int64_t)b * Lk + w * 32 + acc_row(r, h)) * P.ldk + col0 + d] = dk[dt][r] * scale;
   }
+  MMF_STAMP(6)
+}
+
+template <int HDP, bool BF>
+__global__ __launch_bounds__(NT, 4) void attn_pool_bwd_fused_lean(const AttnArgs A) {
+  __shared__ __attribute__((aligned(16))) float Ks[PKC * (HDP + 4)];   // K, then the dS^T quarters
+  __shared__ __attribute__((aligned(16))) float Qs[PKC * (HDP + 4)];
+  __shared__ __attribute__((aligned(16))) float gk[PKC];
+  const int bid = blockIdx.x;
+  if (bid >= A.B * A.heads) return;
+  const int lane = threadIdx.x & 63;
+  const AttnPair& P = A.p[blockIdx.y];
+  FusedLoads<HDP> LD;
+  fused_issue_loads<HDP>(A, P, bid / A.heads, bid % A.heads, lane & 31, LD);
+  fused_lean_item<HDP, BF>(A, P, bid / A.heads, bid % A.heads, Ks, Qs, gk, lane >> 5, lane & 31, LD);
 }
 
 // "name<a, b>" -> "name<a, b, false|true>" (the rocprof name of the BF instantiation);
@@ -1724,7 +1843,10 @@ const char* with_bf(const char* base, bool bf) {
   if (slot.empty()) {
     std::string b(base);
     const size_t gt = b.rfind('>');
-    slot = gt == std::string::npos ? b : b.substr(0, gt) + (bf ? ", true>" : ", false>");
+    if (b.size() >= 2 && b.compare(b.size() - 2, 2, "<>") == 0)   // "name<>" -> "name<false|true>"
+      slot = b.substr(0, b.size() - 1) + (bf ? "true>" : "false>");
+    else
+      slot = gt == std::string::npos ? b : b.substr(0, gt) + (bf ? ", true>" : ", false>");
   }
   return slot.c_str();
 }
@@ -1832,7 +1954,8 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
         {"attn_poolL_dq_kernel<32>", "attn_poolL_dq_kernel<64>", "", ""}};
     const bool alt = kind == Kind::Prep ? prep_vec : (lean && kind <= Kind::PoolFused);
     const bool bf = math_bf16();
-    ProfLaunch prof_(st, with_bf(kNames[(int)kind][(alt ? 2 : 0) + (small ? 0 : 1)], bf), fl, by);
+    const char* kname = kNames[(int)kind][(alt ? 2 : 0) + (small ? 0 : 1)];
+    ProfLaunch prof_(st, with_bf(kname, bf), fl, by);
     switch (kind) {
       case Kind::PoolLse:
         if (small) { if (bf) hipLaunchKernelGGL((attn_poolL_lse_kernel<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_lse_kernel<32, false>), grid, dim3(NT), 0, st, a); }
@@ -1962,3 +2085,14 @@ hipError_t launch_attn_bwd(const AttnPair* pairs, int npairs, int B, int heads, 
 }
 
 }  // namespace mmf
+
+#ifdef MMF_STAMPS
+extern "C" int mmf_stamps_read(void* out, size_t bytes) {
+  if (bytes > sizeof(mmf::g_mmf_stamps)) bytes = sizeof(mmf::g_mmf_stamps);
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mmf::g_mmf_stamps), bytes) == hipSuccess ? 0 : 3;
+}
+extern "C" int mmf_stamps_clear(void) {
+  static unsigned long long zero[mmf::STAMP_WG][10];
+  return hipMemcpyToSymbol(HIP_SYMBOL(mmf::g_mmf_stamps), zero, sizeof(zero)) == hipSuccess ? 0 : 3;
+}
+#endif

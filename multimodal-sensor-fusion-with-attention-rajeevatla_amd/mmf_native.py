@@ -33,7 +33,9 @@ def matmul_precision() -> int:
     return PRECISION_MEDIUM if torch.get_float32_matmul_precision() == "medium" else PRECISION_HIGHEST
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "csrc", "libmmfusion.so")
+# MMF_LIB_PATH selects another in-tree build (e.g. csrc/libmmfusion_stamps.so, the
+# diagnostic phase-stamp build of scripts/attn_stamps.py)
+LIB_PATH = os.environ.get("MMF_LIB_PATH") or os.path.join(_HERE, "csrc", "libmmfusion.so")
 
 EXPORTED_SYMBOLS = (
     "mmf_hybrid_saved_bytes", "mmf_hybrid_workspace_bytes", "mmf_hybrid_forward",

@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""Phase shares of the fused attention backward from the diagnostic stamp build.
+
+Build: make -C <pkg>/csrc stamps.  Run (box):
+  MMF_LIB_PATH=<pkg>/csrc/libmmfusion_stamps.so MMF_ATTN_BWD=v1 python scripts/attn_stamps.py
+Stamps (s_memtime, wave 0 of every workgroup): 0 start, 1 K/Q images loaded, 2 S/P/D,
+3 dS, 4 dQ stored, 5 dK quarters, 6 dK stored.  Prints per-phase mean cycles, the
+workgroup lifetime, and how the start times of the workgroups on one CU are spread
+(lockstep or not).  Shares, not lengths: the stamps themselves cost cycles.
+"""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "multimodal-sensor-fusion-with-attention-rajeevatla_amd")
+sys.path.insert(0, PKG)
+sys.path.insert(0, ROOT)
+
+import mmf_native  # noqa: E402
+from fusion import HybridFusion  # noqa: E402
+from train_step import HybridTrainStep  # noqa: E402
+import bench  # noqa: E402
+
+
+def main():
+    w = bench.WORKLOADS["c2"]
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    names = [f"m{i}" for i in range(w["M"])]
+    model = HybridFusion({n: w["D"] for n in names}, hidden_dim=w["H"], num_classes=w["C"], num_heads=w["heads"],
+                         dropout=0.1).to(dev)
+    feats, mask, labels = bench.make_inputs(w, w["B"], 42, dev)
+    step = HybridTrainStep(model, feats, mask, labels)
+    L = mmf_native.lib()
+    L.mmf_stamps_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    for _ in range(3):
+        step.forward_backward()
+    torch.cuda.synchronize()
+    nwg = 6 * w["B"] * w["heads"]
+    buf = np.zeros((8192, 10), dtype=np.uint64)
+    assert L.mmf_stamps_read(buf.ctypes.data, buf.nbytes) == 0
+    st = buf[:nwg, :7].astype(np.int64)
+    hw = buf[:nwg, 9]
+    t0 = st[:, 0].min()
+    ph = np.diff(st, axis=1)
+    names_ph = ["load", "S/P/D", "dS", "dQ", "dK quarters", "dK store"]
+    out = {"workgroups": int(nwg),
+           "kernel_cycles": int(st[:, 6].max() - t0),
+           "wg_lifetime_mean": float((st[:, 6] - st[:, 0]).mean()),
+           "phase_mean_cycles": {n: float(ph[:, i].mean()) for i, n in enumerate(names_ph)},
+           "phase_share": {n: round(float(ph[:, i].mean() / (st[:, 6] - st[:, 0]).mean()), 3)
+                           for i, n in enumerate(names_ph)}}
+    # workgroups sharing a CU: HW_ID cu / sh / se fields + XCC id
+    hw32 = (hw & 0xFFFFFFFF).astype(np.int64)
+    xcc = (hw >> 32).astype(np.int64) & 0xF
+    cu_key = xcc * 4096 + ((hw32 >> 8) & 0xFFF)
+    starts = {}
+    for k, s0 in zip(cu_key, st[:, 0] - t0):
+        starts.setdefault(int(k), []).append(int(s0))
+    spreads = []
+    for k, v in starts.items():
+        v = sorted(v)
+        # first 4 residents of this CU: how far apart did they start?
+        if len(v) >= 4:
+            spreads.append(v[3] - v[0])
+    out["cus_seen"] = len(starts)
+    out["wgs_per_cu_mean"] = float(np.mean([len(v) for v in starts.values()]))
+    out["first4_start_spread_cycles_median"] = float(np.median(spreads)) if spreads else None
+    # start-time histogram in units of the mean lifetime
+    life = out["wg_lifetime_mean"]
+    hist = np.histogram((st[:, 0] - t0) / life, bins=12)[0].tolist()
+    out["start_hist_per_lifetime"] = hist
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
