@@ -1288,7 +1288,12 @@ __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(cons
   const int64_t bh = (int64_t)b * A.heads + head;
   float* pbar = P.pbar + bh * Lk;
 
-  if (P.kmask_mode == 1 && P.kmask[(int64_t)b * P.kmask_ld] == 0.f) {
+  // the sample mask, this wave's first query fragment and the K image in one round trip
+  const float msk = P.kmask_mode == 1 ? P.kmask[(int64_t)b * P.kmask_ld] : 1.f;
+  float qf[HALF];   // the query fragment of this wave's current tile (reloaded at the end of an iteration)
+  load_frag_vec<HALF>(qf, P.q + ((int64_t)b * Lq + min(w * 32 + c, Lq - 1)) * P.ldq + col0 + h * HALF);
+  load_rows<PKC, HDP, LS>(Ks, P.k + (int64_t)b * Lk * P.ldk + col0, Lk, P.ldk, 0, hd, true);
+  if (msk == 0.f) {
     for (int k = t; k < Lk; k += NT) pbar[k] = 0.f;
     if (P.pbarT)
       for (int k = t; k < Lk; k += NT) P.pbarT[((int64_t)b * Lk + k) * A.heads + head] = 0.f;
@@ -1298,7 +1303,6 @@ __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(cons
         *reinterpret_cast<uint4*>(P.keep_bits + (bh * Lq + q) * 4) = make_uint4(0, 0, 0, 0);
     return;
   }
-  load_rows<PKC, HDP, LS>(Ks, P.k + (int64_t)b * Lk * P.ldk + col0, Lk, P.ldk, 0, hd, true);
   __syncthreads();
 
   const float c2 = A.scale * LOG2E;
@@ -1310,8 +1314,6 @@ __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(cons
     const int q = qt * 32 + c;
     const bool qvalid = q < Lq;
     const int qq = qvalid ? q : Lq - 1;
-    float qf[HALF];
-    load_frag_vec<HALF>(qf, P.q + ((int64_t)b * Lq + qq) * P.ldq + col0 + h * HALF);
     float sv[NKT][16];
     float mx = -INFINITY;
 #pragma unroll
@@ -1367,6 +1369,8 @@ __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(cons
         *reinterpret_cast<uint4*>(P.keep_bits + rowidx * 4) =
             make_uint4(words[0], NKT > 1 ? words[1] : 0u, NKT > 2 ? words[2] : 0u, NKT > 3 ? words[3] : 0u);
     }
+    if ((qt + 4) * 32 < Lq)
+      load_frag_vec<HALF>(qf, P.q + ((int64_t)b * Lq + min((qt + 4) * 32 + c, Lq - 1)) * P.ldq + col0 + h * HALF);
   }
   if ((c & 1) == 0) {
 #pragma unroll

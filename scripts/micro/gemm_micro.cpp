@@ -77,6 +77,16 @@ int main() {
       one.push_back(j);
     }
     run("dZ_1src", one, MODE_RK, MODE_KR, 3.0 * 4 * 2 * R * H * H);
+    // probe: the same FLOPs with every row tile reading the SAME 128 A rows (L2-resident):
+    // if this is much faster, the real launch is bound by streaming A from HBM
+    {
+      std::vector<GemmJob> l2 = one;
+      for (auto& j : l2) j.src[0].a.row_div = 128;   // row r -> stored row r / 128: 256 distinct rows
+      run("dZ_Al2", l2, MODE_RK, MODE_KR, 3.0 * 4 * 2 * R * H * H);
+      std::vector<GemmJob> l2b = one;
+      for (auto& j : l2b) j.src[0].a.row_div = 32768;
+      run("dZ_Al2one", l2b, MODE_RK, MODE_KR, 3.0 * 4 * 2 * R * H * H);
+    }
     // RK B operand (W^T stored [j][kk]) instead of KR
     run("dZ_1srcRK", one, MODE_RK, MODE_RK, 3.0 * 4 * 2 * R * H * H);
     // the real epilogue: ReLU gate from P_m (EPI_GATE) + row-broadcast c_m / L (EPI_ROWADD)
