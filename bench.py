@@ -181,6 +181,9 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=5)
+    ap.add_argument("--dump-launches", default=None,
+                    help="write every profiled launch (stage, kernel, ms, flops, bytes) of the last profile step "
+                         "to this JSON file")
     ap.add_argument("--precision", default="highest", choices=["highest", "medium"],
                     help="torch.set_float32_matmul_precision for the run: 'highest' = fp32 MFMA (the "
                          "fp32-parity headline), 'medium' = bf16 MFMA operands, fp32 accumulate "
@@ -220,6 +223,12 @@ def main():
     for _ in range(args.profile_steps):
         trainer.forward_backward()
     stages, launches = mmf_native.profile_end()
+    if args.dump_launches and rank == 0:
+        per = len(launches) // max(1, args.profile_steps)
+        with open(args.dump_launches, "w") as f:
+            json.dump([{"stage": st_, "kernel": k_, "ms": ms_, "gflop": fl_ / 1e9, "mb": by_ / 1e6,
+                        "tflops": fl_ / (ms_ * 1e-3) / 1e12 if ms_ > 0 else None}
+                       for st_, k_, ms_, fl_, by_ in launches[-per:]], f, indent=1)
     per_stage = {}
     for name, ms in stages:
         t, n = per_stage.get(name, (0.0, 0))

@@ -130,7 +130,14 @@ inline void add_src(GemmJob& j, Operand a, Operand b, int K) {
 // long contractions (a launch of 8 128x128-output jobs at B*L = 32768 rows is
 // 512 workgroups, 2 per CU; the slabs of all 15 such jobs are 63 MB) and of
 // >= 64 rows for short ones (B = 256 rows -> 4 slabs: a short serial chain).
-inline void split_rows(int rows, int& nsplit, int& kchunk) {
+inline void split_rows(int rows, int& nsplit, int& kchunk, int hint = 0) {
+  if (hint > 0) {
+    // a chosen split count (launch-level wave sizing, plan_wgrads): slabs of >= 32 rows
+    kchunk = (rows + hint - 1) / hint;
+    kchunk = (kchunk + 31) & ~31;
+    nsplit = (rows + kchunk - 1) / kchunk;
+    return;
+  }
   int chunk = rows / 4;
   if (chunk > 512) chunk = 512;
   if (chunk < 64) chunk = 64;
@@ -155,6 +162,7 @@ inline size_t slab_bytes(int M, int N, int rows) {
 struct WgradPlan {
   std::vector<GemmJob> jobs;
   std::vector<ReduceJob> reds;
+  int split_hint = 0;   // > 0: split count of the next plan_wgrad (set per job by the caller)
 };
 
 // has_db: the layer has a bias whose gradient (row sums) is produced too.  It is
@@ -163,7 +171,7 @@ struct WgradPlan {
 inline void plan_wgrad(WgradPlan& wp, Bump& ws, int M, int N, int rows, Operand a, Operand b,
                        float* out_w, float* out_b, bool has_db, float alpha = 1.f) {
   int nsplit, kchunk;
-  split_rows(rows, nsplit, kchunk);
+  split_rows(rows, nsplit, kchunk, wp.split_hint);
   float* part = ws.take<float>((size_t)nsplit * M * N);
   float* part_db = has_db ? ws.take<float>((size_t)nsplit * M) : nullptr;
   GemmJob j = make_job(M, N, part, N, EPI_PARTIAL);

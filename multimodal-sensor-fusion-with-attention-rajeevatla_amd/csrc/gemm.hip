@@ -809,7 +809,7 @@ __global__ __launch_bounds__(NT) void gemm_generic_kernel(const GemmArgs args) {
 
 // ------------------------------------------------------------------ split-K reduce
 struct ReduceArgs {
-  ReduceJob j[16];
+  ReduceJob j[48];
   int32_t njobs;
 };
 
@@ -1022,6 +1022,8 @@ hipError_t launch_wsr(const GemmJob* jobs, int njobs, hipStream_t st) {
 
 }  // namespace
 
+int device_cu_count() { return cu_count(); }
+
 hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, float drop_p,
                        const RngSnap* rng, hipStream_t st) {
   {
@@ -1144,7 +1146,7 @@ hipError_t launch_reduce(const ReduceJob* jobs, int njobs, hipStream_t st) {
     int n = 0;
     int64_t maxmn = 0;
     int maxbatch = 1;
-    while (done < njobs && n < 16) {
+    while (done < njobs && n < 48) {
       a.j[n] = jobs[done++];
       if (a.j[n].nbatch < 1) a.j[n].nbatch = 1;
       if (a.j[n].nbatch > maxbatch) maxbatch = a.j[n].nbatch;

@@ -167,6 +167,29 @@ void plan_wgrads(const mmf_hybrid_desc* d, const float* const* x, const float* m
   const bool pool = use_pool(d);
   static const mmf_hybrid_grads kNull = {};
   const mmf_hybrid_grads* g = G ? G : &kNull;
+  // Split counts of the long (B*L-row) contractions, sized per launch: launch_gemm packs
+  // GEMM_MAX_GROUPS of them per launch (longest slabs first), and a launch should be about
+  // one wave of its 3-per-CU workgroups.  Full launches take slots / GEMM_MAX_GROUPS slabs
+  // per job (512 rows at C2); the r jobs of a remainder launch take slots / r (C2: 15 jobs =
+  // 12 + 3 -> the last 3 are split 256 ways instead of leaving 3/4 of the GPU idle).
+  const int kBigRows = 4096;
+  int nbig = 0;
+  for (int p = 0; p < d->num_pairs; ++p) {
+    const int lq = Lm(d, d->pair_q[p]), lk = Lm(d, d->pair_k[p]);
+    if (!pool) nbig += (B * lq >= kBigRows) + (B * lk >= kBigRows);
+    nbig += (B * lq >= kBigRows) + (B * lk >= kBigRows);
+  }
+  for (int m = 0; m < M; ++m) nbig += (B * Lm(d, m) >= kBigRows);
+  const int slots = 3 * device_cu_count();
+  const int rem = nbig % GEMM_MAX_GROUPS, nfull = nbig - rem;
+  int bi = 0;
+  auto hint = [&](int rows) {
+    if (rows < kBigRows) return 0;
+    const int per = bi++ < nfull ? GEMM_MAX_GROUPS : rem;
+    int sp = slots / per;
+    if (const char* e = getenv("MMF_WGRAD_SPLIT_CAP")) sp = std::min(sp, std::max(1, atoi(e)));
+    return std::max(1, std::min(sp, 256));
+  };
   plan_wgrad(wp, bw, C, H, B, opnd(dlogits, C), opnd(s.h1, H), g->cls2.w, g->cls2.b);
   plan_wgrad(wp, bw, H, H, B, opnd(w.dz1, H), opnd(s.fused, H), g->cls1.w, g->cls1.b);
   // gating_layers[m]: dscore[:, m]^T pooled[:, m, :]
@@ -187,16 +210,23 @@ void plan_wgrads(const mmf_hybrid_desc* d, const float* const* x, const float* m
       plan_wgrad_batched(wp, bw, hd, H, B, dob, u, g->v[p].w, nh, hd, H, hd * H);
       plan_wgrad_batched(wp, bw, hd, 1, B, dob, rr, g->v[p].b, nh, hd, 1, hd);
     } else {
+      wp.split_hint = hint(B * lq);
       plan_wgrad(wp, bw, H, H, B * lq, opnd(cq, M * H, lq), opnd(s.O[p], H), g->o[p].w, g->o[p].b,
                  1.f / (float)lq);
+      wp.split_hint = hint(B * lk);
       plan_wgrad(wp, bw, H, H, B * lk, opnd(w.dV[p], H), opnd(s.P[k], H), g->v[p].w, g->v[p].b);
     }
+    wp.split_hint = hint(B * lq);
     plan_wgrad(wp, bw, H, H, B * lq, opnd(w.dQ[p], H), opnd(s.P[q], H), g->q[p].w, g->q[p].b);
+    wp.split_hint = hint(B * lk);
     plan_wgrad(wp, bw, H, H, B * lk, opnd(w.dK[p], H), opnd(s.P[k], H), g->k[p].w, g->k[p].b);
+    wp.split_hint = 0;
   }
   for (int m = 0; m < M; ++m) {
     const int L = Lm(d, m), D = d->in_dim[m];
+    wp.split_hint = hint(B * L);
     plan_wgrad(wp, bw, H, D, B * L, opnd(w.dZ[m], H), opnd(s.Xd[m], D), g->proj[m].w, g->proj[m].b);
+    wp.split_hint = 0;
   }
 }
 

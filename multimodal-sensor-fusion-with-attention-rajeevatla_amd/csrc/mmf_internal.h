@@ -118,8 +118,8 @@ struct GemmGroup {
   int32_t seg_rows;        // rows per segment for operands with seg_stride (a tile never straddles two)
 };
 
-constexpr int GEMM_MAX_GROUPS = 12;
-constexpr int GEMM_MAX_SRCS = 24;
+constexpr int GEMM_MAX_GROUPS = 24;   // kernel arguments up to ~6.3 KB (measured fine on gfx950)
+constexpr int GEMM_MAX_SRCS = 32;
 
 struct GemmArgs {
   GemmGroup g[GEMM_MAX_GROUPS];
@@ -145,6 +145,7 @@ struct GemmJob {
 // register-staged generic kernel.
 hipError_t launch_gemm(const GemmJob* jobs, int njobs, int amode, int bmode, float drop_p,
                        const RngSnap* rng, hipStream_t st);
+int device_cu_count();   // CUs of the current device (cached)
 
 // X'_m[r][c] = X_m[r][c] * mask[(r / L_m) * M + m] * (keep(site_m, r*D_m + c) ? 1/(1-p) : 0)
 // (the masked, input-dropped modality features of src/fusion.py:364-373,
