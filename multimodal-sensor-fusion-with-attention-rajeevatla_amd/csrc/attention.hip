@@ -1729,25 +1729,9 @@ __device__ __forceinline__ void fused_lean_item(const AttnArgs& A, const AttnPai
   }
   D += __shfl_xor(D, 32);
   MMF_STAMP(2)
-  // dS = P . (G - D), in place
-#pragma unroll
-  for (int kt = 0; kt < NKT; ++kt) {
-    if (kt < nkt) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 gv = *reinterpret_cast<const float4*>(gk + kt * 32 + 8 * g + 4 * h);
-        const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int r = 4 * g + j;
-          const bool keep = (kwa[kt] >> (8 * g + 4 * h + j)) & 1u;
-          pr[kt][r] = pr[kt][r] * ((keep ? gg[j] : 0.f) - D);
-        }
-      }
-    }
-  }
   MMF_STAMP(3)
-  // dQ = scale dS K (query on the lane; dS is the B operand)
+  // dQ = scale dS K (query on the lane; dS is the B operand); dS = P . (G - D) is formed
+  // tile by tile, right before its chain, so that VALU work overlaps the previous chain
   {
     f32x16 dq[NDT];
 #pragma unroll
@@ -1755,6 +1739,17 @@ __device__ __forceinline__ void fused_lean_item(const AttnArgs& A, const AttnPai
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
       if (kt < nkt) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 gv = *reinterpret_cast<const float4*>(gk + kt * 32 + 8 * g + 4 * h);
+          const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int r = 4 * g + j;
+            const bool keep = (kwa[kt] >> (8 * g + 4 * h + j)) & 1u;
+            pr[kt][r] = pr[kt][r] * ((keep ? gg[j] : 0.f) - D);
+          }
+        }
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt)
 MMF_CHAIN16(dq[dt], Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], pr[kt][r])
