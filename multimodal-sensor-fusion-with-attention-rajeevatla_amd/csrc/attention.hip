@@ -34,33 +34,6 @@ namespace {
 
 constexpr int NT = 256;
 
-#ifdef MMF_STAMPS
-// Diagnostic build only (make stamps): s_memtime at phase boundaries of the fused
-// backward, wave 0 of each workgroup; read back with mmf_stamps_read().  Never in
-// the product library.
-constexpr int STAMP_WG = 8192;
-__device__ unsigned long long g_mmf_stamps[STAMP_WG][10];
-#define MMF_STAMP(i)                                                                       \
-  {                                                                                        \
-    unsigned long long t_;                                                                 \
-    __builtin_amdgcn_sched_barrier(0);                                                     \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");            \
-    __builtin_amdgcn_sched_barrier(0);                                                     \
-    const int sid_ = blockIdx.y * gridDim.x + blockIdx.x;                                  \
-    if ((threadIdx.x & 63) == 0 && (threadIdx.x >> 6) == 0 && sid_ < STAMP_WG) g_mmf_stamps[sid_][i] = t_; \
-  }
-#define MMF_STAMP_ID()                                                                     \
-  {                                                                                        \
-    const unsigned hw_ = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));             \
-    const unsigned xcc_ = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (31 << 11));           \
-    const int sid_ = blockIdx.y * gridDim.x + blockIdx.x;                                  \
-    if ((threadIdx.x & 63) == 0 && (threadIdx.x >> 6) == 0 && sid_ < STAMP_WG)             \
-      g_mmf_stamps[sid_][9] = ((unsigned long long)xcc_ << 32) | hw_;                      \
-  }
-#else
-#define MMF_STAMP(i)
-#define MMF_STAMP_ID()
-#endif
 
 __device__ __forceinline__ float kmask_val(const AttnPair& P, int b, int key) {
   if (P.kmask_mode == 1) return P.kmask[(int64_t)b * P.kmask_ld];
@@ -1674,6 +1647,7 @@ __device__ __forceinline__ void fused_lean_item(const AttnArgs& A, const AttnPai
   const int key = w * 32 + c;                 // dK phase: this wave's keys
   const bool kwave = w * 32 < Lk;
 
+  MMF_STAMP_RT(7)
   MMF_STAMP(0)
   MMF_STAMP_ID()
   if (LD.msk == 0.f) {
@@ -1816,6 +1790,7 @@ MMF_CHAIN16(dq[dt], Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], pr[kt][r])
       P.dk[((int64_t)b * Lk + w * 32 + acc_row(r, h)) * P.ldk + col0 + d] = dk[dt][r] * scale;
   }
   MMF_STAMP(6)
+  MMF_STAMP_RT(8)
 }
 
 template <int HDP, bool BF>
@@ -2085,8 +2060,21 @@ hipError_t launch_attn_bwd(const AttnPair* pairs, int npairs, int B, int heads, 
 
 }  // namespace mmf
 
+// Occupancy the runtime reports for the C2 attention kernels (blocks per CU at 256
+// threads): [0] fused backward, [1] pooled forward.  Diagnostic (scripts/attn_stamps.py).
+extern "C" int mmf_attn_occupancy(int* out) {
+  int a = 0, b = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, mmf::attn_pool_bwd_fused_lean<32, false>, 256, 0) !=
+          hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, mmf::attn_pool_fwd_lean<32, false>, 256, 0) != hipSuccess)
+    return 3;
+  out[0] = a;
+  out[1] = b;
+  return 0;
+}
+
 #ifdef MMF_STAMPS
-extern "C" int mmf_stamps_read(void* out, size_t bytes) {
+extern "C" int mmf_stamps_read(void* out, size_t bytes) {   // fused attention backward
   if (bytes > sizeof(mmf::g_mmf_stamps)) bytes = sizeof(mmf::g_mmf_stamps);
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(mmf::g_mmf_stamps), bytes) == hipSuccess ? 0 : 3;
 }

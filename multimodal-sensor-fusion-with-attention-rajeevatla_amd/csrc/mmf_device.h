@@ -142,4 +142,57 @@ __device__ __forceinline__ uint32_t keep_tile16(const RngSnap& s, uint32_t site,
   return mine;
 }
 
+#ifdef MMF_STAMPS
+// Diagnostic build only (make stamps): s_memtime at phase boundaries, wave 0 of each
+// workgroup, into a per-translation-unit buffer (no relocatable device code) that
+// the TU's own reader copies out (mmf_stamps_read: attention.hip, mmf_tail_stamps_read:
+// tail.hip).  Never in the product library.
+namespace {
+constexpr int STAMP_WG = 8192;
+__device__ unsigned long long g_mmf_stamps[STAMP_WG][10];
+}  // namespace
+#define MMF_STAMP(i)                                                                       \
+  {                                                                                        \
+    unsigned long long t_;                                                                 \
+    __builtin_amdgcn_sched_barrier(0);                                                     \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");            \
+    __builtin_amdgcn_sched_barrier(0);                                                     \
+    const int sid_ = blockIdx.y * gridDim.x + blockIdx.x;                                  \
+    if ((threadIdx.x & 63) == 0 && (threadIdx.x >> 6) == 0 && sid_ < STAMP_WG) g_mmf_stamps[sid_][i] = t_; \
+  }
+// s_memrealtime (constant 100 MHz) into slot i: with two s_memtime stamps it gives the
+// shader clock the workgroup ran at (MI355X_MICROARCH.md, DVFS item 6)
+#define MMF_STAMP_RT(i)                                                                    \
+  {                                                                                        \
+    unsigned long long t_;                                                                 \
+    __builtin_amdgcn_sched_barrier(0);                                                     \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");        \
+    __builtin_amdgcn_sched_barrier(0);                                                     \
+    const int sid_ = blockIdx.y * gridDim.x + blockIdx.x;                                  \
+    if ((threadIdx.x & 63) == 0 && (threadIdx.x >> 6) == 0 && sid_ < STAMP_WG) g_mmf_stamps[sid_][i] = t_; \
+  }
+#define MMF_STAMP_ID()                                                                     \
+  {                                                                                        \
+    const unsigned hw_ = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));             \
+    const unsigned xcc_ = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (31 << 11));           \
+    const int sid_ = blockIdx.y * gridDim.x + blockIdx.x;                                  \
+    if ((threadIdx.x & 63) == 0 && (threadIdx.x >> 6) == 0 && sid_ < STAMP_WG)             \
+      g_mmf_stamps[sid_][9] = ((unsigned long long)xcc_ << 32) | hw_;                      \
+  }
+#else
+#define MMF_STAMP(i)
+// s_memrealtime (constant 100 MHz) into slot i: with two s_memtime stamps it gives the
+// shader clock the workgroup ran at (MI355X_MICROARCH.md, DVFS item 6)
+#define MMF_STAMP_RT(i)                                                                    \
+  {                                                                                        \
+    unsigned long long t_;                                                                 \
+    __builtin_amdgcn_sched_barrier(0);                                                     \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");        \
+    __builtin_amdgcn_sched_barrier(0);                                                     \
+    const int sid_ = blockIdx.y * gridDim.x + blockIdx.x;                                  \
+    if ((threadIdx.x & 63) == 0 && (threadIdx.x >> 6) == 0 && sid_ < STAMP_WG) g_mmf_stamps[sid_][i] = t_; \
+  }
+#define MMF_STAMP_ID()
+#endif
+
 }  // namespace mmf

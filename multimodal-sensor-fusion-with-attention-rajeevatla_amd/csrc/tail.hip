@@ -164,6 +164,8 @@ __global__ __launch_bounds__(NT) void tail_pair_fwd_kernel(const TailArgs a) {
   const int t = threadIdx.x;
   const int H = a.H, nh = a.heads, hd = a.hd, Lk = P.Lk, H4 = H >> 2;
   const int ncol = nh * H4;
+  MMF_STAMP(0)
+  MMF_STAMP_ID()
   for (int si = 0; si < S; ++si) {
     float* us = u_s + si * nh * H;
     if (si >= ns) {   // no sample: zero inputs keep the batched GEMVs finite
@@ -181,6 +183,7 @@ __global__ __launch_bounds__(NT) void tail_pair_fwd_kernel(const TailArgs a) {
       r_s[si * MAXHEADS + t] = s;
       P.r[(int64_t)b * nh + t] = s;
     }
+    MMF_STAMP(1)
     // U: tasks = (head, float4 column); RG row groups split the Lk keys
     const float* pk = P.Pk + (int64_t)b * Lk * H;
     for (int task0 = 0; task0 < ncol; task0 += NT) {
@@ -221,9 +224,11 @@ __global__ __launch_bounds__(NT) void tail_pair_fwd_kernel(const TailArgs a) {
     }
   }
   __syncthreads();
+  MMF_STAMP(2)
   // Obar = U W_v^T (per head) + r b_v;  Abar = Obar W_o^T + b_o
   gemv_nt_s<S>(u_s, nh * H, hd, H, P.Wv, H, H, v1, TH);
   __syncthreads();
+  MMF_STAMP(3)
   for (int i = t; i < S * H; i += NT) {
     const int si = i / H, n = i - si * H;
     const float o = v1[si * TH + n] + r_s[si * MAXHEADS + n / hd] * P.bv[n];
@@ -233,10 +238,12 @@ __global__ __launch_bounds__(NT) void tail_pair_fwd_kernel(const TailArgs a) {
   __syncthreads();
   gemv_nt_s<S>(v1, TH, 1 << 30, 0, P.Wo, H, H, v2, TH);
   __syncthreads();
+  MMF_STAMP(4)
   for (int i = t; i < ns * H; i += NT) {
     const int si = i / H, n = i - si * H;
     P.Ab[(int64_t)(b0 + si) * H + n] = v2[si * TH + n] + P.bo[n];
   }
+  MMF_STAMP(5)
 }
 
 // Backward: dObar = cvec_q W_o; dU_h = dObar_h W_v[h rows];
@@ -555,3 +562,10 @@ hipError_t launch_tail_bwd(const TailArgs& a, hipStream_t st) {
 }
 
 }  // namespace mmf
+
+#ifdef MMF_STAMPS
+extern "C" int mmf_tail_stamps_read(void* out, size_t bytes) {   // tail_pair_fwd_kernel phases
+  if (bytes > sizeof(mmf::g_mmf_stamps)) bytes = sizeof(mmf::g_mmf_stamps);
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mmf::g_mmf_stamps), bytes) == hipSuccess ? 0 : 3;
+}
+#endif

@@ -28,6 +28,7 @@ import bench  # noqa: E402
 
 
 def main():
+    kernel = sys.argv[1] if len(sys.argv) > 1 else "attn"
     w = bench.WORKLOADS["c2"]
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
@@ -37,28 +38,55 @@ def main():
     feats, mask, labels = bench.make_inputs(w, w["B"], 42, dev)
     step = HybridTrainStep(model, feats, mask, labels)
     L = mmf_native.lib()
-    L.mmf_stamps_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    occ = (ctypes.c_int * 2)()
+    L.mmf_attn_occupancy(occ)
+    print("runtime occupancy (blocks/CU): fused bwd", occ[0], "pooled fwd", occ[1], flush=True)
+    reader = L.mmf_stamps_read if kernel == "attn" else L.mmf_tail_stamps_read
+    reader.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     for _ in range(3):
         step.forward_backward()
     torch.cuda.synchronize()
-    nwg = 6 * w["B"] * w["heads"]
     buf = np.zeros((8192, 10), dtype=np.uint64)
-    assert L.mmf_stamps_read(buf.ctypes.data, buf.nbytes) == 0
-    st = buf[:nwg, :7].astype(np.int64)
+    assert reader(buf.ctypes.data, buf.nbytes) == 0
+    if kernel == "attn":
+        nwg, nst = 6 * w["B"] * w["heads"], 7
+        names_ph = ["load", "S/P/D", "dS", "dQ", "dK quarters", "dK store"]
+    else:   # tail_pair_fwd_kernel: grid (B, pairs)
+        nwg, nst = 6 * w["B"], 6
+        names_ph = ["pbar + r", "U = pbar P_k", "Obar GEMV", "Abar GEMV", "stores"]
+    st = buf[:nwg, :nst].astype(np.int64)
     hw = buf[:nwg, 9]
     t0 = st[:, 0].min()
     ph = np.diff(st, axis=1)
-    names_ph = ["load", "S/P/D", "dS", "dQ", "dK quarters", "dK store"]
-    out = {"workgroups": int(nwg),
-           "kernel_cycles": int(st[:, 6].max() - t0),
-           "wg_lifetime_mean": float((st[:, 6] - st[:, 0]).mean()),
+    last = nst - 1
+    out = {"kernel": kernel, "workgroups": int(nwg),
+           "kernel_cycles": int(st[:, last].max() - t0),
+           "wg_lifetime_mean": float((st[:, last] - st[:, 0]).mean()),
            "phase_mean_cycles": {n: float(ph[:, i].mean()) for i, n in enumerate(names_ph)},
-           "phase_share": {n: round(float(ph[:, i].mean() / (st[:, 6] - st[:, 0]).mean()), 3)
+           "phase_share": {n: round(float(ph[:, i].mean() / (st[:, last] - st[:, 0]).mean()), 3)
                            for i, n in enumerate(names_ph)}}
+    # s_memtime counters are per XCD: spans and residency per XCC
+    xcc_all = ((hw >> 32).astype(np.int64)) & 0xF
+    spans, resid = [], []
+    for x in np.unique(xcc_all):
+        sel = xcc_all == x
+        span = int(st[sel, last].max() - st[sel, 0].min())
+        spans.append(span)
+        # mean workgroups resident = sum of lifetimes / span
+        resid.append(float((st[sel, last] - st[sel, 0]).sum() / span))
+    if kernel == "attn":
+        rt = (buf[:nwg, 8].astype(np.int64) - buf[:nwg, 7].astype(np.int64))
+        ok = rt > 0
+        out["shader_clock_ghz_median"] = float(np.median((st[ok, last] - st[ok, 0]) / rt[ok] * 0.1))
+        out["wg_lifetime_us_median"] = float(np.median(rt[ok]) * 0.01)
+    out["xcc_span_cycles_mean"] = float(np.mean(spans))
+    out["resident_wgs_per_xcc_mean"] = float(np.mean(resid))
+    out["resident_wgs_per_cu_mean"] = float(np.mean(resid)) / 32.0
     # workgroups sharing a CU: HW_ID cu / sh / se fields + XCC id
     hw32 = (hw & 0xFFFFFFFF).astype(np.int64)
     xcc = (hw >> 32).astype(np.int64) & 0xF
-    cu_key = xcc * 4096 + ((hw32 >> 8) & 0xFFF)
+    cu_key = xcc * 4096 + ((hw32 >> 8) & 0xFF) + (((hw32 >> 12) & 0xF) << 8) * 0   # cu_id | sh_id | se_id (tg_id dropped)
+    cu_key = xcc * 65536 + (((hw32 >> 8) & 0xF) | (((hw32 >> 12) & 0x1) << 4) | (((hw32 >> 13) & 0x7) << 5))
     starts = {}
     for k, s0 in zip(cu_key, st[:, 0] - t0):
         starts.setdefault(int(k), []).append(int(s0))
