@@ -181,17 +181,7 @@ __device__ unsigned long long g_mmf_stamps[STAMP_WG][10];
   }
 #else
 #define MMF_STAMP(i)
-// s_memrealtime (constant 100 MHz) into slot i: with two s_memtime stamps it gives the
-// shader clock the workgroup ran at (MI355X_MICROARCH.md, DVFS item 6)
-#define MMF_STAMP_RT(i)                                                                    \
-  {                                                                                        \
-    unsigned long long t_;                                                                 \
-    __builtin_amdgcn_sched_barrier(0);                                                     \
-    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");        \
-    __builtin_amdgcn_sched_barrier(0);                                                     \
-    const int sid_ = blockIdx.y * gridDim.x + blockIdx.x;                                  \
-    if ((threadIdx.x & 63) == 0 && (threadIdx.x >> 6) == 0 && sid_ < STAMP_WG) g_mmf_stamps[sid_][i] = t_; \
-  }
+#define MMF_STAMP_RT(i)
 #define MMF_STAMP_ID()
 #endif
 

@@ -118,7 +118,7 @@ struct GemmGroup {
   int32_t seg_rows;        // rows per segment for operands with seg_stride (a tile never straddles two)
 };
 
-constexpr int GEMM_MAX_GROUPS = 24;   // kernel arguments up to ~6.3 KB (measured fine on gfx950)
+constexpr int GEMM_MAX_GROUPS = 32;   // kernel arguments ~7.8 KB (measured fine on gfx950)
 constexpr int GEMM_MAX_SRCS = 32;
 
 struct GemmArgs {
