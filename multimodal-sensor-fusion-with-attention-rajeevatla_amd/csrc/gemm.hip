@@ -807,6 +807,81 @@ __global__ __launch_bounds__(NT) void gemm_generic_kernel(const GemmArgs args) {
   epilogue(G, T, acc, sm, rs, p, inv_keep, wm, wn, h, c);
 }
 
+// ------------------------------------------------------------------ small split-K slabs
+// The weight gradients of the B-row tail layers that are not LDS-DMA-able (C x H
+// classifier output, 1 x H gates, per-head value biases: odd or unaligned
+// extents) are a few thousand outputs of <= 64-row dot products.  As 128 x 128
+// generic tiles they cost a tile's whole prologue / epilogue chain each (18 us
+// for ~0.1 MFLOP at C2); here one thread computes one slab element
+// C[split][i][j] = alpha sum_{k in split} A(i, k) B(k, j) (A, B stored [k][e]),
+// j == N standing for the bias-row slab part_db[split][i] = alpha sum_k A(i, k),
+// with its rows' loads 8 at a time in flight.  Same fixed summation order per
+// slab every call (deterministic); the split-K reduce then sums the slabs.
+struct SmallSlabArgs {
+  GemmGroup g[GEMM_MAX_GROUPS];
+  GemmSrc s[GEMM_MAX_GROUPS];
+  int32_t off[GEMM_MAX_GROUPS + 1];   // first thread of each group (1-D grid)
+  int32_t ngroups;
+};
+
+// 8 lanes per slab element: lane q of the group takes rows k0 + q, k0 + q + 8, ... (all
+// its loads in flight at once), the 8 partial sums are combined by xor shuffles in a
+// fixed order.
+__global__ __launch_bounds__(256) void small_slab_kernel(const SmallSlabArgs a) {
+  const int gtid = blockIdx.x * 256 + threadIdx.x;
+  const int tid = gtid >> 3, q = gtid & 7;
+  const bool live = tid < a.off[a.ngroups];
+  int gi = 0;
+  for (int i = 1; i < a.ngroups; ++i)
+    if (tid >= a.off[i]) gi = i;
+  const GemmGroup& G = a.g[gi];
+  const GemmSrc& S = a.s[gi];
+  const int ncol = G.N + (G.part_db ? 1 : 0);
+  int r = live ? tid - a.off[gi] : 0;
+  const int j = r % ncol; r /= ncol;
+  const int i = r % G.M; r /= G.M;
+  const int split = r % G.nsplit;
+  const int batch = r / G.nsplit;
+  const int k0 = split * G.kchunk, k1 = min(S.K, k0 + G.kchunk);
+  const float* ap = S.a.ptr + (int64_t)batch * G.bs_a + i;
+  const float* bp = S.b.ptr + (int64_t)batch * G.bs_b + j;
+  const bool bias = j == G.N;
+  constexpr int MAXR = 256 / 8;   // kchunk <= 256 (job_small_slab)
+  float av[MAXR], bv[MAXR];
+#pragma unroll
+  for (int u = 0; u < MAXR; ++u) {
+    const int kk = k0 + q + 8 * u;
+    const bool in = live && kk < k1;
+    const int ka = S.a.row_div == 1 ? kk : kk / S.a.row_div;
+    const int kb = S.b.row_div == 1 ? kk : kk / S.b.row_div;
+    av[u] = in ? ap[(int64_t)ka * S.a.ld] : 0.f;
+    bv[u] = in ? (bias ? 1.f : bp[(int64_t)kb * S.b.ld]) : 0.f;
+    if (k0 + 8 * (u + 1) >= k1) break;   // uniform per group of 8 lanes only: a bound, not a branch on data
+  }
+  float acc = 0.f;
+#pragma unroll
+  for (int u = 0; u < MAXR; ++u) {
+    if (k0 + 8 * u >= k1) break;
+    acc = fmaf(av[u], bv[u], acc);
+  }
+  acc += __shfl_xor(acc, 1);
+  acc += __shfl_xor(acc, 2);
+  acc += __shfl_xor(acc, 4);
+  if (!live || q != 0) return;
+  if (bias)
+    G.part_db[((int64_t)batch * G.nsplit + split) * G.M + i] = acc * G.alpha;
+  else
+    G.C[(((int64_t)batch * G.nsplit + split) * G.M + i) * G.N + j] = acc * G.alpha;
+}
+
+bool job_small_slab(const GemmJob& J, int amode, int bmode) {
+  const GemmGroup& g = J.g;
+  if (amode != MODE_KR || bmode != MODE_KR || J.nsrc != 1 || !(g.epi & EPI_PARTIAL)) return false;
+  if (g.seg_rows > 0 || J.src[0].a.seg_stride || J.src[0].b.seg_stride) return false;
+  const int64_t n = (int64_t)(g.nbatch < 1 ? 1 : g.nbatch) * g.nsplit * g.M * (g.N + 1);
+  return n <= (1 << 20) && g.kchunk <= 256;
+}
+
 // ------------------------------------------------------------------ split-K reduce
 struct ReduceArgs {
   ReduceJob j[48];
@@ -1031,6 +1106,45 @@ hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, 
     for (int i = 0; i < njobs && wsr; ++i)
       wsr = job_wsr(jobs_in[i], amode, bmode) && jobs_in[i].src[0].K == jobs_in[0].src[0].K;
     if (wsr && getenv("MMF_NO_WSR") == nullptr) return launch_wsr(jobs_in, njobs, st);
+  }
+  // Small, non-DMA-able split-K slabs: one thread per slab element, all in one launch
+  // (the remaining jobs go through the tiled kernels below).
+  std::vector<GemmJob> rest;
+  {
+    SmallSlabArgs sa;
+    memset(&sa, 0, sizeof(sa));
+    int total = 0;
+    double fl = 0.0, by = 0.0;
+    auto flush = [&]() -> hipError_t {
+      if (sa.ngroups == 0) return hipSuccess;
+      sa.off[sa.ngroups] = total;
+      ProfLaunch prof_(st, "small_slab_kernel", fl, by);
+      hipLaunchKernelGGL(small_slab_kernel, dim3((8 * total + 255) / 256), dim3(256), 0, st, sa);
+      memset(&sa, 0, sizeof(sa));
+      total = 0; fl = by = 0.0;
+      return hipGetLastError();
+    };
+    for (int i = 0; i < njobs; ++i) {
+      const GemmJob& J = jobs_in[i];
+      if (job_fast(J, amode, bmode) || !job_small_slab(J, amode, bmode)) {
+        rest.push_back(J);
+        continue;
+      }
+      GemmGroup g = J.g;
+      if (g.nbatch < 1) g.nbatch = 1;
+      sa.g[sa.ngroups] = g;
+      sa.s[sa.ngroups] = J.src[0];
+      sa.off[sa.ngroups] = total;
+      total += g.nbatch * g.nsplit * g.M * (g.N + (g.part_db ? 1 : 0));
+      fl += 2.0 * g.nbatch * g.M * g.N * J.src[0].K;
+      by += 4.0 * g.nbatch * ((double)g.M + g.N) * J.src[0].K + 4.0 * g.nbatch * g.nsplit * g.M * g.N;
+      if (++sa.ngroups == GEMM_MAX_GROUPS)
+        if (hipError_t e = flush()) return e;
+    }
+    if (hipError_t e = flush()) return e;
+    if (rest.empty()) return hipSuccess;
+    jobs_in = rest.data();
+    njobs = (int)rest.size();
   }
   // The jobs of one call are independent outputs, so they may be launched in
   // any order: longest contraction per tile first (the first-dispatched blocks
