@@ -94,6 +94,9 @@ __device__ __forceinline__ bool tile_ctx(const GemmGroup& G, int local, TileCtx&
 // small grids).  Order: v = alpha*acc; +bias[j] (x bias_rs[i]); +rowadd;
 // +addm; relu; gate; rowscale; dropout (keep(site, i*N + j)).
 constexpr int CS = BN + 4;
+// Register budget: gemm_lds_kernel sits at ~163 VGPRs; past 168 it drops from 3
+// to 2 waves/SIMD, which measured ~30% slower on every GEMM.  Keep epilogue
+// state out of registers that live across the passes (EPI_COLSUM reuses the image).
 
 // 8 consecutive floats of a side operand row (vec: two 16-B loads)
 __device__ __forceinline__ void load8(float (&d)[8], const float* p, int nv, bool vec) {
@@ -132,6 +135,7 @@ __device__ __forceinline__ void epilogue(const GemmGroup& G, const TileCtx& T, f
   float bias[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) bias[e] = (!partial && (epi & EPI_BIAS) && e < nv) ? T.biasb[j0 + e] : 0.f;
+  float csum = 0.f;   // EPI_COLSUM: thread t < BN owns column T.j0 + t (rows in fixed order)
   for (int pass = 0; pass < BM / PR; ++pass) {
     __syncthreads();
 #pragma unroll
@@ -194,6 +198,10 @@ __device__ __forceinline__ void epilogue(const GemmGroup& G, const TileCtx& T, f
           v[e] = x;
         }
       }
+      if (epi & EPI_COLSUM) {   // the final values back into the image for the column sums
+        *reinterpret_cast<f32x4*>(cs + lr * CS + cg) = f32x4{v[0], v[1], v[2], v[3]};
+        *reinterpret_cast<f32x4*>(cs + lr * CS + cg + 4) = f32x4{v[4], v[5], v[6], v[7]};
+      }
       float* o = out + (int64_t)i * ldc + j0;
       if (vst && nv == 8) {
         *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};
@@ -204,6 +212,16 @@ __device__ __forceinline__ void epilogue(const GemmGroup& G, const TileCtx& T, f
           if (e < nv) o[e] = v[e];
       }
     }
+    if (epi & EPI_COLSUM) {
+      __syncthreads();
+      const int nr = min(PR, G.M - T.i0 - pass * PR);
+      if (t < BN)
+        for (int r = 0; r < nr; ++r) csum += cs[r * CS + t];
+    }
+  }
+  if ((epi & EPI_COLSUM) && t < BN && T.j0 + t < G.N) {
+    const int tiles_m = (G.M + BM - 1) / BM;
+    G.colsum[((int64_t)T.batch * tiles_m + T.i0 / BM) * G.N + T.j0 + t] = csum;
   }
 }
 

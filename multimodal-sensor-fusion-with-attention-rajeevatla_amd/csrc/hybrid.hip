@@ -40,10 +40,19 @@ inline bool long_keys(const mmf_hybrid_desc* d) {
   return false;
 }
 
+bool use_tail(const mmf_hybrid_desc* d);
+
+// The tail head takes mean_L P_m from per-tile column sums written by the
+// projection GEMM's epilogue when every 128-row tile lies inside one sample.
+bool pcol_in_proj(const mmf_hybrid_desc* d, int m) {
+  return d->num_pairs && use_tail(d) && Lm(d, m) % 128 == 0 && !getenv("MMF_NO_PCOL");
+}
+
 struct Saved {
   RngSnap* rng;
   float* Xd[MMF_MAX_MODALITIES];   // X_m * mask_m with input dropout (fusion.py:364-373)
   float* P[MMF_MAX_MODALITIES];
+  float* Pcol[MMF_MAX_MODALITIES];  // per-128-row column sums of P_m (proj GEMM epilogue; tail plan)
   float *Q[MMF_MAX_PAIRS], *K[MMF_MAX_PAIRS], *lse[MMF_MAX_PAIRS];
   // general plan
   float *V[MMF_MAX_PAIRS], *O[MMF_MAX_PAIRS], *A[MMF_MAX_PAIRS];
@@ -61,6 +70,8 @@ void layout_saved(const mmf_hybrid_desc* d, Bump& bp, Saved& s) {
   s.rng = bp.take<RngSnap>(1);
   for (int m = 0; m < d->num_modalities; ++m) s.Xd[m] = bp.take<float>(B * Lm(d, m) * d->in_dim[m]);
   for (int m = 0; m < d->num_modalities; ++m) s.P[m] = bp.take<float>(B * Lm(d, m) * H);
+  for (int m = 0; m < d->num_modalities; ++m)
+    if (pcol_in_proj(d, m)) s.Pcol[m] = bp.take<float>(B * (Lm(d, m) / 128) * H);
   for (int g = 0; g < d->num_pairs; ++g) {
     const size_t lq = Lm(d, d->pair_q[g]), lk = Lm(d, d->pair_k[g]);
     s.Q[g] = bp.take<float>(B * lq * H);
@@ -293,6 +304,8 @@ void fill_tail(TailArgs& ta, const mmf_hybrid_desc* d, const mmf_hybrid_params* 
   for (int m = 0; m < M; ++m) {
     ta.P[m] = s.P[m];
     ta.L[m] = Lm(d, m);
+    ta.Pcol[m] = s.Pcol[m];
+    ta.ncol[m] = Lm(d, m) / 128;
     ta.gate_w[m] = W->gate[m].w;
     ta.gate_b[m] = W->gate[m].b;
     cnt[m] = 1;
@@ -389,8 +402,10 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
       const int L = Lm(d, m), D = d->in_dim[m];
       ma.j[m].x = x[m]; ma.j[m].out = s.Xd[m]; ma.j[m].rows = (int64_t)B * L; ma.j[m].D = D; ma.j[m].L = L;
       ma.j[m].site = SITE_IN + m;
-      GemmJob j = make_job(B * L, H, s.P[m], H, EPI_BIAS | EPI_RELU | (drop ? EPI_DROP : 0));
+      GemmJob j = make_job(B * L, H, s.P[m], H,
+                           EPI_BIAS | EPI_RELU | (drop ? EPI_DROP : 0) | (s.Pcol[m] ? EPI_COLSUM : 0));
       j.g.bias = W->proj[m].b;
+      j.g.colsum = s.Pcol[m];
       j.g.drop_site = SITE_PROJ + m;
       add_src(j, opnd(s.Xd[m], D), opnd(W->proj[m].w, D), D);
       jobs.push_back(j);

@@ -86,7 +86,8 @@ struct GemmSrc {
 
 enum : int32_t {
   EPI_BIAS = 1, EPI_RELU = 2, EPI_DROP = 4, EPI_ROWADD = 8, EPI_GATE = 16,
-  EPI_ROWSCALE = 32, EPI_PARTIAL = 64, EPI_BIAS_RS = 128, EPI_ADDMAT = 256
+  EPI_ROWSCALE = 32, EPI_PARTIAL = 64, EPI_BIAS_RS = 128, EPI_ADDMAT = 256,
+  EPI_COLSUM = 512
 };
 
 // Epilogue order: v = alpha*acc; +bias[j] (x bias_rs[i*ld+off] with EPI_BIAS_RS);
@@ -109,7 +110,9 @@ struct GemmGroup {
   // EPI_PARTIAL (split-K over the contraction): C := part[split][M][N] (ldc = N),
   // part_db[split][M] = row sums of A over the split (bias grad of a TN dW).
   int32_t nsplit, kchunk;
-  float* part_db;
+  // EPI_COLSUM (not with EPI_PARTIAL): colsum[(batch*tiles_m + i0/BM)*N + j] = sum over the
+  // tile's rows of the final stored value (per-tile column sums, fixed order)
+  union { float* part_db; float* colsum; };
   // strided batch: nbatch identical problems, element i offsets every source's A/B
   // by i*bs_a / i*bs_b, C by i*bs_c (partial: i*nsplit*M*N, part_db i*nsplit*M),
   // bias by i*bs_bias and bias_rs_off by i*bs_brs.
@@ -341,6 +344,7 @@ struct TailArgs {
   int32_t B, M, H, C, heads, hd, npairs;
   const float* mask;                   // (B, M)
   const float* P[8]; int32_t L[8];     // projected features (B, L_m, H)
+  const float* Pcol[8]; int32_t ncol[8];  // optional per-128-row column sums of P_m (B, ncol, H)
   float inv_cnt[8];
   const float* gate_w[8]; const float* gate_b[8];
   const float* W1; const float* b1; const float* W2; const float* b2;

@@ -337,6 +337,18 @@ __global__ __launch_bounds__(NT) void tail_head_fwd_kernel(const TailArgs a) {
   // (1) mean over L of P_m (the modality's own entry of the aggregation list)
   for (int m = 0; m < M; ++m) {
     const int L = a.L[m];
+    if (a.Pcol[m]) {
+      // the projection GEMM's per-tile column sums: ncol rows per sample
+      const int nc = a.ncol[m];
+      const float* pc = a.Pcol[m] + (int64_t)b * nc * H;
+      for (int n = t; n < H; n += NT) {
+        float s = 0.f;
+        for (int c = 0; c < nc; ++c) s += pc[(int64_t)c * H + n];
+        pooled_s[m * H + n] = s * (1.f / (float)L);
+      }
+      __syncthreads();
+      continue;
+    }
     const float* base = a.P[m] + (int64_t)b * L * H;
     const int RG = NT / H4;
     const int c4 = t % H4, rg = t / H4;
