@@ -179,6 +179,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--dropout", type=float, default=0.1,
+                    help="diagnostics only: the benchmark workload is dropout 0.1")
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=5)
     ap.add_argument("--dump-launches", default=None,
@@ -211,7 +213,7 @@ def main():
     torch.manual_seed(0)                      # identical initial weights on every rank
     names = [f"m{i}" for i in range(M)]
     model = HybridFusion({n: D for n in names}, hidden_dim=H, num_classes=C, num_heads=heads,
-                         dropout=0.1).to(dev)
+                         dropout=args.dropout).to(dev)
     feats, mask, labels = make_inputs(w, B, 42 + rank, dev)
     trainer = HybridTrainStep(model, feats, mask, labels, process_group=pg)
 
@@ -276,7 +278,7 @@ def main():
             "data": "synthetic (N(0,1) encoder outputs, random-init weights, seeded)",
             "config": {"workload": f"{args.workload}: HybridFusion M={M} B={B}/gpu L={lens or 1}"
                                    f"{'' if max(Ls) else ' (2-D reference semantics)'} D={D} H={H} heads={heads} "
-                                   f"C={C} dropout=0.1 train"
+                                   f"C={C} dropout={args.dropout} train"
                                    f"{mask_note}"
                                    f", fwd+CE(ls=0.05)+bwd+clip(1.0)+AdamW",
                        "global_batch": B * world, "seq_len": lens or 1, "parallelism": f"dp{world}",

@@ -21,6 +21,7 @@
 // each lane's operand is contiguous.
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <string>
@@ -34,6 +35,24 @@ namespace {
 
 constexpr int NT = 256;
 
+
+// Diagnostic stamps (make stamps / stampsf): the fused backward's phases, or with
+// MMF_STAMPS_FWD the pooled forward's, into the TU's one stamp buffer.
+#if defined(MMF_STAMPS) && defined(MMF_STAMPS_FWD)
+#define FSTAMP(i) MMF_STAMP(i)
+#define FSTAMP_RT(i) MMF_STAMP_RT(i)
+#define FSTAMP_ID() MMF_STAMP_ID()
+#define BSTAMP(i)
+#define BSTAMP_RT(i)
+#define BSTAMP_ID()
+#else
+#define FSTAMP(i)
+#define FSTAMP_RT(i)
+#define FSTAMP_ID()
+#define BSTAMP(i) MMF_STAMP(i)
+#define BSTAMP_RT(i) MMF_STAMP_RT(i)
+#define BSTAMP_ID() MMF_STAMP_ID()
+#endif
 
 __device__ __forceinline__ float kmask_val(const AttnPair& P, int b, int key) {
   if (P.kmask_mode == 1) return P.kmask[(int64_t)b * P.kmask_ld];
@@ -227,7 +246,7 @@ __global__ __launch_bounds__(NT) void attn_fwd_kernel(const AttnArgs A) {
         mx = fmaxf(mx, sv[r]);
       }
       if (MODE == 0) {
-        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        mx = max_xor32(mx);
         const float mnew = fmaxf(m, mx);
         const float alpha = (m == -INFINITY) ? 0.f : __expf(m - mnew);
         float ls = 0.f;
@@ -236,7 +255,7 @@ __global__ __launch_bounds__(NT) void attn_fwd_kernel(const AttnArgs A) {
           sv[r] = (sv[r] == -INFINITY) ? 0.f : __expf(sv[r] - mnew);
           ls += sv[r];
         }
-        ls += __shfl_xor(ls, 32);
+        ls = sum_xor32(ls);
         l = l * alpha + ls;
         m = mnew;
 #pragma unroll
@@ -565,29 +584,34 @@ constexpr float LOG2E = 1.4426950408889634f;
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // Column-sum of a 32x32 S^T tile over its 32 query lanes (reduce-scatter
-// butterfly, 16 shuffles).  Returns, in lane c, the sum for tile row
-// r = (c >> 1) & 15 (lanes c and c^1 hold the same value).
+// butterfly without LDS: permlane16_swap for the lane-16 stage, DPP row_ror:8 /
+// row_half_mirror / quad_perm for the rest).  Returns, in lane c, the sum for
+// tile row r = (c >> 1) & 15 (lanes c and c^1 hold the same value).
 __device__ __forceinline__ float colsum_tile(const float (&v)[16], int c) {
   float a8[8], a4[4], a2[2];
-  const bool b4 = c & 16, b3 = c & 8, b2 = c & 4, b1 = c & 2;
+  const bool b3 = c & 8, b2 = c & 4, b1 = c & 2;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const float recv = __shfl_xor(b4 ? v[i] : v[i + 8], 16);
-    a8[i] = (b4 ? v[i + 8] : v[i]) + recv;
+  for (int i = 0; i < 8; ++i) {   // lane c < 16 keeps rows i, c >= 16 rows i + 8 (of the pair c, c ^ 16)
+    float x = v[i], y = v[i + 8];
+    swap16(x, y);
+    a8[i] = x + y;
   }
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float recv = __shfl_xor(b3 ? a8[i] : a8[i + 4], 8);
-    a4[i] = (b3 ? a8[i + 4] : a8[i]) + recv;
+  for (int i = 0; i < 4; ++i) {   // partner c ^ 8
+    const float lo = a8[i] + dpp<DPP_ROR8>(a8[i]);
+    const float hi = a8[i + 4] + dpp<DPP_ROR8>(a8[i + 4]);
+    a4[i] = b3 ? hi : lo;
   }
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const float recv = __shfl_xor(b2 ? a4[i] : a4[i + 2], 4);
-    a2[i] = (b2 ? a4[i + 2] : a4[i]) + recv;
+  for (int i = 0; i < 2; ++i) {   // partner c ^ 7 (flips bit 2)
+    const float lo = a4[i] + dpp<DPP_HALF_MIRROR>(a4[i]);
+    const float hi = a4[i + 2] + dpp<DPP_HALF_MIRROR>(a4[i + 2]);
+    a2[i] = b2 ? hi : lo;
   }
-  float a1 = (b1 ? a2[1] : a2[0]) + __shfl_xor(b1 ? a2[0] : a2[1], 2);
-  a1 += __shfl_xor(a1, 1);
-  return a1;
+  const float lo = a2[0] + dpp<DPP_XOR2>(a2[0]);
+  const float hi = a2[1] + dpp<DPP_XOR2>(a2[1]);
+  const float a1 = b1 ? hi : lo;
+  return a1 + dpp<DPP_XOR1>(a1);
 }
 
 template <int HDP, bool BF>
@@ -653,7 +677,7 @@ __global__ __launch_bounds__(NT) void attn_pool_fwd_kernel(const AttnArgs A) {
         for (int r = 0; r < 16; ++r) sv[kt][r] = -INFINITY;
       }
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    mx = max_xor32(mx);
     float l = 0.f;
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt)
@@ -662,7 +686,7 @@ __global__ __launch_bounds__(NT) void attn_pool_fwd_kernel(const AttnArgs A) {
         sv[kt][r] = (sv[kt][r] == -INFINITY) ? 0.f : __expf(sv[kt][r] - mx);
         l += sv[kt][r];
       }
-    l += __shfl_xor(l, 32);
+    l = sum_xor32(l);
     const float inv_l = (l > 0.f && qvalid) ? 1.f / l : 0.f;
     const int64_t rowidx = bh * Lq + q;
     uint32_t words[NKT];
@@ -683,7 +707,7 @@ __global__ __launch_bounds__(NT) void attn_pool_fwd_kernel(const AttnArgs A) {
           sv[kt][4 * g + j] = (pdrop > 0.f) ? (((kb >> j) & 1u) ? pv * inv_keep : 0.f) : pv;
         }
       }
-      words[kt] = bits | __shfl_xor(bits, 32);
+      words[kt] = or_xor32(bits);
       if (kt < nkt) {
         const float colsum = colsum_tile(sv[kt], c);
         if ((c & 1) == 0) cs[w][kt * 32 + acc_row((c >> 1) & 15, h)] += colsum;
@@ -777,7 +801,7 @@ __global__ __launch_bounds__(NT) void attn_pool_bwd_dq_kernel(const AttnArgs A) 
       for (int r = 0; r < 16; ++r) pr[kt][r] = 0.f;
     }
   }
-  D = (D + __shfl_xor(D, 32)) * inv_lq;
+  D = sum_xor32(D) * inv_lq;
   if (qvalid && h == 0) P.dsum[rowidx] = D;
   f32x16 dq[NDT];
 #pragma unroll
@@ -985,13 +1009,13 @@ __global__ __launch_bounds__(NT) void attn_poolL_lse_kernel(const AttnArgs A) {
       float mx = sv[0];
 #pragma unroll
       for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sv[r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      mx = max_xor32(mx);
       const float mnew = fmaxf(m, mx);
       const float mref = mnew == -INFINITY ? 0.f : mnew;   // exp2(-inf - mref) = 0, no NaN
       float ls = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) ls += fast_exp2(sv[r] - mref);
-      ls += __shfl_xor(ls, 32);
+      ls = sum_xor32(ls);
       l = l * fast_exp2(m - mref) + ls;
       m = mnew;
       if (bits_out) {
@@ -1000,7 +1024,7 @@ __global__ __launch_bounds__(NT) void attn_poolL_lse_kernel(const AttnArgs A) {
         uint32_t bits = 0;
 #pragma unroll
         for (int g = 0; g < 4; ++g) bits |= ((kb16 >> (4 * g)) & 0xFu) << (8 * g + 4 * h);
-        bits |= __shfl_xor(bits, 32);
+        bits = or_xor32(bits);
         if (qvalid && h == 0) P.keep_bits[rowidx * kwl + ((kbase >> 5) + kt)] = bits;
       }
     }
@@ -1079,7 +1103,7 @@ __global__ __launch_bounds__(NT) void attn_poolL_colsum_kernel(const AttnArgs A)
     }
   }
   if (!kvalid) cs = 0.f;
-  cs = (cs + __shfl_xor(cs, 32)) * inv_keep * (1.f / (float)Lq);
+  cs = sum_xor32(cs) * inv_keep * (1.f / (float)Lq);
   if (wave_active && h == 0 && key < Lk) {
     P.pbar[bh * Lk + key] = cs;
     if (P.pbarT) P.pbarT[((int64_t)b * Lk + key) * A.heads + head] = cs;
@@ -1175,7 +1199,7 @@ __global__ __launch_bounds__(NT, 4) void attn_poolL_dq_kernel(const AttnArgs A) 
       }
     }
   }
-  D += __shfl_xor(D, 32);
+  D = sum_xor32(D);
   if (qvalid && h == 0) P.dsum[rowidx] = D;
 
   // pass B: dS = P (dP - D), dQ = scale dS K
@@ -1239,7 +1263,9 @@ __device__ __forceinline__ void load_frag_vec(float* f, const float* row) {
   }
 }
 
-template <int HDP, bool BF>
+// DROP (train mode with p > 0, launch-time choice): the loop body has no dropout
+// branches, so the draws schedule between the S MFMAs.
+template <int HDP, bool BF, bool DROP = true>
 __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(const AttnArgs A) {
   constexpr int LS = HDP + 4;
   constexpr int HALF = HDP / 2;
@@ -1254,12 +1280,15 @@ __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(cons
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, c = lane & 31;
   const int hd = A.hd, col0 = head * hd;
   const int Lq = P.Lq, Lk = P.Lk, nkt = Lk >> 5;
-  const float pdrop = A.drop_p;
+  const float pdrop = DROP ? A.drop_p : 0.f;
   const float inv_keep = pdrop < 1.f ? 1.f / (1.f - pdrop) : 0.f;
   RngSnap rs{0, 0};
   if (pdrop > 0.f && A.rng) rs = *A.rng;
   const int64_t bh = (int64_t)b * A.heads + head;
   float* pbar = P.pbar + bh * Lk;
+  FSTAMP_RT(7)
+  FSTAMP(0)
+  FSTAMP_ID()
 
   // the sample mask, this wave's first query fragment and the K image in one round trip
   const float msk = P.kmask_mode == 1 ? P.kmask[(int64_t)b * P.kmask_ld] : 1.f;
@@ -1277,6 +1306,7 @@ __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(cons
     return;
   }
   __syncthreads();
+  FSTAMP(1)
 
   const float c2 = A.scale * LOG2E;
   float colacc[NKT];
@@ -1287,8 +1317,11 @@ __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(cons
     const int q = qt * 32 + c;
     const bool qvalid = q < Lq;
     const int qq = qvalid ? q : Lq - 1;
+    const int64_t rowidx = bh * Lq + qq;
     float sv[NKT][16];
+    uint32_t kb[NKT];   // keep bits of the lane's 16 registers per key tile
     float mx = -INFINITY;
+    // the dropout draws do not depend on S: issued beside the S MFMAs
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
       if (kt < nkt) {
@@ -1299,11 +1332,13 @@ __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(cons
           mx = fmaxf(mx, s[r]);
         }
       } else {
+        kb[kt] = 0u;
 #pragma unroll
         for (int r = 0; r < 16; ++r) sv[kt][r] = 0.f;
       }
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    mx = max_xor32(mx);
+    FSTAMP(2)
     const float mc = mx * c2;
     float l = 0.f;
 #pragma unroll
@@ -1317,20 +1352,20 @@ __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(cons
         }
       }
     }
-    l += __shfl_xor(l, 32);
+    l = sum_xor32(l);
+    FSTAMP(3)
     const float f = qvalid ? (pdrop > 0.f ? inv_keep : 1.f) / l : 0.f;
-    const int64_t rowidx = bh * Lq + qq;
     uint32_t words[NKT];
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
       words[kt] = 0u;
       if (kt < nkt) {
-        uint32_t kb16 = 0xFFFFu;
-        if (pdrop > 0.f) kb16 = keep_tile16(rs, P.drop_site, (uint64_t)rowidx * Lk + kt * 32, pdrop, h, qvalid, true);
+        const uint32_t kb16 =
+            DROP ? keep_tile16(rs, P.drop_site, (uint64_t)rowidx * Lk + kt * 32, pdrop, h, true, true) : 0xFFFFu;
         uint32_t bits = 0;
 #pragma unroll
         for (int g = 0; g < 4; ++g) bits |= ((kb16 >> (4 * g)) & 0xFu) << (8 * g + 4 * h);
-        words[kt] = bits | __shfl_xor(bits, 32);
+        words[kt] = or_xor32(bits);
 #pragma unroll
         for (int r = 0; r < 16; ++r) sv[kt][r] = ((kb16 >> r) & 1u) ? sv[kt][r] * f : 0.f;
         colacc[kt] += colsum_tile(sv[kt], c);
@@ -1342,6 +1377,7 @@ __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(cons
         *reinterpret_cast<uint4*>(P.keep_bits + rowidx * 4) =
             make_uint4(words[0], NKT > 1 ? words[1] : 0u, NKT > 2 ? words[2] : 0u, NKT > 3 ? words[3] : 0u);
     }
+    FSTAMP(4)
     if ((qt + 4) * 32 < Lq)
       load_frag_vec<HALF>(qf, P.q + ((int64_t)b * Lq + min((qt + 4) * 32 + c, Lq - 1)) * P.ldq + col0 + h * HALF);
   }
@@ -1356,6 +1392,193 @@ __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(cons
     const float v = ((cs[0][k] + cs[1][k]) + (cs[2][k] + cs[3][k])) * inv_lq;
     pbar[k] = v;
     if (P.pbarT) P.pbarT[((int64_t)b * Lk + k) * A.heads + head] = v;
+  }
+  FSTAMP(5)
+  FSTAMP_RT(8)
+}
+
+// Persistent pooled forward for head_dim 32 (the lean case of the benchmark
+// shape): each workgroup walks items (pair, sample, head) with stride gridDim.x.
+// The next item's K image is DMA'd (global_load_lds, no VGPRs) into the other
+// half of a double buffer and its first query fragment loaded into registers
+// while the current item computes, so after the first item the MFMAs no longer
+// wait on a K/Q round trip (the lean kernel's workgroups all load, then all
+// compute, in lockstep: a quarter of their lifetime).  Same arithmetic and
+// outputs as attn_pool_fwd_lean<32>.
+// K image [PKC][32] floats, 128-B rows, 16-B slots XOR-swizzled by (row >> 1) & 7:
+// the 16 rows of a ds_read_b128 quarter-wave land on distinct bank groups.
+__device__ __forceinline__ int fs_swz(int row) { return (row >> 1) & 7; }
+
+struct FsItem { int b, head; };
+
+// this wave's quarter of the K image of an item (4 x 1 KB, rows past Lk skipped)
+__device__ __forceinline__ void fs_issue_k(const AttnPair& P, const FsItem& it, float* buf, int w, int lane) {
+  const float* base = P.k + (int64_t)it.b * P.Lk * P.ldk + it.head * 32;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int ins = w * 4 + u;
+    if (ins * 8 < P.Lk) {
+      const int row = ins * 8 + (lane >> 3), slot = lane & 7;
+      const float* src = base + (int64_t)row * P.ldk + 4 * (slot ^ fs_swz(row));
+      __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(buf + ins * 256),
+                                       16, 0, 0);
+    }
+  }
+}
+
+__device__ __forceinline__ void fs_load_q(const AttnPair& P, const FsItem& it, int qt, int c, int h, float (&qf)[16]) {
+  load_frag_vec<16>(qf, P.q + ((int64_t)it.b * P.Lq + min(qt * 32 + c, P.Lq - 1)) * P.ldq + it.head * 32 + h * 16);
+}
+
+// grid (workgroups per pair, pairs): a workgroup walks the (sample, head) items of one pair
+template <bool BF, bool DROP>
+__global__ __launch_bounds__(NT, 3) void attn_pool_fwd_stream(const AttnArgs A) {
+  constexpr int HALF = 16, NKT = PKC / 32, ROWF = 32;
+  __shared__ __attribute__((aligned(16))) float Kb[2][PKC * ROWF];
+  __shared__ float cs[4][PKC];
+  const AttnPair& P = A.p[blockIdx.y];
+  const int total = A.B * A.heads;
+  const int t0 = threadIdx.x, lane = t0 & 63, w = t0 >> 6;
+  const float pdrop = DROP ? A.drop_p : 0.f;
+  const float inv_keep = pdrop < 1.f ? 1.f / (1.f - pdrop) : 0.f;
+  RngSnap rs{0, 0};
+  if (pdrop > 0.f && A.rng) rs = *A.rng;
+  const float c2 = A.scale * LOG2E;
+  const int Lq = P.Lq, Lk = P.Lk, nkt = Lk >> 5;
+
+  int item = blockIdx.x;
+  if (item >= total) return;
+  FsItem cur{item / A.heads, item % A.heads};
+  float qf[HALF];
+  fs_issue_k(P, cur, Kb[0], w, lane);
+  fs_load_q(P, cur, w, lane & 31, lane >> 5, qf);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int tt = t0, hh = lane >> 5, cc = lane & 31;
+  for (int buf = 0; item < total; item += gridDim.x, buf ^= 1) {
+    // launder the lane ids: otherwise every lane-derived address of the body is hoisted
+    // out of the item loop and held in VGPRs across it (spills)
+    asm volatile("" : "+v"(tt), "+v"(hh), "+v"(cc));
+    const int t = tt, h = hh, c = cc;
+    const int next = item + gridDim.x;
+    const bool more = next < total;
+    const FsItem nxt{next / A.heads, next % A.heads};
+    if (more) fs_issue_k(P, nxt, Kb[buf ^ 1], w, lane);
+    const int64_t bh = (int64_t)cur.b * A.heads + cur.head;
+    float* pbar = P.pbar + bh * Lk;
+    const float msk = P.kmask_mode == 1 ? P.kmask[(int64_t)cur.b * P.kmask_ld] : 1.f;
+    const float* Ks = Kb[buf];
+    if (msk == 0.f) {
+      for (int k = t; k < Lk; k += NT) pbar[k] = 0.f;
+      if (P.pbarT)
+        for (int k = t; k < Lk; k += NT) P.pbarT[((int64_t)cur.b * Lk + k) * A.heads + cur.head] = 0.f;
+      for (int q = t; q < Lq; q += NT) P.lse[bh * Lq + q] = -INFINITY;
+      if (P.keep_bits)
+        for (int q = t; q < Lq; q += NT)
+          *reinterpret_cast<uint4*>(P.keep_bits + (bh * Lq + q) * 4) = make_uint4(0, 0, 0, 0);
+      if (more) fs_load_q(P, nxt, w, c, h, qf);
+    } else {
+      float colacc[NKT];
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) colacc[kt] = 0.f;
+      bool loaded = false;   // the next item's first fragment (a wave without a query tile loads it below)
+      for (int qt = w; qt * 32 < Lq; qt += 4) {
+        const int q = qt * 32 + c;
+        const bool qvalid = q < Lq;
+        const int qq = qvalid ? q : Lq - 1;
+        const int64_t rowidx = bh * Lq + qq;
+        float sv[NKT][16];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt) {
+          if (kt < nkt) {
+            const int row = kt * 32 + c;
+            const float* kr = Ks + row * ROWF;
+            const int sw = fs_swz(row);
+            f32x16 acc = zero16();
+#pragma unroll
+            for (int s8 = 0; s8 < HALF; s8 += 8) {
+              const int j = (h * HALF + s8) >> 2;    // 16-B chunk of the head row
+              const float4 a0 = *reinterpret_cast<const float4*>(kr + 4 * (j ^ sw));
+              const float4 a1 = *reinterpret_cast<const float4*>(kr + 4 * ((j + 1) ^ sw));
+              const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+              float bv[8];
+#pragma unroll
+              for (int e = 0; e < 8; ++e) bv[e] = qf[s8 + e];
+              acc = mfma_k16<BF>(av, bv, acc);
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              sv[kt][r] = acc[r];
+              mx = fmaxf(mx, acc[r]);
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sv[kt][r] = 0.f;
+          }
+        }
+        // the fragment registers are free: the next query tile (or the next item's first)
+        if ((qt + 4) * 32 < Lq) fs_load_q(P, cur, qt + 4, c, h, qf);
+        else if (more) { fs_load_q(P, nxt, w, c, h, qf); loaded = true; }
+        mx = max_xor32(mx);
+        const float mc = mx * c2;
+        float l = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt) {
+          if (kt < nkt) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const float e = fast_exp2(fmaf(sv[kt][r], c2, -mc));
+              sv[kt][r] = e;
+              l += e;
+            }
+          }
+        }
+        l = sum_xor32(l);
+        const float f = qvalid ? (pdrop > 0.f ? inv_keep : 1.f) / l : 0.f;
+        uint32_t words[NKT];
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt) {
+          words[kt] = 0u;
+          if (kt < nkt) {
+            // (the other workgroups' MFMAs overlap this wave's draws: no lockstep here)
+            const uint32_t kb16 =
+                DROP ? keep_tile16(rs, P.drop_site, (uint64_t)rowidx * Lk + kt * 32, pdrop, h, true, true) : 0xFFFFu;
+            uint32_t bits = 0;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) bits |= ((kb16 >> (4 * g)) & 0xFu) << (8 * g + 4 * h);
+            words[kt] = or_xor32(bits);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sv[kt][r] = ((kb16 >> r) & 1u) ? sv[kt][r] * f : 0.f;
+            colacc[kt] += colsum_tile(sv[kt], c);
+          }
+        }
+        if (qvalid && h == 0) {
+          P.lse[rowidx] = mx * A.scale + __logf(l);
+          if (P.keep_bits && pdrop > 0.f)
+            *reinterpret_cast<uint4*>(P.keep_bits + rowidx * 4) =
+                make_uint4(words[0], NKT > 1 ? words[1] : 0u, NKT > 2 ? words[2] : 0u, NKT > 3 ? words[3] : 0u);
+        }
+      }
+      if (more && !loaded) fs_load_q(P, nxt, w, c, h, qf);
+      if ((c & 1) == 0) {
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt)
+          if (kt < nkt) cs[w][kt * 32 + acc_row((c >> 1) & 15, h)] = colacc[kt];
+      }
+      __syncthreads();
+      const float inv_lq = 1.f / (float)Lq;
+      for (int k = t; k < Lk; k += NT) {
+        const float v = ((cs[0][k] + cs[1][k]) + (cs[2][k] + cs[3][k])) * inv_lq;
+        pbar[k] = v;
+        if (P.pbarT) P.pbarT[((int64_t)cur.b * Lk + k) * A.heads + cur.head] = v;
+      }
+    }
+    // the next item's K image and query fragment have landed; every wave is done with
+    // this item's image and cs before either is overwritten
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    cur = nxt;
   }
 }
 
@@ -1433,7 +1656,7 @@ __global__ __launch_bounds__(NT) void attn_pool_bwd_dq_lean(const AttnArgs A) {
       }
     }
   }
-  D += __shfl_xor(D, 32);
+  D = sum_xor32(D);
   if (qvalid && h == 0) P.dsum[rowidx] = D;
   f32x16 dq[NDT];
 #pragma unroll
@@ -1647,9 +1870,9 @@ __device__ __forceinline__ void fused_lean_item(const AttnArgs& A, const AttnPai
   const int key = w * 32 + c;                 // dK phase: this wave's keys
   const bool kwave = w * 32 < Lk;
 
-  MMF_STAMP_RT(7)
-  MMF_STAMP(0)
-  MMF_STAMP_ID()
+  BSTAMP_RT(7)
+  BSTAMP(0)
+  BSTAMP_ID()
   if (LD.msk == 0.f) {
     // fully masked sample: P = 0 -> dQ = dK = 0
     if (qvalid)
@@ -1670,7 +1893,7 @@ __device__ __forceinline__ void fused_lean_item(const AttnArgs& A, const AttnPai
   const uint32_t kwa[4] = {LD.kw.x, LD.kw.y, LD.kw.z, LD.kw.w};
   (void)pdrop;
   __syncthreads();
-  MMF_STAMP(1)
+  BSTAMP(1)
 
   float qf[HALF];
   load_frag_vec<HALF>(qf, Qs + q * LS + h * HALF);
@@ -1701,9 +1924,9 @@ __device__ __forceinline__ void fused_lean_item(const AttnArgs& A, const AttnPai
       for (int r = 0; r < 16; ++r) pr[kt][r] = 0.f;
     }
   }
-  D += __shfl_xor(D, 32);
-  MMF_STAMP(2)
-  MMF_STAMP(3)
+  D = sum_xor32(D);
+  BSTAMP(2)
+  BSTAMP(3)
   // dQ = scale dS K (query on the lane; dS is the B operand); dS = P . (G - D) is formed
   // tile by tile, right before its chain, so that VALU work overlaps the previous chain
   {
@@ -1741,7 +1964,7 @@ MMF_CHAIN16(dq[dt], Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], pr[kt][r])
         }
     }
   }
-  MMF_STAMP(4)
+  BSTAMP(4)
   // dK = scale dS^T Q (key on the lane), over four 32-query quarters of dS^T
   // staged in the K image (K is dead once every wave is past the dQ phase)
   f32x16 dk[NDT];
@@ -1779,7 +2002,7 @@ MMF_CHAIN16(dq[dt], Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], pr[kt][r])
       }
     }
   }
-  MMF_STAMP(5)
+  BSTAMP(5)
   if (!kwave) return;
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) {
@@ -1789,8 +2012,8 @@ MMF_CHAIN16(dq[dt], Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], pr[kt][r])
     for (int r = 0; r < 16; ++r)
       P.dk[((int64_t)b * Lk + w * 32 + acc_row(r, h)) * P.ldk + col0 + d] = dk[dt][r] * scale;
   }
-  MMF_STAMP(6)
-  MMF_STAMP_RT(8)
+  BSTAMP(6)
+  BSTAMP_RT(8)
 }
 
 template <int HDP, bool BF>
@@ -1844,6 +2067,9 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
            (((uintptr_t)P.q & 15) == 0) && (((uintptr_t)P.k & 15) == 0) &&
            (kind != Kind::PoolDq || (((uintptr_t)P.dq & 15) == 0));
   }
+  // head_dim 32 lean forward: the persistent double-buffered kernel (opt-in: MMF_FWD_STREAM=1)
+  static const bool stream_env = getenv("MMF_FWD_STREAM") && getenv("MMF_FWD_STREAM")[0] == '1';
+  const bool stream = kind == Kind::PoolFwd && lean && hd == 32 && stream_env;
   if (kind == Kind::PoolFused) {
     // lean conditions plus a single query block and float4-able dQ rows
     for (int i = 0; i < npairs && lean; ++i)
@@ -1928,7 +2154,7 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
         {"attn_poolL_dq_kernel<32>", "attn_poolL_dq_kernel<64>", "", ""}};
     const bool alt = kind == Kind::Prep ? prep_vec : (lean && kind <= Kind::PoolFused);
     const bool bf = math_bf16();
-    const char* kname = kNames[(int)kind][(alt ? 2 : 0) + (small ? 0 : 1)];
+    const char* kname = stream ? "attn_pool_fwd_stream<>" : kNames[(int)kind][(alt ? 2 : 0) + (small ? 0 : 1)];
     ProfLaunch prof_(st, with_bf(kname, bf), fl, by);
     switch (kind) {
       case Kind::PoolLse:
@@ -1964,8 +2190,20 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
         else { if (bf) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_bwd_dq_kernel<64, false>), grid, dim3(NT), 0, st, a); }
         break;
       case Kind::PoolFwd:
-        if (lean && small) { if (bf) hipLaunchKernelGGL((attn_pool_fwd_lean<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_fwd_lean<32, false>), grid, dim3(NT), 0, st, a); }
-        else if (lean) { if (bf) hipLaunchKernelGGL((attn_pool_fwd_lean<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_fwd_lean<64, false>), grid, dim3(NT), 0, st, a); }
+        if (stream) {
+          // persistent: one wave of resident workgroups walks every (pair, sample, head) item
+          const int per_pair = B * heads;
+          const int nx = std::max(1, std::min(per_pair, (3 * device_cu_count() + n - 1) / n));
+          const dim3 sg(nx, n);
+          if (a.drop_p > 0.f) { if (bf) hipLaunchKernelGGL((attn_pool_fwd_stream<true, true>), sg, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_fwd_stream<false, true>), sg, dim3(NT), 0, st, a); }
+          else { if (bf) hipLaunchKernelGGL((attn_pool_fwd_stream<true, false>), sg, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_fwd_stream<false, false>), sg, dim3(NT), 0, st, a); }
+        } else if (lean && a.drop_p > 0.f) {
+          if (small) { if (bf) hipLaunchKernelGGL((attn_pool_fwd_lean<32, true, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_fwd_lean<32, false, true>), grid, dim3(NT), 0, st, a); }
+          else { if (bf) hipLaunchKernelGGL((attn_pool_fwd_lean<64, true, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_fwd_lean<64, false, true>), grid, dim3(NT), 0, st, a); }
+        } else if (lean) {
+          if (small) { if (bf) hipLaunchKernelGGL((attn_pool_fwd_lean<32, true, false>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_fwd_lean<32, false, false>), grid, dim3(NT), 0, st, a); }
+          else { if (bf) hipLaunchKernelGGL((attn_pool_fwd_lean<64, true, false>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_fwd_lean<64, false, false>), grid, dim3(NT), 0, st, a); }
+        }
         else if (small) { if (bf) hipLaunchKernelGGL((attn_pool_fwd_kernel<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_fwd_kernel<32, false>), grid, dim3(NT), 0, st, a); }
         else { if (bf) hipLaunchKernelGGL((attn_pool_fwd_kernel<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_fwd_kernel<64, false>), grid, dim3(NT), 0, st, a); }
         break;

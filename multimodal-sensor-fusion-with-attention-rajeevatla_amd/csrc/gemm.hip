@@ -526,12 +526,22 @@ __global__ __launch_bounds__(NT, 2) void gemm_wsr_kernel(const GemmArgs args, in
     rowtile = item - args.tile_off[g];
     return g;
   };
+  // DMA cursor: (item, k-tile) advance monotonically, so the group is tracked
+  // incrementally (a 32-way tile_off search per issue held all 32 offsets in
+  // SGPRs and spilled them)
+  int di = item0, dk = 0, drt = 0;
+  int dg = item_group(item0, drt);
+  const int g_first = dg, rt_first = drt;
   auto issue = [&](int f) {
-    int rt;
-    const int g = item_group(item0 + f / nkt, rt);
-    const GemmSrc& S = args.s[args.g[g].src_begin];
-    stage_tile<MODE_RK, WSR_DK>(ring + (f % WSR_NS) * DTILE, S.a, 0, rt * BM, args.g[g].M, (f % nkt) * WSR_DK, K,
-                                wave, lane);
+    const int slot = f % WSR_NS;
+    const GemmSrc& S = args.s[args.g[dg].src_begin];
+    stage_tile<MODE_RK, WSR_DK>(ring + slot * DTILE, S.a, 0, drt * BM, args.g[dg].M, dk * WSR_DK, K, wave, lane);
+    if (++dk == nkt) {
+      dk = 0;
+      ++di;
+      ++drt;
+      while (dg + 1 < args.ngroups && di >= args.tile_off[dg + 1]) { ++dg; drt = di - args.tile_off[dg]; }
+    }
   };
   // Wait for k-tile f: every later k-tile (2 LDS-DMAs per wave each) and the
   // epilogue stores issued after it (16 per wave per tile, exact: WSR tiles are
@@ -566,9 +576,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_wsr_kernel(const GemmArgs args, in
   int cur_g = -1;
   int f = 0;
   int epi_mark = 0;   // k-tiles issued before the latest epilogue's stores
-  for (int item = item0; item < item1; ++item) {
-    int rt;
-    const int g = item_group(item, rt);
+  int g = g_first, rt = rt_first;   // compute cursor (the same walk as the DMA cursor, behind it)
+  for (int item = item0; item < item1; ++item, ++rt) {
+    while (g + 1 < args.ngroups && item >= args.tile_off[g + 1]) { ++g; rt = item - args.tile_off[g]; }
     const GemmGroup& G = args.g[g];
     if (g != cur_g) {
       // this group's W^T slice for the wave's 64 columns, in the A fragments' k-order:
@@ -663,15 +673,15 @@ if constexpr (BF) {
           // v[r] = M[r][x]; step 1 swaps the off-diagonal 2x2 blocks (partner x^2)
           {
             const bool up = (x & 2) != 0;
-            const float s0 = __shfl_xor(up ? v[0] : v[2], 2);
-            const float s1 = __shfl_xor(up ? v[1] : v[3], 2);
+            const float s0 = dpp<DPP_XOR2>(up ? v[0] : v[2]);
+            const float s1 = dpp<DPP_XOR2>(up ? v[1] : v[3]);
             if (up) { v[0] = s0; v[1] = s1; } else { v[2] = s0; v[3] = s1; }
           }
           // now lane x holds M[x&2 .. +1][x&1 + (0|2)]; step 2 swaps within 2x2 (partner x^1)
           {
             const bool odd = (x & 1) != 0;
-            const float s0 = __shfl_xor(odd ? v[0] : v[1], 1);
-            const float s1 = __shfl_xor(odd ? v[2] : v[3], 1);
+            const float s0 = dpp<DPP_XOR1>(odd ? v[0] : v[1]);
+            const float s1 = dpp<DPP_XOR1>(odd ? v[2] : v[3]);
             if (odd) { v[0] = s0; v[2] = s1; } else { v[1] = s0; v[3] = s1; }
           }
           const int row = i0 + a * 32 + 8 * q + 4 * h + x;
@@ -882,9 +892,7 @@ __global__ __launch_bounds__(256) void small_slab_kernel(const SmallSlabArgs a) 
     if (k0 + 8 * u >= k1) break;
     acc = fmaf(av[u], bv[u], acc);
   }
-  acc += __shfl_xor(acc, 1);
-  acc += __shfl_xor(acc, 2);
-  acc += __shfl_xor(acc, 4);
+  acc = sum8(acc);
   if (!live || q != 0) return;
   if (bias)
     G.part_db[((int64_t)batch * G.nsplit + split) * G.M + i] = acc * G.alpha;

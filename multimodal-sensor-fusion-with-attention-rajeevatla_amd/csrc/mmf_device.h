@@ -47,8 +47,69 @@ __device__ __forceinline__ f32x16 mfma_k16(const float (&a)[8], const float (&b)
   }
 }
 
+// ---------------------------------------------------------------- cross-lane without LDS
+// gfx950 v_permlane{16,32}_swap and DPP moves instead of ds_bpermute (__shfl_xor):
+// no LDS round trip, and the DPP move folds into the consuming VALU op.
+// permlane16_swap(x, y): x' = [x.r0, y.r0, x.r2, y.r2], y' = [x.r1, y.r1, x.r3, y.r3]
+// (rows of 16 lanes); permlane32_swap(x, y): x' = [x.lo, y.lo], y' = [x.hi, y.hi]
+// (measured, scripts/micro/lane_micro.cpp).
+__device__ __forceinline__ void swap16(float& x, float& y) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+  x = __uint_as_float(r[0]);
+  y = __uint_as_float(r[1]);
+}
+__device__ __forceinline__ void swap32(float& x, float& y) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+  x = __uint_as_float(r[0]);
+  y = __uint_as_float(r[1]);
+}
+__device__ __forceinline__ uint32_t swap32u_partner(uint32_t x, bool upper) {   // x of lane ^ 32
+  const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return upper ? r[0] : r[1];
+}
+// max / sum of a value over the lane pair (l, l ^ 32); every lane gets the result
+__device__ __forceinline__ float max_xor32(float v) {
+  float a = v, b = v;
+  swap32(a, b);
+  return fmaxf(a, b);
+}
+__device__ __forceinline__ float sum_xor32(float v) {
+  float a = v, b = v;
+  swap32(a, b);
+  return a + b;
+}
+__device__ __forceinline__ uint32_t or_xor32(uint32_t v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return r[0] | r[1];
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+constexpr int DPP_ROR8 = 0x128, DPP_HALF_MIRROR = 0x141, DPP_XOR2 = 0x4E, DPP_XOR1 = 0xB1;
+
+// all-reduce sums without LDS.  Pairings: lane ^ 16 (permlane16_swap), ^ 8 (row_ror:8),
+// the 8-lane mirror (lane ^ 7: disjoint from the pairs before it), ^ 2, ^ 1; every
+// lane ends with the same bits.
+__device__ __forceinline__ float sum8(float v) {   // over lanes (l & ~7) .. +7
+  v += dpp<DPP_XOR1>(v);
+  v += dpp<DPP_XOR2>(v);
+  return v + dpp<DPP_HALF_MIRROR>(v);
+}
+__device__ __forceinline__ float sum32(float v) {  // over the lane's half (32 lanes)
+  float a = v, b = v;
+  swap16(a, b);
+  v = a + b;
+  v += dpp<DPP_ROR8>(v);
+  return sum8(v);
+}
+__device__ __forceinline__ float sum64(float v) { return sum32(sum_xor32(v)); }
+
 // ---------------------------------------------------------------- Philox4x32-10
 __device__ __forceinline__ uint4 philox10(uint4 c, uint32_t k0, uint32_t k1) {
+  // the key schedule is rebuilt per call (2 SALU per round): hoisted, its 20 words
+  // stay live in SGPRs across whole loops and spill in the register-tight kernels
+  asm volatile("" : "+s"(k0), "+s"(k1));
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
     // one v_mad_u64_u32 per 32x32->64 product (hi and lo together)
@@ -56,7 +117,9 @@ __device__ __forceinline__ uint4 philox10(uint4 c, uint32_t k0, uint32_t k1) {
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
     const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
     const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+    // three-input XORs as one v_bitop3_b32 each (gfx950): -25% per Philox call, same bits
+    c = make_uint4(__builtin_amdgcn_bitop3_b32(hi1, c.y, k0, 0x96), lo1,
+                   __builtin_amdgcn_bitop3_b32(hi0, c.w, k1, 0x96), lo0);
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }
@@ -133,7 +196,7 @@ __device__ __forceinline__ uint32_t keep_tile16(const RngSnap& s, uint32_t site,
         }
       }
     }
-    return mine | __shfl_xor(other, 32);
+    return mine | swap32u_partner(other, half != 0);
   }
   if (active) {
 #pragma unroll

@@ -23,11 +23,7 @@ constexpr int NT = 256;
 constexpr int MAXM = 8;
 constexpr int MAXHEADS = 8;
 
-__device__ __forceinline__ float wsum(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
+__device__ __forceinline__ float wsum(float v) { return sum64(v); }
 
 // GEMVs against L2-resident weights, over S samples of one workgroup: each
 // weight element is loaded once and feeds S accumulators.  Sample s's input
@@ -60,7 +56,7 @@ __device__ __forceinline__ void gemv_nt_s(const float* xs, int xsamp, int xdiv, 
     }
 #pragma unroll
     for (int q = 0; q < S; ++q) {
-      const float v = acc[q] + __shfl_xor(acc[q], 1);
+      const float v = acc[q] + dpp<DPP_XOR1>(acc[q]);
       if (half == 0) y[q * ysamp + n] = v;
     }
   }
@@ -311,9 +307,7 @@ __global__ __launch_bounds__(NT) void tail_pair_bwd_kernel(const TailArgs a) {
 #pragma unroll
       for (int hh = 0; hh < MAXHEADS; ++hh) {
         if (hh < nh) {
-          float sv = acc[hh];
-#pragma unroll
-          for (int o = 16; o >= 1; o >>= 1) sv += __shfl_xor(sv, o);
+          const float sv = sum32(acc[hh]);
           if (l32 == 0 && j < Lk) P.dpbar[((int64_t)b * nh + hh) * Lk + j] = sv + dr_s[si * MAXHEADS + hh];
         }
       }

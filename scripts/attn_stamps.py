@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Phase shares of the fused attention backward from the diagnostic stamp build.
 
-Build: make -C <pkg>/csrc stamps.  Run (box):
+Build: make -C <pkg>/csrc stamps (stampsf for the forward, argument "fwd").  Run (box):
   MMF_LIB_PATH=<pkg>/csrc/libmmfusion_stamps.so MMF_ATTN_BWD=v1 python scripts/attn_stamps.py
 Stamps (s_memtime, wave 0 of every workgroup): 0 start, 1 K/Q images loaded, 2 S/P/D,
 3 dS, 4 dQ stored, 5 dK quarters, 6 dK stored.  Prints per-phase mean cycles, the
@@ -41,7 +41,7 @@ def main():
     occ = (ctypes.c_int * 2)()
     L.mmf_attn_occupancy(occ)
     print("runtime occupancy (blocks/CU): fused bwd", occ[0], "pooled fwd", occ[1], flush=True)
-    reader = L.mmf_stamps_read if kernel == "attn" else L.mmf_tail_stamps_read
+    reader = L.mmf_stamps_read if kernel in ("attn", "fwd") else L.mmf_tail_stamps_read
     reader.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     for _ in range(3):
         step.forward_backward()
@@ -51,6 +51,9 @@ def main():
     if kernel == "attn":
         nwg, nst = 6 * w["B"] * w["heads"], 7
         names_ph = ["load", "S/P/D", "dS", "dQ", "dK quarters", "dK store"]
+    elif kernel == "fwd":   # attn_pool_fwd_lean, libmmfusion_stampsf.so (make stampsf)
+        nwg, nst = 6 * w["B"] * w["heads"], 6
+        names_ph = ["K/Q load", "S = K Q^T + max", "exp + sum", "dropout + colsum", "pbar store"]
     else:   # tail_pair_fwd_kernel: grid (B, pairs)
         nwg, nst = 6 * w["B"], 6
         names_ph = ["pbar + r", "U = pbar P_k", "Obar GEMV", "Abar GEMV", "stores"]
@@ -74,7 +77,7 @@ def main():
         spans.append(span)
         # mean workgroups resident = sum of lifetimes / span
         resid.append(float((st[sel, last] - st[sel, 0]).sum() / span))
-    if kernel == "attn":
+    if kernel in ("attn", "fwd"):
         rt = (buf[:nwg, 8].astype(np.int64) - buf[:nwg, 7].astype(np.int64))
         ok = rt > 0
         out["shader_clock_ghz_median"] = float(np.median((st[ok, last] - st[ok, 0]) / rt[ok] * 0.1))
