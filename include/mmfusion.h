@@ -304,6 +304,16 @@ size_t mmf_grad_clip_workspace_bytes(void);
 int mmf_grad_clip_coef(int64_t n, const float* grad, float grad_scale, float max_norm, float* total_norm,
                        float* clip_coef, void* workspace, void* stream);
 
+/* mmf_grad_clip_coef followed by mmf_adamw_step_dev in two launches instead of
+ * four (sum-of-squares partials; then every AdamW block re-reduces them itself):
+ * the same total_norm / clip_coef outputs (either may be NULL) and the same
+ * update, step_dev advanced by one.  workspace: mmf_grad_clip_workspace_bytes().
+ * Replaces the clip_grad_norm_ + AdamW pair of src/train.py:374-430. */
+int mmf_clip_adamw_step_dev(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                            int64_t* step_dev, const float* lr_dev, float max_norm, float* total_norm,
+                            float* clip_coef, void* workspace, float beta1, float beta2, float eps,
+                            float weight_decay, float grad_scale, void* stream);
+
 /* Timing for the benchmark: between begin and end every launch group AND
  * every kernel launch of the entry points above is bracketed by hipEvents on
  * its stream.  end() synchronises those events and writes tab-separated lines

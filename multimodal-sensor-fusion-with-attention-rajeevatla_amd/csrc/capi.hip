@@ -400,6 +400,20 @@ int mmf_grad_clip_coef(int64_t n, const float* grad, float grad_scale, float max
   return MMF_OK;
 }
 
+int mmf_clip_adamw_step_dev(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                            int64_t* step_dev, const float* lr_dev, float max_norm, float* total_norm,
+                            float* clip_coef, void* workspace, float beta1, float beta2, float eps,
+                            float weight_decay, float grad_scale, void* stream) {
+  if (n < 0 || !param || !grad || !exp_avg || !exp_avg_sq || !step_dev || !lr_dev || !workspace)
+    return fail(MMF_EINVAL, "bad clip+AdamW arguments");
+  if (reinterpret_cast<uintptr_t>(grad) & 15) return fail(MMF_EINVAL, "clip+AdamW: grad must be 16-byte aligned");
+  hipStream_t st = (hipStream_t)stream;
+  STAGE_TRY("optim.clip_adamw", launch_clip_adamw(n, param, grad, exp_avg, exp_avg_sq, step_dev, lr_dev, beta1,
+                                                  beta2, eps, weight_decay, grad_scale, max_norm, total_norm,
+                                                  clip_coef, (float*)workspace, st));
+  return MMF_OK;
+}
+
 int mmf_adamw_step_dev(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                        int64_t* step_dev, const float* lr_dev, const float* grad_coef_dev, float beta1,
                        float beta2, float eps, float weight_decay, float grad_scale, void* stream) {

@@ -258,9 +258,11 @@ __global__ __launch_bounds__(NT) void cross_entropy_kernel(int B, int C, const f
 constexpr int CLIP_BLOCKS = 256;
 
 __global__ __launch_bounds__(NT) void grad_sumsq_kernel(int64_t n, const float* __restrict__ g,
-                                                        float* __restrict__ partial) {
+                                                        float* __restrict__ partial, int64_t* step_incr) {
   __shared__ float red[NT];
   const int t = threadIdx.x;
+  // fused clip + AdamW: the step counter advances here, one launch before the update reads it
+  if (step_incr && blockIdx.x == 0 && t == 0) *step_incr = *step_incr + 1;
   float acc = 0.f;
   const int64_t n4 = n / 4;
   const float4* g4 = reinterpret_cast<const float4*>(g);
@@ -279,10 +281,10 @@ __global__ __launch_bounds__(NT) void grad_sumsq_kernel(int64_t n, const float* 
   if (t == 0) partial[blockIdx.x] = red[0];
 }
 
-// total_norm = gscale * sqrt(sum); coef = min(1, max_norm / (total_norm + 1e-6)) (1 when max_norm <= 0)
-__global__ __launch_bounds__(NT) void clip_coef_kernel(const float* __restrict__ partial, float gscale,
-                                                       float max_norm, float* norm_out, float* coef_out) {
-  __shared__ double red[NT];
+// total_norm = gscale * sqrt(sum); coef = min(1, max_norm / (total_norm + 1e-6)) (1 when max_norm <= 0).
+// Every thread of the block gets the same norm / coef (fixed tree order).
+__device__ __forceinline__ void clip_norm_coef(const float* __restrict__ partial, float gscale, float max_norm,
+                                               double* red, float& norm, float& coef) {
   const int t = threadIdx.x;
   double acc = 0.0;
   for (int i = t; i < CLIP_BLOCKS; i += NT) acc += (double)partial[i];
@@ -292,10 +294,17 @@ __global__ __launch_bounds__(NT) void clip_coef_kernel(const float* __restrict__
     if (t < s) red[t] += red[t + s];
     __syncthreads();
   }
-  if (t == 0) {
-    const float norm = (float)(sqrt(red[0]) * (double)gscale);
-    float coef = 1.f;
-    if (max_norm > 0.f) coef = fminf(1.f, max_norm / (norm + 1e-6f));
+  norm = (float)(sqrt(red[0]) * (double)gscale);
+  coef = 1.f;
+  if (max_norm > 0.f) coef = fminf(1.f, max_norm / (norm + 1e-6f));
+}
+
+__global__ __launch_bounds__(NT) void clip_coef_kernel(const float* __restrict__ partial, float gscale,
+                                                       float max_norm, float* norm_out, float* coef_out) {
+  __shared__ double red[NT];
+  float norm, coef;
+  clip_norm_coef(partial, gscale, max_norm, red, norm, coef);
+  if (threadIdx.x == 0) {
     if (norm_out) norm_out[0] = norm;
     coef_out[0] = coef;
   }
@@ -318,6 +327,41 @@ __global__ __launch_bounds__(NT) void adamw_kernel(int64_t n, float* __restrict_
   const float step_size = lr / bc1;
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
     const float gi = g[i] * gscale;
+    float pi = p[i] * (1.f - lr * wd);
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    pi -= step_size * mi / (sqrtf(vi) / bc2s + eps);
+    p[i] = pi;
+  }
+}
+
+// Clip + AdamW in one launch after grad_sumsq_kernel (which advanced *step): every
+// block re-reduces the CLIP_BLOCKS partials itself (the same bits as clip_coef_kernel),
+// block 0 publishes norm / coef.  Same update as adamw_kernel at step *step.
+__global__ __launch_bounds__(NT) void clip_adamw_kernel(int64_t n, float* __restrict__ p,
+                                                        const float* __restrict__ g, float* __restrict__ m,
+                                                        float* __restrict__ v, const int64_t* step,
+                                                        const float* __restrict__ lr_dev, float b1, float b2,
+                                                        float eps, float wd, float gscale,
+                                                        const float* __restrict__ partial, float max_norm,
+                                                        float* norm_out, float* coef_out) {
+  __shared__ double red[NT];
+  float norm, coef;
+  clip_norm_coef(partial, gscale, max_norm, red, norm, coef);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (norm_out) norm_out[0] = norm;
+    if (coef_out) coef_out[0] = coef;
+  }
+  const float lr = lr_dev[0];
+  const float gs = gscale * coef;
+  const double st = (double)(*step);
+  const float bc1 = (float)(1.0 - pow((double)b1, st));
+  const float bc2s = (float)sqrt(1.0 - pow((double)b2, st));
+  const float step_size = lr / bc1;
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+    const float gi = g[i] * gs;
     float pi = p[i] * (1.f - lr * wd);
     const float mi = b1 * m[i] + (1.f - b1) * gi;
     const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
@@ -381,7 +425,7 @@ hipError_t launch_grad_clip_coef(int64_t n, const float* g, float gscale, float 
                                  float* coef_out, float* partial, hipStream_t st) {
   {
     ProfLaunch prof_(st, "grad_sumsq_kernel", 2.0 * n, 4.0 * n);
-    hipLaunchKernelGGL(grad_sumsq_kernel, dim3(CLIP_BLOCKS), dim3(NT), 0, st, n, g, partial);
+    hipLaunchKernelGGL(grad_sumsq_kernel, dim3(CLIP_BLOCKS), dim3(NT), 0, st, n, g, partial, (int64_t*)nullptr);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -403,6 +447,24 @@ hipError_t launch_adamw(int64_t n, float* p, const float* g, float* m, float* v,
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(step_incr_kernel, dim3(1), dim3(64), 0, st, step);
+  return hipGetLastError();
+}
+
+hipError_t launch_clip_adamw(int64_t n, float* p, const float* g, float* m, float* v, int64_t* step,
+                             const float* lr_dev, float b1, float b2, float eps, float wd, float gscale,
+                             float max_norm, float* norm_out, float* coef_out, float* partial, hipStream_t st) {
+  {
+    ProfLaunch prof_(st, "grad_sumsq_kernel", 2.0 * n, 4.0 * n);
+    hipLaunchKernelGGL(grad_sumsq_kernel, dim3(CLIP_BLOCKS), dim3(NT), 0, st, n, g, partial, step);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  int64_t blocks = (n + NT - 1) / NT;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  ProfLaunch prof_(st, "clip_adamw_kernel", 0.0, 28.0 * n);
+  hipLaunchKernelGGL(clip_adamw_kernel, dim3((unsigned)blocks), dim3(NT), 0, st, n, p, g, m, v, (const int64_t*)step,
+                     lr_dev, b1, b2, eps, wd, gscale, (const float*)partial, max_norm, norm_out, coef_out);
   return hipGetLastError();
 }
 

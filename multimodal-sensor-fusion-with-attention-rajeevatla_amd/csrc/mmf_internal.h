@@ -311,6 +311,10 @@ hipError_t launch_adamw(int64_t n, float* p, const float* g, float* m, float* v,
 size_t grad_clip_workspace_bytes();
 hipError_t launch_grad_clip_coef(int64_t n, const float* g, float gscale, float max_norm, float* norm_out,
                                  float* coef_out, float* partial, hipStream_t st);
+// grad_sumsq (advancing *step) + one clip-and-AdamW launch (mmf_clip_adamw_step_dev)
+hipError_t launch_clip_adamw(int64_t n, float* p, const float* g, float* m, float* v, int64_t* step,
+                             const float* lr_dev, float b1, float b2, float eps, float wd, float gscale,
+                             float max_norm, float* norm_out, float* coef_out, float* partial, hipStream_t st);
 
 }  // namespace mmf
 

@@ -159,7 +159,6 @@ __global__ __launch_bounds__(NT) void tail_pair_fwd_kernel(const TailArgs a) {
   const TailPair& P = a.p[blockIdx.y];
   const int t = threadIdx.x;
   const int H = a.H, nh = a.heads, hd = a.hd, Lk = P.Lk, H4 = H >> 2;
-  const int ncol = nh * H4;
   MMF_STAMP(0)
   MMF_STAMP_ID()
   for (int si = 0; si < S; ++si) {
@@ -180,42 +179,40 @@ __global__ __launch_bounds__(NT) void tail_pair_fwd_kernel(const TailArgs a) {
       P.r[(int64_t)b * nh + t] = s;
     }
     MMF_STAMP(1)
-    // U: tasks = (head, float4 column); RG row groups split the Lk keys
+    // U: thread (float4 column c4, row group rg) loads each P_k float4 once and feeds
+    // every head with it (one pass over P_k[b]); the RG row groups are summed in order
     const float* pk = P.Pk + (int64_t)b * Lk * H;
-    for (int task0 = 0; task0 < ncol; task0 += NT) {
-      const int nact = min(NT, ncol - task0);
-      const int RG = NT / nact;
-      const int task = task0 + t % nact, rg = t / nact;
-      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f), acc2 = acc;
-      if (rg < RG) {
-        const int hh = task / H4, c4 = task % H4;
-        int j = rg;
-#pragma unroll 4
-        for (; j + RG < Lk; j += 2 * RG) {
-          const float4 v = *reinterpret_cast<const float4*>(pk + (int64_t)j * H + 4 * c4);
-          const float4 u = *reinterpret_cast<const float4*>(pk + (int64_t)(j + RG) * H + 4 * c4);
-          const float w = pb_s[hh * Lk + j], w2 = pb_s[hh * Lk + j + RG];
-          acc.x += w * v.x; acc.y += w * v.y; acc.z += w * v.z; acc.w += w * v.w;
-          acc2.x += w2 * u.x; acc2.y += w2 * u.y; acc2.z += w2 * u.z; acc2.w += w2 * u.w;
-        }
-        if (j < Lk) {
-          const float4 v = *reinterpret_cast<const float4*>(pk + (int64_t)j * H + 4 * c4);
+    const int RG = NT / H4;
+    const int c4 = t % H4, rg = t / H4;
+    float4 acc[MAXHEADS];
+#pragma unroll
+    for (int hh = 0; hh < MAXHEADS; ++hh) acc[hh] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 2
+    for (int j = rg; j < Lk; j += RG) {
+      const float4 v = *reinterpret_cast<const float4*>(pk + (int64_t)j * H + 4 * c4);
+#pragma unroll
+      for (int hh = 0; hh < MAXHEADS; ++hh) {
+        if (hh < nh) {
           const float w = pb_s[hh * Lk + j];
-          acc.x += w * v.x; acc.y += w * v.y; acc.z += w * v.z; acc.w += w * v.w;
+          acc[hh].x += w * v.x; acc[hh].y += w * v.y; acc[hh].z += w * v.z; acc[hh].w += w * v.w;
         }
       }
-      __syncthreads();
-      red4[t] = make_float4(acc.x + acc2.x, acc.y + acc2.y, acc.z + acc2.z, acc.w + acc2.w);
-      __syncthreads();
-      if (t < nact) {
-        float4 sum = red4[t];
-        for (int g = 1; g < RG; ++g) {
-          const float4 v = red4[g * nact + t];
-          sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
+    }
+#pragma unroll
+    for (int hh = 0; hh < MAXHEADS; ++hh) {
+      if (hh < nh) {
+        __syncthreads();
+        red4[t] = acc[hh];
+        __syncthreads();
+        if (t < H4) {
+          float4 sum = red4[t];
+          for (int g = 1; g < RG; ++g) {
+            const float4 v = red4[g * H4 + t];
+            sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
+          }
+          *reinterpret_cast<float4*>(&us[hh * H + 4 * t]) = sum;
+          *reinterpret_cast<float4*>(P.U + ((int64_t)b * nh + hh) * H + 4 * t) = sum;
         }
-        const int tt = task0 + t;
-        *reinterpret_cast<float4*>(&us[4 * tt]) = sum;
-        *reinterpret_cast<float4*>(P.U + (int64_t)b * nh * H + 4 * tt) = sum;
       }
     }
   }

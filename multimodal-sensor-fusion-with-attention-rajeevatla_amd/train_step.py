@@ -193,14 +193,13 @@ class HybridTrainStep:
         L = _nat.lib()
         st = _nat.stream_ptr(self.dev)
         gscale = 1.0 / self.world
-        rc = L.mmf_grad_clip_coef(self.grad.numel(), self.grad.data_ptr(), gscale, float(self.clip_norm),
-                                  self.grad_norm.data_ptr(), self.clip_coef.data_ptr(), self.clip_ws.data_ptr(), st)
-        _nat.check(rc, "gradient clipping")
-        rc = L.mmf_adamw_step_dev(self.flat.numel(), self.flat.data_ptr(), self.grad.data_ptr(),
-                                  self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), self.step_dev.data_ptr(),
-                                  self.lr_dev.data_ptr(), self.clip_coef.data_ptr(), self.betas[0], self.betas[1],
-                                  self.eps, self.wd, gscale, st)
-        _nat.check(rc, "AdamW")
+        rc = L.mmf_clip_adamw_step_dev(self.flat.numel(), self.flat.data_ptr(), self.grad.data_ptr(),
+                                       self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
+                                       self.step_dev.data_ptr(), self.lr_dev.data_ptr(), float(self.clip_norm),
+                                       self.grad_norm.data_ptr(), self.clip_coef.data_ptr(),
+                                       self.clip_ws.data_ptr(), self.betas[0], self.betas[1], self.eps, self.wd,
+                                       gscale, st)
+        _nat.check(rc, "clip + AdamW")
 
     # ---------------------------------------------------------------- driver
     def capture(self) -> None:

@@ -115,3 +115,44 @@ def test_load_batch_rejects_new_shapes(mods):
         st.load_batch([f[:4].cuda() for f in feats], mask[:4].cuda(), labels[:4].cuda())
     with pytest.raises(ValueError, match="load_batch"):
         st.load_batch([f.cuda() for f in feats[:2]], mask.cuda(), labels.cuda())
+
+
+@pytest.mark.parametrize("max_norm", [0.05, 1e9])
+def test_fused_clip_adamw_matches_two_call_path(mods, max_norm):
+    """mmf_clip_adamw_step_dev (2 launches) == mmf_grad_clip_coef + mmf_adamw_step_dev (4), bit for bit."""
+    import mmf_native as nat
+    L = nat.lib()
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(7)
+    n = 70001                                   # not a multiple of 4: the scalar tail of the sum of squares
+    grad = torch.randn(n, generator=g).to(dev)
+    base = [torch.randn(n, generator=g).to(dev) for _ in range(3)]
+    base[2] = base[2].abs()
+    runs = []
+    for fused in (False, True):
+        p, m, v = (t.clone() for t in base)
+        step = torch.full((1,), 4, dtype=torch.int64, device=dev)
+        lr = torch.full((1,), 3e-3, dtype=torch.float32, device=dev)
+        norm = torch.zeros(1, device=dev)
+        coef = torch.zeros(1, device=dev)
+        ws = torch.empty(L.mmf_grad_clip_workspace_bytes(), dtype=torch.uint8, device=dev)
+        st = nat.stream_ptr(dev)
+        for _ in range(2):
+            if fused:
+                rc = L.mmf_clip_adamw_step_dev(n, p.data_ptr(), grad.data_ptr(), m.data_ptr(), v.data_ptr(),
+                                               step.data_ptr(), lr.data_ptr(), max_norm, norm.data_ptr(),
+                                               coef.data_ptr(), ws.data_ptr(), 0.9, 0.999, 1e-8, 1e-4, 0.5, st)
+                nat.check(rc, "fused")
+            else:
+                nat.check(L.mmf_grad_clip_coef(n, grad.data_ptr(), 0.5, max_norm, norm.data_ptr(), coef.data_ptr(),
+                                               ws.data_ptr(), st), "clip")
+                nat.check(L.mmf_adamw_step_dev(n, p.data_ptr(), grad.data_ptr(), m.data_ptr(), v.data_ptr(),
+                                               step.data_ptr(), lr.data_ptr(), coef.data_ptr(), 0.9, 0.999, 1e-8,
+                                               1e-4, 0.5, st), "adamw")
+        torch.cuda.synchronize()
+        runs.append((p, m, v, step, norm, coef))
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
+    assert int(runs[1][3].item()) == 6
+    if max_norm < 1.0:
+        assert float(runs[1][5].item()) < 1.0
