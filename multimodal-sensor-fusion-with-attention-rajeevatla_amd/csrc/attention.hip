@@ -1397,191 +1397,6 @@ __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(cons
   FSTAMP_RT(8)
 }
 
-// Persistent pooled forward for head_dim 32 (the lean case of the benchmark
-// shape): each workgroup walks items (pair, sample, head) with stride gridDim.x.
-// The next item's K image is DMA'd (global_load_lds, no VGPRs) into the other
-// half of a double buffer and its first query fragment loaded into registers
-// while the current item computes, so after the first item the MFMAs no longer
-// wait on a K/Q round trip (the lean kernel's workgroups all load, then all
-// compute, in lockstep: a quarter of their lifetime).  Same arithmetic and
-// outputs as attn_pool_fwd_lean<32>.
-// K image [PKC][32] floats, 128-B rows, 16-B slots XOR-swizzled by (row >> 1) & 7:
-// the 16 rows of a ds_read_b128 quarter-wave land on distinct bank groups.
-__device__ __forceinline__ int fs_swz(int row) { return (row >> 1) & 7; }
-
-struct FsItem { int b, head; };
-
-// this wave's quarter of the K image of an item (4 x 1 KB, rows past Lk skipped)
-__device__ __forceinline__ void fs_issue_k(const AttnPair& P, const FsItem& it, float* buf, int w, int lane) {
-  const float* base = P.k + (int64_t)it.b * P.Lk * P.ldk + it.head * 32;
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int ins = w * 4 + u;
-    if (ins * 8 < P.Lk) {
-      const int row = ins * 8 + (lane >> 3), slot = lane & 7;
-      const float* src = base + (int64_t)row * P.ldk + 4 * (slot ^ fs_swz(row));
-      __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(buf + ins * 256),
-                                       16, 0, 0);
-    }
-  }
-}
-
-__device__ __forceinline__ void fs_load_q(const AttnPair& P, const FsItem& it, int qt, int c, int h, float (&qf)[16]) {
-  load_frag_vec<16>(qf, P.q + ((int64_t)it.b * P.Lq + min(qt * 32 + c, P.Lq - 1)) * P.ldq + it.head * 32 + h * 16);
-}
-
-// grid (workgroups per pair, pairs): a workgroup walks the (sample, head) items of one pair
-template <bool BF, bool DROP>
-__global__ __launch_bounds__(NT, 3) void attn_pool_fwd_stream(const AttnArgs A) {
-  constexpr int HALF = 16, NKT = PKC / 32, ROWF = 32;
-  __shared__ __attribute__((aligned(16))) float Kb[2][PKC * ROWF];
-  __shared__ float cs[4][PKC];
-  const AttnPair& P = A.p[blockIdx.y];
-  const int total = A.B * A.heads;
-  const int t0 = threadIdx.x, lane = t0 & 63, w = t0 >> 6;
-  const float pdrop = DROP ? A.drop_p : 0.f;
-  const float inv_keep = pdrop < 1.f ? 1.f / (1.f - pdrop) : 0.f;
-  RngSnap rs{0, 0};
-  if (pdrop > 0.f && A.rng) rs = *A.rng;
-  const float c2 = A.scale * LOG2E;
-  const int Lq = P.Lq, Lk = P.Lk, nkt = Lk >> 5;
-
-  int item = blockIdx.x;
-  if (item >= total) return;
-  FsItem cur{item / A.heads, item % A.heads};
-  float qf[HALF];
-  fs_issue_k(P, cur, Kb[0], w, lane);
-  fs_load_q(P, cur, w, lane & 31, lane >> 5, qf);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int tt = t0, hh = lane >> 5, cc = lane & 31;
-  for (int buf = 0; item < total; item += gridDim.x, buf ^= 1) {
-    // launder the lane ids: otherwise every lane-derived address of the body is hoisted
-    // out of the item loop and held in VGPRs across it (spills)
-    asm volatile("" : "+v"(tt), "+v"(hh), "+v"(cc));
-    const int t = tt, h = hh, c = cc;
-    const int next = item + gridDim.x;
-    const bool more = next < total;
-    const FsItem nxt{next / A.heads, next % A.heads};
-    if (more) fs_issue_k(P, nxt, Kb[buf ^ 1], w, lane);
-    const int64_t bh = (int64_t)cur.b * A.heads + cur.head;
-    float* pbar = P.pbar + bh * Lk;
-    const float msk = P.kmask_mode == 1 ? P.kmask[(int64_t)cur.b * P.kmask_ld] : 1.f;
-    const float* Ks = Kb[buf];
-    if (msk == 0.f) {
-      for (int k = t; k < Lk; k += NT) pbar[k] = 0.f;
-      if (P.pbarT)
-        for (int k = t; k < Lk; k += NT) P.pbarT[((int64_t)cur.b * Lk + k) * A.heads + cur.head] = 0.f;
-      for (int q = t; q < Lq; q += NT) P.lse[bh * Lq + q] = -INFINITY;
-      if (P.keep_bits)
-        for (int q = t; q < Lq; q += NT)
-          *reinterpret_cast<uint4*>(P.keep_bits + (bh * Lq + q) * 4) = make_uint4(0, 0, 0, 0);
-      if (more) fs_load_q(P, nxt, w, c, h, qf);
-    } else {
-      float colacc[NKT];
-#pragma unroll
-      for (int kt = 0; kt < NKT; ++kt) colacc[kt] = 0.f;
-      bool loaded = false;   // the next item's first fragment (a wave without a query tile loads it below)
-      for (int qt = w; qt * 32 < Lq; qt += 4) {
-        const int q = qt * 32 + c;
-        const bool qvalid = q < Lq;
-        const int qq = qvalid ? q : Lq - 1;
-        const int64_t rowidx = bh * Lq + qq;
-        float sv[NKT][16];
-        float mx = -INFINITY;
-#pragma unroll
-        for (int kt = 0; kt < NKT; ++kt) {
-          if (kt < nkt) {
-            const int row = kt * 32 + c;
-            const float* kr = Ks + row * ROWF;
-            const int sw = fs_swz(row);
-            f32x16 acc = zero16();
-#pragma unroll
-            for (int s8 = 0; s8 < HALF; s8 += 8) {
-              const int j = (h * HALF + s8) >> 2;    // 16-B chunk of the head row
-              const float4 a0 = *reinterpret_cast<const float4*>(kr + 4 * (j ^ sw));
-              const float4 a1 = *reinterpret_cast<const float4*>(kr + 4 * ((j + 1) ^ sw));
-              const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-              float bv[8];
-#pragma unroll
-              for (int e = 0; e < 8; ++e) bv[e] = qf[s8 + e];
-              acc = mfma_k16<BF>(av, bv, acc);
-            }
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              sv[kt][r] = acc[r];
-              mx = fmaxf(mx, acc[r]);
-            }
-          } else {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) sv[kt][r] = 0.f;
-          }
-        }
-        // the fragment registers are free: the next query tile (or the next item's first)
-        if ((qt + 4) * 32 < Lq) fs_load_q(P, cur, qt + 4, c, h, qf);
-        else if (more) { fs_load_q(P, nxt, w, c, h, qf); loaded = true; }
-        mx = max_xor32(mx);
-        const float mc = mx * c2;
-        float l = 0.f;
-#pragma unroll
-        for (int kt = 0; kt < NKT; ++kt) {
-          if (kt < nkt) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const float e = fast_exp2(fmaf(sv[kt][r], c2, -mc));
-              sv[kt][r] = e;
-              l += e;
-            }
-          }
-        }
-        l = sum_xor32(l);
-        const float f = qvalid ? (pdrop > 0.f ? inv_keep : 1.f) / l : 0.f;
-        uint32_t words[NKT];
-#pragma unroll
-        for (int kt = 0; kt < NKT; ++kt) {
-          words[kt] = 0u;
-          if (kt < nkt) {
-            // (the other workgroups' MFMAs overlap this wave's draws: no lockstep here)
-            const uint32_t kb16 =
-                DROP ? keep_tile16(rs, P.drop_site, (uint64_t)rowidx * Lk + kt * 32, pdrop, h, true, true) : 0xFFFFu;
-            uint32_t bits = 0;
-#pragma unroll
-            for (int g = 0; g < 4; ++g) bits |= ((kb16 >> (4 * g)) & 0xFu) << (8 * g + 4 * h);
-            words[kt] = or_xor32(bits);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) sv[kt][r] = ((kb16 >> r) & 1u) ? sv[kt][r] * f : 0.f;
-            colacc[kt] += colsum_tile(sv[kt], c);
-          }
-        }
-        if (qvalid && h == 0) {
-          P.lse[rowidx] = mx * A.scale + __logf(l);
-          if (P.keep_bits && pdrop > 0.f)
-            *reinterpret_cast<uint4*>(P.keep_bits + rowidx * 4) =
-                make_uint4(words[0], NKT > 1 ? words[1] : 0u, NKT > 2 ? words[2] : 0u, NKT > 3 ? words[3] : 0u);
-        }
-      }
-      if (more && !loaded) fs_load_q(P, nxt, w, c, h, qf);
-      if ((c & 1) == 0) {
-#pragma unroll
-        for (int kt = 0; kt < NKT; ++kt)
-          if (kt < nkt) cs[w][kt * 32 + acc_row((c >> 1) & 15, h)] = colacc[kt];
-      }
-      __syncthreads();
-      const float inv_lq = 1.f / (float)Lq;
-      for (int k = t; k < Lk; k += NT) {
-        const float v = ((cs[0][k] + cs[1][k]) + (cs[2][k] + cs[3][k])) * inv_lq;
-        pbar[k] = v;
-        if (P.pbarT) P.pbarT[((int64_t)cur.b * Lk + k) * A.heads + cur.head] = v;
-      }
-    }
-    // the next item's K image and query fragment have landed; every wave is done with
-    // this item's image and cs before either is overwritten
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    cur = nxt;
-  }
-}
-
 // dq pass, query on the lane: G[k] = keep ? dpbar[k] / ((1-p) Lq) : 0;
 // D = rowsum(P . G) (saved for the dk pass); dS = P . (G - D); dQ = scale dS K.
 template <int HDP, bool BF>
@@ -2067,9 +1882,6 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
            (((uintptr_t)P.q & 15) == 0) && (((uintptr_t)P.k & 15) == 0) &&
            (kind != Kind::PoolDq || (((uintptr_t)P.dq & 15) == 0));
   }
-  // head_dim 32 lean forward: the persistent double-buffered kernel (opt-in: MMF_FWD_STREAM=1)
-  static const bool stream_env = getenv("MMF_FWD_STREAM") && getenv("MMF_FWD_STREAM")[0] == '1';
-  const bool stream = kind == Kind::PoolFwd && lean && hd == 32 && stream_env;
   if (kind == Kind::PoolFused) {
     // lean conditions plus a single query block and float4-able dQ rows
     for (int i = 0; i < npairs && lean; ++i)
@@ -2154,7 +1966,7 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
         {"attn_poolL_dq_kernel<32>", "attn_poolL_dq_kernel<64>", "", ""}};
     const bool alt = kind == Kind::Prep ? prep_vec : (lean && kind <= Kind::PoolFused);
     const bool bf = math_bf16();
-    const char* kname = stream ? "attn_pool_fwd_stream<>" : kNames[(int)kind][(alt ? 2 : 0) + (small ? 0 : 1)];
+    const char* kname = kNames[(int)kind][(alt ? 2 : 0) + (small ? 0 : 1)];
     ProfLaunch prof_(st, with_bf(kname, bf), fl, by);
     switch (kind) {
       case Kind::PoolLse:
@@ -2190,14 +2002,7 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
         else { if (bf) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_bwd_dq_kernel<64, false>), grid, dim3(NT), 0, st, a); }
         break;
       case Kind::PoolFwd:
-        if (stream) {
-          // persistent: one wave of resident workgroups walks every (pair, sample, head) item
-          const int per_pair = B * heads;
-          const int nx = std::max(1, std::min(per_pair, (3 * device_cu_count() + n - 1) / n));
-          const dim3 sg(nx, n);
-          if (a.drop_p > 0.f) { if (bf) hipLaunchKernelGGL((attn_pool_fwd_stream<true, true>), sg, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_fwd_stream<false, true>), sg, dim3(NT), 0, st, a); }
-          else { if (bf) hipLaunchKernelGGL((attn_pool_fwd_stream<true, false>), sg, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_fwd_stream<false, false>), sg, dim3(NT), 0, st, a); }
-        } else if (lean && a.drop_p > 0.f) {
+        if (lean && a.drop_p > 0.f) {
           if (small) { if (bf) hipLaunchKernelGGL((attn_pool_fwd_lean<32, true, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_fwd_lean<32, false, true>), grid, dim3(NT), 0, st, a); }
           else { if (bf) hipLaunchKernelGGL((attn_pool_fwd_lean<64, true, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_fwd_lean<64, false, true>), grid, dim3(NT), 0, st, a); }
         } else if (lean) {
