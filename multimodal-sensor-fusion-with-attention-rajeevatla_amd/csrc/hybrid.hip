@@ -317,6 +317,7 @@ void fill_tail(TailArgs& ta, const mmf_hybrid_desc* d, const mmf_hybrid_params* 
     P.Wv = W->v[g].w; P.bv = W->v[g].b; P.Wo = W->o[g].w; P.bo = W->o[g].b;
     P.Ob = s.Ob[g]; P.Ab = s.Ab[g];
     P.q = d->pair_q[g];
+    P.k = d->pair_k[g];
     cnt[d->pair_q[g]]++;
   }
   for (int m = 0; m < M; ++m) ta.inv_cnt[m] = 1.0f / (float)cnt[m];

@@ -335,6 +335,7 @@ namespace mmf {
 struct TailPair {
   const float* pbar; const float* Pk; int32_t Lk;   // (B, h, Lk) query-mean probs; key features (B, Lk, H)
   int32_t q;                                         // query modality of the pair
+  int32_t k;                                         // key modality of the pair
   float* U; float* r;                  // (B, h, H), (B, h) written by the forward
   const float* Wv; const float* bv; const float* Wo; const float* bo;
   float* Ob; float* Ab;                // (B, H) Obar (saved) and Abar
@@ -357,6 +358,10 @@ struct TailArgs {
   // backward
   const float* dlogits; float* dz1; float* cvec; float* dscore; float gscale;
   TailPair p[TAIL_MAX_PAIRS];
+  // pairs grouped by key modality (launch_tail_*: the P_k-side kernels read P_k[b] once per group)
+  int32_t nkg;
+  int32_t kg_cnt[8];
+  int8_t kg_pair[8][TAIL_MAX_PAIRS];
 };
 bool tail_supported(int M, int H, int C, int heads, int hd, int npairs);
 hipError_t launch_tail_fwd(const TailArgs& a, hipStream_t st);

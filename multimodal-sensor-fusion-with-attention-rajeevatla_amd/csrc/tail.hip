@@ -172,11 +172,14 @@ __global__ __launch_bounds__(NT) void tail_pair_fwd_kernel(const TailArgs a) {
     __syncthreads();   // pb_s of the previous sample consumed
     for (int i = t; i < nh * Lk; i += NT) pb_s[i] = P.pbar[(int64_t)b * nh * Lk + i];
     __syncthreads();
-    if (t < nh) {
+    for (int hh = t >> 6; hh < nh; hh += NT / 64) {   // r_h: one wave per head
       float s = 0.f;
-      for (int j = 0; j < Lk; ++j) s += pb_s[t * Lk + j];
-      r_s[si * MAXHEADS + t] = s;
-      P.r[(int64_t)b * nh + t] = s;
+      for (int j = t & 63; j < Lk; j += 64) s += pb_s[hh * Lk + j];
+      s = wsum(s);
+      if ((t & 63) == 0) {
+        r_s[si * MAXHEADS + hh] = s;
+        P.r[(int64_t)b * nh + hh] = s;
+      }
     }
     MMF_STAMP(1)
     // U: thread (float4 column c4, row group rg) loads each P_k float4 once and feeds
@@ -307,6 +310,322 @@ __global__ __launch_bounds__(NT) void tail_pair_bwd_kernel(const TailArgs a) {
           const float sv = sum32(acc[hh]);
           if (l32 == 0 && j < Lk) P.dpbar[((int64_t)b * nh + hh) * Lk + j] = sv + dr_s[si * MAXHEADS + hh];
         }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- MFMA pair tail
+// The pair tail as two kinds of launch per direction, on fp32 MFMA tiles
+// (v_mfma_f32_32x32x2_f32, exact f32 products) when hd % 32 == 0, H % 32 == 0
+// and at most 32 (pair, head) rows share a key modality:
+//  * P_k side, one workgroup per (sample, key modality k): every pair whose key
+//    is k reads P_k[b] once.  Forward U_{g,h} = pbar_{g,h} P_k and r_{g,h} =
+//    sum_j pbar_{g,h}[j]; backward dpbar_{g,h} = P_k dU_{g,h} + dObar_{g,h} . b_v,h.
+//    The (pair, head) rows are one 32-row MFMA tile.
+//  * weight side, one workgroup per (pair, 32 samples): forward Obar = U W_v^T
+//    (per head) + r b_v, Abar = Obar W_o^T + b_o; backward dObar = c_q W_o and
+//    dU_h = dObar_h W_v[h rows].  A weight element is read once per 32 samples
+//    (the per-sample GEMV kernels above read the 128 KB of W_v, W_o per sample).
+// MFMA k order: within each 8-deep chunk, lane half hf feeds k = 8 q + 4 hf + s at
+// step s (one float4 per lane and chunk for row-contiguous operands).
+constexpr int KG_ROWS = 32;
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+__device__ __forceinline__ f32x16 mfma4(const float4& a, const float4& b, f32x16 acc) {
+  acc = mfma32(a.x, b.x, acc);
+  acc = mfma32(a.y, b.y, acc);
+  acc = mfma32(a.z, b.z, acc);
+  return mfma32(a.w, b.w, acc);
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) z[r] = 0.f;
+  return z;
+}
+
+// Forward, P_k side: grid (B, key groups).  Thread (float4 column c4, row group rg)
+// loads its Lk / RG rows of P_k[b] at once (before the pbar rows are staged) and
+// accumulates eight (pair, head) rows per pass; the row groups are summed in order.
+__global__ __launch_bounds__(NT, 3) void tail_u_kernel(const TailArgs a) {
+  constexpr int PS = 128 + 4;   // pbar image pitch (keys <= 128)
+  constexpr int RPT = 16;       // P_k rows per thread and batch
+  __shared__ __attribute__((aligned(16))) float pb_s[KG_ROWS * PS];
+  __shared__ __attribute__((aligned(16))) float4 red4[8 * NT];
+  const int b = blockIdx.x, kg = blockIdx.y;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int H = a.H, nh = a.heads, R = a.kg_cnt[kg] * nh, H4 = H >> 2, RG = NT / H4;
+  const int c4 = t % H4, rg = t / H4;
+  const TailPair& P0 = a.p[a.kg_pair[kg][0]];
+  const int Lk = P0.Lk;
+  const float* pk = P0.Pk + (int64_t)b * Lk * H + 4 * c4;
+  float4 v[RPT];
+  auto load_rows = [&](int j0) {
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int j = j0 + rg + RG * i;
+      v[i] = j < Lk ? ld4(pk + (int64_t)j * H) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  load_rows(0);
+  for (int i = t; i < R * Lk; i += NT) {
+    const int row = i / Lk, j = i - row * Lk;
+    pb_s[row * PS + j] = a.p[a.kg_pair[kg][row / nh]].pbar[((int64_t)b * nh + row % nh) * Lk + j];
+  }
+  __syncthreads();
+  for (int row = w; row < R; row += NT / 64) {   // r_{g,h}
+    float s = 0.f;
+    for (int j = lane; j < Lk; j += 64) s += pb_s[row * PS + j];
+    s = wsum(s);
+    if (lane == 0) a.p[a.kg_pair[kg][row / nh]].r[(int64_t)b * nh + row % nh] = s;
+  }
+  for (int r0 = 0; r0 < R; r0 += 8) {
+    float4 acc[8];
+#pragma unroll
+    for (int rr = 0; rr < 8; ++rr) acc[rr] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int j0 = 0; j0 < Lk; j0 += RG * RPT) {
+      if (j0 > 0) load_rows(j0);
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) {
+        const int j = j0 + rg + RG * i;
+        if (j < Lk) {
+#pragma unroll
+          for (int rr = 0; rr < 8; ++rr) {
+            if (r0 + rr < R) {
+              const float wgt = pb_s[(r0 + rr) * PS + j];
+              acc[rr].x += wgt * v[i].x; acc[rr].y += wgt * v[i].y;
+              acc[rr].z += wgt * v[i].z; acc[rr].w += wgt * v[i].w;
+            }
+          }
+        }
+      }
+    }
+    if (R > 8 && Lk > RG * RPT) load_rows(0);   // the next pass starts from the first batch again
+#pragma unroll
+    for (int rr = 0; rr < 8; ++rr) red4[rr * NT + t] = acc[rr];
+    __syncthreads();
+    for (int task = t; task < 8 * H4; task += NT) {
+      const int rr = task / H4, cc = task - rr * H4;
+      if (r0 + rr < R) {
+        float4 s = red4[rr * NT + cc];
+        for (int g = 1; g < RG; ++g) {
+          const float4 u = red4[rr * NT + g * H4 + cc];
+          s.x += u.x; s.y += u.y; s.z += u.z; s.w += u.w;
+        }
+        const int row = r0 + rr;
+        *reinterpret_cast<float4*>(a.p[a.kg_pair[kg][row / nh]].U + ((int64_t)b * nh + row % nh) * H + 4 * cc) = s;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Weight side (H = 128): 8 waves per workgroup of 32 samples.  Wave (ts, kq)
+// owns output tile ts (32 features) over the K half kq; the upper half goes
+// through LDS and the lower-half wave adds it (fixed order, deterministic).  Every
+// global operand of both phases is loaded at kernel start (one round trip).
+constexpr int NTW = 512;
+constexpr int WH = 128;   // hidden size of the weight-side kernels
+
+// acc += sum over 8 chunks of a[q] . b[q] (k = 8 q + 4 hf + s)
+__device__ __forceinline__ f32x16 mfma8(const float4 (&a)[8], const float4 (&b)[8], f32x16 acc) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) acc = mfma4(a[q], b[q], acc);
+  return acc;
+}
+
+// Finishes a split-K tile (every wave calls it: it holds a barrier).
+__device__ __forceinline__ void split_reduce(float (*part)[16][64], f32x16& acc, int kq, int ts, int lane) {
+  if (kq == 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) part[ts][r][lane] = acc[r];
+  }
+  __syncthreads();
+  if (kq == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] += part[ts][r][lane];
+  }
+}
+
+// Forward, weight side: grid (ceil(B / 32), pairs).  C[i = sample][j = feature].
+__global__ __launch_bounds__(NTW) void tail_ob_mfma_kernel(const TailArgs a) {
+  constexpr int OS = WH + 4;
+  __shared__ __attribute__((aligned(16))) float ob_s[32 * OS];
+  __shared__ float part[4][16][64];
+  const TailPair& P = a.p[blockIdx.y];
+  const int s0 = blockIdx.x * 32;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, hf = lane >> 5, c = lane & 31;
+  const int ts = w & 3, kq = w >> 2, k0 = kq * 64 + 4 * hf;
+  const int nh = a.heads, hd = a.hd, B = a.B;
+  const int sa = min(s0 + c, B - 1);   // this lane's A row (rows past B are never stored)
+  const int n = ts * 32 + c, hh = (ts * 32) / hd;
+  float4 au[8], bv[8], bo[8];
+  const float* urow = P.U + ((int64_t)sa * nh + hh) * WH + k0;
+  const float* vrow = P.Wv + (int64_t)n * WH + k0;
+  const float* orow = P.Wo + (int64_t)n * WH + k0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    au[q] = ld4(urow + 8 * q);
+    bv[q] = ld4(vrow + 8 * q);
+    bo[q] = ld4(orow + 8 * q);
+  }
+  float rs[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int s = s0 + acc_row(r, hf);
+    rs[r] = s < B ? P.r[(int64_t)s * nh + hh] : 0.f;
+  }
+  const float bvn = P.bv[n], bon = P.bo[n];
+  // Obar = U W_v^T + r b_v
+  f32x16 acc = mfma8(au, bv, zero16());
+  split_reduce(part, acc, kq, ts, lane);
+  if (kq == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = acc_row(r, hf), s = s0 + i;
+      const float o = acc[r] + rs[r] * bvn;
+      ob_s[i * OS + n] = o;
+      if (s < B) P.Ob[(int64_t)s * WH + n] = o;
+    }
+  }
+  __syncthreads();
+  // Abar = Obar W_o^T + b_o
+  float4 ao[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) ao[q] = ld4(ob_s + c * OS + k0 + 8 * q);
+  acc = mfma8(ao, bo, zero16());
+  split_reduce(part, acc, kq, ts, lane);
+  if (kq == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int s = s0 + acc_row(r, hf);
+      if (s < B) P.Ab[(int64_t)s * WH + n] = acc[r] + bon;
+    }
+  }
+}
+
+// Backward, weight side: grid (ceil(B / 32), pairs).
+__global__ __launch_bounds__(NTW) void tail_dob_mfma_kernel(const TailArgs a) {
+  constexpr int OS = WH + 4;
+  __shared__ __attribute__((aligned(16))) float dob_s[32 * OS];
+  __shared__ float part[4][16][64];
+  const TailPair& P = a.p[blockIdx.y];
+  const int s0 = blockIdx.x * 32;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, hf = lane >> 5, c = lane & 31;
+  const int ts = w & 3, kq = w >> 2, k0 = kq * 64 + 4 * hf;
+  const int nh = a.heads, hd = a.hd, B = a.B, M = a.M;
+  const int sa = min(s0 + c, B - 1);
+  const int n = ts * 32 + c;
+  // phase 1 operands: A = c_q row (k-contiguous), B = W_o column n (k-strided)
+  float4 ac[8], bw[8];
+  const float* crow = a.cvec + ((int64_t)sa * M + P.q) * WH + k0;
+  const float* wcol = P.Wo + (int64_t)k0 * WH + n;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    ac[q] = ld4(crow + 8 * q);
+    bw[q] = make_float4(wcol[(8 * q) * WH], wcol[(8 * q + 1) * WH], wcol[(8 * q + 2) * WH], wcol[(8 * q + 3) * WH]);
+  }
+  // phase 2 operands (dU tiles tt = w, w + 8 of nh x 4): W_v[h hd + kk][32 kt + c], kk < hd
+  const int ntile = nh * (WH / 32);
+  float4 bu[2][8];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int tt = w + 8 * u;
+    const int hh = tt >> 2, kc = (tt & 3) * 32 + c;
+    const float* vcol = P.Wv + (int64_t)(hh * hd + 4 * hf) * WH + kc;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      bu[u][q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (tt < ntile && 8 * q < hd)
+        bu[u][q] = make_float4(vcol[(8 * q) * WH], vcol[(8 * q + 1) * WH], vcol[(8 * q + 2) * WH],
+                               vcol[(8 * q + 3) * WH]);
+    }
+  }
+  // dObar = c_q W_o
+  f32x16 acc = mfma8(ac, bw, zero16());
+  split_reduce(part, acc, kq, ts, lane);
+  if (kq == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = acc_row(r, hf), s = s0 + i;
+      dob_s[i * OS + n] = acc[r];
+      if (s < B) P.dOb[(int64_t)s * WH + n] = acc[r];
+    }
+  }
+  __syncthreads();
+  // dU_h = dObar_h W_v[h hd : (h+1) hd, :]  (K = hd <= 64 here: 8 chunks cover it)
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int tt = w + 8 * u;
+    if (tt >= ntile) break;
+    const int hh = tt >> 2, kc = (tt & 3) * 32 + c;
+    f32x16 acc2 = zero16();
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (8 * q < hd) acc2 = mfma4(ld4(dob_s + c * OS + hh * hd + 4 * hf + 8 * q), bu[u][q], acc2);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int s = s0 + acc_row(r, hf);
+      if (s < B) P.dU[((int64_t)s * nh + hh) * WH + kc] = acc2[r];
+    }
+  }
+}
+
+// Backward, P_k side: grid (B, key groups).  C[i = key][j = (pair, head) row].
+// The P_k rows of a wave's key tile are loaded before the dU rows are staged.
+__global__ __launch_bounds__(NT) void tail_dpbar_mfma_kernel(const TailArgs a) {
+  __shared__ __attribute__((aligned(16))) float du_s[KG_ROWS * (TAIL_MAX_H + 4)];
+  __shared__ float dr_s[KG_ROWS];
+  __shared__ float* rowp[KG_ROWS];
+  const int b = blockIdx.x, kg = blockIdx.y;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, hf = lane >> 5, c = lane & 31;
+  const int H = a.H, nh = a.heads, hd = a.hd, R = a.kg_cnt[kg] * nh, DS = H + 4;
+  const TailPair& P0 = a.p[a.kg_pair[kg][0]];
+  const int Lk = P0.Lk;
+  const float* pk = P0.Pk + (int64_t)b * Lk * H;
+  float4 av[16];
+  auto load_a = [&](int mt, int k0) {   // P_k rows of key tile mt, features [k0, k0 + 128)
+    const float* arow = pk + (int64_t)min(mt * 32 + c, Lk - 1) * H + k0 + 4 * hf;
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      if (k0 + 8 * q < H) av[q] = ld4(arow + 8 * q);
+  };
+  if (w * 32 < Lk) load_a(w, 0);
+  for (int i = t; i < KG_ROWS * (H / 4); i += NT) {
+    const int row = i / (H / 4), c4 = (i - row * (H / 4)) * 4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (row < R) v = ld4(a.p[a.kg_pair[kg][row / nh]].dU + ((int64_t)b * nh + row % nh) * H + c4);
+    *reinterpret_cast<float4*>(&du_s[row * DS + c4]) = v;
+  }
+  if (t < R) rowp[t] = a.p[a.kg_pair[kg][t / nh]].dpbar + ((int64_t)b * nh + t % nh) * Lk;
+  for (int row = w; row < R; row += NT / 64) {   // dr_{g,h} = dObar_{g,h} . b_v,h
+    const TailPair& P = a.p[a.kg_pair[kg][row / nh]];
+    const int hh = row % nh;
+    float s = 0.f;
+    for (int d = lane; d < hd; d += 64) s += P.dOb[(int64_t)b * H + hh * hd + d] * P.bv[hh * hd + d];
+    s = wsum(s);
+    if (lane == 0) dr_s[row] = s;
+  }
+  __syncthreads();
+  const float* brow = du_s + c * DS + 4 * hf;
+  for (int mt = w; mt * 32 < Lk; mt += NT / 64) {
+    f32x16 acc = zero16();
+    for (int k0 = 0; k0 < H; k0 += 128) {
+      if (mt != w || k0 > 0) load_a(mt, k0);
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        if (k0 + 8 * q < H) acc = mfma4(av[q], ld4(brow + k0 + 8 * q), acc);
+    }
+    if (c < R) {
+      float* outp = rowp[c];
+      const float dr = dr_s[c];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kk = mt * 32 + acc_row(r, hf);
+        if (kk < Lk) outp[kk] = acc[r] + dr;
       }
     }
   }
@@ -520,12 +839,56 @@ bool tail_supported(int M, int H, int C, int heads, int hd, int npairs) {
          npairs <= TAIL_MAX_PAIRS && hd % 8 == 0 && (NT % (H / 4)) == 0;
 }
 
+// Groups the pairs by key modality into `m` and reports whether the MFMA pair
+// tail applies (MMF_TAIL_GEMV=1 forces the per-sample GEMV kernels, for A/B).
+static bool tail_mfma_groups(TailArgs& m) {
+  static const bool gemv = getenv("MMF_TAIL_GEMV") != nullptr;
+  if (gemv || m.H != WH || (m.hd != 32 && m.hd != 64)) return false;
+  int mod_of[8];
+  m.nkg = 0;
+  for (int g = 0; g < m.npairs; ++g) {
+    int i = 0;
+    while (i < m.nkg && mod_of[i] != m.p[g].k) ++i;
+    if (i == m.nkg) {
+      if (m.nkg == 8) return false;
+      mod_of[m.nkg] = m.p[g].k;
+      m.kg_cnt[m.nkg++] = 0;
+    }
+    m.kg_pair[i][m.kg_cnt[i]++] = (int8_t)g;
+  }
+  for (int i = 0; i < m.nkg; ++i)
+    if (m.kg_cnt[i] * m.heads > KG_ROWS) return false;
+  return true;
+}
+
 hipError_t launch_tail_fwd(const TailArgs& a, hipStream_t st) {
   if (!tail_supported(a.M, a.H, a.C, a.heads, a.hd, a.npairs)) return hipErrorInvalidValue;
   for (int g = 0; g < a.npairs; ++g)
     if (a.p[g].Lk > 128) return hipErrorInvalidValue;
   const double B = a.B, H = a.H;
-  if (a.npairs) {
+  TailArgs m = a;
+  if (a.npairs && tail_mfma_groups(m)) {
+    double fl = 0.0, by = 0.0;   // U = pbar P_k: P_k read once per key group
+    for (int i = 0; i < m.nkg; ++i) {
+      const double lk = m.p[m.kg_pair[i][0]].Lk, rows = (double)m.kg_cnt[i] * m.heads;
+      fl += 2.0 * B * rows * lk * H;
+      by += 4.0 * B * (lk * H + rows * (lk + H + 1));
+    }
+    {
+      ProfLaunch prof_(st, "tail_u_kernel", fl, by);
+      hipLaunchKernelGGL(tail_u_kernel, dim3(a.B, m.nkg), dim3(NT), 0, st, m);
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    {
+      // Obar = U W_v^T (+ r b_v), Abar = Obar W_o^T + b_o: weights read once per 32 samples
+      ProfLaunch prof_(st, "tail_ob_mfma_kernel", 4.0 * B * H * H * a.npairs,
+                       4.0 * a.npairs * (2 * H * H * ((a.B + 31) / 32) + B * (a.heads * H + 2 * H)));
+      hipLaunchKernelGGL(tail_ob_mfma_kernel, dim3((a.B + 31) / 32, a.npairs), dim3(NTW), 0, st, m);
+    }
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  } else if (a.npairs) {
     // per pair: Vbar = U W_v^T (+ r b_v), Obar = Vbar W_o^T + b_o; weights read once
     ProfLaunch prof_(st, "tail_pair_fwd_kernel", 4.0 * B * H * H * a.npairs,
                      4.0 * a.npairs * (2 * H * H + B * (a.heads * H + 2 * H)));
@@ -553,6 +916,26 @@ hipError_t launch_tail_bwd(const TailArgs& a, hipStream_t st) {
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !a.npairs) return e;
+  TailArgs m = a;
+  if (tail_mfma_groups(m)) {
+    {
+      // dObar = c_q W_o, dU_h = dObar_h W_v,h: weights read once per 32 samples
+      ProfLaunch prof_(st, "tail_dob_mfma_kernel", 4.0 * B * H * H * a.npairs,
+                       4.0 * a.npairs * (2 * H * H * ((a.B + 31) / 32) + B * (a.heads * H + 2 * H)));
+      hipLaunchKernelGGL(tail_dob_mfma_kernel, dim3((a.B + 31) / 32, a.npairs), dim3(NTW), 0, st, m);
+    }
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    double fl = 0.0, by = 0.0;   // dpbar = P_k dU + dr: P_k read once per key group
+    for (int i = 0; i < m.nkg; ++i) {
+      const double lk = m.p[m.kg_pair[i][0]].Lk, rows = (double)m.kg_cnt[i] * m.heads;
+      fl += 2.0 * B * rows * lk * H;
+      by += 4.0 * B * (lk * H + rows * (lk + H) + m.kg_cnt[i] * H);
+    }
+    ProfLaunch prof_(st, "tail_dpbar_mfma_kernel", fl, by);
+    hipLaunchKernelGGL(tail_dpbar_mfma_kernel, dim3(a.B, m.nkg), dim3(NT), 0, st, m);
+    return hipGetLastError();
+  }
   {
     ProfLaunch prof_(st, "tail_pair_bwd_kernel", 4.0 * B * H * H * a.npairs,
                      4.0 * a.npairs * (2 * H * H + B * (a.heads * H + 2 * H)));
