@@ -632,81 +632,161 @@ __global__ __launch_bounds__(NT) void tail_dpbar_mfma_kernel(const TailArgs a) {
 }
 
 // ---------------------------------------------------------------- per sample
+// PRE (H = 128, M <= 4, C <= 8): every weight element a thread's GEMVs / dot
+// products read (W1 row half, gating row slice, W2 rows) is loaded at kernel
+// start, beside the activations: one memory round trip instead of one per stage.
+constexpr int PH = 128;
+
+// y[n] = x . W[n] (N = K = 128): thread pair (n = t >> 1, k half t & 1), its 64 weights in wr
+__device__ __forceinline__ void gemv128_pre(const float* x, const float4 (&wr)[16], float* y) {
+  const int t = threadIdx.x, half = t & 1;
+  const float* x0 = x + half * 64;
+  float acc = 0.f;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const float4 xv = *reinterpret_cast<const float4*>(x0 + 4 * q);
+    acc += wr[q].x * xv.x + wr[q].y * xv.y + wr[q].z * xv.z + wr[q].w * xv.w;
+  }
+  const float v = acc + dpp<DPP_XOR1>(acc);
+  if (half == 0) y[t >> 1] = v;
+}
+
+// y[k] = sum_n x[n] W[n][k] (K = 128): thread (k = t & 127, n half t >> 7) holds its cnt <= NW
+// weights W[n0 + i][k] in wc; the halves are summed in order through red
+template <int NW>
+__device__ __forceinline__ void gemv_nn128_pre(const float* x, const float (&wc)[NW], int n0, int cnt, float* y,
+                                               float* red) {
+  const int t = threadIdx.x;
+  float acc = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i)
+    if (i < cnt) acc += x[n0 + i] * wc[i];
+  red[t] = acc;
+  __syncthreads();
+  if (t < 128) y[t] = red[t] + red[t + 128];
+}
+
 // Forward head: pooled_m = mask_m / n_m (mean_L P_m + sum_{g: q(g)=m} Abar_g), gating
 // scores, adaptive weights, fused, classifier.  grid (B).
+template <bool PRE>
 __global__ __launch_bounds__(NT) void tail_head_fwd_kernel(const TailArgs a) {
   __shared__ __attribute__((aligned(16))) float pooled_s[MAXM * TAIL_MAX_H];
   __shared__ __attribute__((aligned(16))) float v1[TAIL_MAX_H], v2[TAIL_MAX_H];
   __shared__ __attribute__((aligned(16))) float4 red4[NT];
   __shared__ float score_s[MAXM], w_s[MAXM];
   const int b = blockIdx.x;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int M = a.M, H = a.H;
   const int H4 = H >> 2;
-
-  // (1) mean over L of P_m (the modality's own entry of the aggregation list)
-  for (int m = 0; m < M; ++m) {
-    const int L = a.L[m];
-    if (a.Pcol[m]) {
-      // the projection GEMM's per-tile column sums: ncol rows per sample
+  float4 w1r[16];
+  float gw[2] = {0.f, 0.f}, w2r[2][2] = {{0.f, 0.f}, {0.f, 0.f}}, b1n = 0.f;
+  if constexpr (PRE) {
+    const float* wr = a.W1 + (int64_t)(t >> 1) * PH + (t & 1) * 64;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) w1r[q] = *reinterpret_cast<const float4*>(wr + 4 * q);
+    if (wave < M) {
+      gw[0] = a.gate_w[wave][lane];
+      gw[1] = a.gate_w[wave][lane + 64];
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (wave + 4 * u < a.C) {
+        w2r[u][0] = a.W2[(int64_t)(wave + 4 * u) * PH + lane];
+        w2r[u][1] = a.W2[(int64_t)(wave + 4 * u) * PH + lane + 64];
+      }
+    if (t < PH) b1n = a.b1[t];
+  }
+  if constexpr (PRE) {   // (head_pre: every modality has the projection GEMM's column sums)
+    // (1 + 2) in one pass: mean_L P_m from the projection GEMM's per-tile column sums
+    // (ncol rows per sample), + the attended means of every pair whose query is m,
+    // then agg * mask / n_m
+    for (int m = 0; m < M; ++m) {   // m wave-uniform (kernel-argument arrays indexed by it)
       const int nc = a.ncol[m];
-      const float* pc = a.Pcol[m] + (int64_t)b * nc * H;
+      const float f = a.inv_cnt[m] * a.mask[(int64_t)b * M + m], il = 1.f / (float)a.L[m];
       for (int n = t; n < H; n += NT) {
+        const float* pc = a.Pcol[m] + (int64_t)b * nc * H + n;
         float s = 0.f;
-        for (int c = 0; c < nc; ++c) s += pc[(int64_t)c * H + n];
-        pooled_s[m * H + n] = s * (1.f / (float)L);
+        for (int c = 0; c < nc; ++c) s += pc[(int64_t)c * H];
+        float v = s * il;
+        for (int g = 0; g < a.npairs; ++g)
+          if (a.p[g].q == m) v += a.p[g].Ab[(int64_t)b * H + n];
+        v *= f;
+        pooled_s[m * H + n] = v;
+        a.pooled[(int64_t)b * M * H + m * H + n] = v;
+      }
+    }
+  } else {
+    // (1) mean over L of P_m (the modality's own entry of the aggregation list)
+    for (int m = 0; m < M; ++m) {
+      const int L = a.L[m];
+      if (a.Pcol[m]) {
+        const int nc = a.ncol[m];
+        const float* pc = a.Pcol[m] + (int64_t)b * nc * H;
+        for (int n = t; n < H; n += NT) {
+          float s = 0.f;
+          for (int c = 0; c < nc; ++c) s += pc[(int64_t)c * H + n];
+          pooled_s[m * H + n] = s * (1.f / (float)L);
+        }
+        __syncthreads();
+        continue;
+      }
+      const float* base = a.P[m] + (int64_t)b * L * H;
+      const int RG = NT / H4;
+      const int c4 = t % H4, rg = t / H4;
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f), acc2 = acc;
+      if (rg < RG) {
+        int r = rg;
+#pragma unroll 4
+        for (; r + RG < L; r += 2 * RG) {
+          const float4 v = *reinterpret_cast<const float4*>(base + (int64_t)r * H + 4 * c4);
+          const float4 u = *reinterpret_cast<const float4*>(base + (int64_t)(r + RG) * H + 4 * c4);
+          acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+          acc2.x += u.x; acc2.y += u.y; acc2.z += u.z; acc2.w += u.w;
+        }
+        if (r < L) {
+          const float4 v = *reinterpret_cast<const float4*>(base + (int64_t)r * H + 4 * c4);
+          acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        }
+      }
+      red4[t] = make_float4(acc.x + acc2.x, acc.y + acc2.y, acc.z + acc2.z, acc.w + acc2.w);
+      __syncthreads();
+      if (t < H4) {
+        float4 s = red4[t];
+        for (int g = 1; g < RG; ++g) {
+          const float4 v = red4[g * H4 + t];
+          s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        }
+        const float f = 1.f / (float)L;
+        *reinterpret_cast<float4*>(&pooled_s[m * H + 4 * t]) = make_float4(s.x * f, s.y * f, s.z * f, s.w * f);
       }
       __syncthreads();
-      continue;
     }
-    const float* base = a.P[m] + (int64_t)b * L * H;
-    const int RG = NT / H4;
-    const int c4 = t % H4, rg = t / H4;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f), acc2 = acc;
-    if (rg < RG) {
-      int r = rg;
-#pragma unroll 4
-      for (; r + RG < L; r += 2 * RG) {
-        const float4 v = *reinterpret_cast<const float4*>(base + (int64_t)r * H + 4 * c4);
-        const float4 u = *reinterpret_cast<const float4*>(base + (int64_t)(r + RG) * H + 4 * c4);
-        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-        acc2.x += u.x; acc2.y += u.y; acc2.z += u.z; acc2.w += u.w;
-      }
-      if (r < L) {
-        const float4 v = *reinterpret_cast<const float4*>(base + (int64_t)r * H + 4 * c4);
-        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-      }
+    // (2) + the attended means of every pair whose query is m, then agg * mask / n_m
+    for (int i = t; i < M * H; i += NT) {
+      const int m = i / H, n = i - m * H;
+      float v = pooled_s[i];
+      for (int g = 0; g < a.npairs; ++g)
+        if (a.p[g].q == m) v += a.p[g].Ab[(int64_t)b * H + n];
+      v *= a.inv_cnt[m] * a.mask[(int64_t)b * M + m];
+      pooled_s[i] = v;
+      a.pooled[(int64_t)b * M * H + i] = v;
     }
-    red4[t] = make_float4(acc.x + acc2.x, acc.y + acc2.y, acc.z + acc2.z, acc.w + acc2.w);
-    __syncthreads();
-    if (t < H4) {
-      float4 s = red4[t];
-      for (int g = 1; g < RG; ++g) {
-        const float4 v = red4[g * H4 + t];
-        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-      }
-      const float f = 1.f / (float)L;
-      *reinterpret_cast<float4*>(&pooled_s[m * H + 4 * t]) = make_float4(s.x * f, s.y * f, s.z * f, s.w * f);
-    }
-    __syncthreads();
-  }
-  // (2) + the attended means of every pair whose query is m, then agg * mask / n_m
-  for (int i = t; i < M * H; i += NT) {
-    const int m = i / H, n = i - m * H;
-    float v = pooled_s[i];
-    for (int g = 0; g < a.npairs; ++g)
-      if (a.p[g].q == m) v += a.p[g].Ab[(int64_t)b * H + n];
-    v *= a.inv_cnt[m] * a.mask[(int64_t)b * M + m];
-    pooled_s[i] = v;
-    a.pooled[(int64_t)b * M * H + i] = v;
   }
   __syncthreads();
   // (3) gating scores (nn.Linear(H, 1), src/fusion.py:316-321,452-461), adaptive weights
-  for (int m = wave; m < M; m += NT / 64) {
-    float s = 0.f;
-    for (int j = lane; j < H; j += 64) s += pooled_s[m * H + j] * a.gate_w[m][j];
-    s = wsum(s);
-    if (lane == 0) score_s[m] = s + a.gate_b[m][0];
+  if constexpr (PRE) {
+    if (wave < M) {
+      float s = pooled_s[wave * PH + lane] * gw[0] + pooled_s[wave * PH + lane + 64] * gw[1];
+      s = wsum(s);
+      if (lane == 0) score_s[wave] = s + a.gate_b[wave][0];
+    }
+  } else {
+    for (int m = wave; m < M; m += NT / 64) {
+      float s = 0.f;
+      for (int j = lane; j < H; j += 64) s += pooled_s[m * H + j] * a.gate_w[m][j];
+      s = wsum(s);
+      if (lane == 0) score_s[m] = s + a.gate_b[m][0];
+    }
   }
   __syncthreads();
   if (t == 0) {
@@ -729,7 +809,8 @@ __global__ __launch_bounds__(NT) void tail_head_fwd_kernel(const TailArgs a) {
     a.fused[(int64_t)b * H + j] = f;
   }
   __syncthreads();
-  gemv_nt_s<1>(v1, 0, 1 << 30, 0, a.W1, H, H, v2, 0);
+  if constexpr (PRE) gemv128_pre(v1, w1r, v2);
+  else gemv_nt_s<1>(v1, 0, 1 << 30, 0, a.W1, H, H, v2, 0);
   __syncthreads();
   const float p = a.drop_p;
   const bool drop = p > 0.f && a.rng != nullptr;
@@ -737,36 +818,65 @@ __global__ __launch_bounds__(NT) void tail_head_fwd_kernel(const TailArgs a) {
   if (drop) rs = *a.rng;
   const float inv_keep = p < 1.f ? 1.f / (1.f - p) : 0.f;
   for (int n = t; n < H; n += NT) {
-    float x = fmaxf(v2[n] + a.b1[n], 0.f);
+    float x = fmaxf(v2[n] + (PRE ? b1n : a.b1[n]), 0.f);
     if (drop) x = keep1(rs, a.drop_site, (uint64_t)b * H + n, p) ? x * inv_keep : 0.f;
     v2[n] = x;
     a.h1[(int64_t)b * H + n] = x;
   }
   __syncthreads();
-  for (int c = wave; c < a.C; c += NT / 64) {
-    float s = 0.f;
-    for (int j = lane; j < H; j += 64) s += v2[j] * a.W2[(int64_t)c * H + j];
-    s = wsum(s);
-    if (lane == 0) a.logits[(int64_t)b * a.C + c] = s + a.b2[c];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = wave + 4 * u;
+      if (c < a.C) {
+        float s = v2[lane] * w2r[u][0] + v2[lane + 64] * w2r[u][1];
+        s = wsum(s);
+        if (lane == 0) a.logits[(int64_t)b * a.C + c] = s + a.b2[c];
+      }
+    }
+  } else {
+    for (int c = wave; c < a.C; c += NT / 64) {
+      float s = 0.f;
+      for (int j = lane; j < H; j += 64) s += v2[j] * a.W2[(int64_t)c * H + j];
+      s = wsum(s);
+      if (lane == 0) a.logits[(int64_t)b * a.C + c] = s + a.b2[c];
+    }
   }
 }
 
 // Backward head: dz1 = ReLU'/Dropout'(dlogits W2), dfused = dz1 W1, head backward
 // (dscore, cvec = dpooled * mask / n).  grid (B).
+template <bool PRE>
 __global__ __launch_bounds__(NT) void tail_head_bwd_kernel(const TailArgs a) {
   __shared__ __attribute__((aligned(16))) float pooled_s[MAXM * TAIL_MAX_H];
   __shared__ __attribute__((aligned(16))) float v1[TAIL_MAX_H], v2[TAIL_MAX_H], dl_s[256];
   __shared__ float red[NT];
   __shared__ float dw_s[MAXM], dscore_s[MAXM];
   const int b = blockIdx.x;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int M = a.M, H = a.H, C = a.C;
-
+  // PRE: thread (k = t & 127, n half t >> 7) columns of W2 (rows [n0, n0 + cnt)) and
+  // W1 (rows [64 rh, 64 rh + 64)); the gating weights of its cvec elements
+  const int kc = t & 127, rh = t >> 7;
+  const int c0 = rh ? (C >> 1) : 0, ccnt = rh ? C - (C >> 1) : (C >> 1);
+  float w2c[4], w1c[64], gwc[2];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w2c[i] = i < ccnt ? a.W2[(int64_t)(c0 + i) * PH + kc] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 64; ++i) w1c[i] = a.W1[(int64_t)(rh * 64 + i) * PH + kc];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = t + u * NT;
+      gwc[u] = i < M * PH ? a.gate_w[i / PH][i % PH] : 0.f;
+    }
+  }
   for (int c = t; c < C; c += NT) dl_s[c] = a.dlogits[(int64_t)b * C + c];
   for (int i = t; i < M * H; i += NT) pooled_s[i] = a.pooled[(int64_t)b * M * H + i];
   __syncthreads();
   // the saved h1 is post-dropout, so h1 > 0 marks kept, active units (gscale = 1/(1-p))
-  gemv_nn_s<1>(dl_s, 0, a.W2, C, H, v1, 0, red);
+  if constexpr (PRE) gemv_nn128_pre<4>(dl_s, w2c, c0, ccnt, v1, red);
+  else gemv_nn_s<1>(dl_s, 0, a.W2, C, H, v1, 0, red);
   __syncthreads();
   for (int n = t; n < H; n += NT) {
     const float z = a.h1[(int64_t)b * H + n] > 0.f ? v1[n] * a.gscale : 0.f;
@@ -774,7 +884,8 @@ __global__ __launch_bounds__(NT) void tail_head_bwd_kernel(const TailArgs a) {
     a.dz1[(int64_t)b * H + n] = z;
   }
   __syncthreads();
-  gemv_nn_s<1>(v1, 0, a.W1, H, H, v2, 0, red);
+  if constexpr (PRE) gemv_nn128_pre<64>(v1, w1c, rh * 64, 64, v2, red);
+  else gemv_nn_s<1>(v1, 0, a.W1, H, H, v2, 0, red);
   __syncthreads();
   // head backward (head.hip head_bwd_kernel): dw_m = dfused . pooled_m
   for (int m = wave; m < M; m += NT / 64) {
@@ -809,11 +920,24 @@ __global__ __launch_bounds__(NT) void tail_head_bwd_kernel(const TailArgs a) {
     }
   }
   __syncthreads();
-  for (int i = t; i < M * H; i += NT) {
-    const int m = i / H, j = i - m * H;
-    const float wm = a.weights[(int64_t)b * M + m];
-    const float f = a.mask[(int64_t)b * M + m] * a.inv_cnt[m];
-    a.cvec[(int64_t)b * M * H + i] = (wm * v2[j] + dscore_s[m] * a.gate_w[m][j]) * f;
+  if constexpr (PRE) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = t + u * NT;
+      if (i < M * PH) {
+        const int m = i / PH, j = i - m * PH;
+        const float wm = a.weights[(int64_t)b * M + m];
+        const float f = a.mask[(int64_t)b * M + m] * a.inv_cnt[m];
+        a.cvec[(int64_t)b * M * PH + i] = (wm * v2[j] + dscore_s[m] * gwc[u]) * f;
+      }
+    }
+  } else {
+    for (int i = t; i < M * H; i += NT) {
+      const int m = i / H, j = i - m * H;
+      const float wm = a.weights[(int64_t)b * M + m];
+      const float f = a.mask[(int64_t)b * M + m] * a.inv_cnt[m];
+      a.cvec[(int64_t)b * M * H + i] = (wm * v2[j] + dscore_s[m] * a.gate_w[m][j]) * f;
+    }
   }
 }
 
@@ -837,6 +961,14 @@ int tail_samples() {
 bool tail_supported(int M, int H, int C, int heads, int hd, int npairs) {
   return M <= MAXM && heads <= MAXHEADS && H % 16 == 0 && H <= TAIL_MAX_H && C <= 256 &&
          npairs <= TAIL_MAX_PAIRS && hd % 8 == 0 && (NT % (H / 4)) == 0;
+}
+
+// Prefetching head kernels (MMF_TAIL_GEMV=1 also selects the plain ones, for A/B)
+static bool head_pre(const TailArgs& a) {
+  static const bool gemv = getenv("MMF_TAIL_GEMV") != nullptr;
+  bool allcol = true;
+  for (int m = 0; m < a.M; ++m) allcol = allcol && a.Pcol[m] != nullptr;
+  return !gemv && allcol && a.H == PH && a.M <= 4 && a.C <= 8;
 }
 
 // Groups the pairs by key modality into `m` and reports whether the MFMA pair
@@ -900,9 +1032,10 @@ hipError_t launch_tail_fwd(const TailArgs& a, hipStream_t st) {
     if (e != hipSuccess) return e;
   }
   // pooling, gating, adaptive weights, weighted sum, classifier
-  ProfLaunch prof_(st, "tail_head_fwd_kernel", 2.0 * B * H * (H + a.C) + 4.0 * a.M * B * H,
+  ProfLaunch prof_(st, head_pre(a) ? "tail_head_fwd_kernel<true>" : "tail_head_fwd_kernel<false>", 2.0 * B * H * (H + a.C) + 4.0 * a.M * B * H,
                    4.0 * (H * (H + a.C) + B * (a.M * H + a.C)));
-  hipLaunchKernelGGL(tail_head_fwd_kernel, dim3(a.B), dim3(NT), 0, st, a);
+  if (head_pre(a)) hipLaunchKernelGGL(tail_head_fwd_kernel<true>, dim3(a.B), dim3(NT), 0, st, a);
+  else hipLaunchKernelGGL(tail_head_fwd_kernel<false>, dim3(a.B), dim3(NT), 0, st, a);
   return hipGetLastError();
 }
 
@@ -910,9 +1043,10 @@ hipError_t launch_tail_bwd(const TailArgs& a, hipStream_t st) {
   if (!tail_supported(a.M, a.H, a.C, a.heads, a.hd, a.npairs)) return hipErrorInvalidValue;
   const double B = a.B, H = a.H;
   {
-    ProfLaunch prof_(st, "tail_head_bwd_kernel", 2.0 * B * H * (H + a.C) + 4.0 * a.M * B * H,
+    ProfLaunch prof_(st, head_pre(a) ? "tail_head_bwd_kernel<true>" : "tail_head_bwd_kernel<false>", 2.0 * B * H * (H + a.C) + 4.0 * a.M * B * H,
                      4.0 * (H * (H + a.C) + B * (a.M * H + a.C)));
-    hipLaunchKernelGGL(tail_head_bwd_kernel, dim3(a.B), dim3(NT), 0, st, a);
+    if (head_pre(a)) hipLaunchKernelGGL(tail_head_bwd_kernel<true>, dim3(a.B), dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL(tail_head_bwd_kernel<false>, dim3(a.B), dim3(NT), 0, st, a);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !a.npairs) return e;
