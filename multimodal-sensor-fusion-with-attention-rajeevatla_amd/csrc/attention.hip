@@ -1263,8 +1263,28 @@ __device__ __forceinline__ void load_frag_vec(float* f, const float* row) {
   }
 }
 
+// Packed keep words of one 32-query tile (query on the lane) of the lean forward:
+// words[kt] bit 8g + 4h' + j = keep decision of key kt*32 + 8g + 4h' + j for the
+// lane's query (the layout of the saved keep_bits rows); both lane halves end with
+// the same words.  Every lane of the wave must call it (it shuffles).
+template <int NKT, bool DROP>
+__device__ __forceinline__ void lean_keep_words(uint32_t (&words)[NKT], const RngSnap& rs, uint32_t site,
+                                                uint64_t rowbase, int nkt, float pdrop, int h) {
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    words[kt] = 0u;
+    if (kt < nkt) {
+      const uint32_t kb16 = DROP ? keep_tile16(rs, site, rowbase + kt * 32, pdrop, h, true, true) : 0xFFFFu;
+      uint32_t bits = 0;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) bits |= ((kb16 >> (4 * g)) & 0xFu) << (8 * g + 4 * h);
+      words[kt] = or_xor32(bits);
+    }
+  }
+}
+
 // DROP (train mode with p > 0, launch-time choice): the loop body has no dropout
-// branches, so the draws schedule between the S MFMAs.
+// branches.
 template <int HDP, bool BF, bool DROP = true>
 __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(const AttnArgs A) {
   constexpr int LS = HDP + 4;
@@ -1294,7 +1314,25 @@ __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(cons
   const float msk = P.kmask_mode == 1 ? P.kmask[(int64_t)b * P.kmask_ld] : 1.f;
   float qf[HALF];   // the query fragment of this wave's current tile (reloaded at the end of an iteration)
   load_frag_vec<HALF>(qf, P.q + ((int64_t)b * Lq + min(w * 32 + c, Lq - 1)) * P.ldq + col0 + h * HALF);
-  load_rows<PKC, HDP, LS>(Ks, P.k + (int64_t)b * Lk * P.ldk + col0, Lk, P.ldk, 0, hd, true);
+  constexpr int C4 = HDP / 4;
+  constexpr int KPER = PKC * C4 / NT;   // float4 slots of the K image per thread
+  float4 kv[KPER];
+  {
+    // branch-free: clamped addresses, out-of-image slots zeroed at the LDS write (a
+    // guarded load per slot made the compiler drain vmcnt between the loads)
+    const float* kb = P.k + (int64_t)b * Lk * P.ldk + col0;
+#pragma unroll
+    for (int i = 0; i < KPER; ++i) {
+      const int idx = t + i * NT;
+      const int r = min(idx / C4, Lk - 1), c4 = min((idx % C4) * 4, hd - 4);
+      kv[i] = *reinterpret_cast<const float4*>(kb + (int64_t)r * P.ldk + c4);
+    }
+  }
+  // the dropout keep words of the wave's first query tile do not depend on any load:
+  // drawn while the loads above are in flight (Philox is ~20 % of the kernel's VALU work)
+  uint32_t words[NKT];
+  lean_keep_words<NKT, DROP>(words, rs, P.drop_site, (uint64_t)(bh * Lq + min(w * 32 + c, Lq - 1)) * Lk, nkt,
+                             pdrop, h);
   if (msk == 0.f) {
     for (int k = t; k < Lk; k += NT) pbar[k] = 0.f;
     if (P.pbarT)
@@ -1304,6 +1342,12 @@ __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(cons
       for (int q = t; q < Lq; q += NT)
         *reinterpret_cast<uint4*>(P.keep_bits + (bh * Lq + q) * 4) = make_uint4(0, 0, 0, 0);
     return;
+  }
+#pragma unroll
+  for (int i = 0; i < KPER; ++i) {
+    const int idx = t + i * NT;
+    const bool in = idx / C4 < Lk && (idx % C4) * 4 < hd;
+    *reinterpret_cast<float4*>(&Ks[(idx / C4) * LS + (idx % C4) * 4]) = in ? kv[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   __syncthreads();
   FSTAMP(1)
@@ -1355,19 +1399,12 @@ __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(cons
     l = sum_xor32(l);
     FSTAMP(3)
     const float f = qvalid ? (pdrop > 0.f ? inv_keep : 1.f) / l : 0.f;
-    uint32_t words[NKT];
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
-      words[kt] = 0u;
       if (kt < nkt) {
-        const uint32_t kb16 =
-            DROP ? keep_tile16(rs, P.drop_site, (uint64_t)rowidx * Lk + kt * 32, pdrop, h, true, true) : 0xFFFFu;
-        uint32_t bits = 0;
+        const uint32_t wk = words[kt] >> (4 * h);   // reg r = 4g + j <-> key bit 8g + 4h + j
 #pragma unroll
-        for (int g = 0; g < 4; ++g) bits |= ((kb16 >> (4 * g)) & 0xFu) << (8 * g + 4 * h);
-        words[kt] = or_xor32(bits);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sv[kt][r] = ((kb16 >> r) & 1u) ? sv[kt][r] * f : 0.f;
+        for (int r = 0; r < 16; ++r) sv[kt][r] = ((wk >> (8 * (r >> 2) + (r & 3))) & 1u) ? sv[kt][r] * f : 0.f;
         colacc[kt] += colsum_tile(sv[kt], c);
       }
     }
@@ -1378,8 +1415,11 @@ __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(cons
             make_uint4(words[0], NKT > 1 ? words[1] : 0u, NKT > 2 ? words[2] : 0u, NKT > 3 ? words[3] : 0u);
     }
     FSTAMP(4)
-    if ((qt + 4) * 32 < Lq)
-      load_frag_vec<HALF>(qf, P.q + ((int64_t)b * Lq + min((qt + 4) * 32 + c, Lq - 1)) * P.ldq + col0 + h * HALF);
+    if ((qt + 4) * 32 < Lq) {
+      const int qn = min((qt + 4) * 32 + c, Lq - 1);
+      load_frag_vec<HALF>(qf, P.q + ((int64_t)b * Lq + qn) * P.ldq + col0 + h * HALF);
+      lean_keep_words<NKT, DROP>(words, rs, P.drop_site, (uint64_t)(bh * Lq + qn) * Lk, nkt, pdrop, h);
+    }
   }
   if ((c & 1) == 0) {
 #pragma unroll

@@ -259,7 +259,7 @@ constexpr int CLIP_BLOCKS = 256;
 
 __global__ __launch_bounds__(NT) void grad_sumsq_kernel(int64_t n, const float* __restrict__ g,
                                                         float* __restrict__ partial, int64_t* step_incr) {
-  __shared__ float red[NT];
+  __shared__ float red[NT / 64];
   const int t = threadIdx.x;
   // fused clip + AdamW: the step counter advances here, one launch before the update reads it
   if (step_incr && blockIdx.x == 0 && t == 0) *step_incr = *step_incr + 1;
@@ -272,36 +272,82 @@ __global__ __launch_bounds__(NT) void grad_sumsq_kernel(int64_t n, const float* 
   }
   if (blockIdx.x == 0)
     for (int64_t i = 4 * n4 + t; i < n; i += NT) acc += g[i] * g[i];
-  red[t] = acc;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);   // fixed order per wave
+  if ((t & 63) == 0) red[t >> 6] = acc;
   __syncthreads();
-  for (int s = NT / 2; s > 0; s >>= 1) {
-    if (t < s) red[t] += red[t + s];
-    __syncthreads();
-  }
-  if (t == 0) partial[blockIdx.x] = red[0];
+  if (t == 0) partial[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // total_norm = gscale * sqrt(sum); coef = min(1, max_norm / (total_norm + 1e-6)) (1 when max_norm <= 0).
-// Every thread of the block gets the same norm / coef (fixed tree order).
+// Every thread of the block gets the same norm / coef: one partial per thread, a fixed
+// xor-butterfly per wave, the four wave sums in a fixed order (the same bits in every block).
+static_assert(CLIP_BLOCKS == NT, "one clip partial per thread");
 __device__ __forceinline__ void clip_norm_coef(const float* __restrict__ partial, float gscale, float max_norm,
                                                double* red, float& norm, float& coef) {
   const int t = threadIdx.x;
-  double acc = 0.0;
-  for (int i = t; i < CLIP_BLOCKS; i += NT) acc += (double)partial[i];
-  red[t] = acc;
+  double acc = (double)partial[t];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  if ((t & 63) == 0) red[t >> 6] = acc;
   __syncthreads();
-  for (int s = NT / 2; s > 0; s >>= 1) {
-    if (t < s) red[t] += red[t + s];
-    __syncthreads();
-  }
-  norm = (float)(sqrt(red[0]) * (double)gscale);
+  const double sum = (red[0] + red[1]) + (red[2] + red[3]);
+  norm = (float)(sqrt(sum) * (double)gscale);
   coef = 1.f;
   if (max_norm > 0.f) coef = fminf(1.f, max_norm / (norm + 1e-6f));
 }
 
+// One AdamW element update (shared by adamw_kernel and clip_adamw_kernel: the same
+// float operations, so the fused and two-call paths agree bit for bit).
+__device__ __forceinline__ void adamw_elem(float& p, float g, float& m, float& v, float gs, float lr, float wd,
+                                           float b1, float b2, float eps, float step_size, float bc2s) {
+  const float gi = g * gs;
+  float pi = p * (1.f - lr * wd);
+  const float mi = b1 * m + (1.f - b1) * gi;
+  const float vi = b2 * v + (1.f - b2) * gi * gi;
+  m = mi;
+  v = vi;
+  pi -= step_size * mi / (sqrtf(vi) / bc2s + eps);
+  p = pi;
+}
+
+// The update over [0, n): float4 slots grid-stride when every pointer is 16-B aligned
+// (vec), then the scalar remainder; otherwise scalar throughout.
+__device__ __forceinline__ void adamw_range(int64_t n, float* __restrict__ p, const float* __restrict__ g,
+                                            float* __restrict__ m, float* __restrict__ v, bool vec, float gs,
+                                            float lr, float wd, float b1, float b2, float eps, float step_size,
+                                            float bc2s) {
+  const int64_t tid = (int64_t)blockIdx.x * NT + threadIdx.x, nth = (int64_t)gridDim.x * NT;
+  int64_t done = 0;
+  if (vec) {
+    const int64_t n4 = n / 4;
+    for (int64_t i = tid; i < n4; i += nth) {
+      float4 pv = reinterpret_cast<float4*>(p)[i];
+      const float4 gv = reinterpret_cast<const float4*>(g)[i];
+      float4 mv = reinterpret_cast<float4*>(m)[i];
+      float4 vv = reinterpret_cast<float4*>(v)[i];
+      adamw_elem(pv.x, gv.x, mv.x, vv.x, gs, lr, wd, b1, b2, eps, step_size, bc2s);
+      adamw_elem(pv.y, gv.y, mv.y, vv.y, gs, lr, wd, b1, b2, eps, step_size, bc2s);
+      adamw_elem(pv.z, gv.z, mv.z, vv.z, gs, lr, wd, b1, b2, eps, step_size, bc2s);
+      adamw_elem(pv.w, gv.w, mv.w, vv.w, gs, lr, wd, b1, b2, eps, step_size, bc2s);
+      reinterpret_cast<float4*>(p)[i] = pv;
+      reinterpret_cast<float4*>(m)[i] = mv;
+      reinterpret_cast<float4*>(v)[i] = vv;
+    }
+    done = 4 * n4;
+  }
+  for (int64_t i = done + tid; i < n; i += nth) {
+    float pi = p[i], mi = m[i], vi = v[i];
+    adamw_elem(pi, g[i], mi, vi, gs, lr, wd, b1, b2, eps, step_size, bc2s);
+    p[i] = pi;
+    m[i] = mi;
+    v[i] = vi;
+  }
+}
+
 __global__ __launch_bounds__(NT) void clip_coef_kernel(const float* __restrict__ partial, float gscale,
                                                        float max_norm, float* norm_out, float* coef_out) {
-  __shared__ double red[NT];
+  __shared__ double red[NT / 64];
   float norm, coef;
   clip_norm_coef(partial, gscale, max_norm, red, norm, coef);
   if (threadIdx.x == 0) {
@@ -318,23 +364,14 @@ __global__ __launch_bounds__(NT) void adamw_kernel(int64_t n, float* __restrict_
                                                    float* __restrict__ v, const int64_t* step, float lr,
                                                    float b1, float b2, float eps, float wd, float gscale,
                                                    const float* __restrict__ lr_dev,
-                                                   const float* __restrict__ coef_dev) {
+                                                   const float* __restrict__ coef_dev, int vec) {
   if (lr_dev) lr = lr_dev[0];
   if (coef_dev) gscale *= coef_dev[0];
   const double st = (double)(*step + 1);
   const float bc1 = (float)(1.0 - pow((double)b1, st));
   const float bc2s = (float)sqrt(1.0 - pow((double)b2, st));
   const float step_size = lr / bc1;
-  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
-    const float gi = g[i] * gscale;
-    float pi = p[i] * (1.f - lr * wd);
-    const float mi = b1 * m[i] + (1.f - b1) * gi;
-    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
-    m[i] = mi;
-    v[i] = vi;
-    pi -= step_size * mi / (sqrtf(vi) / bc2s + eps);
-    p[i] = pi;
-  }
+  adamw_range(n, p, g, m, v, vec != 0, gscale, lr, wd, b1, b2, eps, step_size, bc2s);
 }
 
 // Clip + AdamW in one launch after grad_sumsq_kernel (which advanced *step): every
@@ -346,8 +383,8 @@ __global__ __launch_bounds__(NT) void clip_adamw_kernel(int64_t n, float* __rest
                                                         const float* __restrict__ lr_dev, float b1, float b2,
                                                         float eps, float wd, float gscale,
                                                         const float* __restrict__ partial, float max_norm,
-                                                        float* norm_out, float* coef_out) {
-  __shared__ double red[NT];
+                                                        float* norm_out, float* coef_out, int vec) {
+  __shared__ double red[NT / 64];
   float norm, coef;
   clip_norm_coef(partial, gscale, max_norm, red, norm, coef);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -355,21 +392,11 @@ __global__ __launch_bounds__(NT) void clip_adamw_kernel(int64_t n, float* __rest
     if (coef_out) coef_out[0] = coef;
   }
   const float lr = lr_dev[0];
-  const float gs = gscale * coef;
   const double st = (double)(*step);
   const float bc1 = (float)(1.0 - pow((double)b1, st));
   const float bc2s = (float)sqrt(1.0 - pow((double)b2, st));
   const float step_size = lr / bc1;
-  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
-    const float gi = g[i] * gs;
-    float pi = p[i] * (1.f - lr * wd);
-    const float mi = b1 * m[i] + (1.f - b1) * gi;
-    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
-    m[i] = mi;
-    v[i] = vi;
-    pi -= step_size * mi / (sqrtf(vi) / bc2s + eps);
-    p[i] = pi;
-  }
+  adamw_range(n, p, g, m, v, vec != 0, gscale * coef, lr, wd, b1, b2, eps, step_size, bc2s);
 }
 
 __global__ void step_incr_kernel(int64_t* step) {
@@ -435,15 +462,27 @@ hipError_t launch_grad_clip_coef(int64_t n, const float* g, float gscale, float 
   return hipGetLastError();
 }
 
+// float4 path when every operand is 16-B aligned; about two float4 slots per thread
+// (every block re-reduces the clip partials, so fewer, fuller blocks)
+static int adamw_vec(const float* p, const float* g, const float* m, const float* v) {
+  return ((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0) ? 1 : 0;
+}
+static int64_t adamw_blocks(int64_t n, int vec) {
+  const int64_t per_block = (int64_t)NT * (vec ? 8 : 2);
+  int64_t blocks = (n + per_block - 1) / per_block;
+  if (blocks > 1024) blocks = 1024;
+  if (blocks < 1) blocks = 1;
+  return blocks;
+}
+
 hipError_t launch_adamw(int64_t n, float* p, const float* g, float* m, float* v, int64_t* step,
                         float lr, float b1, float b2, float eps, float wd, float gscale,
                         hipStream_t st, const float* lr_dev, const float* coef_dev) {
-  int64_t blocks = (n + NT - 1) / NT;
-  if (blocks > 4096) blocks = 4096;
-  if (blocks < 1) blocks = 1;
+  const int vec = adamw_vec(p, g, m, v);
+  const int64_t blocks = adamw_blocks(n, vec);
   ProfLaunch prof_(st, "adamw_kernel", 0.0, 28.0 * n);   // p m v read+write, g read
   hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(NT), 0, st, n, p, g, m, v, step, lr, b1,
-                     b2, eps, wd, gscale, lr_dev, coef_dev);
+                     b2, eps, wd, gscale, lr_dev, coef_dev, vec);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(step_incr_kernel, dim3(1), dim3(64), 0, st, step);
@@ -459,12 +498,11 @@ hipError_t launch_clip_adamw(int64_t n, float* p, const float* g, float* m, floa
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  int64_t blocks = (n + NT - 1) / NT;
-  if (blocks > 4096) blocks = 4096;
-  if (blocks < 1) blocks = 1;
+  const int vec = adamw_vec(p, g, m, v);
+  const int64_t blocks = adamw_blocks(n, vec);
   ProfLaunch prof_(st, "clip_adamw_kernel", 0.0, 28.0 * n);
   hipLaunchKernelGGL(clip_adamw_kernel, dim3((unsigned)blocks), dim3(NT), 0, st, n, p, g, m, v, (const int64_t*)step,
-                     lr_dev, b1, b2, eps, wd, gscale, (const float*)partial, max_norm, norm_out, coef_out);
+                     lr_dev, b1, b2, eps, wd, gscale, (const float*)partial, max_norm, norm_out, coef_out, vec);
   return hipGetLastError();
 }
 
