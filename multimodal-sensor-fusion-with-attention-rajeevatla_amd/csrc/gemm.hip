@@ -333,6 +333,7 @@ __global__ __launch_bounds__(NT, (NSTAGE * DK <= 32 ? 4 : 2)) void gemm_lds_kern
   const float p = args.drop_p;
   const float inv_keep = p < 1.f ? 1.f / (1.f - p) : 0.f;
   if (p > 0.f && args.rng) rs = *args.rng;
+  if (args.rng_advance && blockIdx.x == 0 && threadIdx.x == 0) args.rng_advance[1] += 1;   // see launch_gemm
 
   f32x16 acc[2][2];
 #pragma unroll
@@ -511,6 +512,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_wsr_kernel(const GemmArgs args, in
   const int wm = wave >> 1, wn = wave & 1;
   const int nkt = K / WSR_DK, nkc = K / 8;
 
+  if (args.rng_advance && blockIdx.x == 0 && threadIdx.x == 0) args.rng_advance[1] += 1;   // see launch_gemm
   const int nwg = gridDim.x;
   const int item0 = (int)(((int64_t)blockIdx.x * total_items) / nwg);
   const int item1 = (int)(((int64_t)(blockIdx.x + 1) * total_items) / nwg);
@@ -780,6 +782,7 @@ __global__ __launch_bounds__(NT) void gemm_generic_kernel(const GemmArgs args) {
   const float p = args.drop_p;
   const float inv_keep = p < 1.f ? 1.f / (1.f - p) : 0.f;
   if (p > 0.f && args.rng) rs = *args.rng;
+  if (args.rng_advance && blockIdx.x == 0 && threadIdx.x == 0) args.rng_advance[1] += 1;   // see launch_gemm
 
   f32x16 acc[2][2];
 #pragma unroll
@@ -999,9 +1002,16 @@ __global__ __launch_bounds__(256) void mask_dropout_rows_kernel(const MaskDropAr
   const int m = blockIdx.y;
   const MaskDropJob& J = a.j[m];
   const int64_t n = J.rows * J.D;
-  const bool drop = a.p > 0.f && a.rng != nullptr;
+  const bool drop = a.p > 0.f && (a.rng != nullptr || a.rng_live != nullptr);
   RngSnap rs{0, 0};
-  if (drop) rs = *a.rng;
+  {
+    // live state (the hybrid forward) or a snapshot: a uniform pointer either way
+    const uint64_t* src = a.rng_live ? a.rng_live : (drop ? reinterpret_cast<const uint64_t*>(a.rng) : nullptr);
+    if (src) {
+      rs.seed = src[0];
+      rs.offset = src[1];
+    }
+  }
   const uint32_t thr = p16(a.p);
   const float inv_keep = a.p < 1.f ? 1.f / (1.f - a.p) : 0.f;
   const int D = J.D, L = J.L, M = a.M;
@@ -1032,6 +1042,9 @@ __global__ __launch_bounds__(256) void mask_dropout_rows_kernel(const MaskDropAr
       }
     }
   }
+  // the call's rng snapshot (after the loop: a store ahead of the Philox key's SGPR
+  // constraint made the backend fail to keep the key uniform)
+  if (a.rng_snap && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.rng_snap = rs;
 }
 
 // LDS-DMA eligibility of one operand: 16-B aligned rows (and batch strides),
@@ -1084,12 +1097,14 @@ int cu_count() {
 
 // Every job weight-stationary-eligible with one common K: persistent launches
 // of up to GEMM_MAX_GROUPS groups.
-hipError_t launch_wsr(const GemmJob* jobs, int njobs, hipStream_t st) {
+hipError_t launch_wsr(const GemmJob* jobs, int njobs, hipStream_t st, uint64_t* rng_advance) {
   for (int done = 0; done < njobs;) {
     GemmArgs args;
     memset(&args, 0, sizeof(args));
     args.amode = MODE_RK;
     args.bmode = MODE_RK;
+    args.rng_advance = rng_advance;
+    rng_advance = nullptr;
     int ng = 0, items = 0;
     double fl = 0.0, by = 0.0;
     while (done < njobs && ng < GEMM_MAX_GROUPS) {
@@ -1126,13 +1141,20 @@ hipError_t launch_wsr(const GemmJob* jobs, int njobs, hipStream_t st) {
 int device_cu_count() { return cu_count(); }
 
 hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, float drop_p,
-                       const RngSnap* rng, hipStream_t st) {
+                       const RngSnap* rng, hipStream_t st, uint64_t* rng_advance) {
   {
     bool wsr = njobs > 0;
     for (int i = 0; i < njobs && wsr; ++i)
       wsr = job_wsr(jobs_in[i], amode, bmode) && jobs_in[i].src[0].K == jobs_in[0].src[0].K;
-    if (wsr && getenv("MMF_NO_WSR") == nullptr) return launch_wsr(jobs_in, njobs, st);
+    if (wsr && getenv("MMF_NO_WSR") == nullptr) return launch_wsr(jobs_in, njobs, st, rng_advance);
   }
+  // the tiled launches below take the rng advance on their first launch; a call that
+  // ends in small slabs only advances with a launch of its own
+  struct AdvanceLeft {
+    uint64_t*& adv;
+    hipStream_t st;
+    hipError_t finish(hipError_t e) { return (e == hipSuccess && adv) ? launch_rng_advance(adv, st) : e; }
+  } left{rng_advance, st};
   // Small, non-DMA-able split-K slabs: one thread per slab element, all in one launch
   // (the remaining jobs go through the tiled kernels below).
   std::vector<GemmJob> rest;
@@ -1168,7 +1190,7 @@ hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, 
         if (hipError_t e = flush()) return e;
     }
     if (hipError_t e = flush()) return e;
-    if (rest.empty()) return hipSuccess;
+    if (rest.empty()) return left.finish(hipSuccess);
     jobs_in = rest.data();
     njobs = (int)rest.size();
   }
@@ -1198,6 +1220,8 @@ hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, 
     args.bmode = bmode;
     args.drop_p = drop_p;
     args.rng = rng;
+    args.rng_advance = rng_advance;
+    rng_advance = nullptr;
     int ng = 0, ns = 0, max_blocks = 0;
     // one launch = consecutive jobs of the same kernel flavour
     const bool fast = job_fast(jobs_in[order[done]], amode, bmode);
@@ -1273,9 +1297,11 @@ hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, 
 #undef MMF_LAUNCH_CFG2
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
+    } else if (args.rng_advance) {
+      rng_advance = args.rng_advance;   // nothing launched: the next launch (or finish) takes it
     }
   }
-  return hipSuccess;
+  return left.finish(hipSuccess);
 }
 
 hipError_t launch_reduce(const ReduceJob* jobs, int njobs, hipStream_t st) {

@@ -399,6 +399,10 @@ __global__ __launch_bounds__(NT) void clip_adamw_kernel(int64_t n, float* __rest
   adamw_range(n, p, g, m, v, vec != 0, gscale * coef, lr, wd, b1, b2, eps, step_size, bc2s);
 }
 
+__global__ void rng_advance_kernel(uint64_t* state) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) state[1] = state[1] + 1;
+}
+
 __global__ void step_incr_kernel(int64_t* step) {
   if (threadIdx.x == 0 && blockIdx.x == 0) *step = *step + 1;
 }
@@ -434,6 +438,12 @@ hipError_t launch_gate_wgrad(int B, int M, int H, const float* dscore, const flo
 hipError_t launch_rng_snapshot(const uint64_t* state, RngSnap* snap, hipStream_t st) {
   ProfLaunch prof_(st, "rng_snapshot_kernel", 0.0, 32.0);
   hipLaunchKernelGGL(rng_snapshot_kernel, dim3(1), dim3(64), 0, st, const_cast<uint64_t*>(state), snap);
+  return hipGetLastError();
+}
+
+hipError_t launch_rng_advance(uint64_t* state, hipStream_t st) {
+  ProfLaunch prof_(st, "rng_advance_kernel", 0.0, 16.0);
+  hipLaunchKernelGGL(rng_advance_kernel, dim3(1), dim3(64), 0, st, state);
   return hipGetLastError();
 }
 

@@ -389,7 +389,9 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
   Bump bp(saved);
   Saved s{};
   layout_saved(d, bp, s);
-  if (rng_state) STAGE_TRY("fwd.rng", launch_rng_snapshot(rng_state, s.rng, st));
+  // the rng snapshot {seed, offset} is written by the input-mask kernel (which draws from
+  // the live state) and the live offset advanced by the projection GEMM's first launch:
+  // no launch of its own
   const RngSnap* rng = rng_state ? s.rng : nullptr;
 
   // (1) per-modality projection: P_m = Drop(ReLU(X'_m W_m^T + b_m)), X'_m = Drop(X_m * mask_m)
@@ -398,6 +400,7 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
     MaskDropArgs ma;
     memset(&ma, 0, sizeof(ma));
     ma.n = M; ma.M = M; ma.mask = mask; ma.p = p; ma.rng = rng;
+    ma.rng_live = rng_state; ma.rng_snap = rng_state ? s.rng : nullptr;
     std::vector<GemmJob> jobs;
     for (int m = 0; m < M; ++m) {
       const int L = Lm(d, m), D = d->in_dim[m];
@@ -412,7 +415,8 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
       jobs.push_back(j);
     }
     STAGE_TRY("fwd.input_mask", launch_mask_dropout(ma, st));
-    STAGE_TRY("fwd.proj_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, p, rng, st));
+    STAGE_TRY("fwd.proj_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, p, rng, st,
+                                           const_cast<uint64_t*>(rng_state)));
   }
   // (2) Q/K (and V for the general plan) projections of every present pair (attention.py:104-106)
   if (d->num_pairs) {

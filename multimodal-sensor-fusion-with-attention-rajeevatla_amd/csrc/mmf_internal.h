@@ -132,6 +132,7 @@ struct GemmArgs {
   int32_t amode, bmode;
   float drop_p;              // p of every dropout site in this launch
   const RngSnap* rng;
+  uint64_t* rng_advance;     // optional: block 0 advances this live rng state's offset
 };
 
 // Host-side description of one output (group) and its sources; launch_gemm
@@ -146,8 +147,11 @@ struct GemmJob {
 // operands are all float4-able (16-B aligned, ld % 4 == 0, K % 4 == 0, KR
 // extents % 4 == 0) runs the LDS-DMA pipelined kernel; anything else runs the
 // register-staged generic kernel.
+// rng_advance (optional): a live {seed, offset} rng state whose offset the call's first
+// launch advances by one (the hybrid forward's snapshot is written by the input-mask
+// kernel, which reads the live state from every block and so cannot advance it itself).
 hipError_t launch_gemm(const GemmJob* jobs, int njobs, int amode, int bmode, float drop_p,
-                       const RngSnap* rng, hipStream_t st);
+                       const RngSnap* rng, hipStream_t st, uint64_t* rng_advance = nullptr);
 int device_cu_count();   // CUs of the current device (cached)
 
 // X'_m[r][c] = X_m[r][c] * mask[(r / L_m) * M + m] * (keep(site_m, r*D_m + c) ? 1/(1-p) : 0)
@@ -164,6 +168,11 @@ struct MaskDropArgs {
   const float* mask;
   float p;
   const RngSnap* rng;
+  // optional: read the draws' {seed, offset} from this live state instead of rng, and
+  // write it to rng_snap (block 0) as the call's snapshot; the offset is advanced by
+  // a later launch of the call (launch_gemm's rng_advance)
+  const uint64_t* rng_live;
+  RngSnap* rng_snap;
 };
 hipError_t launch_mask_dropout(MaskDropArgs a, hipStream_t st);
 
@@ -302,6 +311,7 @@ hipError_t launch_gate_wgrad(int B, int M, int H, const float* dscore, const flo
                              float* const* dgw, float* const* dgb, hipStream_t st);
 
 hipError_t launch_rng_snapshot(const uint64_t* state, RngSnap* snap, hipStream_t st);
+hipError_t launch_rng_advance(uint64_t* state, hipStream_t st);   // state[1] += 1
 hipError_t launch_cross_entropy(int B, int C, const float* logits, const int64_t* labels,
                                 float smoothing, float grad_scale, float* loss, float* dlogits,
                                 hipStream_t st);
