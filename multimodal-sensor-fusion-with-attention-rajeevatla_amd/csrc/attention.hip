@@ -949,7 +949,9 @@ MMF_CHAIN16(dk[dt], ds[r], Qs[(qt * 32 + acc_row(r, h)) * LS + dt * 32 + c])
 //   bwd dQ (query on the lane, two passes over key chunks): D, then dS and dQ;
 //   bwd dK: attn_pool_bwd_dk_kernel (key on the lane; any Lk).
 // ---------------------------------------------------------------------------
-template <int HDP, bool BF>
+// LEAN (launch-time: every pair has Lk % 32 == 0 and no per-key mask): whole key tiles
+// only, so the per-register validity tests and the unaligned keep-bit path compile out.
+template <int HDP, bool BF, bool LEAN = false>
 __global__ __launch_bounds__(NT) void attn_poolL_lse_kernel(const AttnArgs A) {
   constexpr int KC = 128;   // keys per LDS chunk (34 KB at HDP = 64: 4 workgroups / CU)
   constexpr int LS = HDP + 4;
@@ -999,7 +1001,7 @@ __global__ __launch_bounds__(NT) void attn_poolL_lse_kernel(const AttnArgs A) {
       float sv[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) sv[r] = s[r] * sl2;
-      if (kbase + kt * 32 + 32 > Lk || P.kmask_mode == 2) {   // partial tile / per-key mask only
+      if (!LEAN && (kbase + kt * 32 + 32 > Lk || P.kmask_mode == 2)) {   // partial tile / per-key mask only
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int key = kbase + kt * 32 + acc_row(r, h);
@@ -1019,8 +1021,9 @@ __global__ __launch_bounds__(NT) void attn_poolL_lse_kernel(const AttnArgs A) {
       l = l * fast_exp2(m - mref) + ls;
       m = mnew;
       if (bits_out) {
-        const uint32_t kb16 =
-            keep_tile16(rs, P.drop_site, (uint64_t)rowidx * Lk + kbase + kt * 32, pdrop, h, qvalid, aligned8);
+        // LEAN: invalid query lanes draw too (their words are never stored)
+        const uint32_t kb16 = keep_tile16(rs, P.drop_site, (uint64_t)rowidx * Lk + kbase + kt * 32, pdrop, h,
+                                          LEAN || qvalid, LEAN || aligned8);
         uint32_t bits = 0;
 #pragma unroll
         for (int g = 0; g < 4; ++g) bits |= ((kb16 >> (4 * g)) & 0xFu) << (8 * g + 4 * h);
@@ -1110,7 +1113,7 @@ __global__ __launch_bounds__(NT) void attn_poolL_colsum_kernel(const AttnArgs A)
   }
 }
 
-template <int HDP, bool BF>
+template <int HDP, bool BF, bool LEAN = false>   // LEAN: as attn_poolL_lse_kernel
 __global__ __launch_bounds__(NT, 4) void attn_poolL_dq_kernel(const AttnArgs A) {
   constexpr int KC = 128;   // keys per LDS chunk (34 KB at HDP = 64: 4 workgroups / CU)
   constexpr int LS = HDP + 4;
@@ -1163,7 +1166,7 @@ __global__ __launch_bounds__(NT, 4) void attn_poolL_dq_kernel(const AttnArgs A) 
     const f32x16 s = dot_rows<HALF, BF>(Ks + (kt * 32 + c) * LS + h * HALF, qf, zero16());
 #pragma unroll
     for (int r = 0; r < 16; ++r) pr[r] = fast_exp2(s[r] * sl2 - lse2);
-    if (kbase + kt * 32 + 32 > Lk || P.kmask_mode == 2) {
+    if (!LEAN && (kbase + kt * 32 + 32 > Lk || P.kmask_mode == 2)) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int key = kbase + kt * 32 + acc_row(r, h);
@@ -1922,6 +1925,9 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
            (((uintptr_t)P.q & 15) == 0) && (((uintptr_t)P.k & 15) == 0) &&
            (kind != Kind::PoolDq || (((uintptr_t)P.dq & 15) == 0));
   }
+  // lean long-key kernels: whole 32-key tiles and no per-key mask in every pair
+  bool long_lean = kind == Kind::PoolLse || kind == Kind::PoolDqLong;
+  for (int i = 0; i < npairs && long_lean; ++i) long_lean = (pairs[i].Lk % 32 == 0) && pairs[i].kmask_mode != 2;
   if (kind == Kind::PoolFused) {
     // lean conditions plus a single query block and float4-able dQ rows
     for (int i = 0; i < npairs && lean; ++i)
@@ -2007,19 +2013,31 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
     const bool alt = kind == Kind::Prep ? prep_vec : (lean && kind <= Kind::PoolFused);
     const bool bf = math_bf16();
     const char* kname = kNames[(int)kind][(alt ? 2 : 0) + (small ? 0 : 1)];
-    ProfLaunch prof_(st, with_bf(kname, bf), fl, by);
+    const char* pname = with_bf(kname, bf);
+    if (long_lean) pname = with_bf(pname, true);   // "<hd, bf, true>": the LEAN instantiation
+    ProfLaunch prof_(st, pname, fl, by);
     switch (kind) {
       case Kind::PoolLse:
-        if (small) { if (bf) hipLaunchKernelGGL((attn_poolL_lse_kernel<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_lse_kernel<32, false>), grid, dim3(NT), 0, st, a); }
-        else { if (bf) hipLaunchKernelGGL((attn_poolL_lse_kernel<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_lse_kernel<64, false>), grid, dim3(NT), 0, st, a); }
+        if (long_lean) {
+          if (small) { if (bf) hipLaunchKernelGGL((attn_poolL_lse_kernel<32, true, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_lse_kernel<32, false, true>), grid, dim3(NT), 0, st, a); }
+          else { if (bf) hipLaunchKernelGGL((attn_poolL_lse_kernel<64, true, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_lse_kernel<64, false, true>), grid, dim3(NT), 0, st, a); }
+        } else {
+          if (small) { if (bf) hipLaunchKernelGGL((attn_poolL_lse_kernel<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_lse_kernel<32, false>), grid, dim3(NT), 0, st, a); }
+          else { if (bf) hipLaunchKernelGGL((attn_poolL_lse_kernel<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_lse_kernel<64, false>), grid, dim3(NT), 0, st, a); }
+        }
         break;
       case Kind::PoolColsum:
         if (small) { if (bf) hipLaunchKernelGGL((attn_poolL_colsum_kernel<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_colsum_kernel<32, false>), grid, dim3(NT), 0, st, a); }
         else { if (bf) hipLaunchKernelGGL((attn_poolL_colsum_kernel<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_colsum_kernel<64, false>), grid, dim3(NT), 0, st, a); }
         break;
       case Kind::PoolDqLong:
-        if (small) { if (bf) hipLaunchKernelGGL((attn_poolL_dq_kernel<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_dq_kernel<32, false>), grid, dim3(NT), 0, st, a); }
-        else { if (bf) hipLaunchKernelGGL((attn_poolL_dq_kernel<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_dq_kernel<64, false>), grid, dim3(NT), 0, st, a); }
+        if (long_lean) {
+          if (small) { if (bf) hipLaunchKernelGGL((attn_poolL_dq_kernel<32, true, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_dq_kernel<32, false, true>), grid, dim3(NT), 0, st, a); }
+          else { if (bf) hipLaunchKernelGGL((attn_poolL_dq_kernel<64, true, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_dq_kernel<64, false, true>), grid, dim3(NT), 0, st, a); }
+        } else {
+          if (small) { if (bf) hipLaunchKernelGGL((attn_poolL_dq_kernel<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_dq_kernel<32, false>), grid, dim3(NT), 0, st, a); }
+          else { if (bf) hipLaunchKernelGGL((attn_poolL_dq_kernel<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_dq_kernel<64, false>), grid, dim3(NT), 0, st, a); }
+        }
         break;
       case Kind::Fwd:
         if (small) { if (bf) hipLaunchKernelGGL((attn_fwd_kernel<32, 0, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_fwd_kernel<32, 0, false>), grid, dim3(NT), 0, st, a); }
