@@ -69,6 +69,24 @@ def total_step_flops(w):
     return 3 * fwd
 
 
+def kernel_precision(kname):
+    """The int matmul-precision template argument of a library MFMA kernel's profiler name
+    (0 fp32, 1 bf16 "medium", 2 bf16x3 "high"): the last integer argument, optionally
+    followed by a trailing bool (e.g. "attn_poolL_lse_kernel<64, 1, true>",
+    "gemm_lds_kernel<0, 1, 16, 3, 2>", "gemm_wsr_kernel<1>").  Kernels without one
+    (the generic GEMM, the tail / head kernels) run fp32."""
+    if kname.startswith("gemm_generic"):
+        return 0
+    m = re.search(r"[<, ]([012])(?:, (?:true|false))?>$", kname)
+    return int(m.group(1)) if m else 0
+
+
+def mfma_peak(kname):
+    """Dense MFMA peak for a kernel's algorithmic FLOPs: fp32 MFMA, bf16 MFMA, or for the
+    bf16x3 form one third of the bf16 peak (three bf16 MFMAs per fp32-equivalent product)."""
+    return {0: FP32_MFMA_PEAK_TFLOPS, 1: BF16_MFMA_PEAK_TFLOPS, 2: BF16_MFMA_PEAK_TFLOPS / 3.0}[kernel_precision(kname)]
+
+
 def kernel_table(launches, steps):
     """Per kernel name: time per step, average launch duration and the roofline
     of its launches (algorithmic FLOPs / bytes from the library's per-launch
@@ -83,8 +101,7 @@ def kernel_table(launches, steps):
     out = {}
     for kname, (ms, n, flops, nbytes) in sorted(acc.items(), key=lambda kv: -kv[1][0]):
         sec = ms * 1e-3
-        # bf16-operand instantiations (matmul precision "medium") end in ", true>"
-        fpeak = BF16_MFMA_PEAK_TFLOPS if re.search(r"[<, ]true>$", kname) else FP32_MFMA_PEAK_TFLOPS
+        fpeak = mfma_peak(kname)
         t_f = flops / (fpeak * 1e12)
         t_b = nbytes / (HBM_PEAK_GBS * 1e9)
         if t_f >= t_b:
@@ -186,10 +203,11 @@ def main():
     ap.add_argument("--dump-launches", default=None,
                     help="write every profiled launch (stage, kernel, ms, flops, bytes) of the last profile step "
                          "to this JSON file")
-    ap.add_argument("--precision", default="highest", choices=["highest", "medium"],
+    ap.add_argument("--precision", default="highest", choices=["highest", "high", "medium"],
                     help="torch.set_float32_matmul_precision for the run: 'highest' = fp32 MFMA (the "
-                         "fp32-parity headline), 'medium' = bf16 MFMA operands, fp32 accumulate "
-                         "(config/base.yaml:80)")
+                         "fp32-parity headline), 'high' = bf16x3 (operands split into bf16 hi + lo, "
+                         "three bf16 MFMAs, fp32 accumulate), 'medium' = bf16 MFMA operands, fp32 "
+                         "accumulate (config/base.yaml:80)")
     args = ap.parse_args()
     torch.set_float32_matmul_precision(args.precision)
 
@@ -274,7 +292,8 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "fp32" if args.precision == "highest" else "bf16 (fp32 accumulate)",
+            "dtype": {"highest": "fp32", "high": "fp32 as bf16x3 (hi + lo operands, fp32 accumulate)",
+                      "medium": "bf16 (fp32 accumulate)"}[args.precision],
             "data": "synthetic (N(0,1) encoder outputs, random-init weights, seeded)",
             "config": {"workload": f"{args.workload}: HybridFusion M={M} B={B}/gpu L={lens or 1}"
                                    f"{'' if max(Ls) else ' (2-D reference semantics)'} D={D} H={H} heads={heads} "

@@ -43,7 +43,10 @@ extern "C" {
 
 enum {
   MMF_PRECISION_HIGHEST = 0, /* "highest": fp32 operands */
-  MMF_PRECISION_MEDIUM = 1   /* "medium": bf16 operands, fp32 accumulate ("high" = TF32 is absent on gfx950: use HIGHEST) */
+  MMF_PRECISION_MEDIUM = 1,  /* "medium": bf16 operands, fp32 accumulate */
+  MMF_PRECISION_HIGH = 2     /* "high": every fp32 operand split into bf16 hi + lo, three bf16 MFMAs
+                                (lo*hi + hi*lo + hi*hi), fp32 accumulate -- torch's "sum of two bfloat16
+                                numbers" form of "high" (gfx950 has no TF32) */
 };
 
 enum {

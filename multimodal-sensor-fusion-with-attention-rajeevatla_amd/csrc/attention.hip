@@ -125,7 +125,7 @@ __device__ __forceinline__ void load_frag(float* f, const float* row, int dbase,
 
 // acc += A_lds_row(lane) . f   over the HALF-long contraction (row-wise LDS operand)
 // (BF: bf16 MFMA operands, see mfma_k16 in mmf_device.h; eight k-steps per chain)
-template <int HALF, bool BF = false>
+template <int HALF, int BF = 0>
 __device__ __forceinline__ f32x16 dot_rows(const float* lds_row, const float* f, f32x16 acc) {
   static_assert(HALF % 8 == 0, "k chains of 8");
 #pragma unroll
@@ -164,7 +164,7 @@ __device__ __forceinline__ f32x16 zero16() {
 // ---------------------------------------------------------------------------
 // Forward (MODE 0) and attention-probability output (MODE 1, needs LSE).
 // ---------------------------------------------------------------------------
-template <int HDP, int MODE, bool BF>
+template <int HDP, int MODE, int BF>
 __global__ __launch_bounds__(NT) void attn_fwd_kernel(const AttnArgs A) {
   constexpr int KC = HDP == 32 ? 128 : 64;
   constexpr int LS = HDP + 4;
@@ -358,7 +358,7 @@ __global__ __launch_bounds__(NT) void attn_bwd_prep_kernel(const AttnArgs A) {
 // ---------------------------------------------------------------------------
 // dK / dV: one workgroup = 128 keys (4 waves x 32, key on the lane).
 // ---------------------------------------------------------------------------
-template <int HDP, bool BF>
+template <int HDP, int BF>
 __global__ __launch_bounds__(NT) void attn_bwd_dkv_kernel(const AttnArgs A) {
   constexpr int QC = HDP == 32 ? 128 : 64;
   constexpr int LS = HDP + 4;
@@ -467,7 +467,7 @@ MMF_CHAIN16(dv[dt], pd[r], Ds[(qt * 32 + acc_row(r, h)) * LS + dt * 32 + c])
 // ---------------------------------------------------------------------------
 // dQ: one workgroup = 128 queries (query on the lane, like the forward).
 // ---------------------------------------------------------------------------
-template <int HDP, bool BF>
+template <int HDP, int BF>
 __global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(const AttnArgs A) {
   constexpr int KC = HDP == 32 ? 128 : 64;
   constexpr int LS = HDP + 4;
@@ -614,7 +614,7 @@ __device__ __forceinline__ float colsum_tile(const float (&v)[16], int c) {
   return a1 + dpp<DPP_XOR1>(a1);
 }
 
-template <int HDP, bool BF>
+template <int HDP, int BF>
 __global__ __launch_bounds__(NT) void attn_pool_fwd_kernel(const AttnArgs A) {
   constexpr int LS = HDP + 4;
   constexpr int HALF = HDP / 2;
@@ -733,7 +733,7 @@ __global__ __launch_bounds__(NT) void attn_pool_fwd_kernel(const AttnArgs A) {
 }
 
 // Pooled backward, query on the lane: D = rowsum(P' dpbar)/Lq, dS, dQ.
-template <int HDP, bool BF>
+template <int HDP, int BF>
 __global__ __launch_bounds__(NT) void attn_pool_bwd_dq_kernel(const AttnArgs A) {
   constexpr int LS = HDP + 4;
   constexpr int HALF = HDP / 2;
@@ -841,7 +841,7 @@ MMF_CHAIN16(dq[dt], Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], ds[r])
 }
 
 // Pooled backward, key on the lane: dK = scale * dS^T Q (needs D from the dq kernel).
-template <int HDP, bool BF>
+template <int HDP, int BF>
 __global__ __launch_bounds__(NT, 4) void attn_pool_bwd_dk_kernel(const AttnArgs A) {
   constexpr int QC = 128;
   constexpr int LS = HDP + 4;
@@ -951,7 +951,7 @@ MMF_CHAIN16(dk[dt], ds[r], Qs[(qt * 32 + acc_row(r, h)) * LS + dt * 32 + c])
 // ---------------------------------------------------------------------------
 // LEAN (launch-time: every pair has Lk % 32 == 0 and no per-key mask): whole key tiles
 // only, so the per-register validity tests and the unaligned keep-bit path compile out.
-template <int HDP, bool BF, bool LEAN = false>
+template <int HDP, int BF, bool LEAN = false>
 __global__ __launch_bounds__(NT) void attn_poolL_lse_kernel(const AttnArgs A) {
   constexpr int KC = 128;   // keys per LDS chunk (34 KB at HDP = 64: 4 workgroups / CU)
   constexpr int LS = HDP + 4;
@@ -1035,7 +1035,7 @@ __global__ __launch_bounds__(NT) void attn_poolL_lse_kernel(const AttnArgs A) {
   if (qvalid && h == 0) P.lse[rowidx] = l > 0.f ? (m + __log2f(l)) * (1.f / LOG2E) : -INFINITY;
 }
 
-template <int HDP, bool BF>
+template <int HDP, int BF>
 __global__ __launch_bounds__(NT) void attn_poolL_colsum_kernel(const AttnArgs A) {
   constexpr int QC = 128;
   constexpr int LS = HDP + 4;
@@ -1113,7 +1113,7 @@ __global__ __launch_bounds__(NT) void attn_poolL_colsum_kernel(const AttnArgs A)
   }
 }
 
-template <int HDP, bool BF, bool LEAN = false>   // LEAN: as attn_poolL_lse_kernel
+template <int HDP, int BF, bool LEAN = false>   // LEAN: as attn_poolL_lse_kernel
 __global__ __launch_bounds__(NT, 4) void attn_poolL_dq_kernel(const AttnArgs A) {
   constexpr int KC = 128;   // keys per LDS chunk (34 KB at HDP = 64: 4 workgroups / CU)
   constexpr int LS = HDP + 4;
@@ -1288,7 +1288,7 @@ __device__ __forceinline__ void lean_keep_words(uint32_t (&words)[NKT], const Rn
 
 // DROP (train mode with p > 0, launch-time choice): the loop body has no dropout
 // branches.
-template <int HDP, bool BF, bool DROP = true>
+template <int HDP, int BF, bool DROP = true>
 __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(const AttnArgs A) {
   constexpr int LS = HDP + 4;
   constexpr int HALF = HDP / 2;
@@ -1442,7 +1442,7 @@ __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(cons
 
 // dq pass, query on the lane: G[k] = keep ? dpbar[k] / ((1-p) Lq) : 0;
 // D = rowsum(P . G) (saved for the dk pass); dS = P . (G - D); dQ = scale dS K.
-template <int HDP, bool BF>
+template <int HDP, int BF>
 __global__ __launch_bounds__(NT) void attn_pool_bwd_dq_lean(const AttnArgs A) {
   constexpr int LS = HDP + 4;
   constexpr int HALF = HDP / 2;
@@ -1552,7 +1552,7 @@ MMF_CHAIN16(dq[dt], Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], ds[r])
 }
 
 // dk pass, key on the lane: dK = scale * dS^T Q, dS = P . (G - D).
-template <int HDP, bool BF>
+template <int HDP, int BF>
 __global__ __launch_bounds__(NT) void attn_pool_bwd_dk_lean(const AttnArgs A) {
   constexpr int QC = 128;
   constexpr int LS = HDP + 4;
@@ -1705,7 +1705,7 @@ __device__ __forceinline__ void fused_issue_loads(const AttnArgs& A, const AttnP
 // One (pair, sample, head) item of the fused lean backward from its issued loads;
 // Ks / Qs are [PKC][HDP + 4] LDS images (Ks doubles as the dS^T quarter image),
 // gk [PKC].  Called by every thread of the workgroup (it holds barriers).
-template <int HDP, bool BF>
+template <int HDP, int BF>
 __device__ __forceinline__ void fused_lean_item(const AttnArgs& A, const AttnPair& P, int b, int head, float* Ks,
                                                 float* Qs, float* gk, int h, int c, const FusedLoads<HDP>& LD) {
   constexpr int LS = HDP + 4;
@@ -1874,7 +1874,7 @@ MMF_CHAIN16(dq[dt], Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], pr[kt][r])
   BSTAMP_RT(8)
 }
 
-template <int HDP, bool BF>
+template <int HDP, int BF>
 __global__ __launch_bounds__(NT, 4) void attn_pool_bwd_fused_lean(const AttnArgs A) {
   __shared__ __attribute__((aligned(16))) float Ks[PKC * (HDP + 4)];   // K, then the dS^T quarters
   __shared__ __attribute__((aligned(16))) float Qs[PKC * (HDP + 4)];
@@ -1888,20 +1888,22 @@ __global__ __launch_bounds__(NT, 4) void attn_pool_bwd_fused_lean(const AttnArgs
   fused_lean_item<HDP, BF>(A, P, bid / A.heads, bid % A.heads, Ks, Qs, gk, lane >> 5, lane & 31, LD);
 }
 
-// "name<a, b>" -> "name<a, b, false|true>" (the rocprof name of the BF instantiation);
-// stable storage for the profiler tags.
-const char* with_bf(const char* base, bool bf) {
+// "name<a, b>" -> "name<a, b, ARG>" ("name<>" -> "name<ARG>"): the rocprof name of an
+// instantiation (ARG: the precision 0 | 1 | 2, or a trailing bool); stable storage for
+// the profiler tags.
+const char* with_arg(const char* base, const char* arg) {
   static std::mutex mu;
-  static std::map<std::string, std::string> names[2];
+  static std::map<std::string, std::string> names;
   std::lock_guard<std::mutex> lk(mu);
-  auto& slot = names[bf ? 1 : 0][base];
+  std::string key = std::string(base) + "|" + arg;
+  auto& slot = names[key];
   if (slot.empty()) {
     std::string b(base);
     const size_t gt = b.rfind('>');
-    if (b.size() >= 2 && b.compare(b.size() - 2, 2, "<>") == 0)   // "name<>" -> "name<false|true>"
-      slot = b.substr(0, b.size() - 1) + (bf ? "true>" : "false>");
+    if (b.size() >= 2 && b.compare(b.size() - 2, 2, "<>") == 0)
+      slot = b.substr(0, b.size() - 1) + arg + ">";
     else
-      slot = gt == std::string::npos ? b : b.substr(0, gt) + (bf ? ", true>" : ", false>");
+      slot = gt == std::string::npos ? b : b.substr(0, gt) + ", " + arg + ">";
   }
   return slot.c_str();
 }
@@ -2011,80 +2013,88 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
         {"attn_poolL_colsum_kernel<32>", "attn_poolL_colsum_kernel<64>", "", ""},
         {"attn_poolL_dq_kernel<32>", "attn_poolL_dq_kernel<64>", "", ""}};
     const bool alt = kind == Kind::Prep ? prep_vec : (lean && kind <= Kind::PoolFused);
-    const bool bf = math_bf16();
+    const int pr = math_mode();
+// one launch of the instantiation for the call's precision: PRV names the kernel's
+// int precision template argument inside KERNEL
+#define MMF_PR_LAUNCH(...)                                                                   \
+  switch (pr) {                                                                              \
+    case 2: { constexpr int PRV = 2; hipLaunchKernelGGL((__VA_ARGS__), grid, dim3(NT), 0, st, a); } break; \
+    case 1: { constexpr int PRV = 1; hipLaunchKernelGGL((__VA_ARGS__), grid, dim3(NT), 0, st, a); } break; \
+    default: { constexpr int PRV = 0; hipLaunchKernelGGL((__VA_ARGS__), grid, dim3(NT), 0, st, a); } break; \
+  }
     const char* kname = kNames[(int)kind][(alt ? 2 : 0) + (small ? 0 : 1)];
-    const char* pname = with_bf(kname, bf);
-    if (long_lean) pname = with_bf(pname, true);   // "<hd, bf, true>": the LEAN instantiation
+    const char* pname = with_arg(kname, pr == 2 ? "2" : (pr == 1 ? "1" : "0"));
+    if (long_lean) pname = with_arg(pname, "true");   // "<hd, pr, true>": the LEAN instantiation
     ProfLaunch prof_(st, pname, fl, by);
     switch (kind) {
       case Kind::PoolLse:
         if (long_lean) {
-          if (small) { if (bf) hipLaunchKernelGGL((attn_poolL_lse_kernel<32, true, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_lse_kernel<32, false, true>), grid, dim3(NT), 0, st, a); }
-          else { if (bf) hipLaunchKernelGGL((attn_poolL_lse_kernel<64, true, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_lse_kernel<64, false, true>), grid, dim3(NT), 0, st, a); }
+          if (small) { MMF_PR_LAUNCH(attn_poolL_lse_kernel<32, PRV, true>) }
+          else { MMF_PR_LAUNCH(attn_poolL_lse_kernel<64, PRV, true>) }
         } else {
-          if (small) { if (bf) hipLaunchKernelGGL((attn_poolL_lse_kernel<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_lse_kernel<32, false>), grid, dim3(NT), 0, st, a); }
-          else { if (bf) hipLaunchKernelGGL((attn_poolL_lse_kernel<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_lse_kernel<64, false>), grid, dim3(NT), 0, st, a); }
+          if (small) { MMF_PR_LAUNCH(attn_poolL_lse_kernel<32, PRV>) }
+          else { MMF_PR_LAUNCH(attn_poolL_lse_kernel<64, PRV>) }
         }
         break;
       case Kind::PoolColsum:
-        if (small) { if (bf) hipLaunchKernelGGL((attn_poolL_colsum_kernel<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_colsum_kernel<32, false>), grid, dim3(NT), 0, st, a); }
-        else { if (bf) hipLaunchKernelGGL((attn_poolL_colsum_kernel<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_colsum_kernel<64, false>), grid, dim3(NT), 0, st, a); }
+        if (small) { MMF_PR_LAUNCH(attn_poolL_colsum_kernel<32, PRV>) }
+        else { MMF_PR_LAUNCH(attn_poolL_colsum_kernel<64, PRV>) }
         break;
       case Kind::PoolDqLong:
         if (long_lean) {
-          if (small) { if (bf) hipLaunchKernelGGL((attn_poolL_dq_kernel<32, true, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_dq_kernel<32, false, true>), grid, dim3(NT), 0, st, a); }
-          else { if (bf) hipLaunchKernelGGL((attn_poolL_dq_kernel<64, true, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_dq_kernel<64, false, true>), grid, dim3(NT), 0, st, a); }
+          if (small) { MMF_PR_LAUNCH(attn_poolL_dq_kernel<32, PRV, true>) }
+          else { MMF_PR_LAUNCH(attn_poolL_dq_kernel<64, PRV, true>) }
         } else {
-          if (small) { if (bf) hipLaunchKernelGGL((attn_poolL_dq_kernel<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_dq_kernel<32, false>), grid, dim3(NT), 0, st, a); }
-          else { if (bf) hipLaunchKernelGGL((attn_poolL_dq_kernel<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_poolL_dq_kernel<64, false>), grid, dim3(NT), 0, st, a); }
+          if (small) { MMF_PR_LAUNCH(attn_poolL_dq_kernel<32, PRV>) }
+          else { MMF_PR_LAUNCH(attn_poolL_dq_kernel<64, PRV>) }
         }
         break;
       case Kind::Fwd:
-        if (small) { if (bf) hipLaunchKernelGGL((attn_fwd_kernel<32, 0, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_fwd_kernel<32, 0, false>), grid, dim3(NT), 0, st, a); }
-        else { if (bf) hipLaunchKernelGGL((attn_fwd_kernel<64, 0, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_fwd_kernel<64, 0, false>), grid, dim3(NT), 0, st, a); }
+        if (small) { MMF_PR_LAUNCH(attn_fwd_kernel<32, 0, PRV>) }
+        else { MMF_PR_LAUNCH(attn_fwd_kernel<64, 0, PRV>) }
         break;
       case Kind::Probs:
-        if (small) { if (bf) hipLaunchKernelGGL((attn_fwd_kernel<32, 1, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_fwd_kernel<32, 1, false>), grid, dim3(NT), 0, st, a); }
-        else { if (bf) hipLaunchKernelGGL((attn_fwd_kernel<64, 1, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_fwd_kernel<64, 1, false>), grid, dim3(NT), 0, st, a); }
+        if (small) { MMF_PR_LAUNCH(attn_fwd_kernel<32, 1, PRV>) }
+        else { MMF_PR_LAUNCH(attn_fwd_kernel<64, 1, PRV>) }
         break;
       case Kind::Prep:
         if (prep_vec) hipLaunchKernelGGL(attn_bwd_prep_vec_kernel, grid, dim3(NT), 0, st, a);
         else hipLaunchKernelGGL(attn_bwd_prep_kernel, grid, dim3(NT), 0, st, a);
         break;
       case Kind::Dkv:
-        if (small) { if (bf) hipLaunchKernelGGL((attn_bwd_dkv_kernel<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_bwd_dkv_kernel<32, false>), grid, dim3(NT), 0, st, a); }
-        else { if (bf) hipLaunchKernelGGL((attn_bwd_dkv_kernel<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_bwd_dkv_kernel<64, false>), grid, dim3(NT), 0, st, a); }
+        if (small) { MMF_PR_LAUNCH(attn_bwd_dkv_kernel<32, PRV>) }
+        else { MMF_PR_LAUNCH(attn_bwd_dkv_kernel<64, PRV>) }
         break;
       case Kind::Dq:
-        if (small) { if (bf) hipLaunchKernelGGL((attn_bwd_dq_kernel<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_bwd_dq_kernel<32, false>), grid, dim3(NT), 0, st, a); }
-        else { if (bf) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_bwd_dq_kernel<64, false>), grid, dim3(NT), 0, st, a); }
+        if (small) { MMF_PR_LAUNCH(attn_bwd_dq_kernel<32, PRV>) }
+        else { MMF_PR_LAUNCH(attn_bwd_dq_kernel<64, PRV>) }
         break;
       case Kind::PoolFwd:
         if (lean && a.drop_p > 0.f) {
-          if (small) { if (bf) hipLaunchKernelGGL((attn_pool_fwd_lean<32, true, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_fwd_lean<32, false, true>), grid, dim3(NT), 0, st, a); }
-          else { if (bf) hipLaunchKernelGGL((attn_pool_fwd_lean<64, true, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_fwd_lean<64, false, true>), grid, dim3(NT), 0, st, a); }
+          if (small) { MMF_PR_LAUNCH(attn_pool_fwd_lean<32, PRV, true>) }
+          else { MMF_PR_LAUNCH(attn_pool_fwd_lean<64, PRV, true>) }
         } else if (lean) {
-          if (small) { if (bf) hipLaunchKernelGGL((attn_pool_fwd_lean<32, true, false>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_fwd_lean<32, false, false>), grid, dim3(NT), 0, st, a); }
-          else { if (bf) hipLaunchKernelGGL((attn_pool_fwd_lean<64, true, false>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_fwd_lean<64, false, false>), grid, dim3(NT), 0, st, a); }
+          if (small) { MMF_PR_LAUNCH(attn_pool_fwd_lean<32, PRV, false>) }
+          else { MMF_PR_LAUNCH(attn_pool_fwd_lean<64, PRV, false>) }
         }
-        else if (small) { if (bf) hipLaunchKernelGGL((attn_pool_fwd_kernel<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_fwd_kernel<32, false>), grid, dim3(NT), 0, st, a); }
-        else { if (bf) hipLaunchKernelGGL((attn_pool_fwd_kernel<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_fwd_kernel<64, false>), grid, dim3(NT), 0, st, a); }
+        else if (small) { MMF_PR_LAUNCH(attn_pool_fwd_kernel<32, PRV>) }
+        else { MMF_PR_LAUNCH(attn_pool_fwd_kernel<64, PRV>) }
         break;
       case Kind::PoolDq:
-        if (lean && small) { if (bf) hipLaunchKernelGGL((attn_pool_bwd_dq_lean<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_bwd_dq_lean<32, false>), grid, dim3(NT), 0, st, a); }
-        else if (lean) { if (bf) hipLaunchKernelGGL((attn_pool_bwd_dq_lean<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_bwd_dq_lean<64, false>), grid, dim3(NT), 0, st, a); }
-        else if (small) { if (bf) hipLaunchKernelGGL((attn_pool_bwd_dq_kernel<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_bwd_dq_kernel<32, false>), grid, dim3(NT), 0, st, a); }
-        else { if (bf) hipLaunchKernelGGL((attn_pool_bwd_dq_kernel<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_bwd_dq_kernel<64, false>), grid, dim3(NT), 0, st, a); }
+        if (lean && small) { MMF_PR_LAUNCH(attn_pool_bwd_dq_lean<32, PRV>) }
+        else if (lean) { MMF_PR_LAUNCH(attn_pool_bwd_dq_lean<64, PRV>) }
+        else if (small) { MMF_PR_LAUNCH(attn_pool_bwd_dq_kernel<32, PRV>) }
+        else { MMF_PR_LAUNCH(attn_pool_bwd_dq_kernel<64, PRV>) }
         break;
       case Kind::PoolFused:
-        if (small) { if (bf) hipLaunchKernelGGL((attn_pool_bwd_fused_lean<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_bwd_fused_lean<32, false>), grid, dim3(NT), 0, st, a); }
-        else { if (bf) hipLaunchKernelGGL((attn_pool_bwd_fused_lean<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_bwd_fused_lean<64, false>), grid, dim3(NT), 0, st, a); }
+        if (small) { MMF_PR_LAUNCH(attn_pool_bwd_fused_lean<32, PRV>) }
+        else { MMF_PR_LAUNCH(attn_pool_bwd_fused_lean<64, PRV>) }
         break;
       case Kind::PoolDk:
-        if (lean && small) { if (bf) hipLaunchKernelGGL((attn_pool_bwd_dk_lean<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_bwd_dk_lean<32, false>), grid, dim3(NT), 0, st, a); }
-        else if (lean) { if (bf) hipLaunchKernelGGL((attn_pool_bwd_dk_lean<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_bwd_dk_lean<64, false>), grid, dim3(NT), 0, st, a); }
-        else if (small) { if (bf) hipLaunchKernelGGL((attn_pool_bwd_dk_kernel<32, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_bwd_dk_kernel<32, false>), grid, dim3(NT), 0, st, a); }
-        else { if (bf) hipLaunchKernelGGL((attn_pool_bwd_dk_kernel<64, true>), grid, dim3(NT), 0, st, a); else hipLaunchKernelGGL((attn_pool_bwd_dk_kernel<64, false>), grid, dim3(NT), 0, st, a); }
+        if (lean && small) { MMF_PR_LAUNCH(attn_pool_bwd_dk_lean<32, PRV>) }
+        else if (lean) { MMF_PR_LAUNCH(attn_pool_bwd_dk_lean<64, PRV>) }
+        else if (small) { MMF_PR_LAUNCH(attn_pool_bwd_dk_kernel<32, PRV>) }
+        else { MMF_PR_LAUNCH(attn_pool_bwd_dk_kernel<64, PRV>) }
         break;
     }
     hipError_t e = hipGetLastError();
@@ -2165,9 +2175,9 @@ hipError_t launch_attn_bwd(const AttnPair* pairs, int npairs, int B, int heads, 
 // threads): [0] fused backward, [1] pooled forward.  Diagnostic (scripts/attn_stamps.py).
 extern "C" int mmf_attn_occupancy(int* out) {
   int a = 0, b = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, mmf::attn_pool_bwd_fused_lean<32, false>, 256, 0) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, mmf::attn_pool_bwd_fused_lean<32, 0>, 256, 0) !=
           hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, mmf::attn_pool_fwd_lean<32, false>, 256, 0) != hipSuccess)
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, mmf::attn_pool_fwd_lean<32, 0>, 256, 0) != hipSuccess)
     return 3;
   out[0] = a;
   out[1] = b;

@@ -53,7 +53,8 @@ void layout_cma_ws(const mmf_cma_desc* d, Bump& bp, CmaWs& w) {
 
 int check_cma(const mmf_cma_desc* d) {
   if (!d) return fail(MMF_EINVAL, "null descriptor");
-  if (d->matmul_precision != MMF_PRECISION_HIGHEST && d->matmul_precision != MMF_PRECISION_MEDIUM)
+  if (d->matmul_precision != MMF_PRECISION_HIGHEST && d->matmul_precision != MMF_PRECISION_MEDIUM &&
+      d->matmul_precision != MMF_PRECISION_HIGH)
     return fail(MMF_EINVAL, "bad matmul_precision %d", d->matmul_precision);
   if (d->batch < 1 || d->lq < 1 || d->lk < 1 || d->query_dim < 1 || d->key_dim < 1)
     return fail(MMF_EINVAL, "bad CrossModalAttention shape");
@@ -271,7 +272,7 @@ int mmf_cma_forward(const mmf_cma_desc* d, const mmf_cma_params* W, const float*
                     void* stream) {
   int rc = check_cma(d);
   if (rc) return rc;
-  mmf::MathScope math_(d->matmul_precision == MMF_PRECISION_MEDIUM);
+  mmf::MathScope math_(d->matmul_precision);
   if (!W || !query || !key || !value || !saved || !attended) return fail(MMF_EINVAL, "null argument");
   if (d->mask_mode && !mask) return fail(MMF_EINVAL, "mask_mode set but mask is null");
   hipStream_t st = (hipStream_t)stream;
@@ -314,7 +315,7 @@ int mmf_cma_backward(const mmf_cma_desc* d, const mmf_cma_params* W, const float
                      float* dkey, float* dvalue, void* stream) {
   int rc = check_cma(d);
   if (rc) return rc;
-  mmf::MathScope math_(d->matmul_precision == MMF_PRECISION_MEDIUM);
+  mmf::MathScope math_(d->matmul_precision);
   if (!W || !query || !key || !value || !saved || !dA || !workspace || !G)
     return fail(MMF_EINVAL, "null argument");
   hipStream_t st = (hipStream_t)stream;

@@ -309,7 +309,7 @@ __device__ __forceinline__ void lds_barrier() {
 // (source, k0) cursor over one tile's contraction
 struct KCursor { int si, k0, kend; };
 
-template <int AMODE, int BMODE, int DK, int NSTAGE, bool BF = false>
+template <int AMODE, int BMODE, int DK, int NSTAGE, int BF = 0>
 __global__ __launch_bounds__(NT, (NSTAGE * DK <= 32 ? 4 : 2)) void gemm_lds_kernel(const GemmArgs args) {
   constexpr int DTILE = BM * DK;                  // floats per operand tile
   constexpr int DMA_PER_TILE = 2 * (BM * DK / 1024);  // glds per wave per (A, B) tile pair
@@ -427,7 +427,7 @@ __global__ __launch_bounds__(NT, (NSTAGE * DK <= 32 ? 4 : 2)) void gemm_lds_kern
                                     : At[row * DK + ((((kk >> 2) ^ swz<DK>(row))) << 2) + (kk & 3)];
         }
       }
-if constexpr (BF) {
+if constexpr (BF != 0) {
         // chunks 2u, 2u+1 (16 k) -> one bf16 MFMA per accumulator
 #pragma unroll
         for (int u = 0; u < DK / 16; ++u) {
@@ -450,7 +450,7 @@ if constexpr (BF) {
 #pragma unroll
           for (int a = 0; a < 2; ++a)
 #pragma unroll
-            for (int b = 0; b < 2; ++b) acc[a][b] = mfma_k16<true>(av[a], bv[b], acc[a][b]);
+            for (int b = 0; b < 2; ++b) acc[a][b] = mfma_k16<BF>(av[a], bv[b], acc[a][b]);
         }
       } else {
 #pragma unroll
@@ -502,7 +502,7 @@ if constexpr (BF) {
 // a tile is written out.  Persistent grid: 2 workgroups per CU.
 constexpr int WSR_DK = 16, WSR_NS = 6, WSR_NKC = 16;   // k-tile, ring depth, max 8-deep k chunks (K <= 128)
 
-template <bool BF>
+template <int BF>
 __global__ __launch_bounds__(NT, 2) void gemm_wsr_kernel(const GemmArgs args, int total_items, int K) {
   constexpr int DTILE = BM * WSR_DK;
   __shared__ __attribute__((aligned(16))) float ring[WSR_NS * DTILE];
@@ -618,7 +618,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_wsr_kernel(const GemmArgs args, in
         lds_barrier();   // tile f landed for every wave; every wave is done with slot (f-1) % NS
         if (nissued < nflat) issue(nissued++);
         const float* At = ring + (f % WSR_NS) * DTILE;
-if constexpr (BF) {
+if constexpr (BF != 0) {
           float av[2][8], bv[2][8];
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
@@ -636,7 +636,7 @@ if constexpr (BF) {
 #pragma unroll
           for (int a = 0; a < 2; ++a)
 #pragma unroll
-            for (int b = 0; b < 2; ++b) acc[a][b] = mfma_k16<true>(av[a], bv[b], acc[a][b]);
+            for (int b = 0; b < 2; ++b) acc[a][b] = mfma_k16<BF>(av[a], bv[b], acc[a][b]);
         } else {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -1123,12 +1123,16 @@ hipError_t launch_wsr(const GemmJob* jobs, int njobs, hipStream_t st, uint64_t* 
     args.ngroups = ng;
     const int K = args.s[0].K;
     const int grid = std::min(items, 2 * cu_count());
-    if (math_bf16()) {
-      ProfLaunch prof_(st, "gemm_wsr_kernel<true>", fl, by);
-      hipLaunchKernelGGL(gemm_wsr_kernel<true>, dim3(grid), dim3(NT), 0, st, args, items, K);
+    const int pr = math_mode();
+    if (pr == 2) {
+      ProfLaunch prof_(st, "gemm_wsr_kernel<2>", fl, by);
+      hipLaunchKernelGGL(gemm_wsr_kernel<2>, dim3(grid), dim3(NT), 0, st, args, items, K);
+    } else if (pr == 1) {
+      ProfLaunch prof_(st, "gemm_wsr_kernel<1>", fl, by);
+      hipLaunchKernelGGL(gemm_wsr_kernel<1>, dim3(grid), dim3(NT), 0, st, args, items, K);
     } else {
-      ProfLaunch prof_(st, "gemm_wsr_kernel<false>", fl, by);
-      hipLaunchKernelGGL(gemm_wsr_kernel<false>, dim3(grid), dim3(NT), 0, st, args, items, K);
+      ProfLaunch prof_(st, "gemm_wsr_kernel<0>", fl, by);
+      hipLaunchKernelGGL(gemm_wsr_kernel<0>, dim3(grid), dim3(NT), 0, st, args, items, K);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -1255,16 +1259,18 @@ hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, 
         }
         by += 4.0 * g.M * g.N * g.nbatch;
       }
-      static const char* const kLdsName[8] = {
-          "gemm_lds_kernel<0, 0, 16, 3, false>", "gemm_lds_kernel<0, 1, 16, 3, false>",
-          "gemm_lds_kernel<1, 0, 16, 3, false>", "gemm_lds_kernel<1, 1, 16, 3, false>",
-          "gemm_lds_kernel<0, 0, 16, 3, true>",  "gemm_lds_kernel<0, 1, 16, 3, true>",
-          "gemm_lds_kernel<1, 0, 16, 3, true>",  "gemm_lds_kernel<1, 1, 16, 3, true>"};
-      const bool bf = math_bf16();
+      static const char* const kLdsName[12] = {
+          "gemm_lds_kernel<0, 0, 16, 3, 0>", "gemm_lds_kernel<0, 1, 16, 3, 0>",
+          "gemm_lds_kernel<1, 0, 16, 3, 0>", "gemm_lds_kernel<1, 1, 16, 3, 0>",
+          "gemm_lds_kernel<0, 0, 16, 3, 1>", "gemm_lds_kernel<0, 1, 16, 3, 1>",
+          "gemm_lds_kernel<1, 0, 16, 3, 1>", "gemm_lds_kernel<1, 1, 16, 3, 1>",
+          "gemm_lds_kernel<0, 0, 16, 3, 2>", "gemm_lds_kernel<0, 1, 16, 3, 2>",
+          "gemm_lds_kernel<1, 0, 16, 3, 2>", "gemm_lds_kernel<1, 1, 16, 3, 2>"};
+      const int pr = math_mode();
       static const char* const kGenName[4] = {"gemm_generic_kernel<0, 0>", "gemm_generic_kernel<0, 1>",
                                               "gemm_generic_kernel<1, 0>", "gemm_generic_kernel<1, 1>"};
       const int flavour = (amode == MODE_KR ? 2 : 0) + (bmode == MODE_KR ? 1 : 0);
-      ProfLaunch prof_(st, fast ? kLdsName[flavour + (bf ? 4 : 0)] : kGenName[flavour], fl, by);
+      ProfLaunch prof_(st, fast ? kLdsName[flavour + 4 * pr] : kGenName[flavour], fl, by);
 #define MMF_LAUNCH_CFG2(DKV, NSV, BFV)                                                              \
       if (amode == MODE_RK && bmode == MODE_RK)                                                     \
         hipLaunchKernelGGL((gemm_lds_kernel<MODE_RK, MODE_RK, DKV, NSV, BFV>), grid, dim3(NT), 0, st, args); \
@@ -1275,7 +1281,8 @@ hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, 
       else                                                                                          \
         hipLaunchKernelGGL((gemm_lds_kernel<MODE_KR, MODE_RK, DKV, NSV, BFV>), grid, dim3(NT), 0, st, args);
 #define MMF_LAUNCH_CFG(DKV, NSV)                                                                    \
-      if (bf) { MMF_LAUNCH_CFG2(DKV, NSV, true) } else { MMF_LAUNCH_CFG2(DKV, NSV, false) }
+      if (pr == 2) { MMF_LAUNCH_CFG2(DKV, NSV, 2) } else if (pr == 1) { MMF_LAUNCH_CFG2(DKV, NSV, 1) } \
+      else { MMF_LAUNCH_CFG2(DKV, NSV, 0) }
 #define MMF_LAUNCH(KERNEL)                                                                 \
       if (amode == MODE_RK && bmode == MODE_RK)                                            \
         hipLaunchKernelGGL((KERNEL<MODE_RK, MODE_RK>), grid, dim3(NT), 0, st, args);       \

@@ -137,7 +137,8 @@ void layout_ws(const mmf_hybrid_desc* d, Bump& bp, Ws& w) {
 
 int check_hybrid(const mmf_hybrid_desc* d) {
   if (!d) return fail(MMF_EINVAL, "null descriptor");
-  if (d->matmul_precision != MMF_PRECISION_HIGHEST && d->matmul_precision != MMF_PRECISION_MEDIUM)
+  if (d->matmul_precision != MMF_PRECISION_HIGHEST && d->matmul_precision != MMF_PRECISION_MEDIUM &&
+      d->matmul_precision != MMF_PRECISION_HIGH)
     return fail(MMF_EINVAL, "bad matmul_precision %d", d->matmul_precision);
   if (d->batch < 1) return fail(MMF_EINVAL, "batch must be >= 1 (got %d)", d->batch);
   if (d->num_modalities < 1 || d->num_modalities > MMF_MAX_MODALITIES)
@@ -376,7 +377,7 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
                        float* fusion_weights, float* const* attn_maps, void* stream) {
   int rc = check_hybrid(d);
   if (rc) return rc;
-  MathScope math_(d->matmul_precision == MMF_PRECISION_MEDIUM);
+  MathScope math_(d->matmul_precision);
   if (!W || !x || !mask || !saved || !logits) return fail(MMF_EINVAL, "null argument");
   hipStream_t st = (hipStream_t)stream;
   const int B = d->batch, M = d->num_modalities, H = d->hidden, C = d->num_classes;
@@ -536,7 +537,7 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
                         const mmf_hybrid_grads* G, float* const* dx, void* stream) {
   int rc = check_hybrid(d);
   if (rc) return rc;
-  MathScope math_(d->matmul_precision == MMF_PRECISION_MEDIUM);
+  MathScope math_(d->matmul_precision);
   if (!W || !x || !mask || !saved || !dlogits || !workspace || !G)
     return fail(MMF_EINVAL, "null argument");
   hipStream_t st = (hipStream_t)stream;

@@ -30,9 +30,29 @@ __device__ __forceinline__ int acc_row(int r, int half) { return (r & 3) + 8 * (
 // accumulator maps 1:1 onto one bf16 MFMA with a[j], b[j] = step j's operands.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-template <bool BF>
+//
+// "high" (PR = 2, torch.set_float32_matmul_precision("high")): torch defines it as fp32
+// matmuls on TF32 operands or with "each float32 number as the sum of two bfloat16
+// numbers"; gfx950 has no TF32, so the bf16x3 form: x = hi + lo with hi = bf16(x) (round
+// to nearest even) and lo = bf16(x - hi) (x - hi is exact in fp32), and
+// a.b = lo_a.hi_b + hi_a.lo_b + hi_a.hi_b (the lo.lo term, < 2^-16 relative, dropped),
+// smallest terms first, all three into the fp32 accumulator: 3 bf16 MFMAs (96 cycles)
+// instead of 8 fp32 ones (512 cycles) per 16 products, ~16 significant bits per operand.
+template <int PR>
 __device__ __forceinline__ f32x16 mfma_k16(const float (&a)[8], const float (&b)[8], f32x16 c) {
-  if constexpr (BF) {
+  if constexpr (PR == 2) {
+    bf16x8 ah, al, bh, bl;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ah[j] = (__bf16)a[j];
+      bh[j] = (__bf16)b[j];
+      al[j] = (__bf16)(a[j] - (float)ah[j]);
+      bl[j] = (__bf16)(b[j] - (float)bh[j]);
+    }
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, c, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, c, 0, 0, 0);
+  } else if constexpr (PR == 1) {
     bf16x8 av, bv;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {

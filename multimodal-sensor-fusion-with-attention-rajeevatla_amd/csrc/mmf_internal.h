@@ -40,14 +40,17 @@ struct ProfLaunch {
 // ---------------------------------------------------------------------------
 // Matmul precision of the current C-ABI call (torch.get_float32_matmul_precision
 // at the caller): 0 = "highest" (fp32 MFMA), 1 = "medium" (bf16 MFMA operands,
-// fp32 accumulate).  Set for the duration of one entry point by MathScope; the
-// launchers pick the kernel instantiation from it (a graph captures that choice).
+// fp32 accumulate), 2 = "high" (bf16x3: split bf16 operands, three MFMAs).  Set for
+// the duration of one entry point by MathScope; the launchers pick the kernel
+// instantiation (its int precision template argument) from it (a graph captures
+// that choice).
 // ---------------------------------------------------------------------------
 extern thread_local int g_math_bf16;
+inline int math_mode() { return g_math_bf16; }
 inline bool math_bf16() { return g_math_bf16 != 0; }
 struct MathScope {
   int prev;
-  explicit MathScope(int bf16) : prev(g_math_bf16) { g_math_bf16 = bf16 ? 1 : 0; }
+  explicit MathScope(int mode) : prev(g_math_bf16) { g_math_bf16 = (mode >= 0 && mode <= 2) ? mode : 0; }
   ~MathScope() { g_math_bf16 = prev; }
   MathScope(const MathScope&) = delete;
   MathScope& operator=(const MathScope&) = delete;

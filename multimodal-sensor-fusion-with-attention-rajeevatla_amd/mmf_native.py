@@ -19,18 +19,23 @@ MAX_PAIRS = MAX_MODALITIES * (MAX_MODALITIES - 1)
 MAX_HEAD_DIM = 64
 PRECISION_HIGHEST = 0   # MMF_PRECISION_HIGHEST: fp32 MFMA
 PRECISION_MEDIUM = 1    # MMF_PRECISION_MEDIUM: bf16 MFMA operands, fp32 accumulate
+PRECISION_HIGH = 2      # MMF_PRECISION_HIGH: bf16x3 (operands split into bf16 hi + lo), fp32 accumulate
 
 
 def matmul_precision() -> int:
     """The caller's torch.get_float32_matmul_precision() as the C-ABI enum.
 
     The reference sets it from ``training.matmul_precision`` (config/base.yaml:80,
-    "medium") through ``_configure_matmul_precision`` (src/train.py:53-68,448).
-    "medium" lets fp32 matmuls use bf16 operands with fp32 accumulation; "high"
-    asks for TF32, which gfx950 does not have, so it runs like "highest" (fp32),
-    as PyTorch does on hardware without TF32.
+    "medium") through ``_configure_matmul_precision`` (src/train.py:53-68,448);
+    the reference's own tests set "high" (tests/test_train.py:45).  "medium" lets
+    fp32 matmuls use bf16 operands with fp32 accumulation.  "high" lets them use
+    TF32 or treat "each float32 number as the sum of two bfloat16 numbers"
+    (torch.set_float32_matmul_precision); gfx950 has no TF32, so "high" runs the
+    bf16x3 form: every MFMA operand split into bf16 hi + lo, three bf16 MFMAs
+    (lo*hi + hi*lo + hi*hi) into the fp32 accumulator (csrc/mmf_device.h mfma_k16).
     """
-    return PRECISION_MEDIUM if torch.get_float32_matmul_precision() == "medium" else PRECISION_HIGHEST
+    mode = torch.get_float32_matmul_precision()
+    return {"medium": PRECISION_MEDIUM, "high": PRECISION_HIGH}.get(mode, PRECISION_HIGHEST)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # MMF_LIB_PATH selects another in-tree build (e.g. csrc/libmmfusion_stamps.so, the

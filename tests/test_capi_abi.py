@@ -45,11 +45,11 @@ def test_struct_layouts_match_header(nat, tmp_path):
 #include <stddef.h>
 #include "{HEADER}"
 int main(void) {{
-  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %d\\n", sizeof(mmf_hybrid_desc), sizeof(mmf_hybrid_params),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %d %d\\n", sizeof(mmf_hybrid_desc), sizeof(mmf_hybrid_params),
          sizeof(mmf_hybrid_grads), sizeof(mmf_cma_desc), sizeof(mmf_cma_params),
          offsetof(mmf_hybrid_desc, dropout), offsetof(mmf_hybrid_params, cls2),
          offsetof(mmf_hybrid_desc, matmul_precision), offsetof(mmf_cma_desc, matmul_precision),
-         (int)MMF_PRECISION_MEDIUM);
+         (int)MMF_PRECISION_MEDIUM, (int)MMF_PRECISION_HIGH);
   return 0;
 }}
 """)
@@ -60,7 +60,8 @@ int main(void) {{
     py = [ctypes.sizeof(nat.HybridDesc), ctypes.sizeof(nat.HybridParams),
           ctypes.sizeof(nat.HybridGrads), ctypes.sizeof(nat.CmaDesc), ctypes.sizeof(nat.CmaParams),
           nat.HybridDesc.dropout.offset, nat.HybridParams.cls2.offset,
-          nat.HybridDesc.matmul_precision.offset, nat.CmaDesc.matmul_precision.offset, nat.PRECISION_MEDIUM]
+          nat.HybridDesc.matmul_precision.offset, nat.CmaDesc.matmul_precision.offset, nat.PRECISION_MEDIUM,
+          nat.PRECISION_HIGH]
     assert out == py
 
 
@@ -94,7 +95,7 @@ def test_size_queries_and_validation(nat):
     # forward refuses a bad descriptor before touching the device
     rc = L.mmf_hybrid_forward(ctypes.byref(bad), None, None, None, None, None, None, None, None, None)
     assert rc != 0
-    odd = _desc(nat, matmul_precision=7)     # neither HIGHEST nor MEDIUM
+    odd = _desc(nat, matmul_precision=7)     # none of HIGHEST, MEDIUM, HIGH
     assert L.mmf_hybrid_saved_bytes(ctypes.byref(odd)) == 0
     assert b"matmul_precision" in L.mmf_last_error()
     assert L.mmf_hybrid_saved_bytes(ctypes.byref(_desc(nat, matmul_precision=nat.PRECISION_MEDIUM))) > 0
@@ -125,7 +126,7 @@ def test_matmul_precision_follows_torch(nat):
     import torch
     prev = torch.get_float32_matmul_precision()
     try:
-        for mode, want in (("highest", nat.PRECISION_HIGHEST), ("high", nat.PRECISION_HIGHEST),
+        for mode, want in (("highest", nat.PRECISION_HIGHEST), ("high", nat.PRECISION_HIGH),
                            ("medium", nat.PRECISION_MEDIUM)):
             torch.set_float32_matmul_precision(mode)
             assert nat.matmul_precision() == want, mode

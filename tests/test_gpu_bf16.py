@@ -26,8 +26,8 @@ seeded inputs):
     flash-style D = rowsum(dO * O) and the bf16 dP = dO V^T differ by
     rounding, as in any reduced-precision attention backward), and the gating
     bias grads (a sum over the batch of per-sample terms of both signs).
-Each test also checks that the bf16 instantiations ran (profiler kernel names
-end in ", true>") and that the result differs from the fp32 path.
+Each test also checks that the bf16 instantiations ran (the precision argument of
+the profiler kernel names is 1) and that the result differs from the fp32 path.
 """
 import re
 
@@ -86,8 +86,14 @@ def group_scale(refs):
     return max(float(_t(r).norm()) for r in refs)
 
 
+def _precision(kname):
+    """The int precision argument of a library MFMA kernel name (bench.kernel_precision)."""
+    m = re.search(r"[<, ]([012])(?:, (?:true|false))?>$", kname)
+    return int(m.group(1)) if m else None
+
+
 def _is_bf16(kname):
-    return re.search(r"[<, ]true>$", kname) is not None
+    return _precision(kname) == 1
 
 
 def _bf16_kernels_ran(nat, launches):
@@ -166,7 +172,7 @@ def test_bf16_differs_from_fp32(mods):
         _, _, l32, _ = run_hybrid(fusion, case)
         _, launches = nat.profile_end()
         mfma = [k for _, k, *_ in launches if k.startswith(("gemm_lds", "gemm_wsr", "attn_"))]
-        assert mfma and not any(_is_bf16(k) for k in mfma), mfma
+        assert mfma and not any(_precision(k) in (1, 2) for k in mfma), mfma
         torch.set_float32_matmul_precision("medium")
         _, _, l16, _ = run_hybrid(fusion, case)
     finally:
