@@ -219,8 +219,11 @@ C5_MINI = HybridCase("c5_mini", [f"m{i}" for i in range(6)], {f"m{i}": 256 for i
                      seed=51, mask=[[1, 1, 0, 1, 1, 1], [1, 0, 1, 1, 1, 0]], full=True)
 
 
-@pytest.mark.parametrize("precision", ["highest", "medium"])
+@pytest.mark.parametrize("precision", ["highest", "high", "medium"])
 def test_c5_shape_vs_oracle(mods, precision):
+    """fp32 tolerance at "highest" and "high" (bf16x3; plus a 1e-4 S floor for the
+    near-zero gradients whose cancelling terms carry the split-operand rounding), the
+    bf16 bounds at "medium"."""
     fusion, _, nat = mods
     out, grads, dx = oracle_hybrid(C5_MINI)
     if precision == "medium":
@@ -231,24 +234,26 @@ def test_c5_shape_vs_oracle(mods, precision):
         model, feats, logits, info = run_hybrid(fusion, C5_MINI)
     finally:
         torch.set_float32_matmul_precision(prev)
-    if precision == "highest":
+    fp32 = precision in ("highest", "high")
+    if fp32:
         err = float((_t(logits) - _t(out["logits"])).abs().max() / _t(out["logits"]).abs().max())
         assert err <= 1e-3, err
     else:
         ok, e = logits_ok(logits.cpu(), out["logits"])
         assert ok, e
     S = group_scale([dx[m] for m in C5_MINI.names] + list(grads.values()))
+    floor = 1e-6 if precision == "highest" else 1e-4 * S
     for m in C5_MINI.names:
-        if precision == "highest":
+        if fp32:
             d = _t(feats[m].grad) - _t(dx[m])
-            assert float(d.norm()) <= 1e-3 * float(_t(dx[m]).norm()) + 1e-6, m
+            assert float(d.norm()) <= 1e-3 * float(_t(dx[m]).norm()) + floor, m
         else:
             ok, e = norm_ok(feats[m].grad, dx[m], edx[m], S)
             assert ok, (m, e)
     for name, p in model.named_parameters():
-        if precision == "highest":
+        if fp32:
             d = _t(p.grad) - _t(grads[name])
-            assert float(d.norm()) <= 1e-3 * float(_t(grads[name]).norm()) + 1e-6, name
+            assert float(d.norm()) <= 1e-3 * float(_t(grads[name]).norm()) + floor, name
         else:
             ok, e = norm_ok(p.grad, grads[name], egrads[name], S)
             assert ok, (name, e)
