@@ -841,8 +841,11 @@ MMF_CHAIN16(dq[dt], Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], ds[r])
 }
 
 // Pooled backward, key on the lane: dK = scale * dS^T Q (needs D from the dq kernel).
+// bf16x3 at hd 64 (here and in attn_poolL_dq_kernel) runs at 3 waves / SIMD: at 4 its
+// split operands spill 73-84 VGPRs (C5 "high": dK 2404 -> 1778 us, dQ 3126 -> 2657 us);
+// bf16 keeps 4 (3 cost its dQ 2199 -> 2478 us).
 template <int HDP, int BF>
-__global__ __launch_bounds__(NT, 4) void attn_pool_bwd_dk_kernel(const AttnArgs A) {
+__global__ __launch_bounds__(NT, (BF == 2 && HDP == 64) ? 3 : 4) void attn_pool_bwd_dk_kernel(const AttnArgs A) {
   constexpr int QC = 128;
   constexpr int LS = HDP + 4;
   constexpr int HALF = HDP / 2;
@@ -1114,7 +1117,7 @@ __global__ __launch_bounds__(NT) void attn_poolL_colsum_kernel(const AttnArgs A)
 }
 
 template <int HDP, int BF, bool LEAN = false>   // LEAN: as attn_poolL_lse_kernel
-__global__ __launch_bounds__(NT, 4) void attn_poolL_dq_kernel(const AttnArgs A) {
+__global__ __launch_bounds__(NT, (BF == 2 && HDP == 64) ? 3 : 4) void attn_poolL_dq_kernel(const AttnArgs A) {
   constexpr int KC = 128;   // keys per LDS chunk (34 KB at HDP = 64: 4 workgroups / CU)
   constexpr int LS = HDP + 4;
   constexpr int HALF = HDP / 2;
