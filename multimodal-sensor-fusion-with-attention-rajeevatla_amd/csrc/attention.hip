@@ -2028,6 +2028,7 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
     const char* kname = kNames[(int)kind][(alt ? 2 : 0) + (small ? 0 : 1)];
     const char* pname = with_arg(kname, pr == 2 ? "2" : (pr == 1 ? "1" : "0"));
     if (long_lean) pname = with_arg(pname, "true");   // "<hd, pr, true>": the LEAN instantiation
+    if (kind == Kind::PoolFwd && lean) pname = with_arg(pname, a.drop_p > 0.f ? "true" : "false");   // DROP
     ProfLaunch prof_(st, pname, fl, by);
     switch (kind) {
       case Kind::PoolLse:
