@@ -104,7 +104,7 @@ void prof_launch_end(void* tok, hipStream_t st, const char* kernel, double flops
   g_prof.launches.push_back({g_prof.cur_stage, kernel, flops, bytes, (hipEvent_t)tok, b});
 }
 
-thread_local int g_math_bf16 = 0;
+thread_local int g_math_mode = 0;
 
 }  // namespace mmf
 

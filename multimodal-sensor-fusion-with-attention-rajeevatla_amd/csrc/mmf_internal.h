@@ -45,13 +45,12 @@ struct ProfLaunch {
 // instantiation (its int precision template argument) from it (a graph captures
 // that choice).
 // ---------------------------------------------------------------------------
-extern thread_local int g_math_bf16;
-inline int math_mode() { return g_math_bf16; }
-inline bool math_bf16() { return g_math_bf16 != 0; }
+extern thread_local int g_math_mode;
+inline int math_mode() { return g_math_mode; }
 struct MathScope {
   int prev;
-  explicit MathScope(int mode) : prev(g_math_bf16) { g_math_bf16 = (mode >= 0 && mode <= 2) ? mode : 0; }
-  ~MathScope() { g_math_bf16 = prev; }
+  explicit MathScope(int mode) : prev(g_math_mode) { g_math_mode = (mode >= 0 && mode <= 2) ? mode : 0; }
+  ~MathScope() { g_math_mode = prev; }
   MathScope(const MathScope&) = delete;
   MathScope& operator=(const MathScope&) = delete;
 };
