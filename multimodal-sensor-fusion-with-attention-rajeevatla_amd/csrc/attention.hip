@@ -2021,9 +2021,9 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
 // int precision template argument inside KERNEL
 #define MMF_PR_LAUNCH(...)                                                                   \
   switch (pr) {                                                                              \
-    case 2: { constexpr int PRV = 2; hipLaunchKernelGGL((__VA_ARGS__), grid, dim3(NT), 0, st, a); } break; \
-    case 1: { constexpr int PRV = 1; hipLaunchKernelGGL((__VA_ARGS__), grid, dim3(NT), 0, st, a); } break; \
-    default: { constexpr int PRV = 0; hipLaunchKernelGGL((__VA_ARGS__), grid, dim3(NT), 0, st, a); } break; \
+    case 2: { constexpr int PRV = 2; mmf_launch((__VA_ARGS__), grid, dim3(NT), 0, st, a); } break; \
+    case 1: { constexpr int PRV = 1; mmf_launch((__VA_ARGS__), grid, dim3(NT), 0, st, a); } break; \
+    default: { constexpr int PRV = 0; mmf_launch((__VA_ARGS__), grid, dim3(NT), 0, st, a); } break; \
   }
     const char* kname = kNames[(int)kind][(alt ? 2 : 0) + (small ? 0 : 1)];
     const char* pname = with_arg(kname, pr == 2 ? "2" : (pr == 1 ? "1" : "0"));
@@ -2062,8 +2062,8 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
         else { MMF_PR_LAUNCH(attn_fwd_kernel<64, 1, PRV>) }
         break;
       case Kind::Prep:
-        if (prep_vec) hipLaunchKernelGGL(attn_bwd_prep_vec_kernel, grid, dim3(NT), 0, st, a);
-        else hipLaunchKernelGGL(attn_bwd_prep_kernel, grid, dim3(NT), 0, st, a);
+        if (prep_vec) mmf_launch(attn_bwd_prep_vec_kernel, grid, dim3(NT), 0, st, a);
+        else mmf_launch(attn_bwd_prep_kernel, grid, dim3(NT), 0, st, a);
         break;
       case Kind::Dkv:
         if (small) { MMF_PR_LAUNCH(attn_bwd_dkv_kernel<32, PRV>) }

@@ -90,18 +90,27 @@ AttnPair cma_pair(const mmf_cma_desc* d, const CmaSaved& s, const float* mask) {
 
 namespace mmf {
 
-void* prof_launch_begin(hipStream_t st) {
-  if (!g_prof.on) return nullptr;
-  hipEvent_t a = g_prof.ev();
-  if (!a || hipEventRecord(a, st) != hipSuccess) return nullptr;
-  return (void*)a;
+thread_local ProfArm* g_prof_arm = nullptr;
+
+bool prof_arm_begin(ProfArm& arm) {
+  if (!g_prof.on) return false;
+  arm.a = g_prof.ev();
+  arm.b = g_prof.ev();
+  arm.launches = 0;
+  if (!arm.a || !arm.b) return false;
+  g_prof_arm = &arm;
+  return true;
 }
 
-void prof_launch_end(void* tok, hipStream_t st, const char* kernel, double flops, double bytes) {
-  if (!tok || !g_prof.on) return;
-  hipEvent_t b = g_prof.ev();
-  if (!b || hipEventRecord(b, st) != hipSuccess) return;
-  g_prof.launches.push_back({g_prof.cur_stage, kernel, flops, bytes, (hipEvent_t)tok, b});
+void prof_arm_end(ProfArm& arm, hipStream_t st, const char* kernel, double flops, double bytes) {
+  if (g_prof_arm == &arm) g_prof_arm = nullptr;
+  if (!g_prof.on || arm.launches == 0) return;
+  hipEvent_t end = arm.b;
+  if (arm.launches > 1) {   // several launches: the scope ends after the last one
+    end = g_prof.ev();
+    if (!end || hipEventRecord(end, st) != hipSuccess) return;
+  }
+  g_prof.launches.push_back({g_prof.cur_stage, kernel, flops, bytes, arm.a, end});
 }
 
 thread_local int g_math_mode = 0;

@@ -90,7 +90,7 @@ int mmf_gather_chunks(const float* table, int64_t rows, int32_t ncols, const int
   hipStream_t st = (hipStream_t)stream;
   const int64_t n = (int64_t)batch * T;
   ProfLaunch prof_(st, "gather_chunks_kernel", 0.0, 8.0 * n * total);
-  hipLaunchKernelGGL(gather_chunks_kernel, dim3((unsigned)((n + NT - 1) / NT)), dim3(NT), 0, st, a);
+  mmf_launch(gather_chunks_kernel, dim3((unsigned)((n + NT - 1) / NT)), dim3(NT), 0, st, a);
   HIP_TRY(hipGetLastError());
   return MMF_OK;
 }

@@ -1126,13 +1126,13 @@ hipError_t launch_wsr(const GemmJob* jobs, int njobs, hipStream_t st, uint64_t* 
     const int pr = math_mode();
     if (pr == 2) {
       ProfLaunch prof_(st, "gemm_wsr_kernel<2>", fl, by);
-      hipLaunchKernelGGL(gemm_wsr_kernel<2>, dim3(grid), dim3(NT), 0, st, args, items, K);
+      mmf_launch(gemm_wsr_kernel<2>, dim3(grid), dim3(NT), 0, st, args, items, K);
     } else if (pr == 1) {
       ProfLaunch prof_(st, "gemm_wsr_kernel<1>", fl, by);
-      hipLaunchKernelGGL(gemm_wsr_kernel<1>, dim3(grid), dim3(NT), 0, st, args, items, K);
+      mmf_launch(gemm_wsr_kernel<1>, dim3(grid), dim3(NT), 0, st, args, items, K);
     } else {
       ProfLaunch prof_(st, "gemm_wsr_kernel<0>", fl, by);
-      hipLaunchKernelGGL(gemm_wsr_kernel<0>, dim3(grid), dim3(NT), 0, st, args, items, K);
+      mmf_launch(gemm_wsr_kernel<0>, dim3(grid), dim3(NT), 0, st, args, items, K);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -1171,7 +1171,7 @@ hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, 
       if (sa.ngroups == 0) return hipSuccess;
       sa.off[sa.ngroups] = total;
       ProfLaunch prof_(st, "small_slab_kernel", fl, by);
-      hipLaunchKernelGGL(small_slab_kernel, dim3((8 * total + 255) / 256), dim3(256), 0, st, sa);
+      mmf_launch(small_slab_kernel, dim3((8 * total + 255) / 256), dim3(256), 0, st, sa);
       memset(&sa, 0, sizeof(sa));
       total = 0; fl = by = 0.0;
       return hipGetLastError();
@@ -1273,25 +1273,25 @@ hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, 
       ProfLaunch prof_(st, fast ? kLdsName[flavour + 4 * pr] : kGenName[flavour], fl, by);
 #define MMF_LAUNCH_CFG2(DKV, NSV, BFV)                                                              \
       if (amode == MODE_RK && bmode == MODE_RK)                                                     \
-        hipLaunchKernelGGL((gemm_lds_kernel<MODE_RK, MODE_RK, DKV, NSV, BFV>), grid, dim3(NT), 0, st, args); \
+        mmf_launch((gemm_lds_kernel<MODE_RK, MODE_RK, DKV, NSV, BFV>), grid, dim3(NT), 0, st, args); \
       else if (amode == MODE_RK && bmode == MODE_KR)                                                \
-        hipLaunchKernelGGL((gemm_lds_kernel<MODE_RK, MODE_KR, DKV, NSV, BFV>), grid, dim3(NT), 0, st, args); \
+        mmf_launch((gemm_lds_kernel<MODE_RK, MODE_KR, DKV, NSV, BFV>), grid, dim3(NT), 0, st, args); \
       else if (amode == MODE_KR && bmode == MODE_KR)                                                \
-        hipLaunchKernelGGL((gemm_lds_kernel<MODE_KR, MODE_KR, DKV, NSV, BFV>), grid, dim3(NT), 0, st, args); \
+        mmf_launch((gemm_lds_kernel<MODE_KR, MODE_KR, DKV, NSV, BFV>), grid, dim3(NT), 0, st, args); \
       else                                                                                          \
-        hipLaunchKernelGGL((gemm_lds_kernel<MODE_KR, MODE_RK, DKV, NSV, BFV>), grid, dim3(NT), 0, st, args);
+        mmf_launch((gemm_lds_kernel<MODE_KR, MODE_RK, DKV, NSV, BFV>), grid, dim3(NT), 0, st, args);
 #define MMF_LAUNCH_CFG(DKV, NSV)                                                                    \
       if (pr == 2) { MMF_LAUNCH_CFG2(DKV, NSV, 2) } else if (pr == 1) { MMF_LAUNCH_CFG2(DKV, NSV, 1) } \
       else { MMF_LAUNCH_CFG2(DKV, NSV, 0) }
 #define MMF_LAUNCH(KERNEL)                                                                 \
       if (amode == MODE_RK && bmode == MODE_RK)                                            \
-        hipLaunchKernelGGL((KERNEL<MODE_RK, MODE_RK>), grid, dim3(NT), 0, st, args);       \
+        mmf_launch((KERNEL<MODE_RK, MODE_RK>), grid, dim3(NT), 0, st, args);       \
       else if (amode == MODE_RK && bmode == MODE_KR)                                       \
-        hipLaunchKernelGGL((KERNEL<MODE_RK, MODE_KR>), grid, dim3(NT), 0, st, args);       \
+        mmf_launch((KERNEL<MODE_RK, MODE_KR>), grid, dim3(NT), 0, st, args);       \
       else if (amode == MODE_KR && bmode == MODE_KR)                                       \
-        hipLaunchKernelGGL((KERNEL<MODE_KR, MODE_KR>), grid, dim3(NT), 0, st, args);       \
+        mmf_launch((KERNEL<MODE_KR, MODE_KR>), grid, dim3(NT), 0, st, args);       \
       else                                                                                 \
-        hipLaunchKernelGGL((KERNEL<MODE_KR, MODE_RK>), grid, dim3(NT), 0, st, args);
+        mmf_launch((KERNEL<MODE_KR, MODE_RK>), grid, dim3(NT), 0, st, args);
       if (fast) {
         // (DK, ring depth) = (16, 3): measured best of (16|32) x (2|3|4) at C2
         // (profiles/tune_gemm_cfg.sh)
@@ -1339,7 +1339,7 @@ hipError_t launch_reduce(const ReduceJob* jobs, int njobs, hipStream_t st) {
       by += 4.0 * r.nbatch * ((double)r.nsplit + 1) * r.M * ((double)r.N + (r.part_db ? 1 : 0));
     }
     ProfLaunch prof_(st, "partial_reduce_kernel", 0.0, by);
-    hipLaunchKernelGGL(partial_reduce_kernel, dim3(blocks, n, maxbatch), dim3(256), 0, st, a);
+    mmf_launch(partial_reduce_kernel, dim3(blocks, n, maxbatch), dim3(256), 0, st, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
@@ -1358,7 +1358,7 @@ hipError_t launch_mask_dropout(MaskDropArgs a, hipStream_t st) {
   double by = 0.0;
   for (int m = 0; m < a.n; ++m) by += 8.0 * a.j[m].rows * a.j[m].D;   // read x, write x'
   ProfLaunch prof_(st, "mask_dropout_rows_kernel", 0.0, by);
-  hipLaunchKernelGGL(mask_dropout_rows_kernel, dim3(grid, a.n), dim3(256), 0, st, a);
+  mmf_launch(mask_dropout_rows_kernel, dim3(grid, a.n), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

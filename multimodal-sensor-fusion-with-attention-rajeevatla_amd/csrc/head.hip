@@ -412,14 +412,14 @@ __global__ void step_incr_kernel(int64_t* step) {
 hipError_t launch_head_fwd(const HeadArgs& a, hipStream_t st) {
   if (a.H % 4 != 0 || a.H > HEAD_MAX_H || a.H < 4 || a.M > 8) return hipErrorInvalidValue;
   ProfLaunch prof_(st, "head_fwd_kernel", 0.0, 0.0);
-  hipLaunchKernelGGL(head_fwd_kernel, dim3(a.B), dim3(NT), 0, st, a);
+  mmf_launch(head_fwd_kernel, dim3(a.B), dim3(NT), 0, st, a);
   return hipGetLastError();
 }
 
 hipError_t launch_head_bwd(const HeadArgs& a, hipStream_t st) {
   if (a.M > 8) return hipErrorInvalidValue;
   ProfLaunch prof_(st, "head_bwd_kernel", 0.0, 0.0);
-  hipLaunchKernelGGL(head_bwd_kernel, dim3(a.B), dim3(NT), 0, st, a);
+  mmf_launch(head_bwd_kernel, dim3(a.B), dim3(NT), 0, st, a);
   return hipGetLastError();
 }
 
@@ -431,19 +431,19 @@ hipError_t launch_gate_wgrad(int B, int M, int H, const float* dscore, const flo
   for (int m = 0; m < M; ++m) { a.dgw[m] = dgw[m]; a.dgb[m] = dgb[m]; }
   const int n = M * (H + 1);
   ProfLaunch prof_(st, "gate_wgrad_kernel", 2.0 * B * M * H, 4.0 * B * M * (H + 1));
-  hipLaunchKernelGGL(gate_wgrad_kernel, dim3((n + NT - 1) / NT), dim3(NT), 0, st, a);
+  mmf_launch(gate_wgrad_kernel, dim3((n + NT - 1) / NT), dim3(NT), 0, st, a);
   return hipGetLastError();
 }
 
 hipError_t launch_rng_snapshot(const uint64_t* state, RngSnap* snap, hipStream_t st) {
   ProfLaunch prof_(st, "rng_snapshot_kernel", 0.0, 32.0);
-  hipLaunchKernelGGL(rng_snapshot_kernel, dim3(1), dim3(64), 0, st, const_cast<uint64_t*>(state), snap);
+  mmf_launch(rng_snapshot_kernel, dim3(1), dim3(64), 0, st, const_cast<uint64_t*>(state), snap);
   return hipGetLastError();
 }
 
 hipError_t launch_rng_advance(uint64_t* state, hipStream_t st) {
   ProfLaunch prof_(st, "rng_advance_kernel", 0.0, 16.0);
-  hipLaunchKernelGGL(rng_advance_kernel, dim3(1), dim3(64), 0, st, state);
+  mmf_launch(rng_advance_kernel, dim3(1), dim3(64), 0, st, state);
   return hipGetLastError();
 }
 
@@ -451,7 +451,7 @@ hipError_t launch_cross_entropy(int B, int C, const float* logits, const int64_t
                                 float smoothing, float grad_scale, float* loss, float* dlogits,
                                 hipStream_t st) {
   ProfLaunch prof_(st, "cross_entropy_kernel", 0.0, 8.0 * B * C + 8.0 * B);
-  hipLaunchKernelGGL(cross_entropy_kernel, dim3(1), dim3(NT), 0, st, B, C, logits, labels, smoothing,
+  mmf_launch(cross_entropy_kernel, dim3(1), dim3(NT), 0, st, B, C, logits, labels, smoothing,
                      grad_scale, loss, dlogits);
   return hipGetLastError();
 }
@@ -462,12 +462,12 @@ hipError_t launch_grad_clip_coef(int64_t n, const float* g, float gscale, float 
                                  float* coef_out, float* partial, hipStream_t st) {
   {
     ProfLaunch prof_(st, "grad_sumsq_kernel", 2.0 * n, 4.0 * n);
-    hipLaunchKernelGGL(grad_sumsq_kernel, dim3(CLIP_BLOCKS), dim3(NT), 0, st, n, g, partial, (int64_t*)nullptr);
+    mmf_launch(grad_sumsq_kernel, dim3(CLIP_BLOCKS), dim3(NT), 0, st, n, g, partial, (int64_t*)nullptr);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   ProfLaunch prof_(st, "clip_coef_kernel", 0.0, 4.0 * CLIP_BLOCKS);
-  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(NT), 0, st, (const float*)partial, gscale, max_norm, norm_out,
+  mmf_launch(clip_coef_kernel, dim3(1), dim3(NT), 0, st, (const float*)partial, gscale, max_norm, norm_out,
                      coef_out);
   return hipGetLastError();
 }
@@ -491,11 +491,11 @@ hipError_t launch_adamw(int64_t n, float* p, const float* g, float* m, float* v,
   const int vec = adamw_vec(p, g, m, v);
   const int64_t blocks = adamw_blocks(n, vec);
   ProfLaunch prof_(st, "adamw_kernel", 0.0, 28.0 * n);   // p m v read+write, g read
-  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(NT), 0, st, n, p, g, m, v, step, lr, b1,
+  mmf_launch(adamw_kernel, dim3((unsigned)blocks), dim3(NT), 0, st, n, p, g, m, v, step, lr, b1,
                      b2, eps, wd, gscale, lr_dev, coef_dev, vec);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(step_incr_kernel, dim3(1), dim3(64), 0, st, step);
+  mmf_launch(step_incr_kernel, dim3(1), dim3(64), 0, st, step);
   return hipGetLastError();
 }
 
@@ -504,14 +504,14 @@ hipError_t launch_clip_adamw(int64_t n, float* p, const float* g, float* m, floa
                              float max_norm, float* norm_out, float* coef_out, float* partial, hipStream_t st) {
   {
     ProfLaunch prof_(st, "grad_sumsq_kernel", 2.0 * n, 4.0 * n);
-    hipLaunchKernelGGL(grad_sumsq_kernel, dim3(CLIP_BLOCKS), dim3(NT), 0, st, n, g, partial, step);
+    mmf_launch(grad_sumsq_kernel, dim3(CLIP_BLOCKS), dim3(NT), 0, st, n, g, partial, step);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int vec = adamw_vec(p, g, m, v);
   const int64_t blocks = adamw_blocks(n, vec);
   ProfLaunch prof_(st, "clip_adamw_kernel", 0.0, 28.0 * n);
-  hipLaunchKernelGGL(clip_adamw_kernel, dim3((unsigned)blocks), dim3(NT), 0, st, n, p, g, m, v, (const int64_t*)step,
+  mmf_launch(clip_adamw_kernel, dim3((unsigned)blocks), dim3(NT), 0, st, n, p, g, m, v, (const int64_t*)step,
                      lr_dev, b1, b2, eps, wd, gscale, (const float*)partial, max_norm, norm_out, coef_out, vec);
   return hipGetLastError();
 }

@@ -440,7 +440,7 @@ int mmf_lstm_forward(int32_t num_lstm, int32_t batch, int32_t steps, int32_t hid
   HIP_TRY(hipMemsetAsync(timeout, 0, sizeof(uint32_t), st));   // per call: a stale flag never aborts waits
   ProfLaunch prof_(st, "lstm_fwd_kernel", 8.0 * num_lstm * batch * steps * hidden * hidden,
                    4.0 * num_lstm * ((double)4 * hidden * hidden + (double)batch * steps * 10 * hidden));
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(LNT), 0, st, a);
+  mmf_launch(kern, dim3(grid), dim3(LNT), 0, st, a);
   HIP_TRY(hipGetLastError());
   return MMF_OK;
 }
@@ -463,7 +463,7 @@ int mmf_lstm_backward(int32_t num_lstm, int32_t batch, int32_t steps, int32_t hi
   HIP_TRY(hipMemsetAsync(timeout, 0, sizeof(uint32_t), st));
   ProfLaunch prof_(st, "lstm_bwd_kernel", 8.0 * num_lstm * batch * steps * hidden * hidden,
                    4.0 * num_lstm * ((double)4 * hidden * hidden + (double)batch * steps * 14 * hidden));
-  hipLaunchKernelGGL(lstm_bwd_kernel, dim3(a.G * a.ninst), dim3(LNT), 0, st, a);
+  mmf_launch(lstm_bwd_kernel, dim3(a.G * a.ninst), dim3(LNT), 0, st, a);
   HIP_TRY(hipGetLastError());
   return MMF_OK;
 }

@@ -2,6 +2,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <stddef.h>
 
@@ -16,26 +17,49 @@ struct RngSnap { uint64_t seed; uint64_t offset; };
 
 // ---------------------------------------------------------------------------
 // Per-launch profiling (capi.hip).  While mmf_profile_begin() is active, every
-// kernel launch of the library is bracketed by two hipEvents on its stream and
-// tagged with the kernel's name (as rocprofv3 prints it, minus the namespace)
-// and its ALGORITHMIC work: FLOPs of the math it implements (no recompute) and
-// the bytes a perfect-reuse kernel would move to/from HBM.  Inactive, a launch
-// pays one branch.  `kernel` must point to static storage.
+// kernel launch of the library is timed by two hipEvents and tagged with the
+// kernel's name (as rocprofv3 prints it, minus the namespace) and its
+// ALGORITHMIC work: FLOPs of the math it implements (no recompute) and the bytes
+// a perfect-reuse kernel would move to/from HBM.  The events ride in the first
+// launch's own dispatch packet (hipExtLaunchKernel start / stop events: the
+// kernel's start and end, as rocprofv3 sees them); a scope with several launches
+// ends at an event recorded after the last.  Inactive, a launch pays one branch.
+// `kernel` must point to static storage.
 // ---------------------------------------------------------------------------
-void* prof_launch_begin(hipStream_t st);
-void prof_launch_end(void* tok, hipStream_t st, const char* kernel, double flops, double bytes);
+struct ProfArm {
+  hipEvent_t a = nullptr, b = nullptr;
+  int launches = 0;
+};
+extern thread_local ProfArm* g_prof_arm;
+bool prof_arm_begin(ProfArm& arm);   // false when profiling is off
+void prof_arm_end(ProfArm& arm, hipStream_t st, const char* kernel, double flops, double bytes);
 struct ProfLaunch {
   hipStream_t st;
   const char* kernel;
   double flops, bytes;
-  void* tok;
+  ProfArm arm;
+  bool armed;
   ProfLaunch(hipStream_t s, const char* k, double f, double b) : st(s), kernel(k), flops(f), bytes(b) {
-    tok = prof_launch_begin(s);
+    armed = prof_arm_begin(arm);
   }
-  ~ProfLaunch() { prof_launch_end(tok, st, kernel, flops, bytes); }
+  ~ProfLaunch() {
+    if (armed) prof_arm_end(arm, st, kernel, flops, bytes);
+  }
   ProfLaunch(const ProfLaunch&) = delete;
   ProfLaunch& operator=(const ProfLaunch&) = delete;
 };
+
+// Every kernel launch of the library: hipLaunchKernelGGL, or while a ProfLaunch
+// scope is armed, its first launch carries the scope's start / stop events.
+template <typename F, typename... Args>
+inline void mmf_launch(F kernel, const dim3& grid, const dim3& block, uint32_t shmem, hipStream_t st,
+                       Args... args) {
+  ProfArm* arm = g_prof_arm;
+  if (arm && arm->launches++ == 0)
+    hipExtLaunchKernelGGL(kernel, grid, block, shmem, st, arm->a, arm->b, 0u, args...);
+  else
+    hipLaunchKernelGGL(kernel, grid, block, shmem, st, args...);
+}
 
 // ---------------------------------------------------------------------------
 // Matmul precision of the current C-ABI call (torch.get_float32_matmul_precision

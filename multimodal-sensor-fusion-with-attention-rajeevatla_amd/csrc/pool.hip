@@ -175,10 +175,10 @@ hipError_t launch_pool(bool fwd, const PoolPair* pairs, int npairs, int B, int h
     }
     ProfLaunch prof_(st, fwd ? "pool_u_kernel" : "pool_dpbar_kernel", fl, by);
     if (fwd) {
-      hipLaunchKernelGGL(pool_u_kernel, dim3(B, n), dim3(NT), 0, st, a);
+      mmf_launch(pool_u_kernel, dim3(B, n), dim3(NT), 0, st, a);
     } else {
       const size_t shm = (size_t)heads * H * sizeof(float);
-      hipLaunchKernelGGL(pool_dpbar_kernel, dim3(B, n), dim3(NT), shm, st, a);
+      mmf_launch(pool_dpbar_kernel, dim3(B, n), dim3(NT), shm, st, a);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -217,7 +217,7 @@ hipError_t launch_pool_e(const PoolEMod* mods, int nmods, int B, int heads, int 
     by += 4.0 * B * ((double)mods[i].L * H + mods[i].nsrc * heads * (mods[i].L + H) + H);
   }
   ProfLaunch prof_(st, "pool_e_kernel", fl, by);
-  hipLaunchKernelGGL(pool_e_kernel, dim3(maxb, nmods), dim3(NT), 0, st, a);
+  mmf_launch(pool_e_kernel, dim3(maxb, nmods), dim3(NT), 0, st, a);
   return hipGetLastError();
 }
 

@@ -305,7 +305,7 @@ int mmf_attention_pool_forward(int32_t batch, int32_t frames, int32_t dim, const
   hipStream_t st = (hipStream_t)stream;
   PoolFwdArgs a{batch, frames, dim, x, score_w, score_b, mask, pooled, weights};
   ProfLaunch prof_(st, "attn_pool_frames_fwd", 4.0 * batch * frames * dim, 4.0 * batch * frames * dim);
-  hipLaunchKernelGGL(attn_pool_frames_fwd, dim3(batch), dim3(NT), 0, st, a);
+  mmf_launch(attn_pool_frames_fwd, dim3(batch), dim3(NT), 0, st, a);
   HIP_TRY(hipGetLastError());
   return MMF_OK;
 }
@@ -325,12 +325,12 @@ int mmf_attention_pool_backward(int32_t batch, int32_t frames, int32_t dim, cons
   PoolBwdArgs a{batch, frames, dim, x, score_w, weights, dpooled, dx, part};
   {
     ProfLaunch prof_(st, "attn_pool_frames_bwd", 6.0 * batch * frames * dim, 8.0 * batch * frames * dim);
-    hipLaunchKernelGGL(attn_pool_frames_bwd, dim3(batch), dim3(NT), 0, st, a);
+    mmf_launch(attn_pool_frames_bwd, dim3(batch), dim3(NT), 0, st, a);
     HIP_TRY(hipGetLastError());
   }
   const int n = dim + 1;
   ProfLaunch prof_(st, "column_sum", (double)batch * n, 4.0 * batch * n);
-  hipLaunchKernelGGL(column_sum, dim3((n + NT - 1) / NT), dim3(NT), 0, st, (const float*)part, batch, n, dscore_w,
+  mmf_launch(column_sum, dim3((n + NT - 1) / NT), dim3(NT), 0, st, (const float*)part, batch, n, dscore_w,
                      dim, dscore_b);
   HIP_TRY(hipGetLastError());
   return MMF_OK;
@@ -353,7 +353,7 @@ int mmf_late_fusion_forward(int32_t batch, int32_t num_modalities, int32_t num_c
   a.logits = logits; a.wl = weight_logits; a.mask = mask; a.fused = fused; a.weights = weights;
   ProfLaunch prof_(st, "late_weights_fwd", 2.0 * batch * num_modalities * num_classes,
                    4.0 * batch * num_modalities * (num_classes + 2));
-  hipLaunchKernelGGL(late_weights_fwd, dim3(batch), dim3(NT), 0, st, a);
+  mmf_launch(late_weights_fwd, dim3(batch), dim3(NT), 0, st, a);
   HIP_TRY(hipGetLastError());
   return MMF_OK;
 }
@@ -377,11 +377,11 @@ int mmf_late_fusion_backward(int32_t batch, int32_t num_modalities, int32_t num_
   {
     ProfLaunch prof_(st, "late_weights_bwd", 4.0 * batch * num_modalities * num_classes,
                      4.0 * batch * num_modalities * (2 * num_classes + 2));
-    hipLaunchKernelGGL(late_weights_bwd, dim3(batch), dim3(NT), 0, st, a);
+    mmf_launch(late_weights_bwd, dim3(batch), dim3(NT), 0, st, a);
     HIP_TRY(hipGetLastError());
   }
   ProfLaunch prof_(st, "late_logits_grad", 2.0 * batch * num_modalities, 4.0 * batch * num_modalities);
-  hipLaunchKernelGGL(late_logits_grad, dim3(1), dim3(64), 0, st, weight_logits, (const float*)a.part, batch,
+  mmf_launch(late_logits_grad, dim3(1), dim3(64), 0, st, weight_logits, (const float*)a.part, batch,
                      num_modalities, dweight_logits);
   HIP_TRY(hipGetLastError());
   return MMF_OK;

@@ -1008,7 +1008,7 @@ hipError_t launch_tail_fwd(const TailArgs& a, hipStream_t st) {
     }
     {
       ProfLaunch prof_(st, "tail_u_kernel", fl, by);
-      hipLaunchKernelGGL(tail_u_kernel, dim3(a.B, m.nkg), dim3(NT), 0, st, m);
+      mmf_launch(tail_u_kernel, dim3(a.B, m.nkg), dim3(NT), 0, st, m);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -1016,7 +1016,7 @@ hipError_t launch_tail_fwd(const TailArgs& a, hipStream_t st) {
       // Obar = U W_v^T (+ r b_v), Abar = Obar W_o^T + b_o: weights read once per 32 samples
       ProfLaunch prof_(st, "tail_ob_mfma_kernel", 4.0 * B * H * H * a.npairs,
                        4.0 * a.npairs * (2 * H * H * ((a.B + 31) / 32) + B * (a.heads * H + 2 * H)));
-      hipLaunchKernelGGL(tail_ob_mfma_kernel, dim3((a.B + 31) / 32, a.npairs), dim3(NTW), 0, st, m);
+      mmf_launch(tail_ob_mfma_kernel, dim3((a.B + 31) / 32, a.npairs), dim3(NTW), 0, st, m);
     }
     e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -1025,17 +1025,17 @@ hipError_t launch_tail_fwd(const TailArgs& a, hipStream_t st) {
     ProfLaunch prof_(st, "tail_pair_fwd_kernel", 4.0 * B * H * H * a.npairs,
                      4.0 * a.npairs * (2 * H * H + B * (a.heads * H + 2 * H)));
     const int S = tail_samples();
-    if (S == 4) hipLaunchKernelGGL(tail_pair_fwd_kernel<4>, dim3((a.B + 3) / 4, a.npairs), dim3(NT), 0, st, a);
-    else if (S == 2) hipLaunchKernelGGL(tail_pair_fwd_kernel<2>, dim3((a.B + 1) / 2, a.npairs), dim3(NT), 0, st, a);
-    else hipLaunchKernelGGL(tail_pair_fwd_kernel<1>, dim3(a.B, a.npairs), dim3(NT), 0, st, a);
+    if (S == 4) mmf_launch(tail_pair_fwd_kernel<4>, dim3((a.B + 3) / 4, a.npairs), dim3(NT), 0, st, a);
+    else if (S == 2) mmf_launch(tail_pair_fwd_kernel<2>, dim3((a.B + 1) / 2, a.npairs), dim3(NT), 0, st, a);
+    else mmf_launch(tail_pair_fwd_kernel<1>, dim3(a.B, a.npairs), dim3(NT), 0, st, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   // pooling, gating, adaptive weights, weighted sum, classifier
   ProfLaunch prof_(st, head_pre(a) ? "tail_head_fwd_kernel<true>" : "tail_head_fwd_kernel<false>", 2.0 * B * H * (H + a.C) + 4.0 * a.M * B * H,
                    4.0 * (H * (H + a.C) + B * (a.M * H + a.C)));
-  if (head_pre(a)) hipLaunchKernelGGL(tail_head_fwd_kernel<true>, dim3(a.B), dim3(NT), 0, st, a);
-  else hipLaunchKernelGGL(tail_head_fwd_kernel<false>, dim3(a.B), dim3(NT), 0, st, a);
+  if (head_pre(a)) mmf_launch(tail_head_fwd_kernel<true>, dim3(a.B), dim3(NT), 0, st, a);
+  else mmf_launch(tail_head_fwd_kernel<false>, dim3(a.B), dim3(NT), 0, st, a);
   return hipGetLastError();
 }
 
@@ -1045,8 +1045,8 @@ hipError_t launch_tail_bwd(const TailArgs& a, hipStream_t st) {
   {
     ProfLaunch prof_(st, head_pre(a) ? "tail_head_bwd_kernel<true>" : "tail_head_bwd_kernel<false>", 2.0 * B * H * (H + a.C) + 4.0 * a.M * B * H,
                      4.0 * (H * (H + a.C) + B * (a.M * H + a.C)));
-    if (head_pre(a)) hipLaunchKernelGGL(tail_head_bwd_kernel<true>, dim3(a.B), dim3(NT), 0, st, a);
-    else hipLaunchKernelGGL(tail_head_bwd_kernel<false>, dim3(a.B), dim3(NT), 0, st, a);
+    if (head_pre(a)) mmf_launch(tail_head_bwd_kernel<true>, dim3(a.B), dim3(NT), 0, st, a);
+    else mmf_launch(tail_head_bwd_kernel<false>, dim3(a.B), dim3(NT), 0, st, a);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !a.npairs) return e;
@@ -1056,7 +1056,7 @@ hipError_t launch_tail_bwd(const TailArgs& a, hipStream_t st) {
       // dObar = c_q W_o, dU_h = dObar_h W_v,h: weights read once per 32 samples
       ProfLaunch prof_(st, "tail_dob_mfma_kernel", 4.0 * B * H * H * a.npairs,
                        4.0 * a.npairs * (2 * H * H * ((a.B + 31) / 32) + B * (a.heads * H + 2 * H)));
-      hipLaunchKernelGGL(tail_dob_mfma_kernel, dim3((a.B + 31) / 32, a.npairs), dim3(NTW), 0, st, m);
+      mmf_launch(tail_dob_mfma_kernel, dim3((a.B + 31) / 32, a.npairs), dim3(NTW), 0, st, m);
     }
     e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -1067,16 +1067,16 @@ hipError_t launch_tail_bwd(const TailArgs& a, hipStream_t st) {
       by += 4.0 * B * (lk * H + rows * (lk + H) + m.kg_cnt[i] * H);
     }
     ProfLaunch prof_(st, "tail_dpbar_mfma_kernel", fl, by);
-    hipLaunchKernelGGL(tail_dpbar_mfma_kernel, dim3(a.B, m.nkg), dim3(NT), 0, st, m);
+    mmf_launch(tail_dpbar_mfma_kernel, dim3(a.B, m.nkg), dim3(NT), 0, st, m);
     return hipGetLastError();
   }
   {
     ProfLaunch prof_(st, "tail_pair_bwd_kernel", 4.0 * B * H * H * a.npairs,
                      4.0 * a.npairs * (2 * H * H + B * (a.heads * H + 2 * H)));
     const int S = tail_samples();
-    if (S == 4) hipLaunchKernelGGL(tail_pair_bwd_kernel<4>, dim3((a.B + 3) / 4, a.npairs), dim3(NT), 0, st, a);
-    else if (S == 2) hipLaunchKernelGGL(tail_pair_bwd_kernel<2>, dim3((a.B + 1) / 2, a.npairs), dim3(NT), 0, st, a);
-    else hipLaunchKernelGGL(tail_pair_bwd_kernel<1>, dim3(a.B, a.npairs), dim3(NT), 0, st, a);
+    if (S == 4) mmf_launch(tail_pair_bwd_kernel<4>, dim3((a.B + 3) / 4, a.npairs), dim3(NT), 0, st, a);
+    else if (S == 2) mmf_launch(tail_pair_bwd_kernel<2>, dim3((a.B + 1) / 2, a.npairs), dim3(NT), 0, st, a);
+    else mmf_launch(tail_pair_bwd_kernel<1>, dim3(a.B, a.npairs), dim3(NT), 0, st, a);
   }
   return hipGetLastError();
 }
