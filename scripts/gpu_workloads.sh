@@ -1,5 +1,5 @@
-# Secondary BASELINE workloads on the box: C4 / C5 bench lines at both matmul
-# precisions and a rocprofv3 kernel summary of each C5 run.
+# Secondary BASELINE workloads on the box: C4 / C5 bench lines at every matmul
+# precision and a rocprofv3 kernel summary of each C5 run.
 # usage: bash scripts/gpu_workloads.sh <run-name>
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -7,13 +7,13 @@ export TMPDIR=/tmp
 RUN=${1:-w}
 O=gpurun_out/$RUN
 mkdir -p $O
-for cfg in "c2 medium 50 10" "c4 highest 30 5" "c4 medium 30 5" "c5 highest 8 2" "c5 medium 10 3"; do
+for cfg in "c4 highest 30 5" "c4 high 30 5" "c4 medium 30 5" "c5 highest 8 2" "c5 high 10 3" "c5 medium 10 3"; do
   set -- $cfg
   timeout -k 10 300 python -u bench.py --workload $1 --precision $2 --steps $3 --warmup $4 --skip-cpu \
     > $O/${1}_${2}.json 2> $O/${1}_${2}.err || exit 1
   python3 -c "import json;d=json.load(open('$O/${1}_${2}.json'));print('$1 $2', d['ms_per_step'], d['value'])"
 done
-for pr in highest medium; do
+for pr in highest high medium; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5_$pr -o run -- \
     python3 bench.py --workload c5 --precision $pr --steps 4 --warmup 1 --skip-cpu --profile-steps 2 \
     > $O/prof_c5_$pr.json 2> $O/prof_c5_$pr.err || exit 1
