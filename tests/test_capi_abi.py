@@ -99,11 +99,14 @@ def test_size_queries_and_validation(nat):
     assert L.mmf_hybrid_saved_bytes(ctypes.byref(odd)) == 0
     assert b"matmul_precision" in L.mmf_last_error()
     assert L.mmf_hybrid_saved_bytes(ctypes.byref(_desc(nat, matmul_precision=nat.PRECISION_MEDIUM))) > 0
+    assert L.mmf_hybrid_saved_bytes(ctypes.byref(_desc(nat, matmul_precision=nat.PRECISION_HIGH))) > 0
     c = nat.CmaDesc(2, 5, 7, 8, 8, 16, 4, 2, 0.0, 0)
     assert L.mmf_cma_saved_bytes(ctypes.byref(c)) > 0
     c.matmul_precision = 3
     assert L.mmf_cma_saved_bytes(ctypes.byref(c)) == 0
     c.matmul_precision = nat.PRECISION_MEDIUM
+    assert L.mmf_cma_saved_bytes(ctypes.byref(c)) > 0
+    c.matmul_precision = nat.PRECISION_HIGH
     assert L.mmf_cma_saved_bytes(ctypes.byref(c)) > 0
     c.mask_mode = 5
     assert L.mmf_cma_saved_bytes(ctypes.byref(c)) == 0
