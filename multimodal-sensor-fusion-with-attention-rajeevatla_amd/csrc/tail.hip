@@ -700,16 +700,35 @@ __global__ __launch_bounds__(NT) void tail_head_fwd_kernel(const TailArgs a) {
     // (1 + 2) in one pass: mean_L P_m from the projection GEMM's per-tile column sums
     // (ncol rows per sample), + the attended means of every pair whose query is m,
     // then agg * mask / n_m
-    for (int m = 0; m < M; ++m) {   // m wave-uniform (kernel-argument arrays indexed by it)
-      const int nc = a.ncol[m];
-      const float f = a.inv_cnt[m] * a.mask[(int64_t)b * M + m], il = 1.f / (float)a.L[m];
-      for (int n = t; n < H; n += NT) {
-        const float* pc = a.Pcol[m] + (int64_t)b * nc * H + n;
-        float s = 0.f;
-        for (int c = 0; c < nc; ++c) s += pc[(int64_t)c * H];
-        float v = s * il;
-        for (int g = 0; g < a.npairs; ++g)
-          if (a.p[g].q == m) v += a.p[g].Ab[(int64_t)b * H + n];
+    // Every activation this thread's feature n needs (the column sums, the attended
+    // means of every pair, the mask row) is loaded before the first store: one round
+    // trip (the stores to `pooled` would otherwise order each modality's loads behind
+    // the previous modality's stores).  head_pre: M <= 4, so at most 12 pairs.
+    constexpr int PM = 4, PG = 12;
+    const int n = t;   // H == PH <= NT
+    if (n < H) {
+      float pcs[PM], ab[PG], mk[PM];
+#pragma unroll
+      for (int m = 0; m < PM; ++m) {
+        pcs[m] = 0.f;
+        mk[m] = 0.f;
+        if (m < M) {
+          const int nc = a.ncol[m];
+          const float* pc = a.Pcol[m] + (int64_t)b * nc * H + n;
+          for (int c = 0; c < nc; ++c) pcs[m] += pc[(int64_t)c * H];
+          mk[m] = a.mask[(int64_t)b * M + m];
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < PG; ++g) ab[g] = g < a.npairs ? a.p[g].Ab[(int64_t)b * H + n] : 0.f;
+#pragma unroll
+      for (int m = 0; m < PM; ++m) {
+        if (m >= M) break;
+        const float f = a.inv_cnt[m] * mk[m], il = 1.f / (float)a.L[m];
+        float v = pcs[m] * il;
+#pragma unroll
+        for (int g = 0; g < PG; ++g)
+          if (g < a.npairs && a.p[g].q == m) v += ab[g];
         v *= f;
         pooled_s[m * H + n] = v;
         a.pooled[(int64_t)b * M * H + m * H + n] = v;
