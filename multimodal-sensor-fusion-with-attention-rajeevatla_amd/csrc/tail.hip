@@ -1043,7 +1043,10 @@ hipError_t launch_tail_fwd(const TailArgs& a, hipStream_t st) {
     // per pair: Vbar = U W_v^T (+ r b_v), Obar = Vbar W_o^T + b_o; weights read once
     ProfLaunch prof_(st, "tail_pair_fwd_kernel", 4.0 * B * H * H * a.npairs,
                      4.0 * a.npairs * (2 * H * H + B * (a.heads * H + 2 * H)));
-    const int S = tail_samples();
+    // at H = 256 the forward's weight reads (2 x 256 KB per pair) outweigh the lost
+    // parallelism: 2 samples per workgroup (C4: 42.2 -> 35.7 us; the backward stays at 1:
+    // 45.3 -> 56.6 us at 2)
+    const int S = getenv("MMF_TAIL_S") ? tail_samples() : (a.H >= 256 ? 2 : 1);
     if (S == 4) mmf_launch(tail_pair_fwd_kernel<4>, dim3((a.B + 3) / 4, a.npairs), dim3(NT), 0, st, a);
     else if (S == 2) mmf_launch(tail_pair_fwd_kernel<2>, dim3((a.B + 1) / 2, a.npairs), dim3(NT), 0, st, a);
     else mmf_launch(tail_pair_fwd_kernel<1>, dim3(a.B, a.npairs), dim3(NT), 0, st, a);
