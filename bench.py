@@ -10,8 +10,20 @@ backward (all parameter grads + input grads) -> [RCCL all-reduce of the flat
 gradient when N > 1] -> global-norm gradient clipping (1.0) -> AdamW
 (lr 1e-3, weight decay 1e-4: config/base.yaml:69-74).  Weak scaling: every rank runs B=256.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c2_l1]
-N > 1 is launched by torch.distributed.run (one process per GPU, RCCL).
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c2_l1|c4|c5]
+                       [--scaling weak|strong] [--path step|module] [--precision highest|high|medium]
+N > 1: one process per GPU over RCCL.  Under torch.distributed.run (WORLD_SIZE set) the
+ranks join directly; a plain `python bench.py --gpus N` starts
+`python -m torch.distributed.run --nproc-per-node N ... bench.py ...` as a CHILD process
+before this process touches the GPU, and exits with its return code.
+--scaling weak (default): every rank runs the workload's per-GPU batch (C2: B = 256 per GPU).
+--scaling strong: the workload's global batch (C2: 256, C5: 1024) is split over the ranks
+(128 / 64 / 32 per GPU at 2 / 4 / 8), each rank running its shard of the same
+global batch.
+--path step (default): the fused training step (train_step.HybridTrainStep: flat buffers,
+one hipGraph per step).  --path module: what src/train.py calls -- the nn.Module forward,
+torch CrossEntropyLoss, autograd backward, eager, no graph -- timed the same way (diagnostic:
+the gap to the captured step).
 Prints ONE JSON line on rank 0.
 """
 
@@ -21,6 +33,8 @@ import argparse
 import json
 import re
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -40,14 +54,37 @@ HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 #   L: per-modality sequence lengths (0 => 2-D (B, D) inputs, reference semantics)
 #   keep: per-(sample, modality) keep probability of the modality mask (>= 1 kept
 #         per row) plus 1 % all-masked rows when < 1
+#   B: per-GPU batch under weak scaling; GB: the global batch strong scaling splits
 WORKLOADS = {
-    "c2": dict(M=3, B=256, L=[128] * 3, D=128, H=128, heads=4, C=5, keep=1.0),
-    "c2_l1": dict(M=3, B=256, L=[0] * 3, D=128, H=128, heads=4, C=5, keep=1.0),
+    "c2": dict(M=3, B=256, GB=256, L=[128] * 3, D=128, H=128, heads=4, C=5, keep=1.0),
+    "c2_l1": dict(M=3, B=256, GB=256, L=[0] * 3, D=128, H=128, heads=4, C=5, keep=1.0),
     # C4 shape: video (30 frame embeddings) + IMU (50 steps), Lq != Lk, H = 256, 11 classes
-    "c4": dict(M=2, B=256, L=[30, 50], D=256, H=256, heads=4, C=11, keep=1.0),
+    "c4": dict(M=2, B=256, GB=256, L=[30, 50], D=256, H=256, heads=4, C=11, keep=1.0),
     # C5: 6 modalities, global B = 1024 over 8 GPUs, T = 512, d_model = 256, missing-modality masks
-    "c5": dict(M=6, B=128, L=[512] * 6, D=256, H=256, heads=4, C=5, keep=0.9),
+    "c5": dict(M=6, B=128, GB=1024, L=[512] * 6, D=256, H=256, heads=4, C=5, keep=0.9),
 }
+
+
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_command(gpus: int, argv, port: int, script: str = None):
+    """The child command a plain `bench.py --gpus N` (N > 1) runs: torch.distributed.run with
+    one process per GPU on this node, rendezvous on 127.0.0.1, the same bench arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", script or os.path.abspath(__file__)] + list(argv)
+
+
+def rank_batch(w, scaling: str, world: int) -> int:
+    """Per-rank batch: the per-GPU batch (weak) or the rank's share of the global batch (strong)."""
+    if scaling == "weak":
+        return w["B"]
+    if w["GB"] % world:
+        raise ValueError(f"strong scaling: global batch {w['GB']} is not divisible by {world} ranks")
+    return w["GB"] // world
 
 
 def total_step_flops(w):
@@ -189,12 +226,45 @@ def cpu_baseline(w, budget_s=12.0, max_steps=400):
                       f"{dt:.1f}s"}
 
 
-def main():
+class ModuleRunner:
+    """--path module: the nn.Module path src/train.py drives -- HybridFusion.forward under
+    autograd, torch cross_entropy(label_smoothing=0.05), loss.backward() (parameter and input
+    grads), then the exchange + clip + AdamW of harness.DPTrainer (flat buffers, bucketed
+    all-reduce).  Eager; no graph."""
+
+    def __init__(self, model, feats, mask, labels, pg):
+        from harness import DPTrainer
+        self.model = model.train()
+        self.names = list(model.modality_names)
+        self.feats = [f.clone().requires_grad_(True) for f in feats]
+        self.mask, self.labels = mask, labels
+        self.trainer = DPTrainer(model, accumulate=1, process_group=pg)
+        self.loss = torch.zeros(())
+
+    def forward_backward(self):
+        for f in self.feats:
+            f.grad = None
+        feats = dict(zip(self.names, self.feats))
+        self.trainer.flat.arm()
+        logits = self.model(feats, self.mask)
+        loss = torch.nn.functional.cross_entropy(logits, self.labels, label_smoothing=0.05)
+        loss.backward()
+        self.loss = loss.detach()
+
+    def step(self):
+        self.forward_backward()
+        self.trainer.optimizer_step()
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--path", default="step", choices=["step", "module"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--dropout", type=float, default=0.1,
                     help="diagnostics only: the benchmark workload is dropout 0.1")
@@ -208,12 +278,22 @@ def main():
                          "fp32-parity headline), 'high' = bf16x3 (operands split into bf16 hi + lo, "
                          "three bf16 MFMAs, fp32 accumulate), 'medium' = bf16 MFMA operands, fp32 "
                          "accumulate (config/base.yaml:80)")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: torch.distributed.run as a child, started before this process
+        # touches the GPU (never an exec from a GPU-initialised process)
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        return subprocess.call(launcher_command(args.gpus, argv, free_port()), env=env)
     torch.set_float32_matmul_precision(args.precision)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pg = None
@@ -221,19 +301,32 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
         pg = dist.group.WORLD
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, expected {args.gpus}")
 
     import mmf_native
     from fusion import HybridFusion
-    from train_step import HybridTrainStep
+    from train_step import HybridTrainStep, shard_batch
 
     w = WORKLOADS[args.workload]
-    M, B, D, H, heads, C = w["M"], w["B"], w["D"], w["H"], w["heads"], w["C"]
+    M, D, H, heads, C = w["M"], w["D"], w["H"], w["heads"], w["C"]
+    B = rank_batch(w, args.scaling, world)
+    wr = dict(w, B=B)                         # the per-rank workload
     torch.manual_seed(0)                      # identical initial weights on every rank
     names = [f"m{i}" for i in range(M)]
     model = HybridFusion({n: D for n in names}, hidden_dim=H, num_classes=C, num_heads=heads,
                          dropout=args.dropout).to(dev)
-    feats, mask, labels = make_inputs(w, B, 42 + rank, dev)
-    trainer = HybridTrainStep(model, feats, mask, labels, process_group=pg)
+    if args.scaling == "strong":
+        # every rank takes its contiguous shard of ONE global batch (train_step.shard_batch)
+        gf, gm, gl = make_inputs(w, w["GB"], 42, "cpu")
+        feats, mask, labels = shard_batch(gf, gm, gl, rank, world)
+        feats, mask, labels = [f.to(dev) for f in feats], mask.to(dev), labels.to(dev)
+    else:
+        feats, mask, labels = make_inputs(w, B, 42 + rank, dev)
+    if args.path == "module":
+        trainer = ModuleRunner(model, feats, mask, labels, pg)
+    else:
+        trainer = HybridTrainStep(model, feats, mask, labels, process_group=pg)
 
     # kernel-level timing (eager): hipEvents around each launch group and each
     # kernel launch, on the launch stream (mmf_profile_begin/end)
@@ -256,17 +349,23 @@ def main():
     avg_ms = {k: t / n for k, (t, n) in per_stage.items()}
     kernels = kernel_table(launches, args.profile_steps)
 
-    if not args.no_graph:
+    graph = args.path == "step" and not args.no_graph
+    if graph:
         trainer.capture()
     for _ in range(args.warmup):
         trainer.step()
     torch.cuda.synchronize(dev)
+    # per-step boundaries: one event per step on the stream the steps run on (the median below;
+    # `value` is the whole timed region)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        evs[i].record()
         trainer.step()
+    evs[-1].record()
     torch.cuda.synchronize(dev)
     if world > 1:
         torch.distributed.barrier()
@@ -277,21 +376,27 @@ def main():
     dt = float(dt_t.item())
     ms_per_step = dt / args.steps * 1e3
     value = world * B * args.steps / dt
+    per_step = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
+    med = per_step[len(per_step) // 2] if len(per_step) % 2 else 0.5 * (per_step[len(per_step) // 2 - 1] +
+                                                                          per_step[len(per_step) // 2])
     loss = float(trainer.loss.item())
 
     if rank == 0:
         roofline = dominant_roofline(kernels)
-        step_fl = total_step_flops(w)
+        step_fl = total_step_flops(wr)
         cpu = None
         if world == 1 and not args.skip_cpu:
             cpu = cpu_baseline(w)
         Ls = w["L"]
         lens = Ls[0] if len(set(Ls)) == 1 else Ls
         mask_note = "" if w["keep"] >= 1 else f", modality masks keep={w['keep']} (+1% all-masked rows)"
+        path_note = ("fused step (flat buffers, one hipGraph)" if graph else
+                     "fused step, eager" if args.path == "step" else
+                     "nn.Module forward + autograd backward, eager (src/train.py's call path)")
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
             "dtype": {"highest": "fp32", "high": "fp32 as bf16x3 (hi + lo operands, fp32 accumulate)",
                       "medium": "bf16 (fp32 accumulate)"}[args.precision],
             "data": "synthetic (N(0,1) encoder outputs, random-init weights, seeded)",
@@ -299,9 +404,13 @@ def main():
                                    f"{'' if max(Ls) else ' (2-D reference semantics)'} D={D} H={H} heads={heads} "
                                    f"C={C} dropout={args.dropout} train"
                                    f"{mask_note}"
-                                   f", fwd+CE(ls=0.05)+bwd+clip(1.0)+AdamW",
-                       "global_batch": B * world, "seq_len": lens or 1, "parallelism": f"dp{world}",
-                       "graph": not args.no_graph, "matmul_precision": args.precision},
+                                   f", fwd+CE(ls=0.05)+bwd+clip(1.0)+AdamW; {path_note}",
+                       "global_batch": B * world, "per_gpu_batch": B, "seq_len": lens or 1,
+                       "parallelism": f"dp{world}", "path": args.path,
+                       "graph": graph, "matmul_precision": args.precision},
+            "ms_per_step_median": round(med, 4),
+            "ms_per_step_p10_p90": [round(per_step[len(per_step) // 10], 4),
+                                    round(per_step[min(len(per_step) - 1, (9 * len(per_step)) // 10)], 4)],
             "roofline": roofline,
             "cpu_baseline": cpu,
             "step_tflops_algorithmic": round(step_fl / (ms_per_step * 1e-3) / 1e12, 3),
@@ -317,7 +426,8 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -30,24 +30,30 @@ namespace {
 // ------------------------------------------------------------ CrossModalAttention
 struct CmaSaved { RngSnap* rng; float *Q, *K, *V, *O, *lse; };
 
+// Lk == 1 (the reference's 2-D inputs): softmax over one key, no Q / K work
+// (single_key.hip); Q, K and the LSE are not kept.
+inline bool cma_single_key(const mmf_cma_desc* d) { return d->lk == 1; }
+
 void layout_cma(const mmf_cma_desc* d, Bump& bp, CmaSaved& s) {
   const size_t B = d->batch, H = d->hidden;
+  const bool sk = cma_single_key(d);
   s.rng = bp.take<RngSnap>(1);
-  s.Q = bp.take<float>(B * d->lq * H);
-  s.K = bp.take<float>(B * d->lk * H);
+  s.Q = sk ? nullptr : bp.take<float>(B * d->lq * H);
+  s.K = sk ? nullptr : bp.take<float>(B * d->lk * H);
   s.V = bp.take<float>(B * d->lk * H);
   s.O = bp.take<float>(B * d->lq * H);
-  s.lse = bp.take<float>(B * d->num_heads * d->lq);
+  s.lse = sk ? nullptr : bp.take<float>(B * d->num_heads * d->lq);
 }
 
 struct CmaWs { float *dO, *dsum, *dQ, *dK, *dV; };
 
 void layout_cma_ws(const mmf_cma_desc* d, Bump& bp, CmaWs& w) {
   const size_t B = d->batch, H = d->hidden;
+  const bool sk = cma_single_key(d);
   w.dO = bp.take<float>(B * d->lq * H);
-  w.dsum = bp.take<float>(B * d->num_heads * d->lq);
-  w.dQ = bp.take<float>(B * d->lq * H);
-  w.dK = bp.take<float>(B * d->lk * H);
+  w.dsum = sk ? nullptr : bp.take<float>(B * d->num_heads * d->lq);
+  w.dQ = sk ? nullptr : bp.take<float>(B * d->lq * H);
+  w.dK = sk ? nullptr : bp.take<float>(B * d->lk * H);
   w.dV = bp.take<float>(B * d->lk * H);
 }
 
@@ -83,6 +89,17 @@ AttnPair cma_pair(const mmf_cma_desc* d, const CmaSaved& s, const float* mask) {
   a.Lq = d->lq; a.Lk = d->lk;
   a.ldq = a.ldk = a.ldv = a.ldo = d->hidden;
   a.drop_site = SITE_ATTN;
+  return a;
+}
+
+SkPair cma_sk(const mmf_cma_desc* d, const CmaSaved& s, const float* mask) {
+  SkPair a;
+  memset(&a, 0, sizeof(a));
+  a.kmask = mask; a.kmask_mode = d->mask_mode; a.kmask_ld = 1;   // (B,) or (B, Lk = 1)
+  a.Lq = d->lq;
+  a.drop_site = SITE_ATTN;
+  a.v = s.V; a.ldv = d->hidden;
+  a.o = s.O; a.ldo = d->hidden;
   return a;
 }
 
@@ -294,23 +311,37 @@ int mmf_cma_forward(const mmf_cma_desc* d, const mmf_cma_params* W, const float*
   layout_cma(d, bp, s);
   if (rng_state) STAGE_TRY("cma.fwd.rng", launch_rng_snapshot(rng_state, s.rng, st));
   const RngSnap* rng = rng_state ? s.rng : nullptr;
+  const bool sk = cma_single_key(d);
   GemmJob jobs[3];
-  jobs[0] = make_job(B * d->lq, H, s.Q, H, EPI_BIAS);
-  jobs[0].g.bias = W->q.b;
-  add_src(jobs[0], opnd(query, d->query_dim), opnd(W->q.w, d->query_dim), d->query_dim);
-  jobs[1] = make_job(B * d->lk, H, s.K, H, EPI_BIAS);
-  jobs[1].g.bias = W->k.b;
-  add_src(jobs[1], opnd(key, d->key_dim), opnd(W->k.w, d->key_dim), d->key_dim);
-  jobs[2] = make_job(B * d->lk, H, s.V, H, EPI_BIAS);
-  jobs[2].g.bias = W->v.b;
-  add_src(jobs[2], opnd(value, d->key_dim), opnd(W->v.w, d->key_dim), d->key_dim);
-  STAGE_TRY("cma.fwd.qkv_gemm", launch_gemm(jobs, 3, MODE_RK, MODE_RK, 0.f, rng, st));
-  AttnPair a = cma_pair(d, s, mask);
-  a.probs = attn_weights;
-  const float scale = 1.0f / std::sqrt((float)hd);
-  STAGE_TRY("cma.fwd.attn", launch_attn_fwd(&a, 1, B, d->num_heads, hd, scale, p, rng, st));
-  if (attn_weights)
-    STAGE_TRY("cma.fwd.attn_probs", launch_attn_probs(&a, 1, B, d->num_heads, hd, scale, p, rng, st));
+  int nj = 0;
+  if (!sk) {
+    jobs[nj] = make_job(B * d->lq, H, s.Q, H, EPI_BIAS);
+    jobs[nj].g.bias = W->q.b;
+    add_src(jobs[nj++], opnd(query, d->query_dim), opnd(W->q.w, d->query_dim), d->query_dim);
+    jobs[nj] = make_job(B * d->lk, H, s.K, H, EPI_BIAS);
+    jobs[nj].g.bias = W->k.b;
+    add_src(jobs[nj++], opnd(key, d->key_dim), opnd(W->k.w, d->key_dim), d->key_dim);
+  }
+  jobs[nj] = make_job(B * d->lk, H, s.V, H, EPI_BIAS);
+  jobs[nj].g.bias = W->v.b;
+  add_src(jobs[nj++], opnd(value, d->key_dim), opnd(W->v.w, d->key_dim), d->key_dim);
+  STAGE_TRY("cma.fwd.qkv_gemm", launch_gemm(jobs, nj, MODE_RK, MODE_RK, 0.f, rng, st));
+  if (sk) {
+    // softmax over one key (src/attention.py:118-130): P' = mask indicator * dropout keep
+    SkPair a = cma_sk(d, s, mask);
+    STAGE_TRY("cma.fwd.attn_single_key", launch_sk_out(&a, 1, B, d->num_heads, hd, p, rng, st));
+    if (attn_weights) {
+      a.probs = attn_weights;
+      STAGE_TRY("cma.fwd.attn_probs_single_key", launch_sk_fwd(&a, 1, B, d->num_heads, hd, p, rng, st));
+    }
+  } else {
+    AttnPair a = cma_pair(d, s, mask);
+    a.probs = attn_weights;
+    const float scale = 1.0f / std::sqrt((float)hd);
+    STAGE_TRY("cma.fwd.attn", launch_attn_fwd(&a, 1, B, d->num_heads, hd, scale, p, rng, st));
+    if (attn_weights)
+      STAGE_TRY("cma.fwd.attn_probs", launch_attn_probs(&a, 1, B, d->num_heads, hd, scale, p, rng, st));
+  }
   GemmJob jo = make_job(B * d->lq, H, attended, H, EPI_BIAS);
   jo.g.bias = W->o.b;
   add_src(jo, opnd(s.O, H), opnd(W->o.w, H), H);
@@ -338,10 +369,17 @@ int mmf_cma_backward(const mmf_cma_desc* d, const mmf_cma_params* W, const float
   Bump bw(workspace);
   CmaWs w;
   layout_cma_ws(d, bw, w);
+  const bool sk = cma_single_key(d);
   WgradPlan wp;
   plan_wgrad(wp, bw, H, H, B * d->lq, opnd(dA, H), opnd(s.O, H), G->o.w, G->o.b);
-  plan_wgrad(wp, bw, H, d->query_dim, B * d->lq, opnd(w.dQ, H), opnd(query, d->query_dim), G->q.w, G->q.b);
-  plan_wgrad(wp, bw, H, d->key_dim, B * d->lk, opnd(w.dK, H), opnd(key, d->key_dim), G->k.w, G->k.b);
+  if (sk) {
+    // softmax over one key: query_proj / key_proj get exactly zero gradient
+    plan_zero(wp, H, d->query_dim, G->q.w, G->q.b);
+    plan_zero(wp, H, d->key_dim, G->k.w, G->k.b);
+  } else {
+    plan_wgrad(wp, bw, H, d->query_dim, B * d->lq, opnd(w.dQ, H), opnd(query, d->query_dim), G->q.w, G->q.b);
+    plan_wgrad(wp, bw, H, d->key_dim, B * d->lk, opnd(w.dK, H), opnd(key, d->key_dim), G->k.w, G->k.b);
+  }
   plan_wgrad(wp, bw, H, d->key_dim, B * d->lk, opnd(w.dV, H), opnd(value, d->key_dim), G->v.w, G->v.b);
   if (bw.off > mmf_cma_workspace_bytes(d)) return fail(MMF_EINVAL, "internal: workspace overflow");
   {
@@ -349,17 +387,26 @@ int mmf_cma_backward(const mmf_cma_desc* d, const mmf_cma_params* W, const float
     add_src(j, opnd(dA, H), opnd(W->o.w, H), H);
     STAGE_TRY("cma.bwd.dO_gemm", launch_gemm(&j, 1, MODE_RK, MODE_KR, 0.f, rng, st));
   }
-  AttnPair a = cma_pair(d, s, mask);
-  a.dout = w.dO; a.dsum = w.dsum; a.dq = w.dQ; a.dk = w.dK; a.dv = w.dV;
-  const float scale = 1.0f / std::sqrt((float)hd);
-  STAGE_TRY("cma.bwd.attn", launch_attn_bwd(&a, 1, B, d->num_heads, hd, scale, p, rng, st));
   std::vector<GemmJob> jobs;
-  if (dquery) {
+  if (sk) {
+    SkPair a = cma_sk(d, s, mask);
+    a.dout = w.dO; a.dv = w.dV;
+    STAGE_TRY("cma.bwd.attn_single_key_dv", launch_sk_dv(&a, 1, B, d->num_heads, hd, p, rng, st));
+    // the query and the key reach the output only through the one-key softmax: zero gradient
+    if (dquery) HIP_TRY(hipMemsetAsync(dquery, 0, (size_t)B * d->lq * d->query_dim * sizeof(float), st));
+    if (dkey) HIP_TRY(hipMemsetAsync(dkey, 0, (size_t)B * d->lk * d->key_dim * sizeof(float), st));
+  } else {
+    AttnPair a = cma_pair(d, s, mask);
+    a.dout = w.dO; a.dsum = w.dsum; a.dq = w.dQ; a.dk = w.dK; a.dv = w.dV;
+    const float scale = 1.0f / std::sqrt((float)hd);
+    STAGE_TRY("cma.bwd.attn", launch_attn_bwd(&a, 1, B, d->num_heads, hd, scale, p, rng, st));
+  }
+  if (dquery && !sk) {
     GemmJob j = make_job(B * d->lq, d->query_dim, dquery, d->query_dim, 0);
     add_src(j, opnd(w.dQ, H), opnd(W->q.w, d->query_dim), H);
     jobs.push_back(j);
   }
-  if (dkey) {
+  if (dkey && !sk) {
     GemmJob j = make_job(B * d->lk, d->key_dim, dkey, d->key_dim, 0);
     add_src(j, opnd(w.dK, H), opnd(W->k.w, d->key_dim), H);
     jobs.push_back(j);

@@ -222,6 +222,20 @@ inline void plan_wgrad_batched(WgradPlan& wp, Bump& ws, int M, int N, int rows, 
   wp.reds.push_back(r);
 }
 
+// A weight (and bias) gradient that is exactly zero: a reduce job over no slabs, so the
+// split-K reduce launch writes the zeros (no launch of its own).
+inline void plan_zero(WgradPlan& wp, int M, int N, float* out_w, float* out_b) {
+  ReduceJob r;
+  memset(&r, 0, sizeof(r));
+  r.nbatch = 1;
+  r.out = out_w;
+  r.db = out_b;
+  r.nsplit = 0;
+  r.M = M;
+  r.N = N;
+  if (out_w) wp.reds.push_back(r);
+}
+
 // Linear layer with bias (the common case).
 inline void plan_wgrad(WgradPlan& wp, Bump& ws, int M, int N, int rows, Operand a, Operand b,
                        float* out_w, float* out_b, float alpha = 1.f) {

@@ -149,12 +149,13 @@ __device__ __forceinline__ void epilogue(const GemmGroup& G, const TileCtx& T, f
       }
     }
     __syncthreads();
-    if (nv <= 0) continue;
+    // (threads whose 8 columns lie past N skip the rows, not the pass: every thread
+    // reaches the EPI_COLSUM barrier below)
 #pragma unroll
     for (int it = 0; it < PR / 16; ++it) {
       const int lr = (t >> 4) + 16 * it;
       const int i = T.i0 + pass * PR + lr;
-      if (i >= G.M) continue;
+      if (i >= G.M || nv <= 0) continue;
       const f32x4 lo = *reinterpret_cast<const f32x4*>(cs + lr * CS + cg);
       const f32x4 hi = *reinterpret_cast<const f32x4*>(cs + lr * CS + cg + 4);
       float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -971,7 +972,9 @@ __global__ __launch_bounds__(256) void partial_reduce_kernel(const ReduceArgs a)
   // (launch_reduce adds it past the column blocks).  Same split-group layout as
   // the columns: 64 rows x 4 groups, 4 partial sums per thread (16 loads in
   // flight), combined in a fixed order => deterministic.
-  if (J.db && J.part_db && blockIdx.x == gridDim.x - 1) {
+  // (nsplit == 0: a gradient that is exactly zero, e.g. query_proj / key_proj at Lk = 1,
+  // single_key.hip; the column blocks above wrote zeros, this block zeroes the bias)
+  if (J.db && (J.part_db || J.nsplit == 0) && blockIdx.x == gridDim.x - 1) {
     __shared__ float redb[4][64];
     for (int i0 = 0; i0 < J.M; i0 += 64) {
       const int i = i0 + el;
@@ -1332,7 +1335,7 @@ hipError_t launch_reduce(const ReduceJob* jobs, int njobs, hipStream_t st) {
     if (blocks < 1) blocks = 1;
     if (blocks > 4096) blocks = 4096;
     for (int i = 0; i < n; ++i)
-      if (a.j[i].db && a.j[i].part_db) { ++blocks; break; }   // dedicated bias-row block
+      if (a.j[i].db && (a.j[i].part_db || a.j[i].nsplit == 0)) { ++blocks; break; }   // dedicated bias-row block
     double by = 0.0;   // slabs (+ bias-row slabs) read once, sums written once
     for (int i = 0; i < n; ++i) {
       const ReduceJob& r = a.j[i];

@@ -23,6 +23,10 @@ namespace {
 
 inline int Lm(const mmf_hybrid_desc* d, int m) { return d->seq_len[m] > 0 ? d->seq_len[m] : 1; }
 inline bool dropping(const mmf_hybrid_desc* d) { return d->training && d->dropout > 0.f; }
+// Pair g attends over ONE key (2-D inputs, the reference's own case, or a 3-D key of
+// length 1): softmax over one key is the mask indicator, so the pair has no Q / K /
+// QK^T work and its query_proj / key_proj gradients are exactly zero (single_key.hip).
+inline bool single_key(const mmf_hybrid_desc* d, int g) { return Lm(d, d->pair_k[g]) == 1; }
 
 // Pooled plan (attention.hip "Pooled-output attention"): keys up to 128 run the
 // one-chunk kernels, longer keys the streamed long-key kernels; the pooled
@@ -74,9 +78,12 @@ void layout_saved(const mmf_hybrid_desc* d, Bump& bp, Saved& s) {
     if (pcol_in_proj(d, m)) s.Pcol[m] = bp.take<float>(B * (Lm(d, m) / 128) * H);
   for (int g = 0; g < d->num_pairs; ++g) {
     const size_t lq = Lm(d, d->pair_q[g]), lk = Lm(d, d->pair_k[g]);
-    s.Q[g] = bp.take<float>(B * lq * H);
-    s.K[g] = bp.take<float>(B * lk * H);
-    s.lse[g] = bp.take<float>(B * nh * lq);
+    const bool sk = single_key(d, g);
+    if (!sk) {
+      s.Q[g] = bp.take<float>(B * lq * H);
+      s.K[g] = bp.take<float>(B * lk * H);
+      s.lse[g] = bp.take<float>(B * nh * lq);
+    }
     if (pool) {
       s.pbar[g] = bp.take<float>(B * nh * lk);
       s.pbarT[g] = bp.take<float>(B * nh * lk);
@@ -84,7 +91,7 @@ void layout_saved(const mmf_hybrid_desc* d, Bump& bp, Saved& s) {
       s.r[g] = bp.take<float>(B * nh);
       s.Ob[g] = bp.take<float>(B * H);
       s.Ab[g] = bp.take<float>(B * H);
-      if (dropping(d)) s.bits[g] = bp.take<uint32_t>(B * nh * lq * kw_ld((int)lk));
+      if (dropping(d) && !sk) s.bits[g] = bp.take<uint32_t>(B * nh * lq * kw_ld((int)lk));
     } else {
       s.V[g] = bp.take<float>(B * lk * H);
       s.O[g] = bp.take<float>(B * lq * H);
@@ -117,9 +124,11 @@ void layout_ws(const mmf_hybrid_desc* d, Bump& bp, Ws& w) {
   w.dscore = bp.take<float>(B * M);
   for (int g = 0; g < d->num_pairs; ++g) {
     const size_t lq = Lm(d, d->pair_q[g]), lk = Lm(d, d->pair_k[g]);
-    w.dQ[g] = bp.take<float>(B * lq * H);
-    w.dK[g] = bp.take<float>(B * lk * H);
-    w.dsum[g] = bp.take<float>(B * nh * lq);
+    if (!single_key(d, g)) {
+      w.dQ[g] = bp.take<float>(B * lq * H);
+      w.dK[g] = bp.take<float>(B * lk * H);
+      w.dsum[g] = bp.take<float>(B * nh * lq);
+    }
     if (pool) {
       w.dOb[g] = bp.take<float>(B * H);
       w.dU[g] = bp.take<float>(B * nh * H);
@@ -189,7 +198,7 @@ void plan_wgrads(const mmf_hybrid_desc* d, const float* const* x, const float* m
   for (int p = 0; p < d->num_pairs; ++p) {
     const int lq = Lm(d, d->pair_q[p]), lk = Lm(d, d->pair_k[p]);
     if (!pool) nbig += (B * lq >= kBigRows) + (B * lk >= kBigRows);
-    nbig += (B * lq >= kBigRows) + (B * lk >= kBigRows);
+    if (!single_key(d, p)) nbig += (B * lq >= kBigRows) + (B * lk >= kBigRows);
   }
   for (int m = 0; m < M; ++m) nbig += (B * Lm(d, m) >= kBigRows);
   const int slots = 3 * device_cu_count();
@@ -227,6 +236,12 @@ void plan_wgrads(const mmf_hybrid_desc* d, const float* const* x, const float* m
                  1.f / (float)lq);
       wp.split_hint = hint(B * lk);
       plan_wgrad(wp, bw, H, H, B * lk, opnd(w.dV[p], H), opnd(s.P[k], H), g->v[p].w, g->v[p].b);
+    }
+    if (single_key(d, p)) {
+      // softmax over one key: no gradient reaches query_proj / key_proj (exact zeros)
+      plan_zero(wp, H, H, g->q[p].w, g->q[p].b);
+      plan_zero(wp, H, H, g->k[p].w, g->k[p].b);
+      continue;
     }
     wp.split_hint = hint(B * lq);
     plan_wgrad(wp, bw, H, H, B * lq, opnd(w.dQ[p], H), opnd(s.P[q], H), g->q[p].w, g->q[p].b);
@@ -346,6 +361,20 @@ AttnPair make_pair(const mmf_hybrid_desc* d, const Saved& s, const float* mask, 
   return a;
 }
 
+SkPair make_sk(const mmf_hybrid_desc* d, const Saved& s, const float* mask, int g) {
+  SkPair a;
+  memset(&a, 0, sizeof(a));
+  const int q = d->pair_q[g], k = d->pair_k[g];
+  a.kmask = mask + k; a.kmask_mode = 1; a.kmask_ld = d->num_modalities;
+  a.Lq = Lm(d, q);
+  a.drop_site = SITE_ATTN + g;
+  a.pbar = s.pbar[g];
+  a.pbarT = s.pbarT[g];
+  a.v = s.V[g]; a.ldv = d->hidden;
+  a.o = s.O[g]; a.ldo = d->hidden;
+  return a;
+}
+
 }  // namespace
 
 extern "C" {
@@ -425,14 +454,16 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
     for (int g = 0; g < d->num_pairs; ++g) {
       const int q = d->pair_q[g], k = d->pair_k[g];
       const int lq = Lm(d, q), lk = Lm(d, k);
-      GemmJob jq = make_job(B * lq, H, s.Q[g], H, EPI_BIAS);
-      jq.g.bias = W->q[g].b;
-      add_src(jq, opnd(s.P[q], H), opnd(W->q[g].w, H), H);
-      jobs.push_back(jq);
-      GemmJob jk = make_job(B * lk, H, s.K[g], H, EPI_BIAS);
-      jk.g.bias = W->k[g].b;
-      add_src(jk, opnd(s.P[k], H), opnd(W->k[g].w, H), H);
-      jobs.push_back(jk);
+      if (!single_key(d, g)) {
+        GemmJob jq = make_job(B * lq, H, s.Q[g], H, EPI_BIAS);
+        jq.g.bias = W->q[g].b;
+        add_src(jq, opnd(s.P[q], H), opnd(W->q[g].w, H), H);
+        jobs.push_back(jq);
+        GemmJob jk = make_job(B * lk, H, s.K[g], H, EPI_BIAS);
+        jk.g.bias = W->k[g].b;
+        add_src(jk, opnd(s.P[k], H), opnd(W->k[g].w, H), H);
+        jobs.push_back(jk);
+      }
       if (!pool) {
         GemmJob jv = make_job(B * lk, H, s.V[g], H, EPI_BIAS);
         jv.g.bias = W->v[g].b;
@@ -440,14 +471,27 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
         jobs.push_back(jv);
       }
     }
-    STAGE_TRY("fwd.qkv_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, 0.f, rng, st));
+    if (!jobs.empty())
+      STAGE_TRY("fwd.qkv_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, 0.f, rng, st));
   }
-  std::vector<AttnPair> pairs(d->num_pairs);
-  for (int g = 0; g < d->num_pairs; ++g) pairs[g] = make_pair(d, s, mask, g);
+  // pairs with several keys run the attention kernels; single-key pairs single_key.hip
+  std::vector<AttnPair> pairs;
+  std::vector<SkPair> skp;
+  for (int g = 0; g < d->num_pairs; ++g) {
+    if (single_key(d, g)) {
+      skp.push_back(make_sk(d, s, mask, g));
+      if (d->return_attention && attn_maps) skp.back().probs = attn_maps[g];
+    } else {
+      pairs.push_back(make_pair(d, s, mask, g));
+      if (d->return_attention && attn_maps) pairs.back().probs = attn_maps[g];
+    }
+  }
+  const int nmp = (int)pairs.size(), nsk = (int)skp.size();
   const float scale = 1.0f / std::sqrt((float)hd);
   if (d->num_pairs && pool) {
     // (3p) attention -> LSE, pbar = mean_q P'; U = pbar P_k; Obar = U W_v^T + r b_v; Abar = out_proj
-    STAGE_TRY("fwd.attn", launch_attn_pool_fwd(pairs.data(), d->num_pairs, B, nh, hd, scale, p, rng, st));
+    if (nmp) STAGE_TRY("fwd.attn", launch_attn_pool_fwd(pairs.data(), nmp, B, nh, hd, scale, p, rng, st));
+    if (nsk) STAGE_TRY("fwd.attn_single_key", launch_sk_fwd(skp.data(), nsk, B, nh, hd, p, rng, st));
     std::vector<PoolPair> pp(d->num_pairs);
     for (int g = 0; g < d->num_pairs; ++g) {
       memset(&pp[g], 0, sizeof(PoolPair));
@@ -490,7 +534,8 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
     }
   } else if (d->num_pairs) {
     // (3g) flash attention per pair (key mask = modality mask column k, fusion.py:391-401) + out_proj
-    STAGE_TRY("fwd.attn", launch_attn_fwd(pairs.data(), d->num_pairs, B, nh, hd, scale, p, rng, st));
+    if (nmp) STAGE_TRY("fwd.attn", launch_attn_fwd(pairs.data(), nmp, B, nh, hd, scale, p, rng, st));
+    if (nsk) STAGE_TRY("fwd.attn_single_key", launch_sk_out(skp.data(), nsk, B, nh, hd, p, rng, st));
     std::vector<GemmJob> jobs;
     for (int g = 0; g < d->num_pairs; ++g) {
       const int lq = Lm(d, d->pair_q[g]);
@@ -519,15 +564,23 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
     STAGE_TRY("fwd.cls2_gemm", launch_gemm(&j2, 1, MODE_RK, MODE_RK, 0.f, rng, st));
   }
   // (6) optional attention maps (post-dropout, attention.py:130,144-146)
+  //     (single-key pairs wrote theirs in sk_fwd; the general plan's sk_out does not)
   if (d->return_attention && attn_maps && d->num_pairs) {
     std::vector<AttnPair> pp;
-    for (int g = 0; g < d->num_pairs; ++g)
-      if (attn_maps[g]) {
-        pp.push_back(pairs[g]);
-        pp.back().probs = attn_maps[g];
-      }
+    for (const AttnPair& a : pairs)
+      if (a.probs) pp.push_back(a);
     if (!pp.empty())
       STAGE_TRY("fwd.attn_probs", launch_attn_probs(pp.data(), (int)pp.size(), B, nh, hd, scale, p, rng, st));
+    if (!pool) {
+      std::vector<SkPair> sp;
+      for (SkPair a : skp)
+        if (a.probs) {
+          a.pbar = a.pbarT = nullptr;
+          sp.push_back(a);
+        }
+      if (!sp.empty())
+        STAGE_TRY("fwd.attn_probs_single_key", launch_sk_fwd(sp.data(), (int)sp.size(), B, nh, hd, p, rng, st));
+    }
   }
   return MMF_OK;
 }
@@ -591,12 +644,21 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
     }
   }
   const float scale = 1.0f / std::sqrt((float)hd);
-  std::vector<AttnPair> pairs(d->num_pairs);
+  std::vector<AttnPair> pairs;
+  std::vector<SkPair> skp;
   for (int g = 0; g < d->num_pairs; ++g) {
-    pairs[g] = make_pair(d, s, mask, g);
-    pairs[g].dsum = w.dsum[g]; pairs[g].dq = w.dQ[g]; pairs[g].dk = w.dK[g];
-    pairs[g].dout = w.dO[g]; pairs[g].dv = w.dV[g]; pairs[g].dpbar = w.dpbar[g];
+    if (single_key(d, g)) {
+      skp.push_back(make_sk(d, s, mask, g));
+      skp.back().dout = w.dO[g];
+      skp.back().dv = w.dV[g];
+      continue;
+    }
+    pairs.push_back(make_pair(d, s, mask, g));
+    AttnPair& a = pairs.back();
+    a.dsum = w.dsum[g]; a.dq = w.dQ[g]; a.dk = w.dK[g];
+    a.dout = w.dO[g]; a.dv = w.dV[g]; a.dpbar = w.dpbar[g];
   }
+  const int nmp = (int)pairs.size(), nsk = (int)skp.size();
   if (d->num_pairs && pool) {
     // (3p) dObar = dAbar W_o (dAbar = c_q); dU_h = dObar_h W_v,h; dpbar; attention dQ/dK; E_m
     if (!tail) {
@@ -631,18 +693,21 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
       pp[g].dpbar = w.dpbar[g];
     }
     if (!tail) STAGE_TRY("bwd.pool_dpbar", launch_pool_dpbar(pp.data(), d->num_pairs, B, nh, hd, H, st));
-    hipError_t fe;
-    {
-      Stage stage_("bwd.attn", st);
-      fe = getenv("MMF_NO_FUSED_BWD") ? hipErrorNotSupported
-                                      : launch_attn_pool_bwd(2, pairs.data(), d->num_pairs, B, nh, hd, scale, p, rng, st);
-    }
-    if (fe == hipErrorNotSupported) {
-      (void)hipGetLastError();
-      STAGE_TRY("bwd.attn_dq", launch_attn_pool_bwd(0, pairs.data(), d->num_pairs, B, nh, hd, scale, p, rng, st));
-      STAGE_TRY("bwd.attn_dk", launch_attn_pool_bwd(1, pairs.data(), d->num_pairs, B, nh, hd, scale, p, rng, st));
-    } else {
-      HIP_TRY(fe);
+    // (single-key pairs: no attention backward, dQ = dK = 0)
+    if (nmp) {
+      hipError_t fe;
+      {
+        Stage stage_("bwd.attn", st);
+        fe = getenv("MMF_NO_FUSED_BWD") ? hipErrorNotSupported
+                                        : launch_attn_pool_bwd(2, pairs.data(), nmp, B, nh, hd, scale, p, rng, st);
+      }
+      if (fe == hipErrorNotSupported) {
+        (void)hipGetLastError();
+        STAGE_TRY("bwd.attn_dq", launch_attn_pool_bwd(0, pairs.data(), nmp, B, nh, hd, scale, p, rng, st));
+        STAGE_TRY("bwd.attn_dk", launch_attn_pool_bwd(1, pairs.data(), nmp, B, nh, hd, scale, p, rng, st));
+      } else {
+        HIP_TRY(fe);
+      }
     }
     std::vector<PoolEMod> em;
     for (int m = 0; m < M; ++m) {
@@ -673,9 +738,12 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
       jobs.push_back(j);
     }
     STAGE_TRY("bwd.out_dO_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, 0.f, rng, st));
-    STAGE_TRY("bwd.attn_prep", launch_attn_bwd_stage(0, pairs.data(), d->num_pairs, B, nh, hd, scale, p, rng, st));
-    STAGE_TRY("bwd.attn_dkv", launch_attn_bwd_stage(1, pairs.data(), d->num_pairs, B, nh, hd, scale, p, rng, st));
-    STAGE_TRY("bwd.attn_dq", launch_attn_bwd_stage(2, pairs.data(), d->num_pairs, B, nh, hd, scale, p, rng, st));
+    if (nmp) {
+      STAGE_TRY("bwd.attn_prep", launch_attn_bwd_stage(0, pairs.data(), nmp, B, nh, hd, scale, p, rng, st));
+      STAGE_TRY("bwd.attn_dkv", launch_attn_bwd_stage(1, pairs.data(), nmp, B, nh, hd, scale, p, rng, st));
+      STAGE_TRY("bwd.attn_dq", launch_attn_bwd_stage(2, pairs.data(), nmp, B, nh, hd, scale, p, rng, st));
+    }
+    if (nsk) STAGE_TRY("bwd.attn_single_key_dv", launch_sk_dv(skp.data(), nsk, B, nh, hd, p, rng, st));
   }
   // (4) dZ_m = gate(P_m) * [direct + sum_q dQ W_q + sum_k dK W_k (+ dV W_v)]
   {
@@ -697,9 +765,10 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
       j.g.ld_gate = H;
       j.g.gate_scale = gscale;
       for (int g = 0; g < d->num_pairs; ++g) {
-        if (d->pair_q[g] == m) add_src(j, opnd(w.dQ[g], H), opnd(W->q[g].w, H), H);
+        const bool sk = single_key(d, g);
+        if (d->pair_q[g] == m && !sk) add_src(j, opnd(w.dQ[g], H), opnd(W->q[g].w, H), H);
         if (d->pair_k[g] == m) {
-          add_src(j, opnd(w.dK[g], H), opnd(W->k[g].w, H), H);
+          if (!sk) add_src(j, opnd(w.dK[g], H), opnd(W->k[g].w, H), H);
           if (!pool) add_src(j, opnd(w.dV[g], H), opnd(W->v[g].w, H), H);
         }
       }

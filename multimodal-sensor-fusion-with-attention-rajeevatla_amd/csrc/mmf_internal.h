@@ -265,6 +265,38 @@ hipError_t launch_attn_pool_bwd(int stage, const AttnPair* pairs, int npairs, in
                                 float scale, float drop_p, const RngSnap* rng, hipStream_t st);
 
 // ---------------------------------------------------------------------------
+// Single-key attention (single_key.hip): Lk == 1, the reference's 2-D inputs.
+// P'[b, h, q] = [kmask_b != 0] * keep(b, h, q) / (1 - p), independent of Q and K
+// (softmax over one key), so no Q / K / QK^T work exists and their gradients are
+// exactly zero.  kmask as AttnPair (mode 1 or 2 read element b * kmask_ld).
+// ---------------------------------------------------------------------------
+struct SkPair {
+  const float* kmask; int32_t kmask_mode; int32_t kmask_ld;
+  int32_t Lq;
+  uint32_t drop_site;
+  float* pbar;         // (B, heads) mean_q P'   (sk_fwd; may be null)
+  float* pbarT;        // (B, 1, heads) copy     (sk_fwd; may be null)
+  float* probs;        // (B, heads, Lq, 1)      (sk_fwd; may be null)
+  const float* v; int32_t ldv;   // V (B, 1, ldv)                       (sk_out)
+  float* o; int32_t ldo;         // O (B, Lq, ldo) = P' V               (sk_out)
+  const float* dout;             // dO (B, Lq, ldo)                     (sk_dv)
+  float* dv;                     // dV (B, 1, ldv) = sum_q P' dO        (sk_dv)
+};
+constexpr int SK_MAX_PAIRS = 16;
+struct SkArgs {
+  SkPair p[SK_MAX_PAIRS];
+  int32_t npairs, B, heads, hd;
+  float drop_p;
+  const RngSnap* rng;
+};
+hipError_t launch_sk_fwd(const SkPair* pairs, int npairs, int B, int heads, int hd, float drop_p,
+                         const RngSnap* rng, hipStream_t st);
+hipError_t launch_sk_out(const SkPair* pairs, int npairs, int B, int heads, int hd, float drop_p,
+                         const RngSnap* rng, hipStream_t st);
+hipError_t launch_sk_dv(const SkPair* pairs, int npairs, int B, int heads, int hd, float drop_p,
+                        const RngSnap* rng, hipStream_t st);
+
+// ---------------------------------------------------------------------------
 // Pooled-output helpers (pool.hip), per (pair, sample):
 //   U[h] = pbar_h P_k      r[h] = sum_j pbar_h[j]            (forward)
 //   dpbar_h[j] = P_k[j] . dU[h] + dObar_h . bv_h             (backward)

@@ -1,0 +1,354 @@
+"""Module-path training harness: the reference's MultimodalFusionModule, data-parallel.
+
+The reference trains encoders and the fusion model jointly in one process on the
+CPU through Lightning (src/train.py:125-430, Trainer(devices=1, gradient_clip_val,
+accumulate_grad_batches=4), :511-524).  This is its MI355X-native equivalent for the
+configs that train encoders (C3 PAMAP2, C4 MHAD), one process per GPU:
+
+  * ``MultimodalFusionModel`` mirrors ``MultimodalFusionModule.forward``
+    (src/train.py:233-291): per-modality encoder -> optional LayerNorm ->
+    ``fusion_model(encoded, mask)``; modalities absent from ``features`` are skipped
+    as there (:259-262).  Built from config/base.yaml's keys by ``from_config`` with
+    the reference's ``build_encoder`` dispatch (src/encoders.py:400-451; SequenceEncoder
+    'lstm' on csrc/lstm.hip, FrameEncoder with its attention pooling on
+    csrc/softmax_pool.hip, HybridFusion on the fused HIP path).  When every encoder
+    is a SequenceEncoder with one (B, T), the LSTMs of all modalities share each
+    recurrence launch (``encode_sequences``).
+  * ``FlatGradBuckets`` re-points every parameter into one contiguous fp32 buffer and
+    its gradient into views of another (autograd accumulates into them in place), and
+    all-reduces that gradient in buckets issued from post-accumulate-grad hooks: the
+    fusion model's gradients (its backward runs first) are in flight over RCCL / xGMI
+    while the encoders' LSTM backward still runs.  The only data-path exchange.
+  * ``DPTrainer`` is Lightning's automatic optimisation for this model:
+    CrossEntropyLoss(label_smoothing) (src/train.py:185-186, 310), the loss divided by
+    ``accumulate`` and back-propagated per micro-batch, the gradient exchanged once per
+    optimizer step (the other micro-batches accumulate locally), global-norm clipping
+    and AdamW in two HIP launches over the flat buffers (mmf_clip_adamw_step_dev,
+    src/train.py:374-430), CosineAnnealingLR per epoch (:394-402).
+  * ``shard_indices`` is torch's DistributedSampler partition (pad by wrapping to a
+    multiple of the world size, rank r takes every world-th index), used to shard the
+    PAMAP2 chunk list (manifest loader batch = 1 chunk, src/data.py:560-566).
+"""
+
+from __future__ import annotations
+
+import math
+import os
+import sys
+from typing import Any, Dict, List, Optional, Sequence
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+if _HERE not in sys.path:
+    sys.path.insert(0, _HERE)
+
+
+# ----------------------------------------------------------------------------- sharding
+def shard_indices(n: int, rank: int, world: int, shuffle: bool = False, seed: int = 0, epoch: int = 0) -> List[int]:
+    """torch.utils.data.DistributedSampler(drop_last=False) partition of range(n).
+
+    With shuffle, the permutation is torch.randperm(n) under manual_seed(seed + epoch)
+    (DistributedSampler.__iter__); the list is padded by wrapping to a multiple of
+    world, and rank r takes indices r, r + world, ...  Every rank gets
+    ceil(n / world) indices, so all ranks run the same number of steps."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} for world size {world}")
+    if n < 1:
+        return []
+    if shuffle:
+        g = torch.Generator()
+        g.manual_seed(seed + epoch)
+        idx = torch.randperm(n, generator=g).tolist()
+    else:
+        idx = list(range(n))
+    per = math.ceil(n / world)
+    total = per * world
+    pad = total - n
+    if pad:
+        reps = math.ceil(pad / n)
+        idx += (idx * reps)[:pad]
+    return idx[rank:total:world]
+
+
+# ----------------------------------------------------------------------------- model
+class MultimodalFusionModel(nn.Module):
+    """encoders -> optional LayerNorm -> fusion (src/train.py:140-191, 233-291)."""
+
+    def __init__(self, encoders: Dict[str, nn.Module], fusion_model: nn.Module, output_dim: int,
+                 layer_norm: bool = True):
+        super().__init__()
+        self.encoders = nn.ModuleDict(encoders)
+        self.use_layer_norm = bool(layer_norm)
+        self.layer_norms = nn.ModuleDict({m: nn.LayerNorm(output_dim) for m in encoders} if layer_norm else {})
+        self.fusion_model = fusion_model
+
+    @classmethod
+    def from_config(cls, config: Dict[str, Any]) -> "MultimodalFusionModel":
+        """Build from config/base.yaml's keys: dataset.modalities, dataset.num_classes,
+        model.{encoders, output_dim, hidden_dim, num_heads, dropout, fusion_type, layer_norm}
+        (the construction order of src/train.py:150-182)."""
+        from encoders import FrameEncoder, SequenceEncoder
+        from fusion import build_fusion_model
+        ds, mc = config["dataset"], config["model"]
+        out_dim = int(mc["output_dim"])
+        encs: Dict[str, nn.Module] = {}
+        for m in ds["modalities"]:
+            ec = dict(mc.get("encoders", {}).get(m, {}))
+            in_dim = int(ec.pop("input_dim", 64))
+            kind = ec.pop("type", None)
+            key = m.lower()
+            if kind == "frame" or (kind is None and key in ("video", "frames")):
+                encs[m] = FrameEncoder(frame_dim=in_dim, output_dim=out_dim, **ec)
+            elif kind == "sequence" or (kind is None and (key in ("imu", "audio", "mocap", "accelerometer")
+                                                          or key.startswith("imu_"))):
+                encs[m] = SequenceEncoder(input_dim=in_dim, output_dim=out_dim, **ec)
+            else:
+                # SimpleMLPEncoder (src/encoders.py:339-397) serves config 1's EarlyFusion CPU plumbing only
+                raise NotImplementedError(f"encoder for modality '{m}' ({kind or 'mlp'}) is not on the MI355X path")
+        fusion = build_fusion_model(mc.get("fusion_type", "hybrid"), {m: out_dim for m in encs},
+                                    int(ds.get("num_classes", 11)), hidden_dim=int(mc["hidden_dim"]),
+                                    num_heads=int(mc.get("num_heads", 4)), dropout=float(mc["dropout"]))
+        return cls(encs, fusion, out_dim, bool(mc.get("layer_norm", False)))
+
+    def _batched_sequences(self, features: Dict[str, torch.Tensor]) -> bool:
+        from encoders import SequenceEncoder
+        present = [m for m in self.encoders if m in features]
+        if len(present) < 2:
+            return False
+        encs = [self.encoders[m] for m in present]
+        if not all(isinstance(e, SequenceEncoder) and e.rnn is not None for e in encs):
+            return False
+        r0 = encs[0].rnn
+        shapes = {tuple(features[m].shape[:2]) for m in present}
+        return (len(shapes) == 1 and all(features[m].dim() == 3 for m in present)
+                and all(e.rnn.hidden_size == r0.hidden_size and e.rnn.num_layers == r0.num_layers for e in encs))
+
+    def encode(self, features: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        if self._batched_sequences(features):
+            from encoders import encode_sequences
+            present = [m for m in self.encoders if m in features]
+            enc = encode_sequences({m: self.encoders[m] for m in present}, {m: features[m] for m in present})
+        else:
+            enc = {m: self.encoders[m](features[m]) for m in self.encoders if m in features}
+        out = {}
+        for m in self.encoders:          # modality order = the encoders' order (src/train.py:250)
+            if m not in enc:
+                continue
+            x = enc[m]
+            if self.use_layer_norm and m in self.layer_norms:
+                x = self.layer_norms[m](x)
+            out[m] = x
+        return out
+
+    def forward(self, features: Dict[str, torch.Tensor], mask: Optional[torch.Tensor] = None,
+                return_attention: bool = False):
+        encoded = self.encode(features)
+        if return_attention:
+            output = self.fusion_model(encoded, mask, return_attention=True)
+        else:
+            output = self.fusion_model(encoded, mask)
+        if isinstance(output, tuple):     # LateFusion returns (logits, per-modality logits)
+            logits, aux = output[0], (output[1] if len(output) > 1 else None)
+        else:
+            logits, aux = output, None
+        return (logits, aux) if return_attention else logits
+
+
+# ----------------------------------------------------------------------------- flat buffers + bucketed all-reduce
+class FlatGradBuckets:
+    """All parameters of `modules` in one flat fp32 buffer, their gradients as views of a
+    second one, exchanged in buckets.
+
+    Buckets follow `groups` (lists of parameters, e.g. [fusion params, encoder params]):
+    a bucket is all-reduced (sum, async) from the post-accumulate-grad hook of the last
+    of its parameters to finish accumulating -- while the rest of the backward still
+    runs -- when ``arm()`` was called for this backward.  ``finish()`` issues what is
+    left (parameters that received no gradient) and waits.  Tensors start on 256-byte
+    boundaries (the HIP kernels' 16-byte vector paths)."""
+
+    ALIGN = 64
+
+    def __init__(self, groups: Sequence[Sequence[nn.Parameter]], process_group=None):
+        self.pg = process_group
+        self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
+        params: List[nn.Parameter] = []
+        seen = set()
+        self.groups: List[List[nn.Parameter]] = []
+        for grp in groups:
+            g = [p for p in grp if p.requires_grad and id(p) not in seen]
+            seen.update(id(p) for p in g)
+            if g:
+                self.groups.append(g)
+                params += g
+        if not params:
+            raise ValueError("FlatGradBuckets: no trainable parameters")
+        dev = params[0].device
+        for p in params:
+            if p.dtype != torch.float32 or p.device != dev:
+                raise ValueError("FlatGradBuckets: every parameter must be fp32 on one device")
+        offs, off = [], 0
+        spans = []
+        for g in self.groups:
+            start = off
+            for p in g:
+                offs.append(off)
+                off += -(-p.numel() // self.ALIGN) * self.ALIGN
+            spans.append((start, off))
+        self.numel = off
+        self.params = params
+        self.flat = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(off, dtype=torch.float32, device=dev)
+        for o, p in zip(offs, params):
+            k = p.numel()
+            self.flat[o:o + k].copy_(p.detach().reshape(-1))
+            p.data = self.flat[o:o + k].view_as(p)
+            p.grad = self.grad[o:o + k].view_as(p)
+        self.spans = spans
+        self._bucket_of = {}
+        for b, g in enumerate(self.groups):
+            for p in g:
+                self._bucket_of[id(p)] = b
+        self._pending = [0] * len(self.groups)
+        self._works: List[Any] = [None] * len(self.groups)
+        self._armed = False
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in params]
+
+    def bucket(self, b: int) -> torch.Tensor:
+        s, e = self.spans[b]
+        return self.grad[s:e]
+
+    def zero_grad(self) -> None:
+        self.grad.zero_()
+
+    def arm(self) -> None:
+        """The next backward is the last before an optimizer step: exchange its buckets."""
+        self._armed = True
+        self._pending = [len(g) for g in self.groups]
+        self._works = [None] * len(self.groups)
+
+    def _on_grad(self, p: torch.Tensor) -> None:
+        if not self._armed:
+            return
+        b = self._bucket_of[id(p)]
+        self._pending[b] -= 1
+        if self._pending[b] == 0 and self._works[b] is None:
+            self._launch(b)
+
+    def _launch(self, b: int) -> None:
+        if self.world > 1:
+            self._works[b] = torch.distributed.all_reduce(self.bucket(b), group=self.pg, async_op=True)
+        else:
+            self._works[b] = True
+
+    def finish(self) -> None:
+        """Issue the buckets no hook issued, then wait for every exchange."""
+        if not self._armed:
+            return
+        for b in range(len(self.groups)):
+            if self._works[b] is None:
+                self._launch(b)
+        for w in self._works:
+            if w is not None and w is not True:
+                w.wait()
+        self._armed = False
+
+    def remove_hooks(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+
+# ----------------------------------------------------------------------------- trainer
+class DPTrainer:
+    """Automatic optimisation of the reference's training_step for MultimodalFusionModel
+    (or any module returning logits), one process per GPU.
+
+    step(batches) runs len(batches) == accumulate micro-batches: forward, CE with label
+    smoothing, backward of loss / accumulate (Lightning's scaling), the last one with
+    the bucketed gradient exchange armed; then clip (global norm over the rank-averaged
+    gradient) + AdamW on the flat buffers in two HIP launches.  Defaults are
+    config/base.yaml's training keys."""
+
+    def __init__(self, model: nn.Module, lr: float = 1e-3, weight_decay: float = 1e-4, betas=(0.9, 0.999),
+                 eps: float = 1e-8, label_smoothing: float = 0.05, gradient_clip_norm: float = 1.0,
+                 accumulate: int = 4, process_group=None, buckets: Optional[Sequence[Sequence[nn.Parameter]]] = None):
+        import mmf_native as nat
+        self._nat = nat
+        self.model = model
+        dev = next(model.parameters()).device
+        nat.require_device(next(model.parameters()), "DPTrainer parameters")
+        self.dev = dev
+        if buckets is None:
+            fusion = getattr(model, "fusion_model", None)
+            if fusion is not None:
+                rest = [p for n, p in model.named_parameters() if not n.startswith("fusion_model.")]
+                buckets = [list(fusion.parameters()), rest]
+            else:
+                buckets = [list(model.parameters())]
+        self.flat = FlatGradBuckets(buckets, process_group)
+        self.world = self.flat.world
+        if process_group is not None and self.world > 1:
+            # identical initial weights on every rank (DDP's broadcast from rank 0) ...
+            torch.distributed.broadcast(self.flat.flat, src=torch.distributed.get_global_rank(process_group, 0),
+                                        group=process_group)
+            # ... but distinct dropout streams: the rank folded into each HIP module's Philox key, once
+            rank = torch.distributed.get_rank(process_group)
+            for mod in model.modules():
+                buf = getattr(mod, "_rng_state", None)
+                if isinstance(buf, torch.Tensor) and not getattr(mod, "_mmf_rank_folded", False):
+                    buf[0] ^= rank * 0x9E3779B1
+                    mod._mmf_rank_folded = True
+        self.accumulate = int(accumulate)
+        self.smoothing = label_smoothing
+        self.clip_norm = gradient_clip_norm
+        self.wd, self.betas, self.eps = weight_decay, betas, eps
+        n = self.flat.numel
+        self.exp_avg = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.step_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.lr_dev = torch.full((1,), float(lr), dtype=torch.float32, device=dev)
+        self.grad_norm = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.clip_coef = torch.ones(1, dtype=torch.float32, device=dev)
+        L = nat.lib()
+        self.clip_ws = torch.empty(L.mmf_grad_clip_workspace_bytes(), dtype=torch.uint8, device=dev)
+        self.last_loss = torch.zeros((), device=dev)
+
+    def set_lr(self, lr: float) -> None:
+        self.lr_dev.fill_(float(lr))
+
+    def micro_step(self, features, labels, mask=None, sync: bool = True) -> torch.Tensor:
+        """One micro-batch: forward, loss / accumulate, backward; `sync` arms the exchange."""
+        self.model.train()
+        logits = self.model(features, mask)
+        loss = F.cross_entropy(logits, labels, label_smoothing=self.smoothing)
+        if sync:
+            self.flat.arm()
+        (loss / self.accumulate).backward()
+        return loss.detach()
+
+    def optimizer_step(self) -> None:
+        self.flat.finish()
+        L = self._nat.lib()
+        rc = L.mmf_clip_adamw_step_dev(self.flat.numel, self.flat.flat.data_ptr(), self.flat.grad.data_ptr(),
+                                       self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), self.step_dev.data_ptr(),
+                                       self.lr_dev.data_ptr(), float(self.clip_norm), self.grad_norm.data_ptr(),
+                                       self.clip_coef.data_ptr(), self.clip_ws.data_ptr(), self.betas[0],
+                                       self.betas[1], self.eps, self.wd, 1.0 / self.world,
+                                       self._nat.stream_ptr(self.dev))
+        self._nat.check(rc, "DPTrainer clip + AdamW")
+        self.flat.zero_grad()
+
+    def step(self, batches: Sequence[tuple]) -> torch.Tensor:
+        """batches: `accumulate` tuples (features, labels, mask); returns the mean loss."""
+        if len(batches) != self.accumulate:
+            raise ValueError(f"step: expected {self.accumulate} micro-batches, got {len(batches)}")
+        total = torch.zeros((), device=self.dev)
+        for i, (feats, labels, mask) in enumerate(batches):
+            total = total + self.micro_step(feats, labels, mask, sync=(i == len(batches) - 1))
+        self.optimizer_step()
+        self.last_loss = total / len(batches)
+        return self.last_loss
+

@@ -96,11 +96,12 @@ class HybridTrainStep:
         self.clip_norm = gradient_clip_norm
         self.pg = process_group
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
+        # the step's own dropout state (the module's buffer is left untouched): every rank
+        # starts from the same seed (identical weights), so the rank is folded into the
+        # Philox key of this copy, or the dropout streams would repeat across ranks
+        self.rng = model._rng_state.detach().clone()
         if self.world > 1:
-            # every rank starts from the same seed (identical weights), so the dropout
-            # streams would repeat across ranks: fold the rank into the Philox key
-            rank = torch.distributed.get_rank(process_group)
-            model._rng_state[0] ^= rank * 0x9E3779B1
+            self.rng[0] ^= torch.distributed.get_rank(process_group) * 0x9E3779B1
         # static input buffers (graph replays read these addresses)
         self.x = [_nat.f32c(f.to(dev)).clone() for f in feats]
         self.mask = _nat.f32c(mask).clone()
@@ -171,7 +172,7 @@ class HybridTrainStep:
         st = _nat.stream_ptr(self.dev)
         rc = L.mmf_hybrid_forward(ctypes.byref(d), ctypes.byref(self.pstruct),
                                   ctypes.cast(self.xarr, ctypes.c_void_p), self.mask.data_ptr(),
-                                  self.model._rng_state.data_ptr(), self.saved.data_ptr(),
+                                  self.rng.data_ptr(), self.saved.data_ptr(),
                                   self.logits.data_ptr(), self.fw.data_ptr(), None, st)
         _nat.check(rc, "train forward")
         rc = L.mmf_cross_entropy_ls(d.batch, d.num_classes, self.logits.data_ptr(), self.labels.data_ptr(),

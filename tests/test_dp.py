@@ -143,8 +143,10 @@ def _gpu_rank(rank: int, world: int, port: int, out: str) -> None:
         seed0 = int(model._rng_state[0].item())
         step = HybridTrainStep(model, [f.to(dev) for f in lf], lm.to(dev), ll.to(dev),
                                process_group=dist.group.WORLD)
-        # every rank starts from the same seed; the step folds the rank into the Philox key
-        assert int(model._rng_state[0].item()) == seed0 ^ (rank * 0x9E3779B1)
+        # every rank starts from the same seed; the step folds the rank into the Philox key of
+        # its own copy of the dropout state and leaves the module's buffer untouched
+        assert int(step.rng[0].item()) == seed0 ^ (rank * 0x9E3779B1)
+        assert int(model._rng_state[0].item()) == seed0
         step.forward_backward()
         step.allreduce()
         torch.cuda.synchronize(dev)

@@ -90,8 +90,9 @@ def test_graph_follows_lr_and_new_batches(mods):
         st = train_step.HybridTrainStep(model, [f.cuda() for f in a[0]], a[1].cuda(), a[2].cuda(), lr=1e-3)
         if graph:
             st.capture()
-            # capture() ran one warm-up forward/backward: realign the RNG with the eager run
-            model._rng_state.copy_(torch.tensor([1234, 0], dtype=torch.int64))
+            # capture() ran one warm-up forward/backward: realign the step's own dropout state
+            # (a copy of the module's buffer taken at construction) with the eager run
+            st.rng.copy_(torch.tensor([1234, 0], dtype=torch.int64))
         st.step()
         st.set_lr(train_step.cosine_annealing_lr(50, 1e-3, 100))
         st.load_batch([f.cuda() for f in b[0]], b[1].cuda(), b[2].cuda())
