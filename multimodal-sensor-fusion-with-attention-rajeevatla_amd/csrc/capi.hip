@@ -28,11 +28,15 @@ using namespace mmf;
 namespace {
 
 // ------------------------------------------------------------ CrossModalAttention
-struct CmaSaved { RngSnap* rng; float *Q, *K, *V, *O, *lse; };
+struct CmaSaved { RngSnap* rng; float *Q, *K, *V, *O, *lse, *P, *Pd; };
 
 // Lk == 1 (the reference's 2-D inputs): softmax over one key, no Q / K work
 // (single_key.hip); Q, K and the LSE are not kept.
 inline bool cma_single_key(const mmf_cma_desc* d) { return d->lk == 1; }
+// head_dim > MMF_MAX_HEAD_DIM: materialised scores + GEMMs (wide.hip)
+inline bool cma_wide(const mmf_cma_desc* d) {
+  return !cma_single_key(d) && d->hidden / d->num_heads > MMF_MAX_HEAD_DIM;
+}
 
 void layout_cma(const mmf_cma_desc* d, Bump& bp, CmaSaved& s) {
   const size_t B = d->batch, H = d->hidden;
@@ -43,9 +47,14 @@ void layout_cma(const mmf_cma_desc* d, Bump& bp, CmaSaved& s) {
   s.V = bp.take<float>(B * d->lk * H);
   s.O = bp.take<float>(B * d->lq * H);
   s.lse = sk ? nullptr : bp.take<float>(B * d->num_heads * d->lq);
+  s.P = s.Pd = nullptr;
+  if (cma_wide(d)) {
+    s.P = bp.take<float>(B * d->num_heads * d->lq * d->lk);
+    s.Pd = bp.take<float>(B * d->num_heads * d->lq * d->lk);
+  }
 }
 
-struct CmaWs { float *dO, *dsum, *dQ, *dK, *dV; };
+struct CmaWs { float *dO, *dsum, *dQ, *dK, *dV, *dS, *dPd; };
 
 void layout_cma_ws(const mmf_cma_desc* d, Bump& bp, CmaWs& w) {
   const size_t B = d->batch, H = d->hidden;
@@ -55,6 +64,11 @@ void layout_cma_ws(const mmf_cma_desc* d, Bump& bp, CmaWs& w) {
   w.dQ = sk ? nullptr : bp.take<float>(B * d->lq * H);
   w.dK = sk ? nullptr : bp.take<float>(B * d->lk * H);
   w.dV = bp.take<float>(B * d->lk * H);
+  w.dS = w.dPd = nullptr;
+  if (cma_wide(d)) {
+    w.dS = bp.take<float>(B * d->num_heads * d->lq * d->lk);
+    w.dPd = bp.take<float>(B * d->num_heads * d->lq * d->lk);
+  }
 }
 
 int check_cma(const mmf_cma_desc* d) {
@@ -67,10 +81,11 @@ int check_cma(const mmf_cma_desc* d) {
   if (d->num_heads < 1 || d->hidden % d->num_heads != 0)
     return fail(MMF_EINVAL, "hidden_dim (%d) must be divisible by num_heads (%d)", d->hidden,
                 d->num_heads);
-  if (d->hidden / d->num_heads > MMF_MAX_HEAD_DIM)
-    return fail(MMF_ELIMIT, "head_dim %d > %d is not supported by the HIP kernels",
-                d->hidden / d->num_heads, MMF_MAX_HEAD_DIM);
   if (d->mask_mode < 0 || d->mask_mode > 2) return fail(MMF_EINVAL, "bad mask_mode");
+  if (d->hidden % 4 != 0) return fail(MMF_ELIMIT, "hidden_dim must be a multiple of 4 (got %d)", d->hidden);
+  if (cma_wide(d) && !wide_supported(d->batch, d->num_heads, d->lq, d->lk))
+    return fail(MMF_ELIMIT, "head_dim %d: the (heads x Lq x Lk) score tensor is too large",
+                d->hidden / d->num_heads);
   if (!(d->dropout >= 0.f && d->dropout < 1.f)) return fail(MMF_EINVAL, "dropout must be in [0, 1)");
   return MMF_OK;
 }
@@ -89,6 +104,19 @@ AttnPair cma_pair(const mmf_cma_desc* d, const CmaSaved& s, const float* mask) {
   a.Lq = d->lq; a.Lk = d->lk;
   a.ldq = a.ldk = a.ldv = a.ldo = d->hidden;
   a.drop_site = SITE_ATTN;
+  return a;
+}
+
+WidePair cma_wide_pair(const mmf_cma_desc* d, const CmaSaved& s, const float* mask) {
+  WidePair a;
+  memset(&a, 0, sizeof(a));
+  a.q = s.Q; a.k = s.K; a.v = s.V;
+  a.ldq = a.ldk = a.ldv = a.ldo = d->hidden;
+  a.kmask = mask; a.kmask_mode = d->mask_mode; a.kmask_ld = d->mask_mode == 2 ? d->lk : 1;
+  a.Lq = d->lq; a.Lk = d->lk;
+  a.drop_site = SITE_ATTN;
+  a.P = s.P; a.Pd = s.Pd;
+  a.o = s.O;
   return a;
 }
 
@@ -334,6 +362,11 @@ int mmf_cma_forward(const mmf_cma_desc* d, const mmf_cma_params* W, const float*
       a.probs = attn_weights;
       STAGE_TRY("cma.fwd.attn_probs_single_key", launch_sk_fwd(&a, 1, B, d->num_heads, hd, p, rng, st));
     }
+  } else if (cma_wide(d)) {
+    WidePair a = cma_wide_pair(d, s, mask);
+    a.probs = attn_weights;
+    const float scale = 1.0f / std::sqrt((float)hd);
+    STAGE_TRY("cma.fwd.attn_wide", launch_wide_fwd(&a, 1, B, d->num_heads, hd, scale, p, rng, false, st));
   } else {
     AttnPair a = cma_pair(d, s, mask);
     a.probs = attn_weights;
@@ -395,6 +428,11 @@ int mmf_cma_backward(const mmf_cma_desc* d, const mmf_cma_params* W, const float
     // the query and the key reach the output only through the one-key softmax: zero gradient
     if (dquery) HIP_TRY(hipMemsetAsync(dquery, 0, (size_t)B * d->lq * d->query_dim * sizeof(float), st));
     if (dkey) HIP_TRY(hipMemsetAsync(dkey, 0, (size_t)B * d->lk * d->key_dim * sizeof(float), st));
+  } else if (cma_wide(d)) {
+    WidePair a = cma_wide_pair(d, s, mask);
+    a.dout = w.dO; a.dPd = w.dPd; a.dS = w.dS; a.dq = w.dQ; a.dk = w.dK; a.dv = w.dV;
+    const float scale = 1.0f / std::sqrt((float)hd);
+    STAGE_TRY("cma.bwd.attn_wide", launch_wide_bwd(&a, 1, B, d->num_heads, hd, scale, p, rng, false, st));
   } else {
     AttnPair a = cma_pair(d, s, mask);
     a.dout = w.dO; a.dsum = w.dsum; a.dq = w.dQ; a.dk = w.dK; a.dv = w.dV;

@@ -27,6 +27,11 @@ inline bool dropping(const mmf_hybrid_desc* d) { return d->training && d->dropou
 // length 1): softmax over one key is the mask indicator, so the pair has no Q / K /
 // QK^T work and its query_proj / key_proj gradients are exactly zero (single_key.hip).
 inline bool single_key(const mmf_hybrid_desc* d, int g) { return Lm(d, d->pair_k[g]) == 1; }
+// head_dim beyond the fused attention kernels' register budget (MMF_MAX_HEAD_DIM): the pair's
+// scores are materialised and contracted by GEMMs (wide.hip)
+inline bool wide_pair(const mmf_hybrid_desc* d, int g) {
+  return !single_key(d, g) && d->hidden / d->num_heads > MMF_MAX_HEAD_DIM;
+}
 
 // Pooled plan (attention.hip "Pooled-output attention"): keys up to 128 run the
 // one-chunk kernels, longer keys the streamed long-key kernels; the pooled
@@ -64,6 +69,7 @@ struct Saved {
   float *pbar[MMF_MAX_PAIRS], *U[MMF_MAX_PAIRS], *r[MMF_MAX_PAIRS], *Ob[MMF_MAX_PAIRS], *Ab[MMF_MAX_PAIRS];
   float* pbarT[MMF_MAX_PAIRS];   // (B, Lk, heads): pbar as the RK operand of the dZ GEMM's E_m term
   uint32_t* bits[MMF_MAX_PAIRS];
+  float *Pw[MMF_MAX_PAIRS], *Pdw[MMF_MAX_PAIRS];   // wide pairs: probabilities, post-dropout (general)
   float *pooled, *scores, *weights, *fused, *h1;
 };
 
@@ -78,11 +84,15 @@ void layout_saved(const mmf_hybrid_desc* d, Bump& bp, Saved& s) {
     if (pcol_in_proj(d, m)) s.Pcol[m] = bp.take<float>(B * (Lm(d, m) / 128) * H);
   for (int g = 0; g < d->num_pairs; ++g) {
     const size_t lq = Lm(d, d->pair_q[g]), lk = Lm(d, d->pair_k[g]);
-    const bool sk = single_key(d, g);
+    const bool sk = single_key(d, g), wide = wide_pair(d, g);
     if (!sk) {
       s.Q[g] = bp.take<float>(B * lq * H);
       s.K[g] = bp.take<float>(B * lk * H);
-      s.lse[g] = bp.take<float>(B * nh * lq);
+      if (!wide) s.lse[g] = bp.take<float>(B * nh * lq);
+    }
+    if (wide) {
+      s.Pw[g] = bp.take<float>(B * nh * lq * lk);
+      if (!pool) s.Pdw[g] = bp.take<float>(B * nh * lq * lk);
     }
     if (pool) {
       s.pbar[g] = bp.take<float>(B * nh * lk);
@@ -91,7 +101,7 @@ void layout_saved(const mmf_hybrid_desc* d, Bump& bp, Saved& s) {
       s.r[g] = bp.take<float>(B * nh);
       s.Ob[g] = bp.take<float>(B * H);
       s.Ab[g] = bp.take<float>(B * H);
-      if (dropping(d) && !sk) s.bits[g] = bp.take<uint32_t>(B * nh * lq * kw_ld((int)lk));
+      if (dropping(d) && !sk && !wide) s.bits[g] = bp.take<uint32_t>(B * nh * lq * kw_ld((int)lk));
     } else {
       s.V[g] = bp.take<float>(B * lk * H);
       s.O[g] = bp.take<float>(B * lq * H);
@@ -110,6 +120,7 @@ struct Ws {
   float *dQ[MMF_MAX_PAIRS], *dK[MMF_MAX_PAIRS], *dsum[MMF_MAX_PAIRS];
   float *dO[MMF_MAX_PAIRS], *dV[MMF_MAX_PAIRS];                              // general
   float *dOb[MMF_MAX_PAIRS], *dU[MMF_MAX_PAIRS], *dpbar[MMF_MAX_PAIRS];      // pooled
+  float *dS[MMF_MAX_PAIRS], *dPd[MMF_MAX_PAIRS];                             // wide pairs
   float* E[MMF_MAX_MODALITIES];                                              // pooled
   float* dZ[MMF_MAX_MODALITIES];
 };
@@ -128,6 +139,10 @@ void layout_ws(const mmf_hybrid_desc* d, Bump& bp, Ws& w) {
       w.dQ[g] = bp.take<float>(B * lq * H);
       w.dK[g] = bp.take<float>(B * lk * H);
       w.dsum[g] = bp.take<float>(B * nh * lq);
+    }
+    if (wide_pair(d, g)) {
+      w.dS[g] = bp.take<float>(B * nh * lq * lk);
+      if (!pool) w.dPd[g] = bp.take<float>(B * nh * lq * lk);
     }
     if (pool) {
       w.dOb[g] = bp.take<float>(B * H);
@@ -156,9 +171,6 @@ int check_hybrid(const mmf_hybrid_desc* d) {
   if (d->num_heads < 1 || d->hidden % d->num_heads != 0)
     return fail(MMF_EINVAL, "hidden_dim (%d) must be divisible by num_heads (%d)", d->hidden,
                 d->num_heads);
-  if (d->hidden / d->num_heads > MMF_MAX_HEAD_DIM)
-    return fail(MMF_ELIMIT, "head_dim %d > %d is not supported by the HIP kernels",
-                d->hidden / d->num_heads, MMF_MAX_HEAD_DIM);
   if (d->hidden % 4 != 0 || d->hidden > 1024)
     return fail(MMF_ELIMIT, "hidden_dim must be a multiple of 4 and <= 1024 (got %d)", d->hidden);
   if (d->num_classes < 1) return fail(MMF_EINVAL, "num_classes must be >= 1");
@@ -175,6 +187,10 @@ int check_hybrid(const mmf_hybrid_desc* d) {
   }
   if (!(d->dropout >= 0.f && d->dropout < 1.f))
     return fail(MMF_EINVAL, "dropout must be in [0, 1) (got %g)", (double)d->dropout);
+  for (int g = 0; g < d->num_pairs; ++g)
+    if (wide_pair(d, g) && !wide_supported(d->batch, d->num_heads, Lm(d, d->pair_q[g]), Lm(d, d->pair_k[g])))
+      return fail(MMF_ELIMIT, "head_dim %d: pair %d's (heads x Lq x Lk) score tensor is too large",
+                  d->hidden / d->num_heads, g);
   return MMF_OK;
 }
 
@@ -361,6 +377,21 @@ AttnPair make_pair(const mmf_hybrid_desc* d, const Saved& s, const float* mask, 
   return a;
 }
 
+WidePair make_wide(const mmf_hybrid_desc* d, const Saved& s, const float* mask, int g) {
+  WidePair a;
+  memset(&a, 0, sizeof(a));
+  const int q = d->pair_q[g], k = d->pair_k[g];
+  a.q = s.Q[g]; a.k = s.K[g]; a.v = s.V[g];
+  a.ldq = a.ldk = a.ldv = a.ldo = d->hidden;
+  a.kmask = mask + k; a.kmask_mode = 1; a.kmask_ld = d->num_modalities;
+  a.Lq = Lm(d, q); a.Lk = Lm(d, k);
+  a.drop_site = SITE_ATTN + g;
+  a.P = s.Pw[g]; a.Pd = s.Pdw[g];
+  a.pbar = s.pbar[g]; a.pbarT = s.pbarT[g];
+  a.o = s.O[g];
+  return a;
+}
+
 SkPair make_sk(const mmf_hybrid_desc* d, const Saved& s, const float* mask, int g) {
   SkPair a;
   memset(&a, 0, sizeof(a));
@@ -477,21 +508,27 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
   // pairs with several keys run the attention kernels; single-key pairs single_key.hip
   std::vector<AttnPair> pairs;
   std::vector<SkPair> skp;
+  std::vector<WidePair> wp;
   for (int g = 0; g < d->num_pairs; ++g) {
+    float* maps = d->return_attention && attn_maps ? attn_maps[g] : nullptr;
     if (single_key(d, g)) {
       skp.push_back(make_sk(d, s, mask, g));
-      if (d->return_attention && attn_maps) skp.back().probs = attn_maps[g];
+      skp.back().probs = maps;
+    } else if (wide_pair(d, g)) {
+      wp.push_back(make_wide(d, s, mask, g));
+      wp.back().probs = maps;   // written by the wide softmax itself
     } else {
       pairs.push_back(make_pair(d, s, mask, g));
-      if (d->return_attention && attn_maps) pairs.back().probs = attn_maps[g];
+      pairs.back().probs = maps;
     }
   }
-  const int nmp = (int)pairs.size(), nsk = (int)skp.size();
+  const int nmp = (int)pairs.size(), nsk = (int)skp.size(), nwp = (int)wp.size();
   const float scale = 1.0f / std::sqrt((float)hd);
   if (d->num_pairs && pool) {
     // (3p) attention -> LSE, pbar = mean_q P'; U = pbar P_k; Obar = U W_v^T + r b_v; Abar = out_proj
     if (nmp) STAGE_TRY("fwd.attn", launch_attn_pool_fwd(pairs.data(), nmp, B, nh, hd, scale, p, rng, st));
     if (nsk) STAGE_TRY("fwd.attn_single_key", launch_sk_fwd(skp.data(), nsk, B, nh, hd, p, rng, st));
+    if (nwp) STAGE_TRY("fwd.attn_wide", launch_wide_fwd(wp.data(), nwp, B, nh, hd, scale, p, rng, true, st));
     std::vector<PoolPair> pp(d->num_pairs);
     for (int g = 0; g < d->num_pairs; ++g) {
       memset(&pp[g], 0, sizeof(PoolPair));
@@ -536,6 +573,7 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
     // (3g) flash attention per pair (key mask = modality mask column k, fusion.py:391-401) + out_proj
     if (nmp) STAGE_TRY("fwd.attn", launch_attn_fwd(pairs.data(), nmp, B, nh, hd, scale, p, rng, st));
     if (nsk) STAGE_TRY("fwd.attn_single_key", launch_sk_out(skp.data(), nsk, B, nh, hd, p, rng, st));
+    if (nwp) STAGE_TRY("fwd.attn_wide", launch_wide_fwd(wp.data(), nwp, B, nh, hd, scale, p, rng, false, st));
     std::vector<GemmJob> jobs;
     for (int g = 0; g < d->num_pairs; ++g) {
       const int lq = Lm(d, d->pair_q[g]);
@@ -646,6 +684,7 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
   const float scale = 1.0f / std::sqrt((float)hd);
   std::vector<AttnPair> pairs;
   std::vector<SkPair> skp;
+  std::vector<WidePair> wpairs;
   for (int g = 0; g < d->num_pairs; ++g) {
     if (single_key(d, g)) {
       skp.push_back(make_sk(d, s, mask, g));
@@ -653,12 +692,19 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
       skp.back().dv = w.dV[g];
       continue;
     }
+    if (wide_pair(d, g)) {
+      wpairs.push_back(make_wide(d, s, mask, g));
+      WidePair& a = wpairs.back();
+      a.dpbar = w.dpbar[g]; a.dout = w.dO[g]; a.dPd = w.dPd[g]; a.dS = w.dS[g];
+      a.dq = w.dQ[g]; a.dk = w.dK[g]; a.dv = w.dV[g];
+      continue;
+    }
     pairs.push_back(make_pair(d, s, mask, g));
     AttnPair& a = pairs.back();
     a.dsum = w.dsum[g]; a.dq = w.dQ[g]; a.dk = w.dK[g];
     a.dout = w.dO[g]; a.dv = w.dV[g]; a.dpbar = w.dpbar[g];
   }
-  const int nmp = (int)pairs.size(), nsk = (int)skp.size();
+  const int nmp = (int)pairs.size(), nsk = (int)skp.size(), nwp = (int)wpairs.size();
   if (d->num_pairs && pool) {
     // (3p) dObar = dAbar W_o (dAbar = c_q); dU_h = dObar_h W_v,h; dpbar; attention dQ/dK; E_m
     if (!tail) {
@@ -709,6 +755,7 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
         HIP_TRY(fe);
       }
     }
+    if (nwp) STAGE_TRY("bwd.attn_wide", launch_wide_bwd(wpairs.data(), nwp, B, nh, hd, scale, p, rng, true, st));
     std::vector<PoolEMod> em;
     for (int m = 0; m < M; ++m) {
       if (poole_in_dz(d, m)) continue;   // E_m is formed in the dZ GEMM's epilogue instead
@@ -744,6 +791,7 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
       STAGE_TRY("bwd.attn_dq", launch_attn_bwd_stage(2, pairs.data(), nmp, B, nh, hd, scale, p, rng, st));
     }
     if (nsk) STAGE_TRY("bwd.attn_single_key_dv", launch_sk_dv(skp.data(), nsk, B, nh, hd, p, rng, st));
+    if (nwp) STAGE_TRY("bwd.attn_wide", launch_wide_bwd(wpairs.data(), nwp, B, nh, hd, scale, p, rng, false, st));
   }
   // (4) dZ_m = gate(P_m) * [direct + sum_q dQ W_q + sum_k dK W_k (+ dV W_v)]
   {

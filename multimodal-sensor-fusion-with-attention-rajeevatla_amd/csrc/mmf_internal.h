@@ -297,6 +297,36 @@ hipError_t launch_sk_dv(const SkPair* pairs, int npairs, int B, int heads, int h
                         const RngSnap* rng, hipStream_t st);
 
 // ---------------------------------------------------------------------------
+// Attention with head_dim > 64 (wide.hip): materialised scores, grouped strided-batch
+// GEMMs for QK^T / P'V / dO V^T / P'^T dO / dS K / dS^T Q and row kernels (softmax,
+// query means, softmax backward) between them.  Layout (B, heads, Lq, Lk) for P, P',
+// dP', dS.  kmask as AttnPair.
+// ---------------------------------------------------------------------------
+struct WidePair {
+  const float* q; const float* k; const float* v;
+  int32_t ldq, ldk, ldv;
+  const float* kmask; int32_t kmask_mode; int32_t kmask_ld;
+  int32_t Lq, Lk;
+  uint32_t drop_site;
+  float* P;            // scores, then softmax probabilities in place (fwd; kept for bwd)
+  float* Pd;           // post-dropout P' (general plan; kept for bwd)
+  float* probs;        // optional attention maps (post-dropout)
+  float* pbar; float* pbarT;   // pooled plan: (B, heads, Lk), (B, Lk, heads)
+  const float* dpbar;          // pooled plan bwd input
+  float* o; int32_t ldo;       // general plan: O (B, Lq, ldo)
+  const float* dout;           // general plan bwd: dO (B, Lq, ldo)
+  float* dPd;                  // general plan bwd scratch: dP'
+  float* dS;                   // bwd scratch
+  float* dq; float* dk; float* dv;
+};
+constexpr int WIDE_MAX_PAIRS = 16;
+bool wide_supported(int B, int heads, int Lq, int Lk);
+hipError_t launch_wide_fwd(const WidePair* pairs, int npairs, int B, int heads, int hd, float scale, float drop_p,
+                           const RngSnap* rng, bool pooled, hipStream_t st);
+hipError_t launch_wide_bwd(const WidePair* pairs, int npairs, int B, int heads, int hd, float scale, float drop_p,
+                           const RngSnap* rng, bool pooled, hipStream_t st);
+
+// ---------------------------------------------------------------------------
 // Pooled-output helpers (pool.hip), per (pair, sample):
 //   U[h] = pbar_h P_k      r[h] = sum_j pbar_h[j]            (forward)
 //   dpbar_h[j] = P_k[j] . dU[h] + dObar_h . bv_h             (backward)

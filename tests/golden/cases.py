@@ -202,6 +202,34 @@ HYBRID_CASES: List[HybridCase] = [
     HybridCase("seq_lean_hd64", ["a", "b"], {"a": 64, "b": 32},
                {"a": 64, "b": 96}, batch=2, hidden=128, heads=2, classes=4,
                seed=35, mask=[[1, 1], [1, 0]], full=False, attn_slice=7),
+    # The reference's heads ablation at hidden_dim 256 (num_heads in {1, 4, 8},
+    # .github/workflows/parallel_run.yml:79-97): num_heads 1 / 2 = head_dim 256 / 128, on the
+    # 2-D inputs src/train.py feeds HybridFusion (single-key attention) ...
+    HybridCase("heads1_l1", ["imu_hand", "imu_chest", "heart_rate"],
+               {"imu_hand": 128, "imu_chest": 128, "heart_rate": 128},
+               {"imu_hand": 0, "imu_chest": 0, "heart_rate": 0}, batch=6, hidden=256, heads=1, classes=25,
+               seed=36, mask=[[1, 1, 1], [1, 0, 1], [0, 0, 0], [0.5, 1, 0]], full=False),
+    HybridCase("heads2_l1", ["imu_hand", "imu_chest", "heart_rate"],
+               {"imu_hand": 128, "imu_chest": 128, "heart_rate": 128},
+               {"imu_hand": 0, "imu_chest": 0, "heart_rate": 0}, batch=6, hidden=256, heads=2, classes=25,
+               seed=37, mask=[[1, 1, 1], [0, 1, 1], [1, 1, 0]], full=False),
+    # ... and on sequences (materialised scores + GEMMs, csrc/wide.hip)
+    HybridCase("seq_wide_h2", ["a", "b"], {"a": 32, "b": 48},
+               {"a": 24, "b": 40}, batch=2, hidden=256, heads=2, classes=4,
+               seed=38, mask=[[1, 1], [1, 0]], full=False, attn_slice=5),
+    HybridCase("seq_wide_h1", ["a", "b", "c"], {"a": 16, "b": 24, "c": 8},
+               {"a": 12, "b": 20, "c": 9}, batch=2, hidden=256, heads=1, classes=5,
+               seed=39, mask=[[1, 1, 1], [0, 1, 0.5]], full=False, attn_slice=3),
+    # hidden 64 at L = 128: the projection GEMM's column-sum epilogue with N < 128 (threads
+    # past the last column still reach its barrier)
+    HybridCase("seq_h64_l128", ["a", "b"], {"a": 16, "b": 24},
+               {"a": 128, "b": 128}, batch=2, hidden=64, heads=4, classes=3,
+               seed=40, mask=[[1, 1], [1, 0.5]], full=False, attn_slice=11),
+    # hidden 256, keys <= 128, odd batch: the two-samples-per-workgroup pair tail with its
+    # padding slot
+    HybridCase("seq_h256_odd", ["a", "b"], {"a": 32, "b": 24},
+               {"a": 32, "b": 64}, batch=3, hidden=256, heads=4, classes=5,
+               seed=46, mask=[[1, 1], [0, 1], [1, 0.5]], full=False, attn_slice=13),
 ]
 
 CMA_CASES: List[CMACase] = [
@@ -213,6 +241,13 @@ CMA_CASES: List[CMACase] = [
             heads=4, seed=43),
     CMACase("cma_3d_long", batch=2, lq=160, lk=200, query_dim=32, key_dim=32, hidden=128,
             heads=4, seed=44, mask_kind="1d", mask_1d=[1, 0]),
+    # head_dim 128 / 256 (materialised scores, csrc/wide.hip)
+    CMACase("cma_3d_wide_hd128", batch=4, lq=20, lk=33, query_dim=24, key_dim=40, hidden=256,
+            heads=2, seed=47, mask_kind="2d"),
+    CMACase("cma_3d_wide_hd256", batch=2, lq=17, lk=12, query_dim=16, key_dim=16, hidden=256,
+            heads=1, seed=48, mask_kind="1d", mask_1d=[1, 0]),
+    CMACase("cma_2d_hd256", batch=4, lq=0, lk=0, query_dim=64, key_dim=32, hidden=256,
+            heads=1, seed=49, mask_kind="1d", mask_1d=[1, 0, 1, 1]),
 ]
 
 

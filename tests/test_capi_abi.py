@@ -89,9 +89,13 @@ def test_size_queries_and_validation(nat):
     bad = _desc(nat, num_heads=3)            # 32 % 3 != 0
     assert L.mmf_hybrid_saved_bytes(ctypes.byref(bad)) == 0
     assert b"divisible" in L.mmf_last_error()
-    big = _desc(nat, hidden=256, num_heads=2)  # head_dim 128 > 64
+    wide = _desc(nat, hidden=256, num_heads=2)  # head_dim 128 > 64: single-key / materialised-score plans
+    assert L.mmf_hybrid_saved_bytes(ctypes.byref(wide)) > 0
+    big = _desc(nat, hidden=256, num_heads=1)   # head_dim 256 at L = 50000: the score tensor's int32 strides
+    for m in range(3):
+        big.seq_len[m] = 50000
     assert L.mmf_hybrid_saved_bytes(ctypes.byref(big)) == 0
-    assert b"head_dim" in L.mmf_last_error()
+    assert b"head_dim" in L.mmf_last_error() and b"too large" in L.mmf_last_error()
     # forward refuses a bad descriptor before touching the device
     rc = L.mmf_hybrid_forward(ctypes.byref(bad), None, None, None, None, None, None, None, None, None)
     assert rc != 0

@@ -54,6 +54,18 @@ TRAIN_CASES = [
     HybridCase("train_general_wide", ["x", "y"], {"x": 16, "y": 8},
                {"x": 20, "y": 520}, batch=2, hidden=64, heads=8, classes=3, seed=56,
                mask=[[1, 1], [1, 0]]),
+    # head_dim 128, pooled plan, materialised scores (csrc/wide.hip)
+    HybridCase("train_wide_hd128", ["a", "b"], {"a": 16, "b": 24},
+               {"a": 24, "b": 40}, batch=2, hidden=128, heads=1, classes=4, seed=57,
+               mask=[[1, 1], [0.5, 1]]),
+    # head_dim 256 with heads x Lk = 4100 > POOL_PB_CAP: the general plan, materialised scores
+    HybridCase("train_general_hd256", ["x", "y"], {"x": 16, "y": 8},
+               {"x": 8, "y": 4100}, batch=1, hidden=256, heads=1, classes=3, seed=58,
+               mask=[[1, 1]]),
+    # hidden 256, keys <= 128, odd batch: the two-samples-per-workgroup pair tail
+    HybridCase("train_h256_odd", ["a", "b"], {"a": 32, "b": 24},
+               {"a": 32, "b": 64}, batch=3, hidden=256, heads=4, classes=5, seed=59,
+               mask=[[1, 1], [0, 1], [1, 0.5]]),
 ]
 
 
@@ -155,7 +167,10 @@ def test_long_key_plan_selection(mods):
     import mmf_native
     expect = {"train_long_hd64": ("attn_poolL_lse_kernel", "attn_poolL_colsum_kernel", "attn_poolL_dq_kernel",
                                   "attn_pool_bwd_dk_kernel"),
-              "train_general_wide": ("attn_fwd_kernel", "attn_bwd_dkv_kernel", "attn_bwd_dq_kernel")}
+              "train_general_wide": ("attn_fwd_kernel", "attn_bwd_dkv_kernel", "attn_bwd_dq_kernel"),
+              "train_wide_hd128": ("wide_softmax_kernel", "wide_colmean_kernel", "wide_dsoftmax_kernel"),
+              "train_general_hd256": ("wide_softmax_kernel", "wide_dsoftmax_kernel"),
+              "train_h256_odd": ("tail_pair_fwd_kernel",)}
     for case in TRAIN_CASES:
         if case.name not in expect:
             continue
