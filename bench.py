@@ -23,7 +23,8 @@ global batch.
 --path step (default): the fused training step (train_step.HybridTrainStep: flat buffers,
 one hipGraph per step).  --path module: what src/train.py calls -- the nn.Module forward,
 torch CrossEntropyLoss, autograd backward, eager, no graph -- timed the same way (diagnostic:
-the gap to the captured step).
+the gap to the captured step).  --path compiled: the same under the reference trainer's
+torch.compile(mode="reduce-overhead", fullgraph=True).
 Prints ONE JSON line on rank 0.
 """
 
@@ -114,7 +115,7 @@ def kernel_precision(kname):
     (the generic GEMM, the tail / head kernels) run fp32."""
     if kname.startswith("gemm_generic"):
         return 0
-    m = re.search(r"[<, ]([012])(?:, (?:true|false))?>$", kname)
+    m = re.search(r"[<, ]([012])(?:, (?:true|false)){0,2}>$", kname)
     return int(m.group(1)) if m else 0
 
 
@@ -196,14 +197,11 @@ def make_inputs(w, B, seed, device):
     return [f.to(device) for f in feats], mask.to(device), labels.to(device)
 
 
-def cpu_baseline(w, budget_s=12.0, max_steps=400):
-    """Time the oracle (torch-CPU restatement, oracle/hybrid_cpu.py) on a bounded sample."""
+def _cpu_leg(w, bs, threads, budget_s, max_steps):
+    """Oracle train steps (fwd + CE + bwd, dropout 0.1) at `threads` threads for ~budget_s."""
     from oracle.hybrid_cpu import hybrid_train_step
     from fusion import HybridFusion
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
     torch.set_num_threads(threads)
-    lmax = max(w["L"])
-    bs = 256 if lmax == 0 else (16 if lmax <= 128 else 2)
     torch.manual_seed(0)
     names = [f"m{i}" for i in range(w["M"])]
     model = HybridFusion({n: w["D"] for n in names}, hidden_dim=w["H"], num_classes=w["C"], num_heads=w["heads"],
@@ -214,16 +212,34 @@ def cpu_baseline(w, budget_s=12.0, max_steps=400):
     gen = torch.Generator().manual_seed(5)
     hybrid_train_step(params, names, feats, mask, labels, w["heads"], 0.1, gen)   # warm-up
     n, t0 = 0, time.perf_counter()
-    while n < max_steps and (time.perf_counter() - t0) < budget_s:
+    while n < max_steps and (n == 0 or (time.perf_counter() - t0) < budget_s):
         for p in list(params.values()) + list(feats.values()):
             p.grad = None
         hybrid_train_step(params, names, feats, mask, labels, w["heads"], 0.1, gen)
         n += 1
     dt = time.perf_counter() - t0
-    return {"value": round(bs * n / dt, 2), "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": f"{n} oracle steps of B={bs} (same per-sample work: M={w['M']}, L={w['L']}, "
-                      f"D={w['D']}, H={w['H']}, h={w['heads']}, fwd+CE+bwd, fp32, torch {torch.__version__} CPU), "
-                      f"{dt:.1f}s"}
+    return bs * n / dt, n, dt
+
+
+def cpu_baseline(w, budget_s=10.0, max_steps=400):
+    """The reference CPU path timed on this host's cores: the oracle (oracle/hybrid_cpu.py, a
+    torch-CPU restatement of src/fusion.py / src/attention.py) on the workload's per-GPU batch,
+    at every host thread and at 4 threads (the reference's own cap, src/train.py:446-447).  The
+    proxy is checked against the reference itself in scripts/cpu_proxy_check.py (same ATen ops,
+    within +-15 %: profiles/r03_cpu_proxy_check.json).  C5 (L = 512) is infeasible on a CPU at its
+    batch: B = 2 there, per-sample work identical (samples/s scale linearly in B)."""
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    lmax = max(w["L"])
+    bs = w["B"] if lmax <= 128 else 2
+    v_all, n_all, dt_all = _cpu_leg(w, bs, threads, budget_s, max_steps)
+    v_4, n_4, dt_4 = _cpu_leg(w, bs, min(4, threads), budget_s, max_steps)
+    torch.set_num_threads(threads)
+    return {"value": round(v_all, 2), "unit": "samples/s", "cores": threads, "kind": "port",
+            "value_4_threads": round(v_4, 2),
+            "sample": f"{n_all} oracle steps of B={bs} at {threads} threads ({dt_all:.1f}s) and {n_4} at 4 threads "
+                      f"({dt_4:.1f}s); per step the workload's fwd+CE+bwd (M={w['M']}, L={w['L']}, D={w['D']}, "
+                      f"H={w['H']}, h={w['heads']}, dropout 0.1, fp32, torch {torch.__version__} CPU); proxy "
+                      f"validated against the reference within 15% (scripts/cpu_proxy_check.py)"}
 
 
 class ModuleRunner:
@@ -232,9 +248,12 @@ class ModuleRunner:
     grads), then the exchange + clip + AdamW of harness.DPTrainer (flat buffers, bucketed
     all-reduce).  Eager; no graph."""
 
-    def __init__(self, model, feats, mask, labels, pg):
+    def __init__(self, model, feats, mask, labels, pg, compiled=False):
         from harness import DPTrainer
         self.model = model.train()
+        # --path compiled: the reference trainer's torch.compile(mode="reduce-overhead")
+        # (src/train.py:193-231) around the module; the optimizer step stays outside
+        self.fwd = torch.compile(model, mode="reduce-overhead", fullgraph=True) if compiled else model
         self.names = list(model.modality_names)
         self.feats = [f.clone().requires_grad_(True) for f in feats]
         self.mask, self.labels = mask, labels
@@ -246,7 +265,7 @@ class ModuleRunner:
             f.grad = None
         feats = dict(zip(self.names, self.feats))
         self.trainer.flat.arm()
-        logits = self.model(feats, self.mask)
+        logits = self.fwd(feats, self.mask)
         loss = torch.nn.functional.cross_entropy(logits, self.labels, label_smoothing=0.05)
         loss.backward()
         self.loss = loss.detach()
@@ -264,7 +283,7 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
-    ap.add_argument("--path", default="step", choices=["step", "module"])
+    ap.add_argument("--path", default="step", choices=["step", "module", "compiled"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--dropout", type=float, default=0.1,
                     help="diagnostics only: the benchmark workload is dropout 0.1")
@@ -323,8 +342,8 @@ def main(argv=None):
         feats, mask, labels = [f.to(dev) for f in feats], mask.to(dev), labels.to(dev)
     else:
         feats, mask, labels = make_inputs(w, B, 42 + rank, dev)
-    if args.path == "module":
-        trainer = ModuleRunner(model, feats, mask, labels, pg)
+    if args.path in ("module", "compiled"):
+        trainer = ModuleRunner(model, feats, mask, labels, pg, compiled=args.path == "compiled")
     else:
         trainer = HybridTrainStep(model, feats, mask, labels, process_group=pg)
 
@@ -392,7 +411,10 @@ def main(argv=None):
         mask_note = "" if w["keep"] >= 1 else f", modality masks keep={w['keep']} (+1% all-masked rows)"
         path_note = ("fused step (flat buffers, one hipGraph)" if graph else
                      "fused step, eager" if args.path == "step" else
-                     "nn.Module forward + autograd backward, eager (src/train.py's call path)")
+                     "nn.Module forward + autograd backward, eager (src/train.py's call path)"
+                     if args.path == "module" else
+                     "torch.compile(module, mode='reduce-overhead', fullgraph=True) forward + backward "
+                     "(src/train.py's compiled call path)")
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),

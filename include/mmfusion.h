@@ -39,6 +39,9 @@ extern "C" {
 
 #define MMF_MAX_MODALITIES 8
 #define MMF_MAX_PAIRS (MMF_MAX_MODALITIES * (MMF_MAX_MODALITIES - 1))
+/* head_dim (hidden / num_heads) the fused attention kernels hold in registers; beyond it
+ * (up to hidden) a pair's scores are materialised and contracted by MFMA GEMMs (csrc/wide.hip).
+ * Pairs with ONE key (2-D inputs) have no Q / K work at all and any head_dim. */
 #define MMF_MAX_HEAD_DIM 64
 
 enum {
@@ -85,8 +88,10 @@ typedef struct mmf_hybrid_desc {
   int32_t return_attention; /* write attention maps */
   /* torch.get_float32_matmul_precision() of the caller (config/base.yaml:80
    * training.matmul_precision, applied at src/train.py:53-68,448):
-   * MMF_PRECISION_HIGHEST = fp32 MFMA; MMF_PRECISION_MEDIUM = bf16 MFMA operands
-   * with fp32 accumulation (storage, softmax and reductions stay fp32). */
+   * MMF_PRECISION_HIGHEST = fp32 MFMA; MMF_PRECISION_HIGH = bf16x3 (each fp32
+   * operand split into bf16 hi + lo, three bf16 MFMAs, fp32 accumulate);
+   * MMF_PRECISION_MEDIUM = bf16 MFMA operands with fp32 accumulation (storage,
+   * softmax and reductions stay fp32 in every mode). */
   int32_t matmul_precision;
 } mmf_hybrid_desc;
 
@@ -153,7 +158,8 @@ int mmf_adaptive_weights_backward(int32_t batch, int32_t num_modalities, int32_t
 
 /* ---------------------------------------------------------------------
  * CrossModalAttention (src/attention.py:16-146), standalone.
- * lq/lk: sequence lengths (use 1 for the reference's 2-D inputs).
+ * lq/lk: sequence lengths (use 1 for the reference's 2-D inputs; lk == 1 runs the
+ * single-key plan: no Q / K work, exact-zero query / key gradients).
  * mask_mode: 0 none, 1 per-sample (B,) (src/attention.py:120-121),
  *            2 per-key (B, Lk).
  * ------------------------------------------------------------------- */

@@ -11,7 +11,9 @@ query_proj, key_proj, value_proj, out_proj, dropout, scale), state_dict keys
 and forward(query, key, value, mask=None) -> (attended, attn_weights).
 
 Compute path: include/mmfusion.h mmf_cma_forward / mmf_cma_backward
-(libmmfusion.so, gfx950).  There is no CPU path: CPU tensors raise.
+(libmmfusion.so, gfx950), reached as torch.ops.mmfusion.cma_fwd / cma_bwd
+(mmf_ops.py custom ops: traceable by torch.compile without a graph break).
+There is no CPU path: CPU tensors raise.
 Differences from the reference, by design:
   * the returned attention weights are not differentiable (the reference's
     are; nothing in train/eval back-propagates through them);
@@ -33,6 +35,15 @@ if _HERE not in sys.path:
     sys.path.insert(0, _HERE)
 
 import mmf_native as _nat  # noqa: E402
+import mmf_ops as _ops  # noqa: E402
+
+
+@torch._dynamo.assume_constant_result
+def _precision() -> int:
+    """torch.get_float32_matmul_precision() as the C-ABI enum (mmf_native.matmul_precision), a
+    constant of a compiled graph: like the matmuls inductor emits, a traced call keeps the
+    precision that was set when it was traced."""
+    return _nat.matmul_precision()
 
 
 _RNG_COUNTER = [0]
@@ -51,71 +62,6 @@ def _new_rng_state() -> torch.Tensor:
     x = (x * 0x94D049BB133111EB) & (2**64 - 1)
     x ^= x >> 29
     return torch.tensor([x & (2**63 - 1), 0], dtype=torch.int64)
-
-
-class _CMAFunction(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, desc: "_nat.CmaDesc", mask, rng, query, key, value, qw, qb, kw, kb, vw, vb, ow, ob):
-        L = _nat.lib()
-        dev = query.device
-        B, lq, lk, H, h = desc.batch, desc.lq, desc.lk, desc.hidden, desc.num_heads
-        saved = torch.empty(L.mmf_cma_saved_bytes(ctypes_ref(desc)), dtype=torch.uint8, device=dev)
-        attended = torch.empty(B, lq, H, dtype=torch.float32, device=dev)
-        attn = torch.empty(B, h, lq, lk, dtype=torch.float32, device=dev)
-        params = _nat.CmaParams()
-        for name, (w, b) in zip(("q", "k", "v", "o"), ((qw, qb), (kw, kb), (vw, vb), (ow, ob))):
-            setattr(params, name, _nat.Linear(w.data_ptr(), b.data_ptr()))
-        rc = L.mmf_cma_forward(ctypes_ref(desc), ctypes_ref(params), query.data_ptr(), key.data_ptr(),
-                               value.data_ptr(), _nat.ptr(mask), rng.data_ptr(), saved.data_ptr(),
-                               attended.data_ptr(), attn.data_ptr(), _nat.stream_ptr(dev))
-        _nat.check(rc, "CrossModalAttention forward")
-        ctx.desc = desc
-        ctx.saved_buf = saved
-        ctx.save_for_backward(mask if mask is not None else torch.empty(0, device=dev), query, key,
-                              value, qw, qb, kw, kb, vw, vb, ow, ob)
-        ctx.has_mask = mask is not None
-        ctx.mark_non_differentiable(attn)
-        return attended, attn
-
-    @staticmethod
-    def backward(ctx, d_att, _d_attn):
-        L = _nat.lib()
-        mask, query, key, value, qw, qb, kw, kb, vw, vb, ow, ob = ctx.saved_tensors
-        mask = mask if ctx.has_mask else None
-        desc = ctx.desc
-        dev = query.device
-        d_att = _nat.f32c(d_att)
-        ws = torch.empty(L.mmf_cma_workspace_bytes(ctypes_ref(desc)), dtype=torch.uint8, device=dev)
-        params = _nat.CmaParams()
-        grads = _nat.CmaGrads()
-        plist = ((qw, qb), (kw, kb), (vw, vb), (ow, ob))
-        sizes = [w.numel() + b.numel() for w, b in plist]
-        flat = torch.empty(sum(sizes), dtype=torch.float32, device=dev)
-        gviews = []
-        off = 0
-        for name, (w, b) in zip(("q", "k", "v", "o"), plist):
-            gw = flat[off:off + w.numel()].view_as(w)
-            off += w.numel()
-            gb = flat[off:off + b.numel()].view_as(b)
-            off += b.numel()
-            gviews += [gw, gb]
-            setattr(params, name, _nat.Linear(w.data_ptr(), b.data_ptr()))
-            setattr(grads, name, _nat.Linear(gw.data_ptr(), gb.data_ptr()))
-        nq, nk, nv = ctx.needs_input_grad[3:6]
-        dq = torch.empty_like(query) if nq else None
-        dk = torch.empty_like(key) if nk else None
-        dv = torch.empty_like(value) if nv else None
-        rc = L.mmf_cma_backward(ctypes_ref(desc), ctypes_ref(params), query.data_ptr(), key.data_ptr(),
-                                value.data_ptr(), _nat.ptr(mask), ctx.saved_buf.data_ptr(),
-                                d_att.data_ptr(), ws.data_ptr(), ctypes_ref(grads), _nat.ptr(dq),
-                                _nat.ptr(dk), _nat.ptr(dv), _nat.stream_ptr(dev))
-        _nat.check(rc, "CrossModalAttention backward")
-        return (None, None, None, dq, dk, dv, *gviews)
-
-
-def ctypes_ref(s):
-    import ctypes
-    return ctypes.byref(s)
 
 
 class CrossModalAttention(nn.Module):
@@ -150,7 +96,6 @@ class CrossModalAttention(nn.Module):
         cast_self.scale = head_dim ** -0.5
         self.register_buffer("_rng_state", _new_rng_state(), persistent=False)
 
-    @torch.compiler.disable  # HIP library calls: opaque to TorchDynamo (runs eagerly)
     def forward(self, query: torch.Tensor, key: torch.Tensor, value: torch.Tensor,
                 mask: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
         """src/attention.py:68-146: (B,Dq)/(B,Lq,Dq) x (B,Dk)/(B,Lk,Dk) -> (attended, weights)."""
@@ -183,13 +128,14 @@ class CrossModalAttention(nn.Module):
             else:
                 raise RuntimeError(f"mask of shape {tuple(m.shape)} does not broadcast to (B, Lk)")
             m = m.contiguous()
-        desc = _nat.CmaDesc(B, lq, lk, self.query_proj.in_features, self.key_proj.in_features,
-                            self.hidden_dim, self.num_heads, mask_mode, float(self.dropout.p),
-                            int(self.training), _nat.matmul_precision())
-        attended, attn = _CMAFunction.apply(
-            desc, m, self._rng_state, _nat.f32c(q3), _nat.f32c(k3), _nat.f32c(v3),
-            self.query_proj.weight, self.query_proj.bias, self.key_proj.weight, self.key_proj.bias,
-            self.value_proj.weight, self.value_proj.bias, self.out_proj.weight, self.out_proj.bias)
+        idesc = [B, lq, lk, self.query_proj.in_features, self.key_proj.in_features, self.hidden_dim,
+                 self.num_heads, mask_mode, int(self.training), _precision()]
+        attended, attn, _saved, rng_next = torch.ops.mmfusion.cma_fwd(
+            idesc, float(self.dropout.p), self._rng_state, _nat.f32c(q3), _nat.f32c(k3), _nat.f32c(v3), m,
+            [self.query_proj.weight, self.query_proj.bias, self.key_proj.weight, self.key_proj.bias,
+             self.value_proj.weight, self.value_proj.bias, self.out_proj.weight, self.out_proj.bias])
+        self._rng_state.copy_(rng_next)     # the device Philox stream advanced by one call
+        attn = attn.detach()
         if squeeze_q:
             attended = attended.squeeze(1)
         if squeeze_k:
@@ -214,7 +160,6 @@ class TemporalAttention(CrossModalAttention):
         super().__init__(feature_dim, feature_dim, hidden_dim=hidden_dim, num_heads=num_heads, dropout=dropout)
         cast(Any, self).feature_dim = feature_dim
 
-    @torch.compiler.disable  # HIP library calls: opaque to TorchDynamo (runs eagerly)
     def forward(self, sequence: torch.Tensor,  # type: ignore[override]
                 mask: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
         if sequence.dim() != 3:
@@ -271,7 +216,6 @@ class PairwiseModalityAttention(nn.Module):
                                                dropout=dropout)
             for q in dims for k in dims if q != k})
 
-    @torch.compiler.disable  # HIP library calls: opaque to TorchDynamo (runs eagerly)
     def forward(self, modality_features, modality_mask: Optional[torch.Tensor] = None):
         if not self.modality_names:
             raise ValueError("No modalities provided for PairwiseModalityAttention.")

@@ -1291,7 +1291,7 @@ __device__ __forceinline__ void lean_keep_words(uint32_t (&words)[NKT], const Rn
 
 // DROP (train mode with p > 0, launch-time choice): the loop body has no dropout
 // branches.
-template <int HDP, int BF, bool DROP = true>
+template <int HDP, int BF, bool DROP = true, bool PST = false>
 __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(const AttnArgs A) {
   constexpr int LS = HDP + 4;
   constexpr int HALF = HDP / 2;
@@ -1404,14 +1404,40 @@ __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(cons
     }
     l = sum_xor32(l);
     FSTAMP(3)
-    const float f = qvalid ? (pdrop > 0.f ? inv_keep : 1.f) / l : 0.f;
+    if constexpr (PST) {
+      // P = e / l kept for the backward (fire-and-forget 1-KB wave stores in register order);
+      // P' = keep ? P / (1 - p) : 0 into the column sums
+      const float f = qvalid ? 1.f / l : 0.f;
+      float* pst = P.pstore + ((bh * ((Lq + 31) / 32) + qt) * 4) * 1024 + lane * 4;
 #pragma unroll
-    for (int kt = 0; kt < NKT; ++kt) {
-      if (kt < nkt) {
-        const uint32_t wk = words[kt] >> (4 * h);   // reg r = 4g + j <-> key bit 8g + 4h + j
+      for (int kt = 0; kt < NKT; ++kt) {
+        if (kt < nkt) {
+          const uint32_t wk = words[kt] >> (4 * h);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sv[kt][r] = ((wk >> (8 * (r >> 2) + (r & 3))) & 1u) ? sv[kt][r] * f : 0.f;
-        colacc[kt] += colsum_tile(sv[kt], c);
+          for (int g = 0; g < 4; ++g) {
+            float pv[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) pv[j] = sv[kt][4 * g + j] * f;
+            *reinterpret_cast<float4*>(pst + kt * 1024 + g * 256) = make_float4(pv[0], pv[1], pv[2], pv[3]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int r = 4 * g + j;
+              sv[kt][r] = (!DROP || ((wk >> (8 * g + j)) & 1u)) ? (DROP ? pv[j] * inv_keep : pv[j]) : 0.f;
+            }
+          }
+          colacc[kt] += colsum_tile(sv[kt], c);
+        }
+      }
+    } else {
+      const float f = qvalid ? (pdrop > 0.f ? inv_keep : 1.f) / l : 0.f;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+        if (kt < nkt) {
+          const uint32_t wk = words[kt] >> (4 * h);   // reg r = 4g + j <-> key bit 8g + 4h + j
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sv[kt][r] = ((wk >> (8 * (r >> 2) + (r & 3))) & 1u) ? sv[kt][r] * f : 0.f;
+          colacc[kt] += colsum_tile(sv[kt], c);
+        }
       }
     }
     if (qvalid && h == 0) {
@@ -1666,7 +1692,7 @@ MMF_CHAIN16(dk[dt], ds[r], Qs[(qt * 32 + acc_row(r, h)) * LS + dt * 32 + c])
 // memory, issued at once into registers (one round trip instead of one per
 // image / side array): the K and Q head slices, dpbar, LSE, the keep words and
 // the sample's modality mask.
-template <int HDP>
+template <int HDP, bool PST = false>
 struct FusedLoads {
   static constexpr int PER = PKC * (HDP / 4) / NT;   // float4 slots per thread and image
   float4 k[PER], q[PER];
@@ -1674,9 +1700,9 @@ struct FusedLoads {
   uint4 kw;
 };
 
-template <int HDP>
+template <int HDP, bool PST>
 __device__ __forceinline__ void fused_issue_loads(const AttnArgs& A, const AttnPair& P, int b, int head, int c,
-                                                  FusedLoads<HDP>& L) {
+                                                  FusedLoads<HDP, PST>& L) {
   constexpr int C4 = HDP / 4;
   const int t = threadIdx.x, w = t >> 6;
   const int hd = A.hd, col0 = head * hd;
@@ -1684,7 +1710,7 @@ __device__ __forceinline__ void fused_issue_loads(const AttnArgs& A, const AttnP
   const float* kb = P.k + (int64_t)b * Lk * P.ldk + col0;
   const float* qb = P.q + (int64_t)b * Lq * P.ldq + col0;
 #pragma unroll
-  for (int i = 0; i < FusedLoads<HDP>::PER; ++i) {
+  for (int i = 0; i < FusedLoads<HDP, PST>::PER; ++i) {
     const int idx = t + i * NT;
     const int r = idx / C4, c4 = (idx % C4) * 4;
     L.k[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1708,9 +1734,9 @@ __device__ __forceinline__ void fused_issue_loads(const AttnArgs& A, const AttnP
 // One (pair, sample, head) item of the fused lean backward from its issued loads;
 // Ks / Qs are [PKC][HDP + 4] LDS images (Ks doubles as the dS^T quarter image),
 // gk [PKC].  Called by every thread of the workgroup (it holds barriers).
-template <int HDP, int BF>
+template <int HDP, int BF, bool PST = false>
 __device__ __forceinline__ void fused_lean_item(const AttnArgs& A, const AttnPair& P, int b, int head, float* Ks,
-                                                float* Qs, float* gk, int h, int c, const FusedLoads<HDP>& LD) {
+                                                float* Qs, float* gk, int h, int c, const FusedLoads<HDP, PST>& LD) {
   constexpr int LS = HDP + 4;
   constexpr int HALF = HDP / 2;
   constexpr int NDT = HDP / 32;
@@ -1743,7 +1769,7 @@ __device__ __forceinline__ void fused_lean_item(const AttnArgs& A, const AttnPai
     return;
   }
 #pragma unroll
-  for (int i = 0; i < FusedLoads<HDP>::PER; ++i) {
+  for (int i = 0; i < FusedLoads<HDP, PST>::PER; ++i) {
     const int idx = t + i * NT;
     const int off = (idx / C4) * LS + (idx % C4) * 4;
     *reinterpret_cast<float4*>(&Ks[off]) = LD.k[i];
@@ -1751,41 +1777,85 @@ __device__ __forceinline__ void fused_lean_item(const AttnArgs& A, const AttnPai
   }
   if (t < PKC) gk[t] = LD.gk;
   const float lse2 = (!qvalid || LD.lse == -INFINITY) ? INFINITY : LD.lse * LOG2E;
-  const uint32_t kwa[4] = {LD.kw.x, LD.kw.y, LD.kw.z, LD.kw.w};
+  // keep words shifted to this lane half once: the per-element tests are constant-offset bit
+  // extracts (a variable shift made the compiler keep 16 precomputed masks live)
+  uint32_t kwh[4] = {LD.kw.x >> (4 * h), LD.kw.y >> (4 * h), LD.kw.z >> (4 * h), LD.kw.w >> (4 * h)};
   (void)pdrop;
+  float pr[NKT][16];
+  float4 pld[PST ? 16 : 1];
+  if constexpr (PST) {
+    // this wave's query tile of the forward's stored P: 16 x 1-KB wave loads, issued once the
+    // K / Q image registers are free (before the barrier; the scheduler barrier keeps them there)
+    __builtin_amdgcn_sched_barrier(0);
+    const float* pst = P.pstore + (((int64_t)b * A.heads + head) * ((Lq + 31) / 32) + w) * 4096 + (t & 63) * 4;
+    // (unconditional: the blob reserves 4 key tiles per query tile; tiles past nkt are read
+    // and discarded below -- a guarded load per slot made the compiler branch and drain vmcnt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) pld[i] = *reinterpret_cast<const float4*>(pst + (i >> 2) * 1024 + (i & 3) * 256);
+  }
   __syncthreads();
   BSTAMP(1)
 
-  float qf[HALF];
-  load_frag_vec<HALF>(qf, Qs + q * LS + h * HALF);
-  const float c2 = scale * LOG2E;
-  float pr[NKT][16];
   float D = 0.f;
-  f32x16 s_nx = dot_rows<HALF, BF>(Ks + c * LS + h * HALF, qf, zero16());
+  if constexpr (PST) {
+    // P from the forward (no S recompute); invalid query lanes hold 0
+    (void)lse2;
 #pragma unroll
-  for (int kt = 0; kt < NKT; ++kt) {
-    if (kt < nkt) {
-      const f32x16 s = s_nx;
-      if (kt + 1 < nkt) s_nx = dot_rows<HALF, BF>(Ks + ((kt + 1) * 32 + c) * LS + h * HALF, qf, zero16());
+    for (int kt = 0; kt < NKT; ++kt) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
+        const float4 pv = pld[kt * 4 + g];
         const float4 gv = *reinterpret_cast<const float4*>(gk + kt * 32 + 8 * g + 4 * h);
+        const float pp[4] = {pv.x, pv.y, pv.z, pv.w};
         const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int r = 4 * g + j;
-          const float p = fast_exp2(fmaf(s[r], c2, -lse2));
-          pr[kt][r] = p;
-          const bool keep = (kwa[kt] >> (8 * g + 4 * h + j)) & 1u;
+          const float p = kt < nkt ? pp[j] : 0.f;
+          pr[kt][4 * g + j] = p;
+          const bool keep = (kwh[kt] >> (8 * g + j)) & 1u;
           D += keep ? p * gg[j] : 0.f;
         }
       }
-    } else {
+    }
+  } else {
+    float qf[HALF];
+    load_frag_vec<HALF>(qf, Qs + q * LS + h * HALF);
+    const float c2 = scale * LOG2E;
+    f32x16 s_nx = dot_rows<HALF, BF>(Ks + c * LS + h * HALF, qf, zero16());
 #pragma unroll
-      for (int r = 0; r < 16; ++r) pr[kt][r] = 0.f;
+    for (int kt = 0; kt < NKT; ++kt) {
+      if (kt < nkt) {
+        const f32x16 s = s_nx;
+        if (kt + 1 < nkt) s_nx = dot_rows<HALF, BF>(Ks + ((kt + 1) * 32 + c) * LS + h * HALF, qf, zero16());
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 gv = *reinterpret_cast<const float4*>(gk + kt * 32 + 8 * g + 4 * h);
+          const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int r = 4 * g + j;
+            const float p = fast_exp2(fmaf(s[r], c2, -lse2));
+            pr[kt][r] = p;
+            const bool keep = (kwh[kt] >> (8 * g + j)) & 1u;
+            D += keep ? p * gg[j] : 0.f;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) pr[kt][r] = 0.f;
+      }
     }
   }
   D = sum_xor32(D);
+  // the dQ chains' K-image reads stay below (hoisted above the D loop they held 64 more
+  // registers alive across it and spilled), and the keep tests are redone below rather than
+  // kept from the D loop (64 lane masks = 128 SGPRs, spilled); the empty asm makes the
+  // compiler treat the words as new values
+  if constexpr (PST) {
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) asm volatile("" : "+v"(kwh[kt]));
+  }
   BSTAMP(2)
   BSTAMP(3)
   // dQ = scale dS K (query on the lane; dS is the B operand); dS = P . (G - D) is formed
@@ -1804,7 +1874,7 @@ __device__ __forceinline__ void fused_lean_item(const AttnArgs& A, const AttnPai
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int r = 4 * g + j;
-            const bool keep = (kwa[kt] >> (8 * g + 4 * h + j)) & 1u;
+            const bool keep = (kwh[kt] >> (8 * g + j)) & 1u;
             pr[kt][r] = pr[kt][r] * ((keep ? gg[j] : 0.f) - D);
           }
         }
@@ -1877,7 +1947,7 @@ MMF_CHAIN16(dq[dt], Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], pr[kt][r])
   BSTAMP_RT(8)
 }
 
-template <int HDP, int BF>
+template <int HDP, int BF, bool PST = false>
 __global__ __launch_bounds__(NT, 4) void attn_pool_bwd_fused_lean(const AttnArgs A) {
   __shared__ __attribute__((aligned(16))) float Ks[PKC * (HDP + 4)];   // K, then the dS^T quarters
   __shared__ __attribute__((aligned(16))) float Qs[PKC * (HDP + 4)];
@@ -1886,9 +1956,9 @@ __global__ __launch_bounds__(NT, 4) void attn_pool_bwd_fused_lean(const AttnArgs
   if (bid >= A.B * A.heads) return;
   const int lane = threadIdx.x & 63;
   const AttnPair& P = A.p[blockIdx.y];
-  FusedLoads<HDP> LD;
-  fused_issue_loads<HDP>(A, P, bid / A.heads, bid % A.heads, lane & 31, LD);
-  fused_lean_item<HDP, BF>(A, P, bid / A.heads, bid % A.heads, Ks, Qs, gk, lane >> 5, lane & 31, LD);
+  FusedLoads<HDP, PST> LD;
+  fused_issue_loads<HDP, PST>(A, P, bid / A.heads, bid % A.heads, lane & 31, LD);
+  fused_lean_item<HDP, BF, PST>(A, P, bid / A.heads, bid % A.heads, Ks, Qs, gk, lane >> 5, lane & 31, LD);
 }
 
 // "name<a, b>" -> "name<a, b, ARG>" ("name<>" -> "name<ARG>"): the rocprof name of an
@@ -1939,6 +2009,13 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
       lean = pairs[i].Lq <= 128 && (pairs[i].ldq % 4 == 0) && (((uintptr_t)pairs[i].dq & 15) == 0);
     if (!lean) return hipErrorNotSupported;
   }
+  // stored probabilities (every pair of the launch has them, or none): the lean forward writes,
+  // the fused backward reads P instead of recomputing S
+  int npst = 0;
+  for (int i = 0; i < npairs; ++i) npst += pairs[i].pstore != nullptr;
+  if (npst != 0 && (npst != npairs || !lean || (kind != Kind::PoolFwd && kind != Kind::PoolFused)))
+    return hipErrorInvalidValue;
+  const bool pst = npst != 0;
   int done = 0;
   while (done < npairs) {
     AttnArgs a;
@@ -1991,10 +2068,14 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
         case Kind::Prep: fl += 2.0 * bq; by += 4 * 2 * bq; break;                         // dO, O -> D
         case Kind::Dkv: fl += 3 * qk; by += 4 * (3 * bq + 4 * bk); break;               // Q K V dO -> dK dV
         case Kind::Dq: fl += qk; by += 4 * (3 * bq + 2 * bk); break;                    // Q K V dO -> dQ
-        case Kind::PoolFwd: fl += qk; by += 4 * (bq + bk); break;                         // Q K -> lse, pbar
+        case Kind::PoolFwd:                                                               // Q K -> lse, pbar (P)
+          fl += qk; by += 4 * (bq + bk + (pst ? (double)B * heads * attn_pstore_floats((int)lq) : 0.0));
+          break;
         case Kind::PoolDq: fl += qk; by += 4 * (2 * bq + bk); break;                      // Q K -> dQ
         case Kind::PoolDk: fl += qk; by += 4 * (bq + 2 * bk); break;                      // Q K -> dK
-        case Kind::PoolFused: fl += 2 * qk; by += 4 * (2 * bq + 2 * bk); break;           // Q K -> dQ dK
+        case Kind::PoolFused:                                                             // Q K (P) -> dQ dK
+          fl += 2 * qk; by += 4 * (2 * bq + 2 * bk + (pst ? (double)B * heads * attn_pstore_floats((int)lq) : 0.0));
+          break;
         case Kind::PoolLse: fl += qk; by += 4 * (bq + bk); break;                         // Q K -> lse
         case Kind::PoolColsum: by += 4 * (bq + bk); break;                                // (S recomputed) -> pbar
         case Kind::PoolDqLong: fl += qk; by += 4 * (2 * bq + bk); break;                  // Q K -> dQ
@@ -2029,6 +2110,8 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
     const char* pname = with_arg(kname, pr == 2 ? "2" : (pr == 1 ? "1" : "0"));
     if (long_lean) pname = with_arg(pname, "true");   // "<hd, pr, true>": the LEAN instantiation
     if (kind == Kind::PoolFwd && lean) pname = with_arg(pname, a.drop_p > 0.f ? "true" : "false");   // DROP
+    if (kind == Kind::PoolFwd && lean) pname = with_arg(pname, pst ? "true" : "false");              // PST
+    if (kind == Kind::PoolFused) pname = with_arg(pname, pst ? "true" : "false");                    // PST
     ProfLaunch prof_(st, pname, fl, by);
     switch (kind) {
       case Kind::PoolLse:
@@ -2074,7 +2157,13 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
         else { MMF_PR_LAUNCH(attn_bwd_dq_kernel<64, PRV>) }
         break;
       case Kind::PoolFwd:
-        if (lean && a.drop_p > 0.f) {
+        if (lean && pst && a.drop_p > 0.f) {
+          if (small) { MMF_PR_LAUNCH(attn_pool_fwd_lean<32, PRV, true, true>) }
+          else { MMF_PR_LAUNCH(attn_pool_fwd_lean<64, PRV, true, true>) }
+        } else if (lean && pst) {
+          if (small) { MMF_PR_LAUNCH(attn_pool_fwd_lean<32, PRV, false, true>) }
+          else { MMF_PR_LAUNCH(attn_pool_fwd_lean<64, PRV, false, true>) }
+        } else if (lean && a.drop_p > 0.f) {
           if (small) { MMF_PR_LAUNCH(attn_pool_fwd_lean<32, PRV, true>) }
           else { MMF_PR_LAUNCH(attn_pool_fwd_lean<64, PRV, true>) }
         } else if (lean) {
@@ -2091,8 +2180,13 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
         else { MMF_PR_LAUNCH(attn_pool_bwd_dq_kernel<64, PRV>) }
         break;
       case Kind::PoolFused:
-        if (small) { MMF_PR_LAUNCH(attn_pool_bwd_fused_lean<32, PRV>) }
-        else { MMF_PR_LAUNCH(attn_pool_bwd_fused_lean<64, PRV>) }
+        if (pst) {
+          if (small) { MMF_PR_LAUNCH(attn_pool_bwd_fused_lean<32, PRV, true>) }
+          else { MMF_PR_LAUNCH(attn_pool_bwd_fused_lean<64, PRV, true>) }
+        } else {
+          if (small) { MMF_PR_LAUNCH(attn_pool_bwd_fused_lean<32, PRV>) }
+          else { MMF_PR_LAUNCH(attn_pool_bwd_fused_lean<64, PRV>) }
+        }
         break;
       case Kind::PoolDk:
         if (lean && small) { MMF_PR_LAUNCH(attn_pool_bwd_dk_lean<32, PRV>) }

@@ -426,8 +426,11 @@ int mmf_cma_backward(const mmf_cma_desc* d, const mmf_cma_params* W, const float
     a.dout = w.dO; a.dv = w.dV;
     STAGE_TRY("cma.bwd.attn_single_key_dv", launch_sk_dv(&a, 1, B, d->num_heads, hd, p, rng, st));
     // the query and the key reach the output only through the one-key softmax: zero gradient
-    if (dquery) HIP_TRY(hipMemsetAsync(dquery, 0, (size_t)B * d->lq * d->query_dim * sizeof(float), st));
-    if (dkey) HIP_TRY(hipMemsetAsync(dkey, 0, (size_t)B * d->lk * d->key_dim * sizeof(float), st));
+    // (a kernel, not hipMemsetAsync: a memset captured into a torch.compile "reduce-overhead"
+    // HIP graph left the buffers unwritten on replay)
+    float* zp[2] = {dquery, dkey};
+    const int64_t zn[2] = {(int64_t)B * d->lq * d->query_dim, (int64_t)B * d->lk * d->key_dim};
+    STAGE_TRY("cma.bwd.zero_qk_grads", launch_zero_fill(zp, zn, 2, st));
   } else if (cma_wide(d)) {
     WidePair a = cma_wide_pair(d, s, mask);
     a.dout = w.dO; a.dPd = w.dPd; a.dS = w.dS; a.dq = w.dQ; a.dk = w.dK; a.dv = w.dV;

@@ -51,6 +51,21 @@ inline bool long_keys(const mmf_hybrid_desc* d) {
 
 bool use_tail(const mmf_hybrid_desc* d);
 
+// Training forward keeps the pre-dropout probabilities for the fused backward (no S recompute
+// there): the pooled plan with every attention-kernel pair inside the lean fused kernels' shape
+// (attn_pstore_ok).  All pairs or none (one launch each way).  MMF_NO_PSTORE=1: recompute (A/B).
+bool pstore_on(const mmf_hybrid_desc* d) {
+  if (!d->training || !use_pool(d) || getenv("MMF_NO_PSTORE")) return false;
+  const int hd = d->hidden / d->num_heads;
+  int n = 0;
+  for (int g = 0; g < d->num_pairs; ++g) {
+    if (single_key(d, g) || wide_pair(d, g)) continue;
+    if (!attn_pstore_ok(Lm(d, d->pair_q[g]), Lm(d, d->pair_k[g]), 1, hd) || d->hidden % 4 != 0) return false;
+    ++n;
+  }
+  return n > 0;
+}
+
 // The tail head takes mean_L P_m from per-tile column sums written by the
 // projection GEMM's epilogue when every 128-row tile lies inside one sample.
 bool pcol_in_proj(const mmf_hybrid_desc* d, int m) {
@@ -70,6 +85,7 @@ struct Saved {
   float* pbarT[MMF_MAX_PAIRS];   // (B, Lk, heads): pbar as the RK operand of the dZ GEMM's E_m term
   uint32_t* bits[MMF_MAX_PAIRS];
   float *Pw[MMF_MAX_PAIRS], *Pdw[MMF_MAX_PAIRS];   // wide pairs: probabilities, post-dropout (general)
+  float* pst[MMF_MAX_PAIRS];                        // stored probabilities (pstore_on)
   float *pooled, *scores, *weights, *fused, *h1;
 };
 
@@ -102,6 +118,7 @@ void layout_saved(const mmf_hybrid_desc* d, Bump& bp, Saved& s) {
       s.Ob[g] = bp.take<float>(B * H);
       s.Ab[g] = bp.take<float>(B * H);
       if (dropping(d) && !sk && !wide) s.bits[g] = bp.take<uint32_t>(B * nh * lq * kw_ld((int)lk));
+      if (!sk && !wide && pstore_on(d)) s.pst[g] = bp.take<float>(B * nh * attn_pstore_floats((int)lq));
     } else {
       s.V[g] = bp.take<float>(B * lk * H);
       s.O[g] = bp.take<float>(B * lq * H);
@@ -205,10 +222,10 @@ void plan_wgrads(const mmf_hybrid_desc* d, const float* const* x, const float* m
   static const mmf_hybrid_grads kNull = {};
   const mmf_hybrid_grads* g = G ? G : &kNull;
   // Split counts of the long (B*L-row) contractions, sized per launch: launch_gemm packs
-  // GEMM_MAX_GROUPS of them per launch (longest slabs first), and a launch should be about
-  // one wave of its 3-per-CU workgroups.  Full launches take slots / GEMM_MAX_GROUPS slabs
-  // per job (512 rows at C2); the r jobs of a remainder launch take slots / r (C2: 15 jobs =
-  // 12 + 3 -> the last 3 are split 256 ways instead of leaving 3/4 of the GPU idle).
+  // GEMM_MAX_GROUPS (32) of them per launch (longest slabs first), and a launch should be
+  // about one wave of its 3-per-CU workgroups.  Full launches take slots / GEMM_MAX_GROUPS
+  // slabs per job; the r jobs of a remainder launch take slots / r (C2: all 15 big jobs fit
+  // one launch: 768 / 15 = 51 slabs requested, 49 of 672 rows after rounding to 32).
   const int kBigRows = 4096;
   int nbig = 0;
   for (int p = 0; p < d->num_pairs; ++p) {
@@ -374,6 +391,7 @@ AttnPair make_pair(const mmf_hybrid_desc* d, const Saved& s, const float* mask, 
   a.pbarT = s.pbarT[g];
   a.keep_bits = s.bits[g];
   a.kw_ld = kw_ld(a.Lk);
+  a.pstore = s.pst[g];
   return a;
 }
 
@@ -749,6 +767,7 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
       }
       if (fe == hipErrorNotSupported) {
         (void)hipGetLastError();
+        for (AttnPair& a : pairs) a.pstore = nullptr;   // the two-pass kernels recompute S
         STAGE_TRY("bwd.attn_dq", launch_attn_pool_bwd(0, pairs.data(), nmp, B, nh, hd, scale, p, rng, st));
         STAGE_TRY("bwd.attn_dk", launch_attn_pool_bwd(1, pairs.data(), nmp, B, nh, hd, scale, p, rng, st));
       } else {

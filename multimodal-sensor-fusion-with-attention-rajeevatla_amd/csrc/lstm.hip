@@ -408,6 +408,23 @@ int lstm_plan(LstmArgs& a, int num_lstm, int batch, int steps, int hidden, unsig
 
 using namespace mmf;
 
+namespace {
+// the sync granules of every LSTM and the timeout word, zeroed by one kernel
+int zero_sync(int num_lstm, int batch, int hidden, void* const* sync, uint32_t* timeout, hipStream_t st) {
+  float* ptrs[LMAX_N + 1];
+  int64_t counts[LMAX_N + 1];
+  int n = 0;
+  for (int i = 0; i < num_lstm; ++i) {
+    ptrs[n] = (float*)sync[i];
+    counts[n++] = (int64_t)(mmf_lstm_sync_bytes(batch, hidden) / 4);
+  }
+  ptrs[n] = (float*)timeout;
+  counts[n++] = 1;
+  HIP_TRY(launch_zero_fill(ptrs, counts, n, st));
+  return MMF_OK;
+}
+}  // namespace
+
 extern "C" {
 
 size_t mmf_lstm_sync_bytes(int32_t batch, int32_t hidden) {
@@ -428,16 +445,16 @@ int mmf_lstm_forward(int32_t num_lstm, int32_t batch, int32_t steps, int32_t hid
   for (int i = 0; i < num_lstm; ++i) {
     a.xproj[i] = xproj[i]; a.w_hh[i] = w_hh[i]; a.h[i] = h[i]; a.c[i] = c[i]; a.gates[i] = gates[i];
     a.gran[i] = (gu64*)sync[i];
-    // every polled word is zeroed before the launch (epochs start at 1)
-    HIP_TRY(hipMemsetAsync(sync[i], 0, mmf_lstm_sync_bytes(batch, hidden), st));
   }
+  // every polled word is zeroed before the launch (epochs start at 1); the timeout word per
+  // call (a stale flag never aborts waits); one zero-fill kernel (graph-capturable)
+  if (int rc = zero_sync(num_lstm, batch, hidden, sync, timeout, st)) return rc;
   const int grid = a.G * a.ninst;
   void (*kern)(const LstmArgs) = hidden == 64    ? lstm_fwd_kernel<64>
                                  : hidden == 128 ? lstm_fwd_kernel<128>
                                  : hidden == 192 ? lstm_fwd_kernel<192>
                                                  : lstm_fwd_kernel<256>;
   if (int rc = check_coresident(kern, grid, "lstm forward")) return rc;
-  HIP_TRY(hipMemsetAsync(timeout, 0, sizeof(uint32_t), st));   // per call: a stale flag never aborts waits
   ProfLaunch prof_(st, "lstm_fwd_kernel", 8.0 * num_lstm * batch * steps * hidden * hidden,
                    4.0 * num_lstm * ((double)4 * hidden * hidden + (double)batch * steps * 10 * hidden));
   mmf_launch(kern, dim3(grid), dim3(LNT), 0, st, a);
@@ -457,10 +474,9 @@ int mmf_lstm_backward(int32_t num_lstm, int32_t batch, int32_t steps, int32_t hi
   for (int i = 0; i < num_lstm; ++i) {
     a.w_hh[i] = w_hh[i]; a.c[i] = (float*)c[i]; a.gates[i] = (float*)gates[i]; a.dh[i] = dh[i];
     a.dgates[i] = dgates[i]; a.gran[i] = (gu64*)sync[i];
-    HIP_TRY(hipMemsetAsync(sync[i], 0, mmf_lstm_sync_bytes(batch, hidden), st));
   }
+  if (int rc = zero_sync(num_lstm, batch, hidden, sync, timeout, st)) return rc;
   if (int rc = check_coresident(lstm_bwd_kernel, a.G * a.ninst, "lstm backward")) return rc;
-  HIP_TRY(hipMemsetAsync(timeout, 0, sizeof(uint32_t), st));
   ProfLaunch prof_(st, "lstm_bwd_kernel", 8.0 * num_lstm * batch * steps * hidden * hidden,
                    4.0 * num_lstm * ((double)4 * hidden * hidden + (double)batch * steps * 14 * hidden));
   mmf_launch(lstm_bwd_kernel, dim3(a.G * a.ninst), dim3(LNT), 0, st, a);

@@ -235,9 +235,22 @@ struct AttnPair {
   uint32_t* keep_bits; // (B, heads, Lq, kw_ld) dropout keep mask written by the pooled forward
                        // (bit k%32 of word k/32), read by its backward
   int32_t kw_ld;       // words per query row: 4 when Lk <= 128, ceil(Lk/32) otherwise
+  // optional: the pre-dropout probabilities P written by the lean pooled forward and read by
+  // the fused backward instead of recomputing S = QK^T (training, keys and queries <= 128).
+  // "Register order": per (sample, head), per 32-query tile qt, key tile kt and register group
+  // g, 64 lanes x float4 = P of lane (query c, half h) at regs 4g..4g+3 (attn_pstore_index);
+  // attn_pstore_floats(Lq) floats per (sample, head).
+  float* pstore;
 };
 
 constexpr int ATTN_MAX_PAIRS = 12;
+// floats of the stored probabilities per (sample, head) of a pair with Lq queries
+inline int64_t attn_pstore_floats(int Lq) { return (int64_t)((Lq + 31) / 32) * 4 * 4 * 64 * 4; }
+// the pooled pairs whose probabilities can be stored: the lean fused backward's conditions
+// (keys a multiple of 32 and <= 128, queries <= 128, no per-key mask, head_dim <= 64, % 4)
+inline bool attn_pstore_ok(int Lq, int Lk, int kmask_mode, int hd) {
+  return Lk % 32 == 0 && Lk <= 128 && Lq <= 128 && kmask_mode != 2 && hd <= 64 && hd % 4 == 0;
+}
 
 struct AttnArgs {
   AttnPair p[ATTN_MAX_PAIRS];
@@ -295,6 +308,10 @@ hipError_t launch_sk_out(const SkPair* pairs, int npairs, int B, int heads, int 
                          const RngSnap* rng, hipStream_t st);
 hipError_t launch_sk_dv(const SkPair* pairs, int npairs, int B, int heads, int hd, float drop_p,
                         const RngSnap* rng, hipStream_t st);
+// zero-fills up to 16 buffers of counts[i] 4-byte words (null / empty entries skipped) in one
+// kernel launch: a kernel node under stream capture (hipMemsetAsync captured into a torch.compile
+// "reduce-overhead" HIP graph was observed to leave its buffer unwritten on replay)
+hipError_t launch_zero_fill(float* const* ptrs, const int64_t* counts, int n, hipStream_t st);
 
 // ---------------------------------------------------------------------------
 // Attention with head_dim > 64 (wide.hip): materialised scores, grouped strided-batch

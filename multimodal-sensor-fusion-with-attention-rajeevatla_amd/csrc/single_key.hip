@@ -18,6 +18,7 @@
 // of the pair's probability tensor: the same Philox stream every attention kernel
 // of the library draws (mmf_device.h keep1), so the HIP path and the Philox replay
 // in tests/_philox.py agree.
+#include <algorithm>
 #include <cstring>
 
 #include "mmf_device.h"
@@ -87,6 +88,18 @@ __global__ __launch_bounds__(256) void sk_dv_kernel(const SkArgs A) {
   P.dv[(int64_t)b * P.ldv + c] = acc;
 }
 
+// zero-fill of up to 16 buffers of 4-byte words in one launch (a kernel node under graph capture)
+constexpr int ZERO_MAX = 16;
+struct ZeroArgs {
+  float* p[ZERO_MAX];
+  int64_t n[ZERO_MAX];
+};
+__global__ __launch_bounds__(256) void zero_fill_kernel(const ZeroArgs a) {
+  float* p = a.p[blockIdx.y];
+  const int64_t n = a.n[blockIdx.y];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = 0.f;
+}
+
 SkArgs sk_args(const SkPair* pairs, int npairs, int B, int heads, int hd, float drop_p, const RngSnap* rng) {
   SkArgs a;
   memset(&a, 0, sizeof(a));
@@ -149,6 +162,26 @@ hipError_t launch_sk_dv(const SkPair* pairs, int npairs, int B, int heads, int h
   }
   ProfLaunch prof_(st, "sk_dv_kernel", fl, by);
   mmf_launch(sk_dv_kernel, dim3((B * heads * hd + 255) / 256, npairs), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_zero_fill(float* const* ptrs, const int64_t* counts, int n, hipStream_t st) {
+  ZeroArgs a;
+  memset(&a, 0, sizeof(a));
+  int m = 0;
+  int64_t maxn = 0;
+  for (int i = 0; i < n && m < ZERO_MAX; ++i)
+    if (ptrs[i] && counts[i] > 0) {
+      a.p[m] = ptrs[i];
+      a.n[m] = counts[i];
+      maxn = counts[i] > maxn ? counts[i] : maxn;
+      ++m;
+    }
+  if (m == 0) return hipSuccess;
+  if (n > ZERO_MAX) return hipErrorInvalidValue;
+  const unsigned blocks = (unsigned)std::min<int64_t>((maxn + 255) / 256, 1024);
+  ProfLaunch prof_(st, "zero_fill_kernel", 0.0, 4.0 * (double)maxn * m);
+  mmf_launch(zero_fill_kernel, dim3(blocks, m), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

@@ -317,8 +317,9 @@ int mmf_attention_pool_backward(int32_t batch, int32_t frames, int32_t dim, cons
   if (frames > MAX_T) return fail(MMF_ELIMIT, "attention_pool: %d frames > %d", frames, MAX_T);
   hipStream_t st = (hipStream_t)stream;
   if (batch == 0) {
-    HIP_TRY(hipMemsetAsync(dscore_w, 0, (size_t)dim * sizeof(float), st));
-    HIP_TRY(hipMemsetAsync(dscore_b, 0, sizeof(float), st));
+    float* zp[2] = {dscore_w, dscore_b};
+    const int64_t zn[2] = {dim, 1};
+    HIP_TRY(launch_zero_fill(zp, zn, 2, st));
     return MMF_OK;
   }
   float* part = (float*)workspace;
@@ -366,7 +367,9 @@ int mmf_late_fusion_backward(int32_t batch, int32_t num_modalities, int32_t num_
   if (num_modalities > LATE_MAX_M) return fail(MMF_ELIMIT, "late fusion: more than %d modalities", LATE_MAX_M);
   hipStream_t st = (hipStream_t)stream;
   if (batch == 0) {
-    HIP_TRY(hipMemsetAsync(dweight_logits, 0, (size_t)num_modalities * sizeof(float), st));
+    float* zp[1] = {dweight_logits};
+    const int64_t zn[1] = {num_modalities};
+    HIP_TRY(launch_zero_fill(zp, zn, 1, st));
     return MMF_OK;
   }
   LateArgs a;

@@ -45,43 +45,9 @@ if _HERE not in sys.path:
     sys.path.insert(0, _HERE)
 
 import mmf_native as _nat  # noqa: E402
+import mmf_ops as _ops  # noqa: E402
 
 
-class _AttentionPoolFunction(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, frames, weight, bias, mask):
-        L = _nat.lib()
-        dev = frames.device
-        B, T, D = frames.shape
-        pooled = torch.empty(B, D, dtype=torch.float32, device=dev)
-        weights = torch.empty(B, T, dtype=torch.float32, device=dev)
-        rc = L.mmf_attention_pool_forward(B, T, D, frames.data_ptr(), weight.data_ptr(), bias.data_ptr(),
-                                          _nat.ptr(mask), pooled.data_ptr(), weights.data_ptr(),
-                                          _nat.stream_ptr(dev))
-        _nat.check(rc, "FrameEncoder.attention_pool forward")
-        ctx.save_for_backward(frames, weight, weights)
-        ctx.bias_shape = bias.shape
-        return pooled
-
-    @staticmethod
-    def backward(ctx, dpooled):
-        L = _nat.lib()
-        frames, weight, weights = ctx.saved_tensors
-        dev = frames.device
-        B, T, D = frames.shape
-        dpooled = _nat.f32c(dpooled)
-        dx = torch.empty_like(frames)
-        dw = torch.empty(D, dtype=torch.float32, device=dev)
-        db = torch.empty(1, dtype=torch.float32, device=dev)
-        ws = torch.empty(L.mmf_attention_pool_workspace_bytes(B, D), dtype=torch.uint8, device=dev)
-        rc = L.mmf_attention_pool_backward(B, T, D, frames.data_ptr(), weight.data_ptr(), weights.data_ptr(),
-                                           dpooled.data_ptr(), dx.data_ptr(), dw.data_ptr(), db.data_ptr(),
-                                           ws.data_ptr(), _nat.stream_ptr(dev))
-        _nat.check(rc, "FrameEncoder.attention_pool backward")
-        return dx, dw.view(1, D), db.view(ctx.bias_shape), None
-
-
-@torch.compiler.disable  # HIP library calls: opaque to TorchDynamo (runs eagerly)
 def attention_pool(frames: torch.Tensor, attention: nn.Linear, mask: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Learned-score softmax pooling over the frame axis (src/encoders.py:313-336) on HIP."""
     _nat.require_device(frames, "FrameEncoder input")
@@ -91,7 +57,8 @@ def attention_pool(frames: torch.Tensor, attention: nn.Linear, mask: Optional[to
         m = mask.to(device=frames.device, dtype=torch.float32).contiguous()
         if m.shape != frames.shape[:2]:
             raise ValueError(f"mask shape {tuple(m.shape)} does not match frames {tuple(frames.shape[:2])}")
-    return _AttentionPoolFunction.apply(frames, attention.weight, attention.bias, m)
+    pooled, _ = torch.ops.mmfusion.attention_pool_fwd(frames, attention.weight, attention.bias, m)
+    return pooled
 
 
 class FrameEncoder(nn.Module):
@@ -114,7 +81,6 @@ class FrameEncoder(nn.Module):
         self.projection = nn.Sequential(nn.Linear(hidden_dim, hidden_dim), nn.ReLU(), nn.Dropout(dropout),
                                         nn.Linear(hidden_dim, output_dim))
 
-    @torch.compiler.disable  # HIP library calls: opaque to TorchDynamo (runs eagerly)
     def forward(self, frames: torch.Tensor, mask: Optional[torch.Tensor] = None) -> torch.Tensor:
         if frames.dim() != 3:
             raise ValueError(f"Expected 3D frame tensor, got shape {frames.shape}")
@@ -139,7 +105,6 @@ class FrameEncoder(nn.Module):
             raise ValueError(f"Unknown pooling strategy: {self.temporal_pooling}")
         return self.projection(pooled)
 
-    @torch.compiler.disable  # HIP library calls: opaque to TorchDynamo (runs eagerly)
     def attention_pool(self, frames: torch.Tensor, mask: Optional[torch.Tensor] = None) -> torch.Tensor:
         if self.attention is None:
             raise RuntimeError("Attention layer not initialized.")
@@ -172,12 +137,19 @@ def _record_timeout(flag: torch.Tensor) -> None:
     _timeout_acc(flag.device).bitwise_or_(flag)
 
 
+def _drain_op_flags() -> None:
+    """Fold the timeout words of the eager LSTM operator launches (mmf_ops.LSTM_FLAGS)."""
+    while _ops.LSTM_FLAGS:
+        _record_timeout(_ops.LSTM_FLAGS.pop())
+
+
 def lstm_timed_out(device=None, reset: bool = True) -> bool:
     """True if any LSTM launch on `device` since the last check gave up an inter-workgroup
     wait.  Such a launch also writes NaN into the values it never received, so its
     encodings / gradients are NaN, never silently wrong.  Reading syncs the stream;
     call it once per step (or per epoch) rather than per launch."""
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    _drain_op_flags()
     acc = _timeout_acc(dev)
     hit = bool(int(acc.item()))
     if reset:
@@ -192,74 +164,6 @@ def check_lstm_timeouts(device=None) -> None:
                            "fully co-resident); the affected encodings / gradients are NaN")
 
 
-class _LstmLayersFunction(torch.autograd.Function):
-    """One LSTM layer of n independent LSTMs (same B, T, H): h_l = LSTM(x_l) for each l.
-
-    inputs: n, then n x (x, w_ih, w_hh, b_ih, b_hh); outputs: n x h (B, T, H)."""
-
-    @staticmethod
-    def forward(ctx, n, *flat):
-        L = _nat.lib()
-        xs = [_nat.f32c(flat[5 * i]) for i in range(n)]
-        w_ih = [flat[5 * i + 1] for i in range(n)]
-        w_hh = [_nat.f32c(flat[5 * i + 2]) for i in range(n)]
-        b_ih = [flat[5 * i + 3] for i in range(n)]
-        b_hh = [flat[5 * i + 4] for i in range(n)]
-        dev = xs[0].device
-        B, T, _ = xs[0].shape
-        H = w_hh[0].shape[1]
-        xproj = [torch.addmm(b_ih[i] + b_hh[i], xs[i].reshape(B * T, -1), w_ih[i].t()).view(B, T, 4 * H)
-                 for i in range(n)]
-        hs = [torch.empty(B, T, H, dtype=torch.float32, device=dev) for _ in range(n)]
-        cs = [torch.empty(B, T, H, dtype=torch.float32, device=dev) for _ in range(n)]
-        gates = [torch.empty(B, T, 4 * H, dtype=torch.float32, device=dev) for _ in range(n)]
-        sb = L.mmf_lstm_sync_bytes(B, H)
-        sync = torch.empty(n, sb, dtype=torch.uint8, device=dev)
-        flag = _timeout_flag(dev)
-        rc = L.mmf_lstm_forward(
-            n, B, T, H, _nat.ptr_array([t.data_ptr() for t in xproj]), _nat.ptr_array([w.data_ptr() for w in w_hh]),
-            _nat.ptr_array([t.data_ptr() for t in hs]), _nat.ptr_array([t.data_ptr() for t in cs]),
-            _nat.ptr_array([t.data_ptr() for t in gates]), _nat.ptr_array([sync[i].data_ptr() for i in range(n)]),
-            flag.data_ptr(), _nat.stream_ptr(dev))
-        _nat.check(rc, "LSTM forward")
-        _record_timeout(flag)
-        ctx.n = n
-        ctx.save_for_backward(*xs, *w_ih, *w_hh, *hs, *cs, *gates)
-        return tuple(hs)
-
-    @staticmethod
-    def backward(ctx, *dhs):
-        L = _nat.lib()
-        n = ctx.n
-        sv = ctx.saved_tensors
-        xs, w_ih, w_hh, hs, cs, gates = (sv[k * n:(k + 1) * n] for k in range(6))
-        dev = xs[0].device
-        B, T, _ = xs[0].shape
-        H = w_hh[0].shape[1]
-        dh = [None if d is None else _nat.f32c(d) for d in dhs]
-        dgates = [torch.empty(B, T, 4 * H, dtype=torch.float32, device=dev) for _ in range(n)]
-        sync = torch.empty(n, L.mmf_lstm_sync_bytes(B, H), dtype=torch.uint8, device=dev)
-        flag = _timeout_flag(dev)
-        rc = L.mmf_lstm_backward(
-            n, B, T, H, _nat.ptr_array([w.data_ptr() for w in w_hh]), _nat.ptr_array([t.data_ptr() for t in cs]),
-            _nat.ptr_array([t.data_ptr() for t in gates]), _nat.ptr_array([0 if d is None else d.data_ptr() for d in dh]),
-            _nat.ptr_array([t.data_ptr() for t in dgates]), _nat.ptr_array([sync[i].data_ptr() for i in range(n)]),
-            flag.data_ptr(), _nat.stream_ptr(dev))
-        _nat.check(rc, "LSTM backward")
-        _record_timeout(flag)
-        grads: List[Optional[torch.Tensor]] = [None]
-        for i in range(n):
-            dg = dgates[i].view(B * T, 4 * H)
-            x2 = xs[i].reshape(B * T, -1)
-            dx = (dg @ w_ih[i]).view_as(xs[i]) if ctx.needs_input_grad[1 + 5 * i] else None
-            dw_ih = dg.t() @ x2
-            dw_hh = dgates[i][:, 1:].reshape(-1, 4 * H).t() @ hs[i][:, :-1].reshape(-1, H)
-            db = dg.sum(0)
-            grads += [dx, dw_ih, dw_hh, db, db]
-        return tuple(grads)
-
-
-@torch.compiler.disable  # HIP library calls: opaque to TorchDynamo (runs eagerly)
 def lstm_layers(rnns: Sequence[nn.LSTM], inputs: Sequence[torch.Tensor]) -> List[torch.Tensor]:
     """Run several nn.LSTM parameter sets (batch_first, zero initial state) over their inputs on the
     HIP recurrence, every layer of all of them in one launch; returns each LSTM's top-layer output
@@ -281,12 +185,18 @@ def lstm_layers(rnns: Sequence[nn.LSTM], inputs: Sequence[torch.Tensor]) -> List
             raise ValueError("lstm_layers: all sequences need the same (batch, seq_len)")
     cur = list(inputs)
     for k in range(layers):
-        flat: List[torch.Tensor] = []
+        # time-parallel input projection on PyTorch-ROCm (xproj = x W_ih^T + b_ih + b_hh; autograd
+        # gives dx, dW_ih, db), the recurrence as one persistent HIP launch for all LSTMs
+        xproj = []
         for r, x in zip(rnns, cur):
-            flat += [x, getattr(r, f"weight_ih_l{k}"), getattr(r, f"weight_hh_l{k}"),
-                     getattr(r, f"bias_ih_l{k}"), getattr(r, f"bias_hh_l{k}")]
-        outs = _LstmLayersFunction.apply(n, *flat)
-        cur = list(outs)
+            x2 = _nat.f32c(x).reshape(B * T, -1)
+            b = getattr(r, f"bias_ih_l{k}") + getattr(r, f"bias_hh_l{k}")
+            xproj.append(torch.addmm(b, x2, getattr(r, f"weight_ih_l{k}").t()).view(B, T, -1))
+        hs, _cs, _gates, flag = torch.ops.mmfusion.lstm_layer_fwd(
+            xproj, [_nat.f32c(getattr(r, f"weight_hh_l{k}")) for r in rnns])
+        if not torch.compiler.is_compiling():
+            _record_timeout(flag)
+        cur = list(hs)
         if k + 1 < layers:
             cur = [torch.nn.functional.dropout(o, rnns[i].dropout, rnns[i].training) for i, o in enumerate(cur)]
     return cur
@@ -340,7 +250,6 @@ class SequenceEncoder(nn.Module):
     def encode_final_state(self, final_state: torch.Tensor) -> torch.Tensor:
         return self.projection(self.dropout_layer(final_state))
 
-    @torch.compiler.disable  # HIP library calls: opaque to TorchDynamo (runs eagerly)
     def forward(self, sequence: torch.Tensor, lengths: Optional[torch.Tensor] = None) -> torch.Tensor:
         if sequence.dim() != 3:
             raise ValueError(f"Expected 3D input sequence, got shape {sequence.shape}")
@@ -350,7 +259,6 @@ class SequenceEncoder(nn.Module):
         return self.encode_final_state(_final_state(out, lengths))
 
 
-@torch.compiler.disable  # HIP library calls: opaque to TorchDynamo (runs eagerly)
 def encode_sequences(encoders: Dict[str, SequenceEncoder], sequences: Dict[str, torch.Tensor],
                      lengths: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
     """{m: encoders[m](sequences[m], lengths)} with every modality's LSTM layers sharing launches

@@ -18,7 +18,11 @@ build_fusion_model` (src/train.py:25) resolves here unchanged:
 
 The whole fused step (projections, pairwise Q/K/V, QK^T softmax attn.V,
 out_proj, aggregation, gating softmax, weighted sum, classifier) runs as HIP
-kernels through include/mmfusion.h (mmf_hybrid_forward / mmf_hybrid_backward);
+kernels through include/mmfusion.h (mmf_hybrid_forward / mmf_hybrid_backward),
+reached as the torch operators torch.ops.mmfusion.hybrid_fwd / hybrid_bwd
+(mmf_ops.py: custom ops with fake kernels and an autograd formula, so
+torch.compile(..., mode="reduce-overhead", fullgraph=True) -- the reference
+trainer's compile, src/train.py:193-231 -- traces the module without a graph break);
 inputs may be 2-D (B, D_m) (reference semantics) or 3-D (B, L_m, D_m)
 (sequence mode: each modality's aggregate is mean-pooled over L_m before the
 weighting; identical to the reference at L = 1).  No CPU path exists: CPU
@@ -42,7 +46,8 @@ if _HERE not in sys.path:
     sys.path.insert(0, _HERE)
 
 import mmf_native as _nat  # noqa: E402
-from attention import CrossModalAttention, _new_rng_state  # noqa: E402
+import mmf_ops as _ops  # noqa: E402
+from attention import CrossModalAttention, _new_rng_state, _precision  # noqa: E402
 
 
 # --------------------------------------------------------------------------
@@ -110,39 +115,13 @@ class EarlyFusion(nn.Module):
         return self.fusion(torch.cat(parts, dim=1))
 
 
-class _LateWeightFunction(torch.autograd.Function):
+def _late_weights(stacked: torch.Tensor, weight_logits: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
     """LateFusion's masked softmax weighting (src/fusion.py:228-245) on HIP
-    (mmf_late_fusion_forward / _backward, csrc/softmax_pool.hip)."""
-
-    @staticmethod
-    def forward(ctx, stacked, weight_logits, mask):
-        L = _nat.lib()
-        _nat.require_device(stacked, "LateFusion logits")
-        dev = stacked.device
-        B, M, C = stacked.shape
-        fused = torch.empty(B, C, dtype=torch.float32, device=dev)
-        weights = torch.empty(B, M, dtype=torch.float32, device=dev)
-        rc = L.mmf_late_fusion_forward(B, M, C, stacked.data_ptr(), weight_logits.data_ptr(), mask.data_ptr(),
-                                       fused.data_ptr(), weights.data_ptr(), _nat.stream_ptr(dev))
-        _nat.check(rc, "LateFusion weighting forward")
-        ctx.save_for_backward(stacked, weight_logits, mask, weights)
-        return fused
-
-    @staticmethod
-    def backward(ctx, dfused):
-        L = _nat.lib()
-        stacked, weight_logits, mask, weights = ctx.saved_tensors
-        dev = stacked.device
-        B, M, C = stacked.shape
-        dfused = _nat.f32c(dfused)
-        dstacked = torch.empty_like(stacked)
-        dwl = torch.empty(M, dtype=torch.float32, device=dev)
-        ws = torch.empty(L.mmf_late_fusion_workspace_bytes(B, M), dtype=torch.uint8, device=dev)
-        rc = L.mmf_late_fusion_backward(B, M, C, stacked.data_ptr(), weight_logits.data_ptr(), mask.data_ptr(),
-                                        weights.data_ptr(), dfused.data_ptr(), dstacked.data_ptr(), dwl.data_ptr(),
-                                        ws.data_ptr(), _nat.stream_ptr(dev))
-        _nat.check(rc, "LateFusion weighting backward")
-        return dstacked, dwl, None
+    (torch.ops.mmfusion.late_weights_fwd: mmf_late_fusion_forward / _backward,
+    csrc/softmax_pool.hip)."""
+    _nat.require_device(stacked, "LateFusion logits")
+    fused, _ = torch.ops.mmfusion.late_weights_fwd(stacked, weight_logits, mask)
+    return fused
 
 
 class LateFusion(nn.Module):
@@ -164,7 +143,6 @@ class LateFusion(nn.Module):
         self.weight_logits = nn.Parameter(torch.zeros(self.num_modalities))
         self.dropout = nn.Dropout(dropout)
 
-    @torch.compiler.disable  # HIP library calls: opaque to TorchDynamo (runs eagerly)
     def forward(self, modality_features, modality_mask=None):
         if not self.modality_names:
             raise ValueError("No modalities configured for LateFusion.")
@@ -176,80 +154,15 @@ class LateFusion(nn.Module):
             x = modality_features[name].to(mask.device) * mask[:, i:i + 1]
             per[name] = self.classifiers[name](self.dropout(x))
         stacked = torch.stack([per[n] for n in self.modality_names], dim=1)
-        return _LateWeightFunction.apply(_nat.f32c(stacked), self.weight_logits, mask.float().contiguous()), per
+        return _late_weights(_nat.f32c(stacked), self.weight_logits, mask.float().contiguous()), per
 
 
 # --------------------------------------------------------------------------
 # HybridFusion: the accelerated hot path
 # --------------------------------------------------------------------------
-class _HybridFunction(torch.autograd.Function):
-    """Autograd node over mmf_hybrid_forward / mmf_hybrid_backward.
-
-    tensors = (mask, x_0..x_{M-1}, params...) in the plan's parameter order.
-    Outputs: logits (differentiable), fusion_weights and attention maps
-    (returned for inspection, not differentiable).
-    """
-
-    @staticmethod
-    def forward(ctx, plan: "_Plan", rng, mask, *tensors):
-        L = _nat.lib()
-        M = plan.desc.num_modalities
-        xs = tensors[:M]
-        params = tensors[M:]
-        dev = mask.device
-        d = plan.desc
-        saved = torch.empty(L.mmf_hybrid_saved_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
-        logits = torch.empty(d.batch, d.num_classes, dtype=torch.float32, device=dev)
-        fw = torch.empty(d.batch, M, dtype=torch.float32, device=dev)
-        maps: List[torch.Tensor] = []
-        if d.return_attention:
-            for g in range(d.num_pairs):
-                lq = plan.seq[d.pair_q[g]]
-                lk = plan.seq[d.pair_k[g]]
-                maps.append(torch.empty(d.batch, d.num_heads, lq, lk, dtype=torch.float32, device=dev))
-        pstruct = plan.param_struct(params)
-        xarr = _nat.ptr_array([x.data_ptr() for x in xs])
-        marr = _nat.ptr_array([t.data_ptr() for t in maps]) if maps else None
-        rc = L.mmf_hybrid_forward(ctypes.byref(d), ctypes.byref(pstruct), ctypes.cast(xarr, ctypes.c_void_p),
-                                  mask.data_ptr(), rng.data_ptr(), saved.data_ptr(), logits.data_ptr(),
-                                  fw.data_ptr(), ctypes.cast(marr, ctypes.c_void_p) if marr else None,
-                                  _nat.stream_ptr(dev))
-        _nat.check(rc, "HybridFusion forward")
-        ctx.plan = plan
-        ctx.saved_buf = saved
-        ctx.save_for_backward(mask, *xs, *params)
-        ctx.mark_non_differentiable(fw, *maps)
-        return (logits, fw, *maps)
-
-    @staticmethod
-    def backward(ctx, dlogits, *_unused):
-        L = _nat.lib()
-        plan: _Plan = ctx.plan
-        d = plan.desc
-        M = d.num_modalities
-        mask, *rest = ctx.saved_tensors
-        xs, params = rest[:M], rest[M:]
-        dev = mask.device
-        dlogits = _nat.f32c(dlogits)
-        ws = torch.empty(L.mmf_hybrid_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
-        flat = torch.zeros(plan.num_param_elems, dtype=torch.float32, device=dev)
-        gviews = plan.grad_views(flat, params)
-        gstruct = plan.param_struct(gviews)
-        pstruct = plan.param_struct(params)
-        needs = ctx.needs_input_grad[3:3 + M]
-        dxs = [torch.empty_like(x) if need else None for x, need in zip(xs, needs)]
-        xarr = _nat.ptr_array([x.data_ptr() for x in xs])
-        dxarr = _nat.ptr_array([t.data_ptr() if t is not None else None for t in dxs])
-        rc = L.mmf_hybrid_backward(ctypes.byref(d), ctypes.byref(pstruct), ctypes.cast(xarr, ctypes.c_void_p),
-                                   mask.data_ptr(), ctx.saved_buf.data_ptr(), dlogits.data_ptr(),
-                                   ws.data_ptr(), ctypes.byref(gstruct), ctypes.cast(dxarr, ctypes.c_void_p),
-                                   _nat.stream_ptr(dev))
-        _nat.check(rc, "HybridFusion backward")
-        return (None, None, None, *dxs, *gviews)
-
-
 class _Plan:
-    """Shape/pair descriptor + parameter ordering for one forward call."""
+    """Shape/pair descriptor + parameter ordering (ctypes descriptor) for the fused
+    training step (train_step.HybridTrainStep)."""
 
     def __init__(self, model: "HybridFusion", seq: List[int], dims: List[int], batch: int,
                  pairs: List[Tuple[int, int, str]], return_attention: bool):
@@ -372,6 +285,10 @@ class HybridFusion(nn.Module):
         return out
 
     def _plan(self, feats: List[torch.Tensor], return_attention: bool) -> _Plan:
+        seq, dims = self._shapes(feats)
+        return _Plan(self, seq, dims, feats[0].size(0), self.present_pairs(), return_attention)
+
+    def _shapes(self, feats: List[torch.Tensor]) -> Tuple[List[int], List[int]]:
         seq, dims = [], []
         B = feats[0].size(0)
         for name, x in zip(self.modality_names, feats):
@@ -387,10 +304,22 @@ class HybridFusion(nn.Module):
             if x.size(-1) != in_f:
                 raise RuntimeError(f"modality '{name}': expected feature dim {in_f}, got {x.size(-1)}")
             dims.append(int(x.size(-1)))
-        return _Plan(self, seq, dims, B, self.present_pairs(), return_attention)
+        return seq, dims
+
+    def _param_names(self, pairs: List[Tuple[int, int, str]]) -> List[str]:
+        """The operator's parameter order: proj (w, b) per modality; per present pair
+        query, key, value, out (w, b); gates (w, b) per modality; classifier.0; classifier.3."""
+        names: List[str] = []
+        for m in self.modality_names:
+            names += [f"projections.{m}.0.weight", f"projections.{m}.0.bias"]
+        for _, _, key in pairs:
+            for proj in ("query_proj", "key_proj", "value_proj", "out_proj"):
+                names += [f"attention_modules.{key}.{proj}.weight", f"attention_modules.{key}.{proj}.bias"]
+        for m in self.modality_names:
+            names += [f"gating_layers.{m}.weight", f"gating_layers.{m}.bias"]
+        return names + ["classifier.0.weight", "classifier.0.bias", "classifier.3.weight", "classifier.3.bias"]
 
     # ------------------------------------------------------------------ forward
-    @torch.compiler.disable  # HIP library calls: opaque to TorchDynamo (runs eagerly)
     def forward(self, modality_features: Dict[str, torch.Tensor],
                 modality_mask: Optional[torch.Tensor] = None, return_attention: bool = False):
         if not self.modality_names:
@@ -412,19 +341,23 @@ class HybridFusion(nn.Module):
             if p.device != device or p.dtype != torch.float32:
                 raise RuntimeError("mmfusion HybridFusion needs float32 parameters on the input's device "
                                    f"(found {p.dtype} on {p.device})")
-        plan = self._plan(feats, return_attention)
-        params = plan.params(self)
-        mask32 = _nat.f32c(modality_mask)
-        outs = _HybridFunction.apply(plan, self._rng_state, mask32, *[_nat.f32c(x) for x in feats], *params)
-        logits, fw, maps = outs[0], outs[1], outs[2:]
+        seq, dims = self._shapes(feats)
+        pairs = self.present_pairs()
+        named = dict(self.named_parameters())
+        params = [named[n] for n in self._param_names(pairs)]
+        idesc = _ops.hybrid_idesc(batch_size, self.hidden_dim, self.num_heads, self.num_classes, seq, dims,
+                                  [(q, k) for q, k, _ in pairs], self.training, return_attention, _precision())
+        logits, fw, _saved, rng_next, maps = torch.ops.mmfusion.hybrid_fwd(
+            idesc, float(self.dropout.p), self._rng_state, _nat.f32c(modality_mask),
+            [_nat.f32c(x) for x in feats], params)
+        self._rng_state.copy_(rng_next)     # the device Philox stream advanced by one call
         if dtype != torch.float32 and dtype.is_floating_point:
             logits = logits.to(dtype)
         if return_attention:
-            attention_maps = {key: maps[g] for g, (_, _, key) in enumerate(plan.pairs)}
-            return logits, {"attention_maps": attention_maps, "fusion_weights": fw}
+            attention_maps = {key: maps[g].detach() for g, (_, _, key) in enumerate(pairs)}
+            return logits, {"attention_maps": attention_maps, "fusion_weights": fw.detach()}
         return logits
 
-    @torch.compiler.disable  # HIP library calls: opaque to TorchDynamo (runs eagerly)
     def compute_adaptive_weights(self, modality_features: Dict[str, torch.Tensor],
                                  modality_mask: torch.Tensor) -> torch.Tensor:
         """src/fusion.py:429-479 on the device (gating scores -> masked softmax -> renormalise).
@@ -452,69 +385,7 @@ class HybridFusion(nn.Module):
         for name in self.modality_names:
             layer = self.gating_layers[name]
             gparams += [layer.weight, layer.bias]
-        return _AdaptiveWeightsFunction.apply(M, H, _nat.f32c(mask), *[_nat.f32c(f) for f in feats], *gparams)
-
-
-class _AdaptiveWeightsFunction(torch.autograd.Function):
-    """compute_adaptive_weights (src/fusion.py:429-479) forward and backward on HIP
-    (mmf_adaptive_weights / mmf_adaptive_weights_backward, csrc/head.hip).
-    inputs: M, H, mask (B, M), feats x M (B, H), then (gate weight, gate bias) x M."""
-
-    @staticmethod
-    def forward(ctx, M, H, mask, *tensors):
-        L = _nat.lib()
-        feats, gparams = tensors[:M], tensors[M:]
-        dev = mask.device
-        B = mask.size(0)
-        gates = (_nat.Linear * M)()
-        for m in range(M):
-            gates[m] = _nat.Linear(gparams[2 * m].data_ptr(), gparams[2 * m + 1].data_ptr())
-        out = torch.empty(B, M, dtype=torch.float32, device=dev)
-        ws = torch.empty(L.mmf_adaptive_weights_workspace_bytes(B, M, H), dtype=torch.uint8, device=dev)
-        farr = _nat.ptr_array([f.data_ptr() for f in feats])
-        rc = L.mmf_adaptive_weights(B, M, H, ctypes.cast(farr, ctypes.c_void_p), mask.data_ptr(),
-                                    ctypes.cast(gates, ctypes.c_void_p), out.data_ptr(), ws.data_ptr(),
-                                    _nat.stream_ptr(dev))
-        _nat.check(rc, "compute_adaptive_weights")
-        ctx.M, ctx.H = M, H
-        ctx.save_for_backward(mask, *tensors)
-        ctx.mark_non_differentiable(mask)
-        return out
-
-    @staticmethod
-    def backward(ctx, dweights):
-        L = _nat.lib()
-        M, H = ctx.M, ctx.H
-        mask, *tensors = ctx.saved_tensors
-        feats, gparams = tensors[:M], tensors[M:]
-        dev = mask.device
-        B = mask.size(0)
-        dweights = _nat.f32c(dweights)
-        need_x = any(ctx.needs_input_grad[3:3 + M])
-        need_g = any(ctx.needs_input_grad[3 + M:])
-        dfeats = torch.empty(B, M, H, dtype=torch.float32, device=dev) if need_x else None
-        gates = (_nat.Linear * M)()
-        dgates = (_nat.Linear * M)()
-        ggrads: List[Optional[torch.Tensor]] = []
-        for m in range(M):
-            w, b = gparams[2 * m], gparams[2 * m + 1]
-            gates[m] = _nat.Linear(w.data_ptr(), b.data_ptr())
-            if need_g:
-                gw = torch.empty_like(w, dtype=torch.float32)
-                gb = torch.empty_like(b, dtype=torch.float32)
-                dgates[m] = _nat.Linear(gw.data_ptr(), gb.data_ptr())
-                ggrads += [gw, gb]
-            else:
-                ggrads += [None, None]
-        ws = torch.empty(L.mmf_adaptive_weights_workspace_bytes(B, M, H), dtype=torch.uint8, device=dev)
-        farr = _nat.ptr_array([f.data_ptr() for f in feats])
-        rc = L.mmf_adaptive_weights_backward(B, M, H, ctypes.cast(farr, ctypes.c_void_p), mask.data_ptr(),
-                                             ctypes.cast(gates, ctypes.c_void_p), dweights.data_ptr(),
-                                             _nat.ptr(dfeats), ctypes.cast(dgates, ctypes.c_void_p) if need_g
-                                             else None, ws.data_ptr(), _nat.stream_ptr(dev))
-        _nat.check(rc, "compute_adaptive_weights backward")
-        dx = [dfeats[:, m] if dfeats is not None and ctx.needs_input_grad[3 + m] else None for m in range(M)]
-        return (None, None, None, *dx, *ggrads)
+        return torch.ops.mmfusion.adaptive_weights_fwd(_nat.f32c(mask), [_nat.f32c(f) for f in feats], gparams)
 
 
 def build_fusion_model(fusion_type: str, modality_dims: Dict[str, int], num_classes: int,

@@ -214,11 +214,25 @@ class ManifestShards:
         feats, labels, lens = self.gather(torch.tensor([idx]), T=self.chunks[idx][2] - self.chunks[idx][1])
         return feats, labels, self.modality_mask(1)
 
+    def rank_chunk_ids(self, rank: int = 0, world: int = 1, shuffle: bool = False, seed: int = 0,
+                       epoch: int = 0) -> List[int]:
+        """The chunks rank `rank` of `world` data-parallel ranks visits in one epoch: torch's
+        DistributedSampler partition of the split's chunk list (harness.shard_indices).  The
+        manifest loader's batch is one chunk (src/data.py:560-566), so each rank takes every
+        world-th chunk of the (shuffled) list and all ranks run ceil(n / world) steps."""
+        from harness import shard_indices
+        return shard_indices(len(self.chunks), rank, world, shuffle=shuffle, seed=seed, epoch=epoch)
+
     def batches(self, batch_size: int, shuffle: bool = False, generator: Optional[torch.Generator] = None,
-                drop_last: bool = False):
-        """Iterate ({m: (B, T, c_m)}, labels, mask, lengths) batches over every chunk of the split."""
-        n = len(self.chunks)
-        order = torch.randperm(n, generator=generator) if shuffle else torch.arange(n)
+                drop_last: bool = False, rank: int = 0, world: int = 1, seed: int = 0, epoch: int = 0):
+        """Iterate ({m: (B, T, c_m)}, labels, mask, lengths) batches over every chunk of the split
+        (world > 1: over this rank's shard of the chunks, rank_chunk_ids)."""
+        if world > 1:
+            order = torch.tensor(self.rank_chunk_ids(rank, world, shuffle, seed, epoch), dtype=torch.int64)
+        else:
+            n = len(self.chunks)
+            order = torch.randperm(n, generator=generator) if shuffle else torch.arange(n)
+        n = int(order.numel())
         for i in range(0, n, batch_size):
             ids = order[i:i + batch_size]
             if drop_last and ids.numel() < batch_size:

@@ -48,9 +48,12 @@ def _dropout(x: torch.Tensor, p: float, train: bool, gen, site: int = 0) -> torc
         return x
     if callable(gen):
         keep = gen(site, x).to(x.dtype)
-    else:
-        keep = (torch.rand(x.shape, generator=gen, dtype=x.dtype) >= p).to(x.dtype)
-    return x * keep / (1.0 - p)
+        return x * keep / (1.0 - p)
+    # the same ATen ops as nn.Dropout's CPU path (at::dropout: bernoulli_(1 - p) noise scaled
+    # by 1 / (1 - p), times the input), so the timed CPU baseline pays what the reference pays
+    noise = torch.empty_like(x).bernoulli_(1.0 - p, generator=gen)
+    noise.div_(1.0 - p)
+    return x * noise
 
 
 # dropout site ids (mirror of the device's Philox streams, csrc/mmf_internal.h)

@@ -12,10 +12,13 @@ if [ -z "$SKIP_TESTS" ]; then
   if [ $rc -ne 0 ]; then exit $rc; fi
 fi
 i=0
-for spec in "$@"; do
+for spec0 in "$@"; do
+  # spec: workload[:bench args][@VAR=VAL] (one environment assignment for the run)
+  spec=${spec0%%@*}; envset=""
+  [ "$spec0" != "$spec" ] && envset=${spec0#*@}
   wl=${spec%%:*}; extra=""
   [ "$spec" != "$wl" ] && extra=${spec#*:}
   i=$((i+1))
-  timeout -k 10 300 python -u bench.py --workload $wl --steps 50 --warmup 10 --skip-cpu $extra > $O/bench_${i}_$wl.json 2> $O/bench_${i}_$wl.err || exit 1
-  python3 -c "import json;d=json.load(open('$O/bench_${i}_$wl.json'));print('$spec', d['ms_per_step'], d.get('ms_per_step_median'), d['value']);print(json.dumps(d['kernels'],indent=0)[:1500])"
+  env $envset timeout -k 10 300 python -u bench.py --workload $wl --steps 50 --warmup 10 --skip-cpu $extra > $O/bench_${i}_$wl.json 2> $O/bench_${i}_$wl.err || exit 1
+  python3 -c "import json;d=json.load(open('$O/bench_${i}_$wl.json'));print('$spec0', d['ms_per_step'], d.get('ms_per_step_median'), d['value']);print(json.dumps(d['kernels'],indent=0)[:1500])"
 done

@@ -1,59 +1,193 @@
-"""torch.compile wrapping of the drop-in module: the reference's
-trainer may wrap the fusion model with torch.compile (config compile_mode);
-the module must keep working under it, give the eager results, and its state
-dict must round-trip with the `_orig_mod.` prefix compile adds.
+"""torch.compile of the drop-in modules (SURVEY §8b "C-ABI to export").
 
-backend="eager" exercises TorchDynamo's capture of the module (graph breaks
-at the HIP library calls) without needing a code generator."""
+The reference wraps its fusion model and encoders in
+torch.compile(backend="inductor", mode="reduce-overhead") (src/train.py:193-231,
+config/base.yaml:76-79).  The library's entry points are torch custom operators with
+fake kernels and autograd formulas (mmf_ops.py), so TorchDynamo traces each module
+into ONE graph (fullgraph=True: a graph break would raise), AOTAutograd sees the
+forward and backward operators, and "reduce-overhead" replays the step as a HIP graph.
+The compiled forward + backward must equal eager bit for bit (the same kernels run),
+in eval and in train mode (the device dropout state advances identically), and the
+compiled module's state dict round-trips with the `_orig_mod.` prefix.
+"""
 import pytest
 import torch
 
-from cases import HYBRID_CASES, hybrid_inputs, hybrid_state
+from cases import CMA_CASES, HYBRID_CASES, cma_inputs, cma_state, hybrid_inputs, hybrid_state
 
 pytestmark = pytest.mark.gpu
+STEPS = 3   # cudagraph trees record on the first replays: compare every step
 
 
 @pytest.fixture(scope="module")
-def fusion_mod(pkg_on_path):
+def mods(pkg_on_path):
     if not torch.cuda.is_available():
         pytest.fail("no ROCm device visible")
+    import attention
+    import encoders
     import fusion
-    return fusion
+    import harness
+    return fusion, attention, encoders, harness
 
 
-def test_compiled_module_matches_eager(fusion_mod):
-    case = next(c for c in HYBRID_CASES if c.name == "seq_c2_b3")
+def _hybrid(fusion, case, p=0.1):
     sd = hybrid_state(case.names, case.dims, case.hidden, case.classes, case.seed)
-    model = fusion_mod.HybridFusion({m: case.dims[m] for m in case.names}, hidden_dim=case.hidden,
-                                    num_classes=case.classes, num_heads=case.heads, dropout=0.1)
+    model = fusion.HybridFusion({m: case.dims[m] for m in case.names}, hidden_dim=case.hidden,
+                                num_classes=case.classes, num_heads=case.heads, dropout=p)
     model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
-    model = model.cuda().eval()
-    feats_np, mask_np, grad_np = hybrid_inputs(case)
-    mask = torch.from_numpy(mask_np).cuda()
-    g = torch.from_numpy(grad_np).cuda()
+    return model.cuda()
 
-    def run(m):
+
+def _run_steps(m, owner, feats_np, mask, g, rng0):
+    """STEPS fwd+bwd calls from the same device dropout state; clones of every output / grad."""
+    owner._rng_state.copy_(rng0)
+    outs = []
+    for _ in range(STEPS):
         feats = {k: torch.from_numpy(v).cuda().requires_grad_(True) for k, v in feats_np.items()}
-        for p in m.parameters():
-            p.grad = None
+        for prm in owner.parameters():
+            prm.grad = None
         out = m(feats, mask)
         (out * g).sum().backward()
         torch.cuda.synchronize()
-        return out.detach().clone(), {k: f.grad.clone() for k, f in feats.items()}, \
-            {n.replace("_orig_mod.", ""): p.grad.clone() for n, p in m.named_parameters()}
+        outs.append((out.detach().clone(), {k: f.grad.clone() for k, f in feats.items()},
+                     {n: prm.grad.clone() for n, prm in owner.named_parameters()}, owner._rng_state.clone()))
+    return outs
 
-    ref_out, ref_dx, ref_dw = run(model)
+
+@pytest.mark.parametrize("train", [False, True], ids=["eval", "train"])
+@pytest.mark.parametrize("case_name", ["seq_c2_b3", "tiny_l1"])
+def test_hybrid_compile_reduce_overhead_fullgraph_bit_identical(mods, case_name, train):
+    fusion = mods[0]
+    case = next(c for c in HYBRID_CASES if c.name == case_name)
+    model = _hybrid(fusion, case)
+    model.train(train)
+    feats_np, mask_np, grad_np = hybrid_inputs(case)
+    mask, g = torch.from_numpy(mask_np).cuda(), torch.from_numpy(grad_np).cuda()
+    rng0 = torch.tensor([0x5EED, 11], dtype=torch.int64)
+    ref = _run_steps(model, model, feats_np, mask, g, rng0)
     torch._dynamo.reset()
-    compiled = torch.compile(model, backend="eager")
-    out, dx, dw = run(compiled)
-    assert torch.equal(out, ref_out)
-    for k in ref_dx:
-        assert torch.equal(dx[k], ref_dx[k]), k
-    for n in ref_dw:
-        assert torch.equal(dw[n], ref_dw[n]), n
+    compiled = torch.compile(model, mode="reduce-overhead", fullgraph=True)
+    got = _run_steps(compiled, model, feats_np, mask, g, rng0)
+    for step, ((ro, rdx, rdw, rr), (co, cdx, cdw, cr)) in enumerate(zip(ref, got)):
+        assert torch.equal(co, ro), step
+        assert torch.equal(cr, rr), step            # the dropout state advanced the same way
+        for k in rdx:
+            assert torch.equal(cdx[k], rdx[k]), (step, k)
+        for n in rdw:
+            assert torch.equal(cdw[n], rdw[n]), (step, n)
+    if train:
+        assert not torch.equal(ref[0][0], ref[1][0])   # dropout masks differ between steps
     keys = list(compiled.state_dict().keys())
     assert all(k.startswith("_orig_mod.") for k in keys)
-    plain = fusion_mod.HybridFusion({m: case.dims[m] for m in case.names}, hidden_dim=case.hidden,
-                                    num_classes=case.classes, num_heads=case.heads, dropout=0.1).cuda()
+    plain = _hybrid(fusion, case)
     plain.load_state_dict({k[len("_orig_mod."):]: v for k, v in compiled.state_dict().items()})
+    torch._dynamo.reset()
+
+
+def test_hybrid_compile_return_attention_and_adaptive_weights(mods):
+    """return_attention (maps + fusion weights) and the public compute_adaptive_weights trace too."""
+    fusion = mods[0]
+    case = next(c for c in HYBRID_CASES if c.name == "seq_equal")
+    model = _hybrid(fusion, case).eval()
+    feats_np, mask_np, _ = hybrid_inputs(case)
+    feats = {k: torch.from_numpy(v).cuda() for k, v in feats_np.items()}
+    mask = torch.from_numpy(mask_np).cuda()
+    ref_l, ref_i = model(feats, mask, return_attention=True)
+    torch._dynamo.reset()
+    fn = torch.compile(lambda f, m: model(f, m, return_attention=True), fullgraph=True)
+    l, info = fn(feats, mask)
+    assert torch.equal(l, ref_l) and torch.equal(info["fusion_weights"], ref_i["fusion_weights"])
+    for k in ref_i["attention_maps"]:
+        assert torch.equal(info["attention_maps"][k], ref_i["attention_maps"][k]), k
+    pooled = {m: torch.randn(case.batch, case.hidden, device="cuda", requires_grad=True) for m in case.names}
+    aw_ref = model.compute_adaptive_weights(pooled, mask)
+    aw_ref.sum().backward()
+    ref_g = {m: t.grad.clone() for m, t in pooled.items()}
+    for t in pooled.values():
+        t.grad = None
+    torch._dynamo.reset()
+    aw = torch.compile(model.compute_adaptive_weights, fullgraph=True)(pooled, mask)
+    aw.sum().backward()
+    assert torch.equal(aw, aw_ref)
+    for m in case.names:
+        assert torch.equal(pooled[m].grad, ref_g[m]), m
+    torch._dynamo.reset()
+
+
+@pytest.mark.parametrize("case_name", ["cma_3d_mask2d", "cma_2d_mask1d", "cma_3d_wide_hd128"])
+def test_cma_compile_fullgraph_bit_identical(mods, case_name):
+    attention = mods[1]
+    case = next(c for c in CMA_CASES if c.name == case_name)
+    model = attention.CrossModalAttention(case.query_dim, case.key_dim, hidden_dim=case.hidden,
+                                          num_heads=case.heads, dropout=0.1)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in cma_state(case.query_dim, case.key_dim, case.hidden,
+                                                                        case.seed).items()})
+    model = model.cuda().train()
+    q, k, v, mask, grad = cma_inputs(case)
+    mt = torch.from_numpy(mask).cuda() if mask is not None else None
+    gt = torch.from_numpy(grad).cuda()
+
+    def run(m):
+        model._rng_state.copy_(torch.tensor([77, 3], dtype=torch.int64))
+        res = []
+        for _ in range(STEPS):
+            qt, kt, vt = (torch.from_numpy(a).cuda().requires_grad_(True) for a in (q, k, v))
+            for prm in model.parameters():
+                prm.grad = None
+            att, w = m(qt, kt, vt, mt)
+            (att * gt).sum().backward()
+            torch.cuda.synchronize()
+            res.append([att.detach().clone(), w.clone(), qt.grad.clone(), kt.grad.clone(), vt.grad.clone()]
+                       + [prm.grad.clone() for prm in model.parameters()])
+        return res
+
+    ref = run(model)
+    torch._dynamo.reset()
+    got = run(torch.compile(model, mode="reduce-overhead", fullgraph=True))
+    for a, b in zip(ref, got):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+    torch._dynamo.reset()
+
+
+def test_encoders_and_full_model_compile_fullgraph(mods):
+    """The reference compiles each encoder too (src/train.py:203-214): SequenceEncoder (HIP LSTM
+    recurrence), FrameEncoder (HIP attention pooling), and the whole encoders -> LayerNorm ->
+    HybridFusion model, fullgraph, equal to eager."""
+    _, _, encoders, harness = mods
+    torch.manual_seed(4)
+    seq = encoders.SequenceEncoder(17, hidden_dim=64, output_dim=32, num_layers=2, dropout=0.0).cuda()
+    frame = encoders.FrameEncoder(48, hidden_dim=32, output_dim=32, dropout=0.0).cuda()
+    x = torch.randn(3, 20, 17, device="cuda", requires_grad=True)
+    fr = torch.randn(3, 9, 48, device="cuda", requires_grad=True)
+    fmask = torch.ones(3, 9, device="cuda")
+    fmask[1, 4:] = 0
+    for mod, args in ((seq, (x,)), (frame, (fr, fmask))):
+        ref = mod(*args)
+        ref.square().sum().backward()
+        ref_g = [a.grad.clone() for a in args if a.requires_grad] + [p.grad.clone() for p in mod.parameters()]
+        for a in args:
+            a.grad = None
+        for p in mod.parameters():
+            p.grad = None
+        torch._dynamo.reset()
+        out = torch.compile(mod, fullgraph=True)(*args)
+        out.square().sum().backward()
+        got_g = [a.grad.clone() for a in args if a.requires_grad] + [p.grad.clone() for p in mod.parameters()]
+        assert torch.equal(out, ref), type(mod).__name__
+        for a, b in zip(got_g, ref_g):
+            assert torch.equal(a, b), type(mod).__name__
+    # encoders -> LayerNorm -> HybridFusion (config/base.yaml's PAMAP2 model, smaller hidden)
+    enc = {m: {"type": "sequence", "input_dim": 17 if m != "heart_rate" else 1, "encoder_type": "lstm",
+               "num_layers": 1} for m in ("imu_hand", "imu_chest", "heart_rate")}
+    cfg = {"dataset": {"modalities": list(enc), "num_classes": 25},
+           "model": {"fusion_type": "hybrid", "hidden_dim": 64, "output_dim": 32, "num_heads": 4,
+                     "dropout": 0.0, "layer_norm": True, "encoders": enc}}
+    model = harness.MultimodalFusionModel.from_config(cfg).cuda().eval()
+    feats = {m: torch.randn(2, 30, enc[m]["input_dim"], device="cuda") for m in enc}
+    mask = torch.tensor([[1.0, 1.0, 1.0], [1.0, 0.0, 1.0]], device="cuda")
+    ref = model(feats, mask)
+    torch._dynamo.reset()
+    got = torch.compile(model, fullgraph=True)(feats, mask)
+    assert torch.equal(got, ref)
     torch._dynamo.reset()

@@ -54,7 +54,7 @@ def precision(request):
 
 
 def _precision_arg(kname):
-    m = re.search(r"[<, ]([012])(?:, (?:true|false))?>$", kname)
+    m = re.search(r"[<, ]([012])(?:, (?:true|false)){0,2}>$", kname)
     return int(m.group(1)) if m else None
 
 

@@ -164,7 +164,7 @@ def test_late_weights_vs_oracle_large(fusion_mod):
     sr, wr = st.clone().requires_grad_(True), wl.clone().requires_grad_(True)
     (late_weights(sr, wr, mask) * gf).sum().backward()
     sd, wd = st.to(dev).requires_grad_(True), wl.to(dev).requires_grad_(True)
-    out = fusion_mod._LateWeightFunction.apply(sd, wd, mask.to(dev))
+    out = fusion_mod._late_weights(sd, wd, mask.to(dev))
     (out * gf.to(dev)).sum().backward()
     assert rel_err(out.detach(), late_weights(st, wl, mask)) <= TOL
     assert rel_err(sd.grad, sr.grad) <= TOL

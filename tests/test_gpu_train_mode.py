@@ -187,3 +187,40 @@ def test_long_key_plan_selection(mods):
         names = {k.split("<")[0] for _, k, *_ in launches}
         for k in expect[case.name]:
             assert k in names, (case.name, k, sorted(names))
+
+
+def test_stored_probabilities_plan(mods):
+    """Training with every pair inside the lean fused backward's shape keeps the forward's
+    probabilities (attn_pool_fwd_lean<..., PST = true>) and the fused backward reads them
+    instead of recomputing S (attn_pool_bwd_fused_lean<..., true>); MMF_NO_PSTORE=1 in the
+    environment would select the recompute (A/B).  Parity of this plan is
+    test_hybrid_train_mode_matches_oracle[train_lean]."""
+    import os
+    fusion, _ = mods
+    import mmf_native
+    if os.environ.get("MMF_NO_PSTORE"):
+        pytest.skip("MMF_NO_PSTORE set")
+    case = next(c for c in TRAIN_CASES if c.name == "train_lean")
+    sd = hybrid_state(case.names, case.dims, case.hidden, case.classes, case.seed)
+    model = fusion.HybridFusion({m: case.dims[m] for m in case.names}, hidden_dim=case.hidden,
+                                num_classes=case.classes, num_heads=case.heads, dropout=P)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    model = model.cuda().train()
+    feats_np, mask_np, _ = hybrid_inputs(case)
+    feats = {m: torch.from_numpy(v).cuda().requires_grad_(True) for m, v in feats_np.items()}
+    mmf_native.profile_begin()
+    model(feats, torch.from_numpy(mask_np).cuda()).sum().backward()
+    _, launches = mmf_native.profile_end()
+    names = [k for _, k, *_ in launches]
+    fwd = [k for k in names if k.startswith("attn_pool_fwd_lean")]
+    bwd = [k for k in names if k.startswith("attn_pool_bwd_fused_lean")]
+    assert fwd and all(k.endswith("true, true>") for k in fwd), fwd
+    assert bwd and all(k.endswith("true>") for k in bwd), bwd
+    # eval mode: nothing stored, the backward recomputes
+    model.eval()
+    mmf_native.profile_begin()
+    model(feats, torch.from_numpy(mask_np).cuda()).sum().backward()
+    _, launches = mmf_native.profile_end()
+    bwd = [k for _, k, *_ in launches if k.startswith("attn_pool_bwd_fused_lean")]
+    assert bwd and all(k.endswith("false>") for k in bwd), bwd
+

@@ -77,6 +77,23 @@ def test_host_logic_matches_reference(man, tmp_path):
         man.parse_manifest(bad / "splits" / "test.txt")
 
 
+def test_rank_sharding_of_chunks(man, tmp_path):
+    """DP over the PAMAP2 chunk list (one chunk per rank per step): every rank gets
+    ceil(n / world) chunks (DistributedSampler's wrap padding), together they cover the split."""
+    fx = load_fixture("manifest_pamap2")
+    root, _ = _write_split(tmp_path, fx)
+    ds = man.ManifestShards(root, "test", MODALITIES, chunk_size=CHUNK, device="cpu")
+    n = len(ds)
+    assert n == 5
+    for world in (1, 2, 4):
+        parts = [ds.rank_chunk_ids(r, world, shuffle=True, seed=42, epoch=1) for r in range(world)]
+        assert all(len(p) == -(-n // world) for p in parts)
+        assert set(i for p in parts for i in p) == set(range(n))
+    # epochs reshuffle, the same epoch is reproducible
+    assert ds.rank_chunk_ids(0, 2, True, 42, 1) == ds.rank_chunk_ids(0, 2, True, 42, 1)
+    assert ds.rank_chunk_ids(0, 2, True, 42, 1) != ds.rank_chunk_ids(0, 2, True, 42, 2) or n < 3
+
+
 @pytest.mark.gpu
 def test_gpu_gather_matches_reference(man, tmp_path):
     fx = load_fixture("manifest_pamap2")
