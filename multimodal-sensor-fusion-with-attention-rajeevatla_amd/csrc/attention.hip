@@ -2068,14 +2068,12 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
         case Kind::Prep: fl += 2.0 * bq; by += 4 * 2 * bq; break;                         // dO, O -> D
         case Kind::Dkv: fl += 3 * qk; by += 4 * (3 * bq + 4 * bk); break;               // Q K V dO -> dK dV
         case Kind::Dq: fl += qk; by += 4 * (3 * bq + 2 * bk); break;                    // Q K V dO -> dQ
-        case Kind::PoolFwd:                                                               // Q K -> lse, pbar (P)
-          fl += qk; by += 4 * (bq + bk + (pst ? (double)B * heads * attn_pstore_floats((int)lq) : 0.0));
-          break;
+        case Kind::PoolFwd: fl += qk; by += 4 * (bq + bk); break;                         // Q K -> lse, pbar
         case Kind::PoolDq: fl += qk; by += 4 * (2 * bq + bk); break;                      // Q K -> dQ
         case Kind::PoolDk: fl += qk; by += 4 * (bq + 2 * bk); break;                      // Q K -> dK
-        case Kind::PoolFused:                                                             // Q K (P) -> dQ dK
-          fl += 2 * qk; by += 4 * (2 * bq + 2 * bk + (pst ? (double)B * heads * attn_pstore_floats((int)lq) : 0.0));
-          break;
+        // (the stored-P plan's P blob is the plan's own intermediate, not the reference algorithm's
+        // operand bytes: not counted; PMC traffic shows it)
+        case Kind::PoolFused: fl += 2 * qk; by += 4 * (2 * bq + 2 * bk); break;           // Q K -> dQ dK
         case Kind::PoolLse: fl += qk; by += 4 * (bq + bk); break;                         // Q K -> lse
         case Kind::PoolColsum: by += 4 * (bq + bk); break;                                // (S recomputed) -> pbar
         case Kind::PoolDqLong: fl += qk; by += 4 * (2 * bq + bk); break;                  // Q K -> dQ
@@ -2225,6 +2223,8 @@ hipError_t launch_attn_pool_fwd(const AttnPair* pairs, int npairs, int B, int he
   split_by_keys(pairs, npairs, sp, lp);
   hipError_t e = hipSuccess;
   if (!sp.empty()) e = launch_generic(Kind::PoolFwd, sp.data(), (int)sp.size(), B, heads, hd, scale, drop_p, rng, st);
+  if (e == hipSuccess && !lp.empty() && attn_long_fwd_ok(lp.data(), (int)lp.size(), hd, drop_p, rng))
+    return launch_attn_long_fused_fwd(lp.data(), (int)lp.size(), B, heads, hd, scale, drop_p, rng, st);
   if (e == hipSuccess && !lp.empty())
     e = launch_generic(Kind::PoolLse, lp.data(), (int)lp.size(), B, heads, hd, scale, drop_p, rng, st);
   if (e == hipSuccess && !lp.empty())
@@ -2239,8 +2239,14 @@ hipError_t launch_attn_pool_bwd(int stage, const AttnPair* pairs, int npairs, in
   std::vector<AttnPair> sp, lp;
   split_by_keys(pairs, npairs, sp, lp);
   if (stage == 2) {
-    if (!lp.empty()) return hipErrorNotSupported;
-    return launch_generic(Kind::PoolFused, pairs, npairs, B, heads, hd, scale, drop_p, rng, st);
+    // every long-key pair on the one-pass bf16 kernel (attn_long.hip), or none: checked before
+    // anything launches, so hipErrorNotSupported leaves the caller to run stages 0 and 1
+    if (!lp.empty() && !attn_long_fused_ok(lp.data(), (int)lp.size(), hd, drop_p)) return hipErrorNotSupported;
+    hipError_t e = hipSuccess;
+    if (!sp.empty()) e = launch_generic(Kind::PoolFused, sp.data(), (int)sp.size(), B, heads, hd, scale, drop_p, rng, st);
+    if (e == hipSuccess && !lp.empty())
+      e = launch_attn_long_fused_bwd(lp.data(), (int)lp.size(), B, heads, hd, scale, drop_p, st);
+    return e;
   }
   hipError_t e = hipSuccess;
   if (!sp.empty())

@@ -1,0 +1,627 @@
+// Long-key pooled attention backward in one pass, bf16 operands ("medium").
+//
+// The pooled formulation's backward (src/attention.py:118-139 under the pooled output of
+// src/fusion.py:406-408) needs, per (pair, sample, head):
+//   P[q, k]  = exp(s[q, k] - lse[q]),  s = scale q.k
+//   D[q]     = sum_k keep[q, k] P[q, k] g[k],          g[k] = dpbar[k] / ((1 - p) Lq)
+//   dS[q, k] = P[q, k] (keep[q, k] g[k] - D[q])
+//   dQ = scale dS K,  dK = scale dS^T Q.
+// The two-kernel path (attn_poolL_dq_kernel: a D pass and a dS pass over the keys, then
+// attn_pool_bwd_dk_kernel) recomputes S and exp three times per score; at C5's Lk = 512
+// those kernels are bound by the vector ALU, not the matrix cores or HBM.  Here one
+// workgroup (8 waves) owns every key of one (pair, sample, head):
+//   * the key image (Lk x 64 bf16) is staged in LDS once;
+//   * wave w owns key tiles w and w + 8 (32 keys each) and walks the queries in blocks of
+//     32: S^T = K Q^T on the matrix cores (query on the lane), P and its partial D in
+//     registers, the partial D's of the 8 waves summed through LDS (fixed order), then dS
+//     from the registers -- one exp per score;
+//   * dQ = dS K takes dS straight from the accumulator registers and K through transposed
+//     LDS reads (ds_read_b64_tr_b16); the 8 waves' partial dQ tiles are summed through LDS
+//     in a fixed order (deterministic) and stored;
+//   * dK += dS^T Q stays in registers for the whole pass: dS goes through a per-wave LDS
+//     tile and comes back transposed (ds_read_b64_tr_b16), Q likewise from its block image.
+// Images: 128-B rows with the 16-B chunk c of row r at c ^ swk(r) (conflict-free row reads
+// of the 32x32x16 operands and 4-row transposed reads); the dS tile: 64-B rows, chunk
+// g at g ^ ((q >> 1) & 3); the dQ partials: [d][q] fp32, 16-B chunk j at j ^ f(d).
+// Conditions (attn_long_fused_ok): 128 < Lk <= 512, Lk % 32 == 0, no per-key mask,
+// head_dim <= 64 and % 4, float4-able Q / K rows; dropout through the forward's keep words.
+#include <cstdlib>
+#include <cstring>
+
+#include "mmf_device.h"
+
+namespace mmf {
+
+namespace {
+
+constexpr int LF_NT = 512;                 // 8 waves: two per SIMD
+constexpr int LF_MAXK = 512;
+constexpr int LF_QB = 32;                  // queries per block
+constexpr float LF_LOG2E = 1.4426950408889634f;
+
+constexpr int OFF_K = 0;                               // [LF_MAXK][64] bf16
+constexpr int OFF_Q = OFF_K + LF_MAXK * 128;           // [2][32][64] bf16
+constexpr int OFF_S = OFF_Q + 2 * LF_QB * 128;         // [8][32 q][32 keys] bf16
+constexpr int OFF_R = OFF_S + 8 * LF_QB * 64;          // [8][64 d][32 q] fp32
+constexpr int OFF_D = OFF_R + 8 * 64 * LF_QB * 4;      // [2][8][32] fp32
+constexpr int OFF_G = OFF_D + 2 * 8 * LF_QB * 4;       // [LF_MAXK] fp32
+constexpr int OFF_L = OFF_G + LF_MAXK * 4;             // [2][32] fp32
+constexpr int LF_LDS = OFF_L + 2 * LF_QB * 4;          // 160,000 bytes
+static_assert(LF_LDS <= 160 * 1024, "one workgroup per CU");
+
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+__device__ __forceinline__ int swk(int row) { return (((row >> 1) & 1) << 2) | ((row >> 2) & 3); }
+// byte offset of 16-B chunk c (columns 8c .. 8c+7) of row `row` of a 128-B-row bf16 image
+__device__ __forceinline__ int img_off(int row, int c) { return row * 128 + 16 * (c ^ swk(row)); }
+// byte offset of the 4 columns d0 .. d0+3 (d0 % 4 == 0) of row `row`
+__device__ __forceinline__ int img_off4(int row, int d0) { return img_off(row, d0 >> 3) + 2 * (d0 & 7); }
+// the dS tile: 64-B rows (32 keys), 16-B chunk g (keys 8g .. 8g+7) at g ^ ((q >> 1) & 3)
+__device__ __forceinline__ int ds_off4(int q, int key0) {
+  return q * 64 + 16 * ((key0 >> 3) ^ ((q >> 1) & 3)) + 2 * (key0 & 7);
+}
+// the dQ partials: [d][32 q] fp32, 16-B chunk j (queries 4j .. 4j+3) at j ^ f(d)
+__device__ __forceinline__ int red_off(int d, int j) {
+  return d * 32 + 4 * (j ^ ((d & 7) ^ ((d >> 4) & 1)));
+}
+
+__device__ __forceinline__ bf16x4 tr_read(const char* lds, int off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(lds + off));
+}
+__device__ __forceinline__ bf16x8 cat8(bf16x4 lo, bf16x4 hi) {
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+__device__ __forceinline__ bf16x8 to_bf16x8(float4 a, float4 b) {
+  bf16x8 v;
+  v[0] = (__bf16)a.x; v[1] = (__bf16)a.y; v[2] = (__bf16)a.z; v[3] = (__bf16)a.w;
+  v[4] = (__bf16)b.x; v[5] = (__bf16)b.y; v[6] = (__bf16)b.z; v[7] = (__bf16)b.w;
+  return v;
+}
+__device__ __forceinline__ f32x16 mfma_bf16(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 zero16f() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// 8 columns [d0, d0 + 8) of a row (zero past hd; hd % 4 == 0, 16-B aligned rows)
+__device__ __forceinline__ void load8(const float* row, int d0, int hd, bool valid, float4& a, float4& b) {
+  a = make_float4(0.f, 0.f, 0.f, 0.f);
+  b = a;
+  if (valid && d0 < hd) a = *reinterpret_cast<const float4*>(row + d0);
+  if (valid && d0 + 4 < hd) b = *reinterpret_cast<const float4*>(row + d0 + 4);
+}
+
+template <bool BITS>
+__global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const AttnArgs A) {
+  __shared__ __attribute__((aligned(16))) char lds[LF_LDS];
+  const AttnPair& P = A.p[blockIdx.y];
+  if ((int)blockIdx.x >= A.B * A.heads) return;
+  const int head = blockIdx.x % A.heads, b = blockIdx.x / A.heads;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, hh = lane >> 5, r = lane & 31;
+  // transposed-read addressing: lane 4 qp + pp of each 16-lane group g16 names row qp,
+  // columns 4 pp .. 4 pp + 3 of the group's 16 columns (16 (g16 & 1) ..)
+  const int g16 = lane >> 4, qp = (lane & 15) >> 2, pp = lane & 3;
+  const int hd = A.hd, col0 = head * hd;
+  const int Lq = P.Lq, Lk = P.Lk, nkt = Lk >> 5, nqb = (Lq + LF_QB - 1) / LF_QB, kwl = P.kw_ld;
+  const int64_t bh = (int64_t)b * A.heads + head;
+  const float scale = A.scale, pdrop = A.drop_p;
+  const float inv_keep = pdrop > 0.f ? (pdrop < 1.f ? 1.f / (1.f - pdrop) : 0.f) : 1.f;
+  const float sl2 = scale * LF_LOG2E;
+  const float* Qg = P.q + (int64_t)b * Lq * P.ldq + col0;
+  const float* Kg = P.k + (int64_t)b * Lk * P.ldk + col0;
+  float* dQg = P.dq + (int64_t)b * Lq * P.ldq + col0;
+  float* dKg = P.dk + (int64_t)b * Lk * P.ldk + col0;
+
+  if (P.kmask_mode == 1 && P.kmask[(int64_t)b * P.kmask_ld] == 0.f) {
+    // masked key modality: every probability is 0 (src/attention.py:127-129), so are dQ, dK, D
+    for (int i = t; i < Lq * hd; i += LF_NT) dQg[(int64_t)(i / hd) * P.ldq + i % hd] = 0.f;
+    for (int i = t; i < Lk * hd; i += LF_NT) dKg[(int64_t)(i / hd) * P.ldk + i % hd] = 0.f;
+    for (int i = t; i < Lq; i += LF_NT) P.dsum[bh * Lq + i] = 0.f;
+    return;
+  }
+
+  float* gs = reinterpret_cast<float*>(lds + OFF_G);
+  float* lse_s = reinterpret_cast<float*>(lds + OFF_L);
+  float* Dpart = reinterpret_cast<float*>(lds + OFF_D);
+
+  // ---- prologue: the key image, g, and query block 0
+  {
+    const int nch = Lk * 8;   // 16-B chunks of the image
+    for (int i0 = 0; i0 < nch; i0 += LF_NT * 4) {
+      float4 va[4], vb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int idx = i0 + t + j * LF_NT;
+        const int key = idx >> 3, c = idx & 7;
+        load8(Kg + (int64_t)(idx < nch ? key : 0) * P.ldk, 8 * c, hd, idx < nch, va[j], vb[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int idx = i0 + t + j * LF_NT;
+        if (idx < nch) *reinterpret_cast<bf16x8*>(lds + OFF_K + img_off(idx >> 3, idx & 7)) = to_bf16x8(va[j], vb[j]);
+      }
+    }
+    const float gsc = inv_keep / (float)Lq;   // dP'[q, k] = dpbar[k] / Lq, through the dropout scale
+    for (int k = t; k < Lk; k += LF_NT) gs[k] = P.dpbar[bh * Lk + k] * gsc;
+  }
+  // query block images: threads 0..255 stage row t >> 3, chunk t & 7; threads 256..287 the LSE
+  auto q_load = [&](int qb, float4& a, float4& bq, float& l) {
+    const int row = (t >> 3) & 31, q = qb * LF_QB + row;
+    load8(Qg + (int64_t)(q < Lq ? q : 0) * P.ldq, 8 * (t & 7), hd, t < 256 && q < Lq, a, bq);
+    const int ql = qb * LF_QB + (t & 31);
+    l = (t >= 256 && t < 256 + LF_QB && ql < Lq) ? P.lse[bh * Lq + ql] : -INFINITY;
+  };
+  auto q_store = [&](int buf, const float4& a, const float4& bq, float l) {
+    if (t < 256) *reinterpret_cast<bf16x8*>(lds + OFF_Q + buf * 4096 + img_off(t >> 3, t & 7)) = to_bf16x8(a, bq);
+    // log2 units; +inf for an invalid or fully masked query: every p = exp2(s - inf) = 0
+    if (t >= 256 && t < 256 + LF_QB) lse_s[buf * LF_QB + (t - 256)] = l == -INFINITY ? INFINITY : l * LF_LOG2E;
+  };
+  {
+    float4 a, bq;
+    float l;
+    q_load(0, a, bq, l);
+    q_store(0, a, bq, l);
+  }
+  __syncthreads();
+
+  f32x16 dk[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) dk[i][dt] = zero16f();
+  char* Sw = lds + OFF_S + w * 2048;
+  float* redw = reinterpret_cast<float*>(lds + OFF_R) + w * 2048;
+
+  for (int qb = 0; qb < nqb; ++qb) {
+    const int buf = qb & 1, qbase = qb * LF_QB;
+    const bool has_next = qb + 1 < nqb;
+    float4 na = make_float4(0.f, 0.f, 0.f, 0.f), nb = na;
+    float nl = -INFINITY;
+    if (has_next) q_load(qb + 1, na, nb, nl);   // in flight during this block
+    const char* Qi = lds + OFF_Q + buf * 4096;
+    const int q = qbase + r;
+    const bool qvalid = q < Lq;
+    uint32_t words[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
+    if (BITS && qvalid) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int kt = w + 8 * i;
+        if (kt < nkt) words[i] = P.keep_bits[(bh * Lq + q) * kwl + kt] >> (4 * hh);
+      }
+    }
+    bf16x8 qf[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(Qi + img_off(r, 2 * s + hh));
+    const float lse2 = lse_s[buf * LF_QB + r];
+
+    // S^T = K Q^T per own key tile (key in the registers, query on the lane); P, keep * P * g, D
+    float pv[2][16], pk[2][16];
+    float Dp = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int kt = w + 8 * i;
+      if (kt >= nkt) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) pv[i][e] = pk[i][e] = 0.f;
+        continue;
+      }
+      f32x16 s = zero16f();
+      const int krow = kt * 32 + r;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+        s = mfma_bf16(*reinterpret_cast<const bf16x8*>(lds + OFF_K + img_off(krow, 2 * s4 + hh)), qf[s4], s);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 g4 = *reinterpret_cast<const float4*>(gs + kt * 32 + 8 * g + 4 * hh);
+        const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int e = 4 * g + j;
+          const float p = __builtin_amdgcn_exp2f(s[e] * sl2 - lse2);
+          const float gk = ((words[i] >> (j + 8 * g)) & 1u) ? gv[j] : 0.f;
+          pv[i][e] = p;
+          pk[i][e] = p * gk;
+          Dp += pk[i][e];
+        }
+      }
+    }
+    Dp = sum_xor32(Dp);
+    if (hh == 0) Dpart[buf * 256 + w * 32 + r] = Dp;
+    if (has_next) q_store(buf ^ 1, na, nb, nl);
+    __syncthreads();   // (A) partial D's, next query block
+
+    float D = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 8; ++ww) D += Dpart[buf * 256 + ww * 32 + r];
+    if (w == 0 && hh == 0 && qvalid) P.dsum[bh * Lq + q] = D;
+
+    f32x16 dq[2] = {zero16f(), zero16f()};
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int kt = w + 8 * i;
+      if (kt >= nkt) continue;
+      // dS = P (keep g - D) as the bf16 A operand of dQ = dS K (register e = 8 s2 + j)
+      bf16x8 da[2];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int e = 8 * s2 + j;
+          da[s2][j] = (__bf16)__builtin_fmaf(-pv[i][e], D, pk[i][e]);
+        }
+      // dQ[q][d] += sum_key dS[q][key] K[key][d]: K rows 32 kt + 16 s2 + 4 hh + {0..3, 8..11}
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int d0 = 32 * dt + 16 * (g16 & 1) + 4 * pp;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int k0 = kt * 32 + 16 * s2 + 4 * hh + qp;
+          const bf16x8 kb = cat8(tr_read(lds, OFF_K + img_off4(k0, d0)), tr_read(lds, OFF_K + img_off4(k0 + 8, d0)));
+          dq[dt] = mfma_bf16(da[s2], kb, dq[dt]);
+        }
+      }
+      // the dS tile [q][key] (registers 4g .. 4g+3 = keys 8g + 4hh + 0..3 of query r)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = da[g >> 1][4 * (g & 1) + j];
+        *reinterpret_cast<bf16x4*>(Sw + ds_off4(r, 8 * g + 4 * hh)) = v;
+      }
+      // dK[key][d] += sum_q dS[q][key] Q[q][d]: queries 16 s + 8 hh + {0..7}
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int q0 = 16 * s + 8 * hh + qp;
+        const int key0 = 16 * (g16 & 1) + 4 * pp;
+        const bf16x8 sa = cat8(tr_read(Sw, ds_off4(q0, key0)), tr_read(Sw, ds_off4(q0 + 4, key0)));
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const int d0 = 32 * dt + 16 * (g16 & 1) + 4 * pp;
+          const bf16x8 qb8 = cat8(tr_read(Qi, img_off4(q0, d0)), tr_read(Qi, img_off4(q0 + 4, d0)));
+          dk[i][dt] = mfma_bf16(sa, qb8, dk[i][dt]);
+        }
+      }
+    }
+    // this wave's partial dQ tile: lane = d, registers 4g .. 4g+3 = queries 8g + 4hh + 0..3
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      const int d = 32 * dt + r;
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<float4*>(redw + red_off(d, 2 * g + hh)) =
+            make_float4(dq[dt][4 * g], dq[dt][4 * g + 1], dq[dt][4 * g + 2], dq[dt][4 * g + 3]);
+    }
+    __syncthreads();   // (B) partial dQ's
+
+    {
+      const int d = t & 63, j = t >> 6;   // queries 4j .. 4j+3 of column d
+      const float* red = reinterpret_cast<const float*>(lds + OFF_R);
+      float4 acc = *reinterpret_cast<const float4*>(red + red_off(d, j));
+#pragma unroll
+      for (int ww = 1; ww < 8; ++ww) {
+        const float4 v = *reinterpret_cast<const float4*>(red + ww * 2048 + red_off(d, j));
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+      const float av[4] = {acc.x, acc.y, acc.z, acc.w};
+      if (d < hd) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int qq = qbase + 4 * j + e;
+          if (qq < Lq) dQg[(int64_t)qq * P.ldq + d] = av[e] * scale;
+        }
+      }
+    }
+  }
+
+  // dK: lane = d, registers = keys 32 kt + acc_row(e, hh)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int kt = w + 8 * i;
+    if (kt >= nkt) continue;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      const int d = 32 * dt + r;
+      if (d >= hd) continue;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) dKg[(int64_t)(kt * 32 + acc_row(e, hh)) * P.ldk + d] = dk[i][dt][e] * scale;
+    }
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// Forward in one pass (same conditions; "medium"): LSE, the dropout keep words and
+// pbar = mean_q P' for every key of one (pair, sample, head).  Per 32-query block each
+// wave forms S^T for its two key tiles, the 8 waves' row maxima and sums meet in LDS
+// (fixed order), and P' = keep * exp2(s - m) * (1-p)^-1 / (l Lq) -- one exp per score,
+// where the two-kernel path (attn_poolL_lse_kernel + attn_poolL_colsum_kernel) recomputes
+// S and exp in a second pass.  The column sums over the queries (the lanes) go through a
+// per-wave transposed P' tile (bf16, as the reference's P'.V operand at "medium") into an
+// all-ones MFMA whose accumulator carries pbar across the query blocks.
+// ---------------------------------------------------------------------------
+constexpr int FOFF_K = 0;                               // [LF_MAXK][64] bf16
+constexpr int FOFF_Q = FOFF_K + LF_MAXK * 128;          // [2][32][64] bf16
+constexpr int FOFF_P = FOFF_Q + 2 * LF_QB * 128;        // [8][32 q][32 keys] bf16
+constexpr int FOFF_M = FOFF_P + 8 * LF_QB * 64;         // [2][8][32] fp32 row maxima
+constexpr int FOFF_S = FOFF_M + 2 * 8 * LF_QB * 4;      // [2][8][32] fp32 row sums
+constexpr int LFF_LDS = FOFF_S + 2 * 8 * LF_QB * 4;     // 96,256 bytes
+
+template <bool DROP>
+__global__ __launch_bounds__(LF_NT, 1) void attn_poolL_fwd_fused_bf16(const AttnArgs A) {
+  __shared__ __attribute__((aligned(16))) char lds[LFF_LDS];
+  const AttnPair& P = A.p[blockIdx.y];
+  if ((int)blockIdx.x >= A.B * A.heads) return;
+  const int head = blockIdx.x % A.heads, b = blockIdx.x / A.heads;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, hh = lane >> 5, r = lane & 31;
+  const int g16 = lane >> 4, qp = (lane & 15) >> 2, pp = lane & 3;
+  const int hd = A.hd, col0 = head * hd;
+  const int Lq = P.Lq, Lk = P.Lk, nkt = Lk >> 5, nqb = (Lq + LF_QB - 1) / LF_QB, kwl = P.kw_ld;
+  const int64_t bh = (int64_t)b * A.heads + head;
+  const float pdrop = A.drop_p;
+  const float inv_keep = pdrop > 0.f ? (pdrop < 1.f ? 1.f / (1.f - pdrop) : 0.f) : 1.f;
+  const float sl2 = A.scale * LF_LOG2E;
+  const float* Qg = P.q + (int64_t)b * Lq * P.ldq + col0;
+  const float* Kg = P.k + (int64_t)b * Lk * P.ldk + col0;
+
+  if (P.kmask_mode == 1 && P.kmask[(int64_t)b * P.kmask_ld] == 0.f) {
+    // masked key modality: every probability is 0 (src/attention.py:127-129); the keep words
+    // are never read when LSE = -inf
+    for (int i = t; i < Lq; i += LF_NT) P.lse[bh * Lq + i] = -INFINITY;
+    for (int k = t; k < Lk; k += LF_NT) {
+      P.pbar[bh * Lk + k] = 0.f;
+      if (P.pbarT) P.pbarT[((int64_t)b * Lk + k) * A.heads + head] = 0.f;
+    }
+    return;
+  }
+  RngSnap rs{0, 0};
+  if (DROP) rs = *A.rng;
+  float* Mpart = reinterpret_cast<float*>(lds + FOFF_M);
+  float* Spart = reinterpret_cast<float*>(lds + FOFF_S);
+
+  {
+    const int nch = Lk * 8;
+    for (int i0 = 0; i0 < nch; i0 += LF_NT * 4) {
+      float4 va[4], vb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int idx = i0 + t + j * LF_NT;
+        load8(Kg + (int64_t)(idx < nch ? idx >> 3 : 0) * P.ldk, 8 * (idx & 7), hd, idx < nch, va[j], vb[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int idx = i0 + t + j * LF_NT;
+        if (idx < nch) *reinterpret_cast<bf16x8*>(lds + FOFF_K + img_off(idx >> 3, idx & 7)) = to_bf16x8(va[j], vb[j]);
+      }
+    }
+  }
+  auto q_load = [&](int qb, float4& a, float4& bq) {
+    const int q = qb * LF_QB + ((t >> 3) & 31);
+    load8(Qg + (int64_t)(q < Lq ? q : 0) * P.ldq, 8 * (t & 7), hd, t < 256 && q < Lq, a, bq);
+  };
+  auto q_store = [&](int buf, const float4& a, const float4& bq) {
+    if (t < 256) *reinterpret_cast<bf16x8*>(lds + FOFF_Q + buf * 4096 + img_off(t >> 3, t & 7)) = to_bf16x8(a, bq);
+  };
+  {
+    float4 a, bq;
+    q_load(0, a, bq);
+    q_store(0, a, bq);
+  }
+  __syncthreads();
+
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
+  f32x16 cs[2] = {zero16f(), zero16f()};   // every row of C = the column sums of P'
+  char* Pw = lds + FOFF_P + w * 2048;
+
+  for (int qb = 0; qb < nqb; ++qb) {
+    const int buf = qb & 1, qbase = qb * LF_QB;
+    const bool has_next = qb + 1 < nqb;
+    float4 na = make_float4(0.f, 0.f, 0.f, 0.f), nb = na;
+    if (has_next) q_load(qb + 1, na, nb);
+    const char* Qi = lds + FOFF_Q + buf * 4096;
+    const int q = qbase + r;
+    const bool qvalid = q < Lq;
+    bf16x8 qf[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(Qi + img_off(r, 2 * s + hh));
+    float x[2][16];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int kt = w + 8 * i;
+      if (kt >= nkt) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) x[i][e] = -INFINITY;
+        continue;
+      }
+      f32x16 s = zero16f();
+      const int krow = kt * 32 + r;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+        s = mfma_bf16(*reinterpret_cast<const bf16x8*>(lds + FOFF_K + img_off(krow, 2 * s4 + hh)), qf[s4], s);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        x[i][e] = s[e] * sl2;   // log2 units
+        mx = fmaxf(mx, x[i][e]);
+      }
+    }
+    mx = max_xor32(mx);
+    if (hh == 0) Mpart[buf * 256 + w * 32 + r] = mx;
+    if (has_next) q_store(buf ^ 1, na, nb);
+    __syncthreads();   // (A) row maxima, next query block
+    float m = -INFINITY;
+#pragma unroll
+    for (int ww = 0; ww < 8; ++ww) m = fmaxf(m, Mpart[buf * 256 + ww * 32 + r]);
+    const float mref = m == -INFINITY ? 0.f : m;
+    float ls = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        x[i][e] = __builtin_amdgcn_exp2f(x[i][e] - mref);
+        ls += x[i][e];
+      }
+    ls = sum_xor32(ls);
+    if (hh == 0) Spart[buf * 256 + w * 32 + r] = ls;
+    // keep words of the own tiles (all lanes draw: keep_tile16 shuffles)
+    uint32_t kb[2] = {0xFFFFu, 0xFFFFu};
+    if (DROP) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int kt = w + 8 * i;
+        if (kt >= nkt) continue;
+        kb[i] = keep_tile16(rs, P.drop_site, (uint64_t)(bh * Lq + q) * Lk + kt * 32, pdrop, hh, qvalid, true);
+        uint32_t bits = 0;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) bits |= ((kb[i] >> (4 * g)) & 0xFu) << (8 * g + 4 * hh);
+        bits = or_xor32(bits);
+        if (qvalid && hh == 0) P.keep_bits[(bh * Lq + q) * kwl + kt] = bits;
+      }
+    }
+    __syncthreads();   // (B) row sums
+    float l = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 8; ++ww) l += Spart[buf * 256 + ww * 32 + r];
+    if (w == 0 && hh == 0 && qvalid) P.lse[bh * Lq + q] = l > 0.f ? (m + __log2f(l)) * (1.f / LF_LOG2E) : -INFINITY;
+    // P' / Lq of this lane's query (0 for a query past Lq)
+    const float cq = (qvalid && l > 0.f) ? inv_keep / (l * (float)Lq) : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int kt = w + 8 * i;
+      if (kt >= nkt) continue;
+      // the P' tile [q][key], registers 4g .. 4g+3 = keys 8g + 4hh + 0..3
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int e = 4 * g + j;
+          v[j] = (__bf16)(((kb[i] >> e) & 1u) ? x[i][e] * cq : 0.f);
+        }
+        *reinterpret_cast<bf16x4*>(Pw + ds_off4(r, 8 * g + 4 * hh)) = v;
+      }
+      // C[.][key] += sum_q 1 * P'[q][key]
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int q0 = 16 * s + 8 * hh + qp;
+        const int key0 = 16 * (g16 & 1) + 4 * pp;
+        const bf16x8 pb = cat8(tr_read(Pw, ds_off4(q0, key0)), tr_read(Pw, ds_off4(q0 + 4, key0)));
+        cs[i] = mfma_bf16(ones, pb, cs[i]);
+      }
+    }
+  }
+  // pbar: lane = key, every register the same column sum
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int kt = w + 8 * i;
+    if (kt >= nkt || hh != 0) continue;
+    const int key = kt * 32 + r;
+    P.pbar[bh * Lk + key] = cs[i][0];
+    if (P.pbarT) P.pbarT[((int64_t)b * Lk + key) * A.heads + head] = cs[i][0];
+  }
+}
+
+}  // namespace
+
+bool attn_long_fused_ok(const AttnPair* pairs, int npairs, int hd, float drop_p) {
+  if (getenv("MMF_NO_LONG_FUSED")) return false;
+  if (math_mode() != 1 || hd > 64 || hd % 4 != 0 || npairs <= 0) return false;
+  for (int i = 0; i < npairs; ++i) {
+    const AttnPair& P = pairs[i];
+    if (P.Lk <= 128 || P.Lk > LF_MAXK || P.Lk % 32 != 0 || P.Lq < 1 || P.kmask_mode == 2) return false;
+    if (P.ldq % 4 != 0 || P.ldk % 4 != 0 || ((uintptr_t)P.q & 15) != 0 || ((uintptr_t)P.k & 15) != 0) return false;
+    if (!P.dq || !P.dk || !P.dsum || !P.dpbar || !P.lse) return false;
+    if (drop_p > 0.f && (!P.keep_bits || P.kw_ld < P.Lk / 32)) return false;
+  }
+  return true;
+}
+
+bool attn_long_fwd_ok(const AttnPair* pairs, int npairs, int hd, float drop_p, const RngSnap* rng) {
+  if (getenv("MMF_NO_LONG_FUSED")) return false;
+  if (math_mode() != 1 || hd > 64 || hd % 4 != 0 || npairs <= 0) return false;
+  if (drop_p > 0.f && !rng) return false;
+  for (int i = 0; i < npairs; ++i) {
+    const AttnPair& P = pairs[i];
+    if (P.Lk <= 128 || P.Lk > LF_MAXK || P.Lk % 32 != 0 || P.Lq < 1 || P.kmask_mode == 2) return false;
+    if (P.ldq % 4 != 0 || P.ldk % 4 != 0 || ((uintptr_t)P.q & 15) != 0 || ((uintptr_t)P.k & 15) != 0) return false;
+    if (!P.lse || !P.pbar) return false;
+    if (drop_p > 0.f && (!P.keep_bits || P.kw_ld < P.Lk / 32)) return false;
+  }
+  return true;
+}
+
+hipError_t launch_attn_long_fused_fwd(const AttnPair* pairs, int npairs, int B, int heads, int hd, float scale,
+                                      float drop_p, const RngSnap* rng, hipStream_t st) {
+  if (!attn_long_fwd_ok(pairs, npairs, hd, drop_p, rng)) return hipErrorNotSupported;
+  const bool drop = drop_p > 0.f;
+  for (int done = 0; done < npairs;) {
+    AttnArgs a;
+    memset(&a, 0, sizeof(a));
+    int n = 0;
+    double fl = 0.0, by = 0.0;
+    while (done < npairs && n < ATTN_MAX_PAIRS) {
+      a.p[n] = pairs[done++];
+      const double lq = a.p[n].Lq, lk = a.p[n].Lk, H = (double)heads * hd;
+      // S = QK^T and the column-sum contraction (the pooled P'V's share, as PoolFwd)
+      fl += 2.0 * B * lq * lk * H;
+      by += 4.0 * (B * lq * H + B * lk * H);   // Q, K in (lse, pbar, keep words small)
+      ++n;
+    }
+    a.npairs = n;
+    a.B = B;
+    a.heads = heads;
+    a.hd = hd;
+    a.scale = scale;
+    a.drop_p = drop_p;
+    a.rng = rng;
+    a.nblk = B * heads;
+    const dim3 grid((unsigned)(B * heads), (unsigned)n);
+    ProfLaunch prof_(st, drop ? "attn_poolL_fwd_fused_bf16<true>" : "attn_poolL_fwd_fused_bf16<false>", fl, by);
+    if (drop) mmf_launch(attn_poolL_fwd_fused_bf16<true>, grid, dim3(LF_NT), 0, st, a);
+    else mmf_launch(attn_poolL_fwd_fused_bf16<false>, grid, dim3(LF_NT), 0, st, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_attn_long_fused_bwd(const AttnPair* pairs, int npairs, int B, int heads, int hd, float scale,
+                                      float drop_p, hipStream_t st) {
+  if (!attn_long_fused_ok(pairs, npairs, hd, drop_p)) return hipErrorNotSupported;
+  const bool bits = drop_p > 0.f;
+  for (int done = 0; done < npairs;) {
+    AttnArgs a;
+    memset(&a, 0, sizeof(a));
+    int n = 0;
+    double fl = 0.0, by = 0.0;
+    while (done < npairs && n < ATTN_MAX_PAIRS) {
+      a.p[n] = pairs[done++];
+      const double lq = a.p[n].Lq, lk = a.p[n].Lk, H = (double)heads * hd;
+      fl += 2.0 * (2.0 * B * lq * lk * H);          // dQ and dK contractions (S recompute not counted)
+      by += 4.0 * (2.0 * B * lq * H + 2.0 * B * lk * H);   // Q, K in; dQ, dK out
+      ++n;
+    }
+    a.npairs = n;
+    a.B = B;
+    a.heads = heads;
+    a.hd = hd;
+    a.scale = scale;
+    a.drop_p = drop_p;
+    a.nblk = B * heads;
+    const dim3 grid((unsigned)(B * heads), (unsigned)n);
+    ProfLaunch prof_(st, bits ? "attn_poolL_bwd_fused_bf16<true>" : "attn_poolL_bwd_fused_bf16<false>", fl, by);
+    if (bits) mmf_launch(attn_poolL_bwd_fused_bf16<true>, grid, dim3(LF_NT), 0, st, a);
+    else mmf_launch(attn_poolL_bwd_fused_bf16<false>, grid, dim3(LF_NT), 0, st, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace mmf

@@ -276,6 +276,15 @@ hipError_t launch_attn_pool_fwd(const AttnPair* pairs, int npairs, int B, int he
                                 float drop_p, const RngSnap* rng, hipStream_t st);
 hipError_t launch_attn_pool_bwd(int stage, const AttnPair* pairs, int npairs, int B, int heads, int hd,
                                 float scale, float drop_p, const RngSnap* rng, hipStream_t st);
+// Long-key pooled backward in one pass (attn_long.hip, bf16 "medium" only): dQ, dK and D of
+// pairs with 128 < Lk <= 512 (Lk % 32 == 0, no per-key mask, head_dim <= 64 and % 4).
+bool attn_long_fused_ok(const AttnPair* pairs, int npairs, int hd, float drop_p);
+// ... and its forward (LSE, keep words, pbar) in one pass
+bool attn_long_fwd_ok(const AttnPair* pairs, int npairs, int hd, float drop_p, const RngSnap* rng);
+hipError_t launch_attn_long_fused_fwd(const AttnPair* pairs, int npairs, int B, int heads, int hd, float scale,
+                                      float drop_p, const RngSnap* rng, hipStream_t st);
+hipError_t launch_attn_long_fused_bwd(const AttnPair* pairs, int npairs, int B, int heads, int hd, float scale,
+                                      float drop_p, hipStream_t st);
 
 // ---------------------------------------------------------------------------
 // Single-key attention (single_key.hip): Lk == 1, the reference's 2-D inputs.

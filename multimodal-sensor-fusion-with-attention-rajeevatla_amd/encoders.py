@@ -164,18 +164,76 @@ def check_lstm_timeouts(device=None) -> None:
                            "fully co-resident); the affected encodings / gradients are NaN")
 
 
-def lstm_layers(rnns: Sequence[nn.LSTM], inputs: Sequence[torch.Tensor]) -> List[torch.Tensor]:
-    """Run several nn.LSTM parameter sets (batch_first, zero initial state) over their inputs on the
-    HIP recurrence, every layer of all of them in one launch; returns each LSTM's top-layer output
-    sequence (B, T, H).  Inter-layer dropout follows nn.LSTM (training only)."""
+class LSTM(nn.Module):
+    """nn.LSTM's constructor, attributes, parameter names / shapes / registration order and
+    initialisation (uniform(-1/sqrt(hidden), 1/sqrt(hidden)) over the parameters in order), so
+    the same seed gives the same weights and state dicts load either way -- but not an
+    nn.RNNBase: TorchDynamo refuses to trace RNNBase modules at all ("Attempted to wrap RNN"),
+    which would break the reference's torch.compile of its encoders (src/train.py:203-214).
+    The recurrence runs on HIP (csrc/lstm.hip) through lstm_layers.  Supported: biased,
+    unidirectional, no projection, zero initial state (the reference's configuration,
+    src/encoders.py:68-76)."""
+
+    def __init__(self, input_size: int, hidden_size: int, num_layers: int = 1, bias: bool = True,
+                 batch_first: bool = False, dropout: float = 0.0, bidirectional: bool = False, proj_size: int = 0):
+        super().__init__()
+        if not bias or bidirectional or proj_size:
+            raise NotImplementedError("LSTM path: biased, unidirectional, no projection")
+        if num_layers < 1:
+            raise ValueError("num_layers must be >= 1")
+        self.input_size, self.hidden_size, self.num_layers = input_size, hidden_size, num_layers
+        self.bias, self.batch_first, self.dropout = bias, batch_first, float(dropout)
+        self.bidirectional, self.proj_size = False, 0
+        for k in range(num_layers):
+            din = input_size if k == 0 else hidden_size
+            self.register_parameter(f"weight_ih_l{k}", nn.Parameter(torch.empty(4 * hidden_size, din)))
+            self.register_parameter(f"weight_hh_l{k}", nn.Parameter(torch.empty(4 * hidden_size, hidden_size)))
+            self.register_parameter(f"bias_ih_l{k}", nn.Parameter(torch.empty(4 * hidden_size)))
+            self.register_parameter(f"bias_hh_l{k}", nn.Parameter(torch.empty(4 * hidden_size)))
+        self.reset_parameters()
+
+    def reset_parameters(self) -> None:
+        stdv = 1.0 / (self.hidden_size ** 0.5) if self.hidden_size > 0 else 0.0
+        for w in self.parameters():
+            nn.init.uniform_(w, -stdv, stdv)
+
+    def extra_repr(self) -> str:
+        s = f"{self.input_size}, {self.hidden_size}, num_layers={self.num_layers}"
+        if self.batch_first:
+            s += ", batch_first=True"
+        if self.dropout:
+            s += f", dropout={self.dropout}"
+        return s
+
+    def forward(self, input: torch.Tensor, hx=None):
+        """-> output, (h_n, c_n) as nn.LSTM (zero initial state only).  c_n carries no gradient:
+        the recurrence's backward takes d(h) only, which is all the encoders use."""
+        if hx is not None:
+            raise NotImplementedError("LSTM path: zero initial state only")
+        if input.dim() != 3:
+            raise ValueError(f"Expected 3-D input, got shape {tuple(input.shape)}")
+        x = input if self.batch_first else input.transpose(0, 1)
+        finals: List[tuple] = []
+        out = lstm_layers([self], [x], finals)[0]
+        h_n = torch.stack([h for h, _ in finals])
+        c_n = torch.stack([c for _, c in finals]).detach()
+        return (out if self.batch_first else out.transpose(0, 1)), (h_n, c_n)
+
+
+def lstm_layers(rnns: Sequence[LSTM], inputs: Sequence[torch.Tensor],
+                finals: Optional[List[tuple]] = None) -> List[torch.Tensor]:
+    """Run several LSTM parameter sets (batch_first inputs, zero initial state) over their inputs on
+    the HIP recurrence, every layer of all of them in one launch; returns each LSTM's top-layer
+    output sequence (B, T, H).  Inter-layer dropout follows nn.LSTM (training only).  With
+    `finals`, the first LSTM's last (h, c) of every layer is appended to it."""
     n = len(rnns)
     if n == 0:
         return []
     H = rnns[0].hidden_size
     layers = rnns[0].num_layers
     for r in rnns:
-        if not r.batch_first or r.bidirectional or r.proj_size or not r.bias:
-            raise NotImplementedError("LSTM path: batch_first, unidirectional, biased, no projection")
+        if not r.bias or r.bidirectional or r.proj_size:
+            raise NotImplementedError("LSTM path: unidirectional, biased, no projection")
         if r.hidden_size != H or r.num_layers != layers:
             raise ValueError("lstm_layers: all LSTMs need the same hidden_size and num_layers")
     B, T = inputs[0].shape[:2]
@@ -192,10 +250,12 @@ def lstm_layers(rnns: Sequence[nn.LSTM], inputs: Sequence[torch.Tensor]) -> List
             x2 = _nat.f32c(x).reshape(B * T, -1)
             b = getattr(r, f"bias_ih_l{k}") + getattr(r, f"bias_hh_l{k}")
             xproj.append(torch.addmm(b, x2, getattr(r, f"weight_ih_l{k}").t()).view(B, T, -1))
-        hs, _cs, _gates, flag = torch.ops.mmfusion.lstm_layer_fwd(
+        hs, cs, _gates, flag = torch.ops.mmfusion.lstm_layer_fwd(
             xproj, [_nat.f32c(getattr(r, f"weight_hh_l{k}")) for r in rnns])
         if not torch.compiler.is_compiling():
             _record_timeout(flag)
+        if finals is not None:
+            finals.append((hs[0][:, -1], cs[0][:, -1]))
         cur = list(hs)
         if k + 1 < layers:
             cur = [torch.nn.functional.dropout(o, rnns[i].dropout, rnns[i].training) for i, o in enumerate(cur)]
@@ -217,7 +277,7 @@ class SequenceEncoder(nn.Module):
     encoder_type: str
     hidden_dim: int
     output_dim: int
-    rnn: Optional[nn.LSTM]
+    rnn: Optional[LSTM]
     conv_net: Optional[nn.Module]
     pool: Optional[nn.Module]
     input_projection: Optional[nn.Linear]
@@ -239,8 +299,8 @@ class SequenceEncoder(nn.Module):
         cast_self.transformer = None
         self.projection = nn.Identity()
         if encoder_type == "lstm":
-            cast_self.rnn = nn.LSTM(input_dim, hidden_dim, num_layers=num_layers, batch_first=True,
-                                    dropout=dropout if num_layers > 1 else 0.0)
+            cast_self.rnn = LSTM(input_dim, hidden_dim, num_layers=num_layers, batch_first=True,
+                                 dropout=dropout if num_layers > 1 else 0.0)
             self.projection = nn.Linear(hidden_dim, output_dim)
         elif encoder_type in ("gru", "cnn", "transformer"):
             raise NotImplementedError(f"encoder_type '{encoder_type}' is not on the MI355X path (only 'lstm')")

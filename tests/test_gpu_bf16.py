@@ -257,3 +257,60 @@ def test_c5_shape_vs_oracle(mods, precision):
         else:
             ok, e = norm_ok(p.grad, grads[name], egrads[name], S)
             assert ok, (name, e)
+
+
+# One-pass long-key forward and backward (csrc/attn_long.hip, "medium" only) against the
+# two-kernel paths they replace (MMF_NO_LONG_FUSED=1: attn_poolL_lse/colsum_kernel,
+# attn_poolL_dq_kernel + attn_pool_bwd_dk_kernel) on the same inputs, in TRAIN mode (both
+# draw the same Philox keep words), with
+# partial query blocks (a: 500 queries), 256- and 512-key pairs, a masked key modality in
+# one sample and the pairs whose keys are not whole 32-key tiles removed (they would send
+# the call to the two-kernel path).  Both are bf16 computations of the same math; they
+# differ by the rounding of P' (bf16 terms of the column sums) and dS (fma vs two ops) and
+# the summation order, so the bounds are the bf16 ones (LOGIT_RTOL, NORM_RTOL) relative to
+# the two-kernel result.
+LONG_TRAIN = HybridCase("long_train", ["a", "b", "c"], {"a": 48, "b": 64, "c": 32}, {"a": 500, "b": 512, "c": 256},
+                        batch=3, hidden=128, heads=2, classes=5, seed=77,
+                        mask=[[1, 1, 1], [1, 1, 0], [1, 0, 1]], deleted=["b_to_a", "c_to_a"])
+
+
+def test_long_key_one_pass_backward_matches_two_kernel_path(mods, medium, monkeypatch):
+    fusion, _, nat = mods
+    case = LONG_TRAIN
+    feats_np, mask_np, grad_np = hybrid_inputs(case)
+    mask = torch.from_numpy(mask_np).cuda()
+    g = torch.from_numpy(grad_np).cuda()
+
+    def run(two_kernel):
+        if two_kernel:
+            monkeypatch.setenv("MMF_NO_LONG_FUSED", "1")
+        else:
+            monkeypatch.delenv("MMF_NO_LONG_FUSED", raising=False)
+        model = build_hybrid(fusion, case).train()
+        model._rng_state.copy_(torch.tensor([1234, 5], dtype=torch.int64))
+        feats = {m: torch.from_numpy(v).cuda().requires_grad_(True) for m, v in feats_np.items()}
+        nat.profile_begin()
+        logits = model(feats, mask)
+        (logits * g).sum().backward()
+        torch.cuda.synchronize()
+        _, launches = nat.profile_end()
+        names = [k for _, k, *_ in launches]
+        return logits.detach(), {m: f.grad for m, f in feats.items()}, \
+            {n: p.grad.clone() for n, p in model.named_parameters()}, names
+
+    l1, dx1, dw1, n1 = run(False)
+    l2, dx2, dw2, n2 = run(True)
+    monkeypatch.delenv("MMF_NO_LONG_FUSED", raising=False)
+    assert any(k.startswith("attn_poolL_bwd_fused_bf16<true>") for k in n1), n1
+    assert any(k.startswith("attn_poolL_fwd_fused_bf16<true>") for k in n1), n1
+    assert not any(k.startswith(("attn_poolL_dq", "attn_poolL_lse", "attn_poolL_colsum")) for k in n1), n1
+    assert any(k.startswith("attn_poolL_dq") for k in n2), n2
+    ok, e = logits_ok(l1.cpu(), l2.cpu())
+    assert ok, e
+    S = group_scale([_t(v) for v in dx2.values()] + [_t(v) for v in dw2.values()])
+    for m in case.names:
+        ok, e = norm_ok(dx1[m], dx2[m], dx2[m], S)
+        assert ok, (m, e)
+    for n in dw2:
+        ok, e = norm_ok(dw1[n], dw2[n], dw2[n], S)
+        assert ok, (n, e)

@@ -174,9 +174,12 @@ def test_encoders_and_full_model_compile_fullgraph(mods):
         out = torch.compile(mod, fullgraph=True)(*args)
         out.square().sum().backward()
         got_g = [a.grad.clone() for a in args if a.requires_grad] + [p.grad.clone() for p in mod.parameters()]
-        assert torch.equal(out, ref), type(mod).__name__
+        # the encoders' torch ops around the HIP operators (input projections, the bias sum
+        # b_ih + b_hh, the output Linear) become inductor kernels whose reduction order is not
+        # eager's: equal to fp32 rounding, not bit for bit (the HIP operators are the same launches)
+        torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-6, msg=type(mod).__name__)
         for a, b in zip(got_g, ref_g):
-            assert torch.equal(a, b), type(mod).__name__
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6, msg=type(mod).__name__)
     # encoders -> LayerNorm -> HybridFusion (config/base.yaml's PAMAP2 model, smaller hidden)
     enc = {m: {"type": "sequence", "input_dim": 17 if m != "heart_rate" else 1, "encoder_type": "lstm",
                "num_layers": 1} for m in ("imu_hand", "imu_chest", "heart_rate")}
@@ -189,5 +192,5 @@ def test_encoders_and_full_model_compile_fullgraph(mods):
     ref = model(feats, mask)
     torch._dynamo.reset()
     got = torch.compile(model, fullgraph=True)(feats, mask)
-    assert torch.equal(got, ref)
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)
     torch._dynamo.reset()

@@ -167,3 +167,49 @@ def test_encode_sequences_batches_modalities(enc_mod):
     for m in dims:
         alone = encs[m](seqs[m], lengths)
         assert torch.equal(together[m], alone), m
+
+
+def test_lstm_module_matches_torch_layout_cpu(enc_mod):
+    """encoders.LSTM keeps nn.LSTM's parameter names, shapes, order and initialisation (same seed ->
+    same weights, state dicts interchangeable) without being an nn.RNNBase (Dynamo refuses those)."""
+    for layers, first in ((1, True), (2, True), (3, False)):
+        torch.manual_seed(11)
+        ref = torch.nn.LSTM(9, 32, num_layers=layers, batch_first=first, dropout=0.2 if layers > 1 else 0.0)
+        torch.manual_seed(11)
+        mine = enc_mod.LSTM(9, 32, num_layers=layers, batch_first=first, dropout=0.2 if layers > 1 else 0.0)
+        assert not isinstance(mine, torch.nn.RNNBase)
+        a, b = ref.state_dict(), mine.state_dict()
+        assert list(a) == list(b)
+        assert all(torch.equal(a[k], b[k]) for k in a)
+        mine.load_state_dict(a)
+        assert (mine.hidden_size, mine.num_layers, mine.batch_first) == (32, layers, first)
+    with pytest.raises(NotImplementedError):
+        enc_mod.LSTM(9, 32, bidirectional=True)
+    with pytest.raises(NotImplementedError):
+        enc_mod.LSTM(9, 32, proj_size=8)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch_first", [True, False])
+def test_lstm_module_forward_matches_torch(enc_mod, batch_first):
+    """LSTM(...)(x) -> output, (h_n, c_n) on the HIP recurrence == torch's nn.LSTM (eval) with the
+    same weights; d(input) and parameter gradients through output and h_n."""
+    torch.manual_seed(5)
+    ref = torch.nn.LSTM(12, 64, num_layers=2, batch_first=batch_first).to("cuda:0").eval()
+    mine = enc_mod.LSTM(12, 64, num_layers=2, batch_first=batch_first).to("cuda:0").eval()
+    mine.load_state_dict(ref.state_dict())
+    x = torch.randn(3, 25, 12, device="cuda:0")
+    if not batch_first:
+        x = x.transpose(0, 1).contiguous()
+    outs = []
+    for m in (ref, mine):
+        xi = x.clone().requires_grad_(True)
+        out, (h, c) = m(xi)
+        (out.square().sum() + h.sum()).backward()
+        outs.append((out.detach(), h.detach(), c.detach(), xi.grad, [p.grad for p in m.parameters()]))
+    (ro, rh, rc, rdx, rg), (mo, mh, mc, mdx, mg) = outs
+    assert mo.shape == ro.shape and mh.shape == rh.shape == (2, 3, 64) and mc.shape == rc.shape
+    for a, b in ((mo, ro), (mh, rh), (mc, rc), (mdx, rdx)):
+        assert rel_err(a, b.double().cpu().numpy()) <= TOL
+    for a, b in zip(mg, rg):
+        assert rel_err(a, b.double().cpu().numpy()) <= TOL
