@@ -260,12 +260,12 @@ class ModuleRunner:
         self.trainer = DPTrainer(model, accumulate=1, process_group=pg)
         self.loss = torch.zeros(())
 
-    def forward_backward(self):
+    def forward_backward(self, eager=False):
         for f in self.feats:
             f.grad = None
         feats = dict(zip(self.names, self.feats))
         self.trainer.flat.arm()
-        logits = self.fwd(feats, self.mask)
+        logits = (self.model if eager else self.fwd)(feats, self.mask)
         loss = torch.nn.functional.cross_entropy(logits, self.labels, label_smoothing=0.05)
         loss.backward()
         self.loss = loss.detach()
@@ -349,11 +349,15 @@ def main(argv=None):
 
     # kernel-level timing (eager): hipEvents around each launch group and each
     # kernel launch, on the launch stream (mmf_profile_begin/end)
-    trainer.forward_backward()
+    # (the compiled path's profile steps run its module eagerly: the same library launches,
+    # outside the graphs the compiled module captures)
+    prof_fb = (lambda: trainer.forward_backward(eager=True)) if isinstance(trainer, ModuleRunner) \
+        else trainer.forward_backward
+    prof_fb()
     torch.cuda.synchronize(dev)
     mmf_native.profile_begin()
     for _ in range(args.profile_steps):
-        trainer.forward_backward()
+        prof_fb()
     stages, launches = mmf_native.profile_end()
     if args.dump_launches and rank == 0:
         per = len(launches) // max(1, args.profile_steps)

@@ -137,8 +137,13 @@ namespace mmf {
 
 thread_local ProfArm* g_prof_arm = nullptr;
 
-bool prof_arm_begin(ProfArm& arm) {
-  if (!g_prof.on) return false;
+bool prof_capturing(hipStream_t st) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+
+bool prof_arm_begin(ProfArm& arm, hipStream_t st) {
+  if (!g_prof.on || prof_capturing(st)) return false;
   arm.a = g_prof.ev();
   arm.b = g_prof.ev();
   arm.launches = 0;

@@ -44,7 +44,7 @@ struct Stage {
   hipEvent_t a = nullptr;
   const char* outer = nullptr;
   Stage(const char* n, hipStream_t s) : name(n), st(s) {
-    if (g_prof.on) {
+    if (g_prof.on && !prof_capturing(s)) {
       outer = g_prof.cur_stage;
       g_prof.cur_stage = n;
       a = g_prof.ev();

@@ -53,9 +53,11 @@ bool use_tail(const mmf_hybrid_desc* d);
 
 // Training forward keeps the pre-dropout probabilities for the fused backward (no S recompute
 // there): the pooled plan with every attention-kernel pair inside the lean fused kernels' shape
-// (attn_pstore_ok).  All pairs or none (one launch each way).  MMF_NO_PSTORE=1: recompute (A/B).
+// (attn_pstore_ok).  All pairs or none (one launch each way).  Opt-in (MMF_PSTORE=1): measured
+// at C2 it costs more than it saves (the 402 MB blob's write and read slow the
+// neighbouring kernels more than the skipped recompute gains).
 bool pstore_on(const mmf_hybrid_desc* d) {
-  if (!d->training || !use_pool(d) || getenv("MMF_NO_PSTORE")) return false;
+  if (!d->training || !use_pool(d) || !getenv("MMF_PSTORE")) return false;
   const int hd = d->hidden / d->num_heads;
   int n = 0;
   for (int g = 0; g < d->num_pairs; ++g) {
@@ -623,8 +625,11 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
   //     (single-key pairs wrote theirs in sk_fwd; the general plan's sk_out does not)
   if (d->return_attention && attn_maps && d->num_pairs) {
     std::vector<AttnPair> pp;
-    for (const AttnPair& a : pairs)
-      if (a.probs) pp.push_back(a);
+    for (AttnPair a : pairs)
+      if (a.probs) {
+        a.pstore = nullptr;   // the stored-probability blob belongs to the pooled kernels only
+        pp.push_back(a);
+      }
     if (!pp.empty())
       STAGE_TRY("fwd.attn_probs", launch_attn_probs(pp.data(), (int)pp.size(), B, nh, hd, scale, p, rng, st));
     if (!pool) {

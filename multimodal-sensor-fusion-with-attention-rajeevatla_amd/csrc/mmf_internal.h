@@ -31,7 +31,10 @@ struct ProfArm {
   int launches = 0;
 };
 extern thread_local ProfArm* g_prof_arm;
-bool prof_arm_begin(ProfArm& arm);   // false when profiling is off
+// false when profiling is off or `st` is being captured into a graph (events recorded
+// inside a capture cannot be timed afterwards: the captured launches run untimed)
+bool prof_arm_begin(ProfArm& arm, hipStream_t st);
+bool prof_capturing(hipStream_t st);
 void prof_arm_end(ProfArm& arm, hipStream_t st, const char* kernel, double flops, double bytes);
 struct ProfLaunch {
   hipStream_t st;
@@ -40,7 +43,7 @@ struct ProfLaunch {
   ProfArm arm;
   bool armed;
   ProfLaunch(hipStream_t s, const char* k, double f, double b) : st(s), kernel(k), flops(f), bytes(b) {
-    armed = prof_arm_begin(arm);
+    armed = prof_arm_begin(arm, st);
   }
   ~ProfLaunch() {
     if (armed) prof_arm_end(arm, st, kernel, flops, bytes);

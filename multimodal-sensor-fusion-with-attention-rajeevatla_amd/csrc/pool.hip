@@ -7,7 +7,10 @@
 //             E_m = c_m/L_m (row broadcast) + sum_{g: key(g)=m} sum_h pbar_{g,h}^T dU_{g,h}
 // E_m is the part of dP_m that flows through value_proj (and the direct
 // aggregation term); the Q/K parts come from the dZ GEMM that adds E_m.
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "mmf_device.h"
 
@@ -154,9 +157,179 @@ __global__ __launch_bounds__(NT) void pool_e_kernel(const PoolEArgs a) {
   *reinterpret_cast<float4*>(E.out + ((int64_t)b * L + j) * H + 4 * c4) = acc;
 }
 
+// Key-modality groups: every pair whose key modality is m reads the same P_m[b]; one
+// workgroup per (sample, group) reads it once for all of them (a 5-pair group at C5 reads
+// 1/5 of the bytes the per-pair kernels do).  R = pairs x heads rows (<= POOL_GRP_ROWS).
+constexpr int POOL_GRP_MAX = 32;      // pairs per launch
+constexpr int POOL_GRP_ROWS = 32;     // (pair, head) rows per group
+struct PoolGrpArgs {
+  PoolPair p[POOL_GRP_MAX];
+  int32_t gbeg[POOL_GRP_MAX], gcnt[POOL_GRP_MAX];
+  int32_t ngroups, B, heads, hd, H;
+};
+
+// U_row = pbar_row P_k[b] and r_row = sum_j pbar_row[j] for the group's rows: thread
+// (c4 = t & 63, row group t >> 6) accumulates 4 columns of up to 8 rows over the keys
+__global__ __launch_bounds__(NT) void pool_u_grp_kernel(const PoolGrpArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float pbg[];   // [R][Lk]
+  const int b = blockIdx.x, gi = blockIdx.y, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int beg = a.gbeg[gi], heads = a.heads, H = a.H, H4 = H / 4;
+  const int R = a.gcnt[gi] * heads, Lk = a.p[beg].Lk;
+  for (int i = t; i < R * Lk; i += NT) {
+    const int row = i / Lk, j = i - row * Lk;
+    const PoolPair& P = a.p[beg + row / heads];
+    pbg[i] = P.pbar[((int64_t)b * heads + row % heads) * Lk + j];
+  }
+  __syncthreads();
+  for (int row = wave; row < R; row += NT / 64) {
+    float s = 0.f;
+    for (int j = lane; j < Lk; j += 64) s += pbg[row * Lk + j];
+    s = sum64(s);
+    if (lane == 0) a.p[beg + row / heads].r[(int64_t)b * heads + row % heads] = s;
+  }
+  const int c4 = lane, rg = wave;
+  if (c4 >= H4) return;
+  float4 acc[POOL_GRP_ROWS / 4];
+#pragma unroll
+  for (int i = 0; i < POOL_GRP_ROWS / 4; ++i) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float* pk = a.p[beg].pk + (int64_t)b * Lk * H + 4 * c4;
+  int j = 0;
+  for (; j + 2 <= Lk; j += 2) {
+    const float4 v0 = *reinterpret_cast<const float4*>(pk + (int64_t)j * H);
+    const float4 v1 = *reinterpret_cast<const float4*>(pk + (int64_t)(j + 1) * H);
+#pragma unroll
+    for (int i = 0; i < POOL_GRP_ROWS / 4; ++i) {
+      const int row = rg + 4 * i;
+      if (row < R) {
+        const float w0 = pbg[row * Lk + j], w1 = pbg[row * Lk + j + 1];
+        acc[i].x += w0 * v0.x + w1 * v1.x; acc[i].y += w0 * v0.y + w1 * v1.y;
+        acc[i].z += w0 * v0.z + w1 * v1.z; acc[i].w += w0 * v0.w + w1 * v1.w;
+      }
+    }
+  }
+  if (j < Lk) {
+    const float4 v0 = *reinterpret_cast<const float4*>(pk + (int64_t)j * H);
+#pragma unroll
+    for (int i = 0; i < POOL_GRP_ROWS / 4; ++i) {
+      const int row = rg + 4 * i;
+      if (row < R) {
+        const float w0 = pbg[row * Lk + j];
+        acc[i].x += w0 * v0.x; acc[i].y += w0 * v0.y; acc[i].z += w0 * v0.z; acc[i].w += w0 * v0.w;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < POOL_GRP_ROWS / 4; ++i) {
+    const int row = rg + 4 * i;
+    if (row < R)
+      *reinterpret_cast<float4*>(a.p[beg + row / heads].u + ((int64_t)b * heads + row % heads) * H + 4 * c4) = acc[i];
+  }
+}
+
+// dpbar_row[j] = P_k[b][j] . dU_row + dObar_row . b_v,row: half a wave per key, lanes over the
+// columns, every row's dot summed over the 32 lanes (permlane / DPP)
+__global__ __launch_bounds__(NT) void pool_dpbar_grp_kernel(const PoolGrpArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float dug[];   // [R][H]
+  __shared__ float dr_s[POOL_GRP_ROWS];
+  const int b = blockIdx.x, gi = blockIdx.y, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int beg = a.gbeg[gi], heads = a.heads, H = a.H, hd = a.hd, H4 = H / 4;
+  const int R = a.gcnt[gi] * heads, Lk = a.p[beg].Lk;
+  for (int i = t; i < R * H; i += NT) {
+    const int row = i / H, c = i - row * H;
+    dug[i] = a.p[beg + row / heads].du[((int64_t)b * heads + row % heads) * H + c];
+  }
+  for (int row = wave; row < R; row += NT / 64) {
+    const PoolPair& P = a.p[beg + row / heads];
+    const int hh = row % heads;
+    float s = 0.f;
+    for (int d = lane; d < hd; d += 64) s += P.dob[(int64_t)b * H + hh * hd + d] * P.bv[hh * hd + d];
+    s = sum64(s);
+    if (lane == 0) dr_s[row] = s;
+  }
+  __syncthreads();
+  const float* pk = a.p[beg].pk + (int64_t)b * Lk * H;
+  const int half = lane >> 5, l32 = lane & 31;
+  for (int j0 = 2 * wave; j0 < Lk; j0 += 2 * (NT / 64)) {
+    const int j = j0 + half;   // both halves step together (sum32 needs the whole wave)
+    float acc[POOL_GRP_ROWS];
+#pragma unroll
+    for (int row = 0; row < POOL_GRP_ROWS; ++row) acc[row] = 0.f;
+    if (j < Lk) {
+      for (int c4 = l32; c4 < H4; c4 += 32) {
+        const float4 v = *reinterpret_cast<const float4*>(pk + (int64_t)j * H + 4 * c4);
+#pragma unroll
+        for (int row = 0; row < POOL_GRP_ROWS; ++row) {
+          if (row < R) {
+            const float4 u = *reinterpret_cast<const float4*>(&dug[row * H + 4 * c4]);
+            acc[row] += v.x * u.x + v.y * u.y + v.z * u.z + v.w * u.w;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int row = 0; row < POOL_GRP_ROWS; ++row) {
+      if (row < R) {
+        const float s = sum32(acc[row]);
+        if (l32 == 0 && j < Lk)
+          a.p[beg + row / heads].dpbar[((int64_t)b * heads + row % heads) * Lk + j] = s + dr_s[row];
+      }
+    }
+  }
+}
+
+// Group the pairs by key modality (same P_k) and launch the grouped kernels; false when the
+// shapes do not fit them (the caller runs the per-pair kernels)
+bool launch_pool_grouped(bool fwd, const PoolPair* pairs, int npairs, int B, int heads, int hd, int H,
+                         hipStream_t st, hipError_t& err) {
+  err = hipSuccess;
+  if (getenv("MMF_POOL_PER_PAIR") || H % 4 != 0 || H > 256 || npairs < 2) return false;
+  std::vector<std::vector<int>> groups;
+  std::vector<const float*> keyp;
+  for (int g = 0; g < npairs; ++g) {
+    size_t i = 0;
+    while (i < keyp.size() && (keyp[i] != pairs[g].pk || pairs[groups[i][0]].Lk != pairs[g].Lk)) ++i;
+    if (i == keyp.size()) { keyp.push_back(pairs[g].pk); groups.emplace_back(); }
+    groups[i].push_back(g);
+  }
+  if (groups.size() == (size_t)npairs) return false;   // nothing shared
+  for (auto& gr : groups) {
+    const int R = (int)gr.size() * heads, Lk = pairs[gr[0]].Lk;
+    if (R > POOL_GRP_ROWS || (size_t)R * (fwd ? Lk : H) * sizeof(float) > 64 * 1024) return false;
+  }
+  size_t gi = 0;
+  while (gi < groups.size()) {
+    PoolGrpArgs a;
+    memset(&a, 0, sizeof(a));
+    int np = 0, ng = 0;
+    size_t shm = 0;
+    double fl = 0.0, by = 0.0;
+    while (gi < groups.size() && np + (int)groups[gi].size() <= POOL_GRP_MAX) {
+      a.gbeg[ng] = np;
+      a.gcnt[ng] = (int)groups[gi].size();
+      const int Lk = pairs[groups[gi][0]].Lk, R = a.gcnt[ng] * heads;
+      for (int g : groups[gi]) a.p[np++] = pairs[g];
+      shm = std::max(shm, (size_t)R * (fwd ? Lk : H) * sizeof(float));
+      fl += 2.0 * B * R * Lk * H;
+      by += 4.0 * B * ((double)Lk * H + R * (Lk + H));   // P_k once per group
+      ++ng;
+      ++gi;
+    }
+    a.ngroups = ng;
+    a.B = B; a.heads = heads; a.hd = hd; a.H = H;
+    ProfLaunch prof_(st, fwd ? "pool_u_grp_kernel" : "pool_dpbar_grp_kernel", fl, by);
+    if (fwd) mmf_launch(pool_u_grp_kernel, dim3(B, ng), dim3(NT), (uint32_t)shm, st, a);
+    else mmf_launch(pool_dpbar_grp_kernel, dim3(B, ng), dim3(NT), (uint32_t)shm, st, a);
+    err = hipGetLastError();
+    if (err != hipSuccess) return true;
+  }
+  return true;
+}
+
 hipError_t launch_pool(bool fwd, const PoolPair* pairs, int npairs, int B, int heads, int hd, int H,
                        hipStream_t st) {
   if (heads > MAXH || H % 4 != 0) return hipErrorInvalidValue;
+  hipError_t gerr;
+  if (launch_pool_grouped(fwd, pairs, npairs, B, heads, hd, H, st, gerr)) return gerr;
   int done = 0;
   while (done < npairs) {
     PoolArgs a;

@@ -140,7 +140,9 @@ def _record_timeout(flag: torch.Tensor) -> None:
 def _drain_op_flags() -> None:
     """Fold the timeout words of the eager LSTM operator launches (mmf_ops.LSTM_FLAGS)."""
     while _ops.LSTM_FLAGS:
-        _record_timeout(_ops.LSTM_FLAGS.pop())
+        flag = _ops.LSTM_FLAGS.pop()
+        if _ops.eager_tensor(flag):
+            _record_timeout(flag)
 
 
 def lstm_timed_out(device=None, reset: bool = True) -> bool:
@@ -252,7 +254,7 @@ def lstm_layers(rnns: Sequence[LSTM], inputs: Sequence[torch.Tensor],
             xproj.append(torch.addmm(b, x2, getattr(r, f"weight_ih_l{k}").t()).view(B, T, -1))
         hs, cs, _gates, flag = torch.ops.mmfusion.lstm_layer_fwd(
             xproj, [_nat.f32c(getattr(r, f"weight_hh_l{k}")) for r in rnns])
-        if not torch.compiler.is_compiling():
+        if _ops.eager_tensor(flag):
             _record_timeout(flag)
         if finals is not None:
             finals.append((hs[0][:, -1], cs[0][:, -1]))

@@ -214,7 +214,8 @@ class FlatGradBuckets:
         self._pending = [0] * len(self.groups)
         self._works: List[Any] = [None] * len(self.groups)
         self._armed = False
-        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in params]
+        # (one process: nothing to exchange, no per-parameter Python hook in the backward)
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in params] if self.world > 1 else []
 
     def bucket(self, b: int) -> torch.Tensor:
         s, e = self.spans[b]

@@ -566,7 +566,7 @@ def _lstm_backward(ctx, dhs, _dcs, _dgates, _dflag):
     w_hh, hs, cs, gates = (list(sv[k * n:(k + 1) * n]) for k in range(4))
     dh = [hs[i].new_empty(0) if (dhs is None or dhs[i] is None) else dhs[i].contiguous() for i in range(n)]
     dgates, flag = torch.ops.mmfusion.lstm_layer_bwd(w_hh, cs, gates, dh)
-    if not torch.compiler.is_compiling():
+    if eager_tensor(flag):
         LSTM_FLAGS.append(flag)
     B, T, H = hs[0].shape
     # dW_hh = sum_t dgates_t^T h_{t-1} (h_{-1} = 0)
@@ -579,3 +579,10 @@ lstm_layer_fwd.register_autograd(_lstm_backward, setup_context=_lstm_setup)
 # timeout words of the eager LSTM launches, drained by encoders.lstm_timed_out (a compiled
 # graph keeps only the NaN poisoning of values that never arrived, csrc/lstm.hip)
 LSTM_FLAGS: List[Tensor] = []
+
+
+def eager_tensor(t: Tensor) -> bool:
+    """A real tensor of an eager call: not Dynamo tracing, and not one of the fake / functional
+    tensors AOTAutograd traces the backward formula with (torch.compiler.is_compiling() is
+    False there)."""
+    return type(t) is torch.Tensor and not torch.compiler.is_compiling()

@@ -314,3 +314,56 @@ def test_long_key_one_pass_backward_matches_two_kernel_path(mods, medium, monkey
     for n in dw2:
         ok, e = norm_ok(dw1[n], dw2[n], dw2[n], S)
         assert ok, (n, e)
+
+
+def test_long_key_one_pass_train_vs_oracle_medium(mods, medium):
+    """The one-pass long-key kernels in TRAIN mode against the CPU oracle: the device's Philox
+    keep masks replayed on the CPU (tests/_philox.py), the oracle run in fp32 and with
+    bf16-rounded matmul operands (the error a bf16 path must show), the bf16 bounds."""
+    from _philox import mask_provider
+    from _util import bf16_matmul_mode
+    from oracle.hybrid_cpu import hybrid_forward
+    fusion, _, nat = mods
+    case = LONG_TRAIN
+    seed, offset, p = 0x2468_ACE0_1357, 3, 0.1
+    sd = hybrid_state(case.names, case.dims, case.hidden, case.classes, case.seed, case.deleted)
+    model = build_hybrid(fusion, case).train()
+    model._rng_state.copy_(torch.tensor([seed, offset], dtype=torch.int64))
+    feats_np, mask_np, grad_np = hybrid_inputs(case)
+    feats = {m: torch.from_numpy(v).cuda().requires_grad_(True) for m, v in feats_np.items()}
+    nat.profile_begin()
+    logits = model(feats, torch.from_numpy(mask_np).cuda())
+    (logits * torch.from_numpy(grad_np).cuda()).sum().backward()
+    torch.cuda.synchronize()
+    _, launches = nat.profile_end()
+    names = [k for _, k, *_ in launches]
+    assert any(k.startswith("attn_poolL_fwd_fused_bf16<true>") for k in names), names
+    assert any(k.startswith("attn_poolL_bwd_fused_bf16<true>") for k in names), names
+
+    def oracle(bf16):
+        params = {k: torch.from_numpy(v).requires_grad_(True) for k, v in sd.items()}
+        xs = {m: torch.from_numpy(v).requires_grad_(True) for m, v in feats_np.items()}
+
+        def run():
+            ref, _ = hybrid_forward(params, case.names, xs, torch.from_numpy(mask_np), case.heads, p=p,
+                                    train=True, gen=mask_provider(seed, offset, p))
+            (ref * torch.from_numpy(grad_np)).sum().backward()
+            return ref.detach()
+        if bf16:
+            with bf16_matmul_mode():
+                ref = run()
+        else:
+            ref = run()
+        return ref, {m: xs[m].grad for m in case.names}, {n: params[n].grad for n in sd}
+
+    ref, rdx, rdw = oracle(False)
+    emu, edx, edw = oracle(True)
+    ok, e = logits_ok(logits.detach().cpu(), ref)
+    assert ok, e
+    S = group_scale(list(rdx.values()) + list(rdw.values()))
+    for m in case.names:
+        ok, e = norm_ok(feats[m].grad, rdx[m], edx[m], S)
+        assert ok, (m, e)
+    for n, prm in model.named_parameters():
+        ok, e = norm_ok(prm.grad, rdw[n], edw[n], S)
+        assert ok, (n, e)

@@ -192,11 +192,12 @@ def test_lstm_module_matches_torch_layout_cpu(enc_mod):
 @pytest.mark.gpu
 @pytest.mark.parametrize("batch_first", [True, False])
 def test_lstm_module_forward_matches_torch(enc_mod, batch_first):
-    """LSTM(...)(x) -> output, (h_n, c_n) on the HIP recurrence == torch's nn.LSTM (eval) with the
+    """LSTM(...)(x) -> output, (h_n, c_n) on the HIP recurrence == torch's nn.LSTM with the
     same weights; d(input) and parameter gradients through output and h_n."""
     torch.manual_seed(5)
-    ref = torch.nn.LSTM(12, 64, num_layers=2, batch_first=batch_first).to("cuda:0").eval()
-    mine = enc_mod.LSTM(12, 64, num_layers=2, batch_first=batch_first).to("cuda:0").eval()
+    # train mode (MIOpen's RNN backward refuses eval mode), no dropout: deterministic
+    ref = torch.nn.LSTM(12, 64, num_layers=2, batch_first=batch_first).to("cuda:0").train()
+    mine = enc_mod.LSTM(12, 64, num_layers=2, batch_first=batch_first).to("cuda:0").train()
     mine.load_state_dict(ref.state_dict())
     x = torch.randn(3, 25, 12, device="cuda:0")
     if not batch_first:

@@ -189,17 +189,23 @@ def test_long_key_plan_selection(mods):
             assert k in names, (case.name, k, sorted(names))
 
 
-def test_stored_probabilities_plan(mods):
-    """Training with every pair inside the lean fused backward's shape keeps the forward's
-    probabilities (attn_pool_fwd_lean<..., PST = true>) and the fused backward reads them
-    instead of recomputing S (attn_pool_bwd_fused_lean<..., true>); MMF_NO_PSTORE=1 in the
-    environment would select the recompute (A/B).  Parity of this plan is
-    test_hybrid_train_mode_matches_oracle[train_lean]."""
-    import os
+@pytest.mark.parametrize("case", [c for c in TRAIN_CASES if c.name in ("train_lean", "train_h256_odd")],
+                         ids=lambda c: c.name)
+def test_stored_probabilities_parity(mods, case, precision, monkeypatch):
+    """The opt-in stored-probability plan (MMF_PSTORE=1: the lean pooled forward keeps P, the
+    fused backward reads it instead of recomputing S) against the oracle, as above."""
+    monkeypatch.setenv("MMF_PSTORE", "1")
+    test_hybrid_train_mode_matches_oracle(mods, case, precision)
+
+
+def test_stored_probabilities_plan(mods, monkeypatch):
+    """With MMF_PSTORE=1, training with every pair inside the lean fused backward's shape keeps
+    the forward's probabilities (attn_pool_fwd_lean<..., PST = true>) and the fused backward
+    reads them instead of recomputing S (attn_pool_bwd_fused_lean<..., true>); without it
+    (the default) nothing is stored."""
     fusion, _ = mods
     import mmf_native
-    if os.environ.get("MMF_NO_PSTORE"):
-        pytest.skip("MMF_NO_PSTORE set")
+    monkeypatch.setenv("MMF_PSTORE", "1")
     case = next(c for c in TRAIN_CASES if c.name == "train_lean")
     sd = hybrid_state(case.names, case.dims, case.hidden, case.classes, case.seed)
     model = fusion.HybridFusion({m: case.dims[m] for m in case.names}, hidden_dim=case.hidden,
@@ -223,4 +229,13 @@ def test_stored_probabilities_plan(mods):
     _, launches = mmf_native.profile_end()
     bwd = [k for _, k, *_ in launches if k.startswith("attn_pool_bwd_fused_lean")]
     assert bwd and all(k.endswith("false>") for k in bwd), bwd
+    # the default: train mode stores nothing
+    monkeypatch.delenv("MMF_PSTORE")
+    model.train()
+    mmf_native.profile_begin()
+    model(feats, torch.from_numpy(mask_np).cuda()).sum().backward()
+    _, launches = mmf_native.profile_end()
+    names = [k for _, k, *_ in launches]
+    assert all(k.endswith("false>") for k in names if k.startswith("attn_pool_bwd_fused_lean")), names
+    assert all(k.endswith("false>") for k in names if k.startswith("attn_pool_fwd_lean")), names
 
