@@ -111,11 +111,13 @@ def kernel_precision(kname):
     """The int matmul-precision template argument of a library MFMA kernel's profiler name
     (0 fp32, 1 bf16 "medium", 2 bf16x3 "high"): the last integer argument, optionally
     followed by a trailing bool (e.g. "attn_poolL_lse_kernel<64, 1, true>",
-    "gemm_lds_kernel<0, 1, 16, 3, 2>", "gemm_wsr_kernel<1>").  Kernels without one
-    (the generic GEMM, the tail / head kernels) run fp32."""
+    "gemm_lds_kernel<0, 1, 16, 3, 2>", "gemm_wsr_kernel<1>"); the bf16-only kernels are named
+    "..._bf16<...>".  Kernels without one (the generic GEMM, the tail / head kernels) run fp32."""
     if kname.startswith("gemm_generic"):
         return 0
-    m = re.search(r"[<, ]([012])(?:, (?:true|false)){0,2}>$", kname)
+    if "_bf16<" in kname:          # the bf16-only kernels (attn_poolL_*_fused_bf16<DROP>)
+        return 1
+    m = re.search(r"[<, ]([012])(?:, (?:true|false)){0,3}>$", kname)
     return int(m.group(1)) if m else 0
 
 

@@ -1290,8 +1290,9 @@ __device__ __forceinline__ void lean_keep_words(uint32_t (&words)[NKT], const Rn
 }
 
 // DROP (train mode with p > 0, launch-time choice): the loop body has no dropout
-// branches.
-template <int HDP, int BF, bool DROP = true, bool PST = false>
+// branches.  KW: the keep words were drawn beforehand (attn_keep_words_kernel, on a side
+// stream while the projection GEMMs run) -- read, not drawn, and not written back.
+template <int HDP, int BF, bool DROP = true, bool PST = false, bool KW = false>
 __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(const AttnArgs A) {
   constexpr int LS = HDP + 4;
   constexpr int HALF = HDP / 2;
@@ -1337,14 +1338,21 @@ __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(cons
   // the dropout keep words of the wave's first query tile do not depend on any load:
   // drawn while the loads above are in flight (Philox is ~20 % of the kernel's VALU work)
   uint32_t words[NKT];
-  lean_keep_words<NKT, DROP>(words, rs, P.drop_site, (uint64_t)(bh * Lq + min(w * 32 + c, Lq - 1)) * Lk, nkt,
-                             pdrop, h);
+  auto read_words = [&](int qrow) {   // KW: the row's words as the draws would give them
+    const uint4 v = *reinterpret_cast<const uint4*>(P.keep_bits + (bh * Lq + qrow) * 4);
+    const uint32_t a[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) words[kt] = kt < nkt ? a[kt] : 0u;
+  };
+  if constexpr (KW) read_words(min(w * 32 + c, Lq - 1));
+  else lean_keep_words<NKT, DROP>(words, rs, P.drop_site, (uint64_t)(bh * Lq + min(w * 32 + c, Lq - 1)) * Lk, nkt,
+                                  pdrop, h);
   if (msk == 0.f) {
     for (int k = t; k < Lk; k += NT) pbar[k] = 0.f;
     if (P.pbarT)
       for (int k = t; k < Lk; k += NT) P.pbarT[((int64_t)b * Lk + k) * A.heads + head] = 0.f;
     for (int q = t; q < Lq; q += NT) P.lse[bh * Lq + q] = -INFINITY;
-    if (P.keep_bits)
+    if (P.keep_bits && !KW)
       for (int q = t; q < Lq; q += NT)
         *reinterpret_cast<uint4*>(P.keep_bits + (bh * Lq + q) * 4) = make_uint4(0, 0, 0, 0);
     return;
@@ -1442,7 +1450,7 @@ __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(cons
     }
     if (qvalid && h == 0) {
       P.lse[rowidx] = mx * A.scale + __logf(l);
-      if (P.keep_bits && pdrop > 0.f)
+      if (!KW && P.keep_bits && pdrop > 0.f)
         *reinterpret_cast<uint4*>(P.keep_bits + rowidx * 4) =
             make_uint4(words[0], NKT > 1 ? words[1] : 0u, NKT > 2 ? words[2] : 0u, NKT > 3 ? words[3] : 0u);
     }
@@ -1450,7 +1458,8 @@ __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(cons
     if ((qt + 4) * 32 < Lq) {
       const int qn = min((qt + 4) * 32 + c, Lq - 1);
       load_frag_vec<HALF>(qf, P.q + ((int64_t)b * Lq + qn) * P.ldq + col0 + h * HALF);
-      lean_keep_words<NKT, DROP>(words, rs, P.drop_site, (uint64_t)(bh * Lq + qn) * Lk, nkt, pdrop, h);
+      if constexpr (KW) read_words(qn);
+      else lean_keep_words<NKT, DROP>(words, rs, P.drop_site, (uint64_t)(bh * Lq + qn) * Lk, nkt, pdrop, h);
     }
   }
   if ((c & 1) == 0) {
@@ -1984,7 +1993,7 @@ const char* with_arg(const char* base, const char* arg) {
 enum class Kind { Fwd, Probs, Prep, Dkv, Dq, PoolFwd, PoolDq, PoolDk, PoolFused, PoolLse, PoolColsum, PoolDqLong };
 
 hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, int heads, int hd,
-                          float scale, float drop_p, const RngSnap* rng, hipStream_t st) {
+                          float scale, float drop_p, const RngSnap* rng, hipStream_t st, bool words_ready = false) {
   if (hd > 64) return hipErrorInvalidValue;
   const bool small = hd <= 32;
   bool prep_vec = (hd % 4 == 0) && (((hd / 4) & (hd / 4 - 1)) == 0);
@@ -2109,6 +2118,7 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
     if (long_lean) pname = with_arg(pname, "true");   // "<hd, pr, true>": the LEAN instantiation
     if (kind == Kind::PoolFwd && lean) pname = with_arg(pname, a.drop_p > 0.f ? "true" : "false");   // DROP
     if (kind == Kind::PoolFwd && lean) pname = with_arg(pname, pst ? "true" : "false");              // PST
+    if (kind == Kind::PoolFwd && lean && !pst && a.drop_p > 0.f && words_ready) pname = with_arg(pname, "true");   // KW
     if (kind == Kind::PoolFused) pname = with_arg(pname, pst ? "true" : "false");                    // PST
     ProfLaunch prof_(st, pname, fl, by);
     switch (kind) {
@@ -2155,7 +2165,10 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
         else { MMF_PR_LAUNCH(attn_bwd_dq_kernel<64, PRV>) }
         break;
       case Kind::PoolFwd:
-        if (lean && pst && a.drop_p > 0.f) {
+        if (lean && !pst && a.drop_p > 0.f && words_ready) {
+          if (small) { MMF_PR_LAUNCH(attn_pool_fwd_lean<32, PRV, true, false, true>) }
+          else { MMF_PR_LAUNCH(attn_pool_fwd_lean<64, PRV, true, false, true>) }
+        } else if (lean && pst && a.drop_p > 0.f) {
           if (small) { MMF_PR_LAUNCH(attn_pool_fwd_lean<32, PRV, true, true>) }
           else { MMF_PR_LAUNCH(attn_pool_fwd_lean<64, PRV, true, true>) }
         } else if (lean && pst) {
@@ -2218,13 +2231,14 @@ static void split_by_keys(const AttnPair* pairs, int npairs, std::vector<AttnPai
 }
 
 hipError_t launch_attn_pool_fwd(const AttnPair* pairs, int npairs, int B, int heads, int hd, float scale,
-                                float drop_p, const RngSnap* rng, hipStream_t st) {
+                                float drop_p, const RngSnap* rng, hipStream_t st, bool words_ready) {
   std::vector<AttnPair> sp, lp;
   split_by_keys(pairs, npairs, sp, lp);
   hipError_t e = hipSuccess;
-  if (!sp.empty()) e = launch_generic(Kind::PoolFwd, sp.data(), (int)sp.size(), B, heads, hd, scale, drop_p, rng, st);
+  if (!sp.empty())
+    e = launch_generic(Kind::PoolFwd, sp.data(), (int)sp.size(), B, heads, hd, scale, drop_p, rng, st, words_ready);
   if (e == hipSuccess && !lp.empty() && attn_long_fwd_ok(lp.data(), (int)lp.size(), hd, drop_p, rng))
-    return launch_attn_long_fused_fwd(lp.data(), (int)lp.size(), B, heads, hd, scale, drop_p, rng, st);
+    return launch_attn_long_fused_fwd(lp.data(), (int)lp.size(), B, heads, hd, scale, drop_p, rng, st, words_ready);
   if (e == hipSuccess && !lp.empty())
     e = launch_generic(Kind::PoolLse, lp.data(), (int)lp.size(), B, heads, hd, scale, drop_p, rng, st);
   if (e == hipSuccess && !lp.empty())

@@ -25,8 +25,10 @@
 // g at g ^ ((q >> 1) & 3); the dQ partials: [d][q] fp32, 16-B chunk j at j ^ f(d).
 // Conditions (attn_long_fused_ok): 128 < Lk <= 512, Lk % 32 == 0, no per-key mask,
 // head_dim <= 64 and % 4, float4-able Q / K rows; dropout through the forward's keep words.
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "mmf_device.h"
 
@@ -86,6 +88,12 @@ __device__ __forceinline__ f32x16 zero16f() {
 #pragma unroll
   for (int i = 0; i < 16; ++i) z[i] = 0.f;
   return z;
+}
+
+// x where bit `bit` of `word` is set, else +0: one v_bfe_i32 (0 / all ones) and one v_and
+__device__ __forceinline__ float keep_sel(uint32_t word, int bit, float x) {
+  const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)word, bit, 1);
+  return __uint_as_float(__float_as_uint(x) & m);
 }
 
 // 8 columns [d0, d0 + 8) of a row (zero past hd; hd % 4 == 0, 16-B aligned rows)
@@ -176,6 +184,14 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
     for (int dt = 0; dt < 2; ++dt) dk[i][dt] = zero16f();
   char* Sw = lds + OFF_S + w * 2048;
   float* redw = reinterpret_cast<float*>(lds + OFF_R) + w * 2048;
+  uint32_t nwords[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};   // keep words of query block 0 (all kept: no dropout)
+  if (BITS && r < Lq) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int kt = w + 8 * i;
+      if (kt < nkt) nwords[i] = P.keep_bits[(bh * Lq + r) * kwl + kt] >> (4 * hh);
+    }
+  }
 
   for (int qb = 0; qb < nqb; ++qb) {
     const int buf = qb & 1, qbase = qb * LF_QB;
@@ -186,12 +202,14 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
     const char* Qi = lds + OFF_Q + buf * 4096;
     const int q = qbase + r;
     const bool qvalid = q < Lq;
-    uint32_t words[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
-    if (BITS && qvalid) {
+    // this block's keep words (loaded during the previous block), the next block's in flight
+    uint32_t words[2] = {nwords[0], nwords[1]};
+    if (BITS && has_next) {
+      const int qn = q + LF_QB;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int kt = w + 8 * i;
-        if (kt < nkt) words[i] = P.keep_bits[(bh * Lq + q) * kwl + kt] >> (4 * hh);
+        nwords[i] = (kt < nkt && qn < Lq) ? P.keep_bits[(bh * Lq + qn) * kwl + kt] >> (4 * hh) : 0xFFFFFFFFu;
       }
     }
     bf16x8 qf[4];
@@ -223,7 +241,7 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
         for (int j = 0; j < 4; ++j) {
           const int e = 4 * g + j;
           const float p = __builtin_amdgcn_exp2f(s[e] * sl2 - lse2);
-          const float gk = ((words[i] >> (j + 8 * g)) & 1u) ? gv[j] : 0.f;
+          const float gk = keep_sel(words[i], j + 8 * g, gv[j]);
           pv[i][e] = p;
           pk[i][e] = p * gk;
           Dp += pk[i][e];
@@ -240,21 +258,24 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
     for (int ww = 0; ww < 8; ++ww) D += Dpart[buf * 256 + ww * 32 + r];
     if (w == 0 && hh == 0 && qvalid) P.dsum[bh * Lq + q] = D;
 
-    f32x16 dq[2] = {zero16f(), zero16f()};
+    // dS = P (keep g - D) of both tiles first (the bf16 A operands of dQ = dS K, register
+    // e = 8 s2 + j): P and keep * P * g die here, before the matrix-core phase
+    bf16x8 da[2][2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int kt = w + 8 * i;
-      if (kt >= nkt) continue;
-      // dS = P (keep g - D) as the bf16 A operand of dQ = dS K (register e = 8 s2 + j)
-      bf16x8 da[2];
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int e = 8 * s2 + j;
-          da[s2][j] = (__bf16)__builtin_fmaf(-pv[i][e], D, pk[i][e]);
+          da[i][s2][j] = (__bf16)__builtin_fmaf(-pv[i][e], D, pk[i][e]);
         }
-      // dQ[q][d] += sum_key dS[q][key] K[key][d]: K rows 32 kt + 16 s2 + 4 hh + {0..3, 8..11}
+    f32x16 dq[2] = {zero16f(), zero16f()};
+    // dQ[q][d] += sum_key dS[q][key] K[key][d]: K rows 32 kt + 16 s2 + 4 hh + {0..3, 8..11}
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int kt = w + 8 * i;
+      if (kt >= nkt) continue;
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
         const int d0 = 32 * dt + 16 * (g16 & 1) + 4 * pp;
@@ -262,29 +283,39 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
         for (int s2 = 0; s2 < 2; ++s2) {
           const int k0 = kt * 32 + 16 * s2 + 4 * hh + qp;
           const bf16x8 kb = cat8(tr_read(lds, OFF_K + img_off4(k0, d0)), tr_read(lds, OFF_K + img_off4(k0 + 8, d0)));
-          dq[dt] = mfma_bf16(da[s2], kb, dq[dt]);
+          dq[dt] = mfma_bf16(da[i][s2], kb, dq[dt]);
         }
       }
+    }
+    // dK[key][d] += sum_q dS[q][key] Q[q][d]: queries 16 s + 8 hh + {0..7}; the Q operands
+    // (shared by both tiles) read once
+    bf16x8 qb8[2][2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int q0 = 16 * s + 8 * hh + qp, d0 = 32 * dt + 16 * (g16 & 1) + 4 * pp;
+        qb8[s][dt] = cat8(tr_read(Qi, img_off4(q0, d0)), tr_read(Qi, img_off4(q0 + 4, d0)));
+      }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int kt = w + 8 * i;
+      if (kt >= nkt) continue;
       // the dS tile [q][key] (registers 4g .. 4g+3 = keys 8g + 4hh + 0..3 of query r)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         bf16x4 v;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = da[g >> 1][4 * (g & 1) + j];
+        for (int j = 0; j < 4; ++j) v[j] = da[i][g >> 1][4 * (g & 1) + j];
         *reinterpret_cast<bf16x4*>(Sw + ds_off4(r, 8 * g + 4 * hh)) = v;
       }
-      // dK[key][d] += sum_q dS[q][key] Q[q][d]: queries 16 s + 8 hh + {0..7}
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int q0 = 16 * s + 8 * hh + qp;
         const int key0 = 16 * (g16 & 1) + 4 * pp;
         const bf16x8 sa = cat8(tr_read(Sw, ds_off4(q0, key0)), tr_read(Sw, ds_off4(q0 + 4, key0)));
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-          const int d0 = 32 * dt + 16 * (g16 & 1) + 4 * pp;
-          const bf16x8 qb8 = cat8(tr_read(Qi, img_off4(q0, d0)), tr_read(Qi, img_off4(q0 + 4, d0)));
-          dk[i][dt] = mfma_bf16(sa, qb8, dk[i][dt]);
-        }
+        for (int dt = 0; dt < 2; ++dt) dk[i][dt] = mfma_bf16(sa, qb8[s][dt], dk[i][dt]);
       }
     }
     // this wave's partial dQ tile: lane = d, registers 4g .. 4g+3 = queries 8g + 4hh + 0..3
@@ -335,6 +366,35 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
 
 
 // ---------------------------------------------------------------------------
+// Dropout keep words of the attention probabilities, (B, heads, Lq, kw_ld) u32: bit j of
+// word kt of row (b, head, q) keeps element ((b heads + head) Lq + q) Lk + 32 kt + j of the
+// pair's Philox stream (site drop_site) -- the same words the streamed forward
+// (attn_poolL_lse_kernel) draws inline and every backward reads.  One thread per word
+// (4 Philox blocks of 8 elements; Lk % 32 == 0 keeps them aligned): the draws run at full
+// occupancy here instead of inside the one-pass forward's exp phase.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void attn_keep_words_kernel(const AttnArgs A) {
+  const AttnPair& P = A.p[blockIdx.y];
+  const int nkt = P.Lk >> 5;
+  const int64_t nwords = (int64_t)A.B * A.heads * P.Lq * nkt;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nwords) return;
+  const int64_t row = i / nkt;
+  const int kt = (int)(i - row * nkt);
+  const RngSnap rs = *A.rng;
+  const uint32_t thr = p16(A.drop_p);
+  const uint64_t blk0 = ((uint64_t)row * P.Lk + 32 * kt) >> 3;
+  uint32_t bits = 0;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const uint4 rr = philox_block(rs, P.drop_site, blk0 + g);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bits |= keep_from(rr, e, thr) ? (1u << (8 * g + e)) : 0u;
+  }
+  P.keep_bits[row * P.kw_ld + kt] = bits;
+}
+
+// ---------------------------------------------------------------------------
 // Forward in one pass (same conditions; "medium"): LSE, the dropout keep words and
 // pbar = mean_q P' for every key of one (pair, sample, head).  Per 32-query block each
 // wave forms S^T for its two key tiles, the 8 waves' row maxima and sums meet in LDS
@@ -378,8 +438,6 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_fwd_fused_bf16(const Attn
     }
     return;
   }
-  RngSnap rs{0, 0};
-  if (DROP) rs = *A.rng;
   float* Mpart = reinterpret_cast<float*>(lds + FOFF_M);
   float* Spart = reinterpret_cast<float*>(lds + FOFF_S);
 
@@ -427,6 +485,15 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_fwd_fused_bf16(const Attn
     const char* Qi = lds + FOFF_Q + buf * 4096;
     const int q = qbase + r;
     const bool qvalid = q < Lq;
+    // the keep words of the own tiles (attn_keep_words_kernel), consumed after barrier B
+    uint32_t kw[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
+    if (DROP && qvalid) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int kt = w + 8 * i;
+        if (kt < nkt) kw[i] = P.keep_bits[(bh * Lq + q) * kwl + kt] >> (4 * hh);
+      }
+    }
     bf16x8 qf[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(Qi + img_off(r, 2 * s + hh));
@@ -469,21 +536,6 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_fwd_fused_bf16(const Attn
       }
     ls = sum_xor32(ls);
     if (hh == 0) Spart[buf * 256 + w * 32 + r] = ls;
-    // keep words of the own tiles (all lanes draw: keep_tile16 shuffles)
-    uint32_t kb[2] = {0xFFFFu, 0xFFFFu};
-    if (DROP) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int kt = w + 8 * i;
-        if (kt >= nkt) continue;
-        kb[i] = keep_tile16(rs, P.drop_site, (uint64_t)(bh * Lq + q) * Lk + kt * 32, pdrop, hh, qvalid, true);
-        uint32_t bits = 0;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) bits |= ((kb[i] >> (4 * g)) & 0xFu) << (8 * g + 4 * hh);
-        bits = or_xor32(bits);
-        if (qvalid && hh == 0) P.keep_bits[(bh * Lq + q) * kwl + kt] = bits;
-      }
-    }
     __syncthreads();   // (B) row sums
     float l = 0.f;
 #pragma unroll
@@ -502,7 +554,7 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_fwd_fused_bf16(const Attn
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int e = 4 * g + j;
-          v[j] = (__bf16)(((kb[i] >> e) & 1u) ? x[i][e] * cq : 0.f);
+          v[j] = (__bf16)keep_sel(kw[i], j + 8 * g, x[i][e] * cq);
         }
         *reinterpret_cast<bf16x4*>(Pw + ds_off4(r, 8 * g + 4 * hh)) = v;
       }
@@ -556,8 +608,41 @@ bool attn_long_fwd_ok(const AttnPair* pairs, int npairs, int hd, float drop_p, c
   return true;
 }
 
+hipError_t launch_attn_keep_words(const AttnPair* pairs, int npairs, int B, int heads, float drop_p,
+                                  const RngSnap* rng, hipStream_t st) {
+  if (!(drop_p > 0.f) || !rng) return hipSuccess;
+  std::vector<AttnPair> ps;
+  for (int i = 0; i < npairs; ++i)
+    if (pairs[i].keep_bits && pairs[i].Lk % 32 == 0 && pairs[i].Lk > 0 && pairs[i].kw_ld >= pairs[i].Lk / 32)
+      ps.push_back(pairs[i]);
+  for (size_t done = 0; done < ps.size();) {
+    AttnArgs a;
+    memset(&a, 0, sizeof(a));
+    int n = 0;
+    int64_t maxw = 0;
+    double wb = 0.0;
+    while (done < ps.size() && n < ATTN_MAX_PAIRS) {
+      a.p[n] = ps[done++];
+      const int64_t nw = (int64_t)B * heads * a.p[n].Lq * (a.p[n].Lk / 32);
+      maxw = std::max(maxw, nw);
+      wb += 4.0 * nw;
+      ++n;
+    }
+    a.npairs = n;
+    a.B = B;
+    a.heads = heads;
+    a.drop_p = drop_p;
+    a.rng = rng;
+    ProfLaunch prof_(st, "attn_keep_words_kernel", 0.0, wb);
+    mmf_launch(attn_keep_words_kernel, dim3((unsigned)((maxw + 255) / 256), (unsigned)n), dim3(256), 0, st, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 hipError_t launch_attn_long_fused_fwd(const AttnPair* pairs, int npairs, int B, int heads, int hd, float scale,
-                                      float drop_p, const RngSnap* rng, hipStream_t st) {
+                                      float drop_p, const RngSnap* rng, hipStream_t st, bool words_ready) {
   if (!attn_long_fwd_ok(pairs, npairs, hd, drop_p, rng)) return hipErrorNotSupported;
   const bool drop = drop_p > 0.f;
   for (int done = 0; done < npairs;) {
@@ -581,6 +666,19 @@ hipError_t launch_attn_long_fused_fwd(const AttnPair* pairs, int npairs, int B, 
     a.drop_p = drop_p;
     a.rng = rng;
     a.nblk = B * heads;
+    if (drop && !words_ready) {
+      int64_t maxw = 0;
+      double wb = 0.0;
+      for (int i = 0; i < n; ++i) {
+        const int64_t nw = (int64_t)B * heads * a.p[i].Lq * (a.p[i].Lk / 32);
+        maxw = std::max(maxw, nw);
+        wb += 4.0 * nw;
+      }
+      ProfLaunch prof_(st, "attn_keep_words_kernel", 0.0, wb);
+      mmf_launch(attn_keep_words_kernel, dim3((unsigned)((maxw + 255) / 256), (unsigned)n), dim3(256), 0, st, a);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
     const dim3 grid((unsigned)(B * heads), (unsigned)n);
     ProfLaunch prof_(st, drop ? "attn_poolL_fwd_fused_bf16<true>" : "attn_poolL_fwd_fused_bf16<false>", fl, by);
     if (drop) mmf_launch(attn_poolL_fwd_fused_bf16<true>, grid, dim3(LF_NT), 0, st, a);

@@ -3,6 +3,7 @@
 // helpers (cross-entropy, AdamW), profiling and error reporting.  Every entry
 // point validates first, then only enqueues kernels on the caller's stream.
 #include <cmath>
+#include <map>
 
 #include "capi_util.h"
 
@@ -140,6 +141,21 @@ thread_local ProfArm* g_prof_arm = nullptr;
 bool prof_capturing(hipStream_t st) {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   return hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+
+SideStream* side_stream(bool create) {
+  static thread_local std::map<int, SideStream> streams;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  auto it = streams.find(dev);
+  if (it != streams.end()) return &it->second;
+  if (!create) return nullptr;
+  SideStream ss{};
+  if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  if (hipEventCreateWithFlags(&ss.fork_ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ss.join_ev, hipEventDisableTiming) != hipSuccess)
+    return nullptr;
+  return &(streams[dev] = ss);
 }
 
 bool prof_arm_begin(ProfArm& arm, hipStream_t st) {

@@ -475,6 +475,40 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
   // no launch of its own
   const RngSnap* rng = rng_state ? s.rng : nullptr;
 
+  // pairs with several keys run the attention kernels; single-key pairs single_key.hip
+  std::vector<AttnPair> pairs;
+  std::vector<SkPair> skp;
+  std::vector<WidePair> wp;
+  for (int g = 0; g < d->num_pairs; ++g) {
+    float* maps = d->return_attention && attn_maps ? attn_maps[g] : nullptr;
+    if (single_key(d, g)) {
+      skp.push_back(make_sk(d, s, mask, g));
+      skp.back().probs = maps;
+    } else if (wide_pair(d, g)) {
+      wp.push_back(make_wide(d, s, mask, g));
+      wp.back().probs = maps;   // written by the wide softmax itself
+    } else {
+      pairs.push_back(make_pair(d, s, mask, g));
+      pairs.back().probs = maps;
+    }
+  }
+  const int nmp = (int)pairs.size(), nsk = (int)skp.size(), nwp = (int)wp.size();
+  // The attention dropout keep words depend only on the rng snapshot: drawn on a side stream
+  // (attn_keep_words_kernel) while the projection GEMMs run, so the attention forward reads
+  // them instead of drawing inline.  Pooled plan, training; an existing side stream only
+  // while st is being captured.  MMF_NO_SIDE_STREAM=1: draw inline (A/B).
+  SideStream* side = nullptr;
+  auto fork_keep_words = [&]() {
+    if (!(drop && use_pool(d) && nmp) || getenv("MMF_NO_SIDE_STREAM")) return;
+    side = side_stream(!prof_capturing(st));
+    if (!side) return;
+    if (hipEventRecord(side->fork_ev, st) != hipSuccess || hipStreamWaitEvent(side->s, side->fork_ev, 0) != hipSuccess ||
+        launch_attn_keep_words(pairs.data(), nmp, B, nh, p, rng, side->s) != hipSuccess ||
+        hipEventRecord(side->join_ev, side->s) != hipSuccess) {
+      side = nullptr;   // (a failed fork joins nothing; the kernels draw inline)
+    }
+  };
+
   // (1) per-modality projection: P_m = Drop(ReLU(X'_m W_m^T + b_m)), X'_m = Drop(X_m * mask_m)
   //     (fusion.py:364-374); X' is kept for the weight gradient
   {
@@ -496,6 +530,7 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
       jobs.push_back(j);
     }
     STAGE_TRY("fwd.input_mask", launch_mask_dropout(ma, st));
+    fork_keep_words();   // the rng snapshot exists from here on
     STAGE_TRY("fwd.proj_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, p, rng, st,
                                            const_cast<uint64_t*>(rng_state)));
   }
@@ -525,28 +560,12 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
     if (!jobs.empty())
       STAGE_TRY("fwd.qkv_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, 0.f, rng, st));
   }
-  // pairs with several keys run the attention kernels; single-key pairs single_key.hip
-  std::vector<AttnPair> pairs;
-  std::vector<SkPair> skp;
-  std::vector<WidePair> wp;
-  for (int g = 0; g < d->num_pairs; ++g) {
-    float* maps = d->return_attention && attn_maps ? attn_maps[g] : nullptr;
-    if (single_key(d, g)) {
-      skp.push_back(make_sk(d, s, mask, g));
-      skp.back().probs = maps;
-    } else if (wide_pair(d, g)) {
-      wp.push_back(make_wide(d, s, mask, g));
-      wp.back().probs = maps;   // written by the wide softmax itself
-    } else {
-      pairs.push_back(make_pair(d, s, mask, g));
-      pairs.back().probs = maps;
-    }
-  }
-  const int nmp = (int)pairs.size(), nsk = (int)skp.size(), nwp = (int)wp.size();
   const float scale = 1.0f / std::sqrt((float)hd);
+  if (side) HIP_TRY(hipStreamWaitEvent(st, side->join_ev, 0));   // join the keep-word draws
   if (d->num_pairs && pool) {
     // (3p) attention -> LSE, pbar = mean_q P'; U = pbar P_k; Obar = U W_v^T + r b_v; Abar = out_proj
-    if (nmp) STAGE_TRY("fwd.attn", launch_attn_pool_fwd(pairs.data(), nmp, B, nh, hd, scale, p, rng, st));
+    if (nmp)
+      STAGE_TRY("fwd.attn", launch_attn_pool_fwd(pairs.data(), nmp, B, nh, hd, scale, p, rng, st, side != nullptr));
     if (nsk) STAGE_TRY("fwd.attn_single_key", launch_sk_fwd(skp.data(), nsk, B, nh, hd, p, rng, st));
     if (nwp) STAGE_TRY("fwd.attn_wide", launch_wide_fwd(wp.data(), nwp, B, nh, hd, scale, p, rng, true, st));
     std::vector<PoolPair> pp(d->num_pairs);

@@ -35,6 +35,14 @@ extern thread_local ProfArm* g_prof_arm;
 // inside a capture cannot be timed afterwards: the captured launches run untimed)
 bool prof_arm_begin(ProfArm& arm, hipStream_t st);
 bool prof_capturing(hipStream_t st);
+
+// A side stream of the calling thread on the current device with two (untimed) events:
+// record `fork_ev` on st and make `s` wait on it, enqueue on `s`, record `join_ev` on `s`
+// and make st wait on it -- inside a graph capture on st the side work becomes a parallel
+// branch of the graph.  create = false: only an existing one (no stream / event creation
+// while st is being captured); nullptr when there is none or it cannot be created.
+struct SideStream { hipStream_t s; hipEvent_t fork_ev, join_ev; };
+SideStream* side_stream(bool create);
 void prof_arm_end(ProfArm& arm, hipStream_t st, const char* kernel, double flops, double bytes);
 struct ProfLaunch {
   hipStream_t st;
@@ -275,8 +283,10 @@ hipError_t launch_attn_bwd_stage(int stage, const AttnPair* pairs, int npairs, i
                                  float scale, float drop_p, const RngSnap* rng, hipStream_t st);
 // Pooled formulation: forward writes LSE and pbar = mean_q P'[q, :];
 // backward (stage 0: dQ and D = rowsum(P . dP); stage 1: dK) from dpbar.
+// words_ready: the dropout keep words of every pair with Lk % 32 == 0 were drawn beforehand
+// (launch_attn_keep_words): the lean and one-pass kernels read them instead of drawing
 hipError_t launch_attn_pool_fwd(const AttnPair* pairs, int npairs, int B, int heads, int hd, float scale,
-                                float drop_p, const RngSnap* rng, hipStream_t st);
+                                float drop_p, const RngSnap* rng, hipStream_t st, bool words_ready = false);
 hipError_t launch_attn_pool_bwd(int stage, const AttnPair* pairs, int npairs, int B, int heads, int hd,
                                 float scale, float drop_p, const RngSnap* rng, hipStream_t st);
 // Long-key pooled backward in one pass (attn_long.hip, bf16 "medium" only): dQ, dK and D of
@@ -285,7 +295,11 @@ bool attn_long_fused_ok(const AttnPair* pairs, int npairs, int hd, float drop_p)
 // ... and its forward (LSE, keep words, pbar) in one pass
 bool attn_long_fwd_ok(const AttnPair* pairs, int npairs, int hd, float drop_p, const RngSnap* rng);
 hipError_t launch_attn_long_fused_fwd(const AttnPair* pairs, int npairs, int B, int heads, int hd, float scale,
-                                      float drop_p, const RngSnap* rng, hipStream_t st);
+                                      float drop_p, const RngSnap* rng, hipStream_t st, bool words_ready = false);
+// The dropout keep words (B, heads, Lq, kw_ld) of the attention probabilities of the pairs
+// with Lk % 32 == 0 and keep_bits (the others are skipped), as the attention kernels draw them
+hipError_t launch_attn_keep_words(const AttnPair* pairs, int npairs, int B, int heads, float drop_p,
+                                  const RngSnap* rng, hipStream_t st);
 hipError_t launch_attn_long_fused_bwd(const AttnPair* pairs, int npairs, int B, int heads, int hd, float scale,
                                       float drop_p, hipStream_t st);
 

@@ -88,7 +88,7 @@ def group_scale(refs):
 
 def _precision(kname):
     """The int precision argument of a library MFMA kernel name (bench.kernel_precision)."""
-    m = re.search(r"[<, ]([012])(?:, (?:true|false)){0,2}>$", kname)
+    m = re.search(r"[<, ]([012])(?:, (?:true|false)){0,3}>$", kname)
     return int(m.group(1)) if m else None
 
 

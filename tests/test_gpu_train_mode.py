@@ -239,3 +239,51 @@ def test_stored_probabilities_plan(mods, monkeypatch):
     assert all(k.endswith("false>") for k in names if k.startswith("attn_pool_bwd_fused_lean")), names
     assert all(k.endswith("false>") for k in names if k.startswith("attn_pool_fwd_lean")), names
 
+
+
+@pytest.mark.parametrize("case_name,prec", [("train_lean", "highest"), ("train_long_hd64", "medium")])
+def test_side_stream_keep_words_match_inline_draws(mods, case_name, prec, monkeypatch):
+    """The attention dropout keep words drawn on the side stream while the projection GEMMs run
+    (attn_keep_words_kernel; the lean forward's KW variant and the one-pass long forward read
+    them) are the words the kernels draw inline (MMF_NO_SIDE_STREAM=1): same logits and
+    gradients bit for bit."""
+    fusion, _ = mods
+    import mmf_native
+    case = next(c for c in TRAIN_CASES if c.name == case_name)
+    if case_name == "train_long_hd64":   # whole 32-key tiles for the one-pass kernels
+        case = HybridCase("train_long_32", case.names, case.dims, {"a": 160, "b": 288}, batch=2, hidden=128,
+                          heads=2, classes=4, seed=55, mask=[[1, 1], [0.5, 1]])
+    sd = hybrid_state(case.names, case.dims, case.hidden, case.classes, case.seed)
+    feats_np, mask_np, grad_np = hybrid_inputs(case)
+    prev = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision(prec)
+    try:
+        runs = []
+        for inline in (False, True):
+            if inline:
+                monkeypatch.setenv("MMF_NO_SIDE_STREAM", "1")
+            model = fusion.HybridFusion({m: case.dims[m] for m in case.names}, hidden_dim=case.hidden,
+                                        num_classes=case.classes, num_heads=case.heads, dropout=P)
+            model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+            model = model.cuda().train()
+            model._rng_state.copy_(torch.tensor([SEED, OFFSET], dtype=torch.int64))
+            feats = {m: torch.from_numpy(v).cuda().requires_grad_(True) for m, v in feats_np.items()}
+            mmf_native.profile_begin()
+            logits = model(feats, torch.from_numpy(mask_np).cuda())
+            (logits * torch.from_numpy(grad_np).cuda()).sum().backward()
+            torch.cuda.synchronize()
+            _, launches = mmf_native.profile_end()
+            names = [k for _, k, *_ in launches]
+            runs.append((logits.detach(), [feats[m].grad for m in case.names],
+                         [p_.grad.clone() for p_ in model.parameters()], names))
+            monkeypatch.delenv("MMF_NO_SIDE_STREAM", raising=False)
+    finally:
+        torch.set_float32_matmul_precision(prev)
+    (l1, dx1, dw1, n1), (l2, dx2, dw2, n2) = runs
+    assert "attn_keep_words_kernel" in n1, n1
+    if case_name == "train_lean":   # (the one-pass long forward draws with the same kernel, in line)
+        assert "attn_keep_words_kernel" not in n2, n2
+        assert any(k.startswith("attn_pool_fwd_lean") and k.endswith("true, false, true>") for k in n1), n1
+    assert torch.equal(l1, l2)
+    for a, b in zip(dx1 + dw1, dx2 + dw2):
+        assert torch.equal(a, b)
