@@ -404,16 +404,23 @@ __global__ __launch_bounds__(256) void attn_keep_words_kernel(const AttnArgs A) 
 // per-wave transposed P' tile (bf16, as the reference's P'.V operand at "medium") into an
 // all-ones MFMA whose accumulator carries pbar across the query blocks.
 // ---------------------------------------------------------------------------
-constexpr int FOFF_K = 0;                               // [LF_MAXK][64] bf16
-constexpr int FOFF_Q = FOFF_K + LF_MAXK * 128;          // [2][32][64] bf16
-constexpr int FOFF_P = FOFF_Q + 2 * LF_QB * 128;        // [8][32 q][32 keys] bf16
-constexpr int FOFF_M = FOFF_P + 8 * LF_QB * 64;         // [2][8][32] fp32 row maxima
-constexpr int FOFF_S = FOFF_M + 2 * 8 * LF_QB * 4;      // [2][8][32] fp32 row sums
-constexpr int LFF_LDS = FOFF_S + 2 * 8 * LF_QB * 4;     // 96,256 bytes
+// NW waves per workgroup (16: four per SIMD, one key tile each at Lk = 512; 8: two tiles each)
+template <int NW>
+struct FwdLds {
+  static constexpr int K = 0;                                // [LF_MAXK][64] bf16
+  static constexpr int Q = K + LF_MAXK * 128;                // [2][32][64] bf16
+  static constexpr int P = Q + 2 * LF_QB * 128;              // [NW][32 q][32 keys] bf16
+  static constexpr int M = P + NW * LF_QB * 64;              // [2][NW][32] fp32 row maxima
+  static constexpr int S = M + 2 * NW * LF_QB * 4;           // [2][NW][32] fp32 row sums
+  static constexpr int BYTES = S + 2 * NW * LF_QB * 4;       // 94 KB (8 waves) / 112 KB (16)
+};
 
-template <bool DROP>
-__global__ __launch_bounds__(LF_NT, 1) void attn_poolL_fwd_fused_bf16(const AttnArgs A) {
-  __shared__ __attribute__((aligned(16))) char lds[LFF_LDS];
+template <bool DROP, int NW = 16>
+__global__ __launch_bounds__(NW * 64, 1) void attn_poolL_fwd_fused_bf16(const AttnArgs A) {
+  constexpr int NTW = NW * 64, TPW = 16 / NW;   // threads; key tiles per wave (Lk <= 512)
+  using L_ = FwdLds<NW>;
+  constexpr int FOFF_K = L_::K, FOFF_Q = L_::Q, FOFF_P = L_::P, FOFF_M = L_::M, FOFF_S = L_::S;
+  __shared__ __attribute__((aligned(16))) char lds[L_::BYTES];
   const AttnPair& P = A.p[blockIdx.y];
   if ((int)blockIdx.x >= A.B * A.heads) return;
   const int head = blockIdx.x % A.heads, b = blockIdx.x / A.heads;
@@ -431,8 +438,8 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_fwd_fused_bf16(const Attn
   if (P.kmask_mode == 1 && P.kmask[(int64_t)b * P.kmask_ld] == 0.f) {
     // masked key modality: every probability is 0 (src/attention.py:127-129); the keep words
     // are never read when LSE = -inf
-    for (int i = t; i < Lq; i += LF_NT) P.lse[bh * Lq + i] = -INFINITY;
-    for (int k = t; k < Lk; k += LF_NT) {
+    for (int i = t; i < Lq; i += NTW) P.lse[bh * Lq + i] = -INFINITY;
+    for (int k = t; k < Lk; k += NTW) {
       P.pbar[bh * Lk + k] = 0.f;
       if (P.pbarT) P.pbarT[((int64_t)b * Lk + k) * A.heads + head] = 0.f;
     }
@@ -443,16 +450,16 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_fwd_fused_bf16(const Attn
 
   {
     const int nch = Lk * 8;
-    for (int i0 = 0; i0 < nch; i0 += LF_NT * 4) {
+    for (int i0 = 0; i0 < nch; i0 += NTW * 4) {
       float4 va[4], vb[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int idx = i0 + t + j * LF_NT;
+        const int idx = i0 + t + j * NTW;
         load8(Kg + (int64_t)(idx < nch ? idx >> 3 : 0) * P.ldk, 8 * (idx & 7), hd, idx < nch, va[j], vb[j]);
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int idx = i0 + t + j * LF_NT;
+        const int idx = i0 + t + j * NTW;
         if (idx < nch) *reinterpret_cast<bf16x8*>(lds + FOFF_K + img_off(idx >> 3, idx & 7)) = to_bf16x8(va[j], vb[j]);
       }
     }
@@ -474,7 +481,9 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_fwd_fused_bf16(const Attn
   bf16x8 ones;
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
-  f32x16 cs[2] = {zero16f(), zero16f()};   // every row of C = the column sums of P'
+  f32x16 cs[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) cs[i] = zero16f();   // every row of C = the column sums of P'
   char* Pw = lds + FOFF_P + w * 2048;
 
   for (int qb = 0; qb < nqb; ++qb) {
@@ -486,22 +495,24 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_fwd_fused_bf16(const Attn
     const int q = qbase + r;
     const bool qvalid = q < Lq;
     // the keep words of the own tiles (attn_keep_words_kernel), consumed after barrier B
-    uint32_t kw[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
+    uint32_t kw[TPW];
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) kw[i] = 0xFFFFFFFFu;
     if (DROP && qvalid) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int kt = w + 8 * i;
+      for (int i = 0; i < TPW; ++i) {
+        const int kt = w + NW * i;
         if (kt < nkt) kw[i] = P.keep_bits[(bh * Lq + q) * kwl + kt] >> (4 * hh);
       }
     }
     bf16x8 qf[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(Qi + img_off(r, 2 * s + hh));
-    float x[2][16];
+    float x[TPW][16];
     float mx = -INFINITY;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int kt = w + 8 * i;
+    for (int i = 0; i < TPW; ++i) {
+      const int kt = w + NW * i;
       if (kt >= nkt) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) x[i][e] = -INFINITY;
@@ -519,33 +530,33 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_fwd_fused_bf16(const Attn
       }
     }
     mx = max_xor32(mx);
-    if (hh == 0) Mpart[buf * 256 + w * 32 + r] = mx;
+    if (hh == 0) Mpart[buf * NW * 32 + w * 32 + r] = mx;
     if (has_next) q_store(buf ^ 1, na, nb);
     __syncthreads();   // (A) row maxima, next query block
     float m = -INFINITY;
 #pragma unroll
-    for (int ww = 0; ww < 8; ++ww) m = fmaxf(m, Mpart[buf * 256 + ww * 32 + r]);
+    for (int ww = 0; ww < NW; ++ww) m = fmaxf(m, Mpart[buf * NW * 32 + ww * 32 + r]);
     const float mref = m == -INFINITY ? 0.f : m;
     float ls = 0.f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TPW; ++i)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         x[i][e] = __builtin_amdgcn_exp2f(x[i][e] - mref);
         ls += x[i][e];
       }
     ls = sum_xor32(ls);
-    if (hh == 0) Spart[buf * 256 + w * 32 + r] = ls;
+    if (hh == 0) Spart[buf * NW * 32 + w * 32 + r] = ls;
     __syncthreads();   // (B) row sums
     float l = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < 8; ++ww) l += Spart[buf * 256 + ww * 32 + r];
+    for (int ww = 0; ww < NW; ++ww) l += Spart[buf * NW * 32 + ww * 32 + r];
     if (w == 0 && hh == 0 && qvalid) P.lse[bh * Lq + q] = l > 0.f ? (m + __log2f(l)) * (1.f / LF_LOG2E) : -INFINITY;
     // P' / Lq of this lane's query (0 for a query past Lq)
     const float cq = (qvalid && l > 0.f) ? inv_keep / (l * (float)Lq) : 0.f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int kt = w + 8 * i;
+    for (int i = 0; i < TPW; ++i) {
+      const int kt = w + NW * i;
       if (kt >= nkt) continue;
       // the P' tile [q][key], registers 4g .. 4g+3 = keys 8g + 4hh + 0..3
 #pragma unroll
@@ -570,8 +581,8 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_fwd_fused_bf16(const Attn
   }
   // pbar: lane = key, every register the same column sum
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int kt = w + 8 * i;
+  for (int i = 0; i < TPW; ++i) {
+    const int kt = w + NW * i;
     if (kt >= nkt || hh != 0) continue;
     const int key = kt * 32 + r;
     P.pbar[bh * Lk + key] = cs[i][0];
@@ -680,9 +691,18 @@ hipError_t launch_attn_long_fused_fwd(const AttnPair* pairs, int npairs, int B, 
       if (e != hipSuccess) return e;
     }
     const dim3 grid((unsigned)(B * heads), (unsigned)n);
-    ProfLaunch prof_(st, drop ? "attn_poolL_fwd_fused_bf16<true>" : "attn_poolL_fwd_fused_bf16<false>", fl, by);
-    if (drop) mmf_launch(attn_poolL_fwd_fused_bf16<true>, grid, dim3(LF_NT), 0, st, a);
-    else mmf_launch(attn_poolL_fwd_fused_bf16<false>, grid, dim3(LF_NT), 0, st, a);
+    // 16 waves (one key tile each at Lk = 512); MMF_LONG_FWD_W8=1: the 8-wave form (A/B)
+    static const bool w8 = getenv("MMF_LONG_FWD_W8") != nullptr;
+    const char* kn = w8 ? (drop ? "attn_poolL_fwd_fused_bf16<true, 8>" : "attn_poolL_fwd_fused_bf16<false, 8>")
+                        : (drop ? "attn_poolL_fwd_fused_bf16<true, 16>" : "attn_poolL_fwd_fused_bf16<false, 16>");
+    ProfLaunch prof_(st, kn, fl, by);
+    if (w8) {
+      if (drop) mmf_launch(attn_poolL_fwd_fused_bf16<true, 8>, grid, dim3(8 * 64), 0, st, a);
+      else mmf_launch(attn_poolL_fwd_fused_bf16<false, 8>, grid, dim3(8 * 64), 0, st, a);
+    } else {
+      if (drop) mmf_launch(attn_poolL_fwd_fused_bf16<true, 16>, grid, dim3(16 * 64), 0, st, a);
+      else mmf_launch(attn_poolL_fwd_fused_bf16<false, 16>, grid, dim3(16 * 64), 0, st, a);
+    }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
