@@ -375,12 +375,13 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void attn_keep_words_kernel(const AttnArgs A) {
   const AttnPair& P = A.p[blockIdx.y];
-  const int nkt = P.Lk >> 5;
-  const int64_t nwords = (int64_t)A.B * A.heads * P.Lq * nkt;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint32_t nkt = (uint32_t)P.Lk >> 5;
+  // 32-bit word index (the launcher checks B heads Lq nkt < 2^31): no 64-bit division
+  const uint32_t nwords = (uint32_t)A.B * (uint32_t)A.heads * (uint32_t)P.Lq * nkt;
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
   if (i >= nwords) return;
-  const int64_t row = i / nkt;
-  const int kt = (int)(i - row * nkt);
+  const uint32_t row = (nkt & (nkt - 1)) == 0 ? i >> (31 - __builtin_clz(nkt)) : i / nkt;
+  const uint32_t kt = i - row * nkt;
   const RngSnap rs = *A.rng;
   const uint32_t thr = p16(A.drop_p);
   const uint64_t blk0 = ((uint64_t)row * P.Lk + 32 * kt) >> 3;
@@ -388,10 +389,15 @@ __global__ __launch_bounds__(256) void attn_keep_words_kernel(const AttnArgs A) 
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const uint4 rr = philox_block(rs, P.drop_site, blk0 + g);
+    const uint32_t wv[4] = {rr.x, rr.y, rr.z, rr.w};
 #pragma unroll
-    for (int e = 0; e < 8; ++e) bits |= keep_from(rr, e, thr) ? (1u << (8 * g + e)) : 0u;
+    for (int k = 0; k < 4; ++k) {
+      // element 2k: the low 16 bits of word k, element 2k + 1: the high 16 bits (keep_from)
+      bits |= ((wv[k] & 0xFFFFu) >= thr ? 1u : 0u) << (8 * g + 2 * k);
+      bits |= ((wv[k] >> 16) >= thr ? 1u : 0u) << (8 * g + 2 * k + 1);
+    }
   }
-  P.keep_bits[row * P.kw_ld + kt] = bits;
+  P.keep_bits[(uint64_t)row * P.kw_ld + kt] = bits;
 }
 
 // ---------------------------------------------------------------------------
@@ -624,8 +630,10 @@ hipError_t launch_attn_keep_words(const AttnPair* pairs, int npairs, int B, int 
   if (!(drop_p > 0.f) || !rng) return hipSuccess;
   std::vector<AttnPair> ps;
   for (int i = 0; i < npairs; ++i)
-    if (pairs[i].keep_bits && pairs[i].Lk % 32 == 0 && pairs[i].Lk > 0 && pairs[i].kw_ld >= pairs[i].Lk / 32)
+    if (pairs[i].keep_bits && pairs[i].Lk % 32 == 0 && pairs[i].Lk > 0 && pairs[i].kw_ld >= pairs[i].Lk / 32) {
+      if ((int64_t)B * heads * pairs[i].Lq * (pairs[i].Lk / 32) >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
       ps.push_back(pairs[i]);
+    }
   for (size_t done = 0; done < ps.size();) {
     AttnArgs a;
     memset(&a, 0, sizeof(a));

@@ -495,11 +495,17 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
   const int nmp = (int)pairs.size(), nsk = (int)skp.size(), nwp = (int)wp.size();
   // The attention dropout keep words depend only on the rng snapshot: drawn on a side stream
   // (attn_keep_words_kernel) while the projection GEMMs run, so the attention forward reads
-  // them instead of drawing inline.  Pooled plan, training; an existing side stream only
-  // while st is being captured.  MMF_NO_SIDE_STREAM=1: draw inline (A/B).
+  // them instead of drawing inline.  Pooled plan, training, with long-key pairs (C5: the
+  // draws are a third of the one-pass forward's VALU work; at C2's 128 keys the concurrent
+  // draws slow the fp32 GEMMs more than the lean forward gains, 0.979 -> 0.986 ms); an
+  // existing side stream only while st is being captured.  MMF_NO_SIDE_STREAM=1: inline (A/B);
+  // MMF_SIDE_STREAM=1: also without long pairs.
   SideStream* side = nullptr;
+  bool any_long = false;
+  for (const AttnPair& a : pairs) any_long = any_long || a.Lk > 128;
   auto fork_keep_words = [&]() {
     if (!(drop && use_pool(d) && nmp) || getenv("MMF_NO_SIDE_STREAM")) return;
+    if (!any_long && !getenv("MMF_SIDE_STREAM")) return;
     side = side_stream(!prof_capturing(st));
     if (!side) return;
     if (hipEventRecord(side->fork_ev, st) != hipSuccess || hipStreamWaitEvent(side->s, side->fork_ev, 0) != hipSuccess ||

@@ -9,6 +9,8 @@ beyond: several key chunks, several query blocks, unaligned key counts) and
 general (heads x Lk beyond the pooled helpers' LDS budget) -- and the
 standalone CrossModalAttention.
 """
+import re
+
 import numpy as np
 import pytest
 import torch
@@ -237,7 +239,10 @@ def test_stored_probabilities_plan(mods, monkeypatch):
     _, launches = mmf_native.profile_end()
     names = [k for _, k, *_ in launches]
     assert all(k.endswith("false>") for k in names if k.startswith("attn_pool_bwd_fused_lean")), names
-    assert all(k.endswith("false>") for k in names if k.startswith("attn_pool_fwd_lean")), names
+    # (PST, the fourth template argument, false; a trailing KW = true when the keep words came
+    # from the side stream)
+    assert all(re.search(r"<\d+, \d+, (true|false), false(, (true|false))?>$", k)
+               for k in names if k.startswith("attn_pool_fwd_lean")), names
 
 
 
@@ -258,6 +263,7 @@ def test_side_stream_keep_words_match_inline_draws(mods, case_name, prec, monkey
     prev = torch.get_float32_matmul_precision()
     torch.set_float32_matmul_precision(prec)
     try:
+        monkeypatch.setenv("MMF_SIDE_STREAM", "1")   # (the short-key case forks only on request)
         runs = []
         for inline in (False, True):
             if inline:
