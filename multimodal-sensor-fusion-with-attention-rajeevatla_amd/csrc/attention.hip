@@ -2118,7 +2118,8 @@ hipError_t launch_generic(Kind kind, const AttnPair* pairs, int npairs, int B, i
     if (long_lean) pname = with_arg(pname, "true");   // "<hd, pr, true>": the LEAN instantiation
     if (kind == Kind::PoolFwd && lean) pname = with_arg(pname, a.drop_p > 0.f ? "true" : "false");   // DROP
     if (kind == Kind::PoolFwd && lean) pname = with_arg(pname, pst ? "true" : "false");              // PST
-    if (kind == Kind::PoolFwd && lean && !pst && a.drop_p > 0.f && words_ready) pname = with_arg(pname, "true");   // KW
+    if (kind == Kind::PoolFwd && lean)   // KW (rocprofv3 prints every template argument)
+      pname = with_arg(pname, (!pst && a.drop_p > 0.f && words_ready) ? "true" : "false");
     if (kind == Kind::PoolFused) pname = with_arg(pname, pst ? "true" : "false");                    // PST
     ProfLaunch prof_(st, pname, fl, by);
     switch (kind) {
@@ -2239,6 +2240,8 @@ hipError_t launch_attn_pool_fwd(const AttnPair* pairs, int npairs, int B, int he
     e = launch_generic(Kind::PoolFwd, sp.data(), (int)sp.size(), B, heads, hd, scale, drop_p, rng, st, words_ready);
   if (e == hipSuccess && !lp.empty() && attn_long_fwd_ok(lp.data(), (int)lp.size(), hd, drop_p, rng))
     return launch_attn_long_fused_fwd(lp.data(), (int)lp.size(), B, heads, hd, scale, drop_p, rng, st, words_ready);
+  for (const AttnPair& a : lp)   // bf16 Q / K rows only the one-pass kernels read
+    if (a.qk_bf16) return hipErrorInvalidValue;
   if (e == hipSuccess && !lp.empty())
     e = launch_generic(Kind::PoolLse, lp.data(), (int)lp.size(), B, heads, hd, scale, drop_p, rng, st);
   if (e == hipSuccess && !lp.empty())

@@ -104,6 +104,22 @@ __device__ __forceinline__ void load8(const float* row, int d0, int hd, bool val
   if (valid && d0 + 4 < hd) b = *reinterpret_cast<const float4*>(row + d0 + 4);
 }
 
+// Columns [8c, 8c + 8) of element row `off` (element offset of the row's head slice) of a Q
+// or K tensor as bf16: fp32 storage converted (round to nearest even), bf16 storage
+// (AttnPair::qk_bf16, hd % 8 == 0) copied; zero past hd and for an invalid row
+__device__ __forceinline__ bf16x8 row_chunk(const float* base, bool bf, int64_t off, int c, int hd, bool valid) {
+  if (bf) {
+    bf16x8 z;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z[j] = (__bf16)0.f;
+    if (valid && 8 * c < hd) z = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(base) + off + 8 * c);
+    return z;
+  }
+  float4 a, b;
+  load8(base + off, 8 * c, hd, valid, a, b);
+  return to_bf16x8(a, b);
+}
+
 template <bool BITS>
 __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const AttnArgs A) {
   __shared__ __attribute__((aligned(16))) char lds[LF_LDS];
@@ -120,8 +136,8 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
   const float scale = A.scale, pdrop = A.drop_p;
   const float inv_keep = pdrop > 0.f ? (pdrop < 1.f ? 1.f / (1.f - pdrop) : 0.f) : 1.f;
   const float sl2 = scale * LF_LOG2E;
-  const float* Qg = P.q + (int64_t)b * Lq * P.ldq + col0;
-  const float* Kg = P.k + (int64_t)b * Lk * P.ldk + col0;
+  const bool qkb = P.qk_bf16 != 0;
+  const int64_t q_off = (int64_t)b * Lq * P.ldq + col0, k_off = (int64_t)b * Lk * P.ldk + col0;   // elements
   float* dQg = P.dq + (int64_t)b * Lq * P.ldq + col0;
   float* dKg = P.dk + (int64_t)b * Lk * P.ldk + col0;
 
@@ -141,39 +157,39 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
   {
     const int nch = Lk * 8;   // 16-B chunks of the image
     for (int i0 = 0; i0 < nch; i0 += LF_NT * 4) {
-      float4 va[4], vb[4];
+      bf16x8 kv[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int idx = i0 + t + j * LF_NT;
         const int key = idx >> 3, c = idx & 7;
-        load8(Kg + (int64_t)(idx < nch ? key : 0) * P.ldk, 8 * c, hd, idx < nch, va[j], vb[j]);
+        kv[j] = row_chunk(P.k, qkb, k_off + (int64_t)(idx < nch ? key : 0) * P.ldk, c, hd, idx < nch);
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int idx = i0 + t + j * LF_NT;
-        if (idx < nch) *reinterpret_cast<bf16x8*>(lds + OFF_K + img_off(idx >> 3, idx & 7)) = to_bf16x8(va[j], vb[j]);
+        if (idx < nch) *reinterpret_cast<bf16x8*>(lds + OFF_K + img_off(idx >> 3, idx & 7)) = kv[j];
       }
     }
     const float gsc = inv_keep / (float)Lq;   // dP'[q, k] = dpbar[k] / Lq, through the dropout scale
     for (int k = t; k < Lk; k += LF_NT) gs[k] = P.dpbar[bh * Lk + k] * gsc;
   }
   // query block images: threads 0..255 stage row t >> 3, chunk t & 7; threads 256..287 the LSE
-  auto q_load = [&](int qb, float4& a, float4& bq, float& l) {
+  auto q_load = [&](int qb, bf16x8& v, float& l) {
     const int row = (t >> 3) & 31, q = qb * LF_QB + row;
-    load8(Qg + (int64_t)(q < Lq ? q : 0) * P.ldq, 8 * (t & 7), hd, t < 256 && q < Lq, a, bq);
+    v = row_chunk(P.q, qkb, q_off + (int64_t)(q < Lq ? q : 0) * P.ldq, t & 7, hd, t < 256 && q < Lq);
     const int ql = qb * LF_QB + (t & 31);
     l = (t >= 256 && t < 256 + LF_QB && ql < Lq) ? P.lse[bh * Lq + ql] : -INFINITY;
   };
-  auto q_store = [&](int buf, const float4& a, const float4& bq, float l) {
-    if (t < 256) *reinterpret_cast<bf16x8*>(lds + OFF_Q + buf * 4096 + img_off(t >> 3, t & 7)) = to_bf16x8(a, bq);
+  auto q_store = [&](int buf, const bf16x8& v, float l) {
+    if (t < 256) *reinterpret_cast<bf16x8*>(lds + OFF_Q + buf * 4096 + img_off(t >> 3, t & 7)) = v;
     // log2 units; +inf for an invalid or fully masked query: every p = exp2(s - inf) = 0
     if (t >= 256 && t < 256 + LF_QB) lse_s[buf * LF_QB + (t - 256)] = l == -INFINITY ? INFINITY : l * LF_LOG2E;
   };
   {
-    float4 a, bq;
+    bf16x8 v;
     float l;
-    q_load(0, a, bq, l);
-    q_store(0, a, bq, l);
+    q_load(0, v, l);
+    q_store(0, v, l);
   }
   __syncthreads();
 
@@ -196,9 +212,9 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
   for (int qb = 0; qb < nqb; ++qb) {
     const int buf = qb & 1, qbase = qb * LF_QB;
     const bool has_next = qb + 1 < nqb;
-    float4 na = make_float4(0.f, 0.f, 0.f, 0.f), nb = na;
+    bf16x8 nv;
     float nl = -INFINITY;
-    if (has_next) q_load(qb + 1, na, nb, nl);   // in flight during this block
+    if (has_next) q_load(qb + 1, nv, nl);   // in flight during this block
     const char* Qi = lds + OFF_Q + buf * 4096;
     const int q = qbase + r;
     const bool qvalid = q < Lq;
@@ -250,7 +266,7 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
     }
     Dp = sum_xor32(Dp);
     if (hh == 0) Dpart[buf * 256 + w * 32 + r] = Dp;
-    if (has_next) q_store(buf ^ 1, na, nb, nl);
+    if (has_next) q_store(buf ^ 1, nv, nl);
     __syncthreads();   // (A) partial D's, next query block
 
     float D = 0.f;
@@ -438,8 +454,8 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_poolL_fwd_fused_bf16(const At
   const float pdrop = A.drop_p;
   const float inv_keep = pdrop > 0.f ? (pdrop < 1.f ? 1.f / (1.f - pdrop) : 0.f) : 1.f;
   const float sl2 = A.scale * LF_LOG2E;
-  const float* Qg = P.q + (int64_t)b * Lq * P.ldq + col0;
-  const float* Kg = P.k + (int64_t)b * Lk * P.ldk + col0;
+  const bool qkb = P.qk_bf16 != 0;
+  const int64_t q_off = (int64_t)b * Lq * P.ldq + col0, k_off = (int64_t)b * Lk * P.ldk + col0;   // elements
 
   if (P.kmask_mode == 1 && P.kmask[(int64_t)b * P.kmask_ld] == 0.f) {
     // masked key modality: every probability is 0 (src/attention.py:127-129); the keep words
@@ -457,30 +473,30 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_poolL_fwd_fused_bf16(const At
   {
     const int nch = Lk * 8;
     for (int i0 = 0; i0 < nch; i0 += NTW * 4) {
-      float4 va[4], vb[4];
+      bf16x8 kv[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int idx = i0 + t + j * NTW;
-        load8(Kg + (int64_t)(idx < nch ? idx >> 3 : 0) * P.ldk, 8 * (idx & 7), hd, idx < nch, va[j], vb[j]);
+        kv[j] = row_chunk(P.k, qkb, k_off + (int64_t)(idx < nch ? idx >> 3 : 0) * P.ldk, idx & 7, hd, idx < nch);
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int idx = i0 + t + j * NTW;
-        if (idx < nch) *reinterpret_cast<bf16x8*>(lds + FOFF_K + img_off(idx >> 3, idx & 7)) = to_bf16x8(va[j], vb[j]);
+        if (idx < nch) *reinterpret_cast<bf16x8*>(lds + FOFF_K + img_off(idx >> 3, idx & 7)) = kv[j];
       }
     }
   }
-  auto q_load = [&](int qb, float4& a, float4& bq) {
+  auto q_load = [&](int qb, bf16x8& v) {
     const int q = qb * LF_QB + ((t >> 3) & 31);
-    load8(Qg + (int64_t)(q < Lq ? q : 0) * P.ldq, 8 * (t & 7), hd, t < 256 && q < Lq, a, bq);
+    v = row_chunk(P.q, qkb, q_off + (int64_t)(q < Lq ? q : 0) * P.ldq, t & 7, hd, t < 256 && q < Lq);
   };
-  auto q_store = [&](int buf, const float4& a, const float4& bq) {
-    if (t < 256) *reinterpret_cast<bf16x8*>(lds + FOFF_Q + buf * 4096 + img_off(t >> 3, t & 7)) = to_bf16x8(a, bq);
+  auto q_store = [&](int buf, const bf16x8& v) {
+    if (t < 256) *reinterpret_cast<bf16x8*>(lds + FOFF_Q + buf * 4096 + img_off(t >> 3, t & 7)) = v;
   };
   {
-    float4 a, bq;
-    q_load(0, a, bq);
-    q_store(0, a, bq);
+    bf16x8 v;
+    q_load(0, v);
+    q_store(0, v);
   }
   __syncthreads();
 
@@ -495,8 +511,8 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_poolL_fwd_fused_bf16(const At
   for (int qb = 0; qb < nqb; ++qb) {
     const int buf = qb & 1, qbase = qb * LF_QB;
     const bool has_next = qb + 1 < nqb;
-    float4 na = make_float4(0.f, 0.f, 0.f, 0.f), nb = na;
-    if (has_next) q_load(qb + 1, na, nb);
+    bf16x8 nv;
+    if (has_next) q_load(qb + 1, nv);
     const char* Qi = lds + FOFF_Q + buf * 4096;
     const int q = qbase + r;
     const bool qvalid = q < Lq;
@@ -537,7 +553,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_poolL_fwd_fused_bf16(const At
     }
     mx = max_xor32(mx);
     if (hh == 0) Mpart[buf * NW * 32 + w * 32 + r] = mx;
-    if (has_next) q_store(buf ^ 1, na, nb);
+    if (has_next) q_store(buf ^ 1, nv);
     __syncthreads();   // (A) row maxima, next query block
     float m = -INFINITY;
 #pragma unroll
@@ -605,6 +621,7 @@ bool attn_long_fused_ok(const AttnPair* pairs, int npairs, int hd, float drop_p)
     const AttnPair& P = pairs[i];
     if (P.Lk <= 128 || P.Lk > LF_MAXK || P.Lk % 32 != 0 || P.Lq < 1 || P.kmask_mode == 2) return false;
     if (P.ldq % 4 != 0 || P.ldk % 4 != 0 || ((uintptr_t)P.q & 15) != 0 || ((uintptr_t)P.k & 15) != 0) return false;
+    if (P.qk_bf16 && (hd % 8 != 0 || P.ldq % 8 != 0 || P.ldk % 8 != 0)) return false;
     if (!P.dq || !P.dk || !P.dsum || !P.dpbar || !P.lse) return false;
     if (drop_p > 0.f && (!P.keep_bits || P.kw_ld < P.Lk / 32)) return false;
   }
@@ -619,6 +636,7 @@ bool attn_long_fwd_ok(const AttnPair* pairs, int npairs, int hd, float drop_p, c
     const AttnPair& P = pairs[i];
     if (P.Lk <= 128 || P.Lk > LF_MAXK || P.Lk % 32 != 0 || P.Lq < 1 || P.kmask_mode == 2) return false;
     if (P.ldq % 4 != 0 || P.ldk % 4 != 0 || ((uintptr_t)P.q & 15) != 0 || ((uintptr_t)P.k & 15) != 0) return false;
+    if (P.qk_bf16 && (hd % 8 != 0 || P.ldq % 8 != 0 || P.ldk % 8 != 0)) return false;
     if (!P.lse || !P.pbar) return false;
     if (drop_p > 0.f && (!P.keep_bits || P.kw_ld < P.Lk / 32)) return false;
   }

@@ -124,6 +124,7 @@ __device__ __forceinline__ void epilogue(const GemmGroup& G, const TileCtx& T, f
   float* const out = partial ? T.Cb + (int64_t)T.split * G.M * G.N : T.Cb;
   const int ldc = partial ? G.N : G.ldc;
   const bool vst = (ldc % 4) == 0 && ((uintptr_t)out & 15) == 0;
+  const bool vstb = (ldc % 8) == 0 && ((uintptr_t)T.Cb & 15) == 0;   // EPI_BF16: 16-B rows of 8
   // a thread always finishes the same 8 columns (rows t>>4 + 16*it of each 64-row pass)
   const int cg = (t & 15) * 8, j0 = T.j0 + cg;
   const int nv = min(8, G.N - j0);
@@ -202,6 +203,20 @@ __device__ __forceinline__ void epilogue(const GemmGroup& G, const TileCtx& T, f
       if (epi & EPI_COLSUM) {   // the final values back into the image for the column sums
         *reinterpret_cast<f32x4*>(cs + lr * CS + cg) = f32x4{v[0], v[1], v[2], v[3]};
         *reinterpret_cast<f32x4*>(cs + lr * CS + cg + 4) = f32x4{v[4], v[5], v[6], v[7]};
+      }
+      if (epi & EPI_BF16) {   // (never with EPI_PARTIAL; nbatch 1)
+        __bf16* ob = reinterpret_cast<__bf16*>(T.Cb) + (int64_t)i * ldc + j0;
+        if (vstb && nv == 8) {
+          bf16x8 pk;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) pk[e] = (__bf16)v[e];
+          *reinterpret_cast<bf16x8*>(ob) = pk;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (e < nv) ob[e] = (__bf16)v[e];
+        }
+        continue;
       }
       float* o = out + (int64_t)i * ldc + j0;
       if (vst && nv == 8) {
@@ -1149,6 +1164,11 @@ int device_cu_count() { return cu_count(); }
 
 hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, float drop_p,
                        const RngSnap* rng, hipStream_t st, uint64_t* rng_advance) {
+  // bf16 outputs: only the LDS-DMA kernel's epilogue writes them (one batch, no split-K)
+  for (int i = 0; i < njobs; ++i)
+    if ((jobs_in[i].g.epi & EPI_BF16) &&
+        (!job_fast(jobs_in[i], amode, bmode) || jobs_in[i].g.nbatch > 1 || (jobs_in[i].g.epi & EPI_PARTIAL)))
+      return hipErrorInvalidValue;
   {
     bool wsr = njobs > 0;
     for (int i = 0; i < njobs && wsr; ++i)

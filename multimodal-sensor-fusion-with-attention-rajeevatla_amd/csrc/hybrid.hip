@@ -68,10 +68,38 @@ bool pstore_on(const mmf_hybrid_desc* d) {
   return n > 0;
 }
 
-// The tail head takes mean_L P_m from per-tile column sums written by the
-// projection GEMM's epilogue when every 128-row tile lies inside one sample.
+// "medium" long-key pairs on the one-pass kernels (attn_long.hip) keep Q and K in bf16: the
+// Q/K GEMM rounds its output once (EPI_BF16) -- exactly the rounding the kernels applied when
+// they loaded fp32 rows -- so the GEMM writes and the attention kernels read half the bytes.
+// All long pairs or none (the one-pass launches take every long pair); off with
+// return_attention (the attention-map kernels read fp32 Q / K) and whenever the streamed
+// kernels could run (MMF_NO_LONG_FUSED, MMF_NO_FUSED_BWD; MMF_NO_BF16_QK: fp32 Q / K, A/B).
+bool qk_bf16_on(const mmf_hybrid_desc* d) {
+  if (math_mode() != 1 || !use_pool(d) || d->return_attention || getenv("MMF_NO_LONG_FUSED") ||
+      getenv("MMF_NO_FUSED_BWD") || getenv("MMF_NO_BF16_QK"))
+    return false;
+  const int hd = d->hidden / d->num_heads;
+  if (hd > 64 || hd % 8 != 0 || d->hidden % 8 != 0) return false;
+  int n = 0;
+  for (int g = 0; g < d->num_pairs; ++g) {
+    if (single_key(d, g) || wide_pair(d, g)) continue;
+    const int lk = Lm(d, d->pair_k[g]);
+    if (lk <= 128) continue;
+    if (lk > 512 || lk % 32 != 0) return false;
+    ++n;
+  }
+  return n > 0;
+}
+bool pair_qk_bf16(const mmf_hybrid_desc* d, int g) {
+  return !single_key(d, g) && !wide_pair(d, g) && Lm(d, d->pair_k[g]) > 128 && qk_bf16_on(d);
+}
+
+// The head (tail or generic) takes mean_L P_m from per-tile column sums written by the
+// projection GEMM's epilogue when every 128-row tile lies inside one sample (pooled plan):
+// L / 128 rows per sample instead of L (C5: the generic head read 400 MB with one
+// workgroup per sample, 0.35 ms).
 bool pcol_in_proj(const mmf_hybrid_desc* d, int m) {
-  return d->num_pairs && use_tail(d) && Lm(d, m) % 128 == 0 && !getenv("MMF_NO_PCOL");
+  return d->num_pairs && use_pool(d) && Lm(d, m) % 128 == 0 && !getenv("MMF_NO_PCOL");
 }
 
 struct Saved {
@@ -319,9 +347,10 @@ void fill_head(HeadArgs& ha, const mmf_hybrid_desc* d, const mmf_hybrid_params* 
   ha.scale_by_mask = 1;
   int cnt[MMF_MAX_MODALITIES];
   for (int m = 0; m < d->num_modalities; ++m) {
-    ha.src[ha.nsrc] = s.P[m];
+    // mean over L of P_m: from the per-128-row column sums when the projection wrote them
+    ha.src[ha.nsrc] = s.Pcol[m] ? s.Pcol[m] : s.P[m];
     ha.src_mod[ha.nsrc] = m;
-    ha.src_L[ha.nsrc] = Lm(d, m);
+    ha.src_L[ha.nsrc] = s.Pcol[m] ? Lm(d, m) / 128 : Lm(d, m);
     ha.src_scale[ha.nsrc++] = 1.f / (float)Lm(d, m);
     cnt[m] = 1;
     ha.gate_w[m] = W->gate[m].w;
@@ -394,6 +423,7 @@ AttnPair make_pair(const mmf_hybrid_desc* d, const Saved& s, const float* mask, 
   a.keep_bits = s.bits[g];
   a.kw_ld = kw_ld(a.Lk);
   a.pstore = s.pst[g];
+  a.qk_bf16 = pair_qk_bf16(d, g) ? 1 : 0;
   return a;
 }
 
@@ -547,11 +577,12 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
       const int q = d->pair_q[g], k = d->pair_k[g];
       const int lq = Lm(d, q), lk = Lm(d, k);
       if (!single_key(d, g)) {
-        GemmJob jq = make_job(B * lq, H, s.Q[g], H, EPI_BIAS);
+        const int qkb = pair_qk_bf16(d, g) ? EPI_BF16 : 0;
+        GemmJob jq = make_job(B * lq, H, s.Q[g], H, EPI_BIAS | qkb);
         jq.g.bias = W->q[g].b;
         add_src(jq, opnd(s.P[q], H), opnd(W->q[g].w, H), H);
         jobs.push_back(jq);
-        GemmJob jk = make_job(B * lk, H, s.K[g], H, EPI_BIAS);
+        GemmJob jk = make_job(B * lk, H, s.K[g], H, EPI_BIAS | qkb);
         jk.g.bias = W->k[g].b;
         add_src(jk, opnd(s.P[k], H), opnd(W->k[g].w, H), H);
         jobs.push_back(jk);
@@ -797,6 +828,8 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
       }
       if (fe == hipErrorNotSupported) {
         (void)hipGetLastError();
+        for (const AttnPair& a : pairs)
+          if (a.qk_bf16) return fail(MMF_EHIP, "bf16 Q / K pair refused by the one-pass backward");
         for (AttnPair& a : pairs) a.pstore = nullptr;   // the two-pass kernels recompute S
         STAGE_TRY("bwd.attn_dq", launch_attn_pool_bwd(0, pairs.data(), nmp, B, nh, hd, scale, p, rng, st));
         STAGE_TRY("bwd.attn_dk", launch_attn_pool_bwd(1, pairs.data(), nmp, B, nh, hd, scale, p, rng, st));

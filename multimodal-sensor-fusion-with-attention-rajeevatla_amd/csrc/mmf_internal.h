@@ -124,7 +124,8 @@ struct GemmSrc {
 enum : int32_t {
   EPI_BIAS = 1, EPI_RELU = 2, EPI_DROP = 4, EPI_ROWADD = 8, EPI_GATE = 16,
   EPI_ROWSCALE = 32, EPI_PARTIAL = 64, EPI_BIAS_RS = 128, EPI_ADDMAT = 256,
-  EPI_COLSUM = 512
+  EPI_COLSUM = 512,
+  EPI_BF16 = 1024      // store C as bf16 (round to nearest even; C holds __bf16, ldc in elements; nbatch 1)
 };
 
 // Epilogue order: v = alpha*acc; +bias[j] (x bias_rs[i*ld+off] with EPI_BIAS_RS);
@@ -252,6 +253,9 @@ struct AttnPair {
   // g, 64 lanes x float4 = P of lane (query c, half h) at regs 4g..4g+3 (attn_pstore_index);
   // attn_pstore_floats(Lq) floats per (sample, head).
   float* pstore;
+  // Q and K rows stored as bf16 (ldq / ldk in elements): "medium" long-key pairs on the one-pass
+  // kernels (attn_long.hip), whose projections the Q/K GEMM writes in bf16 (EPI_BF16)
+  int32_t qk_bf16;
 };
 
 constexpr int ATTN_MAX_PAIRS = 12;

@@ -222,7 +222,7 @@ def test_stored_probabilities_plan(mods, monkeypatch):
     names = [k for _, k, *_ in launches]
     fwd = [k for k in names if k.startswith("attn_pool_fwd_lean")]
     bwd = [k for k in names if k.startswith("attn_pool_bwd_fused_lean")]
-    assert fwd and all(k.endswith("true, true>") for k in fwd), fwd
+    assert fwd and all(re.search(r"<\d+, \d+, true, true, false>$", k) for k in fwd), fwd   # DROP, PST, KW
     assert bwd and all(k.endswith("true>") for k in bwd), bwd
     # eval mode: nothing stored, the backward recomputes
     model.eval()
