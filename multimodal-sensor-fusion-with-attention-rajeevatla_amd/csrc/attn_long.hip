@@ -83,6 +83,16 @@ __device__ __forceinline__ bf16x8 to_bf16x8(float4 a, float4 b) {
 __device__ __forceinline__ f32x16 mfma_bf16(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
+// sum of N (a power of two) packed pairs as a tree
+template <int N>
+__device__ __forceinline__ float tree_sum(f32x2* p) {
+#pragma unroll
+  for (int n = N / 2; n >= 1; n /= 2)
+#pragma unroll
+    for (int i = 0; i < n; ++i) p[i] = p[i] + p[i + n];
+  return p[0].x + p[0].y;
+}
+
 __device__ __forceinline__ f32x16 zero16f() {
   f32x16 z;
 #pragma unroll
@@ -90,9 +100,12 @@ __device__ __forceinline__ f32x16 zero16f() {
   return z;
 }
 
-// x where bit `bit` of `word` is set, else +0: one v_bfe_i32 (0 / all ones) and one v_and
+// x where bit `bit` of `word` is set, else +0: one v_bfe_i32 (0 / all ones) and one v_and.
+// (Written as asm: from the builtin the compiler forms v_and + v_cmp + v_cndmask, three
+// VALU instructions per element.)
 __device__ __forceinline__ float keep_sel(uint32_t word, int bit, float x) {
-  const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)word, bit, 1);
+  uint32_t m;
+  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(word), "i"(bit));
   return __uint_as_float(__float_as_uint(x) & m);
 }
 
@@ -120,7 +133,9 @@ __device__ __forceinline__ bf16x8 row_chunk(const float* base, bool bf, int64_t 
   return to_bf16x8(a, b);
 }
 
-template <bool BITS>
+// FULL: Lk == LF_MAXK, every wave's two key tiles exist (no per-tile guards, whose skip
+// paths made the compiler zero-fill the tiles' registers every query block)
+template <bool BITS, bool FULL>
 __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const AttnArgs A) {
   __shared__ __attribute__((aligned(16))) char lds[LF_LDS];
   const AttnPair& P = A.p[blockIdx.y];
@@ -205,7 +220,7 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int kt = w + 8 * i;
-      if (kt < nkt) nwords[i] = P.keep_bits[(bh * Lq + r) * kwl + kt] >> (4 * hh);
+      if (FULL || kt < nkt) nwords[i] = P.keep_bits[(bh * Lq + r) * kwl + kt] >> (4 * hh);
     }
   }
 
@@ -225,7 +240,7 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int kt = w + 8 * i;
-        nwords[i] = (kt < nkt && qn < Lq) ? P.keep_bits[(bh * Lq + qn) * kwl + kt] >> (4 * hh) : 0xFFFFFFFFu;
+        nwords[i] = ((FULL || kt < nkt) && qn < Lq) ? P.keep_bits[(bh * Lq + qn) * kwl + kt] >> (4 * hh) : 0xFFFFFFFFu;
       }
     }
     bf16x8 qf[4];
@@ -235,11 +250,11 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
 
     // S^T = K Q^T per own key tile (key in the registers, query on the lane); P, keep * P * g, D
     float pv[2][16], pk[2][16];
-    float Dp = 0.f;
+    f32x2 dpp[16];   // keep * P * g pairs, summed as a packed tree
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int kt = w + 8 * i;
-      if (kt >= nkt) {
+      if (!FULL && kt >= nkt) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) pv[i][e] = pk[i][e] = 0.f;
         continue;
@@ -260,11 +275,14 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
           const float gk = keep_sel(words[i], j + 8 * g, gv[j]);
           pv[i][e] = p;
           pk[i][e] = p * gk;
-          Dp += pk[i][e];
         }
       }
     }
-    Dp = sum_xor32(Dp);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dpp[8 * i + e] = f32x2{pk[i][2 * e], pk[i][2 * e + 1]};
+    const float Dp = sum_xor32(tree_sum<16>(dpp));
     if (hh == 0) Dpart[buf * 256 + w * 32 + r] = Dp;
     if (has_next) q_store(buf ^ 1, nv, nl);
     __syncthreads();   // (A) partial D's, next query block
@@ -291,7 +309,7 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int kt = w + 8 * i;
-      if (kt >= nkt) continue;
+      if (!FULL && kt >= nkt) continue;
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
         const int d0 = 32 * dt + 16 * (g16 & 1) + 4 * pp;
@@ -316,7 +334,7 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int kt = w + 8 * i;
-      if (kt >= nkt) continue;
+      if (!FULL && kt >= nkt) continue;
       // the dS tile [q][key] (registers 4g .. 4g+3 = keys 8g + 4hh + 0..3 of query r)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -348,13 +366,19 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
     {
       const int d = t & 63, j = t >> 6;   // queries 4j .. 4j+3 of column d
       const float* red = reinterpret_cast<const float*>(lds + OFF_R);
-      float4 acc = *reinterpret_cast<const float4*>(red + red_off(d, j));
+      f32x2 a01, a23;   // packed adds
+      {
+        const float4 v = *reinterpret_cast<const float4*>(red + red_off(d, j));
+        a01 = f32x2{v.x, v.y};
+        a23 = f32x2{v.z, v.w};
+      }
 #pragma unroll
       for (int ww = 1; ww < 8; ++ww) {
         const float4 v = *reinterpret_cast<const float4*>(red + ww * 2048 + red_off(d, j));
-        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        a01 += f32x2{v.x, v.y};
+        a23 += f32x2{v.z, v.w};
       }
-      const float av[4] = {acc.x, acc.y, acc.z, acc.w};
+      const float av[4] = {a01.x, a01.y, a23.x, a23.y};
       if (d < hd) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -369,7 +393,7 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int kt = w + 8 * i;
-    if (kt >= nkt) continue;
+    if (!FULL && kt >= nkt) continue;
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt) {
       const int d = 32 * dt + r;
@@ -429,19 +453,18 @@ __global__ __launch_bounds__(256) void attn_keep_words_kernel(const AttnArgs A) 
 // NW waves per workgroup (16: four per SIMD, one key tile each at Lk = 512; 8: two tiles each)
 template <int NW>
 struct FwdLds {
-  static constexpr int K = 0;                                // [LF_MAXK][64] bf16
-  static constexpr int Q = K + LF_MAXK * 128;                // [2][32][64] bf16
+  static constexpr int Q = 0;                                // [2][32][64] bf16
   static constexpr int P = Q + 2 * LF_QB * 128;              // [NW][32 q][32 keys] bf16
   static constexpr int M = P + NW * LF_QB * 64;              // [2][NW][32] fp32 row maxima
   static constexpr int S = M + 2 * NW * LF_QB * 4;           // [2][NW][32] fp32 row sums
-  static constexpr int BYTES = S + 2 * NW * LF_QB * 4;       // 94 KB (8 waves) / 112 KB (16)
+  static constexpr int BYTES = S + 2 * NW * LF_QB * 4;       // 28 KB (8 waves) / 48 KB (16)
 };
 
 template <bool DROP, int NW = 16>
 __global__ __launch_bounds__(NW * 64, 1) void attn_poolL_fwd_fused_bf16(const AttnArgs A) {
   constexpr int NTW = NW * 64, TPW = 16 / NW;   // threads; key tiles per wave (Lk <= 512)
   using L_ = FwdLds<NW>;
-  constexpr int FOFF_K = L_::K, FOFF_Q = L_::Q, FOFF_P = L_::P, FOFF_M = L_::M, FOFF_S = L_::S;
+  constexpr int FOFF_Q = L_::Q, FOFF_P = L_::P, FOFF_M = L_::M, FOFF_S = L_::S;
   __shared__ __attribute__((aligned(16))) char lds[L_::BYTES];
   const AttnPair& P = A.p[blockIdx.y];
   if ((int)blockIdx.x >= A.B * A.heads) return;
@@ -470,21 +493,15 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_poolL_fwd_fused_bf16(const At
   float* Mpart = reinterpret_cast<float*>(lds + FOFF_M);
   float* Spart = reinterpret_cast<float*>(lds + FOFF_S);
 
-  {
-    const int nch = Lk * 8;
-    for (int i0 = 0; i0 < nch; i0 += NTW * 4) {
-      bf16x8 kv[4];
+  // each wave's key tiles stay in registers for every query block (the MFMA A operand:
+  // lane (r, hh) holds columns [16 s4 + 8 hh, +8) of key row 32 kt + r)
+  bf16x8 kf[TPW][4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int idx = i0 + t + j * NTW;
-        kv[j] = row_chunk(P.k, qkb, k_off + (int64_t)(idx < nch ? idx >> 3 : 0) * P.ldk, idx & 7, hd, idx < nch);
-      }
+  for (int i = 0; i < TPW; ++i) {
+    const int krow = (w + NW * i) * 32 + r;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int idx = i0 + t + j * NTW;
-        if (idx < nch) *reinterpret_cast<bf16x8*>(lds + FOFF_K + img_off(idx >> 3, idx & 7)) = kv[j];
-      }
-    }
+    for (int s4 = 0; s4 < 4; ++s4)
+      kf[i][s4] = row_chunk(P.k, qkb, k_off + (int64_t)(krow < Lk ? krow : 0) * P.ldk, 2 * s4 + hh, hd, krow < Lk);
   }
   auto q_load = [&](int qb, bf16x8& v) {
     const int q = qb * LF_QB + ((t >> 3) & 31);
@@ -535,23 +552,17 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_poolL_fwd_fused_bf16(const At
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
       const int kt = w + NW * i;
-      if (kt >= nkt) {
-#pragma unroll
-        for (int e = 0; e < 16; ++e) x[i][e] = -INFINITY;
-        continue;
-      }
+      if (kt >= nkt) continue;   // (x[i] is not read for a missing tile)
       f32x16 s = zero16f();
-      const int krow = kt * 32 + r;
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4)
-        s = mfma_bf16(*reinterpret_cast<const bf16x8*>(lds + FOFF_K + img_off(krow, 2 * s4 + hh)), qf[s4], s);
+      for (int s4 = 0; s4 < 4; ++s4) s = mfma_bf16(kf[i][s4], qf[s4], s);
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        x[i][e] = s[e] * sl2;   // log2 units
+        x[i][e] = s[e];   // raw scores; the scale (> 0) folds into the exp's FMA
         mx = fmaxf(mx, x[i][e]);
       }
     }
-    mx = max_xor32(mx);
+    mx = max_xor32(mx) * sl2;   // log2 units (max(s) * c == max(s * c) for c > 0)
     if (hh == 0) Mpart[buf * NW * 32 + w * 32 + r] = mx;
     if (has_next) q_store(buf ^ 1, nv);
     __syncthreads();   // (A) row maxima, next query block
@@ -559,23 +570,37 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_poolL_fwd_fused_bf16(const At
 #pragma unroll
     for (int ww = 0; ww < NW; ++ww) m = fmaxf(m, Mpart[buf * NW * 32 + ww * 32 + r]);
     const float mref = m == -INFINITY ? 0.f : m;
+    // row sums as packed trees (v_pk_add_f32, two adds per instruction, no serial chain)
     float ls = 0.f;
 #pragma unroll
-    for (int i = 0; i < TPW; ++i)
+    for (int i = 0; i < TPW; ++i) {
+      if (w + NW * i >= nkt) continue;   // wave-uniform
+      f32x2 pr[8];
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        x[i][e] = __builtin_amdgcn_exp2f(x[i][e] - mref);
-        ls += x[i][e];
+      for (int e = 0; e < 16; e += 2) {
+        x[i][e] = __builtin_amdgcn_exp2f(__builtin_fmaf(x[i][e], sl2, -mref));
+        x[i][e + 1] = __builtin_amdgcn_exp2f(__builtin_fmaf(x[i][e + 1], sl2, -mref));
+        pr[e >> 1] = f32x2{x[i][e], x[i][e + 1]};
       }
+      ls += tree_sum<8>(pr);
+    }
     ls = sum_xor32(ls);
     if (hh == 0) Spart[buf * NW * 32 + w * 32 + r] = ls;
     __syncthreads();   // (B) row sums
-    float l = 0.f;
+    float l;
+    {
+      float sp[NW];   // (scalar tree: packed adds would need the ds_read2 pairs re-registered)
 #pragma unroll
-    for (int ww = 0; ww < NW; ++ww) l += Spart[buf * NW * 32 + ww * 32 + r];
+      for (int ww = 0; ww < NW; ++ww) sp[ww] = Spart[buf * NW * 32 + ww * 32 + r];
+#pragma unroll
+      for (int n = NW / 2; n >= 1; n /= 2)
+#pragma unroll
+        for (int i = 0; i < n; ++i) sp[i] += sp[i + n];
+      l = sp[0];
+    }
     if (w == 0 && hh == 0 && qvalid) P.lse[bh * Lq + q] = l > 0.f ? (m + __log2f(l)) * (1.f / LF_LOG2E) : -INFINITY;
     // P' / Lq of this lane's query (0 for a query past Lq)
-    const float cq = (qvalid && l > 0.f) ? inv_keep / (l * (float)Lq) : 0.f;
+    const float cq = (qvalid && l > 0.f) ? inv_keep * __builtin_amdgcn_rcpf(l * (float)Lq) : 0.f;
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
       const int kt = w + NW * i;
@@ -739,31 +764,41 @@ hipError_t launch_attn_long_fused_bwd(const AttnPair* pairs, int npairs, int B, 
                                       float drop_p, hipStream_t st) {
   if (!attn_long_fused_ok(pairs, npairs, hd, drop_p)) return hipErrorNotSupported;
   const bool bits = drop_p > 0.f;
-  for (int done = 0; done < npairs;) {
-    AttnArgs a;
-    memset(&a, 0, sizeof(a));
-    int n = 0;
-    double fl = 0.0, by = 0.0;
-    while (done < npairs && n < ATTN_MAX_PAIRS) {
-      a.p[n] = pairs[done++];
-      const double lq = a.p[n].Lq, lk = a.p[n].Lk, H = (double)heads * hd;
-      fl += 2.0 * (2.0 * B * lq * lk * H);          // dQ and dK contractions (S recompute not counted)
-      by += 4.0 * (2.0 * B * lq * H + 2.0 * B * lk * H);   // Q, K in; dQ, dK out
-      ++n;
+  // pairs with Lk == LF_MAXK take the guard-free FULL instantiation, in launches of their own
+  for (int full = 1; full >= 0; --full) {
+    std::vector<AttnPair> ps;
+    for (int i = 0; i < npairs; ++i)
+      if ((pairs[i].Lk == LF_MAXK) == (full != 0)) ps.push_back(pairs[i]);
+    for (size_t done = 0; done < ps.size();) {
+      AttnArgs a;
+      memset(&a, 0, sizeof(a));
+      int n = 0;
+      double fl = 0.0, by = 0.0;
+      while (done < ps.size() && n < ATTN_MAX_PAIRS) {
+        a.p[n] = ps[done++];
+        const double lq = a.p[n].Lq, lk = a.p[n].Lk, H = (double)heads * hd;
+        fl += 2.0 * (2.0 * B * lq * lk * H);          // dQ and dK contractions (S recompute not counted)
+        by += 4.0 * (2.0 * B * lq * H + 2.0 * B * lk * H);   // Q, K in; dQ, dK out
+        ++n;
+      }
+      a.npairs = n;
+      a.B = B;
+      a.heads = heads;
+      a.hd = hd;
+      a.scale = scale;
+      a.drop_p = drop_p;
+      a.nblk = B * heads;
+      const dim3 grid((unsigned)(B * heads), (unsigned)n);
+      static const char* const kName[4] = {"attn_poolL_bwd_fused_bf16<false, false>", "attn_poolL_bwd_fused_bf16<false, true>",
+                                           "attn_poolL_bwd_fused_bf16<true, false>", "attn_poolL_bwd_fused_bf16<true, true>"};
+      ProfLaunch prof_(st, kName[2 * bits + full], fl, by);
+      if (bits && full) mmf_launch((attn_poolL_bwd_fused_bf16<true, true>), grid, dim3(LF_NT), 0, st, a);
+      else if (bits) mmf_launch((attn_poolL_bwd_fused_bf16<true, false>), grid, dim3(LF_NT), 0, st, a);
+      else if (full) mmf_launch((attn_poolL_bwd_fused_bf16<false, true>), grid, dim3(LF_NT), 0, st, a);
+      else mmf_launch((attn_poolL_bwd_fused_bf16<false, false>), grid, dim3(LF_NT), 0, st, a);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
     }
-    a.npairs = n;
-    a.B = B;
-    a.heads = heads;
-    a.hd = hd;
-    a.scale = scale;
-    a.drop_p = drop_p;
-    a.nblk = B * heads;
-    const dim3 grid((unsigned)(B * heads), (unsigned)n);
-    ProfLaunch prof_(st, bits ? "attn_poolL_bwd_fused_bf16<true>" : "attn_poolL_bwd_fused_bf16<false>", fl, by);
-    if (bits) mmf_launch(attn_poolL_bwd_fused_bf16<true>, grid, dim3(LF_NT), 0, st, a);
-    else mmf_launch(attn_poolL_bwd_fused_bf16<false>, grid, dim3(LF_NT), 0, st, a);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
   }
   return hipSuccess;
 }

@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <vector>
 
 #include "mmf_device.h"
@@ -54,10 +55,31 @@ struct TileCtx {
   int brs_off;
 };
 
+// XCD-aware group interleave (see group_of_block): 0 off, 1 launches without split-K groups
+// (the default: C5 projections 2.58 -> 2.47 ms/step; the split-K weight gradients were
+// slower interleaved, 2.00 -> 2.27 ms), 2 every launch.  MMF_GEMM_ILV overrides.
+int gemm_interleave_mode() {
+  const char* e = getenv("MMF_GEMM_ILV");
+  if (!e || !e[0]) return 1;
+  return e[0] == '0' ? 0 : (e[0] == '2' ? 2 : 1);
+}
+
 // The grid is 1-D over the tiles of every group of the launch, in group order
-// (launch_gemm puts the longest contractions first).
+// (launch_gemm puts the longest contractions first).  With args.ilv the groups
+// are interleaved instead: workgroups are dealt round-robin to the 8 XCDs, so
+// block b runs on XCD b % 8; its (b / 8)-th block there takes group (b/8) % ng
+// at local tile 8 * ((b/8) / ng) + b % 8.  Every group's copy of one local tile
+// then runs back to back on the same XCD, and groups that share an operand
+// (the projections of one modality read the same P_m rows; the weight
+// gradients of one modality the same P_m k-chunk) hit that XCD's L2 for it.
 __device__ __forceinline__ int group_of_block(const GemmArgs& args, int& local) {
   const int b = blockIdx.x;
+  if (args.ilv) {
+    const int idx = b >> 3, ng = args.ngroups;
+    const int k = idx / ng;
+    local = k * 8 + (b & 7);
+    return idx - k * ng;
+  }
   int g = 0;
 #pragma unroll
   for (int i = 1; i < GEMM_MAX_GROUPS; ++i)
@@ -1234,10 +1256,30 @@ hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, 
     for (int s = 0; s < jobs_in[i].nsrc; ++s) kk += jobs_in[i].src[s].K;
     work[i] = partial ? (double)g.kchunk : kk;
   }
+  // With the interleave on, jobs of equal work are further clustered by their
+  // most-shared operand (the pointer that the most jobs of this call read), so
+  // one launch holds the groups that can share it in L2.
+  const int ilv_mode = gemm_interleave_mode();
+  bool any_partial = false;
+  for (int i = 0; i < njobs; ++i) any_partial |= (jobs_in[i].g.epi & EPI_PARTIAL) != 0;
+  const bool ilv_on = ilv_mode == 2 || (ilv_mode == 1 && !any_partial);
+  std::vector<uintptr_t> share(njobs, 0);
+  if (ilv_on) {
+    std::map<uintptr_t, int> uses;
+    for (int i = 0; i < njobs; ++i) {
+      ++uses[(uintptr_t)jobs_in[i].src[0].a.ptr];
+      ++uses[(uintptr_t)jobs_in[i].src[0].b.ptr];
+    }
+    for (int i = 0; i < njobs; ++i) {
+      const uintptr_t a = (uintptr_t)jobs_in[i].src[0].a.ptr, b = (uintptr_t)jobs_in[i].src[0].b.ptr;
+      share[i] = uses[b] > uses[a] ? b : a;
+    }
+  }
   std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
     const bool fx = job_fast(jobs_in[x], amode, bmode), fy = job_fast(jobs_in[y], amode, bmode);
     if (fx != fy) return fx;
-    return work[x] > work[y];
+    if (work[x] != work[y]) return work[x] > work[y];
+    return share[x] < share[y];
   });
   int done = 0;
   while (done < njobs) {
@@ -1271,6 +1313,13 @@ hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, 
     }
     if (ng == 0) return hipErrorInvalidValue;
     args.ngroups = ng;
+    if (ilv_on && ng > 1) {
+      const int T = args.tile_off[1];
+      bool even = T > 0 && T % 8 == 0;
+      for (int gi = 1; gi < ng && even; ++gi)
+        even = (gi + 1 < ng ? args.tile_off[gi + 1] : max_blocks) - args.tile_off[gi] == T;
+      args.ilv = even ? 1 : 0;
+    }
     if (max_blocks > 0) {
       dim3 grid(max_blocks, 1);
       double fl = 0.0, by = 0.0;

@@ -171,6 +171,7 @@ struct GemmArgs {
   float drop_p;              // p of every dropout site in this launch
   const RngSnap* rng;
   uint64_t* rng_advance;     // optional: block 0 advances this live rng state's offset
+  int32_t ilv;               // 1: XCD-aware group interleave (every group has tile_off[1] tiles, a multiple of 8)
 };
 
 // Host-side description of one output (group) and its sources; launch_gemm

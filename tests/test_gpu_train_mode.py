@@ -293,3 +293,39 @@ def test_side_stream_keep_words_match_inline_draws(mods, case_name, prec, monkey
     assert torch.equal(l1, l2)
     for a, b in zip(dx1 + dw1, dx2 + dw2):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("prec", ["highest", "medium"])
+def test_gemm_group_interleave_is_bit_exact(mods, prec, monkeypatch):
+    """The XCD-aware group interleave of the GEMM launcher (MMF_GEMM_ILV=2, every launch: the groups of one
+    launch dealt tile by tile, clustered by their shared operand) only reorders whole output
+    tiles, so a training step gives the same logits and gradients bit for bit."""
+    fusion, _ = mods
+    names, dims = ["a", "b", "c"], {"a": 24, "b": 40, "c": 16}
+    case = HybridCase("ilv", names, dims, {"a": 256, "b": 256, "c": 256}, batch=4, hidden=128,
+                      heads=2, classes=4, seed=57, mask=[[1, 1, 1], [0.5, 1, 1], [1, 0, 1], [1, 1, 1]])
+    sd = hybrid_state(case.names, case.dims, case.hidden, case.classes, case.seed)
+    feats_np, mask_np, grad_np = hybrid_inputs(case)
+    prev = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision(prec)
+    try:
+        runs = []
+        for ilv in ("0", "2"):
+            monkeypatch.setenv("MMF_GEMM_ILV", ilv)
+            model = fusion.HybridFusion({m: case.dims[m] for m in case.names}, hidden_dim=case.hidden,
+                                        num_classes=case.classes, num_heads=case.heads, dropout=P)
+            model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+            model = model.cuda().train()
+            model._rng_state.copy_(torch.tensor([SEED, OFFSET], dtype=torch.int64))
+            feats = {m: torch.from_numpy(v).cuda().requires_grad_(True) for m, v in feats_np.items()}
+            logits = model(feats, torch.from_numpy(mask_np).cuda())
+            (logits * torch.from_numpy(grad_np).cuda()).sum().backward()
+            torch.cuda.synchronize()
+            runs.append((logits.detach(), [feats[m].grad for m in case.names],
+                         [p_.grad.clone() for p_ in model.parameters()]))
+    finally:
+        torch.set_float32_matmul_precision(prev)
+    (l1, dx1, dw1), (l2, dx2, dw2) = runs
+    assert torch.equal(l1, l2)
+    for a, b in zip(dx1 + dw1, dx2 + dw2):
+        assert torch.equal(a, b)
