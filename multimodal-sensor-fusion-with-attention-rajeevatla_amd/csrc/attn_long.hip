@@ -524,13 +524,30 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_poolL_fwd_fused_bf16(const At
 #pragma unroll
   for (int i = 0; i < TPW; ++i) cs[i] = zero16f();   // every row of C = the column sums of P'
   char* Pw = lds + FOFF_P + w * 2048;
+  // S = K Q^T of the own tiles for query block `qb` (raw scores; the scale folds into the
+  // exp's FMA).  Block qb + 1's products are issued right after barrier A of block qb, so
+  // the matrix cores run them under that block's exp / sum phase.
+  auto scores = [&](int qbuf, f32x16 (&sc)[TPW]) {
+    const char* Qi = lds + FOFF_Q + qbuf * 4096;
+    bf16x8 qf[4];
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) qf[s4] = *reinterpret_cast<const bf16x8*>(Qi + img_off(r, 2 * s4 + hh));
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+      if (w + NW * i >= nkt) continue;   // (not read for a missing tile)
+      sc[i] = zero16f();
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) sc[i] = mfma_bf16(kf[i][s4], qf[s4], sc[i]);
+    }
+  };
+  f32x16 sn[TPW];
+  scores(0, sn);
 
   for (int qb = 0; qb < nqb; ++qb) {
     const int buf = qb & 1, qbase = qb * LF_QB;
     const bool has_next = qb + 1 < nqb;
     bf16x8 nv;
     if (has_next) q_load(qb + 1, nv);
-    const char* Qi = lds + FOFF_Q + buf * 4096;
     const int q = qbase + r;
     const bool qvalid = q < Lq;
     // the keep words of the own tiles (attn_keep_words_kernel), consumed after barrier B
@@ -544,21 +561,14 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_poolL_fwd_fused_bf16(const At
         if (kt < nkt) kw[i] = P.keep_bits[(bh * Lq + q) * kwl + kt] >> (4 * hh);
       }
     }
-    bf16x8 qf[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(Qi + img_off(r, 2 * s + hh));
     float x[TPW][16];
     float mx = -INFINITY;
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
-      const int kt = w + NW * i;
-      if (kt >= nkt) continue;   // (x[i] is not read for a missing tile)
-      f32x16 s = zero16f();
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) s = mfma_bf16(kf[i][s4], qf[s4], s);
+      if (w + NW * i >= nkt) continue;   // (x[i] is not read for a missing tile)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        x[i][e] = s[e];   // raw scores; the scale (> 0) folds into the exp's FMA
+        x[i][e] = sn[i][e];
         mx = fmaxf(mx, x[i][e]);
       }
     }
@@ -566,6 +576,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_poolL_fwd_fused_bf16(const At
     if (hh == 0) Mpart[buf * NW * 32 + w * 32 + r] = mx;
     if (has_next) q_store(buf ^ 1, nv);
     __syncthreads();   // (A) row maxima, next query block
+    if (has_next) scores(buf ^ 1, sn);
     float m = -INFINITY;
 #pragma unroll
     for (int ww = 0; ww < NW; ++ww) m = fmaxf(m, Mpart[buf * NW * 32 + ww * 32 + r]);
