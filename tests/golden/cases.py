@@ -418,6 +418,23 @@ LATE_CASES: List[LateCase] = [
 ]
 
 
+# EarlyFusion (src/fusion.py:17-123): BASELINE config C1's fusion (CPU plumbing, no HIP part)
+EARLY_CASES: List[LateCase] = [
+    LateCase("early_3mod", ["imu_hand", "imu_chest", "imu_ankle"], {"imu_hand": 17, "imu_chest": 17, "imu_ankle": 17},
+             batch=6, hidden=32, classes=12, seed=93,
+             mask=[[1, 1, 1], [1, 0, 1], [0, 0, 0], [0, 0, 1], [0.5, 1, 0], [1, 1, 0]]),
+]
+
+
+def early_state(case: LateCase) -> "OrderedDict[str, np.ndarray]":
+    rng = np.random.default_rng(case.seed)
+    sd: "OrderedDict[str, np.ndarray]" = OrderedDict()
+    width = sum(case.dims[m] for m in case.names)
+    for i, (o, k) in enumerate(((case.hidden, width), (case.hidden, case.hidden), (case.classes, case.hidden))):
+        sd[f"fusion.{3 * i}.weight"], sd[f"fusion.{3 * i}.bias"] = _linear(rng, o, k)
+    return sd
+
+
 def late_state(case: LateCase) -> "OrderedDict[str, np.ndarray]":
     rng = np.random.default_rng(case.seed)
     sd: "OrderedDict[str, np.ndarray]" = OrderedDict()

@@ -16,7 +16,8 @@ What is recorded (eval mode, ``torch.set_float32_matmul_precision("highest")``):
   * standalone CrossModalAttention (src/attention.py:68-146), TemporalAttention
     (src/attention.py:149-281) and PairwiseModalityAttention (:284-424).
   * FrameEncoder attention pooling (src/encoders.py:210-336) and LateFusion
-    (src/fusion.py:126-245), the §8(f) masked-softmax weighting ops.
+    (src/fusion.py:126-245), the §8(f) masked-softmax weighting ops; EarlyFusion
+    (src/fusion.py:17-123), config C1's fusion.
   * for a fixed upstream gradient G: d(sum(out * G)) w.r.t. inputs and params.
 
 Run:  python tests/golden/gen_golden.py [case1,case2,...]
@@ -34,8 +35,8 @@ HERE = Path(__file__).resolve().parent
 sys.path.insert(0, str(HERE))
 REF_SRC = Path("/root/reference/src")
 
-from cases import (CMA_CASES, FRAMEPOOL_CASES, HYBRID_CASES, LATE_CASES, PAIRWISE_CASES, SEQENC_CASES,  # noqa: E402
-                   TEMPORAL_CASES, cma_inputs, cma_state, framepool_inputs, framepool_state,
+from cases import (CMA_CASES, EARLY_CASES, FRAMEPOOL_CASES, HYBRID_CASES, LATE_CASES, PAIRWISE_CASES, SEQENC_CASES,  # noqa: E402
+                   TEMPORAL_CASES, cma_inputs, cma_state, early_state, framepool_inputs, framepool_state,
                    hybrid_inputs, hybrid_state, late_inputs, late_state, pair_names,
                    pairwise_inputs, pairwise_state, temporal_inputs, seqenc_inputs, seqenc_state)
 
@@ -250,6 +251,24 @@ def gen_late(ref_fusion, case):
     return out
 
 
+def gen_early(ref_fusion, case):
+    """EarlyFusion (src/fusion.py:17-123): logits and gradients of sum(logits * G)."""
+    model = ref_fusion.EarlyFusion({m: case.dims[m] for m in case.names}, hidden_dim=case.hidden,
+                                   num_classes=case.classes, dropout=0.1)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in early_state(case).items()}, strict=True)
+    model.eval()
+    feats_np, mask_np, grad = late_inputs(case)
+    feats = {m: torch.from_numpy(v).requires_grad_(True) for m, v in feats_np.items()}
+    logits = model(feats, torch.from_numpy(mask_np))
+    (logits * torch.from_numpy(grad)).sum().backward()
+    out = {"logits": logits.detach().numpy()}
+    for m in case.names:
+        out[f"dx/{m}"] = feats[m].grad.numpy()
+    for name, p in model.named_parameters():
+        out[f"grad/{name}"] = p.grad.numpy()
+    return out
+
+
 def gen_seqenc(ref_encoders, case):
     """SequenceEncoder(encoder_type="lstm") (src/encoders.py:34-166): encoding, top-layer output
     sequence, and gradients of sum(encoding * g) w.r.t. the sequence and every parameter."""
@@ -284,6 +303,7 @@ def main():
     for cases, gen, mod in ((CMA_CASES, gen_cma, ref_attention), (TEMPORAL_CASES, gen_temporal, ref_attention),
                             (PAIRWISE_CASES, gen_pairwise, ref_attention),
                             (FRAMEPOOL_CASES, gen_framepool, ref_encoders), (LATE_CASES, gen_late, ref_fusion),
+                            (EARLY_CASES, gen_early, ref_fusion),
                             (SEQENC_CASES, gen_seqenc, ref_encoders)):
         for case in cases:
             if only and case.name not in only:

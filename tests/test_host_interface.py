@@ -175,3 +175,30 @@ def test_deepcopy_and_plan_descriptor(mods):
     assert all(e <= o2 for e, o2 in zip(ends, plan.offsets[1:])) and ends[-1] <= plan.num_param_elems
     views = plan.grad_views(torch.zeros(plan.num_param_elems), params)
     assert [v.shape for v in views] == [p.shape for p in params]
+
+
+def test_early_fusion_matches_reference(mods):
+    """BASELINE config C1's fusion: EarlyFusion (src/fusion.py:17-123) is plain-torch plumbing
+    (concat of masked features -> MLP, no HIP part) and runs on CPU as the reference's does;
+    logits and every gradient equal the reference's on tests/golden/early_3mod.npz."""
+    from cases import EARLY_CASES, early_state, late_inputs
+    fusion, _ = mods
+    torch.set_float32_matmul_precision("highest")
+    for case in EARLY_CASES:
+        fx = load_fixture(case.name)
+        model = fusion.EarlyFusion({m: case.dims[m] for m in case.names}, hidden_dim=case.hidden,
+                                   num_classes=case.classes, dropout=0.1)
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in early_state(case).items()}, strict=True)
+        model.eval()
+        feats_np, mask_np, grad = late_inputs(case)
+        feats = {m: torch.from_numpy(v).requires_grad_(True) for m, v in feats_np.items()}
+        logits = model(feats, torch.from_numpy(mask_np))
+        (logits * torch.from_numpy(grad)).sum().backward()
+        tol = dict(rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(logits.detach().numpy(), fx["logits"], **tol)
+        for m in case.names:
+            np.testing.assert_allclose(feats[m].grad.numpy(), fx[f"dx/{m}"], **tol)
+        for name, p in model.named_parameters():
+            np.testing.assert_allclose(p.grad.numpy(), fx[f"grad/{name}"], **tol, err_msg=name)
+        with pytest.raises(ValueError, match="Expected 2D tensor"):
+            model({m: torch.zeros(2, 3, case.dims[m]) for m in case.names})
