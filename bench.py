@@ -157,11 +157,16 @@ def kernel_table(launches, steps):
     return out
 
 
-def pmc_traffic():
-    """HBM bytes per launch by kernel name from the committed PMC summary
-    (profiles/pmc_traffic.py output: FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE,
-    KiB -> bytes, averaged over the dispatches of an eager run of this bench)."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def pmc_traffic(workload="c2", precision="highest"):
+    """HBM bytes per launch by kernel name from the committed PMC summary of THIS workload
+    and precision (profiles/pmc_traffic.py output: FETCH_SIZE x2 (gfx950 correction) +
+    WRITE_SIZE, KiB -> bytes, averaged over the dispatches of an eager run of this bench):
+    profiles/pmc_traffic.json for the C2 headline, profiles/pmc_traffic_<workload>_<precision>.json
+    otherwise; none (traffic null) when no pass of that workload is committed -- the kernel
+    names repeat across workloads, their bytes do not."""
+    name = "pmc_traffic.json" if (workload, precision) == ("c2", "highest") else \
+        f"pmc_traffic_{workload}_{precision}.json"
+    path = os.path.join(ROOT, "profiles", name)
     if not os.path.exists(path):
         return {}, None
     with open(path) as f:
@@ -169,11 +174,11 @@ def pmc_traffic():
     return d.get("kernels", {}), d.get("source")
 
 
-def dominant_roofline(kernels):
+def dominant_roofline(kernels, workload="c2", precision="highest"):
     """Roofline of the kernel with the most time per step."""
     kname = next(iter(kernels))
     k = kernels[kname]
-    traffic, src = pmc_traffic()
+    traffic, src = pmc_traffic(workload, precision)
     t = traffic.get(kname, {}).get("hbm_bytes_per_launch")
     per_launch = k["flops_per_launch"] if k["bound"] == "mfma" else k["bytes_per_launch"]
     return {
@@ -407,7 +412,7 @@ def main(argv=None):
     loss = float(trainer.loss.item())
 
     if rank == 0:
-        roofline = dominant_roofline(kernels)
+        roofline = dominant_roofline(kernels, args.workload, args.precision)
         step_fl = total_step_flops(wr)
         cpu = None
         if world == 1 and not args.skip_cpu:
