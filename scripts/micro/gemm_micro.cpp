@@ -77,6 +77,23 @@ int main() {
       one.push_back(j);
     }
     run("dZ_1src", one, MODE_RK, MODE_KR, 3.0 * 4 * 2 * R * H * H);
+    // marginal cost of the main loop: the same launch at K = 2H and K = 8H (fixed prologue /
+    // epilogue, k-loop length x1/4 and x2)
+    for (int K : {16, 32, 64, 128, 256, 1024}) {
+      std::vector<GemmJob> kv;
+      float* ak = dev((size_t)3 * R * K);
+      float* wk = dev((size_t)3 * K * H);
+      for (int m = 0; m < 3; ++m) {
+        GemmJob j = make_job(R, H, out + (size_t)m * R * H, H, 0);
+        add_src(j, opnd(ak + (size_t)m * R * K, K), opnd(wk + (size_t)m * K * H, H), K);
+        kv.push_back(j);
+      }
+      char name[32];
+      snprintf(name, sizeof(name), "dZ_K%d", K);
+      run(name, kv, MODE_RK, MODE_KR, 3.0 * 2 * R * H * K);
+      (void)hipFree(ak);
+      (void)hipFree(wk);
+    }
     // probe: the same FLOPs with every row tile reading the SAME 128 A rows (L2-resident):
     // if this is much faster, the real launch is bound by streaming A from HBM
     {
