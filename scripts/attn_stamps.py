@@ -106,6 +106,23 @@ def main():
         # first 4 residents of this CU: how far apart did they start?
         if len(v) >= 4:
             spreads.append(v[3] - v[0])
+    # residency: the most workgroups alive at once on one CU (start / end stamps share that CU's
+    # XCD clock), and the mean number alive over the CU's busy span
+    ev = {}
+    for k, s0, s1 in zip(cu_key, st[:, 0], st[:, last]):
+        ev.setdefault(int(k), []).append((int(s0), int(s1)))
+    peak, mean_alive = [], []
+    for k, v in ev.items():
+        pts = sorted([(a, 1) for a, _ in v] + [(b, -1) for _, b in v])
+        cur = best = 0
+        for _, d in pts:
+            cur += d
+            best = max(best, cur)
+        peak.append(best)
+        span = max(b for _, b in v) - min(a for a, _ in v)
+        mean_alive.append(sum(b - a for a, b in v) / span if span > 0 else 0.0)
+    out["resident_wgs_per_cu_peak_median"] = float(np.median(peak))
+    out["resident_wgs_per_cu_mean_alive"] = float(np.mean(mean_alive))
     out["cus_seen"] = len(starts)
     out["wgs_per_cu_mean"] = float(np.mean([len(v) for v in starts.values()]))
     out["first4_start_spread_cycles_median"] = float(np.median(spreads)) if spreads else None
