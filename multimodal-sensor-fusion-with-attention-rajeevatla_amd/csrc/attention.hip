@@ -1443,7 +1443,7 @@ __global__ __launch_bounds__(NT, HDP == 32 ? 4 : 2) void attn_pool_fwd_lean(cons
         if (kt < nkt) {
           const uint32_t wk = words[kt] >> (4 * h);   // reg r = 4g + j <-> key bit 8g + 4h + j
 #pragma unroll
-          for (int r = 0; r < 16; ++r) sv[kt][r] = ((wk >> (8 * (r >> 2) + (r & 3))) & 1u) ? sv[kt][r] * f : 0.f;
+          for (int r = 0; r < 16; ++r) sv[kt][r] = keep_sel(wk, 8 * (r >> 2) + (r & 3), sv[kt][r] * f);
           colacc[kt] += colsum_tile(sv[kt], c);
         }
       }
@@ -1821,8 +1821,7 @@ __device__ __forceinline__ void fused_lean_item(const AttnArgs& A, const AttnPai
         for (int j = 0; j < 4; ++j) {
           const float p = kt < nkt ? pp[j] : 0.f;
           pr[kt][4 * g + j] = p;
-          const bool keep = (kwh[kt] >> (8 * g + j)) & 1u;
-          D += keep ? p * gg[j] : 0.f;
+          D += p * keep_sel(kwh[kt], 8 * g + j, gg[j]);
         }
       }
     }
@@ -1830,12 +1829,17 @@ __device__ __forceinline__ void fused_lean_item(const AttnArgs& A, const AttnPai
     float qf[HALF];
     load_frag_vec<HALF>(qf, Qs + q * LS + h * HALF);
     const float c2 = scale * LOG2E;
-    f32x16 s_nx = dot_rows<HALF, BF>(Ks + c * LS + h * HALF, qf, zero16());
+    // one accumulator per key tile (tile kt + 1's chain issued before tile kt's exp / D work):
+    // a rotating "next" accumulator was copied each tile, and the copy waited (s_nop) for the
+    // chain it had just issued to finish
+    f32x16 sacc[NKT];
+    sacc[0] = dot_rows<HALF, BF>(Ks + c * LS + h * HALF, qf, zero16());
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
       if (kt < nkt) {
-        const f32x16 s = s_nx;
-        if (kt + 1 < nkt) s_nx = dot_rows<HALF, BF>(Ks + ((kt + 1) * 32 + c) * LS + h * HALF, qf, zero16());
+        if (kt + 1 < NKT && kt + 1 < nkt)
+          sacc[kt + 1] = dot_rows<HALF, BF>(Ks + ((kt + 1) * 32 + c) * LS + h * HALF, qf, zero16());
+        const f32x16& s = sacc[kt];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const float4 gv = *reinterpret_cast<const float4*>(gk + kt * 32 + 8 * g + 4 * h);
@@ -1845,8 +1849,7 @@ __device__ __forceinline__ void fused_lean_item(const AttnArgs& A, const AttnPai
             const int r = 4 * g + j;
             const float p = fast_exp2(fmaf(s[r], c2, -lse2));
             pr[kt][r] = p;
-            const bool keep = (kwh[kt] >> (8 * g + j)) & 1u;
-            D += keep ? p * gg[j] : 0.f;
+            D += p * keep_sel(kwh[kt], 8 * g + j, gg[j]);   // keep ? p * G : 0
           }
         }
       } else {
@@ -1883,8 +1886,7 @@ __device__ __forceinline__ void fused_lean_item(const AttnArgs& A, const AttnPai
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int r = 4 * g + j;
-            const bool keep = (kwh[kt] >> (8 * g + j)) & 1u;
-            pr[kt][r] = pr[kt][r] * ((keep ? gg[j] : 0.f) - D);
+            pr[kt][r] = pr[kt][r] * (keep_sel(kwh[kt], 8 * g + j, gg[j]) - D);
           }
         }
 #pragma unroll

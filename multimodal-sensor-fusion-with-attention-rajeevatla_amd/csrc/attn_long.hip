@@ -100,15 +100,6 @@ __device__ __forceinline__ f32x16 zero16f() {
   return z;
 }
 
-// x where bit `bit` of `word` is set, else +0: one v_bfe_i32 (0 / all ones) and one v_and.
-// (Written as asm: from the builtin the compiler forms v_and + v_cmp + v_cndmask, three
-// VALU instructions per element.)
-__device__ __forceinline__ float keep_sel(uint32_t word, int bit, float x) {
-  uint32_t m;
-  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(word), "i"(bit));
-  return __uint_as_float(__float_as_uint(x) & m);
-}
-
 // 8 columns [d0, d0 + 8) of a row (zero past hd; hd % 4 == 0, 16-B aligned rows)
 __device__ __forceinline__ void load8(const float* row, int d0, int hd, bool valid, float4& a, float4& b) {
   a = make_float4(0.f, 0.f, 0.f, 0.f);

@@ -126,6 +126,15 @@ __device__ __forceinline__ float sum32(float v) {  // over the lane's half (32 l
 }
 __device__ __forceinline__ float sum64(float v) { return sum32(sum_xor32(v)); }
 
+// x where bit `bit` of `word` is set, else +0: one v_bfe_i32 (0 / all ones) and one v_and.
+// (Written as asm: from the builtin the compiler forms v_and + v_cmp + v_cndmask, three
+// VALU instructions per element.)
+__device__ __forceinline__ float keep_sel(uint32_t word, int bit, float x) {
+  uint32_t m;
+  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(word), "i"(bit));
+  return __uint_as_float(__float_as_uint(x) & m);
+}
+
 // ---------------------------------------------------------------- Philox4x32-10
 __device__ __forceinline__ uint4 philox10(uint4 c, uint32_t k0, uint32_t k1) {
   // the key schedule is rebuilt per call (2 SALU per round): hoisted, its 20 words
