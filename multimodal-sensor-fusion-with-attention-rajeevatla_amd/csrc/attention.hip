@@ -1718,14 +1718,16 @@ __device__ __forceinline__ void fused_issue_loads(const AttnArgs& A, const AttnP
   const int Lq = P.Lq, Lk = P.Lk;
   const float* kb = P.k + (int64_t)b * Lk * P.ldk + col0;
   const float* qb = P.q + (int64_t)b * Lq * P.ldq + col0;
+  // (32-bit element offsets from the wave-uniform bases: one v_mad per load instead of a
+  // 64-bit address computation each)
 #pragma unroll
   for (int i = 0; i < FusedLoads<HDP, PST>::PER; ++i) {
     const int idx = t + i * NT;
     const int r = idx / C4, c4 = (idx % C4) * 4;
     L.k[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     L.q[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (r < Lk && c4 < hd) L.k[i] = *reinterpret_cast<const float4*>(kb + (int64_t)r * P.ldk + c4);
-    if (r < Lq && c4 < hd) L.q[i] = *reinterpret_cast<const float4*>(qb + (int64_t)r * P.ldq + c4);
+    if (r < Lk && c4 < hd) L.k[i] = *reinterpret_cast<const float4*>(kb + (uint32_t)(r * P.ldk + c4));
+    if (r < Lq && c4 < hd) L.q[i] = *reinterpret_cast<const float4*>(qb + (uint32_t)(r * P.ldq + c4));
   }
   const int q = w * 32 + c;
   const int qq = q < Lq ? q : Lq - 1;
@@ -1946,13 +1948,16 @@ MMF_CHAIN16(dq[dt], Ks[(kt * 32 + acc_row(r, h)) * LS + dt * 32 + c], pr[kt][r])
   }
   BSTAMP(5)
   if (!kwave) return;
+  // the wave's 32 key rows from a uniform base; per store a 32-bit offset (row multiples of
+  // ldk are scalar)
+  float* const dkb = P.dk + ((int64_t)b * Lk + w * 32) * P.ldk + col0;
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) {
     const int d = dt * 32 + c;
     if (d >= hd) continue;
 #pragma unroll
     for (int r = 0; r < 16; ++r)
-      P.dk[((int64_t)b * Lk + w * 32 + acc_row(r, h)) * P.ldk + col0 + d] = dk[dt][r] * scale;
+      dkb[(uint32_t)(acc_row(r, h) * P.ldk + d)] = dk[dt][r] * scale;
   }
   BSTAMP(6)
   BSTAMP_RT(8)
