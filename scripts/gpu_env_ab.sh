@@ -1,15 +1,18 @@
-# One bench workload under several environment settings, same box (top kernels).
-# usage (on the box): bash scripts/gpu_env_ab.sh <run-name> "<bench args>" "<ENV=VAL ...>" ["<ENV=VAL ...>" ...]
+# Same-box A/B of the C2 step under plan switches read from the environment:
+# default, MMF_SIDE_STREAM=1 (keep words on a side stream), MMF_PSTORE=1 (stored probabilities).
+# usage: bash scripts/gpu_env_ab.sh <run-name>
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-RUN=${1:-envab}; shift
-ARGS=$1; shift
-O=gpurun_out/$RUN
+O=gpurun_out/${1:-envab}
 mkdir -p $O
-i=0
-for E in "$@"; do
-  i=$((i+1))
-  env $E timeout -k 10 300 python -u bench.py --steps 50 --warmup 10 --skip-cpu $ARGS > $O/bench_$i.json 2> $O/bench_$i.err || exit 1
-  python3 -c "import json;d=json.load(open('$O/bench_$i.json'));print('$E', d['ms_per_step'], d['value']);[print('   %-40s %8.1f us' % (k[:40], v['avg_launch_ms']*1e3)) for k,v in list(d['kernels'].items())[:12] if 'tail' in k]"
+for i in 1 2; do
+  for v in default side pstore; do
+    unset MMF_SIDE_STREAM MMF_PSTORE
+    [ $v = side ] && export MMF_SIDE_STREAM=1
+    [ $v = pstore ] && export MMF_PSTORE=1
+    timeout -k 10 300 python -u bench.py --workload c2 --steps 50 --warmup 10 --skip-cpu > $O/c2_${v}_$i.json 2> $O/c2_${v}_$i.err || exit 1
+    echo "$v $i ok"
+  done
 done
+echo done
