@@ -531,10 +531,17 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
   // existing side stream only while st is being captured.  MMF_NO_SIDE_STREAM=1: inline (A/B);
   // MMF_SIDE_STREAM=1: also without long pairs.
   SideStream* side = nullptr;
+  // MMF_KW_SERIAL=1 (A/B): the draws on st, ahead of the projection GEMM.  At C2 the lean forward
+  // drops 112-116 -> 90 us but the draw kernel takes 26.5 us: 0.968 -> 0.971-0.975 ms
+  bool kw_serial = false;
   bool any_long = false;
   for (const AttnPair& a : pairs) any_long = any_long || a.Lk > 128;
   auto fork_keep_words = [&]() {
     if (!(drop && use_pool(d) && nmp) || getenv("MMF_NO_SIDE_STREAM")) return;
+    if (getenv("MMF_KW_SERIAL")) {
+      kw_serial = launch_attn_keep_words(pairs.data(), nmp, B, nh, p, rng, st) == hipSuccess;
+      return;
+    }
     if (!any_long && !getenv("MMF_SIDE_STREAM")) return;
     side = side_stream(!prof_capturing(st));
     if (!side) return;
@@ -602,7 +609,7 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
   if (d->num_pairs && pool) {
     // (3p) attention -> LSE, pbar = mean_q P'; U = pbar P_k; Obar = U W_v^T + r b_v; Abar = out_proj
     if (nmp)
-      STAGE_TRY("fwd.attn", launch_attn_pool_fwd(pairs.data(), nmp, B, nh, hd, scale, p, rng, st, side != nullptr));
+      STAGE_TRY("fwd.attn", launch_attn_pool_fwd(pairs.data(), nmp, B, nh, hd, scale, p, rng, st, side != nullptr || kw_serial));
     if (nsk) STAGE_TRY("fwd.attn_single_key", launch_sk_fwd(skp.data(), nsk, B, nh, hd, p, rng, st));
     if (nwp) STAGE_TRY("fwd.attn_wide", launch_wide_fwd(wp.data(), nwp, B, nh, hd, scale, p, rng, true, st));
     std::vector<PoolPair> pp(d->num_pairs);
