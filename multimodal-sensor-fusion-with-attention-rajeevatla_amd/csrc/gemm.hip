@@ -1037,11 +1037,11 @@ __global__ __launch_bounds__(256) void partial_reduce_kernel(const ReduceArgs a)
 
 // ------------------------------------------------------------------ input mask + dropout
 // X'_m = X_m * mask[:, m] * keep / (1-p) for every modality in one launch
-// (blockIdx.y = modality); a thread handles the 8 elements of one Philox block.
+// (blockIdx.x = modality, blockIdx.y = chunk of 256 Philox blocks); a thread handles the 8
+// elements of one Philox block.  Workgroups blockIdx.x >= n draw the attention keep words of
+// pair blockIdx.x - n instead (a.kw): VALU work interleaved with the HBM-bound mask rows.
 __global__ __launch_bounds__(256) void mask_dropout_rows_kernel(const MaskDropArgs a) {
-  const int m = blockIdx.y;
-  const MaskDropJob& J = a.j[m];
-  const int64_t n = J.rows * J.D;
+  const int m = blockIdx.x;
   const bool drop = a.p > 0.f && (a.rng != nullptr || a.rng_live != nullptr);
   RngSnap rs{0, 0};
   {
@@ -1053,10 +1053,37 @@ __global__ __launch_bounds__(256) void mask_dropout_rows_kernel(const MaskDropAr
     }
   }
   const uint32_t thr = p16(a.p);
+  if (m >= a.n) {
+    // keep words, as attn_keep_words_kernel: bit j of word kt of row (b, head, q) keeps element
+    // row Lk + 32 kt + j of the pair's stream
+    const MaskDropArgs::KeepWordJob& K = a.kw[m - a.n];
+    const uint32_t nkt = K.Lk >> 5;
+    const uint32_t nwords = (uint32_t)a.B * (uint32_t)a.heads * K.Lq * nkt;
+    for (uint32_t i = blockIdx.y * 256u + threadIdx.x; i < nwords; i += gridDim.y * 256u) {
+      const uint32_t row = (nkt & (nkt - 1)) == 0 ? i >> (31 - __builtin_clz(nkt)) : i / nkt;
+      const uint32_t kt = i - row * nkt;
+      const uint64_t blk0 = ((uint64_t)row * K.Lk + 32 * kt) >> 3;
+      uint32_t bits = 0;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const uint4 rr = philox_block(rs, K.site, blk0 + g);
+        const uint32_t wv[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          bits |= ((wv[k] & 0xFFFFu) >= thr ? 1u : 0u) << (8 * g + 2 * k);
+          bits |= ((wv[k] >> 16) >= thr ? 1u : 0u) << (8 * g + 2 * k + 1);
+        }
+      }
+      K.bits[(uint64_t)row * K.kw_ld + kt] = bits;
+    }
+    return;
+  }
+  const MaskDropJob& J = a.j[m];
+  const int64_t n = J.rows * J.D;
   const float inv_keep = a.p < 1.f ? 1.f / (1.f - a.p) : 0.f;
   const int D = J.D, L = J.L, M = a.M;
-  for (int64_t blk = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; blk * 8 < n;
-       blk += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t blk = (int64_t)blockIdx.y * blockDim.x + threadIdx.x; blk * 8 < n;
+       blk += (int64_t)gridDim.y * blockDim.x) {
     uint4 r = make_uint4(0, 0, 0, 0);
     if (drop) r = philox_block(rs, J.site, (uint64_t)blk);
     const int64_t base = blk * 8;
@@ -1419,18 +1446,24 @@ hipError_t launch_reduce(const ReduceJob* jobs, int njobs, hipStream_t st) {
 }
 
 hipError_t launch_mask_dropout(MaskDropArgs a, hipStream_t st) {
-  if (a.n < 1 || a.n > 8) return hipErrorInvalidValue;
+  if (a.n < 1 || a.n > 8 || a.nkw < 0 || a.nkw > 16) return hipErrorInvalidValue;
   int64_t maxblk = 1;
   for (int m = 0; m < a.n; ++m) {
     MaskDropJob& J = a.j[m];
     J.vec = (J.D % 8) == 0 && ((uintptr_t)J.x & 15) == 0 && ((uintptr_t)J.out & 15) == 0;
     maxblk = std::max<int64_t>(maxblk, (J.rows * J.D + 7) / 8);
   }
-  const int grid = (int)std::min<int64_t>((maxblk + 255) / 256, 2048);
   double by = 0.0;
   for (int m = 0; m < a.n; ++m) by += 8.0 * a.j[m].rows * a.j[m].D;   // read x, write x'
+  for (int i = 0; i < a.nkw; ++i) {
+    const int64_t nw = (int64_t)a.B * a.heads * a.kw[i].Lq * (a.kw[i].Lk / 32);
+    if (a.kw[i].Lk % 32 != 0 || nw >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+    maxblk = std::max<int64_t>(maxblk, nw);   // one thread per word
+    by += 4.0 * nw;
+  }
+  const int grid = (int)std::min<int64_t>((maxblk + 255) / 256, 2048);
   ProfLaunch prof_(st, "mask_dropout_rows_kernel", 0.0, by);
-  mmf_launch(mask_dropout_rows_kernel, dim3(grid, a.n), dim3(256), 0, st, a);
+  mmf_launch(mask_dropout_rows_kernel, dim3(a.n + a.nkw, grid), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

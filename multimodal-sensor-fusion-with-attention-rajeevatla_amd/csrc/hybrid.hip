@@ -534,10 +534,16 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
   // MMF_KW_SERIAL=1 (A/B): the draws on st, ahead of the projection GEMM.  At C2 the lean forward
   // drops 112-116 -> 90 us but the draw kernel takes 26.5 us: 0.968 -> 0.971-0.975 ms
   bool kw_serial = false;
+  // Without long-key pairs (and at most 16 pairs) the draws are made by extra workgroups of the
+  // input-mask kernel, interleaved with its HBM-bound rows: at C2 the lean forward drops
+  // 113 -> 91 us and the mask kernel grows 23 -> 41 us, step 0.969 -> 0.960 ms median
+  // (DESIGN §7).  MMF_NO_KW_FUSED=1: off; MMF_KW_FUSED=1: also with long-key pairs.
+  bool kw_fused = false;
   bool any_long = false;
   for (const AttnPair& a : pairs) any_long = any_long || a.Lk > 128;
   auto fork_keep_words = [&]() {
     if (!(drop && use_pool(d) && nmp) || getenv("MMF_NO_SIDE_STREAM")) return;
+    if (kw_fused) return;
     if (getenv("MMF_KW_SERIAL")) {
       kw_serial = launch_attn_keep_words(pairs.data(), nmp, B, nh, p, rng, st) == hipSuccess;
       return;
@@ -571,6 +577,20 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
       j.g.drop_site = SITE_PROJ + m;
       add_src(j, opnd(s.Xd[m], D), opnd(W->proj[m].w, D), D);
       jobs.push_back(j);
+    }
+    if (drop && use_pool(d) && nmp && !getenv("MMF_NO_SIDE_STREAM") && !getenv("MMF_SIDE_STREAM") &&
+        !getenv("MMF_KW_SERIAL") && !getenv("MMF_NO_KW_FUSED") && (!any_long || getenv("MMF_KW_FUSED"))) {
+      int nkw = 0;
+      bool fits = true;
+      for (const AttnPair& a : pairs) {
+        if (!(a.keep_bits && a.Lk % 32 == 0 && a.Lk > 0 && a.kw_ld >= a.Lk / 32)) continue;
+        if (nkw == 16) { fits = false; break; }
+        ma.kw[nkw++] = {a.keep_bits, (uint32_t)a.Lq, (uint32_t)a.Lk, (uint32_t)a.kw_ld, a.drop_site};
+      }
+      ma.nkw = fits ? nkw : 0;
+      ma.B = B;
+      ma.heads = nh;
+      kw_fused = fits;
     }
     STAGE_TRY("fwd.input_mask", launch_mask_dropout(ma, st));
     fork_keep_words();   // the rng snapshot exists from here on
@@ -609,7 +629,7 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
   if (d->num_pairs && pool) {
     // (3p) attention -> LSE, pbar = mean_q P'; U = pbar P_k; Obar = U W_v^T + r b_v; Abar = out_proj
     if (nmp)
-      STAGE_TRY("fwd.attn", launch_attn_pool_fwd(pairs.data(), nmp, B, nh, hd, scale, p, rng, st, side != nullptr || kw_serial));
+      STAGE_TRY("fwd.attn", launch_attn_pool_fwd(pairs.data(), nmp, B, nh, hd, scale, p, rng, st, side != nullptr || kw_serial || kw_fused));
     if (nsk) STAGE_TRY("fwd.attn_single_key", launch_sk_fwd(skp.data(), nsk, B, nh, hd, p, rng, st));
     if (nwp) STAGE_TRY("fwd.attn_wide", launch_wide_fwd(wp.data(), nwp, B, nh, hd, scale, p, rng, true, st));
     std::vector<PoolPair> pp(d->num_pairs);

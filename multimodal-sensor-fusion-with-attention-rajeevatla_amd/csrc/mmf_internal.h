@@ -212,6 +212,10 @@ struct MaskDropArgs {
   // a later launch of the call (launch_gemm's rng_advance)
   const uint64_t* rng_live;
   RngSnap* rng_snap;
+  // optional: the attention dropout keep words of up to 16 pairs (attn_keep_words_kernel's
+  // words, same Philox stream), drawn by extra workgroups interleaved with the mask ones
+  struct KeepWordJob { uint32_t* bits; uint32_t Lq, Lk, kw_ld, site; } kw[16];
+  int32_t nkw, B, heads;
 };
 hipError_t launch_mask_dropout(MaskDropArgs a, hipStream_t st);
 

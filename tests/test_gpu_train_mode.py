@@ -259,12 +259,13 @@ def test_stored_probabilities_plan(mods, monkeypatch):
 
 
 
-@pytest.mark.parametrize("case_name,prec", [("train_lean", "highest"), ("train_long_hd64", "medium")])
-def test_side_stream_keep_words_match_inline_draws(mods, case_name, prec, monkeypatch):
-    """The attention dropout keep words drawn on the side stream while the projection GEMMs run
-    (attn_keep_words_kernel; the lean forward's KW variant and the one-pass long forward read
-    them) are the words the kernels draw inline (MMF_NO_SIDE_STREAM=1): same logits and
-    gradients bit for bit."""
+@pytest.mark.parametrize("case_name,prec,mode", [("train_lean", "highest", "side"), ("train_long_hd64", "medium", "side"),
+                                                 ("train_lean", "highest", "fused"), ("train_lean", "medium", "fused")])
+def test_side_stream_keep_words_match_inline_draws(mods, case_name, prec, mode, monkeypatch):
+    """The attention dropout keep words drawn ahead of the attention forward -- on the side stream
+    while the projection GEMMs run (attn_keep_words_kernel, mode "side") or by extra workgroups of
+    the input-mask kernel (the default without long-key pairs, mode "fused") -- are the words the
+    kernels draw inline (MMF_NO_SIDE_STREAM=1): same logits and gradients bit for bit."""
     fusion, _ = mods
     import mmf_native
     case = next(c for c in TRAIN_CASES if c.name == case_name)
@@ -276,7 +277,8 @@ def test_side_stream_keep_words_match_inline_draws(mods, case_name, prec, monkey
     prev = torch.get_float32_matmul_precision()
     torch.set_float32_matmul_precision(prec)
     try:
-        monkeypatch.setenv("MMF_SIDE_STREAM", "1")   # (the short-key case forks only on request)
+        if mode == "side":
+            monkeypatch.setenv("MMF_SIDE_STREAM", "1")   # (the short-key case forks only on request)
         runs = []
         for inline in (False, True):
             if inline:
@@ -299,8 +301,13 @@ def test_side_stream_keep_words_match_inline_draws(mods, case_name, prec, monkey
     finally:
         torch.set_float32_matmul_precision(prev)
     (l1, dx1, dw1, n1), (l2, dx2, dw2, n2) = runs
-    assert "attn_keep_words_kernel" in n1, n1
-    if case_name == "train_lean":   # (the one-pass long forward draws with the same kernel, in line)
+    if mode == "fused":
+        assert "attn_keep_words_kernel" not in n1 and "mask_dropout_rows_kernel" in n1, n1
+        assert any(k.startswith("attn_pool_fwd_lean") and k.endswith("true, false, true>") for k in n1), n1
+        assert not any(k.startswith("attn_pool_fwd_lean") and k.endswith("true, false, true>") for k in n2), n2
+    else:
+        assert "attn_keep_words_kernel" in n1, n1
+    if case_name == "train_lean" and mode == "side":   # (the one-pass long forward draws with the same kernel, in line)
         assert "attn_keep_words_kernel" not in n2, n2
         assert any(k.startswith("attn_pool_fwd_lean") and k.endswith("true, false, true>") for k in n1), n1
     assert torch.equal(l1, l2)
