@@ -430,7 +430,7 @@ def main(argv=None):
             "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
-            "dtype": {"highest": "fp32", "high": "fp32 as bf16x3 (hi + lo operands, fp32 accumulate)",
+            "dtype": {"highest": "fp32", "high": "bf16x3 (fp32 operands split into bf16 hi + lo, three bf16 MFMAs, fp32 accumulate)",
                       "medium": "bf16 (fp32 accumulate)"}[args.precision],
             "data": "synthetic (N(0,1) encoder outputs, random-init weights, seeded)",
             "config": {"workload": f"{args.workload}: HybridFusion M={M} B={B}/gpu L={lens or 1}"

@@ -96,12 +96,16 @@ class HybridTrainStep:
         self.clip_norm = gradient_clip_norm
         self.pg = process_group
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
-        # the step's own dropout state (the module's buffer is left untouched): every rank
-        # starts from the same seed (identical weights), so the rank is folded into the
-        # Philox key of this copy, or the dropout streams would repeat across ranks
-        self.rng = model._rng_state.detach().clone()
-        if self.world > 1:
-            self.rng[0] ^= torch.distributed.get_rank(process_group) * 0x9E3779B1
+        # dropout state: the module's own {seed, offset} buffer, which every step advances on the
+        # device -- a second step object on the same model (a new batch shape, the next epoch)
+        # continues the stream instead of repeating its masks.  Every rank starts from the same
+        # seed (identical weights), so the rank is folded into the module's Philox key once
+        # (as harness.DPTrainer does), or the dropout streams would repeat across ranks
+        if self.world > 1 and not getattr(model, "_mmf_rank_folded", False):
+            with torch.no_grad():
+                model._rng_state[0] ^= torch.distributed.get_rank(process_group) * 0x9E3779B1
+            model._mmf_rank_folded = True
+        self.rng = model._rng_state
         # static input buffers (graph replays read these addresses)
         self.x = [_nat.f32c(f.to(dev)).clone() for f in feats]
         self.mask = _nat.f32c(mask).clone()

@@ -34,15 +34,15 @@ def keep_mask(shape, site: int, seed: int, offset: int, p: float) -> np.ndarray:
     """8 decisions per Philox call: block idx>>3, word (idx>>1)&3, 16-bit half idx&1;
     keep iff u16 >= ceil(p * 65536) (csrc/mmf_device.h keep1/keep4)."""
     n = int(np.prod(shape))
-    idx = np.arange(n, dtype=np.uint64)
-    blk = idx >> np.uint64(3)
-    words = philox10(blk & _MASK, blk >> np.uint64(32), np.full(n, site, np.uint64),
-                     np.full(n, offset & 0xFFFFFFFF, np.uint64), seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
-    sel = ((idx >> np.uint64(1)) & np.uint64(3)).astype(np.int64)
-    w = np.choose(sel, words)
-    half = (idx & np.uint64(1)) * np.uint64(16)
-    u16 = (w >> half) & np.uint64(0xFFFF)
-    thr = np.uint64(int(np.ceil(np.float32(p) * np.float32(65536.0))))
+    nblk = (n + 7) // 8
+    blk = np.arange(nblk, dtype=np.uint64)
+    words = philox10(blk & _MASK, blk >> np.uint64(32), np.full(nblk, site, np.uint64),
+                     np.full(nblk, offset & 0xFFFFFFFF, np.uint64), seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
+    # one call per 8 elements: element idx takes word (idx >> 1) & 3, half idx & 1 -- the
+    # little-endian u16 order of the call's four u32 words
+    w32 = np.stack([w.astype(np.uint32) for w in words], axis=1)
+    u16 = w32.view("<u2").reshape(-1)[:n]
+    thr = np.uint16(int(np.ceil(np.float32(p) * np.float32(65536.0))))
     return (u16 >= thr).reshape(shape)
 
 

@@ -55,6 +55,51 @@ class bf16_matmul_mode(torch.overrides.TorchFunctionMode):
         return func(*args, **kwargs)
 
 
+def _split3(x: torch.Tensor):
+    hi = _bf16(x)
+    return hi, _bf16(x - hi)
+
+
+class _Bf16x3MatMul(torch.autograd.Function):
+    """matmul as matmul precision "high" computes it on the device (csrc/mmf_device.h, PR = 2):
+    each fp32 operand split into hi = bf16(x) and lo = bf16(x - hi), the three products
+    lo_a hi_b + hi_a lo_b + hi_a hi_b accumulated in fp32, lo_a lo_b dropped -- forward AND
+    backward (every dS / dP / weight-gradient contraction takes the same split)."""
+
+    @staticmethod
+    def _mm(a, b):
+        ah, al = _split3(a)
+        bh, bl = _split3(b)
+        return torch.matmul(al, bh) + torch.matmul(ah, bl) + torch.matmul(ah, bh)
+
+    @staticmethod
+    def forward(ctx, a, b):
+        ctx.save_for_backward(a, b)
+        return _Bf16x3MatMul._mm(a, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        ga = _Bf16x3MatMul._mm(g, b.transpose(-1, -2))
+        gb = _Bf16x3MatMul._mm(a.transpose(-1, -2), g)
+        while ga.dim() > a.dim():
+            ga = ga.sum(0)
+        while gb.dim() > b.dim():
+            gb = gb.sum(0)
+        return ga, gb
+
+
+class bf16x3_matmul_mode(torch.overrides.TorchFunctionMode):
+    """Routes every Tensor.matmul / torch.matmul of the oracle through _Bf16x3MatMul."""
+
+    def __torch_function__(self, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        if func in (torch.Tensor.matmul, torch.matmul) and not kwargs:
+            with torch._C.DisableTorchFunction():
+                return _Bf16x3MatMul.apply(*args)
+        return func(*args, **kwargs)
+
+
 def oracle_hybrid(case: HybridCase, dtype=torch.float32, bf16_matmul: bool = False):
     """Run the CPU oracle on the case; returns (outputs dict, param grads, input grads).
     bf16_matmul: every matmul with bf16 operands (bf16_matmul_mode)."""

@@ -144,9 +144,11 @@ def _gpu_rank(rank: int, world: int, port: int, out: str) -> None:
         step = HybridTrainStep(model, [f.to(dev) for f in lf], lm.to(dev), ll.to(dev),
                                process_group=dist.group.WORLD)
         # every rank starts from the same seed; the step folds the rank into the Philox key of
-        # its own copy of the dropout state and leaves the module's buffer untouched
+        # the module's dropout state (once) and advances that buffer itself
         assert int(step.rng[0].item()) == seed0 ^ (rank * 0x9E3779B1)
-        assert int(model._rng_state[0].item()) == seed0
+        assert step.rng.data_ptr() == model._rng_state.data_ptr()
+        HybridTrainStep(model, [f.to(dev) for f in lf], lm.to(dev), ll.to(dev), process_group=dist.group.WORLD)
+        assert int(model._rng_state[0].item()) == seed0 ^ (rank * 0x9E3779B1)   # not folded twice
         step.forward_backward()
         step.allreduce()
         torch.cuda.synchronize(dev)

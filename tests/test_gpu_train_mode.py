@@ -16,7 +16,7 @@ import pytest
 import torch
 
 from _philox import keep_mask, mask_provider
-from _util import close
+from _util import bf16x3_matmul_mode, close
 from cases import HybridCase, hybrid_inputs, hybrid_state
 
 pytestmark = pytest.mark.gpu
@@ -79,10 +79,17 @@ TRAIN_CASES = [
 
 @pytest.fixture(params=["highest", "high"])
 def precision(request):
-    """Train mode at "highest" (fp32 MFMA) and "high" (bf16x3), same tolerance; at "high"
-    key_proj.bias grads at the reference's noise level (<= 1e-3 of the call's largest
-    gradient: mathematically zero by softmax shift invariance) get an absolute floor of 1e-3
-    of that gradient (tests/test_gpu_parity.py); Q / K grads at L = 1 must be exact zeros."""
+    """Train mode at "highest" (fp32 MFMA) and "high" (bf16x3), same 1e-3 tolerance.  At "high"
+    each tensor must match the bf16x3-emulated oracle (tests/_util.bf16x3_matmul_mode: every
+    matmul of the reference algorithm, forward and backward, on hi / lo bf16 operand splits) or
+    the fp32 oracle.  The emulation is needed where a projection pre-activation sits within the
+    bf16x3 rounding of zero: its ReLU gate flips (train_b128: z = -7.6e-7 at m1[115, 24, 14] and
+    -1.0e-8 at m2[25, 88, 16]) and that row's dZ / dX moves by up to 4.5e-2 of the tensor's
+    largest element -- in the reference algorithm itself under "high" (scripts/diag_bf16x3_oracle.py
+    reproduces the device's errors digit for digit).  key_proj.bias grads at the
+    reference's noise level (<= 1e-3 of the call's largest gradient: mathematically zero by
+    softmax shift invariance) get an absolute floor of 1e-3 of that gradient
+    (tests/test_gpu_parity.py); Q / K grads at L = 1 must be exact zeros."""
     prev = torch.get_float32_matmul_precision()
     torch.set_float32_matmul_precision(request.param)
     yield request.param
@@ -91,12 +98,6 @@ def precision(request):
 
 @pytest.mark.parametrize("case", TRAIN_CASES, ids=lambda c: c.name)
 def test_hybrid_train_mode_matches_oracle(mods, case, precision):
-    if case.name == "train_b128" and precision == "high":
-        # at 128 samples the Q / K input-gradient path's cancellation (dS = P (G - D) on
-        # probabilities from bf16x3 scores) shows at the 1e-2 level in a few samples' dX
-        # (scripts/diag_train_case.py): this case is pinned at fp32 MFMA, where
-        # every tensor agrees to <= 4e-6 of its largest element
-        pytest.skip("bf16x3 cancellation at this batch size; the case is pinned at fp32")
     fusion, _ = mods
     from oracle.hybrid_cpu import hybrid_forward
     sd = hybrid_state(case.names, case.dims, case.hidden, case.classes, case.seed)
@@ -117,25 +118,39 @@ def test_hybrid_train_mode_matches_oracle(mods, case, precision):
     ref, rinfo = hybrid_forward(params, case.names, xs, torch.from_numpy(mask_np), case.heads, p=P,
                                 train=True, gen=mask_provider(SEED, OFFSET, P))
     (ref * torch.from_numpy(grad_np)).sum().backward()
-    assert close(logits.detach().cpu(), ref.detach(), RTOL, ATOL)
-    assert close(info["fusion_weights"].cpu(), rinfo["fusion_weights"].detach(), RTOL, ATOL)
-    for key, amap in info["attention_maps"].items():
-        assert close(amap.cpu(), rinfo["attention_maps"][key].detach(), RTOL, ATOL), key
-    refs = [xs[m].grad for m in case.names] + [params[n].grad for n, _ in model.named_parameters()]
-    scale = max(float(r.abs().max()) for r in refs)
+    want = {"logits": ref.detach(), "fusion_weights": rinfo["fusion_weights"].detach()}
+    want.update({f"attn/{k}": v.detach() for k, v in rinfo["attention_maps"].items()})
+    want.update({f"dx/{m}": xs[m].grad for m in case.names})
+    want.update({n: params[n].grad for n, _ in model.named_parameters()})
+    alt = {}
+    if precision == "high":   # the reference algorithm under bf16x3 matmuls (see the fixture)
+        with bf16x3_matmul_mode():
+            p3 = {k: torch.from_numpy(v).requires_grad_(True) for k, v in sd.items()}
+            x3 = {m: torch.from_numpy(v).requires_grad_(True) for m, v in feats_np.items()}
+            r3, i3 = hybrid_forward(p3, case.names, x3, torch.from_numpy(mask_np), case.heads, p=P,
+                                    train=True, gen=mask_provider(SEED, OFFSET, P))
+            (r3 * torch.from_numpy(grad_np)).sum().backward()
+        alt = {"logits": r3.detach(), "fusion_weights": i3["fusion_weights"].detach()}
+        alt.update({f"attn/{k}": v.detach() for k, v in i3["attention_maps"].items()})
+        alt.update({f"dx/{m}": x3[m].grad for m in case.names})
+        alt.update({n: p3[n].grad for n, _ in model.named_parameters()})
+    got = {"logits": logits.detach(), "fusion_weights": info["fusion_weights"]}
+    got.update({f"attn/{k}": v for k, v in info["attention_maps"].items()})
+    got.update({f"dx/{m}": feats[m].grad for m in case.names})
+    got.update({n: p.grad for n, p in model.named_parameters()})
+    scale = max(float(want[k].abs().max()) for k in want if k.startswith("dx/") or "." in k)
 
     def atol(name, ref):
         # key_proj.bias: mathematically zero (softmax shift invariance), see the fixture docstring
         small = float(ref.abs().max()) <= 1e-3 * scale
         return 1e-3 * scale if precision == "high" and name.endswith("key_proj.bias") and small else ATOL
 
-    for m in case.names:
-        assert close(feats[m].grad.cpu(), xs[m].grad, RTOL, ATOL), m
-    for name, p in model.named_parameters():
+    for name, g in got.items():
         if not case.seq_mode and (".query_proj." in name or ".key_proj." in name):
-            assert torch.all(p.grad == 0), name   # softmax over one key: exact zeros
+            assert torch.all(g == 0), name   # softmax over one key: exact zeros
             continue
-        assert close(p.grad.cpu(), params[name].grad, RTOL, atol(name, params[name].grad)), name
+        tol = atol(name, want[name])
+        assert close(g.cpu(), want[name], RTOL, tol) or (name in alt and close(g.cpu(), alt[name], RTOL, tol)), name
 
 
 def test_cma_train_mode_matches_oracle(mods):
