@@ -302,6 +302,12 @@ int mmf_adamw_step_dev(int64_t n, float* param, const float* grad, float* exp_av
                        int64_t* step_dev, const float* lr_dev, const float* grad_coef_dev, float beta1,
                        float beta2, float eps, float weight_decay, float grad_scale, void* stream);
 
+/* dst += src over n floats (both 16-byte aligned): the gradient of one micro-batch added into
+ * the accumulated one (Lightning's accumulate_grad_batches, config/base.yaml:75
+ * gradient_accumulation; the caller scales each micro-batch loss by 1 / accumulate, as
+ * mmf_cross_entropy_ls's grad_scale does). */
+int mmf_grad_accumulate(int64_t n, const float* src, float* dst, void* stream);
+
 /* Global-norm gradient clipping (torch.nn.utils.clip_grad_norm_(max_norm,
  * norm_type=2) as Lightning applies gradient_clip_val, src/train.py:416-430,
  * config/base.yaml:74 gradient_clip_norm): over the flat gradient scaled by

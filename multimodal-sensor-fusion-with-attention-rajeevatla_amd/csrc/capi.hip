@@ -533,6 +533,15 @@ int mmf_clip_adamw_step_dev(int64_t n, float* param, const float* grad, float* e
   return MMF_OK;
 }
 
+int mmf_grad_accumulate(int64_t n, const float* src, float* dst, void* stream) {
+  if (n < 0 || (n > 0 && (!src || !dst))) return fail(MMF_EINVAL, "bad gradient-accumulate arguments");
+  if ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15)
+    return fail(MMF_EINVAL, "gradient accumulate: buffers must be 16-byte aligned");
+  hipStream_t st = (hipStream_t)stream;
+  STAGE_TRY("optim.grad_accum", launch_grad_accum(n, src, dst, st));
+  return MMF_OK;
+}
+
 int mmf_adamw_step_dev(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                        int64_t* step_dev, const float* lr_dev, const float* grad_coef_dev, float beta1,
                        float beta2, float eps, float weight_decay, float grad_scale, void* stream) {

@@ -485,6 +485,29 @@ static int64_t adamw_blocks(int64_t n, int vec) {
   return blocks;
 }
 
+// dst += src over a flat fp32 buffer (gradient accumulation over micro-batches, Lightning's
+// accumulate_grad_batches, config/base.yaml:75): float4 body, scalar tail
+__global__ __launch_bounds__(256) void grad_accum_kernel(int64_t n, const float* __restrict__ src,
+                                                          float* __restrict__ dst) {
+  const int64_t n4 = n >> 2;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const float4 a = reinterpret_cast<const float4*>(src)[i];
+    float4 b = reinterpret_cast<float4*>(dst)[i];
+    b.x += a.x; b.y += a.y; b.z += a.z; b.w += a.w;
+    reinterpret_cast<float4*>(dst)[i] = b;
+  }
+  for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    dst[i] += src[i];
+}
+
+hipError_t launch_grad_accum(int64_t n, const float* src, float* dst, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>((n / 4 + 255) / 256 + 1, 4 * (int64_t)device_cu_count());
+  ProfLaunch prof_(st, "grad_accum_kernel", (double)n, 12.0 * (double)n);
+  mmf_launch(grad_accum_kernel, dim3((unsigned)blocks), dim3(256), 0, st, n, src, dst);
+  return hipGetLastError();
+}
+
 hipError_t launch_adamw(int64_t n, float* p, const float* g, float* m, float* v, int64_t* step,
                         float lr, float b1, float b2, float eps, float wd, float gscale,
                         hipStream_t st, const float* lr_dev, const float* coef_dev) {

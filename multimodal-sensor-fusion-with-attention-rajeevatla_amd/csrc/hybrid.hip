@@ -456,6 +456,63 @@ SkPair make_sk(const mmf_hybrid_desc* d, const Saved& s, const float* mask, int 
   return a;
 }
 
+// Launch-lean single-key step (l1.hip): every modality 2-D (L = 1, the reference's own
+// semantics), every ordered pair present, fp32 ("highest"), H, D_m <= 128 (% 4),
+// C <= 16, float4-able inputs and weights.  It writes the single-key pooled plan's Saved / Ws
+// slots (Ob = O = P' V, Ab = A, dOb = dV, dU = dP_k|g), so both plans size the buffers alike; the
+// choice depends only on the descriptor and the pointers forward and backward both receive.
+// MMF_NO_L1_LEAN=1: the general single-key plan (A/B).
+bool lean_l1(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, const float* const* x) {
+  const bool off = getenv("MMF_NO_L1_LEAN") != nullptr;
+  const int M = d->num_modalities, H = d->hidden;
+  if (off || d->matmul_precision != MMF_PRECISION_HIGHEST || !W || !x) return false;
+  if (M < 2 || M > L1_MAXM || d->num_pairs != M * (M - 1)) return false;
+  if (H % 4 != 0 || H > L1_MAXH || d->num_heads > 8 || d->num_classes > L1_MAXC) return false;
+  unsigned seen = 0;
+  for (int g = 0; g < d->num_pairs; ++g) seen |= 1u << (d->pair_q[g] * L1_MAXM + d->pair_k[g]);
+  if (__builtin_popcount(seen) != d->num_pairs) return false;
+  for (int m = 0; m < M; ++m) {
+    if (Lm(d, m) != 1 || d->in_dim[m] % 4 != 0 || d->in_dim[m] > L1_MAXD) return false;
+    if (!aligned16(x[m]) || !aligned16(W->proj[m].w)) return false;
+  }
+  for (int g = 0; g < d->num_pairs; ++g)
+    if (!aligned16(W->v[g].w) || !aligned16(W->o[g].w)) return false;
+  return aligned16(W->cls1.w);
+}
+
+void fill_l1(L1Args& a, const mmf_hybrid_desc* d, const mmf_hybrid_params* W, const float* const* x,
+             const float* mask, const Saved& s) {
+  memset(&a, 0, sizeof(a));
+  const int M = d->num_modalities;
+  a.B = d->batch; a.M = M; a.H = d->hidden; a.C = d->num_classes; a.heads = d->num_heads;
+  a.npairs = d->num_pairs;
+  a.p = dropping(d) ? d->dropout : 0.f;
+  a.gscale = dropping(d) ? 1.f / (1.f - d->dropout) : 1.f;
+  a.mask = mask;
+  int cnt[L1_MAXM];
+  for (int m = 0; m < M; ++m) {
+    a.D[m] = d->in_dim[m];
+    a.x[m] = x[m];
+    a.Wp[m] = W->proj[m].w; a.bp[m] = W->proj[m].b;
+    a.gw[m] = W->gate[m].w; a.gb[m] = W->gate[m].b;
+    a.Xd[m] = s.Xd[m]; a.P[m] = s.P[m];
+    a.kdesig[m] = -1;
+    cnt[m] = 1;
+  }
+  for (int g = 0; g < d->num_pairs; ++g) {
+    const int q = d->pair_q[g], k = d->pair_k[g];
+    a.pq[g] = q; a.pk[g] = k;
+    if (a.kdesig[k] < 0) a.kdesig[k] = g;
+    a.Wv[g] = W->v[g].w; a.bv[g] = W->v[g].b; a.Wo[g] = W->o[g].w; a.bo[g] = W->o[g].b;
+    a.O[g] = s.Ob[g]; a.A[g] = s.Ab[g];
+    cnt[q]++;
+  }
+  for (int m = 0; m < M; ++m) a.inv_cnt[m] = 1.0f / (float)cnt[m];
+  a.W1 = W->cls1.w; a.b1 = W->cls1.b; a.W2 = W->cls2.w; a.b2 = W->cls2.b;
+  a.pooled = s.pooled; a.scores = s.scores; a.weights = s.weights; a.fused = s.fused; a.h1 = s.h1;
+  a.snap = s.rng;
+}
+
 }  // namespace
 
 extern "C" {
@@ -504,6 +561,19 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
   // the live state) and the live offset advanced by the projection GEMM's first launch:
   // no launch of its own
   const RngSnap* rng = rng_state ? s.rng : nullptr;
+
+  if (lean_l1(d, W, x)) {
+    L1Args a;
+    fill_l1(a, d, W, x, mask, s);
+    a.rng_live = rng_state;
+    a.rng_advance = const_cast<uint64_t*>(rng_state);
+    a.logits = logits;
+    a.weights_out = fusion_weights;
+    if (d->return_attention && attn_maps)
+      for (int g = 0; g < d->num_pairs; ++g) a.maps[g] = attn_maps[g];
+    STAGE_TRY("fwd.l1", launch_l1_forward(a, st));
+    return MMF_OK;
+  }
 
   // pairs with several keys run the attention kernels; single-key pairs single_key.hip
   std::vector<AttnPair> pairs;
@@ -752,6 +822,51 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
   Bump bw(workspace);
   Ws w;
   layout_ws(d, bw, w);
+  if (lean_l1(d, W, x)) {
+    L1Args a;
+    fill_l1(a, d, W, x, mask, s);
+    a.dlogits = dlogits;
+    a.dz1 = w.dz1; a.cvec = w.cvec; a.dscore = w.dscore;
+    for (int g = 0; g < d->num_pairs; ++g) {
+      a.dV[g] = w.dOb[g];
+      a.dPk[g] = w.dU[g];
+    }
+    for (int m = 0; m < M; ++m) {
+      a.dZ[m] = w.dZ[m];
+      a.dx[m] = dx ? dx[m] : nullptr;
+    }
+    // every weight gradient: dW = G^T X over the batch (l1_wgrad_kernel)
+    L1WgArgs wa;
+    memset(&wa, 0, sizeof(wa));
+    wa.B = B;
+    auto job = [&](const float* Gp, int ldg, const float* Xp, int ldx, int N, int K, float* dW, float* db) {
+      if (!dW && !db) return;
+      L1WgJob& j = wa.j[wa.njobs++];
+      j.G = Gp; j.ldg = ldg; j.X = Xp; j.ldx = ldx; j.N = N; j.K = K; j.dW = dW; j.db = db;
+      j.tiles_k = (K + 31) / 32;
+      j.tile0 = wa.ntiles;
+      wa.ntiles += ((N + 31) / 32) * j.tiles_k;
+    };
+    auto zero = [&](float* p, int n) {
+      if (!p || n <= 0) return;
+      wa.z[wa.nz] = p; wa.zn[wa.nz] = n;
+      wa.zoff[wa.nz + 1] = wa.zoff[wa.nz] + (n + 4095) / 4096;
+      wa.nz++;
+    };
+    for (int m = 0; m < M; ++m)
+      job(w.dZ[m], H, s.Xd[m], d->in_dim[m], H, d->in_dim[m], G->proj[m].w, G->proj[m].b);
+    for (int g = 0; g < d->num_pairs; ++g) {
+      job(w.dOb[g], H, s.P[d->pair_k[g]], H, H, H, G->v[g].w, G->v[g].b);
+      job(w.cvec + (size_t)d->pair_q[g] * H, M * H, s.Ob[g], H, H, H, G->o[g].w, G->o[g].b);
+      // softmax over one key: no gradient reaches query_proj / key_proj (exact zeros)
+      zero(G->q[g].w, H * H); zero(G->q[g].b, H); zero(G->k[g].w, H * H); zero(G->k[g].b, H);
+    }
+    job(w.dz1, H, s.fused, H, H, H, G->cls1.w, G->cls1.b);
+    job(dlogits, C, s.h1, H, C, H, G->cls2.w, G->cls2.b);
+    for (int m = 0; m < M; ++m) job(w.dscore + m, M, s.pooled + (size_t)m * H, M * H, 1, H, G->gate[m].w, G->gate[m].b);
+    STAGE_TRY("bwd.l1", launch_l1_backward(a, wa, st));
+    return MMF_OK;
+  }
   WgradPlan wp;
   plan_wgrads(d, x, mask, dlogits, s, w, G, bw, wp);
   if (bw.off > workspace_bytes(d)) return fail(MMF_EINVAL, "internal: workspace overflow");

@@ -1,0 +1,845 @@
+// Launch-lean single-key HybridFusion step (every modality 2-D: L = 1).
+//
+// src/train.py:261-279 feeds HybridFusion the pooled encoder outputs (B, D_m), so every
+// CrossModalAttention of the reference attends over ONE key (src/attention.py:92-146): the
+// post-dropout probability of (b, head) is [mask_k != 0] keep / (1 - p), independent of Q and K
+// (single_key.hip), and the whole forward / backward is a chain of (B x 128) x (128 x 128)
+// products: 0.4 GFLOP per C2 step, 2.6 us of fp32 MFMA on the chip.  The general plan runs it as
+// ~17 launches of 5-30 us (the GEMM library's fixed cost, per-sample GEMV tails).  Here each
+// stage is ONE launch over 16-sample tiles (v_mfma_f32_16x16x4_f32, 16 rows = 16 samples),
+// every weight a wave needs loaded into registers at kernel start beside the activations (one
+// memory round trip per kernel), the intermediates of a tile kept in LDS between the chained
+// products of one launch:
+//   l1_pair_fwd   (tile, pair)     X'_k = Drop(X_k mask_k), P_k = Drop(ReLU(X'_k W_k^T + b_k))
+//                                  (recomputed by both pairs keyed by k: cheaper than a launch),
+//                                  V = P_k W_v^T + b_v, O = P' V, A = O W_o^T + b_o
+//                                  (src/fusion.py:364-404, src/attention.py:104-140)
+//   l1_head_fwd   (tile)           pooled, gating, adaptive weights, fused, classifier
+//                                  (src/fusion.py:406-427, :429-479)
+//   l1_head_bwd   (tile)           dz1, dfused = dz1 W1, dscore, cvec = dpooled mask / n
+//   l1_pair_bwd   (tile, pair)     dO = cvec_q W_o, dV = P' dO, dP_k|g = dV W_v
+//   l1_mod_bwd    (tile, m)        dZ_m = gate(cvec_m + sum_g dP_k|g), dX_m = (dZ_m W_m) mask keep
+//   l1_wgrad      (32 x 32 tiles)  every weight / bias gradient as G^T X over the batch
+//                                  (K = B split over 4 waves, summed in a fixed order: deterministic)
+//                                  + the exactly-zero query / key projection gradients
+// Dropout draws are the library's Philox streams (same sites and element indices as the
+// general plan: tests/_philox.py replays them for the oracle).
+#include <cstring>
+
+#include "mmf_device.h"
+
+namespace mmf {
+namespace {
+
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int NT = 256;          // 4 waves
+constexpr int S = 16;            // samples per tile (the 16 rows of a 16x16x4 MFMA)
+constexpr int KG = L1_MAXD / 16; // 16-deep k groups (K <= 128)
+constexpr int NTL = 2;           // 16-column tiles per wave (N <= 128: tiles wave, wave + 4)
+constexpr int LD = 128 + 4;      // LDS row stride (floats) of a 16 x 128 activation tile
+
+// v_mfma_f32_16x16x4_f32: lane l supplies A[i = l & 15][k = l >> 4], B[k = l >> 4][j = l & 15];
+// the 16x16 result: lane l, reg r holds row 4 (l >> 4) + r, column l & 15.  The contraction runs
+// in 16-deep groups with lane quarter kq feeding k = 16 g + 4 kq + s at step s (one float4 per
+// lane and group for row-contiguous operands; the same permutation on A and B).
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+struct WTile {
+  float4 w[NTL][KG];
+};
+
+
+// Weight loads are unconditional (clamped indices, out-of-range values zeroed after the load): a
+// guarded load becomes a branch, and the compiler's wait counts cannot see through the branches
+// (it then drains every load in flight at the first use of any of them).
+__device__ __forceinline__ float4 zero_if(bool z, float4 v) {
+  return z ? make_float4(0.f, 0.f, 0.f, 0.f) : v;
+}
+
+// y = x W^T with W (N x K) row-major (nn.Linear): B[k][j] = W[n0 + j][k]
+__device__ __forceinline__ void wload_nt(const float* __restrict__ W, int N, int K, int wave, int lane, WTile& t) {
+  const int r = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int u = 0; u < NTL; ++u) {
+    const int n = 16 * (wave + 4 * u) + r;
+#pragma unroll
+    for (int g = 0; g < KG; ++g) {
+      const int k = 16 * g + 4 * kq;
+      const float4 v = *reinterpret_cast<const float4*>(W + (int64_t)min(n, N - 1) * K + min(k, K - 4));
+      t.w[u][g] = zero_if(n >= N || k >= K, v);
+    }
+  }
+}
+
+// y = x W with W (K x N) row-major: B[k][j] = W[k][n0 + j] (four rows per lane and group)
+__device__ __forceinline__ void wload_nn(const float* __restrict__ W, int N, int K, int wave, int lane, WTile& t) {
+  const int r = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int u = 0; u < NTL; ++u) {
+    const int n = 16 * (wave + 4 * u) + r;
+#pragma unroll
+    for (int g = 0; g < KG; ++g) {
+      const int k = 16 * g + 4 * kq;
+      const float* p = W + (int64_t)min(k, K - 4) * N + min(n, N - 1);
+      t.w[u][g] = zero_if(n >= N || k >= K, make_float4(p[0], p[N], p[2 * N], p[3 * N]));
+    }
+  }
+}
+
+// acc[u] (this wave's 16-column tiles of a 16 x N product) = xs (16 x 128, LDS, row stride LD) * B:
+// every k group and both tiles unconditionally (no branches in the MFMA chain: columns past K
+// of xs are zero-padded, weights past K / N zero), so the chain is one straight sequence
+__device__ __forceinline__ void mma(const float* xs, const WTile& t, f32x4 (&acc)[NTL], int lane) {
+  const int r = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int u = 0; u < NTL; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int g = 0; g < KG; ++g) {
+    const float4 a = *reinterpret_cast<const float4*>(xs + r * LD + 16 * g + 4 * kq);
+#pragma unroll
+    for (int u = 0; u < NTL; ++u) {
+      acc[u] = mfma16(a.x, t.w[u][g].x, acc[u]);
+      acc[u] = mfma16(a.y, t.w[u][g].y, acc[u]);
+      acc[u] = mfma16(a.z, t.w[u][g].z, acc[u]);
+      acc[u] = mfma16(a.w, t.w[u][g].w, acc[u]);
+    }
+  }
+}
+
+// 8 keep decisions (bit e: element 8 blk + e kept) of one Philox block
+__device__ __forceinline__ uint32_t keep8(const RngSnap& rs, uint32_t site, uint64_t blk, uint32_t thr) {
+  const uint4 r = philox_block(rs, site, blk);
+  uint32_t bits = 0;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bits |= keep_from(r, e, thr) ? (1u << e) : 0u;
+  return bits;
+}
+
+// keep bits of a tile's rows b0 .. b0 + 15 of a (B, N) tensor of site `site` (element (b) N + j,
+// a contiguous range: one Philox block per 8 elements), byte c = block (b0 N) / 8 + c
+constexpr int KB_BYTES = S * 128 / 8 + 8;
+__device__ __forceinline__ void keep_tile(const RngSnap& rs, uint32_t site, int b0, int N, float p, uint8_t* kb) {
+  const uint32_t thr = p16(p);
+  const uint64_t lo = (uint64_t)b0 * N, hi = (uint64_t)(b0 + S) * N;
+  const int nblk = (int)(((hi + 7) >> 3) - (lo >> 3));
+  for (int e = threadIdx.x; e < nblk; e += NT) kb[e] = (uint8_t)keep8(rs, site, (lo >> 3) + e, thr);
+}
+
+__device__ __forceinline__ bool kept(const uint8_t* kb, int b0, int N, int i, int j) {
+  const uint32_t e = (uint32_t)(((uint64_t)(b0 + i) * N + j) - (((uint64_t)b0 * N) & ~7ull));
+  return (kb[e >> 3] >> (e & 7)) & 1;
+}
+
+// columns [n, 128) of a 16-row LDS tile := 0 (the zero-padded tail of a contraction)
+__device__ __forceinline__ void zero_pad(float* tile, int n) {
+  const int w = 128 - n;
+  for (int e = threadIdx.x; e < S * w; e += NT) tile[(e / w) * LD + n + e % w] = 0.f;
+}
+
+// P'[i][h] of pair g: [mask_k != 0] keep(b h) / (1 - p) (src/attention.py:118-130 at one key)
+__device__ __forceinline__ void pprime_tile(const L1Args& a, const RngSnap& rs, int g, int b0, float* pp) {
+  const int k = a.pk[g];
+  for (int e = threadIdx.x; e < S * a.heads; e += NT) {
+    const int i = e / a.heads, h = e - i * a.heads, b = b0 + i;
+    float v = 0.f;
+    if (b < a.B && a.mask[(int64_t)b * a.M + k] != 0.f) {
+      v = 1.f;
+      if (a.p > 0.f) v = keep1(rs, SITE_ATTN + g, (uint64_t)b * a.heads + h, a.p) ? a.gscale : 0.f;
+    }
+    pp[e] = v;
+  }
+}
+
+// 16 x N activation tile rows b0.. of a (B, ld) tensor into LDS (zeros past B); float4 loads from
+// clamped rows (unconditional: see wload_nt)
+__device__ __forceinline__ void load_tile(const float* __restrict__ src, int ld, int B, int b0, int N, float* dst) {
+  const int n4 = N / 4;
+  for (int e = threadIdx.x; e < S * n4; e += NT) {
+    const int i = e / n4, c = e - i * n4;
+    const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)min(b0 + i, B - 1) * ld + 4 * c);
+    *reinterpret_cast<float4*>(dst + i * LD + 4 * c) = b0 + i < B ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+// sum over the 16 lanes of a lane row (l & ~15 .. +15); every lane of the row gets it
+__device__ __forceinline__ float sum16(float v) {
+  v += dpp<DPP_ROR8>(v);
+  return sum8(v);
+}
+
+// out[i][c] = xs[i] . W[c] + bias[c] for i < 16, c < N (16 lanes per dot), rows < B written
+template <typename F>
+__device__ __forceinline__ void rowdots(const float* xs, const float* W, int ldw, int K, int nout, F&& emit) {
+  const int t = threadIdx.x, grp = t >> 4, l16 = t & 15;
+  for (int d = grp; d < S * nout; d += NT / 16) {
+    const int i = d / nout, c = d - i * nout;
+    float s = 0.f;
+    for (int k = l16; k < K; k += 16) s += xs[i * LD + k] * W[(int64_t)c * ldw + k];
+    s = sum16(s);
+    if (l16 == 0) emit(i, c, s);
+  }
+}
+
+// adaptive weights of one sample (src/fusion.py:462-478; head.hip adaptive_fwd arithmetic)
+__device__ float adaptive(int M, const float* score, const float* mask, float* sm, float* w) {
+  float mx = -INFINITY;
+  for (int m = 0; m < M; ++m)
+    if (mask[m] > 0.f) mx = fmaxf(mx, score[m]);
+  float z = 0.f;
+  for (int m = 0; m < M; ++m) {
+    sm[m] = (mask[m] > 0.f) ? __expf(score[m] - mx) : 0.f;
+    z += sm[m];
+  }
+  float sw = 0.f, ms = 0.f;
+  for (int m = 0; m < M; ++m) {
+    sm[m] = (mx == -INFINITY) ? 0.f : sm[m] / z;
+    w[m] = sm[m] * mask[m];
+    sw += w[m];
+    ms += mask[m];
+  }
+  if (sw > 0.f) {
+    const float den = sw + 1e-8f;
+    for (int m = 0; m < M; ++m) w[m] = w[m] / den;
+  } else {
+    for (int m = 0; m < M; ++m) w[m] = ms > 0.f ? mask[m] / (ms + 1e-8f) : 1.f / (float)M;
+  }
+  return sw;
+}
+
+// ------------------------------------------------------------------------------ forward
+__global__ __launch_bounds__(NT) void l1_pair_fwd_kernel(const L1Args a) {
+  __shared__ __attribute__((aligned(16))) float xs[S * LD];
+  __shared__ __attribute__((aligned(16))) float ps[S * LD];
+  __shared__ __attribute__((aligned(16))) float os[S * LD];
+  __shared__ uint8_t kin[KB_BYTES], kpr[KB_BYTES];
+  __shared__ float pp[S * 8];
+  __shared__ float msk[S];
+  const int g = blockIdx.y, b0 = blockIdx.x * S;
+  const int k = a.pk[g], D = a.D[k], H = a.H, B = a.B;
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const bool desig = a.kdesig[k] == g;
+  // every global operand first, those needed first issued first (the input rows, the mask and the
+  // rng state, then the three weights of this wave's columns: the waits before the keep draws and
+  // X' leave the weight loads in flight)
+  RngSnap rs{0, 0};
+  if (a.rng_live) rs = RngSnap{a.rng_live[0], a.rng_live[1]};
+  const int d4 = D / 4;
+  float4 xr[2];
+  int xi[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int e = t + u * NT;
+    const int i = e / d4;
+    xi[u] = (i < S && b0 + i < B) ? e : -1;
+    // unconditional loads from clamped rows (a guarded load becomes a branch whose wait the
+    // compiler places right behind it, ahead of the weight loads)
+    const int row = min(b0 + min(i, S - 1), B - 1);
+    xr[u] = *reinterpret_cast<const float4*>(a.x[k] + (int64_t)row * D + 4 * (e - i * d4));
+  }
+  const float mk = a.mask[(int64_t)min(b0 + (t & (S - 1)), B - 1) * a.M + k];
+  const int ih = t / a.heads;
+  const float mkh = a.mask[(int64_t)min(b0 + min(ih, S - 1), B - 1) * a.M + k];
+  __builtin_amdgcn_sched_barrier(0);   // (these loads issue before the weights')
+  WTile wk, wv, wo;
+  wload_nt(a.Wp[k], H, D, wave, lane, wk);
+  wload_nt(a.Wv[g], H, H, wave, lane, wv);
+  wload_nt(a.Wo[g], H, H, wave, lane, wo);
+  float bpk[NTL], bvv[NTL], bov[NTL];
+#pragma unroll
+  for (int u = 0; u < NTL; ++u) {
+    const int j = 16 * (wave + 4 * u) + (lane & 15), jc = min(j, H - 1);
+    const bool on = j < H;
+    bpk[u] = a.bp[k][jc];
+    bvv[u] = a.bv[g][jc];
+    bov[u] = a.bo[g][jc];
+    if (!on) bpk[u] = bvv[u] = bov[u] = 0.f;
+  }
+  if (t < S) msk[t] = b0 + t < B ? mk : 0.f;
+  if (a.p > 0.f) {
+    keep_tile(rs, SITE_IN + k, b0, D, a.p, kin);
+    keep_tile(rs, SITE_PROJ + k, b0, H, a.p, kpr);
+  }
+  // P'[i][h] = [mask_k != 0] keep(b h) / (1 - p) (src/attention.py:118-130 at one key)
+  if (t < S * a.heads) {
+    float v = 0.f;
+    if (b0 + ih < B && mkh != 0.f) {
+      v = 1.f;
+      if (a.p > 0.f) v = keep1(rs, SITE_ATTN + g, (uint64_t)(b0 + ih) * a.heads + (t - ih * a.heads), a.p) ? a.gscale : 0.f;
+    }
+    pp[t] = v;
+  }
+  if (a.snap && blockIdx.x == 0 && blockIdx.y == 0 && t == 0 && a.rng_live) *a.snap = rs;
+  __syncthreads();
+  // X' = X mask (input dropout), src/fusion.py:373
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int e = xi[u] >= 0 ? xi[u] : t + u * NT;
+    const int i = e / d4, c = 4 * (e - i * d4);
+    if (i >= S) continue;
+    if (xi[u] < 0) xr[u] = make_float4(0.f, 0.f, 0.f, 0.f);   // a row past B: zeros
+    float v[4] = {xr[u].x, xr[u].y, xr[u].z, xr[u].w};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      v[s] *= msk[i];
+      if (a.p > 0.f) v[s] = kept(kin, b0, D, i, c + s) ? v[s] * a.gscale : 0.f;
+    }
+    const float4 o = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(xs + i * LD + c) = o;
+    if (desig && b0 + i < B) *reinterpret_cast<float4*>(a.Xd[k] + (int64_t)(b0 + i) * D + c) = o;
+  }
+  zero_pad(xs, D);
+  if (a.maps[g])
+    for (int e = t; e < S * a.heads; e += NT)
+      if (b0 + e / a.heads < B) a.maps[g][(int64_t)b0 * a.heads + e] = pp[e];
+  __syncthreads();
+  const int kq = lane >> 4, jl = lane & 15;
+  f32x4 acc[NTL];
+  // P_k = Drop(ReLU(X' W_k^T + b_k))  (projections[k], src/fusion.py:291-298)
+  mma(xs, wk, acc, lane);
+#pragma unroll
+  for (int u = 0; u < NTL; ++u) {
+    const int j = 16 * (wave + 4 * u) + jl;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = 4 * kq + r;
+      float v = fmaxf(acc[u][r] + bpk[u], 0.f);
+      if (j >= H) v = 0.f;
+      else if (a.p > 0.f) v = kept(kpr, b0, H, i, j) ? v * a.gscale : 0.f;
+      ps[i * LD + j] = v;
+      if (desig && b0 + i < B && j < H) a.P[k][(int64_t)(b0 + i) * H + j] = v;
+    }
+  }
+  __syncthreads();
+  // V = P_k W_v^T + b_v;  O = P' V per head (one key: attn @ v, src/attention.py:132)
+  mma(ps, wv, acc, lane);
+  const int hd = H / a.heads;
+#pragma unroll
+  for (int u = 0; u < NTL; ++u) {
+    const int j = 16 * (wave + 4 * u) + jl;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = 4 * kq + r;
+      const float v = j < H ? (acc[u][r] + bvv[u]) * pp[i * a.heads + j / hd] : 0.f;
+      os[i * LD + j] = v;
+      if (b0 + i < B && j < H) a.O[g][(int64_t)(b0 + i) * H + j] = v;
+    }
+  }
+  __syncthreads();
+  // A = O W_o^T + b_o  (out_proj, src/attention.py:140)
+  mma(os, wo, acc, lane);
+#pragma unroll
+  for (int u = 0; u < NTL; ++u) {
+    const int j = 16 * (wave + 4 * u) + jl;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = 4 * kq + r;
+      if (b0 + i < B && j < H) a.A[g][(int64_t)(b0 + i) * H + j] = acc[u][r] + bov[u];
+    }
+  }
+}
+
+// the small head operands (gating rows, classifier output rows, biases) staged in LDS at kernel
+// start beside the activation loads: no global load inside a dot-product loop
+struct HeadSmall {
+  float gw[L1_MAXM * L1_MAXH];
+  float w2[L1_MAXC * L1_MAXH];
+  float gb[L1_MAXM], b2[L1_MAXC];
+};
+__device__ __forceinline__ void stage_small(const L1Args& a, HeadSmall& hs) {
+  const int t = threadIdx.x, M = a.M, H = a.H, C = a.C;
+  for (int e = t; e < M * H; e += NT) hs.gw[e] = a.gw[e / H][e % H];
+  for (int e = t; e < C * H; e += NT) hs.w2[e] = a.W2[e];
+  if (t < M) hs.gb[t] = a.gb[t][0];
+  if (t >= 64 && t < 64 + C) hs.b2[t - 64] = a.b2[t - 64];
+}
+
+__global__ __launch_bounds__(NT) void l1_head_fwd_kernel(const L1Args a) {
+  __shared__ __attribute__((aligned(16))) float pl[L1_MAXM * S * LD];
+  __shared__ __attribute__((aligned(16))) float fs[S * LD];
+  __shared__ __attribute__((aligned(16))) float hs[S * LD];
+  __shared__ HeadSmall sm_;
+  __shared__ uint8_t kcl[KB_BYTES];
+  __shared__ float msk[S * L1_MAXM], sc[S * L1_MAXM], wt[S * L1_MAXM];
+  const int b0 = blockIdx.x * S;
+  const int M = a.M, H = a.H, B = a.B, C = a.C;
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  // loads, first-needed first: the mask rows and the rng snapshot, the attended and projected
+  // rows, the small operands, then W1
+  for (int e = t; e < S * M; e += NT) msk[e] = b0 + e / M < B ? a.mask[(int64_t)b0 * M + e] : 0.f;
+  RngSnap rs{0, 0};
+  if (a.p > 0.f) rs = *a.snap;
+  stage_small(a, sm_);
+  // pooled_m = mean(P_m, A_g for every pair with query m) * mask_m (src/fusion.py:406-408): each
+  // thread sums its float4 of every list entry in registers
+  const int h4 = H / 4;
+  float4 pv[2][L1_MAXM];
+  int pe[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int e = t + u * NT, i = e / h4;
+    pe[u] = (i < S) ? e : -1;
+    const int64_t row = (int64_t)min(b0 + min(i, S - 1), B - 1) * H + 4 * (e - i * h4);
+#pragma unroll
+    for (int m = 0; m < L1_MAXM; ++m)
+      pv[u][m] = m < M ? *reinterpret_cast<const float4*>(a.P[m] + row) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int g = 0; g < a.npairs; ++g) {
+      const float4 x = *reinterpret_cast<const float4*>(a.A[g] + row);
+      const int q = a.pq[g];
+#pragma unroll
+      for (int m = 0; m < L1_MAXM; ++m)
+        if (m == q) { pv[u][m].x += x.x; pv[u][m].y += x.y; pv[u][m].z += x.z; pv[u][m].w += x.w; }
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  WTile w1;
+  wload_nt(a.W1, H, H, wave, lane, w1);
+  float b1v[NTL];
+#pragma unroll
+  for (int u = 0; u < NTL; ++u) {
+    const int j = 16 * (wave + 4 * u) + (lane & 15);
+    b1v[u] = j < H ? a.b1[min(j, H - 1)] : 0.f;
+  }
+  if (a.p > 0.f) keep_tile(rs, SITE_CLS, b0, H, a.p, kcl);
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int e = pe[u];
+    if (e < 0) continue;
+    const int i = e / h4, c = 4 * (e - i * h4);
+    const bool in = b0 + i < B;
+#pragma unroll
+    for (int m = 0; m < L1_MAXM; ++m) {
+      if (m >= M) break;
+      const float f = in ? a.inv_cnt[m] * msk[i * M + m] : 0.f;
+      const float4 o = make_float4(pv[u][m].x * f, pv[u][m].y * f, pv[u][m].z * f, pv[u][m].w * f);
+      *reinterpret_cast<float4*>(pl + (m * S + i) * LD + c) = o;
+      if (in) *reinterpret_cast<float4*>(a.pooled + ((int64_t)(b0 + i) * M + m) * H + c) = o;
+    }
+  }
+  __syncthreads();
+  // gating scores (nn.Linear(H, 1), src/fusion.py:452-461): 16 lanes per dot
+  {
+    const int grp = t >> 4, l16 = t & 15;
+    for (int d = grp; d < S * M; d += NT / 16) {
+      const int i = d / M, m = d - i * M;
+      float s = 0.f;
+      for (int j = l16; j < H; j += 16) s += pl[(m * S + i) * LD + j] * sm_.gw[m * H + j];
+      s = sum16(s);
+      if (l16 == 0) sc[i * M + m] = s + sm_.gb[m];
+    }
+  }
+  __syncthreads();
+  if (t < S) {
+    float smx[L1_MAXM], w[L1_MAXM];
+    adaptive(M, sc + t * M, msk + t * M, smx, w);
+    for (int m = 0; m < M; ++m) {
+      wt[t * M + m] = w[m];
+      if (b0 + t < B) {
+        a.scores[(int64_t)(b0 + t) * M + m] = sc[t * M + m];
+        a.weights[(int64_t)(b0 + t) * M + m] = w[m];
+        if (a.weights_out) a.weights_out[(int64_t)(b0 + t) * M + m] = w[m];
+      }
+    }
+  }
+  __syncthreads();
+  // fused = sum_m w_m pooled_m (src/fusion.py:413-418), float4 per thread
+  for (int e = t; e < S * h4; e += NT) {
+    const int i = e / h4, c = 4 * (e - i * h4);
+    float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int m = 0; m < M; ++m) {
+      const float4 v = *reinterpret_cast<const float4*>(pl + (m * S + i) * LD + c);
+      const float wm = wt[i * M + m];
+      f.x += v.x * wm; f.y += v.y * wm; f.z += v.z * wm; f.w += v.w * wm;
+    }
+    *reinterpret_cast<float4*>(fs + i * LD + c) = f;
+    if (b0 + i < B) *reinterpret_cast<float4*>(a.fused + (int64_t)(b0 + i) * H + c) = f;
+  }
+  zero_pad(fs, H);
+  __syncthreads();
+  // h1 = Drop(ReLU(fused W1^T + b1)) (classifier[0..2], src/fusion.py:323-328)
+  f32x4 acc[NTL];
+  mma(fs, w1, acc, lane);
+  const int kq = lane >> 4, jl = lane & 15;
+#pragma unroll
+  for (int u = 0; u < NTL; ++u) {
+    const int j = 16 * (wave + 4 * u) + jl;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = 4 * kq + r;
+      float v = fmaxf(acc[u][r] + b1v[u], 0.f);
+      if (j >= H) v = 0.f;
+      else if (a.p > 0.f) v = kept(kcl, b0, H, i, j) ? v * a.gscale : 0.f;
+      hs[i * LD + j] = v;
+      if (b0 + i < B && j < H) a.h1[(int64_t)(b0 + i) * H + j] = v;
+    }
+  }
+  __syncthreads();
+  // logits = h1 W2^T + b2 (classifier[3])
+  {
+    const int grp = t >> 4, l16 = t & 15;
+    for (int d = grp; d < S * C; d += NT / 16) {
+      const int i = d / C, c = d - i * C;
+      float s = 0.f;
+      for (int j = l16; j < H; j += 16) s += hs[i * LD + j] * sm_.w2[c * H + j];
+      s = sum16(s);
+      if (l16 == 0 && b0 + i < B) a.logits[(int64_t)(b0 + i) * C + c] = s + sm_.b2[c];
+    }
+  }
+  // the live stream advances once per call (the pair kernel read it; the snapshot is saved)
+  if (a.rng_advance && blockIdx.x == 0 && t == 0) a.rng_advance[1] += 1;
+}
+
+// ------------------------------------------------------------------------------ backward
+__global__ __launch_bounds__(NT) void l1_head_bwd_kernel(const L1Args a) {
+  __shared__ __attribute__((aligned(16))) float pl[L1_MAXM * S * LD];
+  __shared__ __attribute__((aligned(16))) float zs[S * LD];
+  __shared__ __attribute__((aligned(16))) float dfs[S * LD];
+  __shared__ HeadSmall sm_;
+  __shared__ float dl[S * L1_MAXC];
+  __shared__ float msk[S * L1_MAXM], sc[S * L1_MAXM], wt[S * L1_MAXM], dw[S * L1_MAXM], dsc[S * L1_MAXM];
+  const int b0 = blockIdx.x * S;
+  const int M = a.M, H = a.H, B = a.B, C = a.C;
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  for (int e = t; e < S * C; e += NT) dl[e] = b0 + e / C < B ? a.dlogits[(int64_t)b0 * C + e] : 0.f;
+  for (int e = t; e < S * M; e += NT) {
+    const bool in = b0 + e / M < B;
+    msk[e] = in ? a.mask[(int64_t)b0 * M + e] : 0.f;
+    sc[e] = in ? a.scores[(int64_t)b0 * M + e] : 0.f;
+    wt[e] = in ? a.weights[(int64_t)b0 * M + e] : 0.f;
+  }
+  stage_small(a, sm_);
+  // this thread's h1 float4s (the ReLU / dropout gate of dz1)
+  const int h4 = H / 4;
+  float4 hv[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int e = t + u * NT, i = e / h4;
+    hv[u] = *reinterpret_cast<const float4*>(a.h1 + (int64_t)min(b0 + min(i, S - 1), B - 1) * H + 4 * (e - i * h4));
+  }
+  for (int e = t; e < M * S * h4; e += NT) {
+    const int mi = e / h4, c = 4 * (e - mi * h4), m = mi / S, i = mi - m * S;
+    const float4 v = *reinterpret_cast<const float4*>(a.pooled + ((int64_t)min(b0 + i, B - 1) * M + m) * H + c);
+    *reinterpret_cast<float4*>(pl + mi * LD + c) = b0 + i < B ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  WTile w1;
+  wload_nn(a.W1, H, H, wave, lane, w1);
+  __syncthreads();
+  // dz1 = ReLU' Drop' (dlogits W2): the saved h1 is post-dropout, so h1 > 0 marks kept, active units
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int e = t + u * NT, i = e / h4, c = 4 * (e - i * h4);
+    if (i >= S) continue;
+    float z[4];
+    const float hvv[4] = {hv[u].x, hv[u].y, hv[u].z, hv[u].w};
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      float acc = 0.f;
+      for (int cc = 0; cc < C; ++cc) acc += dl[i * C + cc] * sm_.w2[cc * H + c + s4];
+      z[s4] = (b0 + i < B && hvv[s4] > 0.f) ? acc * a.gscale : 0.f;
+    }
+    const float4 zv = make_float4(z[0], z[1], z[2], z[3]);
+    *reinterpret_cast<float4*>(zs + i * LD + c) = zv;
+    if (b0 + i < B) *reinterpret_cast<float4*>(a.dz1 + (int64_t)(b0 + i) * H + c) = zv;
+  }
+  zero_pad(zs, H);
+  __syncthreads();
+  // dfused = dz1 W1
+  f32x4 acc[NTL];
+  mma(zs, w1, acc, lane);
+  const int kq = lane >> 4, jl = lane & 15;
+#pragma unroll
+  for (int u = 0; u < NTL; ++u) {
+    const int j = 16 * (wave + 4 * u) + jl;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dfs[(4 * kq + r) * LD + j] = acc[u][r];
+  }
+  __syncthreads();
+  // d weights_m = dfused . pooled_m
+  {
+    const int grp = t >> 4, l16 = t & 15;
+    for (int d = grp; d < S * M; d += NT / 16) {
+      const int i = d / M, m = d - i * M;
+      float s = 0.f;
+      for (int j = l16; j < H; j += 16) s += dfs[i * LD + j] * pl[(m * S + i) * LD + j];
+      s = sum16(s);
+      if (l16 == 0) dw[i * M + m] = s;
+    }
+  }
+  __syncthreads();
+  // compute_adaptive_weights backward (renormalisation and the masked softmax)
+  if (t < S) {
+    const int i = t;
+    float smx[L1_MAXM], w[L1_MAXM], ds[L1_MAXM];
+    const float sw = adaptive(M, sc + i * M, msk + i * M, smx, w);
+    for (int m = 0; m < M; ++m) ds[m] = 0.f;
+    if (sw > 0.f) {
+      const float Sd = sw + 1e-8f;
+      float dot = 0.f;
+      for (int m = 0; m < M; ++m) dot += dw[i * M + m] * smx[m] * msk[i * M + m];
+      float dsm[L1_MAXM], sdot = 0.f;
+      for (int m = 0; m < M; ++m) {
+        dsm[m] = (dw[i * M + m] / Sd - dot / (Sd * Sd)) * msk[i * M + m];
+        sdot += smx[m] * dsm[m];
+      }
+      for (int m = 0; m < M; ++m) ds[m] = msk[i * M + m] > 0.f ? smx[m] * (dsm[m] - sdot) : 0.f;
+    }
+    for (int m = 0; m < M; ++m) {
+      dsc[i * M + m] = ds[m];
+      if (b0 + i < B) a.dscore[(int64_t)(b0 + i) * M + m] = ds[m];
+    }
+  }
+  __syncthreads();
+  // cvec_m = (w_m dfused + dscore_m gate_w_m) mask_m / n_m: the gradient of every entry of m's
+  // aggregation list (P_m and the attended features of the pairs whose query is m), float4 per thread
+  for (int e = t; e < M * S * h4; e += NT) {
+    const int mi = e / h4, c = 4 * (e - mi * h4), m = mi / S, i = mi - m * S;
+    if (b0 + i >= B) continue;
+    const float f = msk[i * M + m] * a.inv_cnt[m], wm = wt[i * M + m], dsm = dsc[i * M + m];
+    const float4 dv = *reinterpret_cast<const float4*>(dfs + i * LD + c);
+    const float4 gv = *reinterpret_cast<const float4*>(sm_.gw + m * H + c);
+    const float4 v = make_float4((wm * dv.x + dsm * gv.x) * f, (wm * dv.y + dsm * gv.y) * f,
+                                 (wm * dv.z + dsm * gv.z) * f, (wm * dv.w + dsm * gv.w) * f);
+    *reinterpret_cast<float4*>(a.cvec + ((int64_t)(b0 + i) * M + m) * H + c) = v;
+  }
+}
+
+__global__ __launch_bounds__(NT) void l1_pair_bwd_kernel(const L1Args a) {
+  __shared__ __attribute__((aligned(16))) float cs[S * LD];
+  __shared__ __attribute__((aligned(16))) float vs[S * LD];
+  __shared__ float pp[S * 8];
+  const int g = blockIdx.y, b0 = blockIdx.x * S;
+  const int q = a.pq[g], H = a.H, B = a.B, M = a.M;
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  RngSnap rs{0, 0};
+  if (a.p > 0.f) rs = *a.snap;
+  load_tile(a.cvec + (int64_t)q * H, M * H, B, b0, H, cs);
+  zero_pad(cs, H);
+  pprime_tile(a, rs, g, b0, pp);
+  __builtin_amdgcn_sched_barrier(0);
+  WTile wo, wv;
+  wload_nn(a.Wo[g], H, H, wave, lane, wo);
+  wload_nn(a.Wv[g], H, H, wave, lane, wv);
+  __syncthreads();
+  const int kq = lane >> 4, jl = lane & 15, hd = H / a.heads;
+  f32x4 acc[NTL];
+  // dO = dA W_o (dA = cvec_q), dV = P' dO per head
+  mma(cs, wo, acc, lane);
+#pragma unroll
+  for (int u = 0; u < NTL; ++u) {
+    const int j = 16 * (wave + 4 * u) + jl;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = 4 * kq + r;
+      const float v = j < H ? acc[u][r] * pp[i * a.heads + j / hd] : 0.f;
+      vs[i * LD + j] = v;
+      if (b0 + i < B && j < H) a.dV[g][(int64_t)(b0 + i) * H + j] = v;
+    }
+  }
+  __syncthreads();
+  // the pair's share of dP_k: dV W_v
+  mma(vs, wv, acc, lane);
+#pragma unroll
+  for (int u = 0; u < NTL; ++u) {
+    const int j = 16 * (wave + 4 * u) + jl;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = 4 * kq + r;
+      if (b0 + i < B && j < H) a.dPk[g][(int64_t)(b0 + i) * H + j] = acc[u][r];
+    }
+  }
+}
+
+__global__ __launch_bounds__(NT) void l1_mod_bwd_kernel(const L1Args a) {
+  __shared__ __attribute__((aligned(16))) float zs[S * LD];
+  __shared__ uint8_t kin[KB_BYTES];
+  __shared__ float msk[S];
+  const int m = blockIdx.y, b0 = blockIdx.x * S;
+  const int H = a.H, B = a.B, M = a.M, D = a.D[m];
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const bool want_dx = a.dx[m] != nullptr;
+  if (t < S) msk[t] = b0 + t < B ? a.mask[(int64_t)(b0 + t) * M + m] : 0.f;
+  RngSnap rs{0, 0};
+  if (a.p > 0.f && want_dx) {
+    rs = *a.snap;
+    keep_tile(rs, SITE_IN + m, b0, D, a.p, kin);
+  }
+  // dZ_m = ReLU' Drop' (cvec_m + sum over the pairs keyed by m of dP_k|g): P_m is post-dropout,
+  // so P_m > 0 marks kept, active units
+  const int h4 = H / 4;
+  for (int e = t; e < S * h4; e += NT) {
+    const int i = e / h4, c = 4 * (e - i * h4);
+    const int bi = min(b0 + i, B - 1);
+    const int64_t row = (int64_t)bi * H + c;
+    float4 s = *reinterpret_cast<const float4*>(a.cvec + ((int64_t)bi * M + m) * H + c);
+    for (int g = 0; g < a.npairs; ++g) {
+      if (a.pk[g] != m) continue;
+      const float4 v = *reinterpret_cast<const float4*>(a.dPk[g] + row);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    const float4 p = *reinterpret_cast<const float4*>(a.P[m] + row);
+    float4 z = make_float4(p.x > 0.f ? s.x * a.gscale : 0.f, p.y > 0.f ? s.y * a.gscale : 0.f,
+                           p.z > 0.f ? s.z * a.gscale : 0.f, p.w > 0.f ? s.w * a.gscale : 0.f);
+    if (b0 + i < B) *reinterpret_cast<float4*>(a.dZ[m] + row) = z;
+    else z = make_float4(0.f, 0.f, 0.f, 0.f);
+    *reinterpret_cast<float4*>(zs + i * LD + c) = z;
+  }
+  if (!want_dx) return;
+  WTile wp;
+  wload_nn(a.Wp[m], D, H, wave, lane, wp);
+  zero_pad(zs, H);
+  __syncthreads();
+  // dX_m = (dZ_m W_m) mask_m input-dropout'
+  f32x4 acc[NTL];
+  mma(zs, wp, acc, lane);
+  const int kq = lane >> 4, jl = lane & 15;
+#pragma unroll
+  for (int u = 0; u < NTL; ++u) {
+    const int j = 16 * (wave + 4 * u) + jl;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = 4 * kq + r;
+      if (b0 + i >= B || j >= D) continue;
+      float v = acc[u][r] * msk[i];
+      if (a.p > 0.f) v = kept(kin, b0, D, i, j) ? v * a.gscale : 0.f;
+      a.dx[m][(int64_t)(b0 + i) * D + j] = v;
+    }
+  }
+}
+
+// One 32 x 32 tile of dW = G^T X (rows of G: the batch) per workgroup; wave w takes batch rows
+// [w R, (w + 1) R) of each 4R-row chunk, the four partial tiles summed in order through LDS.
+// Workgroups past the tiles zero-fill 4096-float chunks of the zero list.
+constexpr int WG_ROWS = 64;   // batch rows per wave per chunk (32 MFMA steps)
+__global__ __launch_bounds__(NT) void l1_wgrad_kernel(const L1WgArgs w) {
+  __shared__ float red[4][16][64];
+  __shared__ float bred[4][32];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  int tile = blockIdx.x;
+  if (tile >= w.ntiles) {
+    const int zb = tile - w.ntiles;
+    int i = 0;
+    while (i < w.nz && w.zoff[i + 1] <= zb) ++i;
+    if (i >= w.nz) return;
+    const int64_t lo = (int64_t)(zb - w.zoff[i]) * 4096, hi = min((int64_t)w.zn[i], lo + 4096);
+    for (int64_t e = lo + t; e < hi; e += NT) w.z[i][e] = 0.f;
+    return;
+  }
+  int ji = 0;
+  while (ji + 1 < w.njobs && w.j[ji + 1].tile0 <= tile) ++ji;
+  const L1WgJob J = w.j[ji];
+  const int lt = tile - J.tile0, n0 = 32 * (lt / J.tiles_k), k0 = 32 * (lt % J.tiles_k);
+  const int col = lane & 31, hf = lane >> 5;
+  const int n = n0 + col, kk = k0 + col;
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  float bsum = 0.f;
+  for (int c0 = 0; c0 < w.B; c0 += 4 * WG_ROWS) {
+    const int rb = c0 + wave * WG_ROWS + hf;
+    float ga[WG_ROWS / 2], xb[WG_ROWS / 2];
+#pragma unroll
+    for (int s = 0; s < WG_ROWS / 2; ++s) {
+      const int b = rb + 2 * s, bc = min(b, w.B - 1);
+      const bool in = b < w.B;
+      const float gv = J.G[(int64_t)bc * J.ldg + min(n, J.N - 1)];
+      const float xv = J.X[(int64_t)bc * J.ldx + min(kk, J.K - 1)];
+      ga[s] = (in && n < J.N) ? gv : 0.f;
+      xb[s] = (in && kk < J.K) ? xv : 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < WG_ROWS / 2; ++s) {
+      acc = mfma32(ga[s], xb[s], acc);
+      bsum += ga[s];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) red[wave][r][lane] = acc[r];
+  const bool do_db = J.db && k0 == 0;
+  if (do_db) {
+    const float v = sum_xor32(bsum);   // both lane halves: column n's sum over this wave's rows
+    if (hf == 0) bred[wave][col] = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int v = t + u * NT;          // (reg r, lane l) of the 32 x 32 tile
+    const int r = v >> 6, l = v & 63;
+    const float s = ((red[0][r][l] + red[1][r][l]) + red[2][r][l]) + red[3][r][l];
+    const int i = n0 + acc_row(r, l >> 5), j = k0 + (l & 31);
+    if (i < J.N && j < J.K) J.dW[(int64_t)i * J.K + j] = s;
+  }
+  if (do_db && t < 32 && n0 + t < J.N) J.db[n0 + t] = ((bred[0][t] + bred[1][t]) + bred[2][t]) + bred[3][t];
+}
+
+}  // namespace
+
+hipError_t launch_l1_forward(const L1Args& a, hipStream_t st) {
+  if (a.M > L1_MAXM || a.npairs > L1_MAXP || a.H > L1_MAXH || a.H % 4 != 0 || a.C > L1_MAXC || a.heads > 8)
+    return hipErrorInvalidValue;
+  for (int m = 0; m < a.M; ++m)
+    if (a.D[m] > L1_MAXD || a.D[m] % 4 != 0) return hipErrorInvalidValue;
+  const unsigned tiles = (unsigned)((a.B + S - 1) / S);
+  const double B = a.B, H = a.H;
+  {
+    double fl = 0.0, by = 0.0;
+    for (int g = 0; g < a.npairs; ++g) {
+      const double D = a.D[a.pk[g]];
+      fl += 2.0 * B * H * (D + 2.0 * H);
+      by += 4.0 * (B * (D + 2.0 * H) + H * (D + 2.0 * H));
+    }
+    ProfLaunch prof_(st, "l1_pair_fwd_kernel", fl, by);
+    mmf_launch(l1_pair_fwd_kernel, dim3(tiles, a.npairs), dim3(NT), 0, st, a);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  ProfLaunch prof_(st, "l1_head_fwd_kernel", 2.0 * B * H * (H + a.C) + 4.0 * a.M * B * H,
+                   4.0 * (B * ((a.M + a.npairs) * H + a.M * H + 2 * H + a.C) + H * (H + a.C)));
+  mmf_launch(l1_head_fwd_kernel, dim3(tiles), dim3(NT), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_l1_backward(const L1Args& a, const L1WgArgs& w, hipStream_t st) {
+  const unsigned tiles = (unsigned)((a.B + S - 1) / S);
+  const double B = a.B, H = a.H;
+  hipError_t e;
+  {
+    ProfLaunch prof_(st, "l1_head_bwd_kernel", 2.0 * B * H * (H + a.C) + 4.0 * a.M * B * H,
+                     4.0 * (B * (a.C + 2 * H + 2 * a.M * H) + H * (H + a.C)));
+    mmf_launch(l1_head_bwd_kernel, dim3(tiles), dim3(NT), 0, st, a);
+  }
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  {
+    ProfLaunch prof_(st, "l1_pair_bwd_kernel", 4.0 * B * H * H * a.npairs,
+                     4.0 * a.npairs * (3.0 * B * H + 2.0 * H * H));
+    mmf_launch(l1_pair_bwd_kernel, dim3(tiles, a.npairs), dim3(NT), 0, st, a);
+  }
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  {
+    double fl = 0.0, by = 0.0;
+    for (int m = 0; m < a.M; ++m) {
+      fl += a.dx[m] ? 2.0 * B * H * a.D[m] : 0.0;
+      by += 4.0 * (B * H * 2 + B * H * (a.M - 1) + (a.dx[m] ? B * a.D[m] + H * a.D[m] : 0.0));
+    }
+    ProfLaunch prof_(st, "l1_mod_bwd_kernel", fl, by);
+    mmf_launch(l1_mod_bwd_kernel, dim3(tiles, a.M), dim3(NT), 0, st, a);
+  }
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  double fl = 0.0, by = 0.0;
+  for (int i = 0; i < w.njobs; ++i) {
+    const L1WgJob& J = w.j[i];
+    fl += 2.0 * B * J.N * J.K;
+    by += 4.0 * (B * (J.N + J.K) + (double)J.N * J.K);
+  }
+  int zblocks = w.nz ? w.zoff[w.nz] : 0;
+  for (int i = 0; i < w.nz; ++i) by += 4.0 * w.zn[i];
+  ProfLaunch prof_(st, "l1_wgrad_kernel", fl, by);
+  mmf_launch(l1_wgrad_kernel, dim3((unsigned)(w.ntiles + zblocks)), dim3(NT), 0, st, w);
+  return hipGetLastError();
+}
+
+}  // namespace mmf
+

@@ -455,6 +455,7 @@ hipError_t launch_rng_advance(uint64_t* state, hipStream_t st);   // state[1] +=
 hipError_t launch_cross_entropy(int B, int C, const float* logits, const int64_t* labels,
                                 float smoothing, float grad_scale, float* loss, float* dlogits,
                                 hipStream_t st);
+hipError_t launch_grad_accum(int64_t n, const float* src, float* dst, hipStream_t st);   // dst += src
 hipError_t launch_adamw(int64_t n, float* p, const float* g, float* m, float* v, int64_t* step,
                         float lr, float b1, float b2, float eps, float wd, float gscale,
                         hipStream_t st, const float* lr_dev = nullptr, const float* coef_dev = nullptr);
@@ -516,5 +517,55 @@ struct TailArgs {
 bool tail_supported(int M, int H, int C, int heads, int hd, int npairs);
 hipError_t launch_tail_fwd(const TailArgs& a, hipStream_t st);
 hipError_t launch_tail_bwd(const TailArgs& a, hipStream_t st);
+
+// ---------------------------------------------------------------------------
+// Launch-lean single-key step (l1.hip): every modality 2-D (L = 1, what src/train.py:261-279
+// feeds HybridFusion), every ordered pair present, fp32 ("highest").  Per 16-sample tile:
+//   pair fwd  (tile, pair):      X'_k, P_k = Drop(ReLU(X'_k W_k^T + b)), V = P_k W_v^T + b_v,
+//                                O = P' V (P' per head), A = O W_o^T + b_o
+//   head fwd  (tile):            pooled, gating scores, adaptive weights, fused, h1, logits
+//   head bwd  (tile):            dz1, dfused = dz1 W1, dscore, cvec
+//   pair bwd  (tile, pair):      dO = cvec_q W_o, dV = P' dO, dP_k|g = dV W_v
+//   modality bwd (tile, m):      dZ_m = gate(cvec_m + sum_g dP_k|g), dX_m = (dZ_m W_m) mask keep
+//   wgrad     (32x32 tiles):     every weight / bias gradient, K = B split over 4 waves, fixed
+//                                order; query / key projection gradients written as zeros
+// ---------------------------------------------------------------------------
+constexpr int L1_MAXM = 4, L1_MAXP = 12, L1_MAXH = 128, L1_MAXD = 128, L1_MAXC = 16;
+struct L1Args {
+  int32_t B, M, H, C, heads, npairs;
+  int32_t D[L1_MAXM];
+  int32_t pq[L1_MAXP], pk[L1_MAXP];
+  int32_t kdesig[L1_MAXM];           // the pair that stores X'_k and P_k (first pair keyed by k)
+  float p, gscale;                    // dropout p (0: no dropout) and 1 / (1 - p) (1 without)
+  float inv_cnt[L1_MAXM];
+  const float* mask;                  // (B, M)
+  const float* x[L1_MAXM];            // (B, D_m)
+  const uint64_t* rng_live;           // forward: the caller's live {seed, offset} (null: eval)
+  uint64_t* rng_advance;              // forward: offset advanced by the head kernel
+  RngSnap* snap;                      // the call's snapshot (saved)
+  const float *Wp[L1_MAXM], *bp[L1_MAXM];
+  const float *Wv[L1_MAXP], *bv[L1_MAXP], *Wo[L1_MAXP], *bo[L1_MAXP];
+  const float *gw[L1_MAXM], *gb[L1_MAXM];
+  const float *W1, *b1, *W2, *b2;
+  float *Xd[L1_MAXM], *P[L1_MAXM], *O[L1_MAXP], *A[L1_MAXP];
+  float *pooled, *scores, *weights, *fused, *h1;
+  float *logits, *weights_out;
+  float* maps[L1_MAXP];               // optional attention maps (B, heads, 1, 1)
+  const float* dlogits;
+  float *dz1, *cvec, *dscore;
+  float *dV[L1_MAXP], *dPk[L1_MAXP], *dZ[L1_MAXM], *dx[L1_MAXM];
+};
+constexpr int L1_MAXJOBS = 40, L1_MAXZ = 48;
+struct L1WgJob {                      // dW (N x K) = G^T X over B rows; db = column sums of G
+  const float* G; const float* X; float* dW; float* db;
+  int32_t ldg, ldx, N, K, tiles_k, tile0;
+};
+struct L1WgArgs {
+  L1WgJob j[L1_MAXJOBS];
+  int32_t njobs, B, ntiles;
+  float* z[L1_MAXZ]; int32_t zn[L1_MAXZ]; int32_t zoff[L1_MAXZ + 1]; int32_t nz;
+};
+hipError_t launch_l1_forward(const L1Args& a, hipStream_t st);
+hipError_t launch_l1_backward(const L1Args& a, const L1WgArgs& w, hipStream_t st);
 
 }  // namespace mmf

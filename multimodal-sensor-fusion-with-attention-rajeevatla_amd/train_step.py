@@ -19,8 +19,11 @@ the clip factor live in device scalars that the replayed kernels read, so an LR
 scheduler (set_lr / cosine_annealing_lr) needs no re-capture, and load_batch()
 copies each new batch into the static input buffers the graph reads.
 
-Not mirrored: Lightning's accumulate_grad_batches (config/base.yaml:75) -- one
-step here is one optimizer step over its batch.
+Gradient accumulation (Lightning's accumulate_grad_batches, config/base.yaml:75
+gradient_accumulation): with accumulate = k the step's batch is k micro-batches of B/k samples
+run one after the other through forward -> CE (loss scaled by 1/k, as Lightning scales it) ->
+backward, the micro-batch gradients summed on the device (mmf_grad_accumulate) before the
+exchange and the optimizer -- the memory of one micro-batch, the gradient of the whole batch.
 """
 
 from __future__ import annotations
@@ -86,7 +89,8 @@ class HybridTrainStep:
     def __init__(self, model: HybridFusion, feats: List[torch.Tensor], mask: torch.Tensor,
                  labels: torch.Tensor, lr: float = 1e-3, weight_decay: float = 1e-4,
                  betas=(0.9, 0.999), eps: float = 1e-8, label_smoothing: float = 0.05,
-                 gradient_clip_norm: float = 1.0, process_group=None, input_grads: bool = True):
+                 gradient_clip_norm: float = 1.0, process_group=None, input_grads: bool = True,
+                 accumulate: int = 1):
         dev = mask.device
         _nat.require_device(mask, "training inputs")
         self.model = model.train()
@@ -110,7 +114,12 @@ class HybridTrainStep:
         self.x = [_nat.f32c(f.to(dev)).clone() for f in feats]
         self.mask = _nat.f32c(mask).clone()
         self.labels = labels.to(dev, torch.int64).contiguous().clone()
-        self.plan = model._plan(self.x, False)
+        self.accumulate = int(accumulate)
+        nb = self.mask.size(0)
+        if self.accumulate < 1 or nb % self.accumulate:
+            raise ValueError(f"accumulate={accumulate}: the batch of {nb} samples does not split into equal micro-batches")
+        self.micro = nb // self.accumulate      # samples per micro-batch
+        self.plan = model._plan([x[:self.micro] for x in self.x], False)
         d = self.plan.desc
         params = self.plan.params(model)
         n = self.plan.num_param_elems
@@ -133,16 +142,27 @@ class HybridTrainStep:
         self.clip_ws = torch.empty(L.mmf_grad_clip_workspace_bytes(), dtype=torch.uint8, device=dev)
         self.saved = torch.empty(L.mmf_hybrid_saved_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
         self.ws = torch.empty(L.mmf_hybrid_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
-        self.logits = torch.empty(d.batch, d.num_classes, dtype=torch.float32, device=dev)
-        self.fw = torch.empty(d.batch, d.num_modalities, dtype=torch.float32, device=dev)
+        self.logits = torch.empty(nb, d.num_classes, dtype=torch.float32, device=dev)
+        self.fw = torch.empty(nb, d.num_modalities, dtype=torch.float32, device=dev)
         self.dlogits = torch.empty_like(self.logits)
-        self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.losses = torch.zeros(self.accumulate, dtype=torch.float32, device=dev)   # per micro-batch
         self.dx = [torch.empty_like(x) for x in self.x] if input_grads else []
         self.pstruct = self.plan.param_struct(params)
         self.gstruct = self.plan.param_struct(self.gviews)
-        self.xarr = _nat.ptr_array([x.data_ptr() for x in self.x])
-        self.dxarr = _nat.ptr_array([t.data_ptr() for t in self.dx]) if input_grads else None
+        # micro-batches after the first write their gradient here; it is added into self.grad
+        self.grad_mb = torch.zeros_like(self.grad) if self.accumulate > 1 else None
+        self.gstruct_mb = (self.plan.param_struct(self.plan.grad_views(self.grad_mb, params))
+                           if self.grad_mb is not None else None)
+        # per micro-batch pointer tables (row offsets into the static buffers)
+        self.xarr = [_nat.ptr_array([x[i * self.micro:].data_ptr() for x in self.x]) for i in range(self.accumulate)]
+        self.dxarr = ([_nat.ptr_array([t[i * self.micro:].data_ptr() for t in self.dx]) for i in range(self.accumulate)]
+                      if input_grads else None)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
+
+    @property
+    def loss(self) -> torch.Tensor:
+        """Mean CE loss of the last step (over its micro-batches)."""
+        return self.losses.mean() if self.accumulate > 1 else self.losses
 
     # ---------------------------------------------------------------- host controls
     def set_lr(self, lr: float) -> None:
@@ -174,20 +194,28 @@ class HybridTrainStep:
         L = _nat.lib()
         d = self.plan.desc
         st = _nat.stream_ptr(self.dev)
-        rc = L.mmf_hybrid_forward(ctypes.byref(d), ctypes.byref(self.pstruct),
-                                  ctypes.cast(self.xarr, ctypes.c_void_p), self.mask.data_ptr(),
-                                  self.rng.data_ptr(), self.saved.data_ptr(),
-                                  self.logits.data_ptr(), self.fw.data_ptr(), None, st)
-        _nat.check(rc, "train forward")
-        rc = L.mmf_cross_entropy_ls(d.batch, d.num_classes, self.logits.data_ptr(), self.labels.data_ptr(),
-                                    self.smoothing, 1.0, self.loss.data_ptr(), self.dlogits.data_ptr(), st)
-        _nat.check(rc, "train cross-entropy")
-        rc = L.mmf_hybrid_backward(ctypes.byref(d), ctypes.byref(self.pstruct),
-                                   ctypes.cast(self.xarr, ctypes.c_void_p), self.mask.data_ptr(),
-                                   self.saved.data_ptr(), self.dlogits.data_ptr(), self.ws.data_ptr(),
-                                   ctypes.byref(self.gstruct),
-                                   ctypes.cast(self.dxarr, ctypes.c_void_p) if self.dxarr else None, st)
-        _nat.check(rc, "train backward")
+        C, M, b = d.num_classes, d.num_modalities, self.micro
+        for i in range(self.accumulate):
+            logits = self.logits[i * b:]
+            rc = L.mmf_hybrid_forward(ctypes.byref(d), ctypes.byref(self.pstruct),
+                                      ctypes.cast(self.xarr[i], ctypes.c_void_p), self.mask[i * b:].data_ptr(),
+                                      self.rng.data_ptr(), self.saved.data_ptr(),
+                                      logits.data_ptr(), self.fw[i * b:].data_ptr(), None, st)
+            _nat.check(rc, "train forward")
+            rc = L.mmf_cross_entropy_ls(b, C, logits.data_ptr(), self.labels[i * b:].data_ptr(),
+                                        self.smoothing, 1.0 / self.accumulate, self.losses[i:].data_ptr(),
+                                        self.dlogits[i * b:].data_ptr(), st)
+            _nat.check(rc, "train cross-entropy")
+            g = self.gstruct if i == 0 else self.gstruct_mb
+            rc = L.mmf_hybrid_backward(ctypes.byref(d), ctypes.byref(self.pstruct),
+                                       ctypes.cast(self.xarr[i], ctypes.c_void_p), self.mask[i * b:].data_ptr(),
+                                       self.saved.data_ptr(), self.dlogits[i * b:].data_ptr(), self.ws.data_ptr(),
+                                       ctypes.byref(g),
+                                       ctypes.cast(self.dxarr[i], ctypes.c_void_p) if self.dxarr else None, st)
+            _nat.check(rc, "train backward")
+            if i > 0:
+                rc = L.mmf_grad_accumulate(self.grad.numel(), self.grad_mb.data_ptr(), self.grad.data_ptr(), st)
+                _nat.check(rc, "gradient accumulation")
 
     def allreduce(self) -> None:
         allreduce_flat(self.grad, self.pg, self.world)

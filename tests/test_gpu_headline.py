@@ -40,7 +40,9 @@ def env(pkg_on_path):
 EXPECT = {   # the benchmarked kernel instantiations (bench.py's kernel table names them)
     "c2": ["mask_dropout_rows_kernel", "attn_pool_fwd_lean<32, 0, true, false, true>",
            "attn_pool_bwd_fused_lean<32, 0, false>", "gemm_wsr_kernel<0>"],
-    "c2_l1": ["mask_dropout_rows_kernel", "sk_fwd_kernel"],
+    # the launch-lean single-key step (csrc/l1.hip)
+    "c2_l1": ["l1_pair_fwd_kernel", "l1_head_fwd_kernel", "l1_head_bwd_kernel", "l1_pair_bwd_kernel",
+              "l1_mod_bwd_kernel", "l1_wgrad_kernel"],
 }
 
 

@@ -80,8 +80,12 @@ def test_hybrid_l1_qk_grads_exactly_zero(mods, case, precision):
     _, launches = nat.profile_end()
     assert _assert_qk_zero(model) == 4 * len(model.attention_modules)
     names = _kernels(launches)
-    # no attention kernel (QK^T / softmax / dQ / dK) ran: the single-key kernel replaced it
-    assert "sk_fwd_kernel" in names, names
+    # no attention kernel (QK^T / softmax / dQ / dK) ran: the single-key kernels replaced it --
+    # the launch-lean step (csrc/l1.hip) where it applies ("highest", every pair present, D_m and
+    # H <= 128 and % 4), the general single-key plan otherwise
+    lean = precision == "highest" and not case.deleted and case.hidden <= 128 and case.hidden % 4 == 0 \
+        and all(case.dims[m] % 4 == 0 and case.dims[m] <= 128 for m in case.names) and case.classes <= 16
+    assert ("l1_pair_fwd_kernel" if lean else "sk_fwd_kernel") in names, names
     assert not [k for k in names if k.startswith("attn_")], names
     # the attention maps are the mask indicator (eval mode): exactly {0, 1}
     fx = load_fixture(case.name)
@@ -149,3 +153,45 @@ def test_cma_l1_query_key_grads_exactly_zero(mods, case, precision):
     if precision != "medium":
         assert close(att.detach().cpu(), fx["attended"], 1e-3, 1e-5)
         assert close(vt.grad.cpu(), fx["dvalue"], 1e-3, 1e-5)
+
+
+@pytest.mark.parametrize("case_name", ["tiny_l1", "c2_l1"])
+@pytest.mark.parametrize("train", [False, True])
+def test_lean_l1_step_matches_general_plan(mods, case_name, train, monkeypatch):
+    """The launch-lean single-key step (csrc/l1.hip) against the general single-key plan
+    (MMF_NO_L1_LEAN=1) on the same weights, inputs and dropout stream: same logits, attention maps
+    and fusion weights to 1e-5, every gradient to 1e-4 of its largest element (fp32 reassociation
+    only), and the same exact zeros."""
+    fusion, _, nat = mods
+    case = next(c for c in HYBRID_CASES if c.name == case_name)
+    feats_np, mask_np, grad_np = hybrid_inputs(case)
+    runs = []
+    for general in (False, True):
+        if general:
+            monkeypatch.setenv("MMF_NO_L1_LEAN", "1")
+        model = _build(fusion, case, train=train, p=0.3)
+        model._rng_state.copy_(torch.tensor([0x5EED, 3], dtype=torch.int64))
+        feats = {m: torch.from_numpy(v).cuda().requires_grad_(True) for m, v in feats_np.items()}
+        nat.profile_begin()
+        logits, info = model(feats, torch.from_numpy(mask_np).cuda(), return_attention=True)
+        (logits * torch.from_numpy(grad_np).cuda()).sum().backward()
+        torch.cuda.synchronize()
+        _, launches = nat.profile_end()
+        names = _kernels(launches)
+        assert ("sk_fwd_kernel" if general else "l1_pair_fwd_kernel") in names, names
+        runs.append((logits.detach().cpu(), {k: v.cpu() for k, v in info["attention_maps"].items()},
+                     info["fusion_weights"].cpu(), [feats[m].grad.cpu() for m in case.names],
+                     {n: p.grad.cpu() for n, p in model.named_parameters()}))
+        monkeypatch.delenv("MMF_NO_L1_LEAN", raising=False)
+    (l1, m1, w1, dx1, g1), (l2, m2, w2, dx2, g2) = runs
+    assert close(l1, l2, 1e-5, 1e-6)
+    assert close(w1, w2, 1e-5, 1e-7)
+    for k in m1:
+        assert torch.equal(m1[k], m2[k]), k
+    for a, b in zip(dx1, dx2):
+        assert close(a, b, 1e-4, 1e-8)
+    for n in g1:
+        if ".query_proj." in n or ".key_proj." in n:
+            assert torch.all(g1[n] == 0) and torch.all(g2[n] == 0), n
+        else:
+            assert close(g1[n], g2[n], 1e-4, 1e-8), n

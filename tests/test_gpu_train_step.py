@@ -157,3 +157,37 @@ def test_fused_clip_adamw_matches_two_call_path(mods, max_norm):
     assert int(runs[1][3].item()) == 6
     if max_norm < 1.0:
         assert float(runs[1][5].item()) < 1.0
+
+
+@pytest.mark.parametrize("accumulate", [2, 4])
+@pytest.mark.parametrize("seq", [True, False])
+def test_gradient_accumulation_equals_full_batch(mods, accumulate, seq):
+    """accumulate = k (config/base.yaml:75 gradient_accumulation, Lightning's accumulate_grad_batches):
+    k micro-batches of B/k samples, each loss scaled by 1/k, gradients summed on the device -- the
+    gradient of the whole batch's mean loss (no dropout, so both runs see the same function), the
+    same mean loss, the same input gradients; sequence mode and the 2-D single-key step."""
+    fusion, train_step = mods
+    feats, mask, labels = _batch(7)
+    if not seq:
+        feats = [f[:, 0] for f in feats]
+    runs = []
+    for acc in (1, accumulate):
+        model = _model(fusion, 0.0).cuda()
+        st = train_step.HybridTrainStep(model, [f.cuda() for f in feats], mask.cuda(), labels.cuda(), accumulate=acc)
+        st.forward_backward()
+        torch.cuda.synchronize()
+        runs.append((st.grad.cpu(), float(st.loss.item()), [t.cpu() for t in st.dx], st.logits.cpu()))
+    (g1, l1, dx1, lg1), (g2, l2, dx2, lg2) = runs
+    assert torch.allclose(lg1, lg2, rtol=1e-5, atol=1e-6)
+    assert abs(l1 - l2) <= 1e-5 * abs(l1)
+    assert (g1 - g2).abs().max() <= 1e-5 * g1.abs().max()
+    for a, b in zip(dx1, dx2):
+        assert (a - b).abs().max() <= 1e-5 * a.abs().max()
+
+
+def test_accumulate_rejects_uneven_micro_batches(mods):
+    fusion, train_step = mods
+    feats, mask, labels = _batch(8)
+    with pytest.raises(ValueError, match="equal micro-batches"):
+        train_step.HybridTrainStep(_model(fusion, 0.0).cuda(), [f.cuda() for f in feats], mask.cuda(), labels.cuda(),
+                                   accumulate=3)
