@@ -210,6 +210,7 @@ __device__ float adaptive(int M, const float* score, const float* mask, float* s
 }
 
 // ------------------------------------------------------------------------------ forward
+template <int FH>
 __global__ __launch_bounds__(NT) void l1_pair_fwd_kernel(const L1Args a) {
   __shared__ __attribute__((aligned(16))) float xs[S * LD];
   __shared__ __attribute__((aligned(16))) float ps[S * LD];
@@ -218,8 +219,8 @@ __global__ __launch_bounds__(NT) void l1_pair_fwd_kernel(const L1Args a) {
   __shared__ float pp[S * 8];
   __shared__ float msk[S];
   const int g = blockIdx.y, b0 = blockIdx.x * S;
-  const int k = a.pk[g], D = a.D[k], H = a.H, B = a.B;
-  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int k = a.pk[g], D = FH ? FH : a.D[k], H = FH ? FH : a.H, B = a.B;
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6) & 3;
   const bool desig = a.kdesig[k] == g;
   // every global operand first, those needed first issued first (the input rows, the mask and the
   // rng state, then the three weights of this wave's columns: the waits before the keep draws and
@@ -356,6 +357,7 @@ __device__ __forceinline__ void stage_small(const L1Args& a, HeadSmall& hs) {
   if (t >= 64 && t < 64 + C) hs.b2[t - 64] = a.b2[t - 64];
 }
 
+template <int FH>
 __global__ __launch_bounds__(NT) void l1_head_fwd_kernel(const L1Args a) {
   __shared__ __attribute__((aligned(16))) float pl[L1_MAXM * S * LD];
   __shared__ __attribute__((aligned(16))) float fs[S * LD];
@@ -364,8 +366,8 @@ __global__ __launch_bounds__(NT) void l1_head_fwd_kernel(const L1Args a) {
   __shared__ uint8_t kcl[KB_BYTES];
   __shared__ float msk[S * L1_MAXM], sc[S * L1_MAXM], wt[S * L1_MAXM];
   const int b0 = blockIdx.x * S;
-  const int M = a.M, H = a.H, B = a.B, C = a.C;
-  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int M = a.M, H = FH ? FH : a.H, B = a.B, C = a.C;
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6) & 3;
   // loads, first-needed first: the mask rows and the rng snapshot, the attended and projected
   // rows, the small operands, then W1
   for (int e = t; e < S * M; e += NT) msk[e] = b0 + e / M < B ? a.mask[(int64_t)b0 * M + e] : 0.f;
@@ -493,6 +495,7 @@ __global__ __launch_bounds__(NT) void l1_head_fwd_kernel(const L1Args a) {
 }
 
 // ------------------------------------------------------------------------------ backward
+template <int FH>
 __global__ __launch_bounds__(NT) void l1_head_bwd_kernel(const L1Args a) {
   __shared__ __attribute__((aligned(16))) float pl[L1_MAXM * S * LD];
   __shared__ __attribute__((aligned(16))) float zs[S * LD];
@@ -501,8 +504,8 @@ __global__ __launch_bounds__(NT) void l1_head_bwd_kernel(const L1Args a) {
   __shared__ float dl[S * L1_MAXC];
   __shared__ float msk[S * L1_MAXM], sc[S * L1_MAXM], wt[S * L1_MAXM], dw[S * L1_MAXM], dsc[S * L1_MAXM];
   const int b0 = blockIdx.x * S;
-  const int M = a.M, H = a.H, B = a.B, C = a.C;
-  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int M = a.M, H = FH ? FH : a.H, B = a.B, C = a.C;
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6) & 3;
   for (int e = t; e < S * C; e += NT) dl[e] = b0 + e / C < B ? a.dlogits[(int64_t)b0 * C + e] : 0.f;
   for (int e = t; e < S * M; e += NT) {
     const bool in = b0 + e / M < B;
@@ -607,105 +610,107 @@ __global__ __launch_bounds__(NT) void l1_head_bwd_kernel(const L1Args a) {
   }
 }
 
-__global__ __launch_bounds__(NT) void l1_pair_bwd_kernel(const L1Args a) {
-  __shared__ __attribute__((aligned(16))) float cs[S * LD];
+// Backward of everything keyed by one modality m, per 16-sample tile (tile, m): for every pair
+// g = (q, m) in order, dO = cvec_q W_o (dA = cvec_q), dV = P' dO per head (stored for dW_v),
+// dP_m += dV W_v; then dZ_m = ReLU' Drop' (cvec_m + dP_m) (P_m is post-dropout: P_m > 0 marks
+// kept, active units) and dX_m = (dZ_m W_m) mask_m input-dropout'.  Every weight of the launch is
+// loaded at kernel start; dP_m accumulates in the registers across the pairs.
+template <int FH, int NPK>
+__global__ __launch_bounds__(NT) void l1_key_bwd_kernel(const L1Args a) {
+  __shared__ __attribute__((aligned(16))) float cs[NPK][S * LD];
   __shared__ __attribute__((aligned(16))) float vs[S * LD];
-  __shared__ float pp[S * 8];
-  const int g = blockIdx.y, b0 = blockIdx.x * S;
-  const int q = a.pq[g], H = a.H, B = a.B, M = a.M;
-  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  RngSnap rs{0, 0};
-  if (a.p > 0.f) rs = *a.snap;
-  load_tile(a.cvec + (int64_t)q * H, M * H, B, b0, H, cs);
-  zero_pad(cs, H);
-  pprime_tile(a, rs, g, b0, pp);
-  __builtin_amdgcn_sched_barrier(0);
-  WTile wo, wv;
-  wload_nn(a.Wo[g], H, H, wave, lane, wo);
-  wload_nn(a.Wv[g], H, H, wave, lane, wv);
-  __syncthreads();
-  const int kq = lane >> 4, jl = lane & 15, hd = H / a.heads;
-  f32x4 acc[NTL];
-  // dO = dA W_o (dA = cvec_q), dV = P' dO per head
-  mma(cs, wo, acc, lane);
-#pragma unroll
-  for (int u = 0; u < NTL; ++u) {
-    const int j = 16 * (wave + 4 * u) + jl;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = 4 * kq + r;
-      const float v = j < H ? acc[u][r] * pp[i * a.heads + j / hd] : 0.f;
-      vs[i * LD + j] = v;
-      if (b0 + i < B && j < H) a.dV[g][(int64_t)(b0 + i) * H + j] = v;
-    }
-  }
-  __syncthreads();
-  // the pair's share of dP_k: dV W_v
-  mma(vs, wv, acc, lane);
-#pragma unroll
-  for (int u = 0; u < NTL; ++u) {
-    const int j = 16 * (wave + 4 * u) + jl;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = 4 * kq + r;
-      if (b0 + i < B && j < H) a.dPk[g][(int64_t)(b0 + i) * H + j] = acc[u][r];
-    }
-  }
-}
-
-__global__ __launch_bounds__(NT) void l1_mod_bwd_kernel(const L1Args a) {
   __shared__ __attribute__((aligned(16))) float zs[S * LD];
+  __shared__ float pp[NPK][S * 8];
   __shared__ uint8_t kin[KB_BYTES];
   __shared__ float msk[S];
   const int m = blockIdx.y, b0 = blockIdx.x * S;
-  const int H = a.H, B = a.B, M = a.M, D = a.D[m];
-  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int H = FH ? FH : a.H, D = FH ? FH : a.D[m], B = a.B, M = a.M;
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6) & 3;
   const bool want_dx = a.dx[m] != nullptr;
-  if (t < S) msk[t] = b0 + t < B ? a.mask[(int64_t)(b0 + t) * M + m] : 0.f;
+  // the pairs keyed by m, in pair order
+  int gl[NPK];
+  {
+    int n = 0;
+    for (int g = 0; g < a.npairs; ++g)
+      if (a.pk[g] == m && n < NPK) gl[n++] = g;
+  }
   RngSnap rs{0, 0};
-  if (a.p > 0.f && want_dx) {
-    rs = *a.snap;
-    keep_tile(rs, SITE_IN + m, b0, D, a.p, kin);
+  if (a.p > 0.f) rs = *a.snap;
+#pragma unroll
+  for (int i = 0; i < NPK; ++i) load_tile(a.cvec + (int64_t)a.pq[gl[i]] * H, M * H, B, b0, H, cs[i]);
+  if (t < S) msk[t] = b0 + t < B ? a.mask[(int64_t)min(b0 + t, B - 1) * M + m] : 0.f;
+  __builtin_amdgcn_sched_barrier(0);
+  WTile wo[NPK], wv[NPK];
+#pragma unroll
+  for (int i = 0; i < NPK; ++i) {
+    wload_nn(a.Wo[gl[i]], H, H, wave, lane, wo[i]);
+    wload_nn(a.Wv[gl[i]], H, H, wave, lane, wv[i]);
   }
-  // dZ_m = ReLU' Drop' (cvec_m + sum over the pairs keyed by m of dP_k|g): P_m is post-dropout,
-  // so P_m > 0 marks kept, active units
-  const int h4 = H / 4;
-  for (int e = t; e < S * h4; e += NT) {
-    const int i = e / h4, c = 4 * (e - i * h4);
-    const int bi = min(b0 + i, B - 1);
-    const int64_t row = (int64_t)bi * H + c;
-    float4 s = *reinterpret_cast<const float4*>(a.cvec + ((int64_t)bi * M + m) * H + c);
-    for (int g = 0; g < a.npairs; ++g) {
-      if (a.pk[g] != m) continue;
-      const float4 v = *reinterpret_cast<const float4*>(a.dPk[g] + row);
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-    }
-    const float4 p = *reinterpret_cast<const float4*>(a.P[m] + row);
-    float4 z = make_float4(p.x > 0.f ? s.x * a.gscale : 0.f, p.y > 0.f ? s.y * a.gscale : 0.f,
-                           p.z > 0.f ? s.z * a.gscale : 0.f, p.w > 0.f ? s.w * a.gscale : 0.f);
-    if (b0 + i < B) *reinterpret_cast<float4*>(a.dZ[m] + row) = z;
-    else z = make_float4(0.f, 0.f, 0.f, 0.f);
-    *reinterpret_cast<float4*>(zs + i * LD + c) = z;
+#pragma unroll
+  for (int i = 0; i < NPK; ++i) {
+    pprime_tile(a, rs, gl[i], b0, pp[i]);
+    zero_pad(cs[i], H);
   }
-  if (!want_dx) return;
-  WTile wp;
-  wload_nn(a.Wp[m], D, H, wave, lane, wp);
-  zero_pad(zs, H);
+  if (a.p > 0.f && want_dx) keep_tile(rs, SITE_IN + m, b0, D, a.p, kin);
   __syncthreads();
-  // dX_m = (dZ_m W_m) mask_m input-dropout'
-  f32x4 acc[NTL];
-  mma(zs, wp, acc, lane);
-  const int kq = lane >> 4, jl = lane & 15;
+  const int kq = lane >> 4, jl = lane & 15, hd = H / a.heads;
+  f32x4 dp[NTL], acc[NTL];
+#pragma unroll
+  for (int u = 0; u < NTL; ++u) dp[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < NPK; ++i) {
+    const int g = gl[i];
+    mma(cs[i], wo[i], acc, lane);
+#pragma unroll
+    for (int u = 0; u < NTL; ++u) {
+      const int j = 16 * (wave + 4 * u) + jl;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ii = 4 * kq + r;
+        const float v = j < H ? acc[u][r] * pp[i][ii * a.heads + j / hd] : 0.f;
+        vs[ii * LD + j] = v;
+        if (b0 + ii < B && j < H) a.dV[g][(int64_t)(b0 + ii) * H + j] = v;
+      }
+    }
+    __syncthreads();
+    mma(vs, wv[i], acc, lane);
+#pragma unroll
+    for (int u = 0; u < NTL; ++u) dp[u] += acc[u];
+    if (i + 1 < NPK) __syncthreads();   // (vs is rewritten by the next pair)
+  }
+  // dZ_m, from the accumulator layout: lane (jl, kq), reg r = row 4 kq + r, column 16 (wave + 4u) + jl
+  WTile wp;
+  if (want_dx) wload_nn(a.Wp[m], D, H, wave, lane, wp);
 #pragma unroll
   for (int u = 0; u < NTL; ++u) {
     const int j = 16 * (wave + 4 * u) + jl;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int i = 4 * kq + r;
-      if (b0 + i >= B || j >= D) continue;
-      float v = acc[u][r] * msk[i];
-      if (a.p > 0.f) v = kept(kin, b0, D, i, j) ? v * a.gscale : 0.f;
-      a.dx[m][(int64_t)(b0 + i) * D + j] = v;
+      const int ii = 4 * kq + r;
+      float z = 0.f;
+      if (b0 + ii < B && j < H) {
+        const int64_t row = (int64_t)(b0 + ii) * H + j;
+        const float c = a.cvec[((int64_t)(b0 + ii) * M + m) * H + j];
+        z = a.P[m][row] > 0.f ? (c + dp[u][r]) * a.gscale : 0.f;
+        a.dZ[m][row] = z;
+      }
+      zs[ii * LD + j] = z;
+    }
+  }
+  if (!want_dx) return;
+  __syncthreads();
+  // dX_m = (dZ_m W_m) mask_m input-dropout'
+  mma(zs, wp, acc, lane);
+#pragma unroll
+  for (int u = 0; u < NTL; ++u) {
+    const int j = 16 * (wave + 4 * u) + jl;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int ii = 4 * kq + r;
+      if (b0 + ii >= B || j >= D) continue;
+      float v = acc[u][r] * msk[ii];
+      if (a.p > 0.f) v = kept(kin, b0, D, ii, j) ? v * a.gscale : 0.f;
+      a.dx[m][(int64_t)(b0 + ii) * D + j] = v;
     }
   }
 }
@@ -775,6 +780,14 @@ __global__ __launch_bounds__(NT) void l1_wgrad_kernel(const L1WgArgs w) {
   if (do_db && t < 32 && n0 + t < J.N) J.db[n0 + t] = ((bred[0][t] + bred[1][t]) + bred[2][t]) + bred[3][t];
 }
 
+// the C2 shape: every hidden and input width 128 (compile-time tile guards)
+bool l1_full(const L1Args& a) {
+  if (a.H != 128) return false;
+  for (int m = 0; m < a.M; ++m)
+    if (a.D[m] != 128) return false;
+  return true;
+}
+
 }  // namespace
 
 hipError_t launch_l1_forward(const L1Args& a, hipStream_t st) {
@@ -791,41 +804,51 @@ hipError_t launch_l1_forward(const L1Args& a, hipStream_t st) {
       fl += 2.0 * B * H * (D + 2.0 * H);
       by += 4.0 * (B * (D + 2.0 * H) + H * (D + 2.0 * H));
     }
-    ProfLaunch prof_(st, "l1_pair_fwd_kernel", fl, by);
-    mmf_launch(l1_pair_fwd_kernel, dim3(tiles, a.npairs), dim3(NT), 0, st, a);
+    ProfLaunch prof_(st, l1_full(a) ? "l1_pair_fwd_kernel<128>" : "l1_pair_fwd_kernel<0>", fl, by);
+    if (l1_full(a)) mmf_launch(l1_pair_fwd_kernel<128>, dim3(tiles, a.npairs), dim3(NT), 0, st, a);
+    else mmf_launch(l1_pair_fwd_kernel<0>, dim3(tiles, a.npairs), dim3(NT), 0, st, a);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  ProfLaunch prof_(st, "l1_head_fwd_kernel", 2.0 * B * H * (H + a.C) + 4.0 * a.M * B * H,
+  ProfLaunch prof_(st, l1_full(a) ? "l1_head_fwd_kernel<128>" : "l1_head_fwd_kernel<0>", 2.0 * B * H * (H + a.C) + 4.0 * a.M * B * H,
                    4.0 * (B * ((a.M + a.npairs) * H + a.M * H + 2 * H + a.C) + H * (H + a.C)));
-  mmf_launch(l1_head_fwd_kernel, dim3(tiles), dim3(NT), 0, st, a);
+  if (l1_full(a)) mmf_launch(l1_head_fwd_kernel<128>, dim3(tiles), dim3(NT), 0, st, a);
+  else mmf_launch(l1_head_fwd_kernel<0>, dim3(tiles), dim3(NT), 0, st, a);
   return hipGetLastError();
 }
 
 hipError_t launch_l1_backward(const L1Args& a, const L1WgArgs& w, hipStream_t st) {
+  if (a.npairs != a.M * (a.M - 1) || a.M < 2) return hipErrorInvalidValue;
   const unsigned tiles = (unsigned)((a.B + S - 1) / S);
   const double B = a.B, H = a.H;
   hipError_t e;
   {
-    ProfLaunch prof_(st, "l1_head_bwd_kernel", 2.0 * B * H * (H + a.C) + 4.0 * a.M * B * H,
+    ProfLaunch prof_(st, l1_full(a) ? "l1_head_bwd_kernel<128>" : "l1_head_bwd_kernel<0>", 2.0 * B * H * (H + a.C) + 4.0 * a.M * B * H,
                      4.0 * (B * (a.C + 2 * H + 2 * a.M * H) + H * (H + a.C)));
-    mmf_launch(l1_head_bwd_kernel, dim3(tiles), dim3(NT), 0, st, a);
-  }
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  {
-    ProfLaunch prof_(st, "l1_pair_bwd_kernel", 4.0 * B * H * H * a.npairs,
-                     4.0 * a.npairs * (3.0 * B * H + 2.0 * H * H));
-    mmf_launch(l1_pair_bwd_kernel, dim3(tiles, a.npairs), dim3(NT), 0, st, a);
+    if (l1_full(a)) mmf_launch(l1_head_bwd_kernel<128>, dim3(tiles), dim3(NT), 0, st, a);
+    else mmf_launch(l1_head_bwd_kernel<0>, dim3(tiles), dim3(NT), 0, st, a);
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   {
     double fl = 0.0, by = 0.0;
     for (int m = 0; m < a.M; ++m) {
       fl += a.dx[m] ? 2.0 * B * H * a.D[m] : 0.0;
-      by += 4.0 * (B * H * 2 + B * H * (a.M - 1) + (a.dx[m] ? B * a.D[m] + H * a.D[m] : 0.0));
+      by += 4.0 * (B * H * 2 + (a.dx[m] ? B * a.D[m] + H * a.D[m] : 0.0));
     }
-    ProfLaunch prof_(st, "l1_mod_bwd_kernel", fl, by);
-    mmf_launch(l1_mod_bwd_kernel, dim3(tiles, a.M), dim3(NT), 0, st, a);
+    fl += 4.0 * B * H * H * a.npairs;
+    by += 4.0 * a.npairs * (2.0 * B * H + 2.0 * H * H);
+    const bool full = l1_full(a);
+    const int npk = a.npairs / a.M;
+    ProfLaunch prof_(st, full ? "l1_key_bwd_kernel<128>" : "l1_key_bwd_kernel<0>", fl, by);
+    const dim3 grid(tiles, a.M);
+#define L1_KEY(FH)                                                                     \
+    switch (npk) {                                                                     \
+      case 1: mmf_launch(l1_key_bwd_kernel<FH, 1>, grid, dim3(NT), 0, st, a); break;   \
+      case 2: mmf_launch(l1_key_bwd_kernel<FH, 2>, grid, dim3(NT), 0, st, a); break;   \
+      default: mmf_launch(l1_key_bwd_kernel<FH, 3>, grid, dim3(NT), 0, st, a); break;  \
+    }
+    if (full) { L1_KEY(128) } else { L1_KEY(0) }
+#undef L1_KEY
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   double fl = 0.0, by = 0.0;
