@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 
 #include "capi_util.h"
 
@@ -654,13 +655,22 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
       bool fits = true;
       for (const AttnPair& a : pairs) {
         if (!(a.keep_bits && a.Lk % 32 == 0 && a.Lk > 0 && a.kw_ld >= a.Lk / 32)) continue;
-        if (nkw == 16) { fits = false; break; }
+        // at most 16 pairs, each under launch_mask_dropout's 2^31-word bound: otherwise the
+        // side-stream / inline draws (never a failed forward)
+        const int64_t nw = (int64_t)B * nh * a.Lq * (a.Lk / 32);
+        if (nkw == 16 || nw >= ((int64_t)1 << 31)) { fits = false; break; }
         ma.kw[nkw++] = {a.keep_bits, (uint32_t)a.Lq, (uint32_t)a.Lk, (uint32_t)a.kw_ld, a.drop_site};
       }
       ma.nkw = fits ? nkw : 0;
       ma.B = B;
       ma.heads = nh;
       kw_fused = fits;
+      static bool warned = false;
+      if (!fits && getenv("MMF_KW_FUSED") && !warned) {
+        warned = true;
+        fprintf(stderr, "mmfusion: MMF_KW_FUSED requested but the keep-word fold does not fit "
+                        "(> 16 pairs or > 2^31 words per pair): drawing them on the side stream / inline\n");
+      }
     }
     STAGE_TRY("fwd.input_mask", launch_mask_dropout(ma, st));
     fork_keep_words();   // the rng snapshot exists from here on

@@ -330,6 +330,77 @@ def test_side_stream_keep_words_match_inline_draws(mods, case_name, prec, mode, 
         assert torch.equal(a, b)
 
 
+_M6 = ["m0", "m1", "m2", "m3", "m4", "m5"]
+FOLD_EDGE_CASES = {
+    # the fold forced with long keys (MMF_KW_FUSED=1): the one-pass long forward reads the words
+    # the input-mask kernel drew
+    "long_forced": (HybridCase("fold_long", ["a", "b"], {"a": 32, "b": 48}, {"a": 160, "b": 288}, batch=2,
+                               hidden=128, heads=2, classes=4, seed=55, mask=[[1, 1], [0.5, 1]]), "medium", True),
+    # mixed key lengths (C4-like 30 / 50 beside 32): only the Lk % 32 == 0 pair is folded, the
+    # launch is not lean (it draws inline over the words the fold wrote: the same bits)
+    "mixed_lk": (HybridCase("fold_mixed", ["a", "b", "c"], {"a": 24, "b": 16, "c": 8}, {"a": 30, "b": 32, "c": 50},
+                            batch=3, hidden=64, heads=2, classes=5, seed=61, mask=[[1, 1, 1], [1, 0, 1], [0.5, 1, 0]]),
+                 "highest", False),
+    # 30 pairs (> 16): no fold; forced with long keys it falls back to the side stream
+    "many_pairs_long": (HybridCase("fold_many", _M6, {m: 8 + 4 * i for i, m in enumerate(_M6)},
+                                   {m: 160 for m in _M6}, batch=1, hidden=64, heads=2, classes=3, seed=62,
+                                   mask=[[1, 1, 0.5, 1, 1, 1]]), "medium", True),
+    "many_pairs_short": (HybridCase("fold_many_s", _M6, {m: 8 + 4 * i for i, m in enumerate(_M6)},
+                                    {m: 64 for m in _M6}, batch=2, hidden=64, heads=2, classes=3, seed=63,
+                                    mask=[[1, 1, 0.5, 1, 1, 1], [1, 0, 1, 1, 1, 1]]), "highest", False),
+}
+
+
+@pytest.mark.parametrize("which", list(FOLD_EDGE_CASES))
+def test_keep_word_fold_edge_cases_match_inline_draws(mods, which, monkeypatch):
+    """The keep-word fold's edge cases: forced with long keys, mixed key lengths where
+    only some pairs are folded, and more than 16 pairs (no fold; with MMF_KW_FUSED=1 the side stream
+    instead, never a failed forward) give the inline draws' logits and gradients bit for bit."""
+    fusion, _ = mods
+    import mmf_native
+    case, prec, forced = FOLD_EDGE_CASES[which]
+    sd = hybrid_state(case.names, case.dims, case.hidden, case.classes, case.seed)
+    feats_np, mask_np, grad_np = hybrid_inputs(case)
+    prev = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision(prec)
+    try:
+        runs = []
+        for inline in (False, True):
+            if forced:
+                monkeypatch.setenv("MMF_KW_FUSED", "1")
+            if inline:
+                monkeypatch.setenv("MMF_NO_SIDE_STREAM", "1")
+            model = fusion.HybridFusion({m: case.dims[m] for m in case.names}, hidden_dim=case.hidden,
+                                        num_classes=case.classes, num_heads=case.heads, dropout=P)
+            model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+            model = model.cuda().train()
+            model._rng_state.copy_(torch.tensor([SEED, OFFSET], dtype=torch.int64))
+            feats = {m: torch.from_numpy(v).cuda().requires_grad_(True) for m, v in feats_np.items()}
+            mmf_native.profile_begin()
+            logits = model(feats, torch.from_numpy(mask_np).cuda())
+            (logits * torch.from_numpy(grad_np).cuda()).sum().backward()
+            torch.cuda.synchronize()
+            _, launches = mmf_native.profile_end()
+            runs.append((logits.detach(), [feats[m].grad for m in case.names],
+                         [p_.grad.clone() for p_ in model.parameters()], [k for _, k, *_ in launches]))
+            monkeypatch.delenv("MMF_NO_SIDE_STREAM", raising=False)
+            monkeypatch.delenv("MMF_KW_FUSED", raising=False)
+    finally:
+        torch.set_float32_matmul_precision(prev)
+    (l1, dx1, dw1, n1), (l2, dx2, dw2, n2) = runs
+    if which == "long_forced":
+        assert "attn_keep_words_kernel" not in n1 and any(k.startswith("attn_poolL_fwd_fused_bf16") for k in n1), n1
+    elif which == "many_pairs_long":
+        assert "attn_keep_words_kernel" in n1, n1   # the side stream took over
+    else:
+        assert "attn_keep_words_kernel" not in n1, n1
+    if which == "many_pairs_short":   # no fold: the lean forward draws its own words
+        assert not any(k.startswith("attn_pool_fwd_lean") and k.endswith("true, false, true>") for k in n1), n1
+    assert torch.equal(l1, l2)
+    for a, b in zip(dx1 + dw1, dx2 + dw2):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("prec", ["highest", "medium"])
 def test_gemm_group_interleave_is_bit_exact(mods, prec, monkeypatch):
     """The XCD-aware group interleave of the GEMM launcher (MMF_GEMM_ILV=2, every launch: the groups of one
