@@ -31,6 +31,33 @@
 namespace mmf {
 namespace {
 
+#ifdef MMF_STAMPS
+// Diagnostic build only (make stampsl1): s_memtime at phase boundaries (slots 0..7) and
+// s_memrealtime (100 MHz, one clock for the whole chip) at the start / end (slots 8 / 9) of
+// thread 0 of every workgroup, per kernel k (0 pair fwd, 1 head fwd, 2 head bwd, 3 key bwd,
+// 4 wgrad); read by mmf_l1_stamps_read (scripts/l1_stamps.py).  Never in the product library.
+constexpr int L1_STAMP_WG = 1024;
+__device__ unsigned long long g_l1_stamps[5][L1_STAMP_WG][10];
+// (the counter moves to VGPRs inside the asm: an SGPR result kept live to a store that the
+// compiler sinks past later code failed in instruction selection, "illegal VGPR to SGPR copy")
+#define L1_TS(k, i, ins)                                                                     \
+  {                                                                                        \
+    unsigned lo_, hi_;                                                                     \
+    __builtin_amdgcn_sched_barrier(0);                                                     \
+    asm volatile(ins " s[92:93]\n\ts_waitcnt lgkmcnt(0)\n\tv_mov_b32 %0, s92\n\tv_mov_b32 %1, s93" \
+                 : "=v"(lo_), "=v"(hi_)::"s92", "s93", "memory");                          \
+    __builtin_amdgcn_sched_barrier(0);                                                     \
+    const int sid_ = blockIdx.y * gridDim.x + blockIdx.x;                                  \
+    if (threadIdx.x == 0 && sid_ < L1_STAMP_WG)                                            \
+      g_l1_stamps[k][sid_][i] = ((unsigned long long)hi_ << 32) | lo_;                     \
+  }
+#define L1_ST(k, i) L1_TS(k, i, "s_memtime")
+#define L1_RT(k, i) L1_TS(k, i, "s_memrealtime")
+#else
+#define L1_ST(k, i)
+#define L1_RT(k, i)
+#endif
+
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int NT = 256;          // 4 waves
@@ -243,6 +270,8 @@ __global__ __launch_bounds__(NT) void l1_pair_fwd_kernel(const L1Args a) {
   const float mk = a.mask[(int64_t)min(b0 + (t & (S - 1)), B - 1) * a.M + k];
   const int ih = t / a.heads;
   const float mkh = a.mask[(int64_t)min(b0 + min(ih, S - 1), B - 1) * a.M + k];
+  L1_RT(0, 8);
+  L1_ST(0, 0);
   __builtin_amdgcn_sched_barrier(0);   // (these loads issue before the weights')
   WTile wk, wv, wo;
   wload_nt(a.Wp[k], H, D, wave, lane, wk);
@@ -274,6 +303,7 @@ __global__ __launch_bounds__(NT) void l1_pair_fwd_kernel(const L1Args a) {
   }
   if (a.snap && blockIdx.x == 0 && blockIdx.y == 0 && t == 0 && a.rng_live) *a.snap = rs;
   __syncthreads();
+  L1_ST(0, 1);
   // X' = X mask (input dropout), src/fusion.py:373
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
@@ -296,6 +326,7 @@ __global__ __launch_bounds__(NT) void l1_pair_fwd_kernel(const L1Args a) {
     for (int e = t; e < S * a.heads; e += NT)
       if (b0 + e / a.heads < B) a.maps[g][(int64_t)b0 * a.heads + e] = pp[e];
   __syncthreads();
+  L1_ST(0, 2);
   const int kq = lane >> 4, jl = lane & 15;
   f32x4 acc[NTL];
   // P_k = Drop(ReLU(X' W_k^T + b_k))  (projections[k], src/fusion.py:291-298)
@@ -314,6 +345,7 @@ __global__ __launch_bounds__(NT) void l1_pair_fwd_kernel(const L1Args a) {
     }
   }
   __syncthreads();
+  L1_ST(0, 3);
   // V = P_k W_v^T + b_v;  O = P' V per head (one key: attn @ v, src/attention.py:132)
   mma(ps, wv, acc, lane);
   const int hd = H / a.heads;
@@ -329,6 +361,7 @@ __global__ __launch_bounds__(NT) void l1_pair_fwd_kernel(const L1Args a) {
     }
   }
   __syncthreads();
+  L1_ST(0, 4);
   // A = O W_o^T + b_o  (out_proj, src/attention.py:140)
   mma(os, wo, acc, lane);
 #pragma unroll
@@ -340,6 +373,8 @@ __global__ __launch_bounds__(NT) void l1_pair_fwd_kernel(const L1Args a) {
       if (b0 + i < B && j < H) a.A[g][(int64_t)(b0 + i) * H + j] = acc[u][r] + bov[u];
     }
   }
+  L1_ST(0, 5);
+  L1_RT(0, 9);
 }
 
 // the small head operands (gating rows, classifier output rows, biases) staged in LDS at kernel
@@ -395,6 +430,8 @@ __global__ __launch_bounds__(NT) void l1_head_fwd_kernel(const L1Args a) {
         if (m == q) { pv[u][m].x += x.x; pv[u][m].y += x.y; pv[u][m].z += x.z; pv[u][m].w += x.w; }
     }
   }
+  L1_RT(1, 8);
+  L1_ST(1, 0);
   __builtin_amdgcn_sched_barrier(0);
   WTile w1;
   wload_nt(a.W1, H, H, wave, lane, w1);
@@ -406,6 +443,7 @@ __global__ __launch_bounds__(NT) void l1_head_fwd_kernel(const L1Args a) {
   }
   if (a.p > 0.f) keep_tile(rs, SITE_CLS, b0, H, a.p, kcl);
   __syncthreads();
+  L1_ST(1, 1);
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int e = pe[u];
@@ -422,6 +460,7 @@ __global__ __launch_bounds__(NT) void l1_head_fwd_kernel(const L1Args a) {
     }
   }
   __syncthreads();
+  L1_ST(1, 2);
   // gating scores (nn.Linear(H, 1), src/fusion.py:452-461): 16 lanes per dot
   {
     const int grp = t >> 4, l16 = t & 15;
@@ -434,6 +473,7 @@ __global__ __launch_bounds__(NT) void l1_head_fwd_kernel(const L1Args a) {
     }
   }
   __syncthreads();
+  L1_ST(1, 3);
   if (t < S) {
     float smx[L1_MAXM], w[L1_MAXM];
     adaptive(M, sc + t * M, msk + t * M, smx, w);
@@ -447,6 +487,7 @@ __global__ __launch_bounds__(NT) void l1_head_fwd_kernel(const L1Args a) {
     }
   }
   __syncthreads();
+  L1_ST(1, 4);
   // fused = sum_m w_m pooled_m (src/fusion.py:413-418), float4 per thread
   for (int e = t; e < S * h4; e += NT) {
     const int i = e / h4, c = 4 * (e - i * h4);
@@ -461,6 +502,7 @@ __global__ __launch_bounds__(NT) void l1_head_fwd_kernel(const L1Args a) {
   }
   zero_pad(fs, H);
   __syncthreads();
+  L1_ST(1, 5);
   // h1 = Drop(ReLU(fused W1^T + b1)) (classifier[0..2], src/fusion.py:323-328)
   f32x4 acc[NTL];
   mma(fs, w1, acc, lane);
@@ -479,6 +521,7 @@ __global__ __launch_bounds__(NT) void l1_head_fwd_kernel(const L1Args a) {
     }
   }
   __syncthreads();
+  L1_ST(1, 6);
   // logits = h1 W2^T + b2 (classifier[3])
   {
     const int grp = t >> 4, l16 = t & 15;
@@ -492,6 +535,8 @@ __global__ __launch_bounds__(NT) void l1_head_fwd_kernel(const L1Args a) {
   }
   // the live stream advances once per call (the pair kernel read it; the snapshot is saved)
   if (a.rng_advance && blockIdx.x == 0 && t == 0) a.rng_advance[1] += 1;
+  L1_ST(1, 7);
+  L1_RT(1, 9);
 }
 
 // ------------------------------------------------------------------------------ backward
@@ -527,10 +572,13 @@ __global__ __launch_bounds__(NT) void l1_head_bwd_kernel(const L1Args a) {
     const float4 v = *reinterpret_cast<const float4*>(a.pooled + ((int64_t)min(b0 + i, B - 1) * M + m) * H + c);
     *reinterpret_cast<float4*>(pl + mi * LD + c) = b0 + i < B ? v : make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  L1_RT(2, 8);
+  L1_ST(2, 0);
   __builtin_amdgcn_sched_barrier(0);
   WTile w1;
   wload_nn(a.W1, H, H, wave, lane, w1);
   __syncthreads();
+  L1_ST(2, 1);
   // dz1 = ReLU' Drop' (dlogits W2): the saved h1 is post-dropout, so h1 > 0 marks kept, active units
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
@@ -550,6 +598,7 @@ __global__ __launch_bounds__(NT) void l1_head_bwd_kernel(const L1Args a) {
   }
   zero_pad(zs, H);
   __syncthreads();
+  L1_ST(2, 2);
   // dfused = dz1 W1
   f32x4 acc[NTL];
   mma(zs, w1, acc, lane);
@@ -561,6 +610,7 @@ __global__ __launch_bounds__(NT) void l1_head_bwd_kernel(const L1Args a) {
     for (int r = 0; r < 4; ++r) dfs[(4 * kq + r) * LD + j] = acc[u][r];
   }
   __syncthreads();
+  L1_ST(2, 3);
   // d weights_m = dfused . pooled_m
   {
     const int grp = t >> 4, l16 = t & 15;
@@ -573,6 +623,7 @@ __global__ __launch_bounds__(NT) void l1_head_bwd_kernel(const L1Args a) {
     }
   }
   __syncthreads();
+  L1_ST(2, 4);
   // compute_adaptive_weights backward (renormalisation and the masked softmax)
   if (t < S) {
     const int i = t;
@@ -596,6 +647,7 @@ __global__ __launch_bounds__(NT) void l1_head_bwd_kernel(const L1Args a) {
     }
   }
   __syncthreads();
+  L1_ST(2, 5);
   // cvec_m = (w_m dfused + dscore_m gate_w_m) mask_m / n_m: the gradient of every entry of m's
   // aggregation list (P_m and the attended features of the pairs whose query is m), float4 per thread
   for (int e = t; e < M * S * h4; e += NT) {
@@ -608,6 +660,8 @@ __global__ __launch_bounds__(NT) void l1_head_bwd_kernel(const L1Args a) {
                                  (wm * dv.z + dsm * gv.z) * f, (wm * dv.w + dsm * gv.w) * f);
     *reinterpret_cast<float4*>(a.cvec + ((int64_t)(b0 + i) * M + m) * H + c) = v;
   }
+  L1_ST(2, 6);
+  L1_RT(2, 9);
 }
 
 // Backward of everything keyed by one modality m, per 16-sample tile (tile, m): for every pair
@@ -639,6 +693,8 @@ __global__ __launch_bounds__(NT) void l1_key_bwd_kernel(const L1Args a) {
 #pragma unroll
   for (int i = 0; i < NPK; ++i) load_tile(a.cvec + (int64_t)a.pq[gl[i]] * H, M * H, B, b0, H, cs[i]);
   if (t < S) msk[t] = b0 + t < B ? a.mask[(int64_t)min(b0 + t, B - 1) * M + m] : 0.f;
+  L1_RT(3, 8);
+  L1_ST(3, 0);
   __builtin_amdgcn_sched_barrier(0);
   WTile wo[NPK], wv[NPK];
 #pragma unroll
@@ -653,6 +709,7 @@ __global__ __launch_bounds__(NT) void l1_key_bwd_kernel(const L1Args a) {
   }
   if (a.p > 0.f && want_dx) keep_tile(rs, SITE_IN + m, b0, D, a.p, kin);
   __syncthreads();
+  L1_ST(3, 1);
   const int kq = lane >> 4, jl = lane & 15, hd = H / a.heads;
   f32x4 dp[NTL], acc[NTL];
 #pragma unroll
@@ -678,6 +735,7 @@ __global__ __launch_bounds__(NT) void l1_key_bwd_kernel(const L1Args a) {
     for (int u = 0; u < NTL; ++u) dp[u] += acc[u];
     if (i + 1 < NPK) __syncthreads();   // (vs is rewritten by the next pair)
   }
+  L1_ST(3, 2);
   // dZ_m, from the accumulator layout: lane (jl, kq), reg r = row 4 kq + r, column 16 (wave + 4u) + jl
   WTile wp;
   if (want_dx) wload_nn(a.Wp[m], D, H, wave, lane, wp);
@@ -699,6 +757,7 @@ __global__ __launch_bounds__(NT) void l1_key_bwd_kernel(const L1Args a) {
   }
   if (!want_dx) return;
   __syncthreads();
+  L1_ST(3, 3);
   // dX_m = (dZ_m W_m) mask_m input-dropout'
   mma(zs, wp, acc, lane);
 #pragma unroll
@@ -713,6 +772,8 @@ __global__ __launch_bounds__(NT) void l1_key_bwd_kernel(const L1Args a) {
       a.dx[m][(int64_t)(b0 + ii) * D + j] = v;
     }
   }
+  L1_ST(3, 4);
+  L1_RT(3, 9);
 }
 
 // One 32 x 32 tile of dW = G^T X (rows of G: the batch) per workgroup; wave w takes batch rows
@@ -737,6 +798,8 @@ __global__ __launch_bounds__(NT) void l1_wgrad_kernel(const L1WgArgs w) {
   while (ji + 1 < w.njobs && w.j[ji + 1].tile0 <= tile) ++ji;
   const L1WgJob J = w.j[ji];
   const int lt = tile - J.tile0, n0 = 32 * (lt / J.tiles_k), k0 = 32 * (lt % J.tiles_k);
+  L1_RT(4, 8);
+  L1_ST(4, 0);
   const int col = lane & 31, hf = lane >> 5;
   const int n = n0 + col, kk = k0 + col;
   f32x16 acc;
@@ -761,6 +824,7 @@ __global__ __launch_bounds__(NT) void l1_wgrad_kernel(const L1WgArgs w) {
       bsum += ga[s];
     }
   }
+  L1_ST(4, 1);
 #pragma unroll
   for (int r = 0; r < 16; ++r) red[wave][r][lane] = acc[r];
   const bool do_db = J.db && k0 == 0;
@@ -778,6 +842,8 @@ __global__ __launch_bounds__(NT) void l1_wgrad_kernel(const L1WgArgs w) {
     if (i < J.N && j < J.K) J.dW[(int64_t)i * J.K + j] = s;
   }
   if (do_db && t < 32 && n0 + t < J.N) J.db[n0 + t] = ((bred[0][t] + bred[1][t]) + bred[2][t]) + bred[3][t];
+  L1_ST(4, 2);
+  L1_RT(4, 9);
 }
 
 // the C2 shape: every hidden and input width 128 (compile-time tile guards)
@@ -863,6 +929,13 @@ hipError_t launch_l1_backward(const L1Args& a, const L1WgArgs& w, hipStream_t st
   mmf_launch(l1_wgrad_kernel, dim3((unsigned)(w.ntiles + zblocks)), dim3(NT), 0, st, w);
   return hipGetLastError();
 }
+
+#ifdef MMF_STAMPS
+extern "C" int mmf_l1_stamps_read(void* out, size_t bytes) {   // l1 kernels' phase stamps
+  if (bytes > sizeof(mmf::g_l1_stamps)) bytes = sizeof(mmf::g_l1_stamps);
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mmf::g_l1_stamps), bytes) == hipSuccess ? 0 : 3;
+}
+#endif
 
 }  // namespace mmf
 

@@ -159,15 +159,25 @@ class MultimodalFusionModel(nn.Module):
 
 # ----------------------------------------------------------------------------- flat buffers + bucketed all-reduce
 class FlatGradBuckets:
-    """All parameters of `modules` in one flat fp32 buffer, their gradients as views of a
-    second one, exchanged in buckets.
+    """All parameters of `modules` in one flat fp32 buffer and their gradients in a second
+    one, exchanged in buckets.
+
+    Gradients are autograd's own tensors, as with ``zero_grad(set_to_none=True)`` (the
+    reference's Lightning default): every parameter's ``.grad`` is None before a backward,
+    AccumulateGrad takes the backward's gradient tensor without a copy (the HIP operators
+    return one flat gradient buffer per call, sliced into views), and gathering copies the
+    gradients of a bucket into its span of the flat buffer with one multi-tensor copy
+    (``torch._foreach_copy_``, a launch or two for the whole bucket) and resets them to
+    None.  (Gradients kept as permanent views of the flat buffer instead cost one
+    in-place add launch per parameter and backward: 65 per HybridFusion step.)  Micro-
+    batches before the armed one accumulate in ``.grad`` as autograd does.
 
     Buckets follow `groups` (lists of parameters, e.g. [fusion params, encoder params]):
-    a bucket is all-reduced (sum, async) from the post-accumulate-grad hook of the last
-    of its parameters to finish accumulating -- while the rest of the backward still
-    runs -- when ``arm()`` was called for this backward.  ``finish()`` issues what is
-    left (parameters that received no gradient) and waits.  Tensors start on 256-byte
-    boundaries (the HIP kernels' 16-byte vector paths)."""
+    a bucket is gathered and all-reduced (sum, async) from the post-accumulate-grad hook of
+    the last of its parameters to finish accumulating -- while the rest of the backward
+    still runs -- when ``arm()`` was called for this backward.  ``finish()`` gathers and
+    issues what is left (parameters that received no gradient) and waits.  Tensors start
+    on 256-byte boundaries (the HIP kernels' 16-byte vector paths)."""
 
     ALIGN = 64
 
@@ -201,16 +211,24 @@ class FlatGradBuckets:
         self.params = params
         self.flat = torch.zeros(off, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(off, dtype=torch.float32, device=dev)
-        for o, p in zip(offs, params):
-            k = p.numel()
-            self.flat[o:o + k].copy_(p.detach().reshape(-1))
-            p.data = self.flat[o:o + k].view_as(p)
-            p.grad = self.grad[o:o + k].view_as(p)
+        # per bucket: its parameters and the views of their spans of the flat gradient
+        self._gviews: List[List[torch.Tensor]] = []
+        it = iter(offs)
+        for g in self.groups:
+            views = []
+            for p in g:
+                o = next(it)
+                self.flat[o:o + p.numel()].copy_(p.detach().reshape(-1))
+                p.data = self.flat[o:o + p.numel()].view_as(p)
+                p.grad = None
+                views.append(self.grad[o:o + p.numel()].view_as(p))
+            self._gviews.append(views)
         self.spans = spans
         self._bucket_of = {}
         for b, g in enumerate(self.groups):
             for p in g:
                 self._bucket_of[id(p)] = b
+        self._fresh = [True] * len(self.groups)    # the bucket's span holds no gradient yet
         self._pending = [0] * len(self.groups)
         self._works: List[Any] = [None] * len(self.groups)
         self._armed = False
@@ -221,8 +239,33 @@ class FlatGradBuckets:
         s, e = self.spans[b]
         return self.grad[s:e]
 
+    def gather(self, b: Optional[int] = None) -> None:
+        """Move the parameters' ``.grad`` tensors of bucket b (every bucket: None) into the flat
+        gradient -- a copy into a fresh span, an add otherwise -- and set them to None."""
+        for bb in (range(len(self.groups)) if b is None else (b,)):
+            dst, src, missing = [], [], []
+            for p, v in zip(self.groups[bb], self._gviews[bb]):
+                if p.grad is None:
+                    missing.append(v)
+                else:
+                    dst.append(v)
+                    src.append(p.grad)
+                    p.grad = None
+            if self._fresh[bb]:
+                if dst:
+                    torch._foreach_copy_(dst, src)
+                if missing:
+                    torch._foreach_zero_(missing)
+            elif dst:
+                torch._foreach_add_(dst, src)
+            self._fresh[bb] = False
+
     def zero_grad(self) -> None:
-        self.grad.zero_()
+        """Forget the flat gradient (the next gather copies instead of adding) and any
+        ungathered ``.grad``."""
+        self._fresh = [True] * len(self.groups)
+        for p in self.params:
+            p.grad = None
 
     def arm(self) -> None:
         """The next backward is the last before an optimizer step: exchange its buckets."""
@@ -239,14 +282,17 @@ class FlatGradBuckets:
             self._launch(b)
 
     def _launch(self, b: int) -> None:
+        self.gather(b)
         if self.world > 1:
             self._works[b] = torch.distributed.all_reduce(self.bucket(b), group=self.pg, async_op=True)
         else:
             self._works[b] = True
 
     def finish(self) -> None:
-        """Issue the buckets no hook issued, then wait for every exchange."""
+        """Gather and issue the buckets no hook issued, then wait for every exchange.  Unarmed
+        (a plain backward, no exchange): gather every bucket."""
         if not self._armed:
+            self.gather()
             return
         for b in range(len(self.groups)):
             if self._works[b] is None:

@@ -135,6 +135,7 @@ def test_flat_buckets_encoder_fusion_gloo_matches_full_batch(tmp_path):
         for mb in (slice(0, half), slice(half, None)):
             loss = _loss(model, {m: f[idx][mb] for m, f in feats.items()}, mask[idx][mb], labels[idx][mb])
             (loss / 4).backward()
+    fb.finish()      # (unarmed: gathers the accumulated .grad tensors into the flat gradient)
     full = fb.grad
     assert r["spans"] == fb.spans
     enc0 = fb.spans[1][0]
@@ -151,15 +152,30 @@ def test_flat_buckets_views_and_layout():
     for p in model.fusion_model.parameters():
         assert p.data.data_ptr() >= fb.flat.data_ptr()
         assert (p.data.data_ptr() - fb.flat.data_ptr()) % 256 == 0          # 256-byte aligned tensors
-        assert p.grad is not None and p.grad.data_ptr() >= fb.grad.data_ptr()
+        assert p.grad is None                                                 # set-to-none gradients
     feats, mask, labels = _batch()
     _loss(model, feats, mask, labels).backward()
-    # autograd accumulated in place into the flat buffer (no new .grad tensors)
-    for p in model.fusion_model.parameters():
-        assert fb.grad.data_ptr() <= p.grad.data_ptr() < fb.grad.data_ptr() + 4 * fb.numel
+    want = [p.grad.clone() for p in fb.params]
+    fb.finish()            # unarmed: gather (a copy into the fresh flat gradient), .grad -> None
+    assert all(p.grad is None for p in fb.params)
+    it = iter(want)
+    for views in fb._gviews:
+        for v in views:
+            assert torch.equal(v, next(it))
     assert fb.grad.abs().sum() > 0
+    # a second backward without zero_grad accumulates (an add into the flat gradient)
+    _loss(model, feats, mask, labels).backward()
+    fb.gather()
+    it = iter(want)
+    for views in fb._gviews:
+        for v in views:
+            assert torch.allclose(v, 2 * next(it), rtol=1e-6, atol=1e-7)
+    # after zero_grad the next gather copies; a parameter without a gradient reads zero
     fb.zero_grad()
-    assert fb.grad.abs().sum() == 0
+    fb.params[0].grad = torch.ones_like(fb.params[0])
+    fb.gather()
+    assert torch.equal(fb._gviews[0][0], torch.ones_like(fb.params[0]))
+    assert fb.grad[fb.params[0].numel():].abs().sum() == 0
     with pytest.raises(ValueError):
         FlatGradBuckets([[]])
 
