@@ -293,6 +293,21 @@ int mmf_adamw_step(int64_t n, float* param, const float* grad, float* exp_avg, f
                    int64_t* step_dev, float lr, float beta1, float beta2, float eps,
                    float weight_decay, float grad_scale, void* stream);
 
+/* One training step's forward, CrossEntropyLoss(label_smoothing) and backward of the
+ * reference's training_step (src/train.py:185-186, 303-313 over src/fusion.py:331-479): the
+ * results of mmf_hybrid_forward -> mmf_cross_entropy_ls(grad_scale = loss_scale) ->
+ * mmf_hybrid_backward(dlogits) in one call (logits, fusion_weights, loss_out[0] = mean loss,
+ * dlogits, every parameter gradient WRITTEN to grads, dx[m] when non-NULL), the dropout state
+ * advanced once.  The launch-lean L = 1 plan runs it in three launches (forward + loss + head
+ * backward in one); other plans issue the three calls.  sync: mmf_hybrid_train_sync_bytes(d)
+ * bytes, zeroed by the caller before the first call; every call leaves it zero. */
+size_t mmf_hybrid_train_sync_bytes(const mmf_hybrid_desc* d);
+int mmf_hybrid_train_step(const mmf_hybrid_desc* d, const mmf_hybrid_params* params, const float* const* x,
+                          const float* mask, const int64_t* labels, float label_smoothing, float loss_scale,
+                          uint64_t* rng_state, void* saved, void* workspace, void* sync, float* logits,
+                          float* fusion_weights, float* loss_out, float* dlogits, const mmf_hybrid_grads* grads,
+                          float* const* dx, void* stream);
+
 /* AdamW with the learning rate and an extra gradient factor read from device
  * scalars (lr_dev[0]; grad_coef_dev[0], may be NULL = 1), so a captured hipGraph
  * step follows an LR scheduler (CosineAnnealingLR, src/train.py:394-402) and

@@ -514,6 +514,52 @@ void fill_l1(L1Args& a, const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
   a.snap = s.rng;
 }
 
+
+// The L = 1 plan's backward arguments: the L1Args of the forward plus the gradient outputs, and
+// every weight gradient as a dW = G^T X job over the batch (l1_wgrad_kernel)
+void fill_l1_bwd(L1Args& a, L1WgArgs& wa, const mmf_hybrid_desc* d, const mmf_hybrid_params* W,
+                 const float* const* x, const float* mask, const Saved& s, const Ws& w, const float* dlogits,
+                 const mmf_hybrid_grads* G, float* const* dx) {
+  const int B = d->batch, M = d->num_modalities, H = d->hidden, C = d->num_classes;
+  fill_l1(a, d, W, x, mask, s);
+  a.dlogits = dlogits;
+  a.dz1 = w.dz1; a.cvec = w.cvec; a.dscore = w.dscore;
+  for (int g = 0; g < d->num_pairs; ++g) {
+    a.dV[g] = w.dOb[g];
+    a.dPk[g] = w.dU[g];
+  }
+  for (int m = 0; m < M; ++m) {
+    a.dZ[m] = w.dZ[m];
+    a.dx[m] = dx ? dx[m] : nullptr;
+  }
+  memset(&wa, 0, sizeof(wa));
+  wa.B = B;
+  auto job = [&](const float* Gp, int ldg, const float* Xp, int ldx, int N, int K, float* dW, float* db) {
+    if (!dW && !db) return;
+    L1WgJob& j = wa.j[wa.njobs++];
+    j.G = Gp; j.ldg = ldg; j.X = Xp; j.ldx = ldx; j.N = N; j.K = K; j.dW = dW; j.db = db;
+    j.tiles_k = (K + 31) / 32;
+    j.tile0 = wa.ntiles;
+    wa.ntiles += ((N + 31) / 32) * j.tiles_k;
+  };
+  auto zero = [&](float* p, int n) {
+    if (!p || n <= 0) return;
+    wa.z[wa.nz] = p; wa.zn[wa.nz] = n;
+    wa.zoff[wa.nz + 1] = wa.zoff[wa.nz] + (n + 4095) / 4096;
+    wa.nz++;
+  };
+  for (int m = 0; m < M; ++m)
+    job(w.dZ[m], H, s.Xd[m], d->in_dim[m], H, d->in_dim[m], G->proj[m].w, G->proj[m].b);
+  for (int g = 0; g < d->num_pairs; ++g) {
+    job(w.dOb[g], H, s.P[d->pair_k[g]], H, H, H, G->v[g].w, G->v[g].b);
+    job(w.cvec + (size_t)d->pair_q[g] * H, M * H, s.Ob[g], H, H, H, G->o[g].w, G->o[g].b);
+    // softmax over one key: no gradient reaches query_proj / key_proj (exact zeros)
+    zero(G->q[g].w, H * H); zero(G->q[g].b, H); zero(G->k[g].w, H * H); zero(G->k[g].b, H);
+  }
+  job(w.dz1, H, s.fused, H, H, H, G->cls1.w, G->cls1.b);
+  job(dlogits, C, s.h1, H, C, H, G->cls2.w, G->cls2.b);
+  for (int m = 0; m < M; ++m) job(w.dscore + m, M, s.pooled + (size_t)m * H, M * H, 1, H, G->gate[m].w, G->gate[m].b);
+}
 }  // namespace
 
 extern "C" {
@@ -834,46 +880,8 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
   layout_ws(d, bw, w);
   if (lean_l1(d, W, x)) {
     L1Args a;
-    fill_l1(a, d, W, x, mask, s);
-    a.dlogits = dlogits;
-    a.dz1 = w.dz1; a.cvec = w.cvec; a.dscore = w.dscore;
-    for (int g = 0; g < d->num_pairs; ++g) {
-      a.dV[g] = w.dOb[g];
-      a.dPk[g] = w.dU[g];
-    }
-    for (int m = 0; m < M; ++m) {
-      a.dZ[m] = w.dZ[m];
-      a.dx[m] = dx ? dx[m] : nullptr;
-    }
-    // every weight gradient: dW = G^T X over the batch (l1_wgrad_kernel)
     L1WgArgs wa;
-    memset(&wa, 0, sizeof(wa));
-    wa.B = B;
-    auto job = [&](const float* Gp, int ldg, const float* Xp, int ldx, int N, int K, float* dW, float* db) {
-      if (!dW && !db) return;
-      L1WgJob& j = wa.j[wa.njobs++];
-      j.G = Gp; j.ldg = ldg; j.X = Xp; j.ldx = ldx; j.N = N; j.K = K; j.dW = dW; j.db = db;
-      j.tiles_k = (K + 31) / 32;
-      j.tile0 = wa.ntiles;
-      wa.ntiles += ((N + 31) / 32) * j.tiles_k;
-    };
-    auto zero = [&](float* p, int n) {
-      if (!p || n <= 0) return;
-      wa.z[wa.nz] = p; wa.zn[wa.nz] = n;
-      wa.zoff[wa.nz + 1] = wa.zoff[wa.nz] + (n + 4095) / 4096;
-      wa.nz++;
-    };
-    for (int m = 0; m < M; ++m)
-      job(w.dZ[m], H, s.Xd[m], d->in_dim[m], H, d->in_dim[m], G->proj[m].w, G->proj[m].b);
-    for (int g = 0; g < d->num_pairs; ++g) {
-      job(w.dOb[g], H, s.P[d->pair_k[g]], H, H, H, G->v[g].w, G->v[g].b);
-      job(w.cvec + (size_t)d->pair_q[g] * H, M * H, s.Ob[g], H, H, H, G->o[g].w, G->o[g].b);
-      // softmax over one key: no gradient reaches query_proj / key_proj (exact zeros)
-      zero(G->q[g].w, H * H); zero(G->q[g].b, H); zero(G->k[g].w, H * H); zero(G->k[g].b, H);
-    }
-    job(w.dz1, H, s.fused, H, H, H, G->cls1.w, G->cls1.b);
-    job(dlogits, C, s.h1, H, C, H, G->cls2.w, G->cls2.b);
-    for (int m = 0; m < M; ++m) job(w.dscore + m, M, s.pooled + (size_t)m * H, M * H, 1, H, G->gate[m].w, G->gate[m].b);
+    fill_l1_bwd(a, wa, d, W, x, mask, s, w, dlogits, G, dx);
     STAGE_TRY("bwd.l1", launch_l1_backward(a, wa, st));
     return MMF_OK;
   }
@@ -1095,6 +1103,56 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
   STAGE_TRY("bwd.wgrad_gemm", launch_gemm(wp.jobs.data(), (int)wp.jobs.size(), MODE_KR, MODE_KR, p, rng, st));
   STAGE_TRY("bwd.wgrad_reduce", launch_reduce(wp.reds.data(), (int)wp.reds.size(), st));
   return MMF_OK;
+}
+
+size_t mmf_hybrid_train_sync_bytes(const mmf_hybrid_desc* d) {
+  if (check_hybrid(d) != MMF_OK) return 0;
+  const size_t tiles = ((size_t)d->batch + 15) / 16;   // one arrival count per 16-sample tile
+  return std::max<size_t>(256, (4 * tiles + 255) / 256 * 256);
+}
+
+int mmf_hybrid_train_step(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, const float* const* x,
+                          const float* mask, const int64_t* labels, float label_smoothing, float loss_scale,
+                          uint64_t* rng_state, void* saved, void* workspace, void* sync, float* logits,
+                          float* fusion_weights, float* loss_out, float* dlogits, const mmf_hybrid_grads* G,
+                          float* const* dx, void* stream) {
+  int rc = check_hybrid(d);
+  if (rc) return rc;
+  if (!W || !x || !mask || !labels || !saved || !workspace || !logits || !loss_out || !dlogits || !G)
+    return fail(MMF_EINVAL, "null argument");
+  if (sync && lean_l1(d, W, x)) {
+    MathScope math_(d->matmul_precision);
+    hipStream_t st = (hipStream_t)stream;
+    Bump bs(saved);
+    Saved s{};
+    layout_saved(d, bs, s);
+    Bump bw(workspace);
+    Ws w;
+    layout_ws(d, bw, w);
+    L1Args a;
+    L1WgArgs wa;
+    fill_l1_bwd(a, wa, d, W, x, mask, s, w, dlogits, G, dx);
+    a.rng_live = rng_state;
+    a.rng_advance = rng_state;
+    a.logits = logits;
+    a.weights_out = fusion_weights;
+    a.tile_cnt = static_cast<uint32_t*>(sync);
+    a.labels = labels;
+    a.ls_eps = label_smoothing;
+    a.loss_scale = loss_scale;
+    a.loss_rows = w.dfused;   // (B x H floats the L = 1 plan leaves unused)
+    a.dlogits_out = dlogits;
+    wa.loss_rows = w.dfused;
+    wa.loss = loss_out;
+    STAGE_TRY("train.l1", launch_l1_train(a, wa, st));
+    return MMF_OK;
+  }
+  rc = mmf_hybrid_forward(d, W, x, mask, rng_state, saved, logits, fusion_weights, nullptr, stream);
+  if (rc) return rc;
+  rc = mmf_cross_entropy_ls(d->batch, d->num_classes, logits, labels, label_smoothing, loss_scale, loss_out,
+                            dlogits, stream);
+  if (rc) return rc;
+  return mmf_hybrid_backward(d, W, x, mask, saved, dlogits, workspace, G, dx, stream);
 }
 
 }  // extern "C"

@@ -74,6 +74,26 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// The one-launch step hands P_k and A tiles from the pair workgroups to the last pair workgroup of
+// a tile (l1_fwd_loss_kernel) without fences: every handed-off element is stored write-through
+// (sc1, an agent-scope relaxed atomic store: the line leaves the producer's XCD L2), every storing
+// wave drains its stores (s_waitcnt vmcnt(0)) before the workgroup barrier behind which one lane
+// counts the tile's arrivals (agent-scope relaxed add), and every load of those bytes in the
+// consumer is a 16-B sc1 buffer load (L1 bypassed, served coherently): MI355X_MICROARCH.md
+// "Workgroup dispatch, XCD placement & inter-workgroup visibility", hand-off table row 1.  (An
+// agent-scope release + acquire per workgroup instead cost ~13 us per step: scripts/l1_stamps.py.)
+typedef __attribute__((address_space(1))) float gfloat;
+typedef __attribute__((address_space(1))) unsigned gu32;
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store((gfloat*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// 16-B sc1 load at byte offset `off` of a (wave-uniform) tensor base of `bytes` bytes
+__device__ __forceinline__ float4 ld_wt4(const float* base, uint32_t bytes, uint32_t off) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, bytes, 0x00020000);
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);   // aux 16: sc1
+  return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+}
+
 struct WTile {
   float4 w[NTL][KG];
 };
@@ -183,11 +203,19 @@ __device__ __forceinline__ void pprime_tile(const L1Args& a, const RngSnap& rs, 
 // 16 x N activation tile rows b0.. of a (B, ld) tensor into LDS (zeros past B); float4 loads from
 // clamped rows (unconditional: see wload_nt)
 __device__ __forceinline__ void load_tile(const float* __restrict__ src, int ld, int B, int b0, int N, float* dst) {
+  // (N <= 128: at most two float4 per thread, both loads issued before either LDS write -- a
+  // runtime-trip loop waited for each load in turn)
   const int n4 = N / 4;
-  for (int e = threadIdx.x; e < S * n4; e += NT) {
-    const int i = e / n4, c = e - i * n4;
-    const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)min(b0 + i, B - 1) * ld + 4 * c);
-    *reinterpret_cast<float4*>(dst + i * LD + 4 * c) = b0 + i < B ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 v[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int e = threadIdx.x + u * NT, i = min(e / n4, S - 1), c = e - (e / n4) * n4;
+    v[u] = *reinterpret_cast<const float4*>(src + (int64_t)min(b0 + i, B - 1) * ld + 4 * c);
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int e = threadIdx.x + u * NT, i = e / n4, c = e - i * n4;
+    if (i < S) *reinterpret_cast<float4*>(dst + i * LD + 4 * c) = b0 + i < B ? v[u] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
 
@@ -210,41 +238,61 @@ __device__ __forceinline__ void rowdots(const float* xs, const float* W, int ldw
   }
 }
 
-// adaptive weights of one sample (src/fusion.py:462-478; head.hip adaptive_fwd arithmetic)
-__device__ float adaptive(int M, const float* score, const float* mask, float* sm, float* w) {
+// adaptive weights of one sample (src/fusion.py:462-478; head.hip adaptive_fwd arithmetic).  The
+// loops run over the compile-time L1_MAXM with m < M guards, so sm / w stay in registers (with a
+// runtime trip count the private arrays went to scratch memory: 4.5 K cycles for three weights in
+// the round-4 stamps, scripts/l1_stamps.py); the padding terms add exact zeros.
+__device__ __forceinline__ float adaptive(int M, const float* score, const float* mask, float (&sm)[L1_MAXM],
+                                          float (&w)[L1_MAXM]) {
   float mx = -INFINITY;
-  for (int m = 0; m < M; ++m)
-    if (mask[m] > 0.f) mx = fmaxf(mx, score[m]);
+#pragma unroll
+  for (int m = 0; m < L1_MAXM; ++m)
+    if (m < M && mask[m] > 0.f) mx = fmaxf(mx, score[m]);
   float z = 0.f;
-  for (int m = 0; m < M; ++m) {
-    sm[m] = (mask[m] > 0.f) ? __expf(score[m] - mx) : 0.f;
+#pragma unroll
+  for (int m = 0; m < L1_MAXM; ++m) {
+    sm[m] = (m < M && mask[m] > 0.f) ? __expf(score[m] - mx) : 0.f;
     z += sm[m];
   }
   float sw = 0.f, ms = 0.f;
-  for (int m = 0; m < M; ++m) {
-    sm[m] = (mx == -INFINITY) ? 0.f : sm[m] / z;
-    w[m] = sm[m] * mask[m];
+#pragma unroll
+  for (int m = 0; m < L1_MAXM; ++m) {
+    const float mk = m < M ? mask[m] : 0.f;
+    sm[m] = (mx == -INFINITY || m >= M) ? 0.f : sm[m] / z;
+    w[m] = sm[m] * mk;
     sw += w[m];
-    ms += mask[m];
+    ms += mk;
   }
   if (sw > 0.f) {
     const float den = sw + 1e-8f;
-    for (int m = 0; m < M; ++m) w[m] = w[m] / den;
+#pragma unroll
+    for (int m = 0; m < L1_MAXM; ++m) w[m] = w[m] / den;
   } else {
-    for (int m = 0; m < M; ++m) w[m] = ms > 0.f ? mask[m] / (ms + 1e-8f) : 1.f / (float)M;
+#pragma unroll
+    for (int m = 0; m < L1_MAXM; ++m) w[m] = m < M ? (ms > 0.f ? mask[m] / (ms + 1e-8f) : 1.f / (float)M) : 0.f;
   }
   return sw;
 }
 
 // ------------------------------------------------------------------------------ forward
+struct PairLds {
+  float xs[S * LD], ps[S * LD], os[S * LD];
+  uint8_t kin[KB_BYTES], kpr[KB_BYTES];
+  float pp[S * 8];
+  float msk[S];
+};
+
+// One (tile, pair) of the forward: X'_k, P_k, V, O, A for the 16 samples of tile blockIdx.x and
+// pair blockIdx.y (stamps: kernel 0)
 template <int FH>
-__global__ __launch_bounds__(NT) void l1_pair_fwd_kernel(const L1Args a) {
-  __shared__ __attribute__((aligned(16))) float xs[S * LD];
-  __shared__ __attribute__((aligned(16))) float ps[S * LD];
-  __shared__ __attribute__((aligned(16))) float os[S * LD];
-  __shared__ uint8_t kin[KB_BYTES], kpr[KB_BYTES];
-  __shared__ float pp[S * 8];
-  __shared__ float msk[S];
+__device__ __forceinline__ RngSnap pair_fwd_tile(const L1Args& a, PairLds& L) {
+  float* xs = L.xs;
+  float* ps = L.ps;
+  float* os = L.os;
+  uint8_t* kin = L.kin;
+  uint8_t* kpr = L.kpr;
+  float* pp = L.pp;
+  float* msk = L.msk;
   const int g = blockIdx.y, b0 = blockIdx.x * S;
   const int k = a.pk[g], D = FH ? FH : a.D[k], H = FH ? FH : a.H, B = a.B;
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6) & 3;
@@ -341,7 +389,7 @@ __global__ __launch_bounds__(NT) void l1_pair_fwd_kernel(const L1Args a) {
       if (j >= H) v = 0.f;
       else if (a.p > 0.f) v = kept(kpr, b0, H, i, j) ? v * a.gscale : 0.f;
       ps[i * LD + j] = v;
-      if (desig && b0 + i < B && j < H) a.P[k][(int64_t)(b0 + i) * H + j] = v;
+      if (desig && b0 + i < B && j < H) st_wt(a.P[k] + (int64_t)(b0 + i) * H + j, v);   // (handed off)
     }
   }
   __syncthreads();
@@ -370,11 +418,18 @@ __global__ __launch_bounds__(NT) void l1_pair_fwd_kernel(const L1Args a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = 4 * kq + r;
-      if (b0 + i < B && j < H) a.A[g][(int64_t)(b0 + i) * H + j] = acc[u][r] + bov[u];
+      if (b0 + i < B && j < H) st_wt(a.A[g] + (int64_t)(b0 + i) * H + j, acc[u][r] + bov[u]);   // (handed off)
     }
   }
   L1_ST(0, 5);
   L1_RT(0, 9);
+  return rs;
+}
+
+template <int FH>
+__global__ __launch_bounds__(NT) void l1_pair_fwd_kernel(const L1Args a) {
+  __shared__ __attribute__((aligned(16))) PairLds L;
+  pair_fwd_tile<FH>(a, L);
 }
 
 // the small head operands (gating rows, classifier output rows, biases) staged in LDS at kernel
@@ -385,30 +440,59 @@ struct HeadSmall {
   float gb[L1_MAXM], b2[L1_MAXC];
 };
 __device__ __forceinline__ void stage_small(const L1Args& a, HeadSmall& hs) {
+  // every load issued before the first LDS write (unrolled over the compile-time maxima: a loop
+  // with a runtime trip count, or a per-lane pointer-table index, waited for each load in turn)
   const int t = threadIdx.x, M = a.M, H = a.H, C = a.C;
-  for (int e = t; e < M * H; e += NT) hs.gw[e] = a.gw[e / H][e % H];
-  for (int e = t; e < C * H; e += NT) hs.w2[e] = a.W2[e];
-  if (t < M) hs.gb[t] = a.gb[t][0];
-  if (t >= 64 && t < 64 + C) hs.b2[t - 64] = a.b2[t - 64];
+  float gv[L1_MAXM], wv[(L1_MAXC * L1_MAXH + NT - 1) / NT];
+#pragma unroll
+  for (int m = 0; m < L1_MAXM; ++m) gv[m] = (m < M && t < H) ? a.gw[m][min(t, H - 1)] : 0.f;
+#pragma unroll
+  for (int r = 0; r < (L1_MAXC * L1_MAXH + NT - 1) / NT; ++r) {
+    const int e = t + r * NT;
+    wv[r] = e < C * H ? a.W2[min(e, C * H - 1)] : 0.f;
+  }
+  const float gbv = t < M ? a.gb[min(t, M - 1)][0] : 0.f;
+  const float b2v = (t >= 64 && t < 64 + C) ? a.b2[min(max(t - 64, 0), C - 1)] : 0.f;
+#pragma unroll
+  for (int m = 0; m < L1_MAXM; ++m)
+    if (m < M && t < H) hs.gw[m * H + t] = gv[m];
+#pragma unroll
+  for (int r = 0; r < (L1_MAXC * L1_MAXH + NT - 1) / NT; ++r)
+    if (t + r * NT < C * H) hs.w2[t + r * NT] = wv[r];
+  if (t < M) hs.gb[t] = gbv;
+  if (t >= 64 && t < 64 + C) hs.b2[t - 64] = b2v;
 }
 
+// LDS of the head phases of one 16-sample tile: the forward, the loss, the backward
+struct HeadLds {
+  float pl[L1_MAXM * S * LD];     // pooled_m rows (forward output, backward operand)
+  float fs[S * LD];               // fused (forward) -> dz1 (backward)
+  float hs[S * LD];               // h1 (forward) -> dfused (backward)
+  HeadSmall sm;
+  uint8_t kcl[KB_BYTES];
+  float msk[S * L1_MAXM], sc[S * L1_MAXM], wt[S * L1_MAXM], dw[S * L1_MAXM], dsc[S * L1_MAXM];
+  float lg[S * L1_MAXC], dl[S * L1_MAXC];   // logits, dlogits rows
+};
+
+// Head forward of tile blockIdx.x (src/fusion.py:406-427, :429-479): pooled, gating scores,
+// adaptive weights, fused, h1 = Drop(ReLU(fused W1^T + b1)), logits.  Leaves pooled (pl), the
+// mask / score / weight rows, h1 (hs) and the logits (lg) in L.  rs: the call's rng snapshot.
 template <int FH>
-__global__ __launch_bounds__(NT) void l1_head_fwd_kernel(const L1Args a) {
-  __shared__ __attribute__((aligned(16))) float pl[L1_MAXM * S * LD];
-  __shared__ __attribute__((aligned(16))) float fs[S * LD];
-  __shared__ __attribute__((aligned(16))) float hs[S * LD];
-  __shared__ HeadSmall sm_;
-  __shared__ uint8_t kcl[KB_BYTES];
-  __shared__ float msk[S * L1_MAXM], sc[S * L1_MAXM], wt[S * L1_MAXM];
+__device__ __forceinline__ void head_fwd_tile(const L1Args& a, HeadLds& L, const RngSnap& rs, int kstamp) {
+  float* pl = L.pl;
+  float* fs = L.fs;
+  float* hs = L.hs;
+  HeadSmall& sm_ = L.sm;
+  uint8_t* kcl = L.kcl;
+  float *msk = L.msk, *sc = L.sc, *wt = L.wt;
   const int b0 = blockIdx.x * S;
   const int M = a.M, H = FH ? FH : a.H, B = a.B, C = a.C;
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6) & 3;
-  // loads, first-needed first: the mask rows and the rng snapshot, the attended and projected
-  // rows, the small operands, then W1
-  for (int e = t; e < S * M; e += NT) msk[e] = b0 + e / M < B ? a.mask[(int64_t)b0 * M + e] : 0.f;
-  RngSnap rs{0, 0};
-  if (a.p > 0.f) rs = *a.snap;
+  // loads, first-needed first: the mask rows, the attended and projected rows, the small
+  // operands, then W1
+  const float mrow = (t < S * M && b0 + t / M < B) ? a.mask[(int64_t)b0 * M + min(t, S * M - 1)] : 0.f;   // (S M <= NT)
   stage_small(a, sm_);
+  if (t < S * M) msk[t] = mrow;
   // pooled_m = mean(P_m, A_g for every pair with query m) * mask_m (src/fusion.py:406-408): each
   // thread sums its float4 of every list entry in registers
   const int h4 = H / 4;
@@ -418,20 +502,29 @@ __global__ __launch_bounds__(NT) void l1_head_fwd_kernel(const L1Args a) {
   for (int u = 0; u < 2; ++u) {
     const int e = t + u * NT, i = e / h4;
     pe[u] = (i < S) ? e : -1;
-    const int64_t row = (int64_t)min(b0 + min(i, S - 1), B - 1) * H + 4 * (e - i * h4);
+    // (the P_k / A tiles of the other pair workgroups: sc1 loads, see st_wt)
+    const uint32_t row = (uint32_t)(((int64_t)min(b0 + min(i, S - 1), B - 1) * H + 4 * (e - i * h4)) * 4);
+    const uint32_t nbytes = (uint32_t)B * (uint32_t)H * 4u;
 #pragma unroll
     for (int m = 0; m < L1_MAXM; ++m)
-      pv[u][m] = m < M ? *reinterpret_cast<const float4*>(a.P[m] + row) : make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int g = 0; g < a.npairs; ++g) {
-      const float4 x = *reinterpret_cast<const float4*>(a.A[g] + row);
-      const int q = a.pq[g];
+      pv[u][m] = m < M ? ld_wt4(a.P[m], nbytes, row) : make_float4(0.f, 0.f, 0.f, 0.f);
+    // (the pair list unrolled over L1_MAXP: every A load issued before the first add)
+    float4 xa[L1_MAXP];
+#pragma unroll
+    for (int g = 0; g < L1_MAXP; ++g)
+      xa[g] = g < a.npairs ? ld_wt4(a.A[g], nbytes, row) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int g = 0; g < L1_MAXP; ++g) {
+      const int q = g < a.npairs ? a.pq[g] : -1;   // (a guard, not a break: the loop stays unrolled)
 #pragma unroll
       for (int m = 0; m < L1_MAXM; ++m)
-        if (m == q) { pv[u][m].x += x.x; pv[u][m].y += x.y; pv[u][m].z += x.z; pv[u][m].w += x.w; }
+        if (m == q) { pv[u][m].x += xa[g].x; pv[u][m].y += xa[g].y; pv[u][m].z += xa[g].z; pv[u][m].w += xa[g].w; }
     }
   }
-  L1_RT(1, 8);
-  L1_ST(1, 0);
+  if (kstamp) {
+    L1_RT(1, 8);
+    L1_ST(1, 0);
+  }
   __builtin_amdgcn_sched_barrier(0);
   WTile w1;
   wload_nt(a.W1, H, H, wave, lane, w1);
@@ -443,7 +536,7 @@ __global__ __launch_bounds__(NT) void l1_head_fwd_kernel(const L1Args a) {
   }
   if (a.p > 0.f) keep_tile(rs, SITE_CLS, b0, H, a.p, kcl);
   __syncthreads();
-  L1_ST(1, 1);
+  if (kstamp) L1_ST(1, 1);
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int e = pe[u];
@@ -460,7 +553,7 @@ __global__ __launch_bounds__(NT) void l1_head_fwd_kernel(const L1Args a) {
     }
   }
   __syncthreads();
-  L1_ST(1, 2);
+  if (kstamp) L1_ST(1, 2);
   // gating scores (nn.Linear(H, 1), src/fusion.py:452-461): 16 lanes per dot
   {
     const int grp = t >> 4, l16 = t & 15;
@@ -473,11 +566,13 @@ __global__ __launch_bounds__(NT) void l1_head_fwd_kernel(const L1Args a) {
     }
   }
   __syncthreads();
-  L1_ST(1, 3);
+  if (kstamp) L1_ST(1, 3);
   if (t < S) {
     float smx[L1_MAXM], w[L1_MAXM];
     adaptive(M, sc + t * M, msk + t * M, smx, w);
-    for (int m = 0; m < M; ++m) {
+#pragma unroll
+    for (int m = 0; m < L1_MAXM; ++m) {
+      if (m >= M) break;
       wt[t * M + m] = w[m];
       if (b0 + t < B) {
         a.scores[(int64_t)(b0 + t) * M + m] = sc[t * M + m];
@@ -487,7 +582,7 @@ __global__ __launch_bounds__(NT) void l1_head_fwd_kernel(const L1Args a) {
     }
   }
   __syncthreads();
-  L1_ST(1, 4);
+  if (kstamp) L1_ST(1, 4);
   // fused = sum_m w_m pooled_m (src/fusion.py:413-418), float4 per thread
   for (int e = t; e < S * h4; e += NT) {
     const int i = e / h4, c = 4 * (e - i * h4);
@@ -502,7 +597,7 @@ __global__ __launch_bounds__(NT) void l1_head_fwd_kernel(const L1Args a) {
   }
   zero_pad(fs, H);
   __syncthreads();
-  L1_ST(1, 5);
+  if (kstamp) L1_ST(1, 5);
   // h1 = Drop(ReLU(fused W1^T + b1)) (classifier[0..2], src/fusion.py:323-328)
   f32x4 acc[NTL];
   mma(fs, w1, acc, lane);
@@ -521,7 +616,7 @@ __global__ __launch_bounds__(NT) void l1_head_fwd_kernel(const L1Args a) {
     }
   }
   __syncthreads();
-  L1_ST(1, 6);
+  if (kstamp) L1_ST(1, 6);
   // logits = h1 W2^T + b2 (classifier[3])
   {
     const int grp = t >> 4, l16 = t & 15;
@@ -530,78 +625,94 @@ __global__ __launch_bounds__(NT) void l1_head_fwd_kernel(const L1Args a) {
       float s = 0.f;
       for (int j = l16; j < H; j += 16) s += hs[i * LD + j] * sm_.w2[c * H + j];
       s = sum16(s);
-      if (l16 == 0 && b0 + i < B) a.logits[(int64_t)(b0 + i) * C + c] = s + sm_.b2[c];
+      if (l16 == 0) {
+        s += sm_.b2[c];
+        L.lg[i * C + c] = s;
+        if (b0 + i < B) a.logits[(int64_t)(b0 + i) * C + c] = s;
+      }
     }
   }
-  // the live stream advances once per call (the pair kernel read it; the snapshot is saved)
-  if (a.rng_advance && blockIdx.x == 0 && t == 0) a.rng_advance[1] += 1;
-  L1_ST(1, 7);
-  L1_RT(1, 9);
+  if (kstamp) {
+    L1_ST(1, 7);
+    L1_RT(1, 9);
+  }
 }
 
-// ------------------------------------------------------------------------------ backward
+// CrossEntropyLoss(label_smoothing) of the tile's samples (src/train.py:185-186, 310) with the
+// arithmetic of head.hip's cross_entropy_kernel: the per-sample loss into loss_rows (the batch
+// mean is taken in the wgrad launch, in the standalone kernel's order), dlogits = (softmax -
+// target) / B * loss_scale into L.dl and the caller's buffer
+__device__ __forceinline__ void loss_tile(const L1Args& a, HeadLds& L) {
+  const int t = threadIdx.x, b0 = blockIdx.x * S, C = a.C, B = a.B;
+  if (t < S) {
+    const int b = b0 + t;
+    const float eps = a.ls_eps;
+    if (b < B) {
+      const float* z = L.lg + t * C;
+      float mx = -INFINITY;
+      for (int c = 0; c < C; ++c) mx = fmaxf(mx, z[c]);
+      float se = 0.f, sz = 0.f;
+      for (int c = 0; c < C; ++c) { se += __expf(z[c] - mx); sz += z[c]; }
+      const float lse = mx + __logf(se);
+      const int y = (int)a.labels[b];
+      a.loss_rows[b] = (1.f - eps) * (lse - z[y]) + eps * (lse - sz / (float)C);
+      for (int c = 0; c < C; ++c) {
+        const float pc = __expf(z[c] - lse);
+        const float tgt = (c == y ? (1.f - eps) : 0.f) + eps / (float)C;
+        const float d = (pc - tgt) / (float)B * a.loss_scale;
+        L.dl[t * C + c] = d;
+        a.dlogits_out[(int64_t)b * C + c] = d;
+      }
+    } else {
+      for (int c = 0; c < C; ++c) L.dl[t * C + c] = 0.f;
+    }
+  }
+}
+
+// Head backward of tile blockIdx.x: dz1 = ReLU' Drop' (dlogits W2), dfused = dz1 W1, d weights,
+// compute_adaptive_weights backward, cvec_m (the gradient of every entry of m's aggregation list).
+// Reads dl, pl, hs (h1), msk / sc / wt and sm from L (the forward left them there, or the
+// standalone kernel staged them); w1n: this wave's W1 columns in y = x W form.
 template <int FH>
-__global__ __launch_bounds__(NT) void l1_head_bwd_kernel(const L1Args a) {
-  __shared__ __attribute__((aligned(16))) float pl[L1_MAXM * S * LD];
-  __shared__ __attribute__((aligned(16))) float zs[S * LD];
-  __shared__ __attribute__((aligned(16))) float dfs[S * LD];
-  __shared__ HeadSmall sm_;
-  __shared__ float dl[S * L1_MAXC];
-  __shared__ float msk[S * L1_MAXM], sc[S * L1_MAXM], wt[S * L1_MAXM], dw[S * L1_MAXM], dsc[S * L1_MAXM];
+__device__ __forceinline__ void head_bwd_tile(const L1Args& a, HeadLds& L, const WTile& w1n, int kstamp) {
+  float* pl = L.pl;
+  float* zs = L.fs;
+  float* dfs = L.hs;   // (h1 until the dz1 phase has read it)
+  HeadSmall& sm_ = L.sm;
+  float *dl = L.dl, *msk = L.msk, *sc = L.sc, *wt = L.wt, *dw = L.dw, *dsc = L.dsc;
   const int b0 = blockIdx.x * S;
   const int M = a.M, H = FH ? FH : a.H, B = a.B, C = a.C;
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6) & 3;
-  for (int e = t; e < S * C; e += NT) dl[e] = b0 + e / C < B ? a.dlogits[(int64_t)b0 * C + e] : 0.f;
-  for (int e = t; e < S * M; e += NT) {
-    const bool in = b0 + e / M < B;
-    msk[e] = in ? a.mask[(int64_t)b0 * M + e] : 0.f;
-    sc[e] = in ? a.scores[(int64_t)b0 * M + e] : 0.f;
-    wt[e] = in ? a.weights[(int64_t)b0 * M + e] : 0.f;
-  }
-  stage_small(a, sm_);
-  // this thread's h1 float4s (the ReLU / dropout gate of dz1)
   const int h4 = H / 4;
-  float4 hv[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int e = t + u * NT, i = e / h4;
-    hv[u] = *reinterpret_cast<const float4*>(a.h1 + (int64_t)min(b0 + min(i, S - 1), B - 1) * H + 4 * (e - i * h4));
-  }
-  for (int e = t; e < M * S * h4; e += NT) {
-    const int mi = e / h4, c = 4 * (e - mi * h4), m = mi / S, i = mi - m * S;
-    const float4 v = *reinterpret_cast<const float4*>(a.pooled + ((int64_t)min(b0 + i, B - 1) * M + m) * H + c);
-    *reinterpret_cast<float4*>(pl + mi * LD + c) = b0 + i < B ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  L1_RT(2, 8);
-  L1_ST(2, 0);
-  __builtin_amdgcn_sched_barrier(0);
-  WTile w1;
-  wload_nn(a.W1, H, H, wave, lane, w1);
-  __syncthreads();
-  L1_ST(2, 1);
   // dz1 = ReLU' Drop' (dlogits W2): the saved h1 is post-dropout, so h1 > 0 marks kept, active units
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int e = t + u * NT, i = e / h4, c = 4 * (e - i * h4);
     if (i >= S) continue;
-    float z[4];
-    const float hvv[4] = {hv[u].x, hv[u].y, hv[u].z, hv[u].w};
+    const float4 hv = *reinterpret_cast<const float4*>(L.hs + i * LD + c);
+    const float hvv[4] = {hv.x, hv.y, hv.z, hv.w};
+    // (the classes unrolled over L1_MAXC: one float4 W2 read per class, the same summation order)
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) {
-      float acc = 0.f;
-      for (int cc = 0; cc < C; ++cc) acc += dl[i * C + cc] * sm_.w2[cc * H + c + s4];
-      z[s4] = (b0 + i < B && hvv[s4] > 0.f) ? acc * a.gscale : 0.f;
+    for (int cc = 0; cc < L1_MAXC; ++cc) {
+      if (cc >= C) break;
+      const float dv = dl[i * C + cc];
+      const float4 w2 = *reinterpret_cast<const float4*>(sm_.w2 + cc * H + c);
+      acc[0] += dv * w2.x; acc[1] += dv * w2.y; acc[2] += dv * w2.z; acc[3] += dv * w2.w;
     }
+    float z[4];
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) z[s4] = (b0 + i < B && hvv[s4] > 0.f) ? acc[s4] * a.gscale : 0.f;
     const float4 zv = make_float4(z[0], z[1], z[2], z[3]);
     *reinterpret_cast<float4*>(zs + i * LD + c) = zv;
     if (b0 + i < B) *reinterpret_cast<float4*>(a.dz1 + (int64_t)(b0 + i) * H + c) = zv;
   }
   zero_pad(zs, H);
   __syncthreads();
-  L1_ST(2, 2);
+  if (kstamp) L1_ST(2, 2);
   // dfused = dz1 W1
   f32x4 acc[NTL];
-  mma(zs, w1, acc, lane);
+  mma(zs, w1n, acc, lane);
   const int kq = lane >> 4, jl = lane & 15;
 #pragma unroll
   for (int u = 0; u < NTL; ++u) {
@@ -610,7 +721,7 @@ __global__ __launch_bounds__(NT) void l1_head_bwd_kernel(const L1Args a) {
     for (int r = 0; r < 4; ++r) dfs[(4 * kq + r) * LD + j] = acc[u][r];
   }
   __syncthreads();
-  L1_ST(2, 3);
+  if (kstamp) L1_ST(2, 3);
   // d weights_m = dfused . pooled_m
   {
     const int grp = t >> 4, l16 = t & 15;
@@ -623,31 +734,44 @@ __global__ __launch_bounds__(NT) void l1_head_bwd_kernel(const L1Args a) {
     }
   }
   __syncthreads();
-  L1_ST(2, 4);
-  // compute_adaptive_weights backward (renormalisation and the masked softmax)
+  if (kstamp) L1_ST(2, 4);
+  // compute_adaptive_weights backward (renormalisation and the masked softmax); register arrays
+  // (compile-time L1_MAXM trip counts, m < M guards)
   if (t < S) {
     const int i = t;
-    float smx[L1_MAXM], w[L1_MAXM], ds[L1_MAXM];
+    float smx[L1_MAXM], w[L1_MAXM], ds[L1_MAXM], dsm[L1_MAXM], mk[L1_MAXM], dwv[L1_MAXM];
+#pragma unroll
+    for (int m = 0; m < L1_MAXM; ++m) {
+      mk[m] = m < M ? msk[i * M + m] : 0.f;
+      dwv[m] = m < M ? dw[i * M + m] : 0.f;
+    }
     const float sw = adaptive(M, sc + i * M, msk + i * M, smx, w);
-    for (int m = 0; m < M; ++m) ds[m] = 0.f;
+#pragma unroll
+    for (int m = 0; m < L1_MAXM; ++m) ds[m] = 0.f;
     if (sw > 0.f) {
       const float Sd = sw + 1e-8f;
       float dot = 0.f;
-      for (int m = 0; m < M; ++m) dot += dw[i * M + m] * smx[m] * msk[i * M + m];
-      float dsm[L1_MAXM], sdot = 0.f;
-      for (int m = 0; m < M; ++m) {
-        dsm[m] = (dw[i * M + m] / Sd - dot / (Sd * Sd)) * msk[i * M + m];
-        sdot += smx[m] * dsm[m];
+#pragma unroll
+      for (int m = 0; m < L1_MAXM; ++m)
+        if (m < M) dot += dwv[m] * smx[m] * mk[m];
+      float sdot = 0.f;
+#pragma unroll
+      for (int m = 0; m < L1_MAXM; ++m) {
+        dsm[m] = (dwv[m] / Sd - dot / (Sd * Sd)) * mk[m];
+        if (m < M) sdot += smx[m] * dsm[m];
       }
-      for (int m = 0; m < M; ++m) ds[m] = msk[i * M + m] > 0.f ? smx[m] * (dsm[m] - sdot) : 0.f;
+#pragma unroll
+      for (int m = 0; m < L1_MAXM; ++m) ds[m] = mk[m] > 0.f ? smx[m] * (dsm[m] - sdot) : 0.f;
     }
-    for (int m = 0; m < M; ++m) {
+#pragma unroll
+    for (int m = 0; m < L1_MAXM; ++m) {
+      if (m >= M) break;
       dsc[i * M + m] = ds[m];
       if (b0 + i < B) a.dscore[(int64_t)(b0 + i) * M + m] = ds[m];
     }
   }
   __syncthreads();
-  L1_ST(2, 5);
+  if (kstamp) L1_ST(2, 5);
   // cvec_m = (w_m dfused + dscore_m gate_w_m) mask_m / n_m: the gradient of every entry of m's
   // aggregation list (P_m and the attended features of the pairs whose query is m), float4 per thread
   for (int e = t; e < M * S * h4; e += NT) {
@@ -660,8 +784,93 @@ __global__ __launch_bounds__(NT) void l1_head_bwd_kernel(const L1Args a) {
                                  (wm * dv.z + dsm * gv.z) * f, (wm * dv.w + dsm * gv.w) * f);
     *reinterpret_cast<float4*>(a.cvec + ((int64_t)(b0 + i) * M + m) * H + c) = v;
   }
-  L1_ST(2, 6);
-  L1_RT(2, 9);
+  if (kstamp) {
+    L1_ST(2, 6);
+    L1_RT(2, 9);
+  }
+}
+
+template <int FH>
+__global__ __launch_bounds__(NT) void l1_head_fwd_kernel(const L1Args a) {
+  __shared__ __attribute__((aligned(16))) HeadLds L;
+  RngSnap rs{0, 0};
+  if (a.p > 0.f) rs = *a.snap;
+  head_fwd_tile<FH>(a, L, rs, 1);
+  // the live stream advances once per call (the pair kernel read it; the snapshot is saved)
+  if (a.rng_advance && blockIdx.x == 0 && threadIdx.x == 0) a.rng_advance[1] += 1;
+}
+
+// ------------------------------------------------------------------------------ backward
+template <int FH>
+__global__ __launch_bounds__(NT) void l1_head_bwd_kernel(const L1Args a) {
+  __shared__ __attribute__((aligned(16))) HeadLds L;
+  const int b0 = blockIdx.x * S;
+  const int M = a.M, H = FH ? FH : a.H, B = a.B, C = a.C;
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6) & 3;
+  // what the fused forward leaves in LDS, from the saved tensors
+  for (int e = t; e < S * C; e += NT) L.dl[e] = b0 + e / C < B ? a.dlogits[(int64_t)b0 * C + e] : 0.f;
+  for (int e = t; e < S * M; e += NT) {
+    const bool in = b0 + e / M < B;
+    L.msk[e] = in ? a.mask[(int64_t)b0 * M + e] : 0.f;
+    L.sc[e] = in ? a.scores[(int64_t)b0 * M + e] : 0.f;
+    L.wt[e] = in ? a.weights[(int64_t)b0 * M + e] : 0.f;
+  }
+  stage_small(a, L.sm);
+  load_tile(a.h1, H, B, b0, H, L.hs);
+  const int h4 = H / 4;
+  for (int e = t; e < M * S * h4; e += NT) {
+    const int mi = e / h4, c = 4 * (e - mi * h4), m = mi / S, i = mi - m * S;
+    const float4 v = *reinterpret_cast<const float4*>(a.pooled + ((int64_t)min(b0 + i, B - 1) * M + m) * H + c);
+    *reinterpret_cast<float4*>(L.pl + mi * LD + c) = b0 + i < B ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  L1_RT(2, 8);
+  L1_ST(2, 0);
+  __builtin_amdgcn_sched_barrier(0);
+  WTile w1;
+  wload_nn(a.W1, H, H, wave, lane, w1);
+  __syncthreads();
+  L1_ST(2, 1);
+  head_bwd_tile<FH>(a, L, w1, 1);
+}
+
+// The forward, the loss and the head backward of a training step in one launch over (tile,
+// pair): every workgroup runs its pair's forward (pair_fwd_tile); the last of a tile's pair
+// workgroups to finish (a per-tile arrival count; every workgroup's stores released before it
+// counts, the last one's loads acquired after) runs the tile's head forward, the cross-entropy
+// and the head backward, with the forward's intermediates still in LDS.  The count returns to 0
+// (the caller zeroes it once: mmf_hybrid_train_sync_bytes).  Replaces the pair / head-forward /
+// cross-entropy / head-backward launches of the split path (scripts/l1_stamps.py: 7.4 and 9 us
+// between them).
+template <int FH>
+__global__ __launch_bounds__(NT) void l1_fwd_loss_kernel(const L1Args a) {
+  // (LDS over 80 KB: one workgroup per CU, the residency the hand-off protocol was measured at)
+  __shared__ __attribute__((aligned(16))) union Lds { PairLds p; HeadLds h; char pad[82 * 1024]; } L;
+  __shared__ int last;
+  const RngSnap rs = pair_fwd_tile<FH>(a, L.p);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
+  __syncthreads();
+  L1_ST(0, 6);
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add((gu32*)(a.tile_cnt + blockIdx.x), 1u, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(a.npairs - 1);
+  __syncthreads();
+  L1_ST(0, 7);
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (keeps the sc1 loads behind the count)
+  if (threadIdx.x == 0)   // every pair workgroup of this tile has counted: back to 0 for the next call
+    __hip_atomic_store((gu32*)(a.tile_cnt + blockIdx.x), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int H = FH ? FH : a.H;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) & 3;
+  head_fwd_tile<FH>(a, L.h, rs, 1);
+  WTile w1n;
+  wload_nn(a.W1, H, H, wave, lane, w1n);   // (in flight through the loss)
+  __syncthreads();
+  loss_tile(a, L.h);
+  __syncthreads();
+  L1_RT(2, 8);
+  L1_ST(2, 0);
+  L1_ST(2, 1);
+  head_bwd_tile<FH>(a, L.h, w1n, 1);
 }
 
 // Backward of everything keyed by one modality m, per 16-sample tile (tile, m): for every pair
@@ -755,6 +964,8 @@ __global__ __launch_bounds__(NT) void l1_key_bwd_kernel(const L1Args a) {
       zs[ii * LD + j] = z;
     }
   }
+  // (launch_l1_train: the live stream advances here, after every forward workgroup has read it)
+  if (a.rng_advance && blockIdx.x == 0 && blockIdx.y == 0 && t == 0) a.rng_advance[1] += 1;
   if (!want_dx) return;
   __syncthreads();
   L1_ST(3, 3);
@@ -785,6 +996,20 @@ __global__ __launch_bounds__(NT) void l1_wgrad_kernel(const L1WgArgs w) {
   __shared__ float bred[4][32];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   int tile = blockIdx.x;
+  if (w.loss && tile == gridDim.x - 1) {
+    // the batch-mean loss in cross_entropy_kernel's order: per-thread strided sums, then a tree
+    __shared__ float lred[NT];
+    float acc = 0.f;
+    for (int i = t; i < w.B; i += NT) acc += w.loss_rows[i];
+    lred[t] = acc;
+    __syncthreads();
+    for (int s = NT / 2; s > 0; s >>= 1) {
+      if (t < s) lred[t] += lred[t + s];
+      __syncthreads();
+    }
+    if (t == 0) w.loss[0] = lred[0] / (float)w.B;
+    return;
+  }
   if (tile >= w.ntiles) {
     const int zb = tile - w.ntiles;
     int i = 0;
@@ -927,6 +1152,66 @@ hipError_t launch_l1_backward(const L1Args& a, const L1WgArgs& w, hipStream_t st
   for (int i = 0; i < w.nz; ++i) by += 4.0 * w.zn[i];
   ProfLaunch prof_(st, "l1_wgrad_kernel", fl, by);
   mmf_launch(l1_wgrad_kernel, dim3((unsigned)(w.ntiles + zblocks)), dim3(NT), 0, st, w);
+  return hipGetLastError();
+}
+
+hipError_t launch_l1_train(const L1Args& a, const L1WgArgs& w, hipStream_t st) {
+  if (a.M > L1_MAXM || a.npairs > L1_MAXP || a.H > L1_MAXH || a.H % 4 != 0 || a.C > L1_MAXC || a.heads > 8)
+    return hipErrorInvalidValue;
+  if (a.npairs != a.M * (a.M - 1) || a.M < 2 || !a.tile_cnt || !a.labels || !a.loss_rows || !a.dlogits_out)
+    return hipErrorInvalidValue;
+  for (int m = 0; m < a.M; ++m)
+    if (a.D[m] > L1_MAXD || a.D[m] % 4 != 0) return hipErrorInvalidValue;
+  const unsigned tiles = (unsigned)((a.B + S - 1) / S);
+  const double B = a.B, H = a.H;
+  const bool full = l1_full(a);
+  hipError_t e;
+  {
+    double fl = 2.0 * B * H * (H + a.C) + 4.0 * a.M * B * H + 2.0 * B * H * (H + a.C);
+    double by = 4.0 * (B * ((a.M + a.npairs) * H + a.M * H + 2 * H + a.C) + 2.0 * H * (H + a.C));
+    for (int g = 0; g < a.npairs; ++g) {
+      const double D = a.D[a.pk[g]];
+      fl += 2.0 * B * H * (D + 2.0 * H);
+      by += 4.0 * (B * (D + 2.0 * H) + H * (D + 2.0 * H));
+    }
+    L1Args af = a;
+    af.rng_advance = nullptr;   // (advanced by the key-modality backward launch)
+    ProfLaunch prof_(st, full ? "l1_fwd_loss_kernel<128>" : "l1_fwd_loss_kernel<0>", fl, by);
+    if (full) mmf_launch(l1_fwd_loss_kernel<128>, dim3(tiles, a.npairs), dim3(NT), 0, st, af);
+    else mmf_launch(l1_fwd_loss_kernel<0>, dim3(tiles, a.npairs), dim3(NT), 0, st, af);
+  }
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  {
+    double fl = 0.0, by = 0.0;
+    for (int m = 0; m < a.M; ++m) {
+      fl += a.dx[m] ? 2.0 * B * H * a.D[m] : 0.0;
+      by += 4.0 * (B * H * 2 + (a.dx[m] ? B * a.D[m] + H * a.D[m] : 0.0));
+    }
+    fl += 4.0 * B * H * H * a.npairs;
+    by += 4.0 * a.npairs * (2.0 * B * H + 2.0 * H * H);
+    const int npk = a.npairs / a.M;
+    ProfLaunch prof_(st, full ? "l1_key_bwd_kernel<128>" : "l1_key_bwd_kernel<0>", fl, by);
+    const dim3 grid(tiles, a.M);
+#define L1_KEY(FH)                                                                     \
+    switch (npk) {                                                                     \
+      case 1: mmf_launch(l1_key_bwd_kernel<FH, 1>, grid, dim3(NT), 0, st, a); break;   \
+      case 2: mmf_launch(l1_key_bwd_kernel<FH, 2>, grid, dim3(NT), 0, st, a); break;   \
+      default: mmf_launch(l1_key_bwd_kernel<FH, 3>, grid, dim3(NT), 0, st, a); break;  \
+    }
+    if (full) { L1_KEY(128) } else { L1_KEY(0) }
+#undef L1_KEY
+  }
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  double fl = 0.0, by = 0.0;
+  for (int i = 0; i < w.njobs; ++i) {
+    const L1WgJob& J = w.j[i];
+    fl += 2.0 * B * J.N * J.K;
+    by += 4.0 * (B * (J.N + J.K) + (double)J.N * J.K);
+  }
+  const int zblocks = w.nz ? w.zoff[w.nz] : 0;
+  for (int i = 0; i < w.nz; ++i) by += 4.0 * w.zn[i];
+  ProfLaunch prof_(st, "l1_wgrad_kernel", fl, by);
+  mmf_launch(l1_wgrad_kernel, dim3((unsigned)(w.ntiles + zblocks + (w.loss ? 1 : 0))), dim3(NT), 0, st, w);
   return hipGetLastError();
 }
 

@@ -554,6 +554,12 @@ struct L1Args {
   const float* dlogits;
   float *dz1, *cvec, *dscore;
   float *dV[L1_MAXP], *dPk[L1_MAXP], *dZ[L1_MAXM], *dx[L1_MAXM];
+  // the one-launch forward + loss + head backward of a training step (launch_l1_train)
+  uint32_t* tile_cnt;                 // per-tile arrival counts (zero between calls)
+  const int64_t* labels;
+  float ls_eps, loss_scale;           // label smoothing; dlogits scale (1 / accumulation steps)
+  float* loss_rows;                   // (B) per-sample loss
+  float* dlogits_out;                 // (B, C)
 };
 constexpr int L1_MAXJOBS = 40, L1_MAXZ = 48;
 struct L1WgJob {                      // dW (N x K) = G^T X over B rows; db = column sums of G
@@ -564,8 +570,11 @@ struct L1WgArgs {
   L1WgJob j[L1_MAXJOBS];
   int32_t njobs, B, ntiles;
   float* z[L1_MAXZ]; int32_t zn[L1_MAXZ]; int32_t zoff[L1_MAXZ + 1]; int32_t nz;
+  const float* loss_rows; float* loss;   // optional: loss = mean of loss_rows (one extra workgroup)
 };
 hipError_t launch_l1_forward(const L1Args& a, hipStream_t st);
 hipError_t launch_l1_backward(const L1Args& a, const L1WgArgs& w, hipStream_t st);
+// forward + cross-entropy + backward of a training step: three launches
+hipError_t launch_l1_train(const L1Args& a, const L1WgArgs& w, hipStream_t st);
 
 }  // namespace mmf

@@ -44,7 +44,8 @@ LIB_PATH = os.environ.get("MMF_LIB_PATH") or os.path.join(_HERE, "csrc", "libmmf
 
 EXPORTED_SYMBOLS = (
     "mmf_hybrid_saved_bytes", "mmf_hybrid_workspace_bytes", "mmf_hybrid_forward",
-    "mmf_hybrid_backward", "mmf_adaptive_weights_workspace_bytes", "mmf_adaptive_weights",
+    "mmf_hybrid_backward", "mmf_hybrid_train_sync_bytes", "mmf_hybrid_train_step",
+    "mmf_adaptive_weights_workspace_bytes", "mmf_adaptive_weights",
     "mmf_adaptive_weights_backward",
     "mmf_cma_saved_bytes", "mmf_cma_workspace_bytes", "mmf_cma_forward", "mmf_cma_backward",
     "mmf_cross_entropy_ls", "mmf_adamw_step", "mmf_adamw_step_dev", "mmf_grad_clip_workspace_bytes",
@@ -126,6 +127,11 @@ def lib() -> ctypes.CDLL:
     L.mmf_hybrid_backward.argtypes = [POINTER(HybridDesc), POINTER(HybridParams), vp, vp, vp, vp,
                                       vp, POINTER(HybridGrads), vp, vp]
     L.mmf_hybrid_backward.restype = c_int32
+    L.mmf_hybrid_train_sync_bytes.argtypes = [POINTER(HybridDesc)]
+    L.mmf_hybrid_train_sync_bytes.restype = sz
+    L.mmf_hybrid_train_step.argtypes = [POINTER(HybridDesc), POINTER(HybridParams), vp, vp, vp, c_float, c_float,
+                                        vp, vp, vp, vp, vp, vp, vp, vp, POINTER(HybridGrads), vp, vp]
+    L.mmf_hybrid_train_step.restype = c_int32
     L.mmf_adaptive_weights_workspace_bytes.argtypes = [c_int32, c_int32, c_int32]
     L.mmf_adaptive_weights_workspace_bytes.restype = sz
     L.mmf_adaptive_weights.argtypes = [c_int32, c_int32, c_int32, vp, vp, vp, vp, vp, vp]

@@ -142,6 +142,8 @@ class HybridTrainStep:
         self.clip_ws = torch.empty(L.mmf_grad_clip_workspace_bytes(), dtype=torch.uint8, device=dev)
         self.saved = torch.empty(L.mmf_hybrid_saved_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
         self.ws = torch.empty(L.mmf_hybrid_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
+        # the one-call step's arrival counts: zero once, every call leaves them zero
+        self.sync = torch.zeros(L.mmf_hybrid_train_sync_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
         self.logits = torch.empty(nb, d.num_classes, dtype=torch.float32, device=dev)
         self.fw = torch.empty(nb, d.num_modalities, dtype=torch.float32, device=dev)
         self.dlogits = torch.empty_like(self.logits)
@@ -191,28 +193,24 @@ class HybridTrainStep:
 
     # ---------------------------------------------------------------- stages
     def forward_backward(self) -> None:
+        """Per micro-batch: forward -> CE (loss / accumulate) -> backward in one library call
+        (mmf_hybrid_train_step: three launches on the L = 1 plan), then the gradient added into
+        the accumulated one."""
         L = _nat.lib()
         d = self.plan.desc
         st = _nat.stream_ptr(self.dev)
         C, M, b = d.num_classes, d.num_modalities, self.micro
         for i in range(self.accumulate):
-            logits = self.logits[i * b:]
-            rc = L.mmf_hybrid_forward(ctypes.byref(d), ctypes.byref(self.pstruct),
-                                      ctypes.cast(self.xarr[i], ctypes.c_void_p), self.mask[i * b:].data_ptr(),
-                                      self.rng.data_ptr(), self.saved.data_ptr(),
-                                      logits.data_ptr(), self.fw[i * b:].data_ptr(), None, st)
-            _nat.check(rc, "train forward")
-            rc = L.mmf_cross_entropy_ls(b, C, logits.data_ptr(), self.labels[i * b:].data_ptr(),
-                                        self.smoothing, 1.0 / self.accumulate, self.losses[i:].data_ptr(),
-                                        self.dlogits[i * b:].data_ptr(), st)
-            _nat.check(rc, "train cross-entropy")
             g = self.gstruct if i == 0 else self.gstruct_mb
-            rc = L.mmf_hybrid_backward(ctypes.byref(d), ctypes.byref(self.pstruct),
-                                       ctypes.cast(self.xarr[i], ctypes.c_void_p), self.mask[i * b:].data_ptr(),
-                                       self.saved.data_ptr(), self.dlogits[i * b:].data_ptr(), self.ws.data_ptr(),
-                                       ctypes.byref(g),
-                                       ctypes.cast(self.dxarr[i], ctypes.c_void_p) if self.dxarr else None, st)
-            _nat.check(rc, "train backward")
+            rc = L.mmf_hybrid_train_step(ctypes.byref(d), ctypes.byref(self.pstruct),
+                                         ctypes.cast(self.xarr[i], ctypes.c_void_p), self.mask[i * b:].data_ptr(),
+                                         self.labels[i * b:].data_ptr(), self.smoothing, 1.0 / self.accumulate,
+                                         self.rng.data_ptr(), self.saved.data_ptr(), self.ws.data_ptr(),
+                                         self.sync.data_ptr(), self.logits[i * b:].data_ptr(),
+                                         self.fw[i * b:].data_ptr(), self.losses[i:].data_ptr(),
+                                         self.dlogits[i * b:].data_ptr(), ctypes.byref(g),
+                                         ctypes.cast(self.dxarr[i], ctypes.c_void_p) if self.dxarr else None, st)
+            _nat.check(rc, "train step (forward, cross-entropy, backward)")
             if i > 0:
                 rc = L.mmf_grad_accumulate(self.grad.numel(), self.grad_mb.data_ptr(), self.grad.data_ptr(), st)
                 _nat.check(rc, "gradient accumulation")

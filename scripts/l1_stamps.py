@@ -29,9 +29,11 @@ from train_step import HybridTrainStep  # noqa: E402
 import bench  # noqa: E402
 
 KERNELS = [
-    ("l1_pair_fwd", ["loads+keep+P'", "X'", "P = relu(X'Wk)", "O = P'(PWv)", "A = OWo + store"]),
-    ("l1_head_fwd", ["loads+keep", "pooled", "gating", "adaptive", "fused", "h1", "logits"]),
-    ("l1_head_bwd", ["loads", "dz1", "dfused", "dw", "adaptive bwd", "cvec"]),
+    ("l1_pair_fwd (l1_fwd_loss: pair part)", ["loads+keep+P'", "X'", "P = relu(X'Wk)", "O = P'(PWv)", "A = OWo + store",
+                                              "store drain", "arrival count"]),
+    ("l1_head_fwd (last pair workgroup of a tile)", ["loads+keep", "pooled", "gating", "adaptive", "fused", "h1",
+                                                     "logits"]),
+    ("l1_head_bwd (loss + head backward)", ["loss", "dz1", "dfused", "dw", "adaptive bwd", "cvec"]),
     ("l1_key_bwd", ["loads+keep", "pairs dO/dV/dP", "dZ", "dX"]),
     ("l1_wgrad", ["main loop", "reduce + store"]),
 ]
@@ -55,13 +57,17 @@ def main():
     buf = np.zeros((5, 1024, 10), dtype=np.uint64)
     assert L.mmf_l1_stamps_read(buf.ctypes.data, buf.nbytes) == 0
     tiles = (w["B"] + 15) // 16
-    nwg = [tiles * 6, tiles, tiles, tiles * 3, None]
+    nwg = [tiles * 6, None, None, tiles * 3, None]
     out = {"kernels": {}}
     spans = []
+    t_first = int(buf[0, :tiles * 6, 8].astype(np.int64).min())   # this replay's first pair workgroup
     for k, (kn, ph) in enumerate(KERNELS):
         b = buf[k].astype(np.int64)
-        n = nwg[k] if nwg[k] is not None else int((b[:, 8] > 0).sum())
+        n = nwg[k] if nwg[k] is not None else int(len(b))
         b = b[:n]
+        # (the one-launch step's head phases are stamped by whichever pair workgroup finished its
+        # tile last, at that workgroup's slot: keep the rows of this replay)
+        b = b[(b[:, 8] >= t_first) & (b[:, 9] > 0)]
         if k == 4:   # zero-fill workgroups carry only the start stamps
             b = b[b[:, 2] > 0]
         st = b[:, :len(ph) + 1]

@@ -40,9 +40,8 @@ def env(pkg_on_path):
 EXPECT = {   # the benchmarked kernel instantiations (bench.py's kernel table names them)
     "c2": ["mask_dropout_rows_kernel", "attn_pool_fwd_lean<32, 0, true, false, true>",
            "attn_pool_bwd_fused_lean<32, 0, false>", "gemm_wsr_kernel<0>"],
-    # the launch-lean single-key step (csrc/l1.hip)
-    "c2_l1": ["l1_pair_fwd_kernel<128>", "l1_head_fwd_kernel<128>", "l1_head_bwd_kernel<128>",
-              "l1_key_bwd_kernel<128>", "l1_wgrad_kernel"],
+    # the launch-lean single-key step (csrc/l1.hip): forward + loss + head backward in one launch
+    "c2_l1": ["l1_fwd_loss_kernel<128>", "l1_key_bwd_kernel<128>", "l1_wgrad_kernel"],
 }
 
 

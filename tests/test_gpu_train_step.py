@@ -191,3 +191,61 @@ def test_accumulate_rejects_uneven_micro_batches(mods):
     with pytest.raises(ValueError, match="equal micro-batches"):
         train_step.HybridTrainStep(_model(fusion, 0.0).cuda(), [f.cuda() for f in feats], mask.cuda(), labels.cuda(),
                                    accumulate=3)
+
+
+def _three_calls(st, nat):
+    """The split path the one-call step replaces: mmf_hybrid_forward -> mmf_cross_entropy_ls ->
+    mmf_hybrid_backward on the step's own buffers (accumulate = 1)."""
+    import ctypes
+    L = nat.lib()
+    d = st.plan.desc
+    s = nat.stream_ptr(st.dev)
+    rc = L.mmf_hybrid_forward(ctypes.byref(d), ctypes.byref(st.pstruct), ctypes.cast(st.xarr[0], ctypes.c_void_p),
+                              st.mask.data_ptr(), st.rng.data_ptr(), st.saved.data_ptr(), st.logits.data_ptr(),
+                              st.fw.data_ptr(), None, s)
+    nat.check(rc, "forward")
+    rc = L.mmf_cross_entropy_ls(st.mask.size(0), d.num_classes, st.logits.data_ptr(), st.labels.data_ptr(),
+                                st.smoothing, 1.0, st.losses.data_ptr(), st.dlogits.data_ptr(), s)
+    nat.check(rc, "cross-entropy")
+    rc = L.mmf_hybrid_backward(ctypes.byref(d), ctypes.byref(st.pstruct), ctypes.cast(st.xarr[0], ctypes.c_void_p),
+                               st.mask.data_ptr(), st.saved.data_ptr(), st.dlogits.data_ptr(), st.ws.data_ptr(),
+                               ctypes.byref(st.gstruct), ctypes.cast(st.dxarr[0], ctypes.c_void_p), s)
+    nat.check(rc, "backward")
+
+
+@pytest.mark.parametrize("seq", [False, True])
+def test_one_call_train_step_matches_three_calls(mods, seq):
+    """mmf_hybrid_train_step (HybridTrainStep's forward + CE + backward: on the 2-D single-key plan
+    one launch for the forward, the loss and the head backward, a per-tile arrival count handing
+    each tile to the last of its pair workgroups) against forward -> cross-entropy -> backward as
+    three calls, train mode with dropout, two consecutive steps: the same logits, loss, dlogits,
+    fusion weights, parameter and input gradients bit for bit, the dropout stream advanced once
+    per step, and the arrival counts back at zero."""
+    import mmf_native as nat
+    fusion, train_step = mods
+    feats, mask, labels = _batch(11)
+    if not seq:
+        feats = [f[:, 0] for f in feats]
+    runs = []
+    for split in (False, True):
+        model = _model(fusion, 0.3).cuda()
+        model._rng_state.copy_(torch.tensor([0xC0FFEE, 5], dtype=torch.int64))
+        st = train_step.HybridTrainStep(model, [f.cuda() for f in feats], mask.cuda(), labels.cuda())
+        nat.profile_begin()
+        outs = []
+        for _ in range(2):
+            _three_calls(st, nat) if split else st.forward_backward()
+            torch.cuda.synchronize()
+            outs.append([t.detach().cpu().clone() for t in (st.logits, st.losses, st.dlogits, st.fw, st.grad,
+                                                            *st.dx, model._rng_state)])
+        _, launches = nat.profile_end()
+        names = [k for _, k, *_ in launches]
+        if not split and not seq:
+            assert any(k.startswith("l1_fwd_loss_kernel") for k in names), names
+            assert not any(k.startswith("cross_entropy_kernel") or k.startswith("l1_head") for k in names), names
+            assert int(st.sync.count_nonzero()) == 0
+        runs.append(outs)
+    for step_a, step_b in zip(*runs):
+        for a, b in zip(step_a, step_b):
+            assert torch.equal(a, b)
+    assert int(runs[0][1][-1][1]) == 7   # offset 5 -> 7 after two steps
