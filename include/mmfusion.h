@@ -300,13 +300,18 @@ int mmf_adamw_step(int64_t n, float* param, const float* grad, float* exp_avg, f
  * dlogits, every parameter gradient WRITTEN to grads, dx[m] when non-NULL), the dropout state
  * advanced once.  The launch-lean L = 1 plan runs it in three launches (forward + loss + head
  * backward in one); other plans issue the three calls.  sync: mmf_hybrid_train_sync_bytes(d)
- * bytes, zeroed by the caller before the first call; every call leaves it zero. */
+ * bytes, zeroed by the caller before the first call; every call leaves it zero.
+ * clip_partial (optional, mmf_grad_clip_workspace_bytes()): also write the squared-norm partials of
+ * the gradient just written -- grad_flat (16-byte aligned, grad_n floats) is the buffer `grads`
+ * points into -- and advance *step_dev, for mmf_clip_adamw_apply_dev (the L = 1 plan fills them in
+ * its weight-gradient launch; others run the reduction pass of mmf_clip_adamw_step_dev here). */
 size_t mmf_hybrid_train_sync_bytes(const mmf_hybrid_desc* d);
 int mmf_hybrid_train_step(const mmf_hybrid_desc* d, const mmf_hybrid_params* params, const float* const* x,
                           const float* mask, const int64_t* labels, float label_smoothing, float loss_scale,
                           uint64_t* rng_state, void* saved, void* workspace, void* sync, float* logits,
                           float* fusion_weights, float* loss_out, float* dlogits, const mmf_hybrid_grads* grads,
-                          float* const* dx, void* stream);
+                          float* const* dx, float* clip_partial, int64_t* step_dev, const float* grad_flat,
+                          int64_t grad_n, void* stream);
 
 /* AdamW with the learning rate and an extra gradient factor read from device
  * scalars (lr_dev[0]; grad_coef_dev[0], may be NULL = 1), so a captured hipGraph
@@ -316,6 +321,13 @@ int mmf_hybrid_train_step(const mmf_hybrid_desc* d, const mmf_hybrid_params* par
 int mmf_adamw_step_dev(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                        int64_t* step_dev, const float* lr_dev, const float* grad_coef_dev, float beta1,
                        float beta2, float eps, float weight_decay, float grad_scale, void* stream);
+
+/* The update half of mmf_clip_adamw_step_dev: clip + AdamW from squared-norm partials already in
+ * `workspace` (written by mmf_hybrid_train_step's clip_partial), *step_dev already advanced. */
+int mmf_clip_adamw_apply_dev(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                             int64_t* step_dev, const float* lr_dev, float max_norm, float* total_norm,
+                             float* clip_coef, void* workspace, float beta1, float beta2, float eps,
+                             float weight_decay, float grad_scale, void* stream);
 
 /* dst += src over n floats (both 16-byte aligned): the gradient of one micro-batch added into
  * the accumulated one (Lightning's accumulate_grad_batches, config/base.yaml:75

@@ -533,6 +533,19 @@ int mmf_clip_adamw_step_dev(int64_t n, float* param, const float* grad, float* e
   return MMF_OK;
 }
 
+int mmf_clip_adamw_apply_dev(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                             int64_t* step_dev, const float* lr_dev, float max_norm, float* total_norm,
+                             float* clip_coef, void* workspace, float beta1, float beta2, float eps,
+                             float weight_decay, float grad_scale, void* stream) {
+  if (n < 0 || !param || !grad || !exp_avg || !exp_avg_sq || !step_dev || !lr_dev || !workspace)
+    return fail(MMF_EINVAL, "bad clip+AdamW arguments");
+  hipStream_t st = (hipStream_t)stream;
+  STAGE_TRY("optim.clip_adamw", launch_clip_adamw_apply(n, param, grad, exp_avg, exp_avg_sq, step_dev, lr_dev, beta1,
+                                                        beta2, eps, weight_decay, grad_scale, max_norm, total_norm,
+                                                        clip_coef, (const float*)workspace, st));
+  return MMF_OK;
+}
+
 int mmf_grad_accumulate(int64_t n, const float* src, float* dst, void* stream) {
   if (n < 0 || (n > 0 && (!src || !dst))) return fail(MMF_EINVAL, "bad gradient-accumulate arguments");
   if ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15)

@@ -256,6 +256,11 @@ __global__ __launch_bounds__(NT) void cross_entropy_kernel(int B, int C, const f
 // Pass 1: CLIP_BLOCKS fixed partial sums of squares (grid-stride, fixed order);
 // pass 2: one workgroup adds them in a fixed tree order -> deterministic.
 constexpr int CLIP_BLOCKS = 256;
+// The partials buffer holds CLIP_SLOTS = 4 CLIP_BLOCKS floats: grad_sumsq_kernel writes slots
+// [0, CLIP_BLOCKS) and zeroes the rest; a producer with more pieces (the L = 1 weight-gradient launch,
+// one slot per output tile) fills up to all of them.  Thread t of the clip reduction adds slots t,
+// t + 256, t + 512, t + 768 in that order (in double: the zero slots add exact zeros).
+constexpr int CLIP_SLOTS = 4 * CLIP_BLOCKS;
 
 __global__ __launch_bounds__(NT) void grad_sumsq_kernel(int64_t n, const float* __restrict__ g,
                                                         float* __restrict__ partial, int64_t* step_incr) {
@@ -277,6 +282,7 @@ __global__ __launch_bounds__(NT) void grad_sumsq_kernel(int64_t n, const float* 
   if ((t & 63) == 0) red[t >> 6] = acc;
   __syncthreads();
   if (t == 0) partial[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+  if (t >= 1 && t < CLIP_SLOTS / CLIP_BLOCKS) partial[blockIdx.x + t * CLIP_BLOCKS] = 0.f;
 }
 
 // total_norm = gscale * sqrt(sum); coef = min(1, max_norm / (total_norm + 1e-6)) (1 when max_norm <= 0).
@@ -287,6 +293,8 @@ __device__ __forceinline__ void clip_norm_coef(const float* __restrict__ partial
                                                double* red, float& norm, float& coef) {
   const int t = threadIdx.x;
   double acc = (double)partial[t];
+#pragma unroll
+  for (int r = 1; r < CLIP_SLOTS / CLIP_BLOCKS; ++r) acc += (double)partial[t + r * CLIP_BLOCKS];
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
   if ((t & 63) == 0) red[t >> 6] = acc;
@@ -456,7 +464,7 @@ hipError_t launch_cross_entropy(int B, int C, const float* logits, const int64_t
   return hipGetLastError();
 }
 
-size_t grad_clip_workspace_bytes() { return CLIP_BLOCKS * sizeof(float); }
+size_t grad_clip_workspace_bytes() { return CLIP_SLOTS * sizeof(float); }
 
 hipError_t launch_grad_clip_coef(int64_t n, const float* g, float gscale, float max_norm, float* norm_out,
                                  float* coef_out, float* partial, hipStream_t st) {
@@ -519,6 +527,28 @@ hipError_t launch_adamw(int64_t n, float* p, const float* g, float* m, float* v,
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   mmf_launch(step_incr_kernel, dim3(1), dim3(64), 0, st, step);
+  return hipGetLastError();
+}
+
+// The squared-norm partials of a flat gradient (and the step counter advanced) for a later
+// launch_clip_adamw_apply
+hipError_t launch_grad_sumsq(int64_t n, const float* g, float* partial, int64_t* step, hipStream_t st) {
+  ProfLaunch prof_(st, "grad_sumsq_kernel", 2.0 * n, 4.0 * n);
+  mmf_launch(grad_sumsq_kernel, dim3(CLIP_BLOCKS), dim3(NT), 0, st, n, g, partial, step);
+  return hipGetLastError();
+}
+
+// clip + AdamW from partials a producer already wrote (grad_sumsq_kernel, or the L = 1 weight-gradient
+// launch), the step counter already advanced: the one launch of launch_clip_adamw's two
+hipError_t launch_clip_adamw_apply(int64_t n, float* p, const float* g, float* m, float* v, const int64_t* step,
+                                   const float* lr_dev, float b1, float b2, float eps, float wd, float gscale,
+                                   float max_norm, float* norm_out, float* coef_out, const float* partial,
+                                   hipStream_t st) {
+  const int vec = adamw_vec(p, g, m, v);
+  const int64_t blocks = adamw_blocks(n, vec);
+  ProfLaunch prof_(st, "clip_adamw_kernel", 0.0, 28.0 * n);
+  mmf_launch(clip_adamw_kernel, dim3((unsigned)blocks), dim3(NT), 0, st, n, p, g, m, v, step, lr_dev, b1, b2, eps,
+             wd, gscale, partial, max_norm, norm_out, coef_out, vec);
   return hipGetLastError();
 }
 

@@ -1115,11 +1115,13 @@ int mmf_hybrid_train_step(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, 
                           const float* mask, const int64_t* labels, float label_smoothing, float loss_scale,
                           uint64_t* rng_state, void* saved, void* workspace, void* sync, float* logits,
                           float* fusion_weights, float* loss_out, float* dlogits, const mmf_hybrid_grads* G,
-                          float* const* dx, void* stream) {
+                          float* const* dx, float* clip_partial, int64_t* step_dev, const float* grad_flat,
+                          int64_t grad_n, void* stream) {
   int rc = check_hybrid(d);
   if (rc) return rc;
   if (!W || !x || !mask || !labels || !saved || !workspace || !logits || !loss_out || !dlogits || !G)
     return fail(MMF_EINVAL, "null argument");
+  if (clip_partial && !step_dev) return fail(MMF_EINVAL, "train step: clip partials need the step counter");
   if (sync && lean_l1(d, W, x)) {
     MathScope math_(d->matmul_precision);
     hipStream_t st = (hipStream_t)stream;
@@ -1144,6 +1146,8 @@ int mmf_hybrid_train_step(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, 
     a.dlogits_out = dlogits;
     wa.loss_rows = w.dfused;
     wa.loss = loss_out;
+    wa.clip_partial = clip_partial;   // (the weight-gradient launch writes the clip partials itself)
+    wa.step_incr = clip_partial ? step_dev : nullptr;
     STAGE_TRY("train.l1", launch_l1_train(a, wa, st));
     return MMF_OK;
   }
@@ -1152,7 +1156,13 @@ int mmf_hybrid_train_step(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, 
   rc = mmf_cross_entropy_ls(d->batch, d->num_classes, logits, labels, label_smoothing, loss_scale, loss_out,
                             dlogits, stream);
   if (rc) return rc;
-  return mmf_hybrid_backward(d, W, x, mask, saved, dlogits, workspace, G, dx, stream);
+  rc = mmf_hybrid_backward(d, W, x, mask, saved, dlogits, workspace, G, dx, stream);
+  if (rc || !clip_partial) return rc;
+  if (!grad_flat || grad_n < 0 || (reinterpret_cast<uintptr_t>(grad_flat) & 15))
+    return fail(MMF_EINVAL, "train step: clip partials need the 16-byte aligned flat gradient");
+  hipStream_t st = (hipStream_t)stream;
+  STAGE_TRY("optim.clip_norm", launch_grad_sumsq(grad_n, grad_flat, clip_partial, step_dev, st));
+  return MMF_OK;
 }
 
 }  // extern "C"

@@ -996,8 +996,13 @@ __global__ __launch_bounds__(NT) void l1_wgrad_kernel(const L1WgArgs w) {
   __shared__ float bred[4][32];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   int tile = blockIdx.x;
-  if (w.loss && tile == gridDim.x - 1) {
-    // the batch-mean loss in cross_entropy_kernel's order: per-thread strided sums, then a tree
+  if ((w.loss || w.clip_partial) && tile == gridDim.x - 1) {
+    // the extra workgroup: the batch-mean loss in cross_entropy_kernel's order (per-thread strided
+    // sums, then a tree); the clip partial slots no tile fills zeroed; the step counter advanced
+    if (w.clip_partial)
+      for (int s = w.ntiles + t; s < CLIP_PARTIAL_SLOTS; s += NT) w.clip_partial[s] = 0.f;
+    if (w.step_incr && t == 0) w.step_incr[0] += 1;
+    if (!w.loss) return;
     __shared__ float lred[NT];
     float acc = 0.f;
     for (int i = t; i < w.B; i += NT) acc += w.loss_rows[i];
@@ -1058,15 +1063,31 @@ __global__ __launch_bounds__(NT) void l1_wgrad_kernel(const L1WgArgs w) {
     if (hf == 0) bred[wave][col] = v;
   }
   __syncthreads();
+  float sq = 0.f;   // this tile's share of the gradient's squared norm (clip_partial)
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int v = t + u * NT;          // (reg r, lane l) of the 32 x 32 tile
     const int r = v >> 6, l = v & 63;
     const float s = ((red[0][r][l] + red[1][r][l]) + red[2][r][l]) + red[3][r][l];
     const int i = n0 + acc_row(r, l >> 5), j = k0 + (l & 31);
-    if (i < J.N && j < J.K) J.dW[(int64_t)i * J.K + j] = s;
+    if (i < J.N && j < J.K) {
+      J.dW[(int64_t)i * J.K + j] = s;
+      sq += s * s;
+    }
   }
-  if (do_db && t < 32 && n0 + t < J.N) J.db[n0 + t] = ((bred[0][t] + bred[1][t]) + bred[2][t]) + bred[3][t];
+  if (do_db && t < 32 && n0 + t < J.N) {
+    const float s = ((bred[0][t] + bred[1][t]) + bred[2][t]) + bred[3][t];
+    J.db[n0 + t] = s;
+    sq += s * s;
+  }
+  if (w.clip_partial) {   // fixed-order block sum: xor butterfly per wave, then the four waves
+    __shared__ float sqr[4];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) sq += __shfl_xor(sq, off);
+    if (lane == 0) sqr[wave] = sq;
+    __syncthreads();
+    if (t == 0) w.clip_partial[tile] = (sqr[0] + sqr[1]) + (sqr[2] + sqr[3]);
+  }
   L1_ST(4, 2);
   L1_RT(4, 9);
 }
@@ -1211,7 +1232,8 @@ hipError_t launch_l1_train(const L1Args& a, const L1WgArgs& w, hipStream_t st) {
   const int zblocks = w.nz ? w.zoff[w.nz] : 0;
   for (int i = 0; i < w.nz; ++i) by += 4.0 * w.zn[i];
   ProfLaunch prof_(st, "l1_wgrad_kernel", fl, by);
-  mmf_launch(l1_wgrad_kernel, dim3((unsigned)(w.ntiles + zblocks + (w.loss ? 1 : 0))), dim3(NT), 0, st, w);
+  if (w.clip_partial && w.ntiles > CLIP_PARTIAL_SLOTS) return hipErrorInvalidValue;
+  mmf_launch(l1_wgrad_kernel, dim3((unsigned)(w.ntiles + zblocks + ((w.loss || w.clip_partial) ? 1 : 0))), dim3(NT), 0, st, w);
   return hipGetLastError();
 }
 

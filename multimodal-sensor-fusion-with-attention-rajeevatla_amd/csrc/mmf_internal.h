@@ -463,6 +463,12 @@ size_t grad_clip_workspace_bytes();
 hipError_t launch_grad_clip_coef(int64_t n, const float* g, float gscale, float max_norm, float* norm_out,
                                  float* coef_out, float* partial, hipStream_t st);
 // grad_sumsq (advancing *step) + one clip-and-AdamW launch (mmf_clip_adamw_step_dev)
+hipError_t launch_grad_sumsq(int64_t n, const float* g, float* partial, int64_t* step, hipStream_t st);
+hipError_t launch_clip_adamw_apply(int64_t n, float* p, const float* g, float* m, float* v, const int64_t* step,
+                                   const float* lr_dev, float b1, float b2, float eps, float wd, float gscale,
+                                   float max_norm, float* norm_out, float* coef_out, const float* partial,
+                                   hipStream_t st);
+constexpr int CLIP_PARTIAL_SLOTS = 1024;   // (head.hip CLIP_SLOTS)
 hipError_t launch_clip_adamw(int64_t n, float* p, const float* g, float* m, float* v, int64_t* step,
                              const float* lr_dev, float b1, float b2, float eps, float wd, float gscale,
                              float max_norm, float* norm_out, float* coef_out, float* partial, hipStream_t st);
@@ -571,6 +577,8 @@ struct L1WgArgs {
   int32_t njobs, B, ntiles;
   float* z[L1_MAXZ]; int32_t zn[L1_MAXZ]; int32_t zoff[L1_MAXZ + 1]; int32_t nz;
   const float* loss_rows; float* loss;   // optional: loss = mean of loss_rows (one extra workgroup)
+  float* clip_partial;                   // optional: squared-norm partial per output tile (CLIP_PARTIAL_SLOTS)
+  int64_t* step_incr;                    // optional: the optimizer step counter, advanced once
 };
 hipError_t launch_l1_forward(const L1Args& a, hipStream_t st);
 hipError_t launch_l1_backward(const L1Args& a, const L1WgArgs& w, hipStream_t st);

@@ -49,7 +49,7 @@ EXPORTED_SYMBOLS = (
     "mmf_adaptive_weights_backward",
     "mmf_cma_saved_bytes", "mmf_cma_workspace_bytes", "mmf_cma_forward", "mmf_cma_backward",
     "mmf_cross_entropy_ls", "mmf_adamw_step", "mmf_adamw_step_dev", "mmf_grad_clip_workspace_bytes",
-    "mmf_grad_clip_coef", "mmf_clip_adamw_step_dev", "mmf_grad_accumulate", "mmf_profile_begin", "mmf_profile_end",
+    "mmf_grad_clip_coef", "mmf_clip_adamw_step_dev", "mmf_clip_adamw_apply_dev", "mmf_grad_accumulate", "mmf_profile_begin", "mmf_profile_end",
     "mmf_last_error", "mmf_version",
     "mmf_attention_pool_workspace_bytes", "mmf_attention_pool_forward", "mmf_attention_pool_backward",
     "mmf_late_fusion_workspace_bytes", "mmf_late_fusion_forward", "mmf_late_fusion_backward",
@@ -130,7 +130,8 @@ def lib() -> ctypes.CDLL:
     L.mmf_hybrid_train_sync_bytes.argtypes = [POINTER(HybridDesc)]
     L.mmf_hybrid_train_sync_bytes.restype = sz
     L.mmf_hybrid_train_step.argtypes = [POINTER(HybridDesc), POINTER(HybridParams), vp, vp, vp, c_float, c_float,
-                                        vp, vp, vp, vp, vp, vp, vp, vp, POINTER(HybridGrads), vp, vp]
+                                        vp, vp, vp, vp, vp, vp, vp, vp, POINTER(HybridGrads), vp, vp, vp, vp,
+                                        c_int64, vp]
     L.mmf_hybrid_train_step.restype = c_int32
     L.mmf_adaptive_weights_workspace_bytes.argtypes = [c_int32, c_int32, c_int32]
     L.mmf_adaptive_weights_workspace_bytes.restype = sz
@@ -163,6 +164,9 @@ def lib() -> ctypes.CDLL:
     L.mmf_clip_adamw_step_dev.argtypes = [c_int64, vp, vp, vp, vp, vp, vp, c_float, vp, vp, vp, c_float, c_float,
                                           c_float, c_float, c_float, vp]
     L.mmf_clip_adamw_step_dev.restype = c_int32
+    L.mmf_clip_adamw_apply_dev.argtypes = [c_int64, vp, vp, vp, vp, vp, vp, c_float, vp, vp, vp, c_float, c_float,
+                                           c_float, c_float, c_float, vp]
+    L.mmf_clip_adamw_apply_dev.restype = c_int32
     L.mmf_grad_accumulate.argtypes = [c_int64, vp, vp, vp]
     L.mmf_grad_accumulate.restype = c_int32
     L.mmf_profile_begin.argtypes = []

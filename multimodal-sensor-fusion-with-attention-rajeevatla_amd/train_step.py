@@ -90,7 +90,7 @@ class HybridTrainStep:
                  labels: torch.Tensor, lr: float = 1e-3, weight_decay: float = 1e-4,
                  betas=(0.9, 0.999), eps: float = 1e-8, label_smoothing: float = 0.05,
                  gradient_clip_norm: float = 1.0, process_group=None, input_grads: bool = True,
-                 accumulate: int = 1):
+                 accumulate: int = 1, fuse_clip: bool = True):
         dev = mask.device
         _nat.require_device(mask, "training inputs")
         self.model = model.train()
@@ -159,6 +159,9 @@ class HybridTrainStep:
         self.xarr = [_nat.ptr_array([x[i * self.micro:].data_ptr() for x in self.x]) for i in range(self.accumulate)]
         self.dxarr = ([_nat.ptr_array([t[i * self.micro:].data_ptr() for t in self.dx]) for i in range(self.accumulate)]
                       if input_grads else None)
+        # one process, one micro-batch: the train step writes the clip norm's partials itself (the L = 1
+        # plan in its weight-gradient launch) and the optimizer runs the update launch only
+        self.fuse_clip = bool(fuse_clip) and self.world == 1 and self.accumulate == 1
         self.graph: Optional[torch.cuda.CUDAGraph] = None
 
     @property
@@ -209,7 +212,10 @@ class HybridTrainStep:
                                          self.sync.data_ptr(), self.logits[i * b:].data_ptr(),
                                          self.fw[i * b:].data_ptr(), self.losses[i:].data_ptr(),
                                          self.dlogits[i * b:].data_ptr(), ctypes.byref(g),
-                                         ctypes.cast(self.dxarr[i], ctypes.c_void_p) if self.dxarr else None, st)
+                                         ctypes.cast(self.dxarr[i], ctypes.c_void_p) if self.dxarr else None,
+                                         self.clip_ws.data_ptr() if self.fuse_clip else None,
+                                         self.step_dev.data_ptr() if self.fuse_clip else None,
+                                         self.grad.data_ptr(), self.grad.numel(), st)
             _nat.check(rc, "train step (forward, cross-entropy, backward)")
             if i > 0:
                 rc = L.mmf_grad_accumulate(self.grad.numel(), self.grad_mb.data_ptr(), self.grad.data_ptr(), st)
@@ -220,27 +226,29 @@ class HybridTrainStep:
 
     def optimizer_step(self) -> None:
         """Clip the (rank-averaged) gradient to gradient_clip_norm, then AdamW; both read
-        their scalars on the device."""
+        their scalars on the device.  With fuse_clip (one process, one micro-batch) the train step
+        already wrote the norm's partials and advanced the step counter: one launch."""
         L = _nat.lib()
         st = _nat.stream_ptr(self.dev)
         gscale = 1.0 / self.world
-        rc = L.mmf_clip_adamw_step_dev(self.flat.numel(), self.flat.data_ptr(), self.grad.data_ptr(),
-                                       self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
-                                       self.step_dev.data_ptr(), self.lr_dev.data_ptr(), float(self.clip_norm),
-                                       self.grad_norm.data_ptr(), self.clip_coef.data_ptr(),
-                                       self.clip_ws.data_ptr(), self.betas[0], self.betas[1], self.eps, self.wd,
-                                       gscale, st)
+        fn = L.mmf_clip_adamw_apply_dev if self.fuse_clip else L.mmf_clip_adamw_step_dev
+        rc = fn(self.flat.numel(), self.flat.data_ptr(), self.grad.data_ptr(), self.exp_avg.data_ptr(),
+                self.exp_avg_sq.data_ptr(), self.step_dev.data_ptr(), self.lr_dev.data_ptr(), float(self.clip_norm),
+                self.grad_norm.data_ptr(), self.clip_coef.data_ptr(), self.clip_ws.data_ptr(), self.betas[0],
+                self.betas[1], self.eps, self.wd, gscale, st)
         _nat.check(rc, "clip + AdamW")
 
     # ---------------------------------------------------------------- driver
     def capture(self) -> None:
         """Capture fwd+CE+bwd (and clip + AdamW when single-process) into one hipGraph."""
+        step0 = self.step_dev.clone()
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(s):
             self.forward_backward()     # warm the path outside capture
         torch.cuda.current_stream(self.dev).wait_stream(s)
         torch.cuda.synchronize(self.dev)
+        self.step_dev.copy_(step0)      # (with fuse_clip the warm-up advanced the optimizer's step count)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self.forward_backward()

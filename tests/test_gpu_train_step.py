@@ -249,3 +249,36 @@ def test_one_call_train_step_matches_three_calls(mods, seq):
         for a, b in zip(step_a, step_b):
             assert torch.equal(a, b)
     assert int(runs[0][1][-1][1]) == 7   # offset 5 -> 7 after two steps
+
+
+@pytest.mark.parametrize("seq", [False, True])
+def test_clip_partials_from_the_train_step(mods, seq):
+    """fuse_clip (one process, one micro-batch): the train step writes the clip norm's squared-norm
+    partials itself (the L = 1 plan in its weight-gradient launch, one partial per output tile; other
+    plans with grad_sumsq_kernel) and advances the step counter, the optimizer runs the update launch
+    only -- against fuse_clip=False (mmf_clip_adamw_step_dev's own reduction pass) over two clipped
+    steps: the same gradient, the norm to 1e-6, the weights to 1e-6, the same step count."""
+    fusion, train_step = mods
+    feats, mask, labels = _batch(13)
+    if not seq:
+        feats = [f[:, 0] for f in feats]
+    runs = []
+    for fuse in (True, False):
+        model = _model(fusion, 0.0).cuda()
+        st = train_step.HybridTrainStep(model, [f.cuda() for f in feats], mask.cuda(), labels.cuda(), lr=3e-3,
+                                        gradient_clip_norm=0.05, fuse_clip=fuse)
+        assert st.fuse_clip == fuse
+        out = []
+        for _ in range(2):
+            st.forward_backward()
+            st.optimizer_step()
+            torch.cuda.synchronize()
+            out.append((st.grad.cpu().clone(), float(st.grad_norm.item()), st.flat.cpu().clone(),
+                        int(st.step_dev.item()), float(st.clip_coef.item())))
+        runs.append(out)
+    for k, ((g1, n1, p1, s1, c1), (g2, n2, p2, s2, c2)) in enumerate(zip(*runs)):
+        if k == 0:
+            assert torch.equal(g1, g2)   # (the second step's gradient sees weights 1e-7 apart)
+        assert abs(n1 - n2) <= 1e-6 * n2 and c1 < 1.0
+        assert s1 == s2
+        torch.testing.assert_close(p1, p2, rtol=1e-6, atol=1e-7)
