@@ -226,6 +226,19 @@ __device__ __forceinline__ void epilogue(const GemmGroup& G, const TileCtx& T, f
         *reinterpret_cast<f32x4*>(cs + lr * CS + cg) = f32x4{v[0], v[1], v[2], v[3]};
         *reinterpret_cast<f32x4*>(cs + lr * CS + cg + 4) = f32x4{v[4], v[5], v[6], v[7]};
       }
+      if (epi & EPI_BF16COPY) {   // (never with EPI_PARTIAL / EPI_BF16; nbatch 1)
+        __bf16* ob = reinterpret_cast<__bf16*>(G.copy) + (int64_t)i * ldc + j0;
+        if (vstb && nv == 8 && ((uintptr_t)G.copy & 15) == 0) {
+          bf16x8 pk;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) pk[e] = (__bf16)v[e];
+          *reinterpret_cast<bf16x8*>(ob) = pk;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (e < nv) ob[e] = (__bf16)v[e];
+        }
+      }
       if (epi & EPI_BF16) {   // (never with EPI_PARTIAL; nbatch 1)
         __bf16* ob = reinterpret_cast<__bf16*>(T.Cb) + (int64_t)i * ldc + j0;
         if (vstb && nv == 8) {
@@ -338,6 +351,39 @@ __device__ __forceinline__ f32x4 frag(const float* lds, int e, int j, int h) {
   }
 }
 
+// bf16 operand tiles (gemm_lds_kernel<..., B16 = 1>, "medium" with bf16 copies of both operands in
+// HBM, RK mode, DK = 32 bf16 k per tile): [e][32] bf16 = 64-B rows, the fp32 DK = 16 image's row
+// size, 16-B slots (8 k each) XOR-swizzled the same way (swz<16>), so the LDS-DMA pieces, the ring
+// footprint and the conflict-free fragment reads carry over; a fragment (lane half h of k-chunk u:
+// k = 16 u + 8 h .. + 7) is ONE ds_read_b128 with no conversion, half the LDS bytes per MFMA of the
+// fp32-operand form.
+__device__ __forceinline__ void stage_tile_b16(float* lds, const Operand& op, int64_t boff, int e0, int eext, int k0,
+                                               int kend, int wave, int lane) {
+  constexpr int PER_WAVE = BM * 32 * 2 / 1024 / 4;   // 1-KB pieces per wave (2)
+#pragma unroll
+  for (int u = 0; u < PER_WAVE; ++u) {
+    const int ins = wave * PER_WAVE + u;
+    const int row = ins * 16 + lane / 4;
+    const int slot = (lane & 3) ^ swz<16>(row);
+    const int e = min(e0 + row, eext - 1);
+    const int k = min(k0 + 8 * slot, kend - 8);
+    const __bf16* src = reinterpret_cast<const __bf16*>(op.ptr) + boff + (int64_t)e * op.ld + k;
+    __builtin_amdgcn_global_load_lds((const void*)src,
+                                     (__attribute__((address_space(3))) void*)(lds + ins * 256), 16, 0, 0);
+  }
+}
+__device__ __forceinline__ void zero_tail_b16(float* lds, int kv) {
+  for (int idx = threadIdx.x; idx < BM * 4; idx += NT) {
+    const int row = idx / 4, slot = idx % 4;
+    if (8 * slot >= kv)
+      *reinterpret_cast<f32x4*>(lds + row * 16 + ((slot ^ swz<16>(row)) << 2)) = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+__device__ __forceinline__ bf16x8 frag_b16(const float* lds, int e, int u, int h) {
+  const int slot = (2 * u + h) ^ swz<16>(e);
+  return *reinterpret_cast<const bf16x8*>(lds + e * 16 + (slot << 2));
+}
+
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -347,10 +393,12 @@ __device__ __forceinline__ void lds_barrier() {
 // (source, k0) cursor over one tile's contraction
 struct KCursor { int si, k0, kend; };
 
-template <int AMODE, int BMODE, int DK, int NSTAGE, int BF = 0>
-__global__ __launch_bounds__(NT, (NSTAGE * DK <= 32 ? 4 : 2)) void gemm_lds_kernel(const GemmArgs args) {
-  constexpr int DTILE = BM * DK;                  // floats per operand tile
-  constexpr int DMA_PER_TILE = 2 * (BM * DK / 1024);  // glds per wave per (A, B) tile pair
+// B16: both operands bf16 in HBM (RK / RK, BF = 1, DK = 32 bf16 k per tile; stage_tile_b16)
+template <int AMODE, int BMODE, int DK, int NSTAGE, int BF = 0, int B16 = 0>
+__global__ __launch_bounds__(NT, (NSTAGE * (B16 ? DK / 2 : DK) <= 32 ? 4 : 2)) void gemm_lds_kernel(const GemmArgs args) {
+  static_assert(!B16 || (AMODE == MODE_RK && BMODE == MODE_RK && BF == 1 && DK == 32), "bf16-operand form");
+  constexpr int DTILE = B16 ? BM * DK / 2 : BM * DK;   // floats per operand tile
+  constexpr int DMA_PER_TILE = B16 ? 2 * (BM * DK / 2048) : 2 * (BM * DK / 1024);  // glds per wave per (A, B) pair
   int local;
   const GemmGroup& G = args.g[group_of_block(args, local)];
   TileCtx T;
@@ -414,8 +462,13 @@ __global__ __launch_bounds__(NT, (NSTAGE * DK <= 32 ? 4 : 2)) void gemm_lds_kern
       op_si = k.si;
     }
     float* At = lds + buf * 2 * DTILE;
-    stage_tile<AMODE, DK>(At, opA, offA + seg * opA.seg_stride, T.i0, G.M, k.k0, k.kend, wave, lane);
-    stage_tile<BMODE, DK>(At + DTILE, opB, offB + seg * opB.seg_stride, T.j0, G.N, k.k0, k.kend, wave, lane);
+    if constexpr (B16) {
+      stage_tile_b16(At, opA, offA + seg * opA.seg_stride, T.i0, G.M, k.k0, k.kend, wave, lane);
+      stage_tile_b16(At + DTILE, opB, offB + seg * opB.seg_stride, T.j0, G.N, k.k0, k.kend, wave, lane);
+    } else {
+      stage_tile<AMODE, DK>(At, opA, offA + seg * opA.seg_stride, T.i0, G.M, k.k0, k.kend, wave, lane);
+      stage_tile<BMODE, DK>(At + DTILE, opB, offB + seg * opB.seg_stride, T.j0, G.N, k.k0, k.kend, wave, lane);
+    }
   };
   // wait until at most `ahead` tiles' DMAs are outstanding (vmcnt needs an immediate)
   auto wait_tiles = [&](int ahead) {
@@ -446,8 +499,13 @@ __global__ __launch_bounds__(NT, (NSTAGE * DK <= 32 ? 4 : 2)) void gemm_lds_kern
       float* Bt = At + DTILE;
       const int kv = cur.kend - cur.k0;
       if (kv < DK) {
-        zero_tail<AMODE, DK>(At, kv);
-        zero_tail<BMODE, DK>(Bt, kv);
+        if constexpr (B16) {
+          zero_tail_b16(At, kv);
+          zero_tail_b16(Bt, kv);
+        } else {
+          zero_tail<AMODE, DK>(At, kv);
+          zero_tail<BMODE, DK>(Bt, kv);
+        }
         lds_barrier();
       }
       if (iss.si < G.src_count) {
@@ -455,7 +513,7 @@ __global__ __launch_bounds__(NT, (NSTAGE * DK <= 32 ? 4 : 2)) void gemm_lds_kern
         iss = advance(iss);
         ++nissued;
       }
-      if (want_db) {
+      if (!B16 && want_db) {
         // bias grad of a TN dW: row sums of A over this k-tile (thread: row t&127, k half t>>7)
         const int row = t & (BM - 1), kh = t >> 7;
 #pragma unroll
@@ -465,7 +523,20 @@ __global__ __launch_bounds__(NT, (NSTAGE * DK <= 32 ? 4 : 2)) void gemm_lds_kern
                                     : At[row * DK + ((((kk >> 2) ^ swz<DK>(row))) << 2) + (kk & 3)];
         }
       }
-if constexpr (BF != 0) {
+if constexpr (B16) {
+#pragma unroll
+        for (int u = 0; u < DK / 16; ++u) {
+          bf16x8 av[2], bv[2];
+#pragma unroll
+          for (int a = 0; a < 2; ++a) av[a] = frag_b16(At, wm * 64 + a * 32 + c, u, h);
+#pragma unroll
+          for (int b = 0; b < 2; ++b) bv[b] = frag_b16(Bt, wn * 64 + b * 32 + c, u, h);
+#pragma unroll
+          for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[a], bv[b], acc[a][b], 0, 0, 0);
+        }
+      } else if constexpr (BF != 0) {
         // chunks 2u, 2u+1 (16 k) -> one bf16 MFMA per accumulator
 #pragma unroll
         for (int u = 0; u < DK / 16; ++u) {
@@ -1408,6 +1479,122 @@ hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, 
     }
   }
   return left.finish(hipSuccess);
+}
+
+// fp32 -> bf16 copies of small tensors (the weights of a bf16-operand GEMM), round to nearest
+// even: blockIdx.y = tensor, float4 -> 4 bf16 per thread step
+__global__ __launch_bounds__(256) void cvt_bf16_kernel(const CvtArgs a) {
+  const int q = blockIdx.y;
+  const float* s = a.src[q];
+  __bf16* d = a.dst[q];
+  const int64_t n = a.n[q];
+  for (int64_t i = 4 * ((int64_t)blockIdx.x * 256 + threadIdx.x); i < n; i += 4 * (int64_t)gridDim.x * 256) {
+    if (i + 4 <= n) {
+      const float4 v = *reinterpret_cast<const float4*>(s + i);
+      d[i] = (__bf16)v.x; d[i + 1] = (__bf16)v.y; d[i + 2] = (__bf16)v.z; d[i + 3] = (__bf16)v.w;
+    } else {
+      for (int64_t e = i; e < n; ++e) d[e] = (__bf16)s[e];
+    }
+  }
+}
+
+hipError_t launch_cvt_bf16(const CvtArgs& a, hipStream_t st) {
+  if (a.count <= 0) return hipSuccess;
+  if (a.count > CVT_MAX) return hipErrorInvalidValue;
+  int64_t mx = 0;
+  double by = 0.0;
+  for (int i = 0; i < a.count; ++i) {
+    if (((uintptr_t)a.src[i] & 15) != 0) return hipErrorInvalidValue;
+    mx = std::max<int64_t>(mx, a.n[i]);
+    by += 6.0 * a.n[i];
+  }
+  const int gx = (int)std::min<int64_t>((mx / 4 + 255) / 256, 64);
+  ProfLaunch prof_(st, "cvt_bf16_kernel", 0.0, by);
+  mmf_launch(cvt_bf16_kernel, dim3(std::max(gx, 1), a.count), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+bool gemm_b16_ok(const GemmJob& J) {
+  const GemmGroup& g = J.g;
+  if ((g.epi & EPI_PARTIAL) || g.nbatch > 1 || g.seg_rows > 0) return false;
+  for (int s = 0; s < J.nsrc; ++s) {
+    const GemmSrc& x = J.src[s];
+    for (const Operand* o : {&x.a, &x.b})
+      if (o->row_div != 1 || o->seg_stride != 0 || o->ld % 8 != 0 || ((uintptr_t)o->ptr & 15) != 0) return false;
+    if (x.K % 8 != 0 || x.K < 8) return false;
+  }
+  return true;
+}
+
+hipError_t launch_gemm_b16(const GemmJob* jobs_in, int njobs, hipStream_t st) {
+  if (njobs <= 0) return hipSuccess;
+  for (int i = 0; i < njobs; ++i)
+    if (!gemm_b16_ok(jobs_in[i]) || jobs_in[i].nsrc > GEMM_MAX_SRCS) return hipErrorInvalidValue;
+  // longest contraction first, then clustered by the most-shared operand (launch_gemm's order)
+  std::vector<int> order(njobs);
+  std::vector<double> work(njobs);
+  std::map<uintptr_t, int> uses;
+  for (int i = 0; i < njobs; ++i) {
+    order[i] = i;
+    double kk = 0.0;
+    for (int s = 0; s < jobs_in[i].nsrc; ++s) kk += jobs_in[i].src[s].K;
+    work[i] = kk;
+    ++uses[(uintptr_t)jobs_in[i].src[0].a.ptr];
+    ++uses[(uintptr_t)jobs_in[i].src[0].b.ptr];
+  }
+  const bool ilv_on = gemm_interleave_mode() != 0;
+  std::vector<uintptr_t> share(njobs, 0);
+  for (int i = 0; i < njobs; ++i) {
+    const uintptr_t a = (uintptr_t)jobs_in[i].src[0].a.ptr, b = (uintptr_t)jobs_in[i].src[0].b.ptr;
+    share[i] = uses[b] > uses[a] ? b : a;
+  }
+  std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
+    if (work[x] != work[y]) return work[x] > work[y];
+    return share[x] < share[y];
+  });
+  int done = 0;
+  while (done < njobs) {
+    GemmArgs args;
+    memset(&args, 0, sizeof(args));
+    args.amode = MODE_RK;
+    args.bmode = MODE_RK;
+    int ng = 0, ns = 0, max_blocks = 0;
+    while (done < njobs && ng < GEMM_MAX_GROUPS) {
+      const GemmJob& J = jobs_in[order[done]];
+      if (ns + J.nsrc > GEMM_MAX_SRCS) break;
+      GemmGroup g = J.g;
+      g.nbatch = 1;
+      g.src_begin = ns;
+      g.src_count = J.nsrc;
+      for (int s = 0; s < J.nsrc; ++s) args.s[ns++] = J.src[s];
+      args.tile_off[ng] = max_blocks;
+      args.g[ng++] = g;
+      max_blocks += ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+      ++done;
+    }
+    args.ngroups = ng;
+    if (ilv_on && ng > 1) {
+      const int T = args.tile_off[1];
+      bool even = T > 0 && T % 8 == 0;
+      for (int gi = 1; gi < ng && even; ++gi)
+        even = (gi + 1 < ng ? args.tile_off[gi + 1] : max_blocks) - args.tile_off[gi] == T;
+      args.ilv = even ? 1 : 0;
+    }
+    double fl = 0.0, by = 0.0;
+    for (int gi = 0; gi < ng; ++gi) {
+      const GemmGroup& g = args.g[gi];
+      for (int si = g.src_begin; si < g.src_begin + g.src_count; ++si) {
+        fl += 2.0 * g.M * g.N * args.s[si].K;
+        by += 2.0 * ((double)g.M + g.N) * args.s[si].K;   // bf16 operands
+      }
+      by += ((g.epi & EPI_BF16) ? 2.0 : 4.0) * g.M * g.N + ((g.epi & EPI_BF16COPY) ? 2.0 * g.M * g.N : 0.0);
+    }
+    ProfLaunch prof_(st, "gemm_lds_kernel<0, 0, 32, 3, 1, 1>", fl, by);
+    mmf_launch((gemm_lds_kernel<MODE_RK, MODE_RK, 32, 3, 1, 1>), dim3(max_blocks, 1), dim3(NT), 0, st, args);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_reduce(const ReduceJob* jobs, int njobs, hipStream_t st) {

@@ -95,6 +95,21 @@ bool pair_qk_bf16(const mmf_hybrid_desc* d, int g) {
   return !single_key(d, g) && !wide_pair(d, g) && Lm(d, d->pair_k[g]) > 128 && qk_bf16_on(d);
 }
 
+// The Q/K projection GEMM on bf16 copies of both operands ("medium", every Q/K pair stores bf16
+// Q / K): the projection GEMM's epilogue also writes P_m as bf16 (EPI_BF16COPY) and the pairs'
+// W_q / W_k are converted once per forward; the GEMM (launch_gemm_b16) then streams half the
+// operand bytes and feeds its MFMAs without conversions.  MMF_NO_GEMM_B16=1: the fp32-operand form.
+bool qk_gemm_b16(const mmf_hybrid_desc* d) {
+  if (math_mode() != 1 || getenv("MMF_NO_GEMM_B16") || d->hidden % 8 != 0) return false;
+  int n = 0;
+  for (int g = 0; g < d->num_pairs; ++g) {
+    if (single_key(d, g) || wide_pair(d, g)) continue;
+    if (!pair_qk_bf16(d, g)) return false;
+    ++n;
+  }
+  return n > 0 && 2 * n <= CVT_MAX;
+}
+
 // The head (tail or generic) takes mean_L P_m from per-tile column sums written by the
 // projection GEMM's epilogue when every 128-row tile lies inside one sample (pooled plan):
 // L / 128 rows per sample instead of L (C5: the generic head read 400 MB with one
@@ -118,6 +133,8 @@ struct Saved {
   float *Pw[MMF_MAX_PAIRS], *Pdw[MMF_MAX_PAIRS];   // wide pairs: probabilities, post-dropout (general)
   float* pst[MMF_MAX_PAIRS];                        // stored probabilities (pstore_on)
   float *pooled, *scores, *weights, *fused, *h1;
+  __bf16* Pb[MMF_MAX_MODALITIES];                  // bf16 copies of P_m (qk_gemm_b16)
+  __bf16 *Wqb[MMF_MAX_PAIRS], *Wkb[MMF_MAX_PAIRS];  // bf16 copies of W_q / W_k (qk_gemm_b16)
 };
 
 void layout_saved(const mmf_hybrid_desc* d, Bump& bp, Saved& s) {
@@ -161,6 +178,17 @@ void layout_saved(const mmf_hybrid_desc* d, Bump& bp, Saved& s) {
   s.weights = bp.take<float>(B * M);
   s.fused = bp.take<float>(B * H);
   s.h1 = bp.take<float>(B * H);
+  if (qk_gemm_b16(d)) {
+    bool used[MMF_MAX_MODALITIES] = {};
+    for (int g = 0; g < d->num_pairs; ++g)
+      if (!single_key(d, g) && !wide_pair(d, g)) {
+        used[d->pair_q[g]] = used[d->pair_k[g]] = true;
+        s.Wqb[g] = bp.take<__bf16>(H * H);
+        s.Wkb[g] = bp.take<__bf16>(H * H);
+      }
+    for (int m = 0; m < d->num_modalities; ++m)
+      if (used[m]) s.Pb[m] = bp.take<__bf16>(B * Lm(d, m) * H);
+  }
 }
 
 struct Ws {
@@ -322,6 +350,7 @@ void plan_wgrads(const mmf_hybrid_desc* d, const float* const* x, const float* m
 }
 
 size_t saved_bytes(const mmf_hybrid_desc* d) {
+  MathScope math_(d->matmul_precision);   // (the layout depends on the precision: qk_gemm_b16)
   Bump bp(nullptr);
   Saved s{};
   layout_saved(d, bp, s);
@@ -329,6 +358,7 @@ size_t saved_bytes(const mmf_hybrid_desc* d) {
 }
 
 size_t workspace_bytes(const mmf_hybrid_desc* d) {
+  MathScope math_(d->matmul_precision);
   Bump bs(nullptr);
   Saved s{};
   layout_saved(d, bs, s);
@@ -604,6 +634,8 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
   Bump bp(saved);
   Saved s{};
   layout_saved(d, bp, s);
+  // (the caller sized `saved` by mmf_hybrid_saved_bytes: the same layout, precision included)
+  if (bp.off > saved_bytes(d)) return fail(MMF_EINVAL, "internal: saved-buffer layout overflow");
   // the rng snapshot {seed, offset} is written by the input-mask kernel (which draws from
   // the live state) and the live offset advanced by the projection GEMM's first launch:
   // no launch of its own
@@ -692,6 +724,10 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
       j.g.bias = W->proj[m].b;
       j.g.colsum = s.Pcol[m];
       j.g.drop_site = SITE_PROJ + m;
+      if (s.Pb[m]) {   // (qk_gemm_b16: the Q/K GEMM's bf16 A operand)
+        j.g.epi |= EPI_BF16COPY;
+        j.g.copy = s.Pb[m];
+      }
       add_src(j, opnd(s.Xd[m], D), opnd(W->proj[m].w, D), D);
       jobs.push_back(j);
     }
@@ -724,7 +760,29 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
                                            const_cast<uint64_t*>(rng_state)));
   }
   // (2) Q/K (and V for the general plan) projections of every present pair (attention.py:104-106)
-  if (d->num_pairs) {
+  if (d->num_pairs && qk_gemm_b16(d)) {
+    // bf16 copies of W_q / W_k, then one bf16-operand GEMM launch over every Q / K projection
+    CvtArgs cv;
+    memset(&cv, 0, sizeof(cv));
+    std::vector<GemmJob> jobs;
+    auto bop = [](const __bf16* p, int ld) { return opnd(reinterpret_cast<const float*>(p), ld); };
+    for (int g = 0; g < d->num_pairs; ++g) {
+      const int q = d->pair_q[g], k = d->pair_k[g];
+      if (single_key(d, g) || wide_pair(d, g)) continue;
+      cv.src[cv.count] = W->q[g].w; cv.dst[cv.count] = s.Wqb[g]; cv.n[cv.count++] = (int64_t)H * H;
+      cv.src[cv.count] = W->k[g].w; cv.dst[cv.count] = s.Wkb[g]; cv.n[cv.count++] = (int64_t)H * H;
+      GemmJob jq = make_job(B * Lm(d, q), H, s.Q[g], H, EPI_BIAS | EPI_BF16);
+      jq.g.bias = W->q[g].b;
+      add_src(jq, bop(s.Pb[q], H), bop(s.Wqb[g], H), H);
+      jobs.push_back(jq);
+      GemmJob jk = make_job(B * Lm(d, k), H, s.K[g], H, EPI_BIAS | EPI_BF16);
+      jk.g.bias = W->k[g].b;
+      add_src(jk, bop(s.Pb[k], H), bop(s.Wkb[g], H), H);
+      jobs.push_back(jk);
+    }
+    STAGE_TRY("fwd.qk_cvt", launch_cvt_bf16(cv, st));
+    STAGE_TRY("fwd.qkv_gemm", launch_gemm_b16(jobs.data(), (int)jobs.size(), st));
+  } else if (d->num_pairs) {
     std::vector<GemmJob> jobs;
     for (int g = 0; g < d->num_pairs; ++g) {
       const int q = d->pair_q[g], k = d->pair_k[g];
@@ -1128,6 +1186,7 @@ int mmf_hybrid_train_step(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, 
     Bump bs(saved);
     Saved s{};
     layout_saved(d, bs, s);
+    if (bs.off > saved_bytes(d)) return fail(MMF_EINVAL, "internal: saved-buffer layout overflow");
     Bump bw(workspace);
     Ws w;
     layout_ws(d, bw, w);

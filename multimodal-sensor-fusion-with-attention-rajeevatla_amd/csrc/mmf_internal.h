@@ -125,7 +125,8 @@ enum : int32_t {
   EPI_BIAS = 1, EPI_RELU = 2, EPI_DROP = 4, EPI_ROWADD = 8, EPI_GATE = 16,
   EPI_ROWSCALE = 32, EPI_PARTIAL = 64, EPI_BIAS_RS = 128, EPI_ADDMAT = 256,
   EPI_COLSUM = 512,
-  EPI_BF16 = 1024      // store C as bf16 (round to nearest even; C holds __bf16, ldc in elements; nbatch 1)
+  EPI_BF16 = 1024,     // store C as bf16 (round to nearest even; C holds __bf16, ldc in elements; nbatch 1)
+  EPI_BF16COPY = 2048  // also store a bf16 copy of the final C to `copy` (same ldc; nbatch 1, not with EPI_BF16)
 };
 
 // Epilogue order: v = alpha*acc; +bias[j] (x bias_rs[i*ld+off] with EPI_BIAS_RS);
@@ -157,6 +158,7 @@ struct GemmGroup {
   int32_t nbatch;
   int32_t bs_a, bs_b, bs_c, bs_bias, bs_brs;
   int32_t seg_rows;        // rows per segment for operands with seg_stride (a tile never straddles two)
+  void* copy;              // EPI_BF16COPY: __bf16 (M, ldc)
 };
 
 constexpr int GEMM_MAX_GROUPS = 32;   // kernel arguments ~7.8 KB (measured fine on gfx950)
@@ -226,6 +228,16 @@ struct ReduceJob {
   int32_t nsplit, M, N;
   int32_t nbatch, bs_out, bs_db;   // batch i: part += i*nsplit*M*N, out += i*bs_out, db += i*bs_db
 };
+// "medium" GEMMs whose operands are BOTH bf16 copies in HBM (Operand.ptr holds a __bf16 address,
+// ld in elements): RK x RK only, K % 8 == 0, 16-B aligned rows, no split-K / batch / segments.
+// The LDS-DMA kernel's B16 form (DK = 32): half the operand bytes and LDS reads, no conversion.
+hipError_t launch_gemm_b16(const GemmJob* jobs, int njobs, hipStream_t st);
+constexpr int CVT_MAX = 64;
+struct CvtArgs {
+  const float* src[CVT_MAX]; __bf16* dst[CVT_MAX]; int64_t n[CVT_MAX]; int32_t count;
+};
+hipError_t launch_cvt_bf16(const CvtArgs& a, hipStream_t st);
+bool gemm_b16_ok(const GemmJob& J);
 hipError_t launch_reduce(const ReduceJob* jobs, int njobs, hipStream_t st);
 
 // ---------------------------------------------------------------------------

@@ -260,7 +260,10 @@ __global__ __launch_bounds__(NT) void pool_dpbar_grp_kernel(const PoolGrpArgs a)
 #pragma unroll
         for (int row = 0; row < POOL_GRP_ROWS; ++row) {
           if (row < R) {
-            const float4 u = *reinterpret_cast<const float4*>(&dug[row * H + 4 * c4]);
+            // (indexed as float4: with a float pointer and a runtime H the compiler could not prove
+            // 16-B alignment and split the read into ds_read2_b32 pairs, 4-way bank conflicts:
+            // SQ conflict ratio 9.2 in round 3)
+            const float4 u = reinterpret_cast<const float4*>(dug)[row * H4 + c4];
             acc[row] += v.x * u.x + v.y * u.y + v.z * u.z + v.w * u.w;
           }
         }

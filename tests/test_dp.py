@@ -131,7 +131,7 @@ def test_shard_batch_rejects_uneven():
 
 
 # ---------------------------------------------------------------------- GPU
-def _gpu_rank(rank: int, world: int, port: int, out: str) -> None:
+def _gpu_rank(rank: int, world: int, port: int, out: str, accumulate: int = 1) -> None:
     _setup(rank, world, port)
     try:
         from train_step import HybridTrainStep, shard_batch
@@ -142,7 +142,8 @@ def _gpu_rank(rank: int, world: int, port: int, out: str) -> None:
         model = _model().to(dev)
         seed0 = int(model._rng_state[0].item())
         step = HybridTrainStep(model, [f.to(dev) for f in lf], lm.to(dev), ll.to(dev),
-                               process_group=dist.group.WORLD)
+                               process_group=dist.group.WORLD, accumulate=accumulate)
+        assert not step.fuse_clip   # (the clip norm is taken after the exchange)
         # every rank starts from the same seed; the step folds the rank into the Philox key of
         # the module's dropout state (once) and advances that buffer itself
         assert int(step.rng[0].item()) == seed0 ^ (rank * 0x9E3779B1)
@@ -165,10 +166,14 @@ def _gpu_rank(rank: int, world: int, port: int, out: str) -> None:
 
 
 @pytest.mark.gpu
-def test_dp_two_ranks_gpu_matches_single_process():
+@pytest.mark.parametrize("accumulate", [1, 4])
+def test_dp_two_ranks_gpu_matches_single_process(accumulate):
+    """Two ranks on one card (gloo) through the HIP fused step: each rank's shard of the global batch,
+    optionally as `accumulate` micro-batches summed on the device before the one exchange (the
+    reference's gradient_accumulation, config/base.yaml:75), equals one process on the whole batch."""
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "dp_gpu.pt")
-        mp.spawn(_gpu_rank, args=(2, _free_port(), out), nprocs=2, join=True)
+        mp.spawn(_gpu_rank, args=(2, _free_port(), out, accumulate), nprocs=2, join=True)
         r = torch.load(out, weights_only=True)
     full, dp, ref = r["full"], r["dp"], r["oracle"]
     assert (dp - full).abs().max() <= 1e-4 * full.abs().max()

@@ -339,6 +339,8 @@ def test_long_key_one_pass_train_vs_oracle_medium(mods, medium):
     names = [k for _, k, *_ in launches]
     assert any(k.startswith("attn_poolL_fwd_fused_bf16<true") for k in names), names
     assert any(k.startswith("attn_poolL_bwd_fused_bf16<true, ") for k in names), names
+    # the Q / K projections on bf16 copies of P_m and of the weights (qk_gemm_b16)
+    assert "gemm_lds_kernel<0, 0, 32, 3, 1, 1>" in names and "cvt_bf16_kernel" in names, names
 
     def oracle(bf16):
         params = {k: torch.from_numpy(v).requires_grad_(True) for k, v in sd.items()}
