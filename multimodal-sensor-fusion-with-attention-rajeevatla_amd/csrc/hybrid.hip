@@ -1165,8 +1165,10 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
 
 size_t mmf_hybrid_train_sync_bytes(const mmf_hybrid_desc* d) {
   if (check_hybrid(d) != MMF_OK) return 0;
-  const size_t tiles = ((size_t)d->batch + 15) / 16;   // one arrival count per 16-sample tile
-  return std::max<size_t>(256, (4 * tiles + 255) / 256 * 256);
+  // per 16-sample tile: arrivals, head done, done seen, one arrival count per key modality; the
+  // error word (l1.hip SyncWords)
+  const size_t tiles = ((size_t)d->batch + 15) / 16;
+  return std::max<size_t>(256, (4 * (tiles * (3 + L1_MAXM) + 1) + 255) / 256 * 256);
 }
 
 int mmf_hybrid_train_step(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, const float* const* x,
@@ -1180,7 +1182,8 @@ int mmf_hybrid_train_step(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, 
   if (!W || !x || !mask || !labels || !saved || !workspace || !logits || !loss_out || !dlogits || !G)
     return fail(MMF_EINVAL, "null argument");
   if (clip_partial && !step_dev) return fail(MMF_EINVAL, "train step: clip partials need the step counter");
-  if (sync && lean_l1(d, W, x)) {
+  // (the one-launch kernel needs its tiles x pairs workgroups resident at once, one per CU)
+  if (sync && lean_l1(d, W, x) && (int64_t)((d->batch + 15) / 16) * d->num_pairs <= device_cu_count()) {
     MathScope math_(d->matmul_precision);
     hipStream_t st = (hipStream_t)stream;
     Bump bs(saved);

@@ -87,6 +87,13 @@ typedef __attribute__((address_space(1))) unsigned gu32;
 __device__ __forceinline__ void st_wt(float* p, float v) {
   __hip_atomic_store((gfloat*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// 16-B sc1 store at byte offset `off` of a (wave-uniform) tensor base of `bytes` bytes
+__device__ __forceinline__ void st_wt4(float* base, uint32_t bytes, uint32_t off, float4 v) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, bytes, 0x00020000);
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 x = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+  __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, 16);   // aux 16: sc1
+}
 // 16-B sc1 load at byte offset `off` of a (wave-uniform) tensor base of `bytes` bytes
 __device__ __forceinline__ float4 ld_wt4(const float* base, uint32_t bytes, uint32_t off) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, bytes, 0x00020000);
@@ -782,7 +789,8 @@ __device__ __forceinline__ void head_bwd_tile(const L1Args& a, HeadLds& L, const
     const float4 gv = *reinterpret_cast<const float4*>(sm_.gw + m * H + c);
     const float4 v = make_float4((wm * dv.x + dsm * gv.x) * f, (wm * dv.y + dsm * gv.y) * f,
                                  (wm * dv.z + dsm * gv.z) * f, (wm * dv.w + dsm * gv.w) * f);
-    *reinterpret_cast<float4*>(a.cvec + ((int64_t)(b0 + i) * M + m) * H + c) = v;
+    // (sc1: the pair workgroups of the one-launch step read cvec in the same launch)
+    st_wt4(a.cvec, (uint32_t)B * (uint32_t)M * (uint32_t)H * 4u, (uint32_t)((((int64_t)(b0 + i) * M + m) * H + c) * 4), v);
   }
   if (kstamp) {
     L1_ST(2, 6);
@@ -833,6 +841,156 @@ __global__ __launch_bounds__(NT) void l1_head_bwd_kernel(const L1Args a) {
   head_bwd_tile<FH>(a, L, w1, 1);
 }
 
+// ---- the key-modality backward inside the one-launch step (round 4) ----
+// After a tile's head (the last pair workgroup of the tile) has written cvec (sc1 stores) and set
+// the tile's done word, every pair workgroup g = (q, k) of the tile runs its share of what
+// l1_key_bwd_kernel does per key modality: dO = cvec_q W_o, dV = P' dO (stored for dW_v), and
+// dP_k|g = dV W_v (stored sc1); the last of the pairs keyed by k to count (per (tile, k) arrival
+// count) forms dZ_k = gate(cvec_k + sum_g dP_k|g) in pair order (the same sums, bit for bit, as the
+// separate launch) and dX_k = (dZ_k W_k) mask_k input-dropout'.  The waiting workgroups poll the
+// done word relaxed (one lane, s_sleep between polls, bounded: a timeout sets the error word and
+// leaves the tile's outputs unwritten, never a hang); every load of a handed-off byte (cvec, dP,
+// P_k) is an sc1 load.  The grid (tiles x pairs <= 16 x 12 at B = 256) is resident at one
+// workgroup per CU, so every poll ends.
+struct SyncWords {
+  gu32 *cnt, *done, *seen, *mcnt, *err;
+};
+__device__ __forceinline__ SyncWords sync_words(const L1Args& a) {
+  const int tiles = (a.B + S - 1) / S;
+  gu32* base = (gu32*)a.tile_cnt;
+  return SyncWords{base, base + tiles, base + 2 * tiles, base + 3 * tiles, base + (3 + L1_MAXM) * tiles};
+}
+__device__ __forceinline__ bool poll_eq(gu32* w, unsigned want) {
+  for (unsigned i = 0; i < (1u << 22); ++i) {
+    if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == want) return true;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return false;
+}
+__device__ __forceinline__ float ld_wt(const float* p) {
+  return __hip_atomic_load((gfloat*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int FH>
+__device__ __forceinline__ void pair_key_bwd(const L1Args& a, PairLds& L, const RngSnap& rs, int* flag) {
+  const int g = blockIdx.y, b0 = blockIdx.x * S, tile = blockIdx.x;
+  const int q = a.pq[g], k = a.pk[g];
+  const int H = FH ? FH : a.H, D = FH ? FH : a.D[k], B = a.B, M = a.M;
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6) & 3;
+  float* cs = L.xs;
+  float* vs = L.ps;
+  float* zs = L.os;
+  float* pp = L.pp;
+  uint8_t* kin = L.kin;
+  float* msk = L.msk;
+  L1_RT(3, 8);
+  L1_ST(3, 0);
+  // cvec_q rows of the tile (sc1: the head wrote them in this launch), P' of the pair, W_o / W_v
+  {
+    const int h4 = H / 4;
+    const uint32_t nbytes = (uint32_t)B * (uint32_t)M * (uint32_t)H * 4u;
+    float4 v[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = t + u * NT, i = min(e / h4, S - 1), c = e - (e / h4) * h4;
+      v[u] = ld_wt4(a.cvec, nbytes, (uint32_t)((((int64_t)min(b0 + i, B - 1) * M + q) * H + 4 * c) * 4));
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = t + u * NT, i = e / h4, c = e - i * h4;
+      if (i < S) *reinterpret_cast<float4*>(cs + i * LD + 4 * c) = b0 + i < B ? v[u] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  WTile wo, wv;
+  wload_nn(a.Wo[g], H, H, wave, lane, wo);
+  wload_nn(a.Wv[g], H, H, wave, lane, wv);
+  pprime_tile(a, rs, g, b0, pp);
+  zero_pad(cs, H);
+  __syncthreads();
+  const int kq = lane >> 4, jl = lane & 15, hd = H / a.heads;
+  f32x4 acc[NTL];
+  mma(cs, wo, acc, lane);
+#pragma unroll
+  for (int u = 0; u < NTL; ++u) {
+    const int j = 16 * (wave + 4 * u) + jl;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int ii = 4 * kq + r;
+      const float v = j < H ? acc[u][r] * pp[ii * a.heads + j / hd] : 0.f;
+      vs[ii * LD + j] = v;
+      if (b0 + ii < B && j < H) a.dV[g][(int64_t)(b0 + ii) * H + j] = v;
+    }
+  }
+  __syncthreads();
+  mma(vs, wv, acc, lane);
+#pragma unroll
+  for (int u = 0; u < NTL; ++u) {
+    const int j = 16 * (wave + 4 * u) + jl;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int ii = 4 * kq + r;
+      if (b0 + ii < B && j < H) st_wt(a.dPk[g] + (int64_t)(b0 + ii) * H + j, acc[u][r]);   // (handed off)
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const SyncWords sw = sync_words(a);
+  const int npk = a.npairs / M;   // pairs keyed by each modality (every ordered pair present)
+  if (t == 0) {
+    gu32* mc = sw.mcnt + tile * L1_MAXM + k;
+    const bool lastk = __hip_atomic_fetch_add(mc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(npk - 1);
+    if (lastk) __hip_atomic_store(mc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = lastk;
+  }
+  __syncthreads();
+  L1_ST(3, 1);
+  L1_RT(3, 9);
+  if (!*flag) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // the last of k's pairs: dZ_k = ReLU' Drop' (cvec_k + sum_g dP_k|g) (P_k post-dropout: > 0 marks
+  // kept, active units), in the accumulator layout; then dX_k
+  const bool want_dx = a.dx[k] != nullptr;
+  WTile wp;
+  if (want_dx) wload_nn(a.Wp[k], D, H, wave, lane, wp);
+  if (t < S) msk[t] = b0 + t < B ? a.mask[(int64_t)min(b0 + t, B - 1) * M + k] : 0.f;
+  if (a.p > 0.f && want_dx) keep_tile(rs, SITE_IN + k, b0, D, a.p, kin);
+#pragma unroll
+  for (int u = 0; u < NTL; ++u) {
+    const int j = 16 * (wave + 4 * u) + jl;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int ii = 4 * kq + r;
+      float z = 0.f;
+      if (b0 + ii < B && j < H) {
+        const int64_t row = (int64_t)(b0 + ii) * H + j;
+        float dp = 0.f;
+        for (int gg = 0; gg < a.npairs; ++gg)
+          if (a.pk[gg] == k) dp += ld_wt(a.dPk[gg] + row);
+        const float c = ld_wt(a.cvec + ((int64_t)(b0 + ii) * M + k) * H + j);
+        z = ld_wt(a.P[k] + row) > 0.f ? (c + dp) * a.gscale : 0.f;
+        a.dZ[k][row] = z;
+      }
+      zs[ii * LD + j] = z;
+    }
+  }
+  if (!want_dx) return;
+  __syncthreads();
+  mma(zs, wp, acc, lane);
+#pragma unroll
+  for (int u = 0; u < NTL; ++u) {
+    const int j = 16 * (wave + 4 * u) + jl;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int ii = 4 * kq + r;
+      if (b0 + ii >= B || j >= D) continue;
+      float v = acc[u][r] * msk[ii];
+      if (a.p > 0.f) v = kept(kin, b0, D, ii, j) ? v * a.gscale : 0.f;
+      a.dx[k][(int64_t)(b0 + ii) * D + j] = v;
+    }
+  }
+}
+
 // The forward, the loss and the head backward of a training step in one launch over (tile,
 // pair): every workgroup runs its pair's forward (pair_fwd_tile); the last of a tile's pair
 // workgroups to finish (a per-tile arrival count; every workgroup's stores released before it
@@ -845,32 +1003,58 @@ template <int FH>
 __global__ __launch_bounds__(NT) void l1_fwd_loss_kernel(const L1Args a) {
   // (LDS over 80 KB: one workgroup per CU, the residency the hand-off protocol was measured at)
   __shared__ __attribute__((aligned(16))) union Lds { PairLds p; HeadLds h; char pad[82 * 1024]; } L;
-  __shared__ int last;
+  __shared__ int last, flag;
+  const int tile = blockIdx.x;
   const RngSnap rs = pair_fwd_tile<FH>(a, L.p);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
   __syncthreads();
   L1_ST(0, 6);
+  const SyncWords sw = sync_words(a);
   if (threadIdx.x == 0)
-    last = __hip_atomic_fetch_add((gu32*)(a.tile_cnt + blockIdx.x), 1u, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(a.npairs - 1);
+    last = __hip_atomic_fetch_add(sw.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+           (unsigned)(a.npairs - 1);
   __syncthreads();
   L1_ST(0, 7);
-  if (!last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (keeps the sc1 loads behind the count)
-  if (threadIdx.x == 0)   // every pair workgroup of this tile has counted: back to 0 for the next call
-    __hip_atomic_store((gu32*)(a.tile_cnt + blockIdx.x), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int H = FH ? FH : a.H;
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) & 3;
-  head_fwd_tile<FH>(a, L.h, rs, 1);
-  WTile w1n;
-  wload_nn(a.W1, H, H, wave, lane, w1n);   // (in flight through the loss)
-  __syncthreads();
-  loss_tile(a, L.h);
-  __syncthreads();
-  L1_RT(2, 8);
-  L1_ST(2, 0);
-  L1_ST(2, 1);
-  head_bwd_tile<FH>(a, L.h, w1n, 1);
+  if (last) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (keeps the sc1 loads behind the count)
+    if (threadIdx.x == 0)   // every pair workgroup of this tile has counted: back to 0 for the next call
+      __hip_atomic_store(sw.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    head_fwd_tile<FH>(a, L.h, rs, 1);
+    const int H = FH ? FH : a.H;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) & 3;
+    WTile w1n;
+    wload_nn(a.W1, H, H, wave, lane, w1n);   // (in flight through the loss)
+    __syncthreads();
+    loss_tile(a, L.h);
+    __syncthreads();
+    L1_RT(2, 8);
+    L1_ST(2, 0);
+    L1_ST(2, 1);
+    head_bwd_tile<FH>(a, L.h, w1n, 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // cvec (sc1) drained by every wave
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(sw.done + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    if (threadIdx.x == 0) {
+      const bool ok = poll_eq(sw.done + tile, 1u);
+      if (ok) {
+        // the last of the tile's waiting workgroups to see the head done returns the words to 0
+        if (__hip_atomic_fetch_add(sw.seen + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            (unsigned)(a.npairs - 2)) {
+          __hip_atomic_store(sw.seen + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(sw.done + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      } else {
+        __hip_atomic_store(sw.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      flag = ok;
+    }
+    __syncthreads();
+    if (!flag) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  __syncthreads();   // (the head's LDS becomes the pair backward's)
+  pair_key_bwd<FH>(a, L.p, rs, &flag);
 }
 
 // Backward of everything keyed by one modality m, per 16-sample tile (tile, m): for every pair
@@ -996,12 +1180,13 @@ __global__ __launch_bounds__(NT) void l1_wgrad_kernel(const L1WgArgs w) {
   __shared__ float bred[4][32];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   int tile = blockIdx.x;
-  if ((w.loss || w.clip_partial) && tile == gridDim.x - 1) {
+  if ((w.loss || w.clip_partial || w.rng_advance) && tile == gridDim.x - 1) {
     // the extra workgroup: the batch-mean loss in cross_entropy_kernel's order (per-thread strided
     // sums, then a tree); the clip partial slots no tile fills zeroed; the step counter advanced
     if (w.clip_partial)
       for (int s = w.ntiles + t; s < CLIP_PARTIAL_SLOTS; s += NT) w.clip_partial[s] = 0.f;
     if (w.step_incr && t == 0) w.step_incr[0] += 1;
+    if (w.rng_advance && t == 0) w.rng_advance[1] += 1;   // (launch_l1_train: every forward workgroup has read it)
     if (!w.loss) return;
     __shared__ float lred[NT];
     float acc = 0.f;
@@ -1176,7 +1361,7 @@ hipError_t launch_l1_backward(const L1Args& a, const L1WgArgs& w, hipStream_t st
   return hipGetLastError();
 }
 
-hipError_t launch_l1_train(const L1Args& a, const L1WgArgs& w, hipStream_t st) {
+hipError_t launch_l1_train(const L1Args& a, const L1WgArgs& w_in, hipStream_t st) {
   if (a.M > L1_MAXM || a.npairs > L1_MAXP || a.H > L1_MAXH || a.H % 4 != 0 || a.C > L1_MAXC || a.heads > 8)
     return hipErrorInvalidValue;
   if (a.npairs != a.M * (a.M - 1) || a.M < 2 || !a.tile_cnt || !a.labels || !a.loss_rows || !a.dlogits_out)
@@ -1184,6 +1369,8 @@ hipError_t launch_l1_train(const L1Args& a, const L1WgArgs& w, hipStream_t st) {
   for (int m = 0; m < a.M; ++m)
     if (a.D[m] > L1_MAXD || a.D[m] % 4 != 0) return hipErrorInvalidValue;
   const unsigned tiles = (unsigned)((a.B + S - 1) / S);
+  // every workgroup of the one-launch kernel resident at once (one per CU): its polls end
+  if (tiles * (unsigned)a.npairs > (unsigned)device_cu_count()) return hipErrorInvalidValue;
   const double B = a.B, H = a.H;
   const bool full = l1_full(a);
   hipError_t e;
@@ -1195,34 +1382,22 @@ hipError_t launch_l1_train(const L1Args& a, const L1WgArgs& w, hipStream_t st) {
       fl += 2.0 * B * H * (D + 2.0 * H);
       by += 4.0 * (B * (D + 2.0 * H) + H * (D + 2.0 * H));
     }
-    L1Args af = a;
-    af.rng_advance = nullptr;   // (advanced by the key-modality backward launch)
-    ProfLaunch prof_(st, full ? "l1_fwd_loss_kernel<128>" : "l1_fwd_loss_kernel<0>", fl, by);
-    if (full) mmf_launch(l1_fwd_loss_kernel<128>, dim3(tiles, a.npairs), dim3(NT), 0, st, af);
-    else mmf_launch(l1_fwd_loss_kernel<0>, dim3(tiles, a.npairs), dim3(NT), 0, st, af);
-  }
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  {
-    double fl = 0.0, by = 0.0;
+    // the key-modality backward (in the same launch)
     for (int m = 0; m < a.M; ++m) {
       fl += a.dx[m] ? 2.0 * B * H * a.D[m] : 0.0;
       by += 4.0 * (B * H * 2 + (a.dx[m] ? B * a.D[m] + H * a.D[m] : 0.0));
     }
     fl += 4.0 * B * H * H * a.npairs;
     by += 4.0 * a.npairs * (2.0 * B * H + 2.0 * H * H);
-    const int npk = a.npairs / a.M;
-    ProfLaunch prof_(st, full ? "l1_key_bwd_kernel<128>" : "l1_key_bwd_kernel<0>", fl, by);
-    const dim3 grid(tiles, a.M);
-#define L1_KEY(FH)                                                                     \
-    switch (npk) {                                                                     \
-      case 1: mmf_launch(l1_key_bwd_kernel<FH, 1>, grid, dim3(NT), 0, st, a); break;   \
-      case 2: mmf_launch(l1_key_bwd_kernel<FH, 2>, grid, dim3(NT), 0, st, a); break;   \
-      default: mmf_launch(l1_key_bwd_kernel<FH, 3>, grid, dim3(NT), 0, st, a); break;  \
-    }
-    if (full) { L1_KEY(128) } else { L1_KEY(0) }
-#undef L1_KEY
+    L1Args af = a;
+    af.rng_advance = nullptr;   // (advanced by the weight-gradient launch)
+    ProfLaunch prof_(st, full ? "l1_fwd_loss_kernel<128>" : "l1_fwd_loss_kernel<0>", fl, by);
+    if (full) mmf_launch(l1_fwd_loss_kernel<128>, dim3(tiles, a.npairs), dim3(NT), 0, st, af);
+    else mmf_launch(l1_fwd_loss_kernel<0>, dim3(tiles, a.npairs), dim3(NT), 0, st, af);
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  L1WgArgs w = w_in;
+  w.rng_advance = a.rng_advance;
   double fl = 0.0, by = 0.0;
   for (int i = 0; i < w.njobs; ++i) {
     const L1WgJob& J = w.j[i];
@@ -1233,7 +1408,8 @@ hipError_t launch_l1_train(const L1Args& a, const L1WgArgs& w, hipStream_t st) {
   for (int i = 0; i < w.nz; ++i) by += 4.0 * w.zn[i];
   ProfLaunch prof_(st, "l1_wgrad_kernel", fl, by);
   if (w.clip_partial && w.ntiles > CLIP_PARTIAL_SLOTS) return hipErrorInvalidValue;
-  mmf_launch(l1_wgrad_kernel, dim3((unsigned)(w.ntiles + zblocks + ((w.loss || w.clip_partial) ? 1 : 0))), dim3(NT), 0, st, w);
+  const bool extra = w.loss || w.clip_partial || w.rng_advance;
+  mmf_launch(l1_wgrad_kernel, dim3((unsigned)(w.ntiles + zblocks + (extra ? 1 : 0))), dim3(NT), 0, st, w);
   return hipGetLastError();
 }
 

@@ -573,7 +573,8 @@ struct L1Args {
   float *dz1, *cvec, *dscore;
   float *dV[L1_MAXP], *dPk[L1_MAXP], *dZ[L1_MAXM], *dx[L1_MAXM];
   // the one-launch forward + loss + head backward of a training step (launch_l1_train)
-  uint32_t* tile_cnt;                 // per-tile arrival counts (zero between calls)
+  uint32_t* tile_cnt;                 // the one-launch step's sync words (zero between calls):
+                                      // tiles x (arrivals, head done, seen, L1_MAXM key arrivals), error
   const int64_t* labels;
   float ls_eps, loss_scale;           // label smoothing; dlogits scale (1 / accumulation steps)
   float* loss_rows;                   // (B) per-sample loss
@@ -591,6 +592,7 @@ struct L1WgArgs {
   const float* loss_rows; float* loss;   // optional: loss = mean of loss_rows (one extra workgroup)
   float* clip_partial;                   // optional: squared-norm partial per output tile (CLIP_PARTIAL_SLOTS)
   int64_t* step_incr;                    // optional: the optimizer step counter, advanced once
+  uint64_t* rng_advance;                 // optional: the live dropout state's offset, advanced once
 };
 hipError_t launch_l1_forward(const L1Args& a, hipStream_t st);
 hipError_t launch_l1_backward(const L1Args& a, const L1WgArgs& w, hipStream_t st);

@@ -34,7 +34,7 @@ KERNELS = [
     ("l1_head_fwd (last pair workgroup of a tile)", ["loads+keep", "pooled", "gating", "adaptive", "fused", "h1",
                                                      "logits"]),
     ("l1_head_bwd (loss + head backward)", ["loss", "dz1", "dfused", "dw", "adaptive bwd", "cvec"]),
-    ("l1_key_bwd", ["loads+keep", "pairs dO/dV/dP", "dZ", "dX"]),
+    ("l1_key_bwd (pair part, after the head)", ["cvec + W_o/W_v + dO/dV/dP + count"]),
     ("l1_wgrad", ["main loop", "reduce + store"]),
 ]
 
@@ -57,7 +57,7 @@ def main():
     buf = np.zeros((5, 1024, 10), dtype=np.uint64)
     assert L.mmf_l1_stamps_read(buf.ctypes.data, buf.nbytes) == 0
     tiles = (w["B"] + 15) // 16
-    nwg = [tiles * 6, None, None, tiles * 3, None]
+    nwg = [tiles * 6, None, None, tiles * 6, None]
     out = {"kernels": {}}
     spans = []
     t_first = int(buf[0, :tiles * 6, 8].astype(np.int64).min())   # this replay's first pair workgroup

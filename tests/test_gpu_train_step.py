@@ -216,11 +216,13 @@ def _three_calls(st, nat):
 @pytest.mark.parametrize("seq", [False, True])
 def test_one_call_train_step_matches_three_calls(mods, seq):
     """mmf_hybrid_train_step (HybridTrainStep's forward + CE + backward: on the 2-D single-key plan
-    one launch for the forward, the loss and the head backward, a per-tile arrival count handing
-    each tile to the last of its pair workgroups) against forward -> cross-entropy -> backward as
-    three calls, train mode with dropout, two consecutive steps: the same logits, loss, dlogits,
+    one launch for the forward, the loss, the head backward and the key-modality backward -- a
+    per-tile arrival count hands each tile to the last of its pair workgroups, which runs the head
+    while the others wait on its done word, then per-(tile, key) counts pick the workgroup that
+    forms dZ / dX -- and one for the weight gradients) against forward -> cross-entropy -> backward
+    as three calls, train mode with dropout, two consecutive steps: the same logits, loss, dlogits,
     fusion weights, parameter and input gradients bit for bit, the dropout stream advanced once
-    per step, and the arrival counts back at zero."""
+    per step, and every sync word (counts, done / seen words, the poll-timeout error word) at zero."""
     import mmf_native as nat
     fusion, train_step = mods
     feats, mask, labels = _batch(11)
@@ -242,7 +244,7 @@ def test_one_call_train_step_matches_three_calls(mods, seq):
         names = [k for _, k, *_ in launches]
         if not split and not seq:
             assert any(k.startswith("l1_fwd_loss_kernel") for k in names), names
-            assert not any(k.startswith("cross_entropy_kernel") or k.startswith("l1_head") for k in names), names
+            assert not any(k.startswith(("cross_entropy_kernel", "l1_head", "l1_key_bwd")) for k in names), names
             assert int(st.sync.count_nonzero()) == 0
         runs.append(outs)
     for step_a, step_b in zip(*runs):
