@@ -477,21 +477,94 @@ struct HeadLds {
   float hs[S * LD];               // h1 (forward) -> dfused (backward)
   HeadSmall sm;
   uint8_t kcl[KB_BYTES];
-  float msk[S * L1_MAXM], sc[S * L1_MAXM], wt[S * L1_MAXM], dw[S * L1_MAXM], dsc[S * L1_MAXM];
-  float lg[S * L1_MAXC], dl[S * L1_MAXC];   // logits, dlogits rows
+  float msk[S * L1_MAXM], sc[S * L1_MAXM];   // mask, gating score rows
+  float dl[S * L1_MAXC];                       // dlogits rows (the standalone head backward)
 };
+
+// Row group of the head's per-sample phases: the 16 lanes t / 16 == i own sample i of the tile
+// (NT / 16 == S groups), lane l16 its float4 columns l16 and l16 + 16 (H <= 128).  A 16-lane sum
+// (sum16) leaves a dot product in every lane of the group, so a chain of per-sample steps (scores
+// -> adaptive weights -> fused, logits -> loss -> dz1, d weights -> adaptive backward -> cvec)
+// runs with no barrier between its steps.
+struct RowGroup {
+  int i, l16;
+  __device__ RowGroup() : i(threadIdx.x >> 4), l16(threadIdx.x & 15) {}
+};
+static_assert(NT / 16 == S, "one 16-lane group per sample of the tile");
+
+// CrossEntropyLoss(label_smoothing) of sample b (src/train.py:185-186, 310) with the arithmetic of
+// head.hip's cross_entropy_kernel, in every lane of its row group: the per-sample loss into
+// loss_rows (the batch mean is taken in the wgrad launch, in the standalone kernel's order), dlogits
+// = (softmax - target) / B * loss_scale into dl and the caller's buffer (zeros past B)
+__device__ __forceinline__ void loss_rows(const L1Args& a, const RowGroup& rg, int b, int y, const float (&z)[L1_MAXC],
+                                          float (&dl)[L1_MAXC]) {
+  const int C = a.C, B = a.B;
+  const float eps = a.ls_eps;
+  float mx = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < L1_MAXC; ++c)
+    if (c < C) mx = fmaxf(mx, z[c]);
+  float se = 0.f, sz = 0.f, zy = 0.f;
+#pragma unroll
+  for (int c = 0; c < L1_MAXC; ++c) {
+    if (c >= C) break;
+    se += __expf(z[c] - mx);
+    sz += z[c];
+    if (c == y) zy = z[c];
+  }
+  const float lse = mx + __logf(se);
+  if (b < B && rg.l16 == 0) a.loss_rows[b] = (1.f - eps) * (lse - zy) + eps * (lse - sz / (float)C);
+#pragma unroll
+  for (int c = 0; c < L1_MAXC; ++c) {
+    dl[c] = 0.f;
+    if (c >= C) continue;
+    const float pc = __expf(z[c] - lse);
+    const float tgt = (c == y ? (1.f - eps) : 0.f) + eps / (float)C;
+    dl[c] = b < B ? (pc - tgt) / (float)B * a.loss_scale : 0.f;
+    if (b < B && rg.l16 == c) a.dlogits_out[(int64_t)b * C + c] = dl[c];
+  }
+}
+
+// dz1 = ReLU' Drop' (dlogits W2) of the row group's sample (its float4 columns; hv: its h1 columns,
+// post-dropout, so h1 > 0 marks kept, active units) into L.fs and the saved dz1
+template <int FH>
+__device__ __forceinline__ void dz1_rows(const L1Args& a, HeadLds& L, const RowGroup& rg, const float4 (&hv)[2],
+                                         const float (&dl)[L1_MAXC]) {
+  const int H = FH ? FH : a.H, h4 = H / 4, C = a.C, b = blockIdx.x * S + rg.i;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int c4 = rg.l16 + 16 * q;
+    if (c4 >= h4) continue;
+    const float hvv[4] = {hv[q].x, hv[q].y, hv[q].z, hv[q].w};
+    // (the classes unrolled over L1_MAXC: one float4 W2 read per class, the same summation order)
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int cc = 0; cc < L1_MAXC; ++cc) {
+      if (cc >= C) break;
+      const float4 w2 = *reinterpret_cast<const float4*>(L.sm.w2 + cc * H + 4 * c4);
+      acc[0] += dl[cc] * w2.x; acc[1] += dl[cc] * w2.y; acc[2] += dl[cc] * w2.z; acc[3] += dl[cc] * w2.w;
+    }
+    float z[4];
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) z[s4] = (b < a.B && hvv[s4] > 0.f) ? acc[s4] * a.gscale : 0.f;
+    const float4 zv = make_float4(z[0], z[1], z[2], z[3]);
+    *reinterpret_cast<float4*>(L.fs + rg.i * LD + 4 * c4) = zv;
+    if (b < a.B) *reinterpret_cast<float4*>(a.dz1 + (int64_t)b * H + 4 * c4) = zv;
+  }
+}
+
 
 // Head forward of tile blockIdx.x (src/fusion.py:406-427, :429-479): pooled, gating scores,
 // adaptive weights, fused, h1 = Drop(ReLU(fused W1^T + b1)), logits.  Leaves pooled (pl), the
 // mask / score / weight rows, h1 (hs) and the logits (lg) in L.  rs: the call's rng snapshot.
-template <int FH>
-__device__ __forceinline__ void head_fwd_tile(const L1Args& a, HeadLds& L, const RngSnap& rs, int kstamp) {
+template <int FH, bool LOSS>
+__device__ __forceinline__ void head_fwd_tile(const L1Args& a, HeadLds& L, const RngSnap& rs, int kstamp, WTile* w1n) {
   float* pl = L.pl;
   float* fs = L.fs;
   float* hs = L.hs;
   HeadSmall& sm_ = L.sm;
   uint8_t* kcl = L.kcl;
-  float *msk = L.msk, *sc = L.sc, *wt = L.wt;
+  float *msk = L.msk, *sc = L.sc;
   const int b0 = blockIdx.x * S;
   const int M = a.M, H = FH ? FH : a.H, B = a.B, C = a.C;
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6) & 3;
@@ -561,53 +634,64 @@ __device__ __forceinline__ void head_fwd_tile(const L1Args& a, HeadLds& L, const
   }
   __syncthreads();
   if (kstamp) L1_ST(1, 2);
-  // gating scores (nn.Linear(H, 1), src/fusion.py:452-461): 16 lanes per dot
+  // gating scores (nn.Linear(H, 1), src/fusion.py:452-461), the adaptive weights (:462-478) and
+  // fused = sum_m w_m pooled_m (:413-418) of sample i by the 16 lanes of row group i (RowGroup):
+  // the 16-lane sums leave the M scores in every lane of the group, so the three need no barrier
   {
-    const int grp = t >> 4, l16 = t & 15;
-    for (int d = grp; d < S * M; d += NT / 16) {
-      const int i = d / M, m = d - i * M;
-      float s = 0.f;
-      for (int j = l16; j < H; j += 16) s += pl[(m * S + i) * LD + j] * sm_.gw[m * H + j];
-      s = sum16(s);
-      if (l16 == 0) sc[i * M + m] = s + sm_.gb[m];
-    }
-  }
-  __syncthreads();
-  if (kstamp) L1_ST(1, 3);
-  if (t < S) {
-    float smx[L1_MAXM], w[L1_MAXM];
-    adaptive(M, sc + t * M, msk + t * M, smx, w);
+    const RowGroup rg;
+    const bool in = b0 + rg.i < B;
+    float4 pr[2][L1_MAXM];
+    float s[L1_MAXM], mr[L1_MAXM];
 #pragma unroll
     for (int m = 0; m < L1_MAXM; ++m) {
-      if (m >= M) break;
-      wt[t * M + m] = w[m];
-      if (b0 + t < B) {
-        a.scores[(int64_t)(b0 + t) * M + m] = sc[t * M + m];
-        a.weights[(int64_t)(b0 + t) * M + m] = w[m];
-        if (a.weights_out) a.weights_out[(int64_t)(b0 + t) * M + m] = w[m];
+      float d = 0.f;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int c4 = rg.l16 + 16 * q;
+        pr[q][m] = (m < M && c4 < h4) ? *reinterpret_cast<const float4*>(pl + (m * S + rg.i) * LD + 4 * c4)
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 gv = (m < M && c4 < h4) ? *reinterpret_cast<const float4*>(sm_.gw + m * H + 4 * c4)
+                                             : make_float4(0.f, 0.f, 0.f, 0.f);
+        d += pr[q][m].x * gv.x + pr[q][m].y * gv.y + pr[q][m].z * gv.z + pr[q][m].w * gv.w;
+      }
+      d = sum16(d);
+      s[m] = m < M ? d + sm_.gb[m] : 0.f;
+      mr[m] = m < M ? msk[rg.i * M + m] : 0.f;
+    }
+    float smx[L1_MAXM], w[L1_MAXM];
+    adaptive(M, s, mr, smx, w);
+#pragma unroll
+    for (int m = 0; m < L1_MAXM; ++m) {
+      if (m < M && rg.l16 == m) {
+        sc[rg.i * M + m] = s[m];
+        if (in) {
+          a.scores[(int64_t)(b0 + rg.i) * M + m] = s[m];
+          a.weights[(int64_t)(b0 + rg.i) * M + m] = w[m];
+          if (a.weights_out) a.weights_out[(int64_t)(b0 + rg.i) * M + m] = w[m];
+        }
       }
     }
-  }
-  __syncthreads();
-  if (kstamp) L1_ST(1, 4);
-  // fused = sum_m w_m pooled_m (src/fusion.py:413-418), float4 per thread
-  for (int e = t; e < S * h4; e += NT) {
-    const int i = e / h4, c = 4 * (e - i * h4);
-    float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int m = 0; m < M; ++m) {
-      const float4 v = *reinterpret_cast<const float4*>(pl + (m * S + i) * LD + c);
-      const float wm = wt[i * M + m];
-      f.x += v.x * wm; f.y += v.y * wm; f.z += v.z * wm; f.w += v.w * wm;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int c4 = rg.l16 + 16 * q;
+      if (c4 >= h4) continue;
+      float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int m = 0; m < L1_MAXM; ++m) {
+        if (m >= M) break;
+        f.x += pr[q][m].x * w[m]; f.y += pr[q][m].y * w[m]; f.z += pr[q][m].z * w[m]; f.w += pr[q][m].w * w[m];
+      }
+      *reinterpret_cast<float4*>(fs + rg.i * LD + 4 * c4) = f;
+      if (in) *reinterpret_cast<float4*>(a.fused + (int64_t)(b0 + rg.i) * H + 4 * c4) = f;
     }
-    *reinterpret_cast<float4*>(fs + i * LD + c) = f;
-    if (b0 + i < B) *reinterpret_cast<float4*>(a.fused + (int64_t)(b0 + i) * H + c) = f;
   }
   zero_pad(fs, H);
   __syncthreads();
-  if (kstamp) L1_ST(1, 5);
+  if (kstamp) L1_ST(1, 3);
   // h1 = Drop(ReLU(fused W1^T + b1)) (classifier[0..2], src/fusion.py:323-328)
   f32x4 acc[NTL];
   mma(fs, w1, acc, lane);
+  if constexpr (LOSS) wload_nn(a.W1, H, H, wave, lane, *w1n);   // (the backward's W1 columns: in flight through the loss)
   const int kq = lane >> 4, jl = lane & 15;
 #pragma unroll
   for (int u = 0; u < NTL; ++u) {
@@ -623,100 +707,61 @@ __device__ __forceinline__ void head_fwd_tile(const L1Args& a, HeadLds& L, const
     }
   }
   __syncthreads();
-  if (kstamp) L1_ST(1, 6);
-  // logits = h1 W2^T + b2 (classifier[3])
+  if (kstamp) L1_ST(1, 4);
+  // logits = h1 W2^T + b2 (classifier[3]) of sample i by row group i; with LOSS the group goes on
+  // with the sample's cross-entropy and dz1 (loss_dz1_rows), no barrier between
   {
-    const int grp = t >> 4, l16 = t & 15;
-    for (int d = grp; d < S * C; d += NT / 16) {
-      const int i = d / C, c = d - i * C;
-      float s = 0.f;
-      for (int j = l16; j < H; j += 16) s += hs[i * LD + j] * sm_.w2[c * H + j];
-      s = sum16(s);
-      if (l16 == 0) {
-        s += sm_.b2[c];
-        L.lg[i * C + c] = s;
-        if (b0 + i < B) a.logits[(int64_t)(b0 + i) * C + c] = s;
+    const RowGroup rg;
+    const int b = b0 + rg.i;
+    int y = 0;
+    if constexpr (LOSS) y = b < B ? (int)a.labels[b] : 0;
+    float4 hv[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int c4 = rg.l16 + 16 * q;
+      hv[q] = c4 < h4 ? *reinterpret_cast<const float4*>(hs + rg.i * LD + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float z[L1_MAXC];
+#pragma unroll
+    for (int cc = 0; cc < L1_MAXC; ++cc) {
+      if (cc >= C) break;
+      float d = 0.f;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int c4 = rg.l16 + 16 * q;
+        const float4 w2 = c4 < h4 ? *reinterpret_cast<const float4*>(sm_.w2 + cc * H + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        d += hv[q].x * w2.x + hv[q].y * w2.y + hv[q].z * w2.z + hv[q].w * w2.w;
       }
+      z[cc] = sum16(d) + sm_.b2[cc];
+      if (rg.l16 == cc && b < B) a.logits[(int64_t)b * C + cc] = z[cc];
+    }
+    if constexpr (LOSS) {
+      float dlv[L1_MAXC];
+      loss_rows(a, rg, b, y, z, dlv);
+      dz1_rows<FH>(a, L, rg, hv, dlv);
     }
   }
   if (kstamp) {
-    L1_ST(1, 7);
+    L1_ST(1, 5);
     L1_RT(1, 9);
   }
 }
 
-// CrossEntropyLoss(label_smoothing) of the tile's samples (src/train.py:185-186, 310) with the
-// arithmetic of head.hip's cross_entropy_kernel: the per-sample loss into loss_rows (the batch
-// mean is taken in the wgrad launch, in the standalone kernel's order), dlogits = (softmax -
-// target) / B * loss_scale into L.dl and the caller's buffer
-__device__ __forceinline__ void loss_tile(const L1Args& a, HeadLds& L) {
-  const int t = threadIdx.x, b0 = blockIdx.x * S, C = a.C, B = a.B;
-  if (t < S) {
-    const int b = b0 + t;
-    const float eps = a.ls_eps;
-    if (b < B) {
-      const float* z = L.lg + t * C;
-      float mx = -INFINITY;
-      for (int c = 0; c < C; ++c) mx = fmaxf(mx, z[c]);
-      float se = 0.f, sz = 0.f;
-      for (int c = 0; c < C; ++c) { se += __expf(z[c] - mx); sz += z[c]; }
-      const float lse = mx + __logf(se);
-      const int y = (int)a.labels[b];
-      a.loss_rows[b] = (1.f - eps) * (lse - z[y]) + eps * (lse - sz / (float)C);
-      for (int c = 0; c < C; ++c) {
-        const float pc = __expf(z[c] - lse);
-        const float tgt = (c == y ? (1.f - eps) : 0.f) + eps / (float)C;
-        const float d = (pc - tgt) / (float)B * a.loss_scale;
-        L.dl[t * C + c] = d;
-        a.dlogits_out[(int64_t)b * C + c] = d;
-      }
-    } else {
-      for (int c = 0; c < C; ++c) L.dl[t * C + c] = 0.f;
-    }
-  }
-}
-
-// Head backward of tile blockIdx.x: dz1 = ReLU' Drop' (dlogits W2), dfused = dz1 W1, d weights,
-// compute_adaptive_weights backward, cvec_m (the gradient of every entry of m's aggregation list).
-// Reads dl, pl, hs (h1), msk / sc / wt and sm from L (the forward left them there, or the
-// standalone kernel staged them); w1n: this wave's W1 columns in y = x W form.
+// Head backward of tile blockIdx.x from dz1 (L.fs, zero-padded past H; dz1_rows wrote it):
+// dfused = dz1 W1, d weights, compute_adaptive_weights backward, cvec_m (the gradient of every
+// entry of m's aggregation list).  Reads pl, msk / sc and sm from L (the forward left them there,
+// or the standalone kernel staged them); w1n: this wave's W1 columns in y = x W form.
 template <int FH>
 __device__ __forceinline__ void head_bwd_tile(const L1Args& a, HeadLds& L, const WTile& w1n, int kstamp) {
   float* pl = L.pl;
   float* zs = L.fs;
-  float* dfs = L.hs;   // (h1 until the dz1 phase has read it)
+  float* dfs = L.hs;   // (h1 until dz1_rows has read it)
   HeadSmall& sm_ = L.sm;
-  float *dl = L.dl, *msk = L.msk, *sc = L.sc, *wt = L.wt, *dw = L.dw, *dsc = L.dsc;
+  float *msk = L.msk, *sc = L.sc;
   const int b0 = blockIdx.x * S;
-  const int M = a.M, H = FH ? FH : a.H, B = a.B, C = a.C;
+  const int M = a.M, H = FH ? FH : a.H, B = a.B;
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6) & 3;
   const int h4 = H / 4;
-  // dz1 = ReLU' Drop' (dlogits W2): the saved h1 is post-dropout, so h1 > 0 marks kept, active units
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int e = t + u * NT, i = e / h4, c = 4 * (e - i * h4);
-    if (i >= S) continue;
-    const float4 hv = *reinterpret_cast<const float4*>(L.hs + i * LD + c);
-    const float hvv[4] = {hv.x, hv.y, hv.z, hv.w};
-    // (the classes unrolled over L1_MAXC: one float4 W2 read per class, the same summation order)
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int cc = 0; cc < L1_MAXC; ++cc) {
-      if (cc >= C) break;
-      const float dv = dl[i * C + cc];
-      const float4 w2 = *reinterpret_cast<const float4*>(sm_.w2 + cc * H + c);
-      acc[0] += dv * w2.x; acc[1] += dv * w2.y; acc[2] += dv * w2.z; acc[3] += dv * w2.w;
-    }
-    float z[4];
-#pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) z[s4] = (b0 + i < B && hvv[s4] > 0.f) ? acc[s4] * a.gscale : 0.f;
-    const float4 zv = make_float4(z[0], z[1], z[2], z[3]);
-    *reinterpret_cast<float4*>(zs + i * LD + c) = zv;
-    if (b0 + i < B) *reinterpret_cast<float4*>(a.dz1 + (int64_t)(b0 + i) * H + c) = zv;
-  }
-  zero_pad(zs, H);
-  __syncthreads();
-  if (kstamp) L1_ST(2, 2);
   // dfused = dz1 W1
   f32x4 acc[NTL];
   mma(zs, w1n, acc, lane);
@@ -728,31 +773,36 @@ __device__ __forceinline__ void head_bwd_tile(const L1Args& a, HeadLds& L, const
     for (int r = 0; r < 4; ++r) dfs[(4 * kq + r) * LD + j] = acc[u][r];
   }
   __syncthreads();
-  if (kstamp) L1_ST(2, 3);
-  // d weights_m = dfused . pooled_m
+  if (kstamp) L1_ST(2, 1);
+  // d weights_m = dfused . pooled_m, the compute_adaptive_weights backward (renormalisation and the
+  // masked softmax) and cvec_m = (w_m dfused + dscore_m gate_w_m) mask_m / n_m of sample i by row
+  // group i (the 16-lane sums leave every d weight in every lane of the group: no barrier)
   {
-    const int grp = t >> 4, l16 = t & 15;
-    for (int d = grp; d < S * M; d += NT / 16) {
-      const int i = d / M, m = d - i * M;
-      float s = 0.f;
-      for (int j = l16; j < H; j += 16) s += dfs[i * LD + j] * pl[(m * S + i) * LD + j];
-      s = sum16(s);
-      if (l16 == 0) dw[i * M + m] = s;
+    const RowGroup rg;
+    const int b = b0 + rg.i;
+    float4 dv[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int c4 = rg.l16 + 16 * q;
+      dv[q] = c4 < h4 ? *reinterpret_cast<const float4*>(dfs + rg.i * LD + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-  }
-  __syncthreads();
-  if (kstamp) L1_ST(2, 4);
-  // compute_adaptive_weights backward (renormalisation and the masked softmax); register arrays
-  // (compile-time L1_MAXM trip counts, m < M guards)
-  if (t < S) {
-    const int i = t;
-    float smx[L1_MAXM], w[L1_MAXM], ds[L1_MAXM], dsm[L1_MAXM], mk[L1_MAXM], dwv[L1_MAXM];
+    float dwv[L1_MAXM], mk[L1_MAXM], scv[L1_MAXM];
 #pragma unroll
     for (int m = 0; m < L1_MAXM; ++m) {
-      mk[m] = m < M ? msk[i * M + m] : 0.f;
-      dwv[m] = m < M ? dw[i * M + m] : 0.f;
+      float d = 0.f;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int c4 = rg.l16 + 16 * q;
+        const float4 pv = (m < M && c4 < h4) ? *reinterpret_cast<const float4*>(pl + (m * S + rg.i) * LD + 4 * c4)
+                                             : make_float4(0.f, 0.f, 0.f, 0.f);
+        d += dv[q].x * pv.x + dv[q].y * pv.y + dv[q].z * pv.z + dv[q].w * pv.w;
+      }
+      dwv[m] = m < M ? sum16(d) : 0.f;
+      mk[m] = m < M ? msk[rg.i * M + m] : 0.f;
+      scv[m] = m < M ? sc[rg.i * M + m] : 0.f;
     }
-    const float sw = adaptive(M, sc + i * M, msk + i * M, smx, w);
+    float smx[L1_MAXM], w[L1_MAXM], ds[L1_MAXM], dsm[L1_MAXM];
+    const float sw = adaptive(M, scv, mk, smx, w);
 #pragma unroll
     for (int m = 0; m < L1_MAXM; ++m) ds[m] = 0.f;
     if (sw > 0.f) {
@@ -770,30 +820,27 @@ __device__ __forceinline__ void head_bwd_tile(const L1Args& a, HeadLds& L, const
 #pragma unroll
       for (int m = 0; m < L1_MAXM; ++m) ds[m] = mk[m] > 0.f ? smx[m] * (dsm[m] - sdot) : 0.f;
     }
+    if (b < B) {
 #pragma unroll
-    for (int m = 0; m < L1_MAXM; ++m) {
-      if (m >= M) break;
-      dsc[i * M + m] = ds[m];
-      if (b0 + i < B) a.dscore[(int64_t)(b0 + i) * M + m] = ds[m];
+      for (int m = 0; m < L1_MAXM; ++m) {
+        if (m >= M) break;
+        if (rg.l16 == m) a.dscore[(int64_t)b * M + m] = ds[m];
+        const float f = mk[m] * a.inv_cnt[m];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int c4 = rg.l16 + 16 * q;
+          if (c4 >= h4) continue;
+          const float4 gv = *reinterpret_cast<const float4*>(sm_.gw + m * H + 4 * c4);
+          const float4 v = make_float4((w[m] * dv[q].x + ds[m] * gv.x) * f, (w[m] * dv[q].y + ds[m] * gv.y) * f,
+                                       (w[m] * dv[q].z + ds[m] * gv.z) * f, (w[m] * dv[q].w + ds[m] * gv.w) * f);
+          // (sc1: the pair workgroups of the one-launch step read cvec in the same launch)
+          st_wt4(a.cvec, (uint32_t)B * (uint32_t)M * (uint32_t)H * 4u, (uint32_t)((((int64_t)b * M + m) * H + 4 * c4) * 4), v);
+        }
+      }
     }
   }
-  __syncthreads();
-  if (kstamp) L1_ST(2, 5);
-  // cvec_m = (w_m dfused + dscore_m gate_w_m) mask_m / n_m: the gradient of every entry of m's
-  // aggregation list (P_m and the attended features of the pairs whose query is m), float4 per thread
-  for (int e = t; e < M * S * h4; e += NT) {
-    const int mi = e / h4, c = 4 * (e - mi * h4), m = mi / S, i = mi - m * S;
-    if (b0 + i >= B) continue;
-    const float f = msk[i * M + m] * a.inv_cnt[m], wm = wt[i * M + m], dsm = dsc[i * M + m];
-    const float4 dv = *reinterpret_cast<const float4*>(dfs + i * LD + c);
-    const float4 gv = *reinterpret_cast<const float4*>(sm_.gw + m * H + c);
-    const float4 v = make_float4((wm * dv.x + dsm * gv.x) * f, (wm * dv.y + dsm * gv.y) * f,
-                                 (wm * dv.z + dsm * gv.z) * f, (wm * dv.w + dsm * gv.w) * f);
-    // (sc1: the pair workgroups of the one-launch step read cvec in the same launch)
-    st_wt4(a.cvec, (uint32_t)B * (uint32_t)M * (uint32_t)H * 4u, (uint32_t)((((int64_t)(b0 + i) * M + m) * H + c) * 4), v);
-  }
   if (kstamp) {
-    L1_ST(2, 6);
+    L1_ST(2, 2);
     L1_RT(2, 9);
   }
 }
@@ -803,7 +850,7 @@ __global__ __launch_bounds__(NT) void l1_head_fwd_kernel(const L1Args a) {
   __shared__ __attribute__((aligned(16))) HeadLds L;
   RngSnap rs{0, 0};
   if (a.p > 0.f) rs = *a.snap;
-  head_fwd_tile<FH>(a, L, rs, 1);
+  head_fwd_tile<FH, false>(a, L, rs, 1, nullptr);
   // the live stream advances once per call (the pair kernel read it; the snapshot is saved)
   if (a.rng_advance && blockIdx.x == 0 && threadIdx.x == 0) a.rng_advance[1] += 1;
 }
@@ -821,7 +868,6 @@ __global__ __launch_bounds__(NT) void l1_head_bwd_kernel(const L1Args a) {
     const bool in = b0 + e / M < B;
     L.msk[e] = in ? a.mask[(int64_t)b0 * M + e] : 0.f;
     L.sc[e] = in ? a.scores[(int64_t)b0 * M + e] : 0.f;
-    L.wt[e] = in ? a.weights[(int64_t)b0 * M + e] : 0.f;
   }
   stage_small(a, L.sm);
   load_tile(a.h1, H, B, b0, H, L.hs);
@@ -831,14 +877,27 @@ __global__ __launch_bounds__(NT) void l1_head_bwd_kernel(const L1Args a) {
     const float4 v = *reinterpret_cast<const float4*>(a.pooled + ((int64_t)min(b0 + i, B - 1) * M + m) * H + c);
     *reinterpret_cast<float4*>(L.pl + mi * LD + c) = b0 + i < B ? v : make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  L1_RT(2, 8);
-  L1_ST(2, 0);
   __builtin_amdgcn_sched_barrier(0);
   WTile w1;
   wload_nn(a.W1, H, H, wave, lane, w1);
   __syncthreads();
-  L1_ST(2, 1);
-  head_bwd_tile<FH>(a, L, w1, 1);
+  // dz1 from the upstream dlogits (the one-launch step forms it beside the loss, the same dz1_rows)
+  {
+    const RowGroup rg;
+    float4 hv[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int c4 = rg.l16 + 16 * q;
+      hv[q] = c4 < h4 ? *reinterpret_cast<const float4*>(L.hs + rg.i * LD + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float dlv[L1_MAXC];
+#pragma unroll
+    for (int cc = 0; cc < L1_MAXC; ++cc) dlv[cc] = cc < C ? L.dl[rg.i * C + cc] : 0.f;
+    dz1_rows<FH>(a, L, rg, hv, dlv);
+  }
+  zero_pad(L.fs, H);
+  __syncthreads();
+  head_bwd_tile<FH>(a, L, w1, 0);
 }
 
 // ---- the key-modality backward inside the one-launch step (round 4) ----
@@ -1019,17 +1078,12 @@ __global__ __launch_bounds__(NT) void l1_fwd_loss_kernel(const L1Args a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (keeps the sc1 loads behind the count)
     if (threadIdx.x == 0)   // every pair workgroup of this tile has counted: back to 0 for the next call
       __hip_atomic_store(sw.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    head_fwd_tile<FH>(a, L.h, rs, 1);
-    const int H = FH ? FH : a.H;
-    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) & 3;
-    WTile w1n;
-    wload_nn(a.W1, H, H, wave, lane, w1n);   // (in flight through the loss)
-    __syncthreads();
-    loss_tile(a, L.h);
+    WTile w1n;   // (the backward's W1 columns, loaded behind the forward's h1 product)
+    head_fwd_tile<FH, true>(a, L.h, rs, 1, &w1n);   // (through the loss and dz1)
+    zero_pad(L.h.fs, FH ? FH : a.H);
     __syncthreads();
     L1_RT(2, 8);
     L1_ST(2, 0);
-    L1_ST(2, 1);
     head_bwd_tile<FH>(a, L.h, w1n, 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // cvec (sc1) drained by every wave
     __syncthreads();

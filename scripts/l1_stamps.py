@@ -31,9 +31,9 @@ import bench  # noqa: E402
 KERNELS = [
     ("l1_pair_fwd (l1_fwd_loss: pair part)", ["loads+keep+P'", "X'", "P = relu(X'Wk)", "O = P'(PWv)", "A = OWo + store",
                                               "store drain", "arrival count"]),
-    ("l1_head_fwd (last pair workgroup of a tile)", ["loads+keep", "pooled", "gating", "adaptive", "fused", "h1",
-                                                     "logits"]),
-    ("l1_head_bwd (loss + head backward)", ["loss", "dz1", "dfused", "dw", "adaptive bwd", "cvec"]),
+    ("l1_head_fwd (last pair workgroup of a tile)", ["loads+keep", "pooled", "gating+adaptive+fused", "h1",
+                                                     "logits+loss+dz1"]),
+    ("l1_head_bwd (head backward)", ["dfused", "dw+adaptive bwd+cvec"]),
     ("l1_key_bwd (pair part, after the head)", ["cvec + W_o/W_v + dO/dV/dP + count"]),
     ("l1_wgrad", ["main loop", "reduce + store"]),
 ]
