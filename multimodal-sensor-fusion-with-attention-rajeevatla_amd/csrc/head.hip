@@ -234,7 +234,9 @@ __global__ __launch_bounds__(NT) void cross_entropy_kernel(int B, int C, const f
     for (int c = 0; c < C; ++c) { se += __expf(z[c] - mx); sz += z[c]; }
     const float lse = mx + __logf(se);
     const int y = (int)labels[i];
-    acc += (1.f - eps) * (lse - z[y]) + eps * (lse - sz / (float)C);
+    // (an explicit fma: l1.hip loss_rows forms the same value bit for bit, whatever contraction
+    // each context's compiler would choose)
+    acc += __builtin_fmaf(1.f - eps, lse - z[y], eps * (lse - sz / (float)C));
     float* d = dlogits + (int64_t)i * C;
     for (int c = 0; c < C; ++c) {
       const float pc = __expf(z[c] - lse);

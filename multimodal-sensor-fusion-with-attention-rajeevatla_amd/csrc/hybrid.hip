@@ -616,9 +616,23 @@ bool poole_in_dz(const mmf_hybrid_desc* d, int m) {
 
 }  // namespace
 
-int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, const float* const* x,
-                       const float* mask, const uint64_t* rng_state, void* saved, float* logits,
-                       float* fusion_weights, float* const* attn_maps, void* stream) {
+// A training step's loss inside the tail's head launch (mmf_hybrid_train_step, the pooled tail plan
+// with the 16-sample tile head): the loss inputs and outputs, the step's sync word (the head
+// launch's tile count) and workspace (dz1, cvec, dscore and the loss rows).  done: the forward's
+// head launch ran the loss, dlogits and the head backward (the step skips the cross-entropy
+// launch, and the backward its head launch).
+struct TailTrain {
+  const int64_t* labels;
+  float ls_eps, loss_scale;
+  float *loss, *dlogits;
+  uint32_t* cnt;
+  void* workspace;
+  bool done;
+};
+
+static int hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, const float* const* x,
+                          const float* mask, const uint64_t* rng_state, void* saved, float* logits,
+                          float* fusion_weights, float* const* attn_maps, void* stream, TailTrain* tt) {
   int rc = check_hybrid(d);
   if (rc) return rc;
   MathScope math_(d->matmul_precision);
@@ -831,6 +845,17 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
       fill_tail(ta, d, W, mask, s);
       ta.weights_out = fusion_weights;
       ta.logits = logits;
+      if (tt && seq_head_ok(ta)) {
+        // (a training step: the loss, dlogits and the head backward in the head launch)
+        Bump bw(tt->workspace);
+        Ws w;
+        layout_ws(d, bw, w);
+        ta.labels = tt->labels; ta.ls_eps = tt->ls_eps; ta.loss_scale = tt->loss_scale;
+        ta.loss_rows = w.dfused;   // (B x H floats the tail plan leaves unused)
+        ta.loss_mean = tt->loss; ta.loss_cnt = tt->cnt; ta.dlogits_out = tt->dlogits;
+        ta.dz1 = w.dz1; ta.cvec = w.cvec; ta.dscore = w.dscore;
+        tt->done = true;
+      }
       STAGE_TRY("fwd.tail", launch_tail_fwd(ta, st));
     } else {
       STAGE_TRY("fwd.pool_u", launch_pool_u(pp.data(), d->num_pairs, B, nh, hd, H, st));
@@ -913,9 +938,16 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
   return MMF_OK;
 }
 
-int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, const float* const* x,
-                        const float* mask, const void* saved, const float* dlogits, void* workspace,
-                        const mmf_hybrid_grads* G, float* const* dx, void* stream) {
+int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, const float* const* x,
+                       const float* mask, const uint64_t* rng_state, void* saved, float* logits,
+                       float* fusion_weights, float* const* attn_maps, void* stream) {
+  return hybrid_forward(d, W, x, mask, rng_state, saved, logits, fusion_weights, attn_maps, stream, nullptr);
+}
+
+// head_done: the training step's head launch ran the head backward (TailTrain)
+static int hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, const float* const* x,
+                           const float* mask, const void* saved, const float* dlogits, void* workspace,
+                           const mmf_hybrid_grads* G, float* const* dx, void* stream, bool head_done) {
   int rc = check_hybrid(d);
   if (rc) return rc;
   MathScope math_(d->matmul_precision);
@@ -953,6 +985,7 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
     TailArgs ta;
     fill_tail(ta, d, W, mask, s);
     ta.dlogits = dlogits; ta.dz1 = w.dz1; ta.cvec = w.cvec; ta.dscore = w.dscore;
+    ta.head_done = head_done;
     for (int g = 0; g < d->num_pairs; ++g) {
       ta.p[g].dOb = w.dOb[g];
       ta.p[g].dU = w.dU[g];
@@ -1163,6 +1196,12 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
   return MMF_OK;
 }
 
+int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, const float* const* x,
+                        const float* mask, const void* saved, const float* dlogits, void* workspace,
+                        const mmf_hybrid_grads* G, float* const* dx, void* stream) {
+  return hybrid_backward(d, W, x, mask, saved, dlogits, workspace, G, dx, stream, false);
+}
+
 size_t mmf_hybrid_train_sync_bytes(const mmf_hybrid_desc* d) {
   if (check_hybrid(d) != MMF_OK) return 0;
   // per 16-sample tile: arrivals, head done, done seen, one arrival count per key modality; the
@@ -1213,12 +1252,16 @@ int mmf_hybrid_train_step(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, 
     STAGE_TRY("train.l1", launch_l1_train(a, wa, st));
     return MMF_OK;
   }
-  rc = mmf_hybrid_forward(d, W, x, mask, rng_state, saved, logits, fusion_weights, nullptr, stream);
+  // (with the sync words: the pooled tail plan runs the loss and the head backward in its head launch)
+  TailTrain tt{labels, label_smoothing, loss_scale, loss_out, dlogits, static_cast<uint32_t*>(sync), workspace, false};
+  rc = hybrid_forward(d, W, x, mask, rng_state, saved, logits, fusion_weights, nullptr, stream, sync ? &tt : nullptr);
   if (rc) return rc;
-  rc = mmf_cross_entropy_ls(d->batch, d->num_classes, logits, labels, label_smoothing, loss_scale, loss_out,
-                            dlogits, stream);
-  if (rc) return rc;
-  rc = mmf_hybrid_backward(d, W, x, mask, saved, dlogits, workspace, G, dx, stream);
+  if (!tt.done) {
+    rc = mmf_cross_entropy_ls(d->batch, d->num_classes, logits, labels, label_smoothing, loss_scale, loss_out,
+                              dlogits, stream);
+    if (rc) return rc;
+  }
+  rc = hybrid_backward(d, W, x, mask, saved, dlogits, workspace, G, dx, stream, tt.done);
   if (rc || !clip_partial) return rc;
   if (!grad_flat || grad_n < 0 || (reinterpret_cast<uintptr_t>(grad_flat) & 15))
     return fail(MMF_EINVAL, "train step: clip partials need the 16-byte aligned flat gradient");

@@ -101,6 +101,10 @@ __device__ __forceinline__ float4 ld_wt4(const float* base, uint32_t bytes, uint
   return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
 }
 
+__device__ __forceinline__ float ld_wt(const float* p) {
+  return __hip_atomic_load((gfloat*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 struct WTile {
   float4 w[NTL][KG];
 };
@@ -513,7 +517,7 @@ __device__ __forceinline__ void loss_rows(const L1Args& a, const RowGroup& rg, i
     if (c == y) zy = z[c];
   }
   const float lse = mx + __logf(se);
-  if (b < B && rg.l16 == 0) a.loss_rows[b] = (1.f - eps) * (lse - zy) + eps * (lse - sz / (float)C);
+  if (b < B && rg.l16 == 0) st_wt(a.loss_rows + b, __builtin_fmaf(1.f - eps, lse - zy, eps * (lse - sz / (float)C)));
 #pragma unroll
   for (int c = 0; c < L1_MAXC; ++c) {
     dl[c] = 0.f;
@@ -557,7 +561,7 @@ __device__ __forceinline__ void dz1_rows(const L1Args& a, HeadLds& L, const RowG
 // Head forward of tile blockIdx.x (src/fusion.py:406-427, :429-479): pooled, gating scores,
 // adaptive weights, fused, h1 = Drop(ReLU(fused W1^T + b1)), logits.  Leaves pooled (pl), the
 // mask / score / weight rows, h1 (hs) and the logits (lg) in L.  rs: the call's rng snapshot.
-template <int FH, bool LOSS>
+template <int FH, bool LOSS, bool SEQ = false>
 __device__ __forceinline__ void head_fwd_tile(const L1Args& a, HeadLds& L, const RngSnap& rs, int kstamp, WTile* w1n) {
   float* pl = L.pl;
   float* fs = L.fs;
@@ -582,17 +586,40 @@ __device__ __forceinline__ void head_fwd_tile(const L1Args& a, HeadLds& L, const
   for (int u = 0; u < 2; ++u) {
     const int e = t + u * NT, i = e / h4;
     pe[u] = (i < S) ? e : -1;
-    // (the P_k / A tiles of the other pair workgroups: sc1 loads, see st_wt)
-    const uint32_t row = (uint32_t)(((int64_t)min(b0 + min(i, S - 1), B - 1) * H + 4 * (e - i * h4)) * 4);
-    const uint32_t nbytes = (uint32_t)B * (uint32_t)H * 4u;
-#pragma unroll
-    for (int m = 0; m < L1_MAXM; ++m)
-      pv[u][m] = m < M ? ld_wt4(a.P[m], nbytes, row) : make_float4(0.f, 0.f, 0.f, 0.f);
-    // (the pair list unrolled over L1_MAXP: every A load issued before the first add)
+    const int bb = min(b0 + min(i, S - 1), B - 1), col = 4 * (e - i * h4);
     float4 xa[L1_MAXP];
+    if constexpr (SEQ) {
+      // mean_L P_m from the projection GEMM's per-128-row column sums (src/fusion.py:406-408),
+      // then the pairs' attended means Abar (earlier launches: plain loads)
 #pragma unroll
-    for (int g = 0; g < L1_MAXP; ++g)
-      xa[g] = g < a.npairs ? ld_wt4(a.A[g], nbytes, row) : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int m = 0; m < L1_MAXM; ++m) {
+        float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (m < M) {
+          const float* pc = a.P[m] + (int64_t)bb * a.ncol[m] * H + col;
+          for (int c = 0; c < a.ncol[m]; ++c) {
+            const float4 v = *reinterpret_cast<const float4*>(pc + (int64_t)c * H);
+            cs.x += v.x; cs.y += v.y; cs.z += v.z; cs.w += v.w;
+          }
+        }
+        const float il = m < M ? a.inv_L[m] : 0.f;
+        pv[u][m] = make_float4(cs.x * il, cs.y * il, cs.z * il, cs.w * il);
+      }
+#pragma unroll
+      for (int g = 0; g < L1_MAXP; ++g)
+        xa[g] = g < a.npairs ? *reinterpret_cast<const float4*>(a.A[g] + (int64_t)bb * H + col)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      // (the P_k / A tiles of the other pair workgroups: sc1 loads, see st_wt)
+      const uint32_t row = (uint32_t)(((int64_t)bb * H + col) * 4);
+      const uint32_t nbytes = (uint32_t)B * (uint32_t)H * 4u;
+#pragma unroll
+      for (int m = 0; m < L1_MAXM; ++m)
+        pv[u][m] = m < M ? ld_wt4(a.P[m], nbytes, row) : make_float4(0.f, 0.f, 0.f, 0.f);
+      // (the pair list unrolled over L1_MAXP: every A load issued before the first add)
+#pragma unroll
+      for (int g = 0; g < L1_MAXP; ++g)
+        xa[g] = g < a.npairs ? ld_wt4(a.A[g], nbytes, row) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 #pragma unroll
     for (int g = 0; g < L1_MAXP; ++g) {
       const int q = g < a.npairs ? a.pq[g] : -1;   // (a guard, not a break: the loop stays unrolled)
@@ -900,6 +927,50 @@ __global__ __launch_bounds__(NT) void l1_head_bwd_kernel(const L1Args a) {
   head_bwd_tile<FH>(a, L, w1, 0);
 }
 
+// ---- the sequence tail's head on 16-sample tiles ----
+// The pooled plan's head (tail.hip launch_tail_fwd / _bwd) with the phases above: pooled_m from the
+// projection GEMM's column sums and the pairs' Abar, then the row-group / MFMA head of the L = 1
+// step.  With LOSS (a training step): the cross-entropy, dz1 and the head backward in the same
+// launch (the forward's tiles still in LDS), and the batch-mean loss by the last tile to count
+// (loss rows stored sc1, drained before the count; cross_entropy_kernel's summation order).
+template <int FH, bool LOSS>
+__global__ __launch_bounds__(NT) void seq_head_kernel(const L1Args a) {
+  __shared__ __attribute__((aligned(16))) HeadLds L;
+  RngSnap rs{0, 0};
+  if (a.p > 0.f) rs = *a.snap;
+  if constexpr (!LOSS) {
+    head_fwd_tile<FH, false, true>(a, L, rs, 0, nullptr);
+  } else {
+    WTile w1n;
+    head_fwd_tile<FH, true, true>(a, L, rs, 0, &w1n);
+    zero_pad(L.fs, FH ? FH : a.H);
+    __syncthreads();
+    head_bwd_tile<FH>(a, L, w1n, 0);
+    if (!a.loss_mean) return;
+    __shared__ int last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's loss rows (sc1) drained
+    __syncthreads();
+    const int t = threadIdx.x;
+    if (t == 0)
+      last = __hip_atomic_fetch_add((gu32*)a.loss_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (t == 0) __hip_atomic_store((gu32*)a.loss_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    float* red = L.hs;   // (the head is done with its LDS)
+    float acc = 0.f;
+    for (int i = t; i < a.B; i += NT) acc += ld_wt(a.loss_rows + i);
+    red[t] = acc;
+    __syncthreads();
+    for (int s = NT / 2; s > 0; s >>= 1) {
+      if (t < s) red[t] += red[t + s];
+      __syncthreads();
+    }
+    if (t == 0) a.loss_mean[0] = red[0] / (float)a.B;
+  }
+}
+
 // ---- the key-modality backward inside the one-launch step (round 4) ----
 // After a tile's head (the last pair workgroup of the tile) has written cvec (sc1 stores) and set
 // the tile's done word, every pair workgroup g = (q, k) of the tile runs its share of what
@@ -925,9 +996,6 @@ __device__ __forceinline__ bool poll_eq(gu32* w, unsigned want) {
     __builtin_amdgcn_s_sleep(2);
   }
   return false;
-}
-__device__ __forceinline__ float ld_wt(const float* p) {
-  return __hip_atomic_load((gfloat*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int FH>
@@ -1464,6 +1532,95 @@ hipError_t launch_l1_train(const L1Args& a, const L1WgArgs& w_in, hipStream_t st
   if (w.clip_partial && w.ntiles > CLIP_PARTIAL_SLOTS) return hipErrorInvalidValue;
   const bool extra = w.loss || w.clip_partial || w.rng_advance;
   mmf_launch(l1_wgrad_kernel, dim3((unsigned)(w.ntiles + zblocks + (extra ? 1 : 0))), dim3(NT), 0, st, w);
+  return hipGetLastError();
+}
+
+bool seq_head_ok(const TailArgs& t) {
+  const bool off = getenv("MMF_TAIL_HEAD_GEMV") != nullptr;   // (the per-sample kernels, for A/B)
+  if (off || t.H > L1_MAXH || t.H % 4 != 0 || t.M < 1 || t.M > L1_MAXM || t.npairs > L1_MAXP || t.C > L1_MAXC ||
+      t.C < 1)
+    return false;
+  for (int m = 0; m < t.M; ++m)
+    if (!t.Pcol[m] || t.ncol[m] < 1) return false;
+  return true;
+}
+
+static L1Args seq_head_args(const TailArgs& t) {
+  L1Args a;
+  memset(&a, 0, sizeof(a));
+  a.B = t.B; a.M = t.M; a.H = t.H; a.C = t.C; a.heads = t.heads; a.npairs = t.npairs;
+  const bool drop = t.drop_p > 0.f && t.rng != nullptr;
+  a.p = drop ? t.drop_p : 0.f;
+  a.gscale = t.gscale;
+  a.snap = const_cast<RngSnap*>(t.rng);
+  a.mask = t.mask;
+  for (int m = 0; m < t.M; ++m) {
+    a.inv_cnt[m] = t.inv_cnt[m];
+    a.P[m] = const_cast<float*>(t.Pcol[m]);
+    a.ncol[m] = t.ncol[m];
+    a.inv_L[m] = 1.f / (float)t.L[m];
+    a.gw[m] = t.gate_w[m];
+    a.gb[m] = t.gate_b[m];
+  }
+  for (int g = 0; g < t.npairs; ++g) {
+    a.pq[g] = t.p[g].q;
+    a.pk[g] = t.p[g].k;
+    a.A[g] = const_cast<float*>(t.p[g].Ab);
+  }
+  a.W1 = t.W1; a.b1 = t.b1; a.W2 = t.W2; a.b2 = t.b2;
+  a.pooled = t.pooled; a.scores = t.scores; a.weights = t.weights; a.fused = t.fused; a.h1 = t.h1;
+  a.logits = t.logits; a.weights_out = t.weights_out;
+  a.dlogits = t.dlogits; a.dz1 = t.dz1; a.cvec = t.cvec; a.dscore = t.dscore;
+  a.labels = t.labels; a.ls_eps = t.ls_eps; a.loss_scale = t.loss_scale;
+  a.loss_rows = t.loss_rows; a.dlogits_out = t.dlogits_out;
+  a.loss_mean = t.loss_mean; a.loss_cnt = t.loss_cnt;
+  return a;
+}
+
+hipError_t launch_seq_head_fwd(const TailArgs& t, hipStream_t st) {
+  if (!seq_head_ok(t)) return hipErrorInvalidValue;
+  const L1Args a = seq_head_args(t);
+  const bool loss = t.labels != nullptr;
+  if (loss && (!t.loss_rows || !t.dlogits_out || !t.dz1 || !t.cvec || !t.dscore || (t.loss_mean && !t.loss_cnt)))
+    return hipErrorInvalidValue;
+  const unsigned tiles = (unsigned)((t.B + S - 1) / S);
+  const double B = t.B, H = t.H, M = t.M, C = t.C;
+  double ncs = 0.0;
+  for (int m = 0; m < t.M; ++m) ncs += t.ncol[m];
+  const bool full = t.H == 128;
+  // forward: W1 / W2 once per tile, the column sums, Abar, mask in; pooled, fused, h1, logits,
+  // scores / weights out.  With the loss: + dlogits, dz1, dscore, cvec out, W1 again
+  double fl = 2.0 * B * H * (H + C) + 4.0 * M * B * H;
+  double by = 4.0 * (tiles * (H * H + C * H) + B * (ncs * H + t.npairs * H + M) +
+                     B * (M * H + 2 * H + C + 2 * M));
+  if (loss) {
+    fl += 2.0 * B * H * (H + C) + 4.0 * M * B * H;
+    by += 4.0 * (tiles * H * H + B * (2 * C + H + M + M * H));
+  }
+  const char* nm = loss ? (full ? "seq_head_kernel<128, 1>" : "seq_head_kernel<0, 1>")
+                        : (full ? "seq_head_kernel<128, 0>" : "seq_head_kernel<0, 0>");
+  ProfLaunch prof_(st, nm, fl, by);
+  if (loss) {
+    if (full) mmf_launch(seq_head_kernel<128, true>, dim3(tiles), dim3(NT), 0, st, a);
+    else mmf_launch(seq_head_kernel<0, true>, dim3(tiles), dim3(NT), 0, st, a);
+  } else {
+    if (full) mmf_launch(seq_head_kernel<128, false>, dim3(tiles), dim3(NT), 0, st, a);
+    else mmf_launch(seq_head_kernel<0, false>, dim3(tiles), dim3(NT), 0, st, a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_seq_head_bwd(const TailArgs& t, hipStream_t st) {
+  if (!seq_head_ok(t) || !t.dlogits || !t.dz1 || !t.cvec || !t.dscore) return hipErrorInvalidValue;
+  const L1Args a = seq_head_args(t);
+  const unsigned tiles = (unsigned)((t.B + S - 1) / S);
+  const double B = t.B, H = t.H, M = t.M, C = t.C;
+  const bool full = t.H == 128;
+  ProfLaunch prof_(st, full ? "l1_head_bwd_kernel<128>" : "l1_head_bwd_kernel<0>",
+                   2.0 * B * H * (H + C) + 4.0 * M * B * H,
+                   4.0 * (tiles * (H * H + C * H) + B * (C + 2 * M + H + M * H) + B * (H + M + M * H)));
+  if (full) mmf_launch(l1_head_bwd_kernel<128>, dim3(tiles), dim3(NT), 0, st, a);
+  else mmf_launch(l1_head_bwd_kernel<0>, dim3(tiles), dim3(NT), 0, st, a);
   return hipGetLastError();
 }
 

@@ -526,6 +526,12 @@ struct TailArgs {
   float drop_p; uint32_t drop_site; const RngSnap* rng;
   // backward
   const float* dlogits; float* dz1; float* cvec; float* dscore; float gscale;
+  // a training step's loss in the head launch (the 16-sample tile head, launch_seq_head_fwd):
+  // per-sample loss rows, the batch mean by the last tile to count (loss_cnt: zero between
+  // calls), dlogits, and the head backward in the same launch (launch_tail_bwd then skips it)
+  const int64_t* labels; float ls_eps, loss_scale;
+  float* loss_rows; float* loss_mean; uint32_t* loss_cnt; float* dlogits_out;
+  int32_t head_done;
   TailPair p[TAIL_MAX_PAIRS];
   // pairs grouped by key modality (launch_tail_*: the P_k-side kernels read P_k[b] once per group)
   int32_t nkg;
@@ -535,6 +541,12 @@ struct TailArgs {
 bool tail_supported(int M, int H, int C, int heads, int hd, int npairs);
 hipError_t launch_tail_fwd(const TailArgs& a, hipStream_t st);
 hipError_t launch_tail_bwd(const TailArgs& a, hipStream_t st);
+// The tail's head on 16-sample tiles (l1.hip's head phases, the pooled sources read from the
+// projection GEMM's column sums and the pairs' Abar): H <= 128, M <= 4, C <= 16, every modality
+// with column sums.  The forward launch also runs the loss and the head backward when a.labels.
+bool seq_head_ok(const TailArgs& a);
+hipError_t launch_seq_head_fwd(const TailArgs& a, hipStream_t st);
+hipError_t launch_seq_head_bwd(const TailArgs& a, hipStream_t st);
 
 // ---------------------------------------------------------------------------
 // Launch-lean single-key step (l1.hip): every modality 2-D (L = 1, what src/train.py:261-279
@@ -579,6 +591,11 @@ struct L1Args {
   float ls_eps, loss_scale;           // label smoothing; dlogits scale (1 / accumulation steps)
   float* loss_rows;                   // (B) per-sample loss
   float* dlogits_out;                 // (B, C)
+  // the sequence tail's head (launch_seq_head_*): P[m] holds the projection GEMM's per-128-row
+  // column sums of P_m (B, ncol, H), scaled by inv_L; A[g] the pair's Abar (B, H)
+  int32_t ncol[L1_MAXM];
+  float inv_L[L1_MAXM];
+  float* loss_mean; uint32_t* loss_cnt;   // optional: the batch-mean loss by the last tile to count
 };
 constexpr int L1_MAXJOBS = 40, L1_MAXZ = 48;
 struct L1WgJob {                      // dW (N x K) = G^T X over B rows; db = column sums of G

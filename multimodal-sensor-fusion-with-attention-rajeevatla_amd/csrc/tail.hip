@@ -1053,7 +1053,10 @@ hipError_t launch_tail_fwd(const TailArgs& a, hipStream_t st) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  // pooling, gating, adaptive weights, weighted sum, classifier
+  // pooling, gating, adaptive weights, weighted sum, classifier: on 16-sample tiles where they
+  // apply (l1.hip seq_head_kernel; a training step's loss and head backward in the same launch)
+  if (seq_head_ok(a)) return launch_seq_head_fwd(a, st);
+  if (a.labels) return hipErrorInvalidValue;   // (the caller checks seq_head_ok first)
   ProfLaunch prof_(st, head_pre(a) ? "tail_head_fwd_kernel<true>" : "tail_head_fwd_kernel<false>", 2.0 * B * H * (H + a.C) + 4.0 * a.M * B * H,
                    4.0 * (H * (H + a.C) + B * (a.M * H + a.C)));
   if (head_pre(a)) mmf_launch(tail_head_fwd_kernel<true>, dim3(a.B), dim3(NT), 0, st, a);
@@ -1064,13 +1067,18 @@ hipError_t launch_tail_fwd(const TailArgs& a, hipStream_t st) {
 hipError_t launch_tail_bwd(const TailArgs& a, hipStream_t st) {
   if (!tail_supported(a.M, a.H, a.C, a.heads, a.hd, a.npairs)) return hipErrorInvalidValue;
   const double B = a.B, H = a.H;
-  {
+  hipError_t e = hipSuccess;
+  if (a.head_done) {
+    // (the training step's head launch ran the head backward)
+  } else if (seq_head_ok(a)) {
+    e = launch_seq_head_bwd(a, st);
+  } else {
     ProfLaunch prof_(st, head_pre(a) ? "tail_head_bwd_kernel<true>" : "tail_head_bwd_kernel<false>", 2.0 * B * H * (H + a.C) + 4.0 * a.M * B * H,
                      4.0 * (H * (H + a.C) + B * (a.M * H + a.C)));
     if (head_pre(a)) mmf_launch(tail_head_bwd_kernel<true>, dim3(a.B), dim3(NT), 0, st, a);
     else mmf_launch(tail_head_bwd_kernel<false>, dim3(a.B), dim3(NT), 0, st, a);
+    e = hipGetLastError();
   }
-  hipError_t e = hipGetLastError();
   if (e != hipSuccess || !a.npairs) return e;
   TailArgs m = a;
   if (tail_mfma_groups(m)) {

@@ -61,8 +61,10 @@ def _precision_arg(kname):
 def check_precision_ran(launches, precision):
     """Every precision-templated MFMA kernel of the call ran the instantiation of the mode."""
     want = {"highest": 0, "high": 2}[precision]
-    if any(k.startswith("l1_") for _, k, *_ in launches):
+    if any(k.startswith(("l1_pair_fwd", "l1_fwd_loss")) for _, k, *_ in launches):
         # the launch-lean single-key step (csrc/l1.hip) is fp32-only: "highest" alone selects it
+        # (the tile head of the pooled plan, seq_head_kernel / l1_head_bwd_kernel, runs fp32 MFMA
+        # at every precision, as the per-sample head kernels it replaces ran fp32 FMA)
         assert precision == "highest", [k for _, k, *_ in launches]
         return
     got = [(k, _precision_arg(k)) for _, k, *_ in launches

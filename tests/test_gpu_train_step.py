@@ -284,3 +284,67 @@ def test_clip_partials_from_the_train_step(mods, seq):
         assert abs(n1 - n2) <= 1e-6 * n2 and c1 < 1.0
         assert s1 == s2
         torch.testing.assert_close(p1, p2, rtol=1e-6, atol=1e-7)
+
+
+def _seq_batch(seed, B=40, L=128, D=32, C=5):
+    g = torch.Generator().manual_seed(seed)
+    feats = [torch.randn(B, L, D, generator=g) for _ in range(M)]
+    mask = (torch.rand(B, M, generator=g) < 0.8).float()
+    mask[3] = 0.0
+    mask[7, 1] = 0.5
+    labels = torch.randint(0, C, (B,), generator=g)
+    return feats, mask, labels
+
+
+@pytest.mark.parametrize("hidden", [64, 128])
+def test_tile_head_train_step(mods, hidden, monkeypatch):
+    """The pooled tail plan's training step on the 16-sample tile head (csrc/l1.hip seq_head_kernel:
+    the head forward, the cross-entropy, dlogits and the head backward in one launch, the batch-mean
+    loss by the last tile to count) against (a) forward -> cross-entropy -> backward as three calls
+    (the tile head's forward and backward launches): bit for bit over two steps, the sync word back
+    at zero; (b) the per-sample head kernels (MMF_TAIL_HEAD_GEMV=1, tail.hip): the same values to
+    fp32 reassociation.  L = 128 (the projection GEMM's column sums feed the pooling), B = 40 (a
+    ragged last tile), dropout 0.3, a fully masked sample and a fractional mask."""
+    import mmf_native as nat
+    fusion, train_step = mods
+    feats, mask, labels = _seq_batch(17)
+    runs = {}
+    for mode in ("one", "three", "gemv"):
+        if mode == "gemv":
+            monkeypatch.setenv("MMF_TAIL_HEAD_GEMV", "1")
+        torch.manual_seed(3)
+        model = fusion.HybridFusion({f"m{i}": 32 for i in range(M)}, hidden_dim=hidden, num_classes=5, num_heads=4,
+                                    dropout=0.3).cuda()
+        model._rng_state.copy_(torch.tensor([0xBEEF, 9], dtype=torch.int64))
+        st = train_step.HybridTrainStep(model, [f.cuda() for f in feats], mask.cuda(), labels.cuda())
+        nat.profile_begin()
+        outs = []
+        for _ in range(2):
+            _three_calls(st, nat) if mode == "three" else st.forward_backward()
+            torch.cuda.synchronize()
+            outs.append([t.detach().cpu().clone() for t in (st.logits, st.losses, st.dlogits, st.fw, st.grad,
+                                                            *st.dx, model._rng_state)])
+        _, launches = nat.profile_end()
+        names = [k for _, k, *_ in launches]
+        if mode == "one":
+            assert any(k.startswith("seq_head_kernel") and k.endswith(", 1>") for k in names), names
+            assert not any(k.startswith(("cross_entropy_kernel", "tail_head", "l1_head_bwd")) for k in names), names
+            assert int(st.sync.count_nonzero()) == 0
+        elif mode == "three":
+            assert any(k.startswith("seq_head_kernel") and k.endswith(", 0>") for k in names), names
+            assert any(k.startswith("l1_head_bwd_kernel") for k in names), names
+        else:
+            assert any(k.startswith("tail_head_fwd_kernel") for k in names), names
+            assert not any(k.startswith("seq_head_kernel") for k in names), names
+        runs[mode] = outs
+        monkeypatch.delenv("MMF_TAIL_HEAD_GEMV", raising=False)
+    for step_a, step_b in zip(runs["one"], runs["three"]):
+        for a, b in zip(step_a, step_b):
+            assert torch.equal(a, b)
+    for step_a, step_b in zip(runs["one"], runs["gemv"]):
+        for a, b in zip(step_a, step_b):
+            if a.dtype == torch.int64:
+                assert torch.equal(a, b)
+                continue
+            tol = 1e-4 * max(float(b.abs().max()), 1e-6)
+            assert float((a - b).abs().max()) <= tol, float((a - b).abs().max())
