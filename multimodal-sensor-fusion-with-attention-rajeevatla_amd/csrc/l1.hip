@@ -94,6 +94,12 @@ __device__ __forceinline__ void st_wt4(float* base, uint32_t bytes, uint32_t off
   const u32x4 x = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
   __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, 16);   // aux 16: sc1
 }
+// 16-B load at byte offset `off` of a (wave-uniform) tensor base of `bytes` bytes (zeros past it)
+__device__ __forceinline__ float4 ld_rb4(const float* base, uint32_t bytes, uint32_t off) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, bytes, 0x00020000);
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+}
 // 16-B sc1 load at byte offset `off` of a (wave-uniform) tensor base of `bytes` bytes
 __device__ __forceinline__ float4 ld_wt4(const float* base, uint32_t bytes, uint32_t off) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, bytes, 0x00020000);
@@ -590,24 +596,28 @@ __device__ __forceinline__ void head_fwd_tile(const L1Args& a, HeadLds& L, const
     float4 xa[L1_MAXP];
     if constexpr (SEQ) {
       // mean_L P_m from the projection GEMM's per-128-row column sums (src/fusion.py:406-408),
-      // then the pairs' attended means Abar (earlier launches: plain loads)
+      // then the pairs' attended means Abar (earlier launches).  Unconditional buffer loads (an
+      // absent modality / pair: a zero-size range, which reads zeros), all issued before the
+      // first add; column-sum rows past the first (L_m > 128) in a loop after them
+      const uint32_t hb = (uint32_t)B * (uint32_t)H * 4u, ho = (uint32_t)(((int64_t)bb * H + col) * 4);
 #pragma unroll
       for (int m = 0; m < L1_MAXM; ++m) {
-        float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (m < M) {
-          const float* pc = a.P[m] + (int64_t)bb * a.ncol[m] * H + col;
-          for (int c = 0; c < a.ncol[m]; ++c) {
-            const float4 v = *reinterpret_cast<const float4*>(pc + (int64_t)c * H);
-            cs.x += v.x; cs.y += v.y; cs.z += v.z; cs.w += v.w;
-          }
-        }
-        const float il = m < M ? a.inv_L[m] : 0.f;
-        pv[u][m] = make_float4(cs.x * il, cs.y * il, cs.z * il, cs.w * il);
+        const int nc = m < M ? a.ncol[m] : 0;
+        pv[u][m] = ld_rb4(m < M ? a.P[m] : a.mask, (uint32_t)nc * hb, (uint32_t)(((int64_t)bb * nc * H + col) * 4));
       }
 #pragma unroll
-      for (int g = 0; g < L1_MAXP; ++g)
-        xa[g] = g < a.npairs ? *reinterpret_cast<const float4*>(a.A[g] + (int64_t)bb * H + col)
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int g = 0; g < L1_MAXP; ++g) xa[g] = ld_rb4(g < a.npairs ? a.A[g] : a.mask, g < a.npairs ? hb : 0u, ho);
+#pragma unroll
+      for (int m = 0; m < L1_MAXM; ++m) {
+        if (m >= M) break;
+        const float* pc = a.P[m] + (int64_t)bb * a.ncol[m] * H + col;
+        for (int c = 1; c < a.ncol[m]; ++c) {
+          const float4 v = *reinterpret_cast<const float4*>(pc + (int64_t)c * H);
+          pv[u][m].x += v.x; pv[u][m].y += v.y; pv[u][m].z += v.z; pv[u][m].w += v.w;
+        }
+        const float il = a.inv_L[m];
+        pv[u][m] = make_float4(pv[u][m].x * il, pv[u][m].y * il, pv[u][m].z * il, pv[u][m].w * il);
+      }
     } else {
       // (the P_k / A tiles of the other pair workgroups: sc1 loads, see st_wt)
       const uint32_t row = (uint32_t)(((int64_t)bb * H + col) * 4);
@@ -1076,30 +1086,60 @@ __device__ __forceinline__ void pair_key_bwd(const L1Args& a, PairLds& L, const 
   if (!*flag) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   // the last of k's pairs: dZ_k = ReLU' Drop' (cvec_k + sum_g dP_k|g) (P_k post-dropout: > 0 marks
-  // kept, active units), in the accumulator layout; then dX_k
+  // kept, active units; the dP in pair order, as l1_key_bwd_kernel sums them), then dX_k.  dZ in
+  // row-major float4 chunks, two per thread: every handed-off operand (cvec, P_k, the dP of k's
+  // pairs) one 16-B sc1 load, all issued before the first add (a per-element load loop waited
+  // for each load in turn: 11 us of the launch in the round-4 stamps)
   const bool want_dx = a.dx[k] != nullptr;
   WTile wp;
   if (want_dx) wload_nn(a.Wp[k], D, H, wave, lane, wp);
   if (t < S) msk[t] = b0 + t < B ? a.mask[(int64_t)min(b0 + t, B - 1) * M + k] : 0.f;
   if (a.p > 0.f && want_dx) keep_tile(rs, SITE_IN + k, b0, D, a.p, kin);
+  {
+    constexpr int MK = L1_MAXM - 1;   // pairs keyed by one modality (every ordered pair present)
+    int kg[MK], nk = 0;
 #pragma unroll
-  for (int u = 0; u < NTL; ++u) {
-    const int j = 16 * (wave + 4 * u) + jl;
+    for (int q = 0; q < MK; ++q) kg[q] = -1;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int ii = 4 * kq + r;
-      float z = 0.f;
-      if (b0 + ii < B && j < H) {
-        const int64_t row = (int64_t)(b0 + ii) * H + j;
-        float dp = 0.f;
-        for (int gg = 0; gg < a.npairs; ++gg)
-          if (a.pk[gg] == k) dp += ld_wt(a.dPk[gg] + row);
-        const float c = ld_wt(a.cvec + ((int64_t)(b0 + ii) * M + k) * H + j);
-        z = ld_wt(a.P[k] + row) > 0.f ? (c + dp) * a.gscale : 0.f;
-        a.dZ[k][row] = z;
+    for (int gg = 0; gg < L1_MAXP; ++gg)
+      if (gg < a.npairs && a.pk[gg] == k) {
+#pragma unroll
+        for (int q = 0; q < MK; ++q)
+          if (nk == q) kg[q] = gg;
+        ++nk;
       }
-      zs[ii * LD + j] = z;
+    const int h4 = H / 4;
+    const uint32_t nbh = (uint32_t)B * (uint32_t)H * 4u, nbc = (uint32_t)B * (uint32_t)M * (uint32_t)H * 4u;
+    float4 cv[2], pv[2], dv[2][MK];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = t + u * NT, i = e / h4, c = 4 * (e - i * h4);
+      const int bb = min(b0 + min(i, S - 1), B - 1);
+      const uint32_t off = (uint32_t)(((int64_t)bb * H + c) * 4);
+      cv[u] = ld_wt4(a.cvec, nbc, (uint32_t)((((int64_t)bb * M + k) * H + c) * 4));
+      pv[u] = ld_wt4(a.P[k], nbh, off);
+#pragma unroll
+      for (int q = 0; q < MK; ++q)
+        dv[u][q] = ld_wt4(kg[q] >= 0 ? a.dPk[kg[q]] : a.cvec, kg[q] >= 0 ? nbh : 0u, off);
     }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = t + u * NT, i = e / h4, c = 4 * (e - i * h4);
+      if (i >= S) continue;
+      float4 dp = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int q = 0; q < MK; ++q)
+        if (q < nk) { dp.x += dv[u][q].x; dp.y += dv[u][q].y; dp.z += dv[u][q].z; dp.w += dv[u][q].w; }
+      const bool in = b0 + i < B;
+      float4 z;
+      z.x = (in && pv[u].x > 0.f) ? (cv[u].x + dp.x) * a.gscale : 0.f;
+      z.y = (in && pv[u].y > 0.f) ? (cv[u].y + dp.y) * a.gscale : 0.f;
+      z.z = (in && pv[u].z > 0.f) ? (cv[u].z + dp.z) * a.gscale : 0.f;
+      z.w = (in && pv[u].w > 0.f) ? (cv[u].w + dp.w) * a.gscale : 0.f;
+      *reinterpret_cast<float4*>(zs + i * LD + c) = z;
+      if (in) *reinterpret_cast<float4*>(a.dZ[k] + (int64_t)(b0 + i) * H + c) = z;
+    }
+    zero_pad(zs, H);
   }
   if (!want_dx) return;
   __syncthreads();
@@ -1116,6 +1156,7 @@ __device__ __forceinline__ void pair_key_bwd(const L1Args& a, PairLds& L, const 
       a.dx[k][(int64_t)(b0 + ii) * D + j] = v;
     }
   }
+  L1_RT(3, 9);   // (the dZ / dX workgroup's end)
 }
 
 // The forward, the loss and the head backward of a training step in one launch over (tile,
