@@ -1009,7 +1009,8 @@ __device__ __forceinline__ bool poll_eq(gu32* w, unsigned want) {
 }
 
 template <int FH>
-__device__ __forceinline__ void pair_key_bwd(const L1Args& a, PairLds& L, const RngSnap& rs, int* flag) {
+__device__ __forceinline__ void pair_key_bwd(const L1Args& a, PairLds& L, const RngSnap& rs, int* flag,
+                                             const WTile& wo, const WTile& wv) {
   const int g = blockIdx.y, b0 = blockIdx.x * S, tile = blockIdx.x;
   const int q = a.pq[g], k = a.pk[g];
   const int H = FH ? FH : a.H, D = FH ? FH : a.D[k], B = a.B, M = a.M;
@@ -1022,7 +1023,8 @@ __device__ __forceinline__ void pair_key_bwd(const L1Args& a, PairLds& L, const 
   float* msk = L.msk;
   L1_RT(3, 8);
   L1_ST(3, 0);
-  // cvec_q rows of the tile (sc1: the head wrote them in this launch), P' of the pair, W_o / W_v
+  // cvec_q rows of the tile (sc1: the head wrote them in this launch), P' of the pair (W_o / W_v:
+  // the caller loaded them, a waiting workgroup before its poll)
   {
     const int h4 = H / 4;
     const uint32_t nbytes = (uint32_t)B * (uint32_t)M * (uint32_t)H * 4u;
@@ -1038,10 +1040,6 @@ __device__ __forceinline__ void pair_key_bwd(const L1Args& a, PairLds& L, const 
       if (i < S) *reinterpret_cast<float4*>(cs + i * LD + 4 * c) = b0 + i < B ? v[u] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
-  __builtin_amdgcn_sched_barrier(0);
-  WTile wo, wv;
-  wload_nn(a.Wo[g], H, H, wave, lane, wo);
-  wload_nn(a.Wv[g], H, H, wave, lane, wv);
   pprime_tile(a, rs, g, b0, pp);
   zero_pad(cs, H);
   __syncthreads();
@@ -1172,7 +1170,10 @@ __global__ __launch_bounds__(NT) void l1_fwd_loss_kernel(const L1Args a) {
   // (LDS over 80 KB: one workgroup per CU, the residency the hand-off protocol was measured at)
   __shared__ __attribute__((aligned(16))) union Lds { PairLds p; HeadLds h; char pad[82 * 1024]; } L;
   __shared__ int last, flag;
-  const int tile = blockIdx.x;
+  const int tile = blockIdx.x, g = blockIdx.y;
+  const int H = FH ? FH : a.H;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) & 3;
+  WTile wo, wv;
   const RngSnap rs = pair_fwd_tile<FH>(a, L.p);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
   __syncthreads();
@@ -1197,7 +1198,12 @@ __global__ __launch_bounds__(NT) void l1_fwd_loss_kernel(const L1Args a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // cvec (sc1) drained by every wave
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(sw.done + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    wload_nn(a.Wo[g], H, H, wave, lane, wo);   // (after the done word: not behind the drain)
+    wload_nn(a.Wv[g], H, H, wave, lane, wv);
   } else {
+    // this pair's backward weights in flight while the head runs
+    wload_nn(a.Wo[g], H, H, wave, lane, wo);
+    wload_nn(a.Wv[g], H, H, wave, lane, wv);
     if (threadIdx.x == 0) {
       const bool ok = poll_eq(sw.done + tile, 1u);
       if (ok) {
@@ -1217,7 +1223,7 @@ __global__ __launch_bounds__(NT) void l1_fwd_loss_kernel(const L1Args a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
   __syncthreads();   // (the head's LDS becomes the pair backward's)
-  pair_key_bwd<FH>(a, L.p, rs, &flag);
+  pair_key_bwd<FH>(a, L.p, rs, &flag, wo, wv);
 }
 
 // Backward of everything keyed by one modality m, per 16-sample tile (tile, m): for every pair
@@ -1365,15 +1371,21 @@ __global__ __launch_bounds__(NT) void l1_wgrad_kernel(const L1WgArgs w) {
   }
   if (tile >= w.ntiles) {
     const int zb = tile - w.ntiles;
-    int i = 0;
-    while (i < w.nz && w.zoff[i + 1] <= zb) ++i;
+    int i = 0;   // (unrolled: every offset's scalar load in flight at once, not one per step)
+#pragma unroll
+    for (int z = 1; z <= L1_MAXZ; ++z)
+      if (z <= w.nz && w.zoff[z] <= zb) i = z;
     if (i >= w.nz) return;
     const int64_t lo = (int64_t)(zb - w.zoff[i]) * 4096, hi = min((int64_t)w.zn[i], lo + 4096);
     for (int64_t e = lo + t; e < hi; e += NT) w.z[i][e] = 0.f;
     return;
   }
+  // the job of this tile: unrolled over L1_MAXJOBS, every tile0 scalar load in flight at once (a
+  // while loop waited for one kernarg load per job: up to 40 round trips before the first load)
   int ji = 0;
-  while (ji + 1 < w.njobs && w.j[ji + 1].tile0 <= tile) ++ji;
+#pragma unroll
+  for (int i = 1; i < L1_MAXJOBS; ++i)
+    if (i < w.njobs && w.j[i].tile0 <= tile) ji = i;
   const L1WgJob J = w.j[ji];
   const int lt = tile - J.tile0, n0 = 32 * (lt / J.tiles_k), k0 = 32 * (lt % J.tiles_k);
   L1_RT(4, 8);
