@@ -111,6 +111,20 @@ __device__ __forceinline__ float ld_wt(const float* p) {
   return __hip_atomic_load((gfloat*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// (tile, pair) of this workgroup (one place, so a different layout of the grid changes one
+// function).  A pair-major-by-XCD layout (every XCD's workgroups on one or two pairs, so their
+// W_v / W_o loads hit that XCD's L2) measured no change: 0.0699 / 0.0697 vs 0.0700 / 0.0706 ms,
+// the weight-load phase 8.3 K vs 8.6 K cycles (scripts/gpu_l1ab.sh, profiles/r04/l1/ab_xcd/).
+__device__ __forceinline__ void l1_ids(int& tile, int& pair) {
+  tile = blockIdx.x;
+  pair = blockIdx.y;
+}
+__device__ __forceinline__ int l1_tile() {
+  int t, p;
+  l1_ids(t, p);
+  return t;
+}
+
 struct WTile {
   float4 w[NTL][KG];
 };
@@ -299,8 +313,8 @@ struct PairLds {
   float msk[S];
 };
 
-// One (tile, pair) of the forward: X'_k, P_k, V, O, A for the 16 samples of tile blockIdx.x and
-// pair blockIdx.y (stamps: kernel 0)
+// One (tile, pair) of the forward: X'_k, P_k, V, O, A for the 16 samples of the
+// workgroup's (tile, pair), l1_ids (stamps: kernel 0)
 template <int FH>
 __device__ __forceinline__ RngSnap pair_fwd_tile(const L1Args& a, PairLds& L) {
   float* xs = L.xs;
@@ -310,7 +324,9 @@ __device__ __forceinline__ RngSnap pair_fwd_tile(const L1Args& a, PairLds& L) {
   uint8_t* kpr = L.kpr;
   float* pp = L.pp;
   float* msk = L.msk;
-  const int g = blockIdx.y, b0 = blockIdx.x * S;
+  int tile_, g;
+  l1_ids(tile_, g);
+  const int b0 = tile_ * S;
   const int k = a.pk[g], D = FH ? FH : a.D[k], H = FH ? FH : a.H, B = a.B;
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6) & 3;
   const bool desig = a.kdesig[k] == g;
@@ -338,10 +354,10 @@ __device__ __forceinline__ RngSnap pair_fwd_tile(const L1Args& a, PairLds& L) {
   L1_RT(0, 8);
   L1_ST(0, 0);
   __builtin_amdgcn_sched_barrier(0);   // (these loads issue before the weights')
+  // (W_v / W_o issue behind the first barrier: 96 workgroups issuing all three weights at once
+  // held the keep / P' phase for 13.7 K cycles, 0.0721 -> 0.0700 ms with the split, scripts/gpu_l1ab.sh)
   WTile wk, wv, wo;
   wload_nt(a.Wp[k], H, D, wave, lane, wk);
-  wload_nt(a.Wv[g], H, H, wave, lane, wv);
-  wload_nt(a.Wo[g], H, H, wave, lane, wo);
   float bpk[NTL], bvv[NTL], bov[NTL];
 #pragma unroll
   for (int u = 0; u < NTL; ++u) {
@@ -366,9 +382,11 @@ __device__ __forceinline__ RngSnap pair_fwd_tile(const L1Args& a, PairLds& L) {
     }
     pp[t] = v;
   }
-  if (a.snap && blockIdx.x == 0 && blockIdx.y == 0 && t == 0 && a.rng_live) *a.snap = rs;
+  if (a.snap && tile_ == 0 && g == 0 && t == 0 && a.rng_live) *a.snap = rs;
   __syncthreads();
   L1_ST(0, 1);
+  wload_nt(a.Wv[g], H, H, wave, lane, wv);
+  wload_nt(a.Wo[g], H, H, wave, lane, wo);
   // X' = X mask (input dropout), src/fusion.py:373
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
@@ -540,7 +558,7 @@ __device__ __forceinline__ void loss_rows(const L1Args& a, const RowGroup& rg, i
 template <int FH>
 __device__ __forceinline__ void dz1_rows(const L1Args& a, HeadLds& L, const RowGroup& rg, const float4 (&hv)[2],
                                          const float (&dl)[L1_MAXC]) {
-  const int H = FH ? FH : a.H, h4 = H / 4, C = a.C, b = blockIdx.x * S + rg.i;
+  const int H = FH ? FH : a.H, h4 = H / 4, C = a.C, b = l1_tile() * S + rg.i;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int c4 = rg.l16 + 16 * q;
@@ -564,7 +582,7 @@ __device__ __forceinline__ void dz1_rows(const L1Args& a, HeadLds& L, const RowG
 }
 
 
-// Head forward of tile blockIdx.x (src/fusion.py:406-427, :429-479): pooled, gating scores,
+// Head forward of tile l1_tile() (src/fusion.py:406-427, :429-479): pooled, gating scores,
 // adaptive weights, fused, h1 = Drop(ReLU(fused W1^T + b1)), logits.  Leaves pooled (pl), the
 // mask / score / weight rows, h1 (hs) and the logits (lg) in L.  rs: the call's rng snapshot.
 template <int FH, bool LOSS, bool SEQ = false>
@@ -575,12 +593,14 @@ __device__ __forceinline__ void head_fwd_tile(const L1Args& a, HeadLds& L, const
   HeadSmall& sm_ = L.sm;
   uint8_t* kcl = L.kcl;
   float *msk = L.msk, *sc = L.sc;
-  const int b0 = blockIdx.x * S;
+  const int b0 = l1_tile() * S;
   const int M = a.M, H = FH ? FH : a.H, B = a.B, C = a.C;
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6) & 3;
   // loads, first-needed first: the mask rows, the attended and projected rows, the small
   // operands, then W1
   const float mrow = (t < S * M && b0 + t / M < B) ? a.mask[(int64_t)b0 * M + min(t, S * M - 1)] : 0.f;   // (S M <= NT)
+  int ylab = 0;   // (the loss's label of this lane's row group, loaded with the first operands)
+  if constexpr (LOSS) ylab = (int)a.labels[min(b0 + (t >> 4), B - 1)];
   stage_small(a, sm_);
   if (t < S * M) msk[t] = mrow;
   // pooled_m = mean(P_m, A_g for every pair with query m) * mask_m (src/fusion.py:406-408): each
@@ -751,7 +771,7 @@ __device__ __forceinline__ void head_fwd_tile(const L1Args& a, HeadLds& L, const
     const RowGroup rg;
     const int b = b0 + rg.i;
     int y = 0;
-    if constexpr (LOSS) y = b < B ? (int)a.labels[b] : 0;
+    if constexpr (LOSS) y = b < B ? ylab : 0;
     float4 hv[2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -784,7 +804,7 @@ __device__ __forceinline__ void head_fwd_tile(const L1Args& a, HeadLds& L, const
   }
 }
 
-// Head backward of tile blockIdx.x from dz1 (L.fs, zero-padded past H; dz1_rows wrote it):
+// Head backward of tile l1_tile() from dz1 (L.fs, zero-padded past H; dz1_rows wrote it):
 // dfused = dz1 W1, d weights, compute_adaptive_weights backward, cvec_m (the gradient of every
 // entry of m's aggregation list).  Reads pl, msk / sc and sm from L (the forward left them there,
 // or the standalone kernel staged them); w1n: this wave's W1 columns in y = x W form.
@@ -795,7 +815,7 @@ __device__ __forceinline__ void head_bwd_tile(const L1Args& a, HeadLds& L, const
   float* dfs = L.hs;   // (h1 until dz1_rows has read it)
   HeadSmall& sm_ = L.sm;
   float *msk = L.msk, *sc = L.sc;
-  const int b0 = blockIdx.x * S;
+  const int b0 = l1_tile() * S;
   const int M = a.M, H = FH ? FH : a.H, B = a.B;
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6) & 3;
   const int h4 = H / 4;
@@ -1011,7 +1031,9 @@ __device__ __forceinline__ bool poll_eq(gu32* w, unsigned want) {
 template <int FH>
 __device__ __forceinline__ void pair_key_bwd(const L1Args& a, PairLds& L, const RngSnap& rs, int* flag,
                                              const WTile& wo, const WTile& wv) {
-  const int g = blockIdx.y, b0 = blockIdx.x * S, tile = blockIdx.x;
+  int tile, g;
+  l1_ids(tile, g);
+  const int b0 = tile * S;
   const int q = a.pq[g], k = a.pk[g];
   const int H = FH ? FH : a.H, D = FH ? FH : a.D[k], B = a.B, M = a.M;
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6) & 3;
@@ -1170,7 +1192,8 @@ __global__ __launch_bounds__(NT) void l1_fwd_loss_kernel(const L1Args a) {
   // (LDS over 80 KB: one workgroup per CU, the residency the hand-off protocol was measured at)
   __shared__ __attribute__((aligned(16))) union Lds { PairLds p; HeadLds h; char pad[82 * 1024]; } L;
   __shared__ int last, flag;
-  const int tile = blockIdx.x, g = blockIdx.y;
+  int tile, g;
+  l1_ids(tile, g);
   const int H = FH ? FH : a.H;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) & 3;
   WTile wo, wv;
