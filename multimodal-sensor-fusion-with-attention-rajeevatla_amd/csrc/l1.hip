@@ -477,17 +477,23 @@ struct HeadSmall {
 __device__ __forceinline__ void stage_small(const L1Args& a, HeadSmall& hs) {
   // every load issued before the first LDS write (unrolled over the compile-time maxima: a loop
   // with a runtime trip count, or a per-lane pointer-table index, waited for each load in turn)
+  // (unconditional loads from clamped indices, the guards as selects after them: a guarded load
+  // compiles to a branch, and the wait counts do not see through branches; the gating biases by
+  // uniform pointers -- a per-lane index into the pointer table is a vector load of the pointer
+  // and a wait for every load in flight before the load through it)
   const int t = threadIdx.x, M = a.M, H = a.H, C = a.C;
   float gv[L1_MAXM], wv[(L1_MAXC * L1_MAXH + NT - 1) / NT];
 #pragma unroll
-  for (int m = 0; m < L1_MAXM; ++m) gv[m] = (m < M && t < H) ? a.gw[m][min(t, H - 1)] : 0.f;
+  for (int m = 0; m < L1_MAXM; ++m) gv[m] = a.gw[min(m, M - 1)][min(t, H - 1)];
 #pragma unroll
-  for (int r = 0; r < (L1_MAXC * L1_MAXH + NT - 1) / NT; ++r) {
-    const int e = t + r * NT;
-    wv[r] = e < C * H ? a.W2[min(e, C * H - 1)] : 0.f;
+  for (int r = 0; r < (L1_MAXC * L1_MAXH + NT - 1) / NT; ++r) wv[r] = a.W2[min(t + r * NT, C * H - 1)];
+  float gbv = 0.f;
+#pragma unroll
+  for (int m = 0; m < L1_MAXM; ++m) {
+    const float v = a.gb[min(m, M - 1)][0];
+    if (t == m) gbv = v;
   }
-  const float gbv = t < M ? a.gb[min(t, M - 1)][0] : 0.f;
-  const float b2v = (t >= 64 && t < 64 + C) ? a.b2[min(max(t - 64, 0), C - 1)] : 0.f;
+  const float b2v = a.b2[min(max(t - 64, 0), C - 1)];
 #pragma unroll
   for (int m = 0; m < L1_MAXM; ++m)
     if (m < M && t < H) hs.gw[m * H + t] = gv[m];
@@ -598,35 +604,50 @@ __device__ __forceinline__ void head_fwd_tile(const L1Args& a, HeadLds& L, const
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6) & 3;
   // loads, first-needed first: the mask rows, the attended and projected rows, the small
   // operands, then W1
-  const float mrow = (t < S * M && b0 + t / M < B) ? a.mask[(int64_t)b0 * M + min(t, S * M - 1)] : 0.f;   // (S M <= NT)
+  // (the row guard applied where msk is written: a select right after the load became a branch whose
+  // other side waited for the load before zeroing its register)
+  const float mrow = a.mask[min((int64_t)b0 * M + min(t, S * M - 1), (int64_t)B * M - 1)];   // (S M <= NT)
   int ylab = 0;   // (the loss's label of this lane's row group, loaded with the first operands)
   if constexpr (LOSS) ylab = (int)a.labels[min(b0 + (t >> 4), B - 1)];
-  stage_small(a, sm_);
-  if (t < S * M) msk[t] = mrow;
   // pooled_m = mean(P_m, A_g for every pair with query m) * mask_m (src/fusion.py:406-408): each
-  // thread sums its float4 of every list entry in registers
+  // thread sums its float4 of every list entry in registers.  Every pooled-source load is issued
+  // first, then the small operands' loads and LDS writes (whose waits then cover one round trip for
+  // both), then the adds.  Unconditional buffer loads: an absent modality / pair reads a zero-size
+  // range, which returns zeros (a guarded load is a branch the wait counts do not see through).
   const int h4 = H / 4;
-  float4 pv[2][L1_MAXM];
+  float4 pv[2][L1_MAXM], xa[2][L1_MAXP];
   int pe[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int e = t + u * NT, i = e / h4;
     pe[u] = (i < S) ? e : -1;
     const int bb = min(b0 + min(i, S - 1), B - 1), col = 4 * (e - i * h4);
-    float4 xa[L1_MAXP];
+    const uint32_t hb = (uint32_t)B * (uint32_t)H * 4u, ho = (uint32_t)(((int64_t)bb * H + col) * 4);
     if constexpr (SEQ) {
-      // mean_L P_m from the projection GEMM's per-128-row column sums (src/fusion.py:406-408),
-      // then the pairs' attended means Abar (earlier launches).  Unconditional buffer loads (an
-      // absent modality / pair: a zero-size range, which reads zeros), all issued before the
-      // first add; column-sum rows past the first (L_m > 128) in a loop after them
-      const uint32_t hb = (uint32_t)B * (uint32_t)H * 4u, ho = (uint32_t)(((int64_t)bb * H + col) * 4);
+      // mean_L P_m from the projection GEMM's per-128-row column sums, then the pairs' attended
+      // means Abar (earlier launches); column-sum rows past the first (L_m > 128) after the adds
 #pragma unroll
       for (int m = 0; m < L1_MAXM; ++m) {
         const int nc = m < M ? a.ncol[m] : 0;
         pv[u][m] = ld_rb4(m < M ? a.P[m] : a.mask, (uint32_t)nc * hb, (uint32_t)(((int64_t)bb * nc * H + col) * 4));
       }
 #pragma unroll
-      for (int g = 0; g < L1_MAXP; ++g) xa[g] = ld_rb4(g < a.npairs ? a.A[g] : a.mask, g < a.npairs ? hb : 0u, ho);
+      for (int g = 0; g < L1_MAXP; ++g) xa[u][g] = ld_rb4(g < a.npairs ? a.A[g] : a.mask, g < a.npairs ? hb : 0u, ho);
+    } else {
+      // (the P_k / A tiles of the other pair workgroups: sc1 loads, see st_wt)
+#pragma unroll
+      for (int m = 0; m < L1_MAXM; ++m) pv[u][m] = ld_wt4(m < M ? a.P[m] : a.mask, m < M ? hb : 0u, ho);
+#pragma unroll
+      for (int g = 0; g < L1_MAXP; ++g) xa[u][g] = ld_wt4(g < a.npairs ? a.A[g] : a.mask, g < a.npairs ? hb : 0u, ho);
+    }
+  }
+  stage_small(a, sm_);
+  if (t < S * M) msk[t] = b0 + t / M < B ? mrow : 0.f;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if constexpr (SEQ) {
+      const int e = t + u * NT, i = e / h4;
+      const int bb = min(b0 + min(i, S - 1), B - 1), col = 4 * (e - i * h4);
 #pragma unroll
       for (int m = 0; m < L1_MAXM; ++m) {
         if (m >= M) break;
@@ -638,24 +659,13 @@ __device__ __forceinline__ void head_fwd_tile(const L1Args& a, HeadLds& L, const
         const float il = a.inv_L[m];
         pv[u][m] = make_float4(pv[u][m].x * il, pv[u][m].y * il, pv[u][m].z * il, pv[u][m].w * il);
       }
-    } else {
-      // (the P_k / A tiles of the other pair workgroups: sc1 loads, see st_wt)
-      const uint32_t row = (uint32_t)(((int64_t)bb * H + col) * 4);
-      const uint32_t nbytes = (uint32_t)B * (uint32_t)H * 4u;
-#pragma unroll
-      for (int m = 0; m < L1_MAXM; ++m)
-        pv[u][m] = m < M ? ld_wt4(a.P[m], nbytes, row) : make_float4(0.f, 0.f, 0.f, 0.f);
-      // (the pair list unrolled over L1_MAXP: every A load issued before the first add)
-#pragma unroll
-      for (int g = 0; g < L1_MAXP; ++g)
-        xa[g] = g < a.npairs ? ld_wt4(a.A[g], nbytes, row) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int g = 0; g < L1_MAXP; ++g) {
       const int q = g < a.npairs ? a.pq[g] : -1;   // (a guard, not a break: the loop stays unrolled)
 #pragma unroll
       for (int m = 0; m < L1_MAXM; ++m)
-        if (m == q) { pv[u][m].x += xa[g].x; pv[u][m].y += xa[g].y; pv[u][m].z += xa[g].z; pv[u][m].w += xa[g].w; }
+        if (m == q) { pv[u][m].x += xa[u][g].x; pv[u][m].y += xa[u][g].y; pv[u][m].z += xa[u][g].z; pv[u][m].w += xa[u][g].w; }
     }
   }
   if (kstamp) {
@@ -669,7 +679,8 @@ __device__ __forceinline__ void head_fwd_tile(const L1Args& a, HeadLds& L, const
 #pragma unroll
   for (int u = 0; u < NTL; ++u) {
     const int j = 16 * (wave + 4 * u) + (lane & 15);
-    b1v[u] = j < H ? a.b1[min(j, H - 1)] : 0.f;
+    b1v[u] = a.b1[min(j, H - 1)];
+    if (j >= H) b1v[u] = 0.f;
   }
   if (a.p > 0.f) keep_tile(rs, SITE_CLS, b0, H, a.p, kcl);
   __syncthreads();
@@ -1048,6 +1059,10 @@ __device__ __forceinline__ void pair_key_bwd(const L1Args& a, PairLds& L, const 
   // cvec_q rows of the tile (sc1: the head wrote them in this launch), P' of the pair (W_o / W_v:
   // the caller loaded them, a waiting workgroup before its poll)
   {
+    // the mask entry of P' first (an unconditional load: a guarded one waited for every load in
+    // flight), the cvec rows, then P' (Philox) while the cvec rows are in flight
+    const int ih = min(t / a.heads, S - 1);
+    const float mkh = a.mask[(int64_t)min(b0 + ih, B - 1) * M + k];
     const int h4 = H / 4;
     const uint32_t nbytes = (uint32_t)B * (uint32_t)M * (uint32_t)H * 4u;
     float4 v[2];
@@ -1056,13 +1071,22 @@ __device__ __forceinline__ void pair_key_bwd(const L1Args& a, PairLds& L, const 
       const int e = t + u * NT, i = min(e / h4, S - 1), c = e - (e / h4) * h4;
       v[u] = ld_wt4(a.cvec, nbytes, (uint32_t)((((int64_t)min(b0 + i, B - 1) * M + q) * H + 4 * c) * 4));
     }
+    // P'[i][h] = [mask_k != 0] keep(b h) / (1 - p) (pprime_tile's arithmetic)
+    if (t < S * a.heads) {
+      const int hh = t - ih * a.heads;
+      float pv = 0.f;
+      if (b0 + ih < B && mkh != 0.f) {
+        pv = 1.f;
+        if (a.p > 0.f) pv = keep1(rs, SITE_ATTN + g, (uint64_t)(b0 + ih) * a.heads + hh, a.p) ? a.gscale : 0.f;
+      }
+      pp[t] = pv;
+    }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int e = t + u * NT, i = e / h4, c = e - i * h4;
       if (i < S) *reinterpret_cast<float4*>(cs + i * LD + 4 * c) = b0 + i < B ? v[u] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
-  pprime_tile(a, rs, g, b0, pp);
   zero_pad(cs, H);
   __syncthreads();
   const int kq = lane >> 4, jl = lane & 15, hd = H / a.heads;
@@ -1113,7 +1137,7 @@ __device__ __forceinline__ void pair_key_bwd(const L1Args& a, PairLds& L, const 
   const bool want_dx = a.dx[k] != nullptr;
   WTile wp;
   if (want_dx) wload_nn(a.Wp[k], D, H, wave, lane, wp);
-  if (t < S) msk[t] = b0 + t < B ? a.mask[(int64_t)min(b0 + t, B - 1) * M + k] : 0.f;
+  const float mk_ = a.mask[(int64_t)min(b0 + (t & (S - 1)), B - 1) * M + k];   // (unconditional: see above)
   if (a.p > 0.f && want_dx) keep_tile(rs, SITE_IN + k, b0, D, a.p, kin);
   {
     constexpr int MK = L1_MAXM - 1;   // pairs keyed by one modality (every ordered pair present)
@@ -1161,6 +1185,7 @@ __device__ __forceinline__ void pair_key_bwd(const L1Args& a, PairLds& L, const 
     }
     zero_pad(zs, H);
   }
+  if (t < S) msk[t] = b0 + t < B ? mk_ : 0.f;
   if (!want_dx) return;
   __syncthreads();
   mma(zs, wp, acc, lane);
@@ -1424,12 +1449,19 @@ __global__ __launch_bounds__(NT) void l1_wgrad_kernel(const L1WgArgs w) {
     float ga[WG_ROWS / 2], xb[WG_ROWS / 2];
 #pragma unroll
     for (int s = 0; s < WG_ROWS / 2; ++s) {
-      const int b = rb + 2 * s, bc = min(b, w.B - 1);
-      const bool in = b < w.B;
-      const float gv = J.G[(int64_t)bc * J.ldg + min(n, J.N - 1)];
-      const float xv = J.X[(int64_t)bc * J.ldx + min(kk, J.K - 1)];
-      ga[s] = (in && n < J.N) ? gv : 0.f;
-      xb[s] = (in && kk < J.K) ? xv : 0.f;
+      const int bc = min(rb + 2 * s, w.B - 1);
+      ga[s] = J.G[(int64_t)bc * J.ldg + min(n, J.N - 1)];
+      xb[s] = J.X[(int64_t)bc * J.ldx + min(kk, J.K - 1)];
+    }
+    // (every load above issued before the first select and MFMA: left to itself the scheduler
+    // interleaved them two or three at a time with the dependent MFMA chain, one round trip per
+    // few steps)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < WG_ROWS / 2; ++s) {
+      const bool in = rb + 2 * s < w.B;
+      ga[s] = (in && n < J.N) ? ga[s] : 0.f;
+      xb[s] = (in && kk < J.K) ? xb[s] : 0.f;
     }
 #pragma unroll
     for (int s = 0; s < WG_ROWS / 2; ++s) {
