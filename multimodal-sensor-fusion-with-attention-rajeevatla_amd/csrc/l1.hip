@@ -125,6 +125,15 @@ __device__ __forceinline__ int l1_tile() {
   return t;
 }
 
+// The rng state / snapshot of the call, read through the constant address space: nothing in the
+// reading launch writes it (the live offset advances in a later launch), so the load is a scalar
+// one whose wait does not drain the vector loads issued beside it.
+typedef __attribute__((address_space(4))) const uint64_t cu64;
+__device__ __forceinline__ RngSnap load_rng(const void* p) {
+  cu64* q = (cu64*)p;
+  return RngSnap{q[0], q[1]};
+}
+
 struct WTile {
   float4 w[NTL][KG];
 };
@@ -334,7 +343,7 @@ __device__ __forceinline__ RngSnap pair_fwd_tile(const L1Args& a, PairLds& L) {
   // rng state, then the three weights of this wave's columns: the waits before the keep draws and
   // X' leave the weight loads in flight)
   RngSnap rs{0, 0};
-  if (a.rng_live) rs = RngSnap{a.rng_live[0], a.rng_live[1]};
+  if (a.rng_live) rs = load_rng(a.rng_live);
   const int d4 = D / 4;
   float4 xr[2];
   int xi[2];
@@ -917,7 +926,7 @@ template <int FH>
 __global__ __launch_bounds__(NT) void l1_head_fwd_kernel(const L1Args a) {
   __shared__ __attribute__((aligned(16))) HeadLds L;
   RngSnap rs{0, 0};
-  if (a.p > 0.f) rs = *a.snap;
+  if (a.p > 0.f) rs = load_rng(a.snap);
   head_fwd_tile<FH, false>(a, L, rs, 1, nullptr);
   // the live stream advances once per call (the pair kernel read it; the snapshot is saved)
   if (a.rng_advance && blockIdx.x == 0 && threadIdx.x == 0) a.rng_advance[1] += 1;
@@ -978,7 +987,7 @@ template <int FH, bool LOSS>
 __global__ __launch_bounds__(NT) void seq_head_kernel(const L1Args a) {
   __shared__ __attribute__((aligned(16))) HeadLds L;
   RngSnap rs{0, 0};
-  if (a.p > 0.f) rs = *a.snap;
+  if (a.p > 0.f) rs = load_rng(a.snap);
   if constexpr (!LOSS) {
     head_fwd_tile<FH, false, true>(a, L, rs, 0, nullptr);
   } else {
@@ -1299,7 +1308,7 @@ __global__ __launch_bounds__(NT) void l1_key_bwd_kernel(const L1Args a) {
       if (a.pk[g] == m && n < NPK) gl[n++] = g;
   }
   RngSnap rs{0, 0};
-  if (a.p > 0.f) rs = *a.snap;
+  if (a.p > 0.f) rs = load_rng(a.snap);
 #pragma unroll
   for (int i = 0; i < NPK; ++i) load_tile(a.cvec + (int64_t)a.pq[gl[i]] * H, M * H, B, b0, H, cs[i]);
   if (t < S) msk[t] = b0 + t < B ? a.mask[(int64_t)min(b0 + t, B - 1) * M + m] : 0.f;

@@ -536,7 +536,7 @@ struct TailArgs {
   // pairs grouped by key modality (launch_tail_*: the P_k-side kernels read P_k[b] once per group)
   int32_t nkg;
   int32_t kg_cnt[8];
-  int8_t kg_pair[8][TAIL_MAX_PAIRS];
+  int32_t kg_pair[8][TAIL_MAX_PAIRS];   // (int32: a byte in the kernarg segment is a vector load and a wait)
 };
 bool tail_supported(int M, int H, int C, int heads, int hd, int npairs);
 hipError_t launch_tail_fwd(const TailArgs& a, hipStream_t st);

@@ -366,14 +366,41 @@ __global__ __launch_bounds__(NT, 3) void tail_u_kernel(const TailArgs a) {
   auto load_rows = [&](int j0) {
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
+      // (unconditional, clamped: every use is guarded by j < Lk; a select here compiled to a
+      // branch whose other side waited for the load before zeroing its registers)
       const int j = j0 + rg + RG * i;
-      v[i] = j < Lk ? ld4(pk + (int64_t)j * H) : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[i] = ld4(pk + (int64_t)min(j, Lk - 1) * H);
     }
   };
   load_rows(0);
-  for (int i = t; i < R * Lk; i += NT) {
-    const int row = i / Lk, j = i - row * Lk;
-    pb_s[row * PS + j] = a.p[a.kg_pair[kg][row / nh]].pbar[((int64_t)b * nh + row % nh) * Lk + j];
+  const int per = nh * Lk;   // pbar floats of one pair for sample b (contiguous: (B, heads, Lk))
+  if (per % 64 == 0) {
+    // wave-uniform pair slot per chunk: its pbar pointer is a scalar load, every value load of
+    // the staging issued before the first LDS write (a per-lane index into the pair table was a
+    // vector load of the pointer and a wait, per element chunk)
+    constexpr int U = 4;
+    for (int i0 = 0; i0 < R * Lk; i0 += U * NT) {
+      float vv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = min(i0 + u * NT + t, R * Lk - 1);
+        const int slot = __builtin_amdgcn_readfirstlane(i / per);
+        vv[u] = a.p[a.kg_pair[kg][slot]].pbar[(int64_t)b * per + (i - slot * per)];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * NT + t;
+        if (i < R * Lk) {
+          const int row = i / Lk, j = i - row * Lk;
+          pb_s[row * PS + j] = vv[u];
+        }
+      }
+    }
+  } else {
+    for (int i = t; i < R * Lk; i += NT) {
+      const int row = i / Lk, j = i - row * Lk;
+      pb_s[row * PS + j] = a.p[a.kg_pair[kg][row / nh]].pbar[((int64_t)b * nh + row % nh) * Lk + j];
+    }
   }
   __syncthreads();
   for (int row = w; row < R; row += NT / 64) {   // r_{g,h}
@@ -594,11 +621,35 @@ __global__ __launch_bounds__(NT) void tail_dpbar_mfma_kernel(const TailArgs a) {
       if (k0 + 8 * q < H) av[q] = ld4(arow + 8 * q);
   };
   if (w * 32 < Lk) load_a(w, 0);
-  for (int i = t; i < KG_ROWS * (H / 4); i += NT) {
-    const int row = i / (H / 4), c4 = (i - row * (H / 4)) * 4;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (row < R) v = ld4(a.p[a.kg_pair[kg][row / nh]].dU + ((int64_t)b * nh + row % nh) * H + c4);
-    *reinterpret_cast<float4*>(&du_s[row * DS + c4]) = v;
+  const int H4 = H / 4, per = nh * H4;   // dU float4 of one pair for sample b (contiguous)
+  if (per % 64 == 0) {
+    // wave-uniform pair slot per chunk (see tail_u_kernel): rows past R are zero-filled
+    constexpr int U = 4;
+    for (int i0 = 0; i0 < KG_ROWS * H4; i0 += U * NT) {
+      float4 vv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = min(i0 + u * NT + t, R * H4 - 1);
+        const int slot = __builtin_amdgcn_readfirstlane(i / per);
+        const int e = i - slot * per;
+        vv[u] = ld4(a.p[a.kg_pair[kg][slot]].dU + (int64_t)b * nh * H + 4 * e);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * NT + t;
+        if (i < KG_ROWS * H4) {
+          const int row = i / H4, c4 = (i - row * H4) * 4;
+          *reinterpret_cast<float4*>(&du_s[row * DS + c4]) = row < R ? vv[u] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+    }
+  } else {
+    for (int i = t; i < KG_ROWS * H4; i += NT) {
+      const int row = i / H4, c4 = (i - row * H4) * 4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (row < R) v = ld4(a.p[a.kg_pair[kg][row / nh]].dU + ((int64_t)b * nh + row % nh) * H + c4);
+      *reinterpret_cast<float4*>(&du_s[row * DS + c4]) = v;
+    }
   }
   if (t < R) rowp[t] = a.p[a.kg_pair[kg][t / nh]].dpbar + ((int64_t)b * nh + t % nh) * Lk;
   for (int row = w; row < R; row += NT / 64) {   // dr_{g,h} = dObar_{g,h} . b_v,h
@@ -1005,7 +1056,7 @@ static bool tail_mfma_groups(TailArgs& m) {
       mod_of[m.nkg] = m.p[g].k;
       m.kg_cnt[m.nkg++] = 0;
     }
-    m.kg_pair[i][m.kg_cnt[i]++] = (int8_t)g;
+    m.kg_pair[i][m.kg_cnt[i]++] = g;
   }
   for (int i = 0; i < m.nkg; ++i)
     if (m.kg_cnt[i] * m.heads > KG_ROWS) return false;
