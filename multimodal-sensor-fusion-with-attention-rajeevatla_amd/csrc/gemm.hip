@@ -983,26 +983,31 @@ __global__ __launch_bounds__(256) void small_slab_kernel(const SmallSlabArgs a) 
   const int split = r % G.nsplit;
   const int batch = r / G.nsplit;
   const int k0 = split * G.kchunk, k1 = min(S.K, k0 + G.kchunk);
-  const float* ap = S.a.ptr + (int64_t)batch * G.bs_a + i;
-  const float* bp = S.b.ptr + (int64_t)batch * G.bs_b + j;
   const bool bias = j == G.N;
+  const float* ap = S.a.ptr + (int64_t)batch * G.bs_a + i;
+  const float* bp = S.b.ptr + (int64_t)batch * G.bs_b + min(j, G.N - 1);   // (the bias column reads column N - 1, unused)
   constexpr int MAXR = 256 / 8;   // kchunk <= 256 (job_small_slab)
+  // Unconditional loads from clamped rows, eight per step, the row guards applied in the sum (a
+  // guarded load compiled to a branch that waited for each load in turn)
   float av[MAXR], bv[MAXR];
 #pragma unroll
-  for (int u = 0; u < MAXR; ++u) {
-    const int kk = k0 + q + 8 * u;
-    const bool in = live && kk < k1;
-    const int ka = S.a.row_div == 1 ? kk : kk / S.a.row_div;
-    const int kb = S.b.row_div == 1 ? kk : kk / S.b.row_div;
-    av[u] = in ? ap[(int64_t)ka * S.a.ld] : 0.f;
-    bv[u] = in ? (bias ? 1.f : bp[(int64_t)kb * S.b.ld]) : 0.f;
-    if (k0 + 8 * (u + 1) >= k1) break;   // uniform per group of 8 lanes only: a bound, not a branch on data
+  for (int u0 = 0; u0 < MAXR; u0 += 8) {
+    if (k0 + 8 * u0 >= k1) break;   // (uniform per group of 8 lanes: a bound, not a branch on data)
+#pragma unroll
+    for (int u = u0; u < u0 + 8; ++u) {
+      const int kk = min(k0 + q + 8 * u, k1 - 1);
+      const int ka = S.a.row_div == 1 ? kk : kk / S.a.row_div;
+      const int kb = S.b.row_div == 1 ? kk : kk / S.b.row_div;
+      av[u] = ap[(int64_t)ka * S.a.ld];
+      bv[u] = bp[(int64_t)kb * S.b.ld];
+    }
   }
   float acc = 0.f;
 #pragma unroll
   for (int u = 0; u < MAXR; ++u) {
     if (k0 + 8 * u >= k1) break;
-    acc = fmaf(av[u], bv[u], acc);
+    const bool in = live && k0 + q + 8 * u < k1;
+    acc = fmaf(in ? av[u] : 0.f, in ? (bias ? 1.f : bv[u]) : 0.f, acc);
   }
   acc = sum8(acc);
   if (!live || q != 0) return;
