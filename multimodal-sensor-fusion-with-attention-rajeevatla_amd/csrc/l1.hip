@@ -768,7 +768,10 @@ __device__ __forceinline__ void head_fwd_tile(const L1Args& a, HeadLds& L, const
   // h1 = Drop(ReLU(fused W1^T + b1)) (classifier[0..2], src/fusion.py:323-328)
   f32x4 acc[NTL];
   mma(fs, w1, acc, lane);
-  if constexpr (LOSS) wload_nn(a.W1, H, H, wave, lane, *w1n);   // (the backward's W1 columns: in flight through the loss)
+  // (the backward's W1 columns, in flight through the loss; issued with the forward's W1 instead,
+  // they lengthened the head's load phase 2.2 -> 6.4 K cycles and the loss phase kept its 6.7 K:
+  // 0.0684 / 0.0677 vs 0.0659 / 0.0673 ms, profiles/r04/l1/ab_w1n/)
+  if constexpr (LOSS) wload_nn(a.W1, H, H, wave, lane, *w1n);
   const int kq = lane >> 4, jl = lane & 15;
 #pragma unroll
   for (int u = 0; u < NTL; ++u) {
