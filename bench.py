@@ -251,12 +251,15 @@ def cpu_baseline(w, budget_s=10.0, max_steps=400):
 
 class ModuleRunner:
     """--path module: the nn.Module path src/train.py drives -- HybridFusion.forward under
-    autograd, torch cross_entropy(label_smoothing=0.05), loss.backward() (parameter and input
+    autograd, cross_entropy(label_smoothing=0.05) (mmf_ops.cross_entropy, the HIP kernel
+    behind torch's functional signature), loss.backward() (parameter and input
     grads), then the exchange + clip + AdamW of harness.DPTrainer (flat buffers, bucketed
     all-reduce).  Eager; no graph."""
 
     def __init__(self, model, feats, mask, labels, pg, compiled=False):
         from harness import DPTrainer
+        import mmf_ops
+        self.ce = mmf_ops.cross_entropy
         self.model = model.train()
         # --path compiled: the reference trainer's torch.compile(mode="reduce-overhead")
         # (src/train.py:193-231) around the module; the optimizer step stays outside
@@ -273,7 +276,8 @@ class ModuleRunner:
         feats = dict(zip(self.names, self.feats))
         self.trainer.flat.arm()
         logits = (self.model if eager else self.fwd)(feats, self.mask)
-        loss = torch.nn.functional.cross_entropy(logits, self.labels, label_smoothing=0.05)
+        # (mmf_ops.cross_entropy: torch's cross_entropy(label_smoothing) in one HIP launch)
+        loss = self.ce(logits, self.labels, label_smoothing=0.05)
         loss.backward()
         self.loss = loss.detach()
 

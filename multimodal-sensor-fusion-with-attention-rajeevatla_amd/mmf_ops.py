@@ -594,3 +594,47 @@ def eager_tensor(t: Tensor) -> bool:
     tensors AOTAutograd traces the backward formula with (torch.compiler.is_compiling() is
     False there)."""
     return type(t) is torch.Tensor and not torch.compiler.is_compiling()
+
+
+# ============================================================================ CrossEntropyLoss(label_smoothing)
+@torch.library.custom_op("mmfusion::cross_entropy_ls_fwd", mutates_args=(), device_types="cuda")
+def cross_entropy_ls_fwd(logits: Tensor, labels: Tensor, label_smoothing: float) -> Tuple[Tensor, Tensor]:
+    """nn.CrossEntropyLoss(label_smoothing=eps) with reduction "mean" (src/train.py:185-186,
+    310) in one launch of head.hip's cross_entropy_kernel: -> (mean loss, d loss / d logits).
+    Labels must lie in [0, C) (the kernel does not check them)."""
+    L = _nat.lib()
+    B, C = logits.shape
+    dev = logits.device
+    loss = torch.empty((), dtype=torch.float32, device=dev)
+    dlogits = torch.empty(B, C, dtype=torch.float32, device=dev)
+    rc = L.mmf_cross_entropy_ls(B, C, logits.data_ptr(), labels.data_ptr(), float(label_smoothing), 1.0,
+                                loss.data_ptr(), dlogits.data_ptr(), _nat.stream_ptr(dev))
+    _nat.check(rc, "CrossEntropyLoss(label_smoothing)")
+    return loss, dlogits
+
+
+@cross_entropy_ls_fwd.register_fake
+def _(logits, labels, label_smoothing):
+    return logits.new_empty(()), torch.empty_like(logits)
+
+
+def _ce_setup(ctx, inputs, output):
+    ctx.save_for_backward(output[1])
+
+
+def _ce_backward(ctx, dloss, _ddlogits):
+    (dlogits,) = ctx.saved_tensors
+    return dlogits * dloss, None, None
+
+
+cross_entropy_ls_fwd.register_autograd(_ce_backward, setup_context=_ce_setup)
+
+
+def cross_entropy(logits: Tensor, labels: Tensor, label_smoothing: float = 0.0) -> Tensor:
+    """Drop-in for torch.nn.functional.cross_entropy(logits, labels, label_smoothing=...) on
+    (B, C) fp32 logits, int64 labels, reduction "mean": the loss and its gradient in one HIP
+    launch (torch's composes it from log_softmax, nll_loss and the smoothing term, about eight
+    launches forward and backward)."""
+    if logits.dim() != 2 or logits.dtype != torch.float32 or labels.dtype != torch.int64:
+        raise ValueError("cross_entropy: (B, C) float32 logits and int64 labels")
+    return torch.ops.mmfusion.cross_entropy_ls_fwd(logits.contiguous(), labels.contiguous(), float(label_smoothing))[0]
