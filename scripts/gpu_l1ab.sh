@@ -1,6 +1,9 @@
 #!/bin/bash
 # L1 A/B: the L1 GPU tests on the product library, then the C2-L1 line alternating the product
-# library (A) and libmmfusion_exp.so (B), and the stamps of both.
+# library (A) and libmmfusion_exp.so (B), and the stamps of both.  B is built beforehand from the
+# product objects with l1.hip recompiled under the variant's -D flag (and libmmfusion_expst.so with
+# -DMMF_STAMPS added), e.g. in csrc/: hipcc $(CXXFLAGS) -DVARIANT -c l1.hip -o /tmp/l1.o &&
+# hipcc -shared --offload-arch=gfx950 -o libmmfusion_exp.so <the other .o files> /tmp/l1.o
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
