@@ -78,7 +78,7 @@ def _oracle_flat_grad(model, feats, mask, labels) -> torch.Tensor:
     return flat
 
 
-def _cpu_rank(rank: int, world: int, port: int, out: str) -> None:
+def _cpu_rank(rank: int, world: int, port: int, out: str, accumulate: int = 1) -> None:
     _setup(rank, world, port)
     try:
         from train_step import allreduce_flat, shard_batch
@@ -86,7 +86,17 @@ def _cpu_rank(rank: int, world: int, port: int, out: str) -> None:
         feats, mask, labels = _global_batch()
         lf, lm, ll = shard_batch(feats, mask, labels, rank, world)
         assert lm.size(0) == B // world
-        flat = _oracle_flat_grad(model, lf, lm, ll)
+        if accumulate == 1:
+            flat = _oracle_flat_grad(model, lf, lm, ll)
+        else:
+            # Lightning's accumulate_grad_batches (config/base.yaml:75): the shard as `accumulate`
+            # equal micro-batches, each loss scaled by 1 / accumulate, gradients summed before the
+            # one exchange (what HybridTrainStep's forward_backward does on the device)
+            flat = None
+            for i in range(accumulate):
+                mf, mm, ml = shard_batch(lf, lm, ll, i, accumulate)
+                g = _oracle_flat_grad(model, mf, mm, ml) / accumulate
+                flat = g if flat is None else flat + g
         allreduce_flat(flat, dist.group.WORLD, world)
         flat /= world
         if rank == 0:
@@ -95,9 +105,10 @@ def _cpu_rank(rank: int, world: int, port: int, out: str) -> None:
         dist.destroy_process_group()
 
 
-def test_dp_gloo_cpu_matches_full_batch(tmp_path):
+@pytest.mark.parametrize("accumulate", [1, 4])
+def test_dp_gloo_cpu_matches_full_batch(tmp_path, accumulate):
     out = str(tmp_path / "dp.pt")
-    mp.spawn(_cpu_rank, args=(2, _free_port(), out), nprocs=2, join=True)
+    mp.spawn(_cpu_rank, args=(2, _free_port(), out, accumulate), nprocs=2, join=True)
     r = torch.load(out, weights_only=True)
     err = (r["dp"] - r["full"]).abs().max() / r["full"].abs().max()
     assert err <= TOL, float(err)
