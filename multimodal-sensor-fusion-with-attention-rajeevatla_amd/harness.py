@@ -370,7 +370,11 @@ class DPTrainer:
         """One micro-batch: forward, loss / accumulate, backward; `sync` arms the exchange."""
         self.model.train()
         logits = self.model(features, mask)
-        loss = F.cross_entropy(logits, labels, label_smoothing=self.smoothing)
+        if logits.is_cuda and logits.dim() == 2 and logits.dtype == torch.float32 and labels.dtype == torch.int64:
+            import mmf_ops   # (the loss and its gradient in one HIP launch)
+            loss = mmf_ops.cross_entropy(logits, labels, label_smoothing=self.smoothing)
+        else:
+            loss = F.cross_entropy(logits, labels, label_smoothing=self.smoothing)
         if sync:
             self.flat.arm()
         (loss / self.accumulate).backward()
