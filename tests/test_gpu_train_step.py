@@ -348,3 +348,37 @@ def test_tile_head_train_step(mods, hidden, monkeypatch):
                 continue
             tol = 1e-4 * max(float(b.abs().max()), 1e-6)
             assert float((a - b).abs().max()) <= tol, float((a - b).abs().max())
+
+
+@pytest.mark.parametrize("M_,H_,C_,B_", [(4, 32, 7, 20), (2, 128, 3, 17)])
+def test_tile_head_module_path_matches_per_sample_head(mods, M_, H_, C_, B_, monkeypatch):
+    """The module path (HybridFusion.forward + autograd) with the 16-sample tile head against the
+    per-sample head kernels (MMF_TAIL_HEAD_GEMV=1) on the same weights, inputs and dropout
+    stream: four modalities (twelve pairs, the tile head's maxima) at H = 32 and two at H = 128,
+    ragged tiles, train mode -- logits and every gradient to 1e-5 of the largest element + 1e-8
+    (fp32 reassociation only)."""
+    fusion, _ = mods
+    g = torch.Generator().manual_seed(M_ * 7 + H_)
+    feats = [torch.randn(B_, 128, 16, generator=g) for _ in range(M_)]
+    mask = (torch.rand(B_, M_, generator=g) < 0.8).float()
+    mask[2] = 0.0
+    runs = []
+    for gemv in (False, True):
+        if gemv:
+            monkeypatch.setenv("MMF_TAIL_HEAD_GEMV", "1")
+        torch.manual_seed(5)
+        model = fusion.HybridFusion({f"m{i}": 16 for i in range(M_)}, hidden_dim=H_, num_classes=C_, num_heads=4,
+                                    dropout=0.2).cuda().train()
+        model._rng_state.copy_(torch.tensor([0xABC, 1], dtype=torch.int64))
+        xs = {f"m{i}": f.cuda().requires_grad_(True) for i, f in enumerate(feats)}
+        logits = model(xs, mask.cuda())
+        (logits * torch.linspace(-1, 1, C_, device="cuda")).sum().backward()
+        torch.cuda.synchronize()
+        runs.append([logits.detach().cpu()] + [xs[k].grad.cpu() for k in sorted(xs)] +
+                    [p.grad.cpu() for _, p in sorted(model.named_parameters())])
+        monkeypatch.delenv("MMF_TAIL_HEAD_GEMV", raising=False)
+    for a, b in zip(*runs):
+        # (+1e-8: gradients that cancel to ~1e-10 -- the gating biases, whose softmax-backward
+        # terms sum to zero over the modalities -- carry only rounding noise)
+        tol = 1e-5 * float(b.abs().max()) + 1e-8
+        assert float((a - b).abs().max()) <= tol, (float((a - b).abs().max()), tol)
