@@ -502,10 +502,13 @@ __global__ __launch_bounds__(NTW) void tail_ob_mfma_kernel(const TailArgs a) {
   float rs[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
+    // (unconditional, clamped: a row past B is computed but never stored; a guarded load was a
+    // branch whose other side waited for every load in flight)
     const int s = s0 + acc_row(r, hf);
-    rs[r] = s < B ? P.r[(int64_t)s * nh + hh] : 0.f;
+    rs[r] = P.r[(int64_t)min(s, B - 1) * nh + hh];
   }
   const float bvn = P.bv[n], bon = P.bo[n];
+  __builtin_amdgcn_sched_barrier(0);   // (every load above in flight before the first MFMA)
   // Obar = U W_v^T + r b_v
   f32x16 acc = mfma8(au, bv, zero16());
   split_reduce(part, acc, kq, ts, lane);
