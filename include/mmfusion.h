@@ -56,7 +56,8 @@ enum {
   MMF_OK = 0,
   MMF_EINVAL = 1,   /* bad shape / argument (reference would raise) */
   MMF_ELIMIT = 2,   /* outside the kernel limits (e.g. head_dim > 64) */
-  MMF_EHIP = 3      /* HIP runtime error while enqueueing */
+  MMF_EHIP = 3,     /* HIP runtime error while enqueueing */
+  MMF_ETIMEOUT = 4  /* a bounded inter-workgroup wait of a training step gave up (mmf_hybrid_train_status) */
 };
 
 /* nn.Linear parameters (and their gradients). */
@@ -306,6 +307,16 @@ int mmf_adamw_step(int64_t n, float* param, const float* grad, float* exp_avg, f
  * points into -- and advance *step_dev, for mmf_clip_adamw_apply_dev (the L = 1 plan fills them in
  * its weight-gradient launch; others run the reduction pass of mmf_clip_adamw_step_dev here). */
 size_t mmf_hybrid_train_sync_bytes(const mmf_hybrid_desc* d);
+/* Status of the train steps issued on `sync` so far: reads the sync buffer's error word on `stream`
+ * (a 4-byte device-to-host copy, then a stream synchronize).  The launch-lean L = 1 step's waiting
+ * workgroups poll for their tile's head a bounded number of times (co-residency is checked against
+ * the device's reported occupancy before launch, but another stream or process may hold CUs); a
+ * wait that gives up leaves that tile's gradients unwritten, sets the error word, and the step's
+ * weight-gradient launch then returns every other sync word to 0, writes loss_out[0] = NaN and one
+ * +inf clip partial (clip coefficient 0: mmf_clip_adamw_apply_dev applies a zero gradient).  Returns
+ * MMF_OK, or MMF_ETIMEOUT when the error word is set (cleared first when `clear`); the next call
+ * after a timeout starts from clean sync words. */
+int mmf_hybrid_train_status(const mmf_hybrid_desc* d, void* sync, int clear, void* stream);
 int mmf_hybrid_train_step(const mmf_hybrid_desc* d, const mmf_hybrid_params* params, const float* const* x,
                           const float* mask, const int64_t* labels, float label_smoothing, float loss_scale,
                           uint64_t* rng_state, void* saved, void* workspace, void* sync, float* logits,

@@ -220,28 +220,48 @@ __global__ void rng_snapshot_kernel(uint64_t* state, RngSnap* snap) {
 
 // nn.CrossEntropyLoss(label_smoothing=eps), reduction='mean':
 // loss_i = -(1-eps) log p_{y_i} - eps/C sum_c log p_c ; dlogits = (p - ((1-eps) onehot + eps/C)) / B
+constexpr int64_t CE_IGNORE_INDEX = -100;   // torch.nn.CrossEntropyLoss(ignore_index=-100)
+
 __global__ __launch_bounds__(NT) void cross_entropy_kernel(int B, int C, const float* logits,
                                                            const int64_t* labels, float eps,
                                                            float gscale, float* loss, float* dlogits) {
   __shared__ float red[NT];
+  __shared__ int cnt[NT / 64];
   const int t = threadIdx.x;
+  // torch's nn.CrossEntropyLoss defaults: rows labelled ignore_index (-100) add nothing and get a
+  // zero gradient, the mean runs over the other rows (every row valid: the count is B, so the same
+  // bits as a plain mean over B).  A label outside [0, C) (torch raises) makes the loss NaN and is
+  // never used as an index.
+  int nv = 0;
+  for (int i = t; i < B; i += NT) nv += labels[i] != CE_IGNORE_INDEX;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) nv += __shfl_xor(nv, off);
+  if ((t & 63) == 0) cnt[t >> 6] = nv;
+  __syncthreads();
+  const float nvalid = (float)((cnt[0] + cnt[1]) + (cnt[2] + cnt[3]));
   float acc = 0.f;
   for (int i = t; i < B; i += NT) {
     const float* z = logits + (int64_t)i * C;
+    const int64_t yl = labels[i];
+    float* d = dlogits + (int64_t)i * C;
+    if (yl == CE_IGNORE_INDEX) {
+      for (int c = 0; c < C; ++c) d[c] = 0.f;
+      continue;
+    }
+    const bool bad = yl < 0 || yl >= C;
+    const int y = bad ? 0 : (int)yl;
     float mx = -INFINITY;
     for (int c = 0; c < C; ++c) mx = fmaxf(mx, z[c]);
     float se = 0.f, sz = 0.f;
     for (int c = 0; c < C; ++c) { se += __expf(z[c] - mx); sz += z[c]; }
     const float lse = mx + __logf(se);
-    const int y = (int)labels[i];
     // (an explicit fma: l1.hip loss_rows forms the same value bit for bit, whatever contraction
     // each context's compiler would choose)
-    acc += __builtin_fmaf(1.f - eps, lse - z[y], eps * (lse - sz / (float)C));
-    float* d = dlogits + (int64_t)i * C;
+    acc += bad ? NAN : __builtin_fmaf(1.f - eps, lse - z[y], eps * (lse - sz / (float)C));
     for (int c = 0; c < C; ++c) {
       const float pc = __expf(z[c] - lse);
       const float tgt = (c == y ? (1.f - eps) : 0.f) + eps / (float)C;
-      d[c] = (pc - tgt) / (float)B * gscale;
+      d[c] = (pc - tgt) / nvalid * gscale;
     }
   }
   red[t] = acc;
@@ -250,7 +270,7 @@ __global__ __launch_bounds__(NT) void cross_entropy_kernel(int B, int C, const f
     if (t < s) red[t] += red[t + s];
     __syncthreads();
   }
-  if (t == 0) loss[0] = red[0] / (float)B;
+  if (t == 0) loss[0] = red[0] / nvalid;
 }
 
 // Global gradient norm for clipping (torch.nn.utils.clip_grad_norm_, norm_type 2, as
@@ -263,6 +283,8 @@ constexpr int CLIP_BLOCKS = 256;
 // one slot per output tile) fills up to all of them.  Thread t of the clip reduction adds slots t,
 // t + 256, t + 512, t + 768 in that order (in double: the zero slots add exact zeros).
 constexpr int CLIP_SLOTS = 4 * CLIP_BLOCKS;
+// (the L = 1 weight-gradient launch fills and zeroes CLIP_PARTIAL_SLOTS of them: the same count)
+static_assert(CLIP_SLOTS == CLIP_PARTIAL_SLOTS, "clip partial slots out of sync with l1.hip's producer");
 
 __global__ __launch_bounds__(NT) void grad_sumsq_kernel(int64_t n, const float* __restrict__ g,
                                                         float* __restrict__ partial, int64_t* step_incr) {

@@ -511,6 +511,14 @@ bool lean_l1(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, const float* 
   return aligned16(W->cls1.w);
 }
 
+// the C2 shape of the L = 1 kernels (l1.hip l1_full): H and every input width 128
+bool l1_desc_full(const mmf_hybrid_desc* d) {
+  if (d->hidden != 128) return false;
+  for (int m = 0; m < d->num_modalities; ++m)
+    if (d->in_dim[m] != 128) return false;
+  return true;
+}
+
 void fill_l1(L1Args& a, const mmf_hybrid_desc* d, const mmf_hybrid_params* W, const float* const* x,
              const float* mask, const Saved& s) {
   memset(&a, 0, sizeof(a));
@@ -1210,6 +1218,30 @@ size_t mmf_hybrid_train_sync_bytes(const mmf_hybrid_desc* d) {
   return std::max<size_t>(256, (4 * (tiles * (3 + L1_MAXM) + 1) + 255) / 256 * 256);
 }
 
+int mmf_hybrid_train_status(const mmf_hybrid_desc* d, void* sync, int clear, void* stream) {
+  const int rc = check_hybrid(d);
+  if (rc) return rc;
+  if (!sync) return fail(MMF_EINVAL, "train status: null sync buffer");
+  // the error word follows the tile words (l1.hip SyncWords)
+  const size_t tiles = ((size_t)d->batch + 15) / 16;
+  uint32_t* err = static_cast<uint32_t*>(sync) + tiles * (3 + L1_MAXM);
+  hipStream_t st = (hipStream_t)stream;
+  uint32_t v = 0;
+  if (hipMemcpyAsync(&v, err, sizeof(v), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return fail(MMF_EHIP, "train status: reading the error word failed");
+  if (v == 0) return MMF_OK;
+  if (clear) {
+    static const uint32_t zero = 0;
+    if (hipMemcpyAsync(err, &zero, sizeof(zero), hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return fail(MMF_EHIP, "train status: clearing the error word failed");
+  }
+  return fail(MMF_ETIMEOUT, "train step: a workgroup of the one-launch L = 1 step gave up waiting for its tile's "
+                            "head (the grid was not co-resident); that step's gradients are incomplete (its loss "
+                            "is NaN, its update applied a zero gradient); the sync words were reset");
+}
+
 int mmf_hybrid_train_step(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, const float* const* x,
                           const float* mask, const int64_t* labels, float label_smoothing, float loss_scale,
                           uint64_t* rng_state, void* saved, void* workspace, void* sync, float* logits,
@@ -1222,7 +1254,8 @@ int mmf_hybrid_train_step(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, 
     return fail(MMF_EINVAL, "null argument");
   if (clip_partial && !step_dev) return fail(MMF_EINVAL, "train step: clip partials need the step counter");
   // (the one-launch kernel needs its tiles x pairs workgroups resident at once, one per CU)
-  if (sync && lean_l1(d, W, x) && (int64_t)((d->batch + 15) / 16) * d->num_pairs <= device_cu_count()) {
+  if (sync && lean_l1(d, W, x) &&
+      (int64_t)((d->batch + 15) / 16) * d->num_pairs <= l1_train_capacity(l1_desc_full(d))) {
     MathScope math_(d->matmul_precision);
     hipStream_t st = (hipStream_t)stream;
     Bump bs(saved);

@@ -24,6 +24,7 @@
 //                                  + the exactly-zero query / key projection gradients
 // Dropout draws are the library's Philox streams (same sites and element indices as the
 // general plan: tests/_philox.py replays them for the oracle).
+#include <cstdlib>
 #include <cstring>
 
 #include "mmf_device.h"
@@ -556,7 +557,11 @@ __device__ __forceinline__ void loss_rows(const L1Args& a, const RowGroup& rg, i
     if (c == y) zy = z[c];
   }
   const float lse = mx + __logf(se);
-  if (b < B && rg.l16 == 0) st_wt(a.loss_rows + b, __builtin_fmaf(1.f - eps, lse - zy, eps * (lse - sz / (float)C)));
+  // (a label outside [0, C) -- torch raises, ignore_index included: the fused step's mean is over
+  // all B rows -- makes the row's loss NaN, so the step's loss reads NaN)
+  const bool bad = (unsigned)y >= (unsigned)C;
+  if (b < B && rg.l16 == 0)
+    st_wt(a.loss_rows + b, bad ? NAN : __builtin_fmaf(1.f - eps, lse - zy, eps * (lse - sz / (float)C)));
 #pragma unroll
   for (int c = 0; c < L1_MAXC; ++c) {
     dl[c] = 0.f;
@@ -1043,8 +1048,8 @@ __device__ __forceinline__ SyncWords sync_words(const L1Args& a) {
   gu32* base = (gu32*)a.tile_cnt;
   return SyncWords{base, base + tiles, base + 2 * tiles, base + 3 * tiles, base + (3 + L1_MAXM) * tiles};
 }
-__device__ __forceinline__ bool poll_eq(gu32* w, unsigned want) {
-  for (unsigned i = 0; i < (1u << 22); ++i) {
+__device__ __forceinline__ bool poll_eq(gu32* w, unsigned want, unsigned bound) {
+  for (unsigned i = 0; i < bound; ++i) {
     if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == want) return true;
     __builtin_amdgcn_s_sleep(2);
   }
@@ -1265,7 +1270,7 @@ __global__ __launch_bounds__(NT) void l1_fwd_loss_kernel(const L1Args a) {
     wload_nn(a.Wo[g], H, H, wave, lane, wo);
     wload_nn(a.Wv[g], H, H, wave, lane, wv);
     if (threadIdx.x == 0) {
-      const bool ok = poll_eq(sw.done + tile, 1u);
+      const bool ok = poll_eq(sw.done + tile, 1u, a.poll_bound);
       if (ok) {
         // the last of the tile's waiting workgroups to see the head done returns the words to 0
         if (__hip_atomic_fetch_add(sw.seen + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
@@ -1412,8 +1417,17 @@ __global__ __launch_bounds__(NT) void l1_wgrad_kernel(const L1WgArgs w) {
   if ((w.loss || w.clip_partial || w.rng_advance) && tile == gridDim.x - 1) {
     // the extra workgroup: the batch-mean loss in cross_entropy_kernel's order (per-thread strided
     // sums, then a tree); the clip partial slots no tile fills zeroed; the step counter advanced
+    // a poll of the forward launch timed out (sync words: the error word after the tile words):
+    // the step's outputs are incomplete.  The tile words go back to 0 so the next call starts
+    // clean, the loss reads NaN and one clip partial +inf (norm inf, clip coefficient 0: the update
+    // applies a zero gradient); the error word stays for the host (mmf_hybrid_train_status)
+    const bool failed = w.sync && __hip_atomic_load(w.sync + w.sync_words, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT) != 0u;
+    if (failed)
+      for (int s = t; s < w.sync_words; s += NT) w.sync[s] = 0u;
     if (w.clip_partial)
-      for (int s = w.ntiles + t; s < CLIP_PARTIAL_SLOTS; s += NT) w.clip_partial[s] = 0.f;
+      for (int s = w.ntiles + t; s < CLIP_PARTIAL_SLOTS; s += NT)
+        w.clip_partial[s] = (failed && s == w.ntiles) ? INFINITY : 0.f;
     if (w.step_incr && t == 0) w.step_incr[0] += 1;
     if (w.rng_advance && t == 0) w.rng_advance[1] += 1;   // (launch_l1_train: every forward workgroup has read it)
     if (!w.loss) return;
@@ -1426,7 +1440,7 @@ __global__ __launch_bounds__(NT) void l1_wgrad_kernel(const L1WgArgs w) {
       if (t < s) lred[t] += lred[t + s];
       __syncthreads();
     }
-    if (t == 0) w.loss[0] = lred[0] / (float)w.B;
+    if (t == 0) w.loss[0] = failed ? NAN : lred[0] / (float)w.B;
     return;
   }
   if (tile >= w.ntiles) {
@@ -1520,6 +1534,14 @@ __global__ __launch_bounds__(NT) void l1_wgrad_kernel(const L1WgArgs w) {
 }
 
 // the C2 shape: every hidden and input width 128 (compile-time tile guards)
+// polls of the head's done word before a waiting workgroup gives up: 2^22 (about 0.3 s with the
+// s_sleep between polls); MMF_L1_POLL_BOUND overrides it (the timeout test sets 0: every waiter
+// times out at once)
+unsigned l1_poll_bound() {
+  const char* e = getenv("MMF_L1_POLL_BOUND");
+  return e ? (unsigned)strtoul(e, nullptr, 0) : (1u << 22);
+}
+
 bool l1_full(const L1Args& a) {
   if (a.H != 128) return false;
   for (int m = 0; m < a.M; ++m)
@@ -1528,6 +1550,20 @@ bool l1_full(const L1Args& a) {
 }
 
 }  // namespace
+
+// workgroups of l1_fwd_loss_kernel the device holds at once: the occupancy the runtime reports
+// for the kernel at its block size and LDS, times the compute units (cached per instantiation)
+int l1_train_capacity(bool full) {
+  static int cap[2] = {-1, -1};
+  int& c = cap[full ? 1 : 0];
+  if (c < 0) {
+    int per_cu = 0;
+    hipError_t e = full ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, l1_fwd_loss_kernel<128>, NT, 0)
+                        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, l1_fwd_loss_kernel<0>, NT, 0);
+    c = (e == hipSuccess && per_cu > 0) ? per_cu * device_cu_count() : 0;
+  }
+  return c;
+}
 
 hipError_t launch_l1_forward(const L1Args& a, hipStream_t st) {
   if (a.M > L1_MAXM || a.npairs > L1_MAXP || a.H > L1_MAXH || a.H % 4 != 0 || a.C > L1_MAXC || a.heads > 8)
@@ -1611,10 +1647,13 @@ hipError_t launch_l1_train(const L1Args& a, const L1WgArgs& w_in, hipStream_t st
   for (int m = 0; m < a.M; ++m)
     if (a.D[m] > L1_MAXD || a.D[m] % 4 != 0) return hipErrorInvalidValue;
   const unsigned tiles = (unsigned)((a.B + S - 1) / S);
-  // every workgroup of the one-launch kernel resident at once (one per CU): its polls end
-  if (tiles * (unsigned)a.npairs > (unsigned)device_cu_count()) return hipErrorInvalidValue;
-  const double B = a.B, H = a.H;
   const bool full = l1_full(a);
+  // every workgroup of the one-launch kernel resident at once, by the occupancy the device reports
+  // for this kernel (one per CU: its LDS); a grid that does not fit is refused before launch.  The
+  // polls are bounded all the same (another stream or process may hold CUs): a timeout is reported
+  // through the error word and the weight-gradient launch resets the sync words
+  if (tiles * (unsigned)a.npairs > (unsigned)l1_train_capacity(full)) return hipErrorInvalidValue;
+  const double B = a.B, H = a.H;
   hipError_t e;
   {
     double fl = 2.0 * B * H * (H + a.C) + 4.0 * a.M * B * H + 2.0 * B * H * (H + a.C);
@@ -1633,6 +1672,7 @@ hipError_t launch_l1_train(const L1Args& a, const L1WgArgs& w_in, hipStream_t st
     by += 4.0 * a.npairs * (2.0 * B * H + 2.0 * H * H);
     L1Args af = a;
     af.rng_advance = nullptr;   // (advanced by the weight-gradient launch)
+    af.poll_bound = l1_poll_bound();
     ProfLaunch prof_(st, full ? "l1_fwd_loss_kernel<128>" : "l1_fwd_loss_kernel<0>", fl, by);
     if (full) mmf_launch(l1_fwd_loss_kernel<128>, dim3(tiles, a.npairs), dim3(NT), 0, st, af);
     else mmf_launch(l1_fwd_loss_kernel<0>, dim3(tiles, a.npairs), dim3(NT), 0, st, af);
@@ -1640,6 +1680,8 @@ hipError_t launch_l1_train(const L1Args& a, const L1WgArgs& w_in, hipStream_t st
   if ((e = hipGetLastError()) != hipSuccess) return e;
   L1WgArgs w = w_in;
   w.rng_advance = a.rng_advance;
+  w.sync = a.tile_cnt;
+  w.sync_words = (int32_t)(tiles * (3 + L1_MAXM));   // (SyncWords: the error word follows them)
   double fl = 0.0, by = 0.0;
   for (int i = 0; i < w.njobs; ++i) {
     const L1WgJob& J = w.j[i];

@@ -480,7 +480,7 @@ hipError_t launch_clip_adamw_apply(int64_t n, float* p, const float* g, float* m
                                    const float* lr_dev, float b1, float b2, float eps, float wd, float gscale,
                                    float max_norm, float* norm_out, float* coef_out, const float* partial,
                                    hipStream_t st);
-constexpr int CLIP_PARTIAL_SLOTS = 1024;   // (head.hip CLIP_SLOTS)
+constexpr int CLIP_PARTIAL_SLOTS = 1024;   // (head.hip: static_assert(CLIP_SLOTS == CLIP_PARTIAL_SLOTS))
 hipError_t launch_clip_adamw(int64_t n, float* p, const float* g, float* m, float* v, int64_t* step,
                              const float* lr_dev, float b1, float b2, float eps, float wd, float gscale,
                              float max_norm, float* norm_out, float* coef_out, float* partial, hipStream_t st);
@@ -587,6 +587,7 @@ struct L1Args {
   // the one-launch forward + loss + head backward of a training step (launch_l1_train)
   uint32_t* tile_cnt;                 // the one-launch step's sync words (zero between calls):
                                       // tiles x (arrivals, head done, seen, L1_MAXM key arrivals), error
+  uint32_t poll_bound;                // polls of the head's done word before a waiter gives up (timeout)
   const int64_t* labels;
   float ls_eps, loss_scale;           // label smoothing; dlogits scale (1 / accumulation steps)
   float* loss_rows;                   // (B) per-sample loss
@@ -610,10 +611,18 @@ struct L1WgArgs {
   float* clip_partial;                   // optional: squared-norm partial per output tile (CLIP_PARTIAL_SLOTS)
   int64_t* step_incr;                    // optional: the optimizer step counter, advanced once
   uint64_t* rng_advance;                 // optional: the live dropout state's offset, advanced once
+  // optional (launch_l1_train): the one-launch step's sync words.  The extra workgroup reads the
+  // error word the forward launch may have set (a waiter's poll timed out); if set it returns the
+  // sync_words tile words to 0 (the next call starts clean), writes loss = NaN and one +inf clip
+  // partial (the update then applies a zero gradient), and leaves the error word for the host
+  // (mmf_hybrid_train_status)
+  uint32_t* sync; int32_t sync_words;
 };
 hipError_t launch_l1_forward(const L1Args& a, hipStream_t st);
 hipError_t launch_l1_backward(const L1Args& a, const L1WgArgs& w, hipStream_t st);
 // forward + cross-entropy + backward of a training step: three launches
 hipError_t launch_l1_train(const L1Args& a, const L1WgArgs& w, hipStream_t st);
+// workgroups of the one-launch step's forward kernel the device holds at once (occupancy x CUs)
+int l1_train_capacity(bool full_h128);
 
 }  // namespace mmf

@@ -44,7 +44,7 @@ LIB_PATH = os.environ.get("MMF_LIB_PATH") or os.path.join(_HERE, "csrc", "libmmf
 
 EXPORTED_SYMBOLS = (
     "mmf_hybrid_saved_bytes", "mmf_hybrid_workspace_bytes", "mmf_hybrid_forward",
-    "mmf_hybrid_backward", "mmf_hybrid_train_sync_bytes", "mmf_hybrid_train_step",
+    "mmf_hybrid_backward", "mmf_hybrid_train_sync_bytes", "mmf_hybrid_train_status", "mmf_hybrid_train_step",
     "mmf_adaptive_weights_workspace_bytes", "mmf_adaptive_weights",
     "mmf_adaptive_weights_backward",
     "mmf_cma_saved_bytes", "mmf_cma_workspace_bytes", "mmf_cma_forward", "mmf_cma_backward",
@@ -129,6 +129,8 @@ def lib() -> ctypes.CDLL:
     L.mmf_hybrid_backward.restype = c_int32
     L.mmf_hybrid_train_sync_bytes.argtypes = [POINTER(HybridDesc)]
     L.mmf_hybrid_train_sync_bytes.restype = sz
+    L.mmf_hybrid_train_status.argtypes = [POINTER(HybridDesc), vp, c_int32, vp]
+    L.mmf_hybrid_train_status.restype = c_int32
     L.mmf_hybrid_train_step.argtypes = [POINTER(HybridDesc), POINTER(HybridParams), vp, vp, vp, c_float, c_float,
                                         vp, vp, vp, vp, vp, vp, vp, vp, POINTER(HybridGrads), vp, vp, vp, vp,
                                         c_int64, vp]

@@ -601,7 +601,9 @@ def eager_tensor(t: Tensor) -> bool:
 def cross_entropy_ls_fwd(logits: Tensor, labels: Tensor, label_smoothing: float) -> Tuple[Tensor, Tensor]:
     """nn.CrossEntropyLoss(label_smoothing=eps) with reduction "mean" (src/train.py:185-186,
     310) in one launch of head.hip's cross_entropy_kernel: -> (mean loss, d loss / d logits).
-    Labels must lie in [0, C) (the kernel does not check them)."""
+    Rows labelled -100 (torch's default ignore_index) add nothing and get a zero gradient, the
+    mean is over the other rows; a label outside [0, C) otherwise (torch raises) makes the loss
+    NaN and is never used as an index."""
     L = _nat.lib()
     B, C = logits.shape
     dev = logits.device
@@ -630,11 +632,16 @@ def _ce_backward(ctx, dloss, _ddlogits):
 cross_entropy_ls_fwd.register_autograd(_ce_backward, setup_context=_ce_setup)
 
 
-def cross_entropy(logits: Tensor, labels: Tensor, label_smoothing: float = 0.0) -> Tensor:
-    """Drop-in for torch.nn.functional.cross_entropy(logits, labels, label_smoothing=...) on
-    (B, C) fp32 logits, int64 labels, reduction "mean": the loss and its gradient in one HIP
-    launch (torch's composes it from log_softmax, nll_loss and the smoothing term, about eight
-    launches forward and backward)."""
+def cross_entropy(logits: Tensor, labels: Tensor, label_smoothing: float = 0.0, ignore_index: int = -100) -> Tensor:
+    """Drop-in for torch.nn.functional.cross_entropy(logits, labels, label_smoothing=...,
+    ignore_index=-100) on (B, C) fp32 logits, int64 labels, reduction "mean": the loss and its
+    gradient in one HIP launch (torch's composes it from log_softmax, nll_loss and the smoothing
+    term, about eight launches forward and backward).  Another ignore_index goes to torch's own
+    (the kernel knows -100 only).  A label outside [0, C) that is not ignored gives a NaN loss
+    (torch raises; checking on the host would synchronise every step)."""
     if logits.dim() != 2 or logits.dtype != torch.float32 or labels.dtype != torch.int64:
         raise ValueError("cross_entropy: (B, C) float32 logits and int64 labels")
+    if ignore_index != -100:
+        import torch.nn.functional as F
+        return F.cross_entropy(logits, labels, label_smoothing=label_smoothing, ignore_index=ignore_index)
     return torch.ops.mmfusion.cross_entropy_ls_fwd(logits.contiguous(), labels.contiguous(), float(label_smoothing))[0]

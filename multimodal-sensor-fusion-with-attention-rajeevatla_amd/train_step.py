@@ -159,15 +159,29 @@ class HybridTrainStep:
         self.xarr = [_nat.ptr_array([x[i * self.micro:].data_ptr() for x in self.x]) for i in range(self.accumulate)]
         self.dxarr = ([_nat.ptr_array([t[i * self.micro:].data_ptr() for t in self.dx]) for i in range(self.accumulate)]
                       if input_grads else None)
-        # one process, one micro-batch: the train step writes the clip norm's partials itself (the L = 1
-        # plan in its weight-gradient launch) and the optimizer runs the update launch only
+        # one process, one micro-batch: step() has the train step write the clip norm's partials itself
+        # (the L = 1 plan in its weight-gradient launch) and advance the step counter, and the
+        # optimizer runs the update launch only
         self.fuse_clip = bool(fuse_clip) and self.world == 1 and self.accumulate == 1
+        self._fused_pending = False   # partials written and the counter advanced by the last fwd/bwd
         self.graph: Optional[torch.cuda.CUDAGraph] = None
 
     @property
     def loss(self) -> torch.Tensor:
-        """Mean CE loss of the last step (over its micro-batches)."""
+        """Mean CE loss of the last step (over its micro-batches).  Reading it first checks the
+        one-launch step's status (check_status: a host read of the sync buffer's error word)."""
+        self.check_status()
         return self.losses.mean() if self.accumulate > 1 else self.losses
+
+    def check_status(self) -> None:
+        """Raise RuntimeError if a train step issued so far had a bounded inter-workgroup wait give
+        up (the launch-lean L = 1 step, mmf_hybrid_train_status): that step's gradients were
+        incomplete (its loss NaN, its update a zero gradient).  The error word is cleared and the
+        device already reset the sync words, so the next step runs clean."""
+        L = _nat.lib()
+        rc = L.mmf_hybrid_train_status(ctypes.byref(self.plan.desc), self.sync.data_ptr(), 1,
+                                       _nat.stream_ptr(self.dev))
+        _nat.check(rc, "train step status")
 
     # ---------------------------------------------------------------- host controls
     def set_lr(self, lr: float) -> None:
@@ -198,7 +212,13 @@ class HybridTrainStep:
     def forward_backward(self) -> None:
         """Per micro-batch: forward -> CE (loss / accumulate) -> backward in one library call
         (mmf_hybrid_train_step: three launches on the L = 1 plan), then the gradient added into
-        the accumulated one."""
+        the accumulated one.  Gradients only: the optimizer state (its step counter included) is
+        untouched until optimizer_step()."""
+        self._forward_backward(False)
+
+    def _forward_backward(self, fused: bool) -> None:
+        """fused (step() with fuse_clip): the train step also writes the clip norm's partials and
+        advances the optimizer's step counter, for the one-launch update of optimizer_step()."""
         L = _nat.lib()
         d = self.plan.desc
         st = _nat.stream_ptr(self.dev)
@@ -213,10 +233,11 @@ class HybridTrainStep:
                                          self.fw[i * b:].data_ptr(), self.losses[i:].data_ptr(),
                                          self.dlogits[i * b:].data_ptr(), ctypes.byref(g),
                                          ctypes.cast(self.dxarr[i], ctypes.c_void_p) if self.dxarr else None,
-                                         self.clip_ws.data_ptr() if self.fuse_clip else None,
-                                         self.step_dev.data_ptr() if self.fuse_clip else None,
+                                         self.clip_ws.data_ptr() if fused else None,
+                                         self.step_dev.data_ptr() if fused else None,
                                          self.grad.data_ptr(), self.grad.numel(), st)
             _nat.check(rc, "train step (forward, cross-entropy, backward)")
+            self._fused_pending = fused
             if i > 0:
                 rc = L.mmf_grad_accumulate(self.grad.numel(), self.grad_mb.data_ptr(), self.grad.data_ptr(), st)
                 _nat.check(rc, "gradient accumulation")
@@ -226,12 +247,14 @@ class HybridTrainStep:
 
     def optimizer_step(self) -> None:
         """Clip the (rank-averaged) gradient to gradient_clip_norm, then AdamW; both read
-        their scalars on the device.  With fuse_clip (one process, one micro-batch) the train step
-        already wrote the norm's partials and advanced the step counter: one launch."""
+        their scalars on the device.  After step()'s fused forward / backward (fuse_clip: one
+        process, one micro-batch) the train step already wrote the norm's partials and advanced
+        the step counter: one launch; otherwise the reduction pass and the update (two)."""
         L = _nat.lib()
         st = _nat.stream_ptr(self.dev)
         gscale = 1.0 / self.world
-        fn = L.mmf_clip_adamw_apply_dev if self.fuse_clip else L.mmf_clip_adamw_step_dev
+        fn = L.mmf_clip_adamw_apply_dev if self._fused_pending else L.mmf_clip_adamw_step_dev
+        self._fused_pending = False
         rc = fn(self.flat.numel(), self.flat.data_ptr(), self.grad.data_ptr(), self.exp_avg.data_ptr(),
                 self.exp_avg_sq.data_ptr(), self.step_dev.data_ptr(), self.lr_dev.data_ptr(), float(self.clip_norm),
                 self.grad_norm.data_ptr(), self.clip_coef.data_ptr(), self.clip_ws.data_ptr(), self.betas[0],
@@ -241,19 +264,18 @@ class HybridTrainStep:
     # ---------------------------------------------------------------- driver
     def capture(self) -> None:
         """Capture fwd+CE+bwd (and clip + AdamW when single-process) into one hipGraph."""
-        step0 = self.step_dev.clone()
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(s):
-            self.forward_backward()     # warm the path outside capture
+            self.forward_backward()     # warm the path outside capture (gradients only)
         torch.cuda.current_stream(self.dev).wait_stream(s)
         torch.cuda.synchronize(self.dev)
-        self.step_dev.copy_(step0)      # (with fuse_clip the warm-up advanced the optimizer's step count)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self.forward_backward()
+            self._forward_backward(self.fuse_clip)
             if self.world == 1:
                 self.optimizer_step()
+        self._fused_pending = False
         self.graph = g
 
     def step(self) -> None:
@@ -263,7 +285,7 @@ class HybridTrainStep:
                 self.allreduce()
                 self.optimizer_step()
             return
-        self.forward_backward()
+        self._forward_backward(self.fuse_clip)
         self.allreduce()
         self.optimizer_step()
 

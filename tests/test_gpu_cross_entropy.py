@@ -33,3 +33,36 @@ def test_cross_entropy_matches_torch(ops, B, C, eps):
     assert la.shape == lb.shape == ()
     torch.testing.assert_close(la, lb, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(a.grad, b.grad, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("eps", [0.05, 0.0])
+def test_ignore_index_rows_match_torch(ops, eps):
+    """Rows labelled -100 (torch's default ignore_index): no loss, zero gradient, the mean over the
+    remaining rows -- as torch.nn.functional.cross_entropy(label_smoothing) computes it."""
+    g = torch.Generator().manual_seed(99)
+    B, C = 50, 7
+    logits = (2 * torch.randn(B, C, generator=g)).cuda()
+    labels = torch.randint(0, C, (B,), generator=g)
+    labels[[0, 7, 8, 31]] = -100
+    labels = labels.cuda()
+    a = logits.clone().requires_grad_(True)
+    b = logits.clone().requires_grad_(True)
+    la = ops.cross_entropy(a, labels, label_smoothing=eps)
+    lb = torch.nn.functional.cross_entropy(b, labels, label_smoothing=eps)
+    la.backward()
+    lb.backward()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(la, lb, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(a.grad, b.grad, rtol=1e-5, atol=1e-7)
+    assert float(a.grad[7].abs().max()) == 0.0
+
+
+def test_out_of_range_label_gives_nan_not_a_stray_read(ops):
+    """A label outside [0, C) that is not ignored (torch raises) makes the loss NaN; the kernel never
+    indexes the logits with it."""
+    logits = torch.randn(6, 4).cuda()
+    for bad in (4, 1 << 40, -3):
+        labels = torch.tensor([0, 1, bad, 3, 2, 1]).cuda()
+        loss = ops.cross_entropy(logits, labels, label_smoothing=0.05)
+        torch.cuda.synchronize()
+        assert torch.isnan(loss).item()

@@ -10,6 +10,8 @@
 """
 from __future__ import annotations
 
+import math
+
 import pytest
 import torch
 
@@ -272,12 +274,16 @@ def test_clip_partials_from_the_train_step(mods, seq):
         assert st.fuse_clip == fuse
         out = []
         for _ in range(2):
-            st.forward_backward()
-            st.optimizer_step()
+            st.step()
             torch.cuda.synchronize()
             out.append((st.grad.cpu().clone(), float(st.grad_norm.item()), st.flat.cpu().clone(),
                         int(st.step_dev.item()), float(st.clip_coef.item())))
         runs.append(out)
+        # gradients only (no optimizer step) leaves the optimizer's step counter alone, fused or not
+        st.forward_backward()
+        st.forward_backward()
+        torch.cuda.synchronize()
+        assert int(st.step_dev.item()) == 2
     for k, ((g1, n1, p1, s1, c1), (g2, n2, p2, s2, c2)) in enumerate(zip(*runs)):
         if k == 0:
             assert torch.equal(g1, g2)   # (the second step's gradient sees weights 1e-7 apart)
@@ -382,3 +388,65 @@ def test_tile_head_module_path_matches_per_sample_head(mods, M_, H_, C_, B_, mon
         # terms sum to zero over the modalities -- carry only rounding noise)
         tol = 1e-5 * float(b.abs().max()) + 1e-8
         assert float((a - b).abs().max()) <= tol, (float((a - b).abs().max()), tol)
+
+
+def test_l1_poll_timeout_surfaces_and_recovers(mods, monkeypatch):
+    """The launch-lean L = 1 step's bounded waits: with the poll
+    bound at 0 (MMF_L1_POLL_BOUND, read per launch) every pair workgroup that waits for its tile's
+    head gives up at once.  The step must (a) not hang, (b) report it: the loss reads NaN and
+    check_status() / reading .loss raise RuntimeError, (c) leave the sync buffer clean (the
+    weight-gradient launch resets the tile words, check_status clears the error word), and (d) with
+    the default bound again, the next call on the same buffers equals a fresh step object's call bit
+    for bit (logits, loss, dlogits, weights, every gradient, dX, the dropout stream).  A fused step
+    (step(): clip partials from the train step) with the timeout reports an infinite norm and a zero
+    clip coefficient (the update applied a zero gradient)."""
+    import mmf_native as nat
+    fusion, train_step = mods
+    feats, mask, labels = _batch(19)
+    feats = [f[:, 0] for f in feats]
+
+    def build():
+        model = _model(fusion, 0.3).cuda()
+        model._rng_state.copy_(torch.tensor([0x5EED, 3], dtype=torch.int64))
+        return train_step.HybridTrainStep(model, [f.cuda() for f in feats], mask.cuda(), labels.cuda())
+
+    def outs(st):
+        return [t.detach().cpu().clone() for t in (st.logits, st.losses, st.dlogits, st.fw, st.grad, *st.dx,
+                                                    st.rng)]
+
+    st = build()
+    monkeypatch.setenv("MMF_L1_POLL_BOUND", "0")
+    nat.profile_begin()
+    st.forward_backward()
+    torch.cuda.synchronize()
+    _, launches = nat.profile_end()
+    assert any(k.startswith("l1_fwd_loss_kernel") for _, k, *_ in launches)
+    assert math.isnan(float(st.losses[0].item()))
+    words = st.sync.view(torch.int32)
+    assert int(words.count_nonzero()) == 1 and int(words[7].item()) == 1   # the error word (1 tile x 7
+    # tile words before it) alone: the weight-gradient launch reset the tile words
+    with pytest.raises(RuntimeError, match="gave up waiting"):
+        st.check_status()
+    assert int(st.sync.count_nonzero()) == 0
+    st.check_status()   # cleared
+    monkeypatch.delenv("MMF_L1_POLL_BOUND")
+    st.rng.copy_(torch.tensor([0x5EED, 3], dtype=torch.int64))
+    st.forward_backward()
+    torch.cuda.synchronize()
+    ref = build()
+    ref.forward_backward()
+    torch.cuda.synchronize()
+    for a, b in zip(outs(st), outs(ref)):
+        assert torch.equal(a, b)
+    assert math.isfinite(float(st.loss.item()))   # (.loss checks the status: nothing pending)
+    # the fused step under a timeout: norm inf, coefficient 0, reported on .loss
+    monkeypatch.setenv("MMF_L1_POLL_BOUND", "0")
+    st.step()
+    torch.cuda.synchronize()
+    assert math.isinf(float(st.grad_norm.item())) and float(st.clip_coef.item()) == 0.0
+    with pytest.raises(RuntimeError, match="gave up waiting"):
+        st.loss
+    monkeypatch.delenv("MMF_L1_POLL_BOUND")
+    st.step()
+    torch.cuda.synchronize()
+    assert math.isfinite(float(st.loss.item())) and int(st.sync.count_nonzero()) == 0
