@@ -324,6 +324,20 @@ int mmf_hybrid_train_step(const mmf_hybrid_desc* d, const mmf_hybrid_params* par
                           float* const* dx, float* clip_partial, int64_t* step_dev, const float* grad_flat,
                           int64_t grad_n, void* stream);
 
+/* mmf_hybrid_train_step in two parts, for a data-parallel caller that overlaps its gradient
+ * exchange with the rest of the backward: part 1 = the forward, the loss and the backward up to
+ * every parameter gradient except the modality projections' (projections.{m}.0.*: all written
+ * when part 1's launches complete); part 2 = dZ, dX and the projections' weight gradients (the
+ * launch-lean L = 1 plan writes every gradient in part 1, its part 2 is empty).  part 0 = both
+ * (mmf_hybrid_train_step).  Parts 1 and 2 are called in that order with the same arguments;
+ * clip_partial needs part 0. */
+int mmf_hybrid_train_step_part(int part, const mmf_hybrid_desc* d, const mmf_hybrid_params* params,
+                               const float* const* x, const float* mask, const int64_t* labels,
+                               float label_smoothing, float loss_scale, uint64_t* rng_state, void* saved,
+                               void* workspace, void* sync, float* logits, float* fusion_weights, float* loss_out,
+                               float* dlogits, const mmf_hybrid_grads* grads, float* const* dx, float* clip_partial,
+                               int64_t* step_dev, const float* grad_flat, int64_t grad_n, void* stream);
+
 /* AdamW with the learning rate and an extra gradient factor read from device
  * scalars (lr_dev[0]; grad_coef_dev[0], may be NULL = 1), so a captured hipGraph
  * step follows an LR scheduler (CosineAnnealingLR, src/train.py:394-402) and

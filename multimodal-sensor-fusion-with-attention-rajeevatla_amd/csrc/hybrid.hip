@@ -272,9 +272,13 @@ int check_hybrid(const mmf_hybrid_desc* d) {
 
 // Every weight gradient as a split-K job; the same code sizes the workspace
 // (called with null bases) and plans the real launch.
+// part (mmf_hybrid_train_step_part): 0 every weight, 1 every weight but the modality projections'
+// (known once the attention backward has run), 2 the projections' alone (after dZ); the split
+// counts are sized for the launch the part makes.
 void plan_wgrads(const mmf_hybrid_desc* d, const float* const* x, const float* mask,
                  const float* dlogits, const Saved& s, const Ws& w, const mmf_hybrid_grads* G,
-                 Bump& bw, WgradPlan& wp) {
+                 Bump& bw, WgradPlan& wp, int part = 0) {
+  const bool want_pairs = part != 2, want_proj = part != 1;
   const int B = d->batch, M = d->num_modalities, H = d->hidden, C = d->num_classes;
   const int nh = d->num_heads, hd = H / nh;
   const bool pool = use_pool(d);
@@ -287,12 +291,12 @@ void plan_wgrads(const mmf_hybrid_desc* d, const float* const* x, const float* m
   // one launch: 768 / 15 = 51 slabs requested, 49 of 672 rows after rounding to 32).
   const int kBigRows = 4096;
   int nbig = 0;
-  for (int p = 0; p < d->num_pairs; ++p) {
+  for (int p = 0; p < d->num_pairs && want_pairs; ++p) {
     const int lq = Lm(d, d->pair_q[p]), lk = Lm(d, d->pair_k[p]);
     if (!pool) nbig += (B * lq >= kBigRows) + (B * lk >= kBigRows);
     if (!single_key(d, p)) nbig += (B * lq >= kBigRows) + (B * lk >= kBigRows);
   }
-  for (int m = 0; m < M; ++m) nbig += (B * Lm(d, m) >= kBigRows);
+  for (int m = 0; m < M && want_proj; ++m) nbig += (B * Lm(d, m) >= kBigRows);
   const int slots = 3 * device_cu_count();
   const int rem = nbig % GEMM_MAX_GROUPS, nfull = nbig - rem;
   int bi = 0;
@@ -303,13 +307,15 @@ void plan_wgrads(const mmf_hybrid_desc* d, const float* const* x, const float* m
     if (const char* e = getenv("MMF_WGRAD_SPLIT_CAP")) sp = std::min(sp, std::max(1, atoi(e)));
     return std::max(1, std::min(sp, 256));
   };
-  plan_wgrad(wp, bw, C, H, B, opnd(dlogits, C), opnd(s.h1, H), g->cls2.w, g->cls2.b);
-  plan_wgrad(wp, bw, H, H, B, opnd(w.dz1, H), opnd(s.fused, H), g->cls1.w, g->cls1.b);
-  // gating_layers[m]: dscore[:, m]^T pooled[:, m, :]
-  for (int m = 0; m < M; ++m)
-    plan_wgrad(wp, bw, 1, H, B, opnd(w.dscore ? w.dscore + m : nullptr, M),
-               opnd(s.pooled ? s.pooled + (size_t)m * H : nullptr, M * H), g->gate[m].w, g->gate[m].b);
-  for (int p = 0; p < d->num_pairs; ++p) {
+  if (want_pairs) {
+    plan_wgrad(wp, bw, C, H, B, opnd(dlogits, C), opnd(s.h1, H), g->cls2.w, g->cls2.b);
+    plan_wgrad(wp, bw, H, H, B, opnd(w.dz1, H), opnd(s.fused, H), g->cls1.w, g->cls1.b);
+    // gating_layers[m]: dscore[:, m]^T pooled[:, m, :]
+    for (int m = 0; m < M; ++m)
+      plan_wgrad(wp, bw, 1, H, B, opnd(w.dscore ? w.dscore + m : nullptr, M),
+                 opnd(s.pooled ? s.pooled + (size_t)m * H : nullptr, M * H), g->gate[m].w, g->gate[m].b);
+  }
+  for (int p = 0; p < d->num_pairs && want_pairs; ++p) {
     const int q = d->pair_q[p], k = d->pair_k[p];
     const int lq = Lm(d, q), lk = Lm(d, k);
     const float* cq = w.cvec ? w.cvec + (size_t)q * H : nullptr;
@@ -341,7 +347,7 @@ void plan_wgrads(const mmf_hybrid_desc* d, const float* const* x, const float* m
     plan_wgrad(wp, bw, H, H, B * lk, opnd(w.dK[p], H), opnd(s.P[k], H), g->k[p].w, g->k[p].b);
     wp.split_hint = 0;
   }
-  for (int m = 0; m < M; ++m) {
+  for (int m = 0; m < M && want_proj; ++m) {
     const int L = Lm(d, m), D = d->in_dim[m];
     wp.split_hint = hint(B * L);
     plan_wgrad(wp, bw, H, D, B * L, opnd(w.dZ[m], H), opnd(s.Xd[m], D), g->proj[m].w, g->proj[m].b);
@@ -365,9 +371,16 @@ size_t workspace_bytes(const mmf_hybrid_desc* d) {
   Bump bw(nullptr);
   Ws w;
   layout_ws(d, bw, w);
-  WgradPlan wp;
-  plan_wgrads(d, nullptr, nullptr, nullptr, s, w, nullptr, bw, wp);
-  return bw.off + 256;
+  // the largest slab area of a one-launch backward and of its two parts (their slabs share the
+  // area: part 1's reduce has run before part 2's slabs are written)
+  size_t top = 0;
+  for (int part = 0; part < 3; ++part) {
+    Bump b = bw;
+    WgradPlan wp;
+    plan_wgrads(d, nullptr, nullptr, nullptr, s, w, nullptr, b, wp, part);
+    top = std::max(top, b.off);
+  }
+  return top + 256;
 }
 
 void fill_head(HeadArgs& ha, const mmf_hybrid_desc* d, const mmf_hybrid_params* W, const float* mask,
@@ -953,9 +966,13 @@ int mmf_hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, con
 }
 
 // head_done: the training step's head launch ran the head backward (TailTrain)
+// part: 0 the whole backward; 1 everything up to the attention backward and every weight gradient
+// but the modality projections'; 2 dZ, dX and the projections' weight gradients (the L = 1 plan
+// runs all of it in part 1)
 static int hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, const float* const* x,
                            const float* mask, const void* saved, const float* dlogits, void* workspace,
-                           const mmf_hybrid_grads* G, float* const* dx, void* stream, bool head_done) {
+                           const mmf_hybrid_grads* G, float* const* dx, void* stream, bool head_done,
+                           int part = 0) {
   int rc = check_hybrid(d);
   if (rc) return rc;
   MathScope math_(d->matmul_precision);
@@ -977,6 +994,7 @@ static int hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W,
   Ws w;
   layout_ws(d, bw, w);
   if (lean_l1(d, W, x)) {
+    if (part == 2) return MMF_OK;
     L1Args a;
     L1WgArgs wa;
     fill_l1_bwd(a, wa, d, W, x, mask, s, w, dlogits, G, dx);
@@ -984,10 +1002,11 @@ static int hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W,
     return MMF_OK;
   }
   WgradPlan wp;
-  plan_wgrads(d, x, mask, dlogits, s, w, G, bw, wp);
+  plan_wgrads(d, x, mask, dlogits, s, w, G, bw, wp, part);
   if (bw.off > workspace_bytes(d)) return fail(MMF_EINVAL, "internal: workspace overflow");
 
   const bool tail = d->num_pairs && use_tail(d);
+  if (part != 2) {
   if (tail) {
     // (1-3p) fused per-sample tail backward: classifier, head, dObar, dU
     TailArgs ta;
@@ -1134,6 +1153,18 @@ static int hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W,
     if (nsk) STAGE_TRY("bwd.attn_single_key_dv", launch_sk_dv(skp.data(), nsk, B, nh, hd, p, rng, st));
     if (nwp) STAGE_TRY("bwd.attn_wide", launch_wide_bwd(wpairs.data(), nwp, B, nh, hd, scale, p, rng, false, st));
   }
+  }   // part != 2
+  if (part == 1) {
+    // every weight gradient but the projections': final once these launches complete
+    std::stable_sort(wp.jobs.begin(), wp.jobs.end(), [](const GemmJob& a, const GemmJob& b) {
+      const int64_t wa = (int64_t)a.g.nsplit * std::max(1, a.g.nbatch) * a.g.M * a.g.N;
+      const int64_t wb = (int64_t)b.g.nsplit * std::max(1, b.g.nbatch) * b.g.M * b.g.N;
+      return wa > wb;
+    });
+    STAGE_TRY("bwd.wgrad_gemm", launch_gemm(wp.jobs.data(), (int)wp.jobs.size(), MODE_KR, MODE_KR, p, rng, st));
+    STAGE_TRY("bwd.wgrad_reduce", launch_reduce(wp.reds.data(), (int)wp.reds.size(), st));
+    return MMF_OK;
+  }
   // (4) dZ_m = gate(P_m) * [direct + sum_q dQ W_q + sum_k dK W_k (+ dV W_v)]
   {
     std::vector<GemmJob> jobs;
@@ -1242,20 +1273,23 @@ int mmf_hybrid_train_status(const mmf_hybrid_desc* d, void* sync, int clear, voi
                             "is NaN, its update applied a zero gradient); the sync words were reset");
 }
 
-int mmf_hybrid_train_step(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, const float* const* x,
-                          const float* mask, const int64_t* labels, float label_smoothing, float loss_scale,
-                          uint64_t* rng_state, void* saved, void* workspace, void* sync, float* logits,
-                          float* fusion_weights, float* loss_out, float* dlogits, const mmf_hybrid_grads* G,
-                          float* const* dx, float* clip_partial, int64_t* step_dev, const float* grad_flat,
-                          int64_t grad_n, void* stream) {
+int mmf_hybrid_train_step_part(int part, const mmf_hybrid_desc* d, const mmf_hybrid_params* W,
+                               const float* const* x, const float* mask, const int64_t* labels,
+                               float label_smoothing, float loss_scale, uint64_t* rng_state, void* saved,
+                               void* workspace, void* sync, float* logits, float* fusion_weights, float* loss_out,
+                               float* dlogits, const mmf_hybrid_grads* G, float* const* dx, float* clip_partial,
+                               int64_t* step_dev, const float* grad_flat, int64_t grad_n, void* stream) {
   int rc = check_hybrid(d);
   if (rc) return rc;
+  if (part < 0 || part > 2) return fail(MMF_EINVAL, "train step: part must be 0, 1 or 2 (got %d)", part);
   if (!W || !x || !mask || !labels || !saved || !workspace || !logits || !loss_out || !dlogits || !G)
     return fail(MMF_EINVAL, "null argument");
   if (clip_partial && !step_dev) return fail(MMF_EINVAL, "train step: clip partials need the step counter");
+  if (clip_partial && part != 0) return fail(MMF_EINVAL, "train step: clip partials need the whole step (part 0)");
   // (the one-launch kernel needs its tiles x pairs workgroups resident at once, one per CU)
   if (sync && lean_l1(d, W, x) &&
       (int64_t)((d->batch + 15) / 16) * d->num_pairs <= l1_train_capacity(l1_desc_full(d))) {
+    if (part == 2) return MMF_OK;   // (every gradient came out of part 1's launches)
     MathScope math_(d->matmul_precision);
     hipStream_t st = (hipStream_t)stream;
     Bump bs(saved);
@@ -1285,6 +1319,11 @@ int mmf_hybrid_train_step(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, 
     STAGE_TRY("train.l1", launch_l1_train(a, wa, st));
     return MMF_OK;
   }
+  if (part == 2) {
+    // the head-done flag of part 1's forward: the same decision, from the same descriptor and
+    // pointers (only the backward's tail launch depends on it, and part 2 runs none)
+    return hybrid_backward(d, W, x, mask, saved, dlogits, workspace, G, dx, stream, false, 2);
+  }
   // (with the sync words: the pooled tail plan runs the loss and the head backward in its head launch)
   TailTrain tt{labels, label_smoothing, loss_scale, loss_out, dlogits, static_cast<uint32_t*>(sync), workspace, false};
   rc = hybrid_forward(d, W, x, mask, rng_state, saved, logits, fusion_weights, nullptr, stream, sync ? &tt : nullptr);
@@ -1294,13 +1333,24 @@ int mmf_hybrid_train_step(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, 
                               dlogits, stream);
     if (rc) return rc;
   }
-  rc = hybrid_backward(d, W, x, mask, saved, dlogits, workspace, G, dx, stream, tt.done);
+  rc = hybrid_backward(d, W, x, mask, saved, dlogits, workspace, G, dx, stream, tt.done, part);
   if (rc || !clip_partial) return rc;
   if (!grad_flat || grad_n < 0 || (reinterpret_cast<uintptr_t>(grad_flat) & 15))
     return fail(MMF_EINVAL, "train step: clip partials need the 16-byte aligned flat gradient");
   hipStream_t st = (hipStream_t)stream;
   STAGE_TRY("optim.clip_norm", launch_grad_sumsq(grad_n, grad_flat, clip_partial, step_dev, st));
   return MMF_OK;
+}
+
+int mmf_hybrid_train_step(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, const float* const* x,
+                          const float* mask, const int64_t* labels, float label_smoothing, float loss_scale,
+                          uint64_t* rng_state, void* saved, void* workspace, void* sync, float* logits,
+                          float* fusion_weights, float* loss_out, float* dlogits, const mmf_hybrid_grads* G,
+                          float* const* dx, float* clip_partial, int64_t* step_dev, const float* grad_flat,
+                          int64_t grad_n, void* stream) {
+  return mmf_hybrid_train_step_part(0, d, W, x, mask, labels, label_smoothing, loss_scale, rng_state, saved,
+                                    workspace, sync, logits, fusion_weights, loss_out, dlogits, G, dx, clip_partial,
+                                    step_dev, grad_flat, grad_n, stream);
 }
 
 }  // extern "C"

@@ -45,6 +45,7 @@ LIB_PATH = os.environ.get("MMF_LIB_PATH") or os.path.join(_HERE, "csrc", "libmmf
 EXPORTED_SYMBOLS = (
     "mmf_hybrid_saved_bytes", "mmf_hybrid_workspace_bytes", "mmf_hybrid_forward",
     "mmf_hybrid_backward", "mmf_hybrid_train_sync_bytes", "mmf_hybrid_train_status", "mmf_hybrid_train_step",
+    "mmf_hybrid_train_step_part",
     "mmf_adaptive_weights_workspace_bytes", "mmf_adaptive_weights",
     "mmf_adaptive_weights_backward",
     "mmf_cma_saved_bytes", "mmf_cma_workspace_bytes", "mmf_cma_forward", "mmf_cma_backward",
@@ -135,6 +136,8 @@ def lib() -> ctypes.CDLL:
                                         vp, vp, vp, vp, vp, vp, vp, vp, POINTER(HybridGrads), vp, vp, vp, vp,
                                         c_int64, vp]
     L.mmf_hybrid_train_step.restype = c_int32
+    L.mmf_hybrid_train_step_part.argtypes = [c_int32] + L.mmf_hybrid_train_step.argtypes
+    L.mmf_hybrid_train_step_part.restype = c_int32
     L.mmf_adaptive_weights_workspace_bytes.argtypes = [c_int32, c_int32, c_int32]
     L.mmf_adaptive_weights_workspace_bytes.restype = sz
     L.mmf_adaptive_weights.argtypes = [c_int32, c_int32, c_int32, vp, vp, vp, vp, vp, vp]

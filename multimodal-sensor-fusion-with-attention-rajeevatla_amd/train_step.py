@@ -165,6 +165,15 @@ class HybridTrainStep:
         self.fuse_clip = bool(fuse_clip) and self.world == 1 and self.accumulate == 1
         self._fused_pending = False   # partials written and the counter advanced by the last fwd/bwd
         self.graph: Optional[torch.cuda.CUDAGraph] = None
+        # several ranks: the exchange in two buckets overlapped with the backward.  The plan's
+        # parameter order puts the modality projections first, so the flat gradient is
+        # [projections | pairs, gates, classifier]; every gradient of the second span is final
+        # after part 1 of the train step (the attention backward), the projections' after part 2
+        # (dZ, dX, their weight gradients).  Part 1's bucket is all-reduced while part 2 runs.
+        self.overlap = self.world > 1
+        split = self.plan.offsets[2 * d.num_modalities] if len(self.plan.offsets) > 2 * d.num_modalities else n
+        self.bucket_spans = ((split, n), (0, split))    # (issued after part 1, after part 2)
+        self.graph2: Optional[torch.cuda.CUDAGraph] = None
 
     @property
     def loss(self) -> torch.Tensor:
@@ -216,16 +225,23 @@ class HybridTrainStep:
         untouched until optimizer_step()."""
         self._forward_backward(False)
 
-    def _forward_backward(self, fused: bool) -> None:
+    def _forward_backward(self, fused: bool, part: int = 0) -> None:
         """fused (step() with fuse_clip): the train step also writes the clip norm's partials and
-        advances the optimizer's step counter, for the one-launch update of optimizer_step()."""
+        advances the optimizer's step counter, for the one-launch update of optimizer_step().
+        part (the overlapped exchange): 1 = every micro-batch but the last whole, the last one's
+        mmf_hybrid_train_step_part 1 (every gradient but the projections'); 2 = the last
+        micro-batch's part 2; 0 = everything."""
         L = _nat.lib()
         d = self.plan.desc
         st = _nat.stream_ptr(self.dev)
         C, M, b = d.num_classes, d.num_modalities, self.micro
+        last = self.accumulate - 1
         for i in range(self.accumulate):
+            if part == 2 and i < last:
+                continue
+            pi = part if i == last else 0
             g = self.gstruct if i == 0 else self.gstruct_mb
-            rc = L.mmf_hybrid_train_step(ctypes.byref(d), ctypes.byref(self.pstruct),
+            rc = L.mmf_hybrid_train_step_part(pi, ctypes.byref(d), ctypes.byref(self.pstruct),
                                          ctypes.cast(self.xarr[i], ctypes.c_void_p), self.mask[i * b:].data_ptr(),
                                          self.labels[i * b:].data_ptr(), self.smoothing, 1.0 / self.accumulate,
                                          self.rng.data_ptr(), self.saved.data_ptr(), self.ws.data_ptr(),
@@ -239,8 +255,12 @@ class HybridTrainStep:
             _nat.check(rc, "train step (forward, cross-entropy, backward)")
             self._fused_pending = fused
             if i > 0:
-                rc = L.mmf_grad_accumulate(self.grad.numel(), self.grad_mb.data_ptr(), self.grad.data_ptr(), st)
-                _nat.check(rc, "gradient accumulation")
+                # the micro-batch's gradient added into the accumulated one: all of it, or the
+                # span this part finished
+                lo, hi = (0, self.grad.numel()) if pi == 0 else self.bucket_spans[pi - 1]
+                if hi > lo:
+                    rc = L.mmf_grad_accumulate(hi - lo, self.grad_mb[lo:].data_ptr(), self.grad[lo:].data_ptr(), st)
+                    _nat.check(rc, "gradient accumulation")
 
     def allreduce(self) -> None:
         allreduce_flat(self.grad, self.pg, self.world)
@@ -263,7 +283,9 @@ class HybridTrainStep:
 
     # ---------------------------------------------------------------- driver
     def capture(self) -> None:
-        """Capture fwd+CE+bwd (and clip + AdamW when single-process) into one hipGraph."""
+        """Capture fwd+CE+bwd (and clip + AdamW when single-process) into one hipGraph; with
+        several ranks, the train step's two parts into two graphs (the exchange of the first
+        bucket runs between their replays, outside the graphs)."""
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(s):
@@ -271,19 +293,40 @@ class HybridTrainStep:
         torch.cuda.current_stream(self.dev).wait_stream(s)
         torch.cuda.synchronize(self.dev)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._forward_backward(self.fuse_clip)
-            if self.world == 1:
-                self.optimizer_step()
+        if self.overlap:
+            with torch.cuda.graph(g):
+                self._forward_backward(False, 1)
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g2):
+                self._forward_backward(False, 2)
+            self.graph2 = g2
+        else:
+            with torch.cuda.graph(g):
+                self._forward_backward(self.fuse_clip)
+                if self.world == 1:
+                    self.optimizer_step()
         self._fused_pending = False
         self.graph = g
 
+    def _bucket(self, k: int) -> torch.Tensor:
+        lo, hi = self.bucket_spans[k]
+        return self.grad[lo:hi]
+
     def step(self) -> None:
+        if self.overlap:
+            # part 1 -> exchange of its bucket (RCCL on its own stream, after part 1) while part 2
+            # runs -> exchange of the projections' bucket -> wait both -> clip + AdamW
+            self.graph.replay() if self.graph is not None else self._forward_backward(False, 1)
+            works = [torch.distributed.all_reduce(self._bucket(0), group=self.pg, async_op=True)]
+            self.graph2.replay() if self.graph2 is not None else self._forward_backward(False, 2)
+            if self.bucket_spans[1][1] > self.bucket_spans[1][0]:
+                works.append(torch.distributed.all_reduce(self._bucket(1), group=self.pg, async_op=True))
+            for w in works:
+                w.wait()
+            self.optimizer_step()
+            return
         if self.graph is not None:
             self.graph.replay()
-            if self.world > 1:
-                self.allreduce()
-                self.optimizer_step()
             return
         self._forward_backward(self.fuse_clip)
         self.allreduce()

@@ -5,7 +5,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/${1:-r05a}
 mkdir -p $O
-timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_train_step.py tests/test_gpu_cross_entropy.py > $O/pytest_sel.log 2>&1
+timeout -k 10 500 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_gpu_train_step.py tests/test_gpu_cross_entropy.py tests/test_dp.py tests/test_gpu_c5_bench.py tests/test_gpu_headline.py > $O/pytest_sel.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> $O/pytest_sel.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest crashed rc=$rc"; exit $rc; fi
 TORCH_LOGS=perf_hints timeout -k 10 400 python -u scripts/host_phase_profile.py --out $O/host_l1.json > $O/host_l1.log 2>&1 || exit $?
