@@ -337,19 +337,30 @@ class HybridFusion(nn.Module):
                 raise KeyError(f"Missing features for modality '{name}' in HybridFusion forward pass.")
             feats.append(modality_features[name].to(device))
         _nat.require_device(ref, "HybridFusion input")
-        for p in self.parameters():
-            if p.device != device or p.dtype != torch.float32:
-                raise RuntimeError("mmfusion HybridFusion needs float32 parameters on the input's device "
-                                   f"(found {p.dtype} on {p.device})")
         seq, dims = self._shapes(feats)
-        pairs = self.present_pairs()
-        named = dict(self.named_parameters())
-        params = [named[n] for n in self._param_names(pairs)]
+        # traced (torch.compile, fake tensors): the custom operator; eager: HybridEager
+        compiling = not _ops.eager_tensor(ref)
+        if compiling:
+            for p in self.parameters():
+                if p.device != device or p.dtype != torch.float32:
+                    raise RuntimeError("mmfusion HybridFusion needs float32 parameters on the input's device "
+                                       f"(found {p.dtype} on {p.device})")
+            pairs = self.present_pairs()
+            named = dict(self.named_parameters())
+            params = [named[n] for n in self._param_names(pairs)]
+        else:
+            pairs, params = self._op_params(device)
         idesc = _ops.hybrid_idesc(batch_size, self.hidden_dim, self.num_heads, self.num_classes, seq, dims,
                                   [(q, k) for q, k, _ in pairs], self.training, return_attention, _precision())
-        logits, fw, _saved, rng_next, maps = torch.ops.mmfusion.hybrid_fwd(
-            idesc, float(self.dropout.p), self._rng_state, _nat.f32c(modality_mask),
-            [_nat.f32c(x) for x in feats], params)
+        xs = [_nat.f32c(x) for x in feats]
+        if compiling:
+            # (traced by TorchDynamo: the custom operator, its fake kernel and autograd formula)
+            logits, fw, _saved, rng_next, maps = torch.ops.mmfusion.hybrid_fwd(
+                idesc, float(self.dropout.p), self._rng_state, _nat.f32c(modality_mask), xs, params)
+        else:
+            # eager: the same implementation through autograd.Function (mmf_ops.HybridEager)
+            logits, fw, _saved, rng_next, *maps = _ops.HybridEager.apply(
+                idesc, float(self.dropout.p), self._rng_state, _nat.f32c(modality_mask), len(xs), *xs, *params)
         self._rng_state.copy_(rng_next)     # the device Philox stream advanced by one call
         if dtype != torch.float32 and dtype.is_floating_point:
             logits = logits.to(dtype)
@@ -357,6 +368,32 @@ class HybridFusion(nn.Module):
             attention_maps = {key: maps[g].detach() for g, (_, _, key) in enumerate(pairs)}
             return logits, {"attention_maps": attention_maps, "fusion_weights": fw.detach()}
         return logits
+
+    def _op_params(self, device) -> Tuple[List[Tuple[int, int, str]], List[torch.Tensor]]:
+        """(present pairs, the operator's parameter list), cached per set of attention modules (a
+        deleted pair changes it) and dropped by every .to() / .cuda() / .float() (_apply), so the
+        float32-on-one-device check runs once per cache: an eager step then costs no walk over
+        the module tree."""
+        keys = tuple(self.attention_modules.keys())
+        c = self.__dict__.get("_mmf_op_params")
+        if c is None or c[0] != keys:
+            pairs = self.present_pairs()
+            named = dict(self.named_parameters())
+            params = [named[n] for n in self._param_names(pairs)]
+            for p in params:
+                if p.device != params[0].device or p.dtype != torch.float32:
+                    raise RuntimeError("mmfusion HybridFusion needs float32 parameters on one device "
+                                       f"(found {p.dtype} on {p.device})")
+            c = (keys, pairs, params)
+            self.__dict__["_mmf_op_params"] = c
+        if c[2][0].device != device:
+            raise RuntimeError("mmfusion HybridFusion needs float32 parameters on the input's device "
+                               f"(found {c[2][0].dtype} on {c[2][0].device})")
+        return c[1], c[2]
+
+    def _apply(self, fn, *args, **kwargs):
+        self.__dict__.pop("_mmf_op_params", None)
+        return super()._apply(fn, *args, **kwargs)
 
     def compute_adaptive_weights(self, modality_features: Dict[str, torch.Tensor],
                                  modality_mask: torch.Tensor) -> torch.Tensor:

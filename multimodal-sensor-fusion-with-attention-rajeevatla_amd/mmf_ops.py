@@ -45,11 +45,19 @@ import mmf_native as _nat  # noqa: E402
 ALIGN = 64   # every tensor of a flat gradient buffer starts on a 256-byte boundary
 
 
+_OFFS: Dict[tuple, Tuple[List[int], int]] = {}
+
+
 def flat_offsets(numels: Sequence[int]) -> Tuple[List[int], int]:
+    key = tuple(int(n) for n in numels)
+    hit = _OFFS.get(key)
+    if hit is not None:
+        return hit
     offs, off = [], 0
-    for n in numels:
+    for n in key:
         offs.append(off)
-        off += -(-int(n) // ALIGN) * ALIGN
+        off += -(-n // ALIGN) * ALIGN
+    _OFFS[key] = (offs, off)
     return offs, off
 
 
@@ -100,10 +108,22 @@ def _hybrid_meta(idesc: Sequence[int]):
     return B, M, C, maps
 
 
+_PSTRUCT: Dict[tuple, "_nat.HybridParams"] = {}
+_SIZES: Dict[tuple, Tuple[int, int]] = {}
+
+
 def _hybrid_params_struct(params: Sequence[Tensor], M: int, P: int) -> "_nat.HybridParams":
+    """The C-ABI parameter (or gradient) struct for these tensors' addresses, cached per address
+    set (a training loop passes the same parameters every step; gradient buffers recur through
+    the caching allocator)."""
+    ptrs = tuple(t.data_ptr() for t in params)
+    key = (M, P, ptrs)
+    s = _PSTRUCT.get(key)
+    if s is not None:
+        return s
     s = _nat.HybridParams()
-    it = iter(params)
-    nxt = lambda: next(it).data_ptr()  # noqa: E731
+    it = iter(ptrs)
+    nxt = lambda: next(it)  # noqa: E731
     for m in range(M):
         s.proj[m] = _nat.Linear(nxt(), nxt())
     for g in range(P):
@@ -115,18 +135,32 @@ def _hybrid_params_struct(params: Sequence[Tensor], M: int, P: int) -> "_nat.Hyb
         s.gate[m] = _nat.Linear(nxt(), nxt())
     s.cls1 = _nat.Linear(nxt(), nxt())
     s.cls2 = _nat.Linear(nxt(), nxt())
+    if len(_PSTRUCT) > 256:
+        _PSTRUCT.clear()
+    _PSTRUCT[key] = s
     return s
 
 
-@torch.library.custom_op("mmfusion::hybrid_fwd", mutates_args=(), device_types="cuda")
-def hybrid_fwd(idesc: List[int], dropout: float, rng_state: Tensor, mask: Tensor, xs: List[Tensor],
-               params: List[Tensor]) -> Tuple[Tensor, Tensor, Tensor, Tensor, List[Tensor]]:
-    """-> logits (B, C), fusion_weights (B, M), saved (bytes), advanced rng state, attention maps."""
+def _hybrid_sizes(d: "_nat.HybridDesc", key: tuple) -> Tuple[int, int]:
+    """(saved, workspace) bytes of a descriptor (host arithmetic in the library), cached."""
+    hit = _SIZES.get(key)
+    if hit is None:
+        L = _nat.lib()
+        hit = (L.mmf_hybrid_saved_bytes(ctypes.byref(d)), L.mmf_hybrid_workspace_bytes(ctypes.byref(d)))
+        _SIZES[key] = hit
+    return hit
+
+
+def hybrid_fwd_impl(idesc: Sequence[int], dropout: float, rng_state: Tensor, mask: Tensor, xs: Sequence[Tensor],
+                    params: Sequence[Tensor]):
+    """mmf_hybrid_forward on the caller's stream -> logits (B, C), fusion_weights (B, M), saved
+    (bytes), advanced rng state, attention maps.  (The hybrid_fwd operator's body, and the eager
+    autograd function's: one implementation.)"""
     L = _nat.lib()
     d = hybrid_desc(idesc, dropout)
     B, M, C, mshapes = _hybrid_meta(idesc)
     dev = mask.device
-    saved = torch.empty(L.mmf_hybrid_saved_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
+    saved = torch.empty(_hybrid_sizes(d, (tuple(idesc), float(dropout)))[0], dtype=torch.uint8, device=dev)
     logits = torch.empty(B, C, dtype=torch.float32, device=dev)
     fw = torch.empty(B, M, dtype=torch.float32, device=dev)
     maps = [torch.empty(s, dtype=torch.float32, device=dev) for s in mshapes]
@@ -140,6 +174,36 @@ def hybrid_fwd(idesc: List[int], dropout: float, rng_state: Tensor, mask: Tensor
                               _nat.stream_ptr(dev))
     _nat.check(rc, "HybridFusion forward")
     return logits, fw, saved, rng_next, maps
+
+
+def hybrid_bwd_impl(idesc: Sequence[int], dropout: float, mask: Tensor, xs: Sequence[Tensor],
+                    params: Sequence[Tensor], saved: Tensor, dlogits: Tensor, need_dx: Sequence[bool],
+                    offsets: Sequence[int], nelem: int):
+    """mmf_hybrid_backward -> dx per modality (an empty tensor where not needed), the flat
+    parameter gradient (every gradient WRITTEN by the library, so no zero fill)."""
+    L = _nat.lib()
+    d = hybrid_desc(idesc, dropout)
+    M, P = d.num_modalities, d.num_pairs
+    dev = mask.device
+    ws = torch.empty(_hybrid_sizes(d, (tuple(idesc), float(dropout)))[1], dtype=torch.uint8, device=dev)
+    flat = torch.empty(nelem, dtype=torch.float32, device=dev)
+    gstruct = _hybrid_params_struct(_views(flat, params, offsets), M, P)
+    pstruct = _hybrid_params_struct(params, M, P)
+    dxs = [torch.empty_like(x) if need else x.new_empty(0) for x, need in zip(xs, need_dx)]
+    xarr = _nat.ptr_array([x.data_ptr() for x in xs])
+    dxarr = _nat.ptr_array([t.data_ptr() if need else None for t, need in zip(dxs, need_dx)])
+    rc = L.mmf_hybrid_backward(ctypes.byref(d), ctypes.byref(pstruct), ctypes.cast(xarr, ctypes.c_void_p),
+                               mask.data_ptr(), saved.data_ptr(), dlogits.data_ptr(), ws.data_ptr(),
+                               ctypes.byref(gstruct), ctypes.cast(dxarr, ctypes.c_void_p), _nat.stream_ptr(dev))
+    _nat.check(rc, "HybridFusion backward")
+    return dxs, flat
+
+
+@torch.library.custom_op("mmfusion::hybrid_fwd", mutates_args=(), device_types="cuda")
+def hybrid_fwd(idesc: List[int], dropout: float, rng_state: Tensor, mask: Tensor, xs: List[Tensor],
+               params: List[Tensor]) -> Tuple[Tensor, Tensor, Tensor, Tensor, List[Tensor]]:
+    """-> logits (B, C), fusion_weights (B, M), saved (bytes), advanced rng state, attention maps."""
+    return hybrid_fwd_impl(idesc, dropout, rng_state, mask, xs, params)
 
 
 @hybrid_fwd.register_fake
@@ -156,22 +220,7 @@ def hybrid_bwd(idesc: List[int], dropout: float, mask: Tensor, xs: List[Tensor],
                saved: Tensor, dlogits: Tensor, need_dx: List[bool], offsets: List[int],
                nelem: int) -> Tuple[List[Tensor], Tensor]:
     """-> dx per modality (an empty tensor where not needed), flat parameter gradient."""
-    L = _nat.lib()
-    d = hybrid_desc(idesc, dropout)
-    M, P = d.num_modalities, d.num_pairs
-    dev = mask.device
-    ws = torch.empty(L.mmf_hybrid_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
-    flat = torch.zeros(nelem, dtype=torch.float32, device=dev)
-    gstruct = _hybrid_params_struct(_views(flat, params, offsets), M, P)
-    pstruct = _hybrid_params_struct(params, M, P)
-    dxs = [torch.empty_like(x) if need else x.new_empty(0) for x, need in zip(xs, need_dx)]
-    xarr = _nat.ptr_array([x.data_ptr() for x in xs])
-    dxarr = _nat.ptr_array([t.data_ptr() if need else None for t, need in zip(dxs, need_dx)])
-    rc = L.mmf_hybrid_backward(ctypes.byref(d), ctypes.byref(pstruct), ctypes.cast(xarr, ctypes.c_void_p),
-                               mask.data_ptr(), saved.data_ptr(), dlogits.data_ptr(), ws.data_ptr(),
-                               ctypes.byref(gstruct), ctypes.cast(dxarr, ctypes.c_void_p), _nat.stream_ptr(dev))
-    _nat.check(rc, "HybridFusion backward")
-    return dxs, flat
+    return hybrid_bwd_impl(idesc, dropout, mask, xs, params, saved, dlogits, need_dx, offsets, nelem)
 
 
 @hybrid_bwd.register_fake
@@ -203,6 +252,37 @@ def _hybrid_backward(ctx, dlogits, _dfw, _dsaved, _drng, _dmaps):
 
 
 hybrid_fwd.register_autograd(_hybrid_backward, setup_context=_hybrid_setup)
+
+
+class HybridEager(torch.autograd.Function):
+    """The eager-mode twin of the hybrid_fwd / hybrid_bwd operators (HybridFusion.forward outside
+    torch.compile): the same implementation functions and the same saved tensors and gradient
+    formula, through autograd.Function.apply instead of the custom-op dispatch (the operator's
+    Python dispatch, schema checks and argument flattening cost host time every call).  Inputs:
+    (idesc, dropout, rng_state, mask, nx, *xs, *params)."""
+
+    @staticmethod
+    def forward(ctx, idesc, dropout, rng_state, mask, nx, *tensors):
+        xs, params = tensors[:nx], tensors[nx:]
+        logits, fw, saved, rng_next, maps = hybrid_fwd_impl(idesc, dropout, rng_state, mask, xs, params)
+        ctx.set_materialize_grads(False)
+        ctx.idesc, ctx.dropout, ctx.nx = idesc, dropout, nx
+        ctx.need_dx = [bool(n) for n in ctx.needs_input_grad[5:5 + nx]]
+        ctx.save_for_backward(mask, saved, *xs, *params)
+        ctx.mark_non_differentiable(fw, saved, rng_next, *maps)
+        return (logits, fw, saved, rng_next, *maps)
+
+    @staticmethod
+    def backward(ctx, dlogits, *_unused):
+        if dlogits is None:
+            return (None,) * len(ctx.needs_input_grad)
+        mask, saved, *rest = ctx.saved_tensors
+        xs, params = rest[:ctx.nx], rest[ctx.nx:]
+        offsets, nelem = flat_offsets([p.numel() for p in params])
+        dxs, flat = hybrid_bwd_impl(ctx.idesc, ctx.dropout, mask, xs, params, saved, dlogits.contiguous(),
+                                    ctx.need_dx, offsets, nelem)
+        dx = [t if need else None for t, need in zip(dxs, ctx.need_dx)]
+        return (None, None, None, None, None, *dx, *_views(flat, params, offsets))
 
 
 # ============================================================================ CrossModalAttention
