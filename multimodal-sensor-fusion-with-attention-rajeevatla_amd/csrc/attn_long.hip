@@ -717,9 +717,12 @@ hipError_t launch_attn_long_fused_fwd(const AttnPair* pairs, int npairs, int B, 
     while (done < npairs && n < ATTN_MAX_PAIRS) {
       a.p[n] = pairs[done++];
       const double lq = a.p[n].Lq, lk = a.p[n].Lk, H = (double)heads * hd;
+      const double esz = a.p[n].qk_bf16 ? 2.0 : 4.0;   // Q / K as stored (bf16 at "medium", §4.4)
       // S = QK^T and the column-sum contraction (the pooled P'V's share, as PoolFwd)
       fl += 2.0 * B * lq * lk * H;
-      by += 4.0 * (B * lq * H + B * lk * H);   // Q, K in (lse, pbar, keep words small)
+      // Q, K in; the dropout keep words (B, h, Lq, Lk / 32) read or written; lse, pbar out
+      by += esz * (B * lq * H + B * lk * H) + (drop ? 4.0 * B * heads * lq * (lk / 32) : 0.0) +
+            4.0 * B * heads * (lq + lk);
       ++n;
     }
     a.npairs = n;
@@ -779,8 +782,11 @@ hipError_t launch_attn_long_fused_bwd(const AttnPair* pairs, int npairs, int B, 
       while (done < ps.size() && n < ATTN_MAX_PAIRS) {
         a.p[n] = ps[done++];
         const double lq = a.p[n].Lq, lk = a.p[n].Lk, H = (double)heads * hd;
+        const double esz = a.p[n].qk_bf16 ? 2.0 : 4.0;   // Q / K as stored (bf16 at "medium", §4.4)
         fl += 2.0 * (2.0 * B * lq * lk * H);          // dQ and dK contractions (S recompute not counted)
-        by += 4.0 * (2.0 * B * lq * H + 2.0 * B * lk * H);   // Q, K in; dQ, dK out
+        // Q, K in (as stored); dQ, dK out (fp32); the keep words in; lse, dpbar, D sums in (small)
+        by += esz * (B * lq * H + B * lk * H) + 4.0 * (B * lq * H + B * lk * H) +
+              (bits ? 4.0 * B * heads * lq * (lk / 32) : 0.0) + 4.0 * B * heads * (2.0 * lq + lk);
         ++n;
       }
       a.npairs = n;

@@ -677,13 +677,7 @@ def eager_tensor(t: Tensor) -> bool:
 
 
 # ============================================================================ CrossEntropyLoss(label_smoothing)
-@torch.library.custom_op("mmfusion::cross_entropy_ls_fwd", mutates_args=(), device_types="cuda")
-def cross_entropy_ls_fwd(logits: Tensor, labels: Tensor, label_smoothing: float) -> Tuple[Tensor, Tensor]:
-    """nn.CrossEntropyLoss(label_smoothing=eps) with reduction "mean" (src/train.py:185-186,
-    310) in one launch of head.hip's cross_entropy_kernel: -> (mean loss, d loss / d logits).
-    Rows labelled -100 (torch's default ignore_index) add nothing and get a zero gradient, the
-    mean is over the other rows; a label outside [0, C) otherwise (torch raises) makes the loss
-    NaN and is never used as an index."""
+def cross_entropy_impl(logits: Tensor, labels: Tensor, label_smoothing: float) -> Tuple[Tensor, Tensor]:
     L = _nat.lib()
     B, C = logits.shape
     dev = logits.device
@@ -693,6 +687,16 @@ def cross_entropy_ls_fwd(logits: Tensor, labels: Tensor, label_smoothing: float)
                                 loss.data_ptr(), dlogits.data_ptr(), _nat.stream_ptr(dev))
     _nat.check(rc, "CrossEntropyLoss(label_smoothing)")
     return loss, dlogits
+
+
+@torch.library.custom_op("mmfusion::cross_entropy_ls_fwd", mutates_args=(), device_types="cuda")
+def cross_entropy_ls_fwd(logits: Tensor, labels: Tensor, label_smoothing: float) -> Tuple[Tensor, Tensor]:
+    """nn.CrossEntropyLoss(label_smoothing=eps) with reduction "mean" (src/train.py:185-186,
+    310) in one launch of head.hip's cross_entropy_kernel: -> (mean loss, d loss / d logits).
+    Rows labelled -100 (torch's default ignore_index) add nothing and get a zero gradient, the
+    mean is over the other rows; a label outside [0, C) otherwise (torch raises) makes the loss
+    NaN and is never used as an index."""
+    return cross_entropy_impl(logits, labels, label_smoothing)
 
 
 @cross_entropy_ls_fwd.register_fake
@@ -712,6 +716,21 @@ def _ce_backward(ctx, dloss, _ddlogits):
 cross_entropy_ls_fwd.register_autograd(_ce_backward, setup_context=_ce_setup)
 
 
+class CrossEntropyEager(torch.autograd.Function):
+    """Eager twin of cross_entropy_ls_fwd (same implementation, autograd.Function dispatch)."""
+
+    @staticmethod
+    def forward(ctx, logits, labels, label_smoothing):
+        loss, dlogits = cross_entropy_impl(logits, labels, label_smoothing)
+        ctx.save_for_backward(dlogits)
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        (dlogits,) = ctx.saved_tensors
+        return dlogits * dloss, None, None
+
+
 def cross_entropy(logits: Tensor, labels: Tensor, label_smoothing: float = 0.0, ignore_index: int = -100) -> Tensor:
     """Drop-in for torch.nn.functional.cross_entropy(logits, labels, label_smoothing=...,
     ignore_index=-100) on (B, C) fp32 logits, int64 labels, reduction "mean": the loss and its
@@ -724,4 +743,6 @@ def cross_entropy(logits: Tensor, labels: Tensor, label_smoothing: float = 0.0, 
     if ignore_index != -100:
         import torch.nn.functional as F
         return F.cross_entropy(logits, labels, label_smoothing=label_smoothing, ignore_index=ignore_index)
+    if eager_tensor(logits):
+        return CrossEntropyEager.apply(logits.contiguous(), labels.contiguous(), float(label_smoothing))
     return torch.ops.mmfusion.cross_entropy_ls_fwd(logits.contiguous(), labels.contiguous(), float(label_smoothing))[0]
