@@ -66,8 +66,13 @@ def test_hybrid_compile_reduce_overhead_fullgraph_bit_identical(mods, case_name,
     rng0 = torch.tensor([0x5EED, 11], dtype=torch.int64)
     ref = _run_steps(model, model, feats_np, mask, g, rng0)
     torch._dynamo.reset()
+    from torch._dynamo.utils import counters
+    counters.clear()
     compiled = torch.compile(model, mode="reduce-overhead", fullgraph=True)
     got = _run_steps(compiled, model, feats_np, mask, g, rng0)
+    # the HIP graphs are really used: inductor skipped cudagraphs for no graph (a skip -- e.g. a
+    # mutated non-static input -- would leave the custom operators' host code running every call)
+    assert not counters["inductor"].get("cudagraph_skips"), dict(counters["inductor"])
     for step, ((ro, rdx, rdw, rr), (co, cdx, cdw, cr)) in enumerate(zip(ref, got)):
         assert torch.equal(co, ro), step
         assert torch.equal(cr, rr), step            # the dropout state advanced the same way
