@@ -260,6 +260,34 @@ class FlatGradBuckets:
                 torch._foreach_add_(dst, src)
             self._fresh[bb] = False
 
+    def direct_grad(self) -> Optional[torch.Tensor]:
+        """One process, one bucket: the tensor the parameters' ``.grad`` already live in, when it
+        has this buffer's layout -- then the optimizer reads it in place and nothing is gathered.
+        The HIP operators return each module's parameter gradients as views of ONE flat buffer,
+        at the same 256-byte-aligned offsets and in the same order (registration order) as this
+        buffer's, so after a HybridFusion backward (eager or a compiled graph's replay) every
+        ``.grad`` is a view of one base at exactly ``offset - span start``.  None when any
+        gradient is missing or elsewhere (several buckets, a gradient produced by a torch op, an
+        accumulated sum that autograd allocated): the caller gathers instead."""
+        if self.world != 1 or len(self.groups) != 1 or not self._fresh[0]:
+            return None
+        params, views = self.groups[0], self._gviews[0]
+        g0 = params[0].grad
+        if g0 is None or g0.dtype != torch.float32 or g0.device != self.grad.device:
+            return None
+        st = g0.untyped_storage()
+        sptr, off0 = st.data_ptr(), g0.storage_offset()
+        if st.nbytes() < 4 * (off0 + self.numel):
+            return None
+        # every gradient in that storage at its offset in this layout, same shape and strides (the
+        # padding between them is zero: the operators allocate their flat gradient zeroed)
+        for p, v in zip(params, views):
+            g = p.grad
+            if (g is None or g.untyped_storage().data_ptr() != sptr or g.storage_offset() - off0 != v.storage_offset()
+                    or g.stride() != v.stride()):
+                return None
+        return g0.as_strided((self.numel,), (1,), off0)
+
     def zero_grad(self) -> None:
         """Forget the flat gradient (the next gather copies instead of adding) and any
         ungathered ``.grad``."""
@@ -362,6 +390,7 @@ class DPTrainer:
         L = nat.lib()
         self.clip_ws = torch.empty(L.mmf_grad_clip_workspace_bytes(), dtype=torch.uint8, device=dev)
         self.last_loss = torch.zeros((), device=dev)
+        self._direct_steps = 0   # optimizer steps that read the backward's gradient buffer in place
 
     def set_lr(self, lr: float) -> None:
         self.lr_dev.fill_(float(lr))
@@ -381,15 +410,24 @@ class DPTrainer:
         return loss.detach()
 
     def optimizer_step(self) -> None:
-        self.flat.finish()
+        # one process, one bucket whose gradients the backward left in one buffer of this layout
+        # (every HybridFusion backward does): clip + AdamW read it in place, nothing is gathered
+        direct = self.flat.direct_grad()
+        if direct is not None:
+            grad = direct
+            self._direct_steps += 1
+        else:
+            self.flat.finish()
+            grad = self.flat.grad
         L = self._nat.lib()
-        rc = L.mmf_clip_adamw_step_dev(self.flat.numel, self.flat.flat.data_ptr(), self.flat.grad.data_ptr(),
+        rc = L.mmf_clip_adamw_step_dev(self.flat.numel, self.flat.flat.data_ptr(), grad.data_ptr(),
                                        self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), self.step_dev.data_ptr(),
                                        self.lr_dev.data_ptr(), float(self.clip_norm), self.grad_norm.data_ptr(),
                                        self.clip_coef.data_ptr(), self.clip_ws.data_ptr(), self.betas[0],
                                        self.betas[1], self.eps, self.wd, 1.0 / self.world,
                                        self._nat.stream_ptr(self.dev))
         self._nat.check(rc, "DPTrainer clip + AdamW")
+        self.flat._armed = False
         self.flat.zero_grad()
 
     def step(self, batches: Sequence[tuple]) -> torch.Tensor:

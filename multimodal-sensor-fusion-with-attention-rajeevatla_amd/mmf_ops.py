@@ -180,13 +180,15 @@ def hybrid_bwd_impl(idesc: Sequence[int], dropout: float, mask: Tensor, xs: Sequ
                     params: Sequence[Tensor], saved: Tensor, dlogits: Tensor, need_dx: Sequence[bool],
                     offsets: Sequence[int], nelem: int):
     """mmf_hybrid_backward -> dx per modality (an empty tensor where not needed), the flat
-    parameter gradient (every gradient WRITTEN by the library, so no zero fill)."""
+    parameter gradient.  The library writes every gradient; the buffer is zeroed for the padding
+    between them, so a trainer whose flat layout matches (harness.FlatGradBuckets.direct_grad)
+    can clip and update from it in place."""
     L = _nat.lib()
     d = hybrid_desc(idesc, dropout)
     M, P = d.num_modalities, d.num_pairs
     dev = mask.device
     ws = torch.empty(_hybrid_sizes(d, (tuple(idesc), float(dropout)))[1], dtype=torch.uint8, device=dev)
-    flat = torch.empty(nelem, dtype=torch.float32, device=dev)
+    flat = torch.zeros(nelem, dtype=torch.float32, device=dev)
     gstruct = _hybrid_params_struct(_views(flat, params, offsets), M, P)
     pstruct = _hybrid_params_struct(params, M, P)
     dxs = [torch.empty_like(x) if need else x.new_empty(0) for x, need in zip(xs, need_dx)]

@@ -245,3 +245,38 @@ def test_model_from_base_config_keys():
         MultimodalFusionModel.from_config(cfg)
 
 
+
+
+def test_direct_grad_reads_the_operator_buffer_in_place():
+    """FlatGradBuckets.direct_grad (one process, one bucket): when every parameter's .grad is a
+    view of one buffer at this buffer's offsets -- what the HIP operators return (mmf_ops
+    flat_offsets: the same 256-byte alignment; HybridFusion's operator order is its registration
+    order) -- the optimizer reads that buffer in place; any other layout, a missing gradient or two
+    buckets fall back to the gather."""
+    _pkg()
+    import mmf_ops
+    from fusion import HybridFusion
+    from harness import FlatGradBuckets
+    torch.manual_seed(0)
+    model = HybridFusion({m: OUT for m in NAMES}, hidden_dim=HID, num_classes=C, num_heads=HEADS, dropout=0.0)
+    params = [p for p in model.parameters()]
+    names = [n for n, _ in model.named_parameters()]
+    pairs = model.present_pairs()
+    assert names == model._param_names(pairs)   # the operator's order is the registration order
+    fb = FlatGradBuckets([params])
+    offs, n = mmf_ops.flat_offsets([p.numel() for p in params])
+    assert n == fb.numel
+    src = torch.zeros(n + 64)[32:]            # (a storage offset of its own, as a pooled output has)
+    src.normal_()
+    for p, o in zip(params, offs):
+        p.grad = src[o:o + p.numel()].view_as(p)
+    d = fb.direct_grad()
+    assert d is not None and d.data_ptr() == src.data_ptr() and d.numel() == fb.numel
+    params[3].grad = params[3].grad.clone()   # one gradient elsewhere
+    assert fb.direct_grad() is None
+    params[3].grad = None
+    assert fb.direct_grad() is None
+    fb2 = FlatGradBuckets([params[:4], params[4:]])
+    for p, o in zip(params, offs):
+        p.grad = src[o:o + p.numel()].view_as(p)
+    assert fb2.direct_grad() is None          # (two buckets: gathered)
