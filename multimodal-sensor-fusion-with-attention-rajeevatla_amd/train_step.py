@@ -90,7 +90,7 @@ class HybridTrainStep:
                  labels: torch.Tensor, lr: float = 1e-3, weight_decay: float = 1e-4,
                  betas=(0.9, 0.999), eps: float = 1e-8, label_smoothing: float = 0.05,
                  gradient_clip_norm: float = 1.0, process_group=None, input_grads: bool = True,
-                 accumulate: int = 1, fuse_clip: bool = True):
+                 accumulate: int = 1, fuse_clip: bool = True, overlap: Optional[bool] = None):
         dev = mask.device
         _nat.require_device(mask, "training inputs")
         self.model = model.train()
@@ -162,7 +162,7 @@ class HybridTrainStep:
         # one process, one micro-batch: step() has the train step write the clip norm's partials itself
         # (the L = 1 plan in its weight-gradient launch) and advance the step counter, and the
         # optimizer runs the update launch only
-        self.fuse_clip = bool(fuse_clip) and self.world == 1 and self.accumulate == 1
+        self.fuse_clip = bool(fuse_clip) and self.world == 1 and self.accumulate == 1 and not overlap
         self._fused_pending = False   # partials written and the counter advanced by the last fwd/bwd
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         # several ranks: the exchange in two buckets overlapped with the backward.  The plan's
@@ -170,7 +170,9 @@ class HybridTrainStep:
         # [projections | pairs, gates, classifier]; every gradient of the second span is final
         # after part 1 of the train step (the attention backward), the projections' after part 2
         # (dZ, dX, their weight gradients).  Part 1's bucket is all-reduced while part 2 runs.
-        self.overlap = self.world > 1
+        # (overlap=True with one rank: the same bucketed path, exchanges of one rank -- how the
+        # RCCL calls and their stream order are exercised on a one-GPU box)
+        self.overlap = (self.world > 1) if overlap is None else (bool(overlap) and self.pg is not None)
         split = self.plan.offsets[2 * d.num_modalities] if len(self.plan.offsets) > 2 * d.num_modalities else n
         self.bucket_spans = ((split, n), (0, split))    # (issued after part 1, after part 2)
         self.graph2: Optional[torch.cuda.CUDAGraph] = None

@@ -5,8 +5,8 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/${1:-r05a}
 mkdir -p $O
-timeout -k 10 500 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_gpu_train_step.py tests/test_gpu_cross_entropy.py tests/test_dp.py tests/test_gpu_c5_bench.py tests/test_gpu_headline.py > $O/pytest_sel.log 2>&1
-rc=$?; echo "pytest rc=$rc" >> $O/pytest_sel.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread > $O/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> $O/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest crashed rc=$rc"; exit $rc; fi
 TORCH_LOGS=perf_hints timeout -k 10 400 python -u scripts/host_phase_profile.py --out $O/host_l1.json > $O/host_l1.log 2>&1 || exit $?
 echo done
