@@ -109,7 +109,6 @@ def _hybrid_meta(idesc: Sequence[int]):
 
 
 _PSTRUCT: Dict[tuple, "_nat.HybridParams"] = {}
-_SIZES: Dict[tuple, Tuple[int, int]] = {}
 
 
 def _hybrid_params_struct(params: Sequence[Tensor], M: int, P: int) -> "_nat.HybridParams":
@@ -141,16 +140,6 @@ def _hybrid_params_struct(params: Sequence[Tensor], M: int, P: int) -> "_nat.Hyb
     return s
 
 
-def _hybrid_sizes(d: "_nat.HybridDesc", key: tuple) -> Tuple[int, int]:
-    """(saved, workspace) bytes of a descriptor (host arithmetic in the library), cached."""
-    hit = _SIZES.get(key)
-    if hit is None:
-        L = _nat.lib()
-        hit = (L.mmf_hybrid_saved_bytes(ctypes.byref(d)), L.mmf_hybrid_workspace_bytes(ctypes.byref(d)))
-        _SIZES[key] = hit
-    return hit
-
-
 def hybrid_fwd_impl(idesc: Sequence[int], dropout: float, rng_state: Tensor, mask: Tensor, xs: Sequence[Tensor],
                     params: Sequence[Tensor]):
     """mmf_hybrid_forward on the caller's stream -> logits (B, C), fusion_weights (B, M), saved
@@ -160,7 +149,7 @@ def hybrid_fwd_impl(idesc: Sequence[int], dropout: float, rng_state: Tensor, mas
     d = hybrid_desc(idesc, dropout)
     B, M, C, mshapes = _hybrid_meta(idesc)
     dev = mask.device
-    saved = torch.empty(_hybrid_sizes(d, (tuple(idesc), float(dropout)))[0], dtype=torch.uint8, device=dev)
+    saved = torch.empty(_nat.lib().mmf_hybrid_saved_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
     logits = torch.empty(B, C, dtype=torch.float32, device=dev)
     fw = torch.empty(B, M, dtype=torch.float32, device=dev)
     maps = [torch.empty(s, dtype=torch.float32, device=dev) for s in mshapes]
@@ -187,7 +176,7 @@ def hybrid_bwd_impl(idesc: Sequence[int], dropout: float, mask: Tensor, xs: Sequ
     d = hybrid_desc(idesc, dropout)
     M, P = d.num_modalities, d.num_pairs
     dev = mask.device
-    ws = torch.empty(_hybrid_sizes(d, (tuple(idesc), float(dropout)))[1], dtype=torch.uint8, device=dev)
+    ws = torch.empty(_nat.lib().mmf_hybrid_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
     flat = torch.zeros(nelem, dtype=torch.float32, device=dev)
     gstruct = _hybrid_params_struct(_views(flat, params, offsets), M, P)
     pstruct = _hybrid_params_struct(params, M, P)
