@@ -256,14 +256,17 @@ class ModuleRunner:
     grads), then the exchange + clip + AdamW of harness.DPTrainer (flat buffers, bucketed
     all-reduce).  Eager; no graph."""
 
-    def __init__(self, model, feats, mask, labels, pg, compiled=False):
+    def __init__(self, model, feats, mask, labels, pg, compiled=False, traceable=False):
         from harness import DPTrainer
         import mmf_ops
         self.ce = mmf_ops.cross_entropy
         self.model = model.train()
-        # --path compiled: the reference trainer's torch.compile(mode="reduce-overhead")
-        # (src/train.py:193-231) around the module; the optimizer step stays outside
-        self.fwd = torch.compile(model, mode="reduce-overhead", fullgraph=True) if compiled else model
+        # --path compiled: the reference trainer's own call, torch.compile(module, backend="inductor",
+        # mode="reduce-overhead") (src/train.py:101-122, 193-231); the optimizer step stays outside.
+        # HybridFusion is opaque to TorchDynamo by default; --traceable compiles its traced form
+        # (custom operators, fullgraph) instead
+        model.traceable = bool(traceable)
+        self.fwd = (torch.compile(model, mode="reduce-overhead", fullgraph=bool(traceable)) if compiled else model)
         self.names = list(model.modality_names)
         self.feats = [f.clone().requires_grad_(True) for f in feats]
         self.mask, self.labels = mask, labels
@@ -296,6 +299,9 @@ def main(argv=None):
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--path", default="step", choices=["step", "module", "compiled"])
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--traceable", action="store_true",
+                    help="--path compiled: compile HybridFusion's traced form (custom operators, fullgraph) "
+                         "instead of the default opaque module")
     ap.add_argument("--dropout", type=float, default=0.1,
                     help="diagnostics only: the benchmark workload is dropout 0.1")
     ap.add_argument("--skip-cpu", action="store_true")
@@ -354,7 +360,8 @@ def main(argv=None):
     else:
         feats, mask, labels = make_inputs(w, B, 42 + rank, dev)
     if args.path in ("module", "compiled"):
-        trainer = ModuleRunner(model, feats, mask, labels, pg, compiled=args.path == "compiled")
+        trainer = ModuleRunner(model, feats, mask, labels, pg, compiled=args.path == "compiled",
+                               traceable=args.traceable)
     else:
         trainer = HybridTrainStep(model, feats, mask, labels, process_group=pg)
 
@@ -428,8 +435,10 @@ def main(argv=None):
                      "fused step, eager" if args.path == "step" else
                      "nn.Module forward + autograd backward, eager (src/train.py's call path)"
                      if args.path == "module" else
-                     "torch.compile(module, mode='reduce-overhead', fullgraph=True) forward + backward "
-                     "(src/train.py's compiled call path)")
+                     ("torch.compile(module, mode='reduce-overhead', fullgraph=True) of the traced form "
+                      "(HybridFusion.traceable) forward + backward" if args.traceable else
+                      "torch.compile(module, mode='reduce-overhead') forward + backward (src/train.py's "
+                      "compiled call path; HybridFusion opaque to TorchDynamo)"))
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
@@ -443,7 +452,7 @@ def main(argv=None):
                                    f"{mask_note}"
                                    f", fwd+CE(ls=0.05)+bwd+clip(1.0)+AdamW; {path_note}",
                        "global_batch": B * world, "per_gpu_batch": B, "seq_len": lens or 1,
-                       "parallelism": f"dp{world}", "path": args.path,
+                       "parallelism": f"dp{world}", "path": args.path + ("+traceable" if args.traceable else ""),
                        "graph": graph, "matmul_precision": args.precision},
             "ms_per_step_median": round(med, 4),
             "ms_per_step_p10_p90": [round(per_step[len(per_step) // 10], 4),

@@ -320,8 +320,23 @@ class HybridFusion(nn.Module):
         return names + ["classifier.0.weight", "classifier.0.bias", "classifier.3.weight", "classifier.3.bias"]
 
     # ------------------------------------------------------------------ forward
+    # torch.compile (the reference compiles the fusion model, src/train.py:193-231, without
+    # fullgraph): by default the module is one opaque native step to TorchDynamo -- its forward runs
+    # as in eager mode (HybridSink: gradients straight into the module's flat buffer) and Dynamo
+    # does not trace it, because tracing buys no fusion here (the work is already a few HIP
+    # launches) and costs a cudagraph-tree replay, AOTAutograd's runtime wrappers and one
+    # AccumulateGrad per parameter per step.  traceable = True keeps the fully
+    # traceable form: custom operators with fake kernels and autograd formulas, fullgraph-capable.
+    traceable: bool = False
+
     def forward(self, modality_features: Dict[str, torch.Tensor],
                 modality_mask: Optional[torch.Tensor] = None, return_attention: bool = False):
+        if torch.compiler.is_compiling() and not self.traceable:
+            return _opaque_forward(self, modality_features, modality_mask, return_attention)
+        return self._forward(modality_features, modality_mask, return_attention)
+
+    def _forward(self, modality_features: Dict[str, torch.Tensor],
+                 modality_mask: Optional[torch.Tensor] = None, return_attention: bool = False):
         if not self.modality_names:
             raise ValueError("No modalities configured for HybridFusion.")
         ref = modality_features[self.modality_names[0]]
@@ -357,8 +372,14 @@ class HybridFusion(nn.Module):
             # (traced by TorchDynamo: the custom operator, its fake kernel and autograd formula)
             logits, fw, _saved, rng_next, maps = torch.ops.mmfusion.hybrid_fwd(
                 idesc, float(self.dropout.p), self._rng_state, _nat.f32c(modality_mask), xs, params)
+        elif torch.is_grad_enabled() and _ops._sink_ok(params):
+            # eager: the parameters' gradients written straight into the module's flat gradient
+            # buffer (mmf_ops.HybridSink: no per-parameter autograd work); params[0] anchors the graph
+            logits, fw, _saved, rng_next, *maps = _ops.HybridSink.apply(
+                idesc, float(self.dropout.p), self._rng_state, _nat.f32c(modality_mask), self, params, params[0], *xs)
         else:
-            # eager: the same implementation through autograd.Function (mmf_ops.HybridEager)
+            # eager, some parameter frozen or hooked: the same implementation with every parameter an
+            # autograd input (mmf_ops.HybridEager)
             logits, fw, _saved, rng_next, *maps = _ops.HybridEager.apply(
                 idesc, float(self.dropout.p), self._rng_state, _nat.f32c(modality_mask), len(xs), *xs, *params)
         self._rng_state.copy_(rng_next)     # the device Philox stream advanced by one call
@@ -391,9 +412,34 @@ class HybridFusion(nn.Module):
                                f"(found {c[2][0].dtype} on {c[2][0].device})")
         return c[1], c[2]
 
+    def _grad_sink(self, params: List[torch.Tensor]) -> "_ops.GradSink":
+        """The flat gradient buffer the eager backward writes into (mmf_ops.HybridSink)."""
+        sk = self.__dict__.get("_mmf_grad_sink")
+        if sk is None or not sk.matches(params):
+            sk = _ops.GradSink(params)
+            self.__dict__["_mmf_grad_sink"] = sk
+        return sk
+
+    def mmf_grads_consumed(self) -> None:
+        """A trainer has applied the gradients the parameters' ``.grad`` hold (views of the
+        module's flat gradient buffer): the next backward writes them afresh instead of adding,
+        without the ``.grad`` attributes being reset to None (harness.DPTrainer calls this)."""
+        sk = self.__dict__.get("_mmf_grad_sink")
+        if sk is not None:
+            sk.fresh = True
+
     def _apply(self, fn, *args, **kwargs):
         self.__dict__.pop("_mmf_op_params", None)
+        self.__dict__.pop("_mmf_grad_sink", None)
         return super()._apply(fn, *args, **kwargs)
+
+    def __getstate__(self):
+        # (copy.deepcopy / pickling, src/train.py:73-76: the caches are rebuilt on first use)
+        st = super().__getstate__() if hasattr(super(), "__getstate__") else self.__dict__.copy()
+        st = dict(st)
+        st.pop("_mmf_op_params", None)
+        st.pop("_mmf_grad_sink", None)
+        return st
 
     def compute_adaptive_weights(self, modality_features: Dict[str, torch.Tensor],
                                  modality_mask: torch.Tensor) -> torch.Tensor:
@@ -423,6 +469,12 @@ class HybridFusion(nn.Module):
             layer = self.gating_layers[name]
             gparams += [layer.weight, layer.bias]
         return torch.ops.mmfusion.adaptive_weights_fwd(_nat.f32c(mask), [_nat.f32c(f) for f in feats], gparams)
+
+
+@torch.compiler.disable
+def _opaque_forward(model: "HybridFusion", modality_features, modality_mask, return_attention):
+    """HybridFusion's forward run outside TorchDynamo (HybridFusion.traceable = False)."""
+    return model._forward(modality_features, modality_mask, return_attention)
 
 
 def build_fusion_model(fusion_type: str, modality_dims: Dict[str, int], num_classes: int,

@@ -229,6 +229,7 @@ class FlatGradBuckets:
             for p in g:
                 self._bucket_of[id(p)] = b
         self._fresh = [True] * len(self.groups)    # the bucket's span holds no gradient yet
+        self._direct_last = None                    # (grad tensors, base) of direct_grad's last match
         self._pending = [0] * len(self.groups)
         self._works: List[Any] = [None] * len(self.groups)
         self._armed = False
@@ -272,6 +273,9 @@ class FlatGradBuckets:
         if self.world != 1 or len(self.groups) != 1 or not self._fresh[0]:
             return None
         params, views = self.groups[0], self._gviews[0]
+        last = self._direct_last
+        if last is not None and all(p.grad is g for p, g in zip(params, last[0])):
+            return last[1]   # the same gradient tensors as the last validated step (a grad sink)
         g0 = params[0].grad
         if g0 is None or g0.dtype != torch.float32 or g0.device != self.grad.device:
             return None
@@ -286,7 +290,9 @@ class FlatGradBuckets:
             if (g is None or g.untyped_storage().data_ptr() != sptr or g.storage_offset() - off0 != v.storage_offset()
                     or g.stride() != v.stride()):
                 return None
-        return g0.as_strided((self.numel,), (1,), off0)
+        base = g0.as_strided((self.numel,), (1,), off0)
+        self._direct_last = ([p.grad for p in params], base)
+        return base
 
     def zero_grad(self) -> None:
         """Forget the flat gradient (the next gather copies instead of adding) and any
@@ -391,6 +397,11 @@ class DPTrainer:
         self.clip_ws = torch.empty(L.mmf_grad_clip_workspace_bytes(), dtype=torch.uint8, device=dev)
         self.last_loss = torch.zeros((), device=dev)
         self._direct_steps = 0   # optimizer steps that read the backward's gradient buffer in place
+        # modules whose backward writes their parameters' gradients into a flat buffer of their own
+        # (fusion.HybridFusion's grad sink), and the parameters no such module owns
+        self._sink_owners = [m for m in model.modules() if hasattr(m, "mmf_grads_consumed")]
+        owned = {id(p) for m in self._sink_owners for p in m.parameters()}
+        self._unsunk = [p for p in self.flat.params if id(p) not in owned]
 
     def set_lr(self, lr: float) -> None:
         self.lr_dev.fill_(float(lr))
@@ -428,7 +439,17 @@ class DPTrainer:
                                        self._nat.stream_ptr(self.dev))
         self._nat.check(rc, "DPTrainer clip + AdamW")
         self.flat._armed = False
-        self.flat.zero_grad()
+        if direct is not None and self._sink_owners:
+            # the gradients lived in the modules' own flat buffers (grad sinks): leave the views
+            # attached and mark them consumed -- the next backward writes afresh -- instead of
+            # resetting every .grad (one attribute write per parameter and step)
+            for m in self._sink_owners:
+                m.mmf_grads_consumed()
+            for p in self._unsunk:
+                p.grad = None
+            self.flat._fresh = [True] * len(self.flat.groups)
+        else:
+            self.flat.zero_grad()
 
     def step(self, batches: Sequence[tuple]) -> torch.Tensor:
         """batches: `accumulate` tuples (features, labels, mask); returns the mean loss."""

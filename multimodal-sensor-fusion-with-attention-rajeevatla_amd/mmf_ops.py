@@ -115,7 +115,17 @@ def _hybrid_params_struct(params: Sequence[Tensor], M: int, P: int) -> "_nat.Hyb
     """The C-ABI parameter (or gradient) struct for these tensors' addresses, cached per address
     set (a training loop passes the same parameters every step; gradient buffers recur through
     the caching allocator)."""
-    ptrs = tuple(t.data_ptr() for t in params)
+    return _struct_from_ptrs(tuple(t.data_ptr() for t in params), M, P)
+
+
+def _grad_struct(flat: Tensor, offsets: Sequence[int], M: int, P: int) -> "_nat.HybridParams":
+    """The gradient struct of a flat gradient buffer laid out at `offsets` (addresses by
+    arithmetic: no per-parameter views to build)."""
+    base = flat.data_ptr()
+    return _struct_from_ptrs(tuple(base + 4 * o for o in offsets), M, P)
+
+
+def _struct_from_ptrs(ptrs: tuple, M: int, P: int) -> "_nat.HybridParams":
     key = (M, P, ptrs)
     s = _PSTRUCT.get(key)
     if s is not None:
@@ -167,7 +177,7 @@ def hybrid_fwd_impl(idesc: Sequence[int], dropout: float, rng_state: Tensor, mas
 
 def hybrid_bwd_impl(idesc: Sequence[int], dropout: float, mask: Tensor, xs: Sequence[Tensor],
                     params: Sequence[Tensor], saved: Tensor, dlogits: Tensor, need_dx: Sequence[bool],
-                    offsets: Sequence[int], nelem: int):
+                    offsets: Sequence[int], nelem: int, flat: Optional[Tensor] = None):
     """mmf_hybrid_backward -> dx per modality (an empty tensor where not needed), the flat
     parameter gradient.  The library writes every gradient; the buffer is zeroed for the padding
     between them, so a trainer whose flat layout matches (harness.FlatGradBuckets.direct_grad)
@@ -177,8 +187,9 @@ def hybrid_bwd_impl(idesc: Sequence[int], dropout: float, mask: Tensor, xs: Sequ
     M, P = d.num_modalities, d.num_pairs
     dev = mask.device
     ws = torch.empty(_nat.lib().mmf_hybrid_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
-    flat = torch.zeros(nelem, dtype=torch.float32, device=dev)
-    gstruct = _hybrid_params_struct(_views(flat, params, offsets), M, P)
+    if flat is None:
+        flat = torch.zeros(nelem, dtype=torch.float32, device=dev)
+    gstruct = _grad_struct(flat, offsets, M, P)
     pstruct = _hybrid_params_struct(params, M, P)
     dxs = [torch.empty_like(x) if need else x.new_empty(0) for x, need in zip(xs, need_dx)]
     xarr = _nat.ptr_array([x.data_ptr() for x in xs])
@@ -243,6 +254,102 @@ def _hybrid_backward(ctx, dlogits, _dfw, _dsaved, _drng, _dmaps):
 
 
 hybrid_fwd.register_autograd(_hybrid_backward, setup_context=_hybrid_setup)
+
+
+class GradSink:
+    """The flat gradient buffer of one HybridFusion module, for the eager grad-sink path
+    (HybridSink): the operator's flat layout (flat_offsets of the operator's parameter order,
+    which is the module's registration order), so every parameter's ``.grad`` is a view of it and
+    a trainer with the same layout (harness.FlatGradBuckets.direct_grad) clips and updates from it
+    in place.
+
+    States between backwards: ``fresh`` -- the next backward WRITES the gradients into the buffer
+    (after the parameters' ``.grad`` were set to None, or after ``consumed()``: a trainer that
+    applied them); otherwise the parameters' ``.grad`` are the buffer's views holding gradients
+    still to be accumulated into (the next backward writes into a scratch buffer and adds it)."""
+
+    def __init__(self, params: Sequence[Tensor]):
+        p0 = params[0]
+        self.offsets, self.nelem = flat_offsets([p.numel() for p in params])
+        self.flat = torch.zeros(self.nelem, dtype=torch.float32, device=p0.device)
+        self.views = [self.flat.as_strided(tuple(p.shape), tuple(p.stride()), o) for p, o in zip(params, self.offsets)]
+        self.fresh = True
+
+    def matches(self, params: Sequence[Tensor]) -> bool:
+        return len(params) == len(self.views) and params[0].device == self.flat.device
+
+
+def _sink_ok(params: Sequence[Tensor]) -> bool:
+    """The grad-sink path keeps autograd's semantics for these parameters: every one trainable,
+    contiguous fp32 (the layout), and none with a tensor hook (register_hook can rewrite a
+    gradient before accumulation: those parameters go through autograd's AccumulateGrad).
+    Post-accumulate-grad hooks are called by the sink path itself, after the gradient lands."""
+    for p in params:
+        if not p.requires_grad or p._backward_hooks:
+            return False
+    return True
+
+
+class HybridSink(torch.autograd.Function):
+    """Eager HybridFusion with the parameters OUTSIDE the autograd graph: the backward writes
+    every parameter gradient straight into the module's GradSink and attaches the sink's views as
+    ``.grad`` (what AccumulateGrad would leave there after a first backward, and the sum after
+    further ones), so a step pays no per-parameter AccumulateGrad nodes, saved-tensor unpacking or
+    gradient views per call -- at the reference's 2-D inputs (launch-bound) those were most of the
+    step.  Only the modality inputs (and one anchor parameter, so a graph exists when
+    no input requires grad) are autograd inputs.  Inputs: (idesc, dropout, rng_state, mask, owner,
+    params, anchor, *xs) with `params` a Python list autograd does not look into."""
+
+    @staticmethod
+    def forward(ctx, idesc, dropout, rng_state, mask, owner, params, anchor, *xs):
+        logits, fw, saved, rng_next, maps = hybrid_fwd_impl(idesc, dropout, rng_state, mask, xs, params)
+        ctx.set_materialize_grads(False)
+        ctx.idesc, ctx.dropout, ctx.owner, ctx.params = idesc, dropout, owner, params
+        ctx.need_dx = [bool(n) for n in ctx.needs_input_grad[7:]]
+        ctx.save_for_backward(mask, saved, *xs)
+        ctx.mark_non_differentiable(fw, saved, rng_next, *maps)
+        return (logits, fw, saved, rng_next, *maps)
+
+    @staticmethod
+    def backward(ctx, dlogits, *_unused):
+        nx = len(ctx.need_dx)
+        if dlogits is None:
+            return (None,) * (7 + nx)
+        mask, saved, *xs = ctx.saved_tensors
+        params = ctx.params
+        sink = ctx.owner._grad_sink(params)
+        grads = [p.grad for p in params]
+        if all(g is None for g in grads) or (sink.fresh and all(g is None or g is v for g, v in zip(grads, sink.views))):
+            mode = 0          # write into the sink (set_to_none zero_grad, or a trainer consumed it)
+        elif all(g is v for g, v in zip(grads, sink.views)):
+            mode = 1          # add into the sink (gradients still to be applied)
+        else:
+            mode = 2          # someone else's .grad tensors: add into them
+        dst = sink.flat if mode == 0 else torch.zeros(sink.nelem, dtype=torch.float32, device=sink.flat.device)
+        dxs, _ = hybrid_bwd_impl(ctx.idesc, ctx.dropout, mask, xs, params, saved, dlogits.contiguous(), ctx.need_dx,
+                                 sink.offsets, sink.nelem, flat=dst)
+        if mode == 0:
+            for p, g, v in zip(params, grads, sink.views):
+                if g is None:
+                    p.grad = v
+            sink.fresh = False
+        elif mode == 1:
+            sink.flat.add_(dst)
+        else:
+            have = [(g, dst.as_strided(tuple(p.shape), tuple(p.stride()), o))
+                    for p, g, o in zip(params, grads, sink.offsets) if g is not None]
+            if have:
+                torch._foreach_add_([g for g, _ in have], [v for _, v in have])
+            for p, g, o in zip(params, grads, sink.offsets):
+                if g is None:
+                    p.grad = dst.as_strided(tuple(p.shape), tuple(p.stride()), o)
+        for p in params:   # (what AccumulateGrad does after accumulating)
+            hooks = p._post_accumulate_grad_hooks
+            if hooks:
+                for h in hooks.values():
+                    h(p)
+        dx = [t if need else None for t, need in zip(dxs, ctx.need_dx)]
+        return (None, None, None, None, None, None, None, *dx)
 
 
 class HybridEager(torch.autograd.Function):

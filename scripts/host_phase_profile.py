@@ -63,7 +63,7 @@ def main():
     ap.add_argument("--workload", default="c2_l1")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--out", default=None)
-    ap.add_argument("--paths", default="module,compiled")
+    ap.add_argument("--paths", default="module,compiled,compiled_traceable")
     args = ap.parse_args()
     from fusion import HybridFusion
     dev = torch.device("cuda", 0)
@@ -75,7 +75,8 @@ def main():
         model = HybridFusion({n: w["D"] for n in names}, hidden_dim=w["H"], num_classes=w["C"],
                              num_heads=w["heads"], dropout=0.1).to(dev)
         feats, mask, labels = bench.make_inputs(w, w["B"], 42, dev)
-        r = bench.ModuleRunner(model, feats, mask, labels, None, compiled=(path == "compiled"))
+        r = bench.ModuleRunner(model, feats, mask, labels, None, compiled=path.startswith("compiled"),
+                               traceable=path.endswith("traceable"))
         for _ in range(10):
             r.step()
         torch.cuda.synchronize()

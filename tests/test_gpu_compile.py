@@ -34,6 +34,7 @@ def _hybrid(fusion, case, p=0.1):
     sd = hybrid_state(case.names, case.dims, case.hidden, case.classes, case.seed)
     model = fusion.HybridFusion({m: case.dims[m] for m in case.names}, hidden_dim=case.hidden,
                                 num_classes=case.classes, num_heads=case.heads, dropout=p)
+    model.traceable = True   # the fully traceable form (custom operators; the default is opaque)
     model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
     return model.cuda()
 
@@ -192,10 +193,41 @@ def test_encoders_and_full_model_compile_fullgraph(mods):
            "model": {"fusion_type": "hybrid", "hidden_dim": 64, "output_dim": 32, "num_heads": 4,
                      "dropout": 0.0, "layer_norm": True, "encoders": enc}}
     model = harness.MultimodalFusionModel.from_config(cfg).cuda().eval()
+    model.fusion_model.traceable = True   # (fullgraph: the traceable form of HybridFusion)
     feats = {m: torch.randn(2, 30, enc[m]["input_dim"], device="cuda") for m in enc}
     mask = torch.tensor([[1.0, 1.0, 1.0], [1.0, 0.0, 1.0]], device="cuda")
     ref = model(feats, mask)
     torch._dynamo.reset()
     got = torch.compile(model, fullgraph=True)(feats, mask)
     torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)
+    torch._dynamo.reset()
+
+
+@pytest.mark.parametrize("case_name", ["seq_c2_b3", "tiny_l1"])
+def test_hybrid_compile_default_is_opaque_and_bit_identical(mods, case_name):
+    """The default (HybridFusion.traceable = False) under the reference's own call,
+    torch.compile(model, mode="reduce-overhead") without fullgraph (src/train.py:101-122): TorchDynamo
+    runs the module as one opaque native step -- no graph is compiled for it -- and forward +
+    backward (the grad-sink path) equal eager bit for bit over several steps, train mode."""
+    fusion = mods[0]
+    case = next(c for c in HYBRID_CASES if c.name == case_name)
+    model = _hybrid(fusion, case)
+    model.traceable = False
+    model.train()
+    feats_np, mask_np, grad_np = hybrid_inputs(case)
+    mask, g = torch.from_numpy(mask_np).cuda(), torch.from_numpy(grad_np).cuda()
+    rng0 = torch.tensor([0x5EED, 11], dtype=torch.int64)
+    ref = _run_steps(model, model, feats_np, mask, g, rng0)
+    torch._dynamo.reset()
+    from torch._dynamo.utils import counters
+    counters.clear()
+    compiled = torch.compile(model, mode="reduce-overhead")
+    got = _run_steps(compiled, model, feats_np, mask, g, rng0)
+    for step, ((ro, rdx, rdw, rr), (co, cdx, cdw, cr)) in enumerate(zip(ref, got)):
+        assert torch.equal(co, ro) and torch.equal(cr, rr), step
+        for k in rdx:
+            assert torch.equal(cdx[k], rdx[k]), (step, k)
+        for n in rdw:
+            assert torch.equal(cdw[n], rdw[n]), (step, n)
+    assert not counters["inductor"].get("cudagraph_recorded_non_static_inputs"), dict(counters["inductor"])
     torch._dynamo.reset()
