@@ -113,10 +113,27 @@ __device__ __forceinline__ float ld_wt(const float* p) {
 }
 
 // (tile, pair) of this workgroup (one place, so a different layout of the grid changes one
-// function).  A pair-major-by-XCD layout (every XCD's workgroups on one or two pairs, so their
-// W_v / W_o loads hit that XCD's L2) measured no change: 0.0699 / 0.0697 vs 0.0700 / 0.0706 ms,
-// the weight-load phase 8.3 K vs 8.6 K cycles (scripts/gpu_l1ab.sh, profiles/r04/l1/ab_xcd/).
+// function).  Workgroups are dealt to the 8 XCDs round-robin in dispatch order (x fastest), so with
+// the plain (tile, pair) = (blockIdx.x, blockIdx.y) every XCD holds tiles of EVERY pair and fetches
+// every pair's W_k / W_v / W_o into its own L2: 8 copies of ~1.1 MB of weights per launch at C2, the
+// 2x of the measured HBM traffic over the algorithmic bytes (profiles/pmc_traffic_c2_l1_highest.json:
+// 18.1 vs 9.25 MB).  XCD-major instead (the grid a multiple of 8, two-dimensional): the workgroup
+// with dispatch index l is work item w = (l % 8) (N / 8) + l / 8 -- consecutive work items, i.e. the
+// tiles of one or two pairs, on one XCD -- so each XCD fetches at most two pairs' weights.  (Measured
+// in round 4 as time-neutral, 0.0699 / 0.0697 vs 0.0700 / 0.0706 ms, scripts/gpu_l1ab.sh,
+// profiles/r04/l1/ab_xcd/; round 5 adopts it for the traffic.)  MMF_L1_LINEAR_IDS: the plain layout
+// (the A/B build, `make l1lin`).
 __device__ __forceinline__ void l1_ids(int& tile, int& pair) {
+#ifndef MMF_L1_LINEAR_IDS
+  const unsigned T = gridDim.x, N = gridDim.x * gridDim.y;
+  if (gridDim.y > 1 && (N & 7u) == 0) {
+    const unsigned l = blockIdx.x + T * blockIdx.y;
+    const unsigned w = (l & 7u) * (N >> 3) + (l >> 3);
+    pair = (int)(w / T);
+    tile = (int)(w - (unsigned)pair * T);
+    return;
+  }
+#endif
   tile = blockIdx.x;
   pair = blockIdx.y;
 }
