@@ -288,10 +288,10 @@ class HybridFusion(nn.Module):
         seq, dims = self._shapes(feats)
         return _Plan(self, seq, dims, feats[0].size(0), self.present_pairs(), return_attention)
 
-    def _shapes(self, feats: List[torch.Tensor]) -> Tuple[List[int], List[int]]:
+    def _shapes(self, feats: List[torch.Tensor], in_dims: Optional[List[int]] = None) -> Tuple[List[int], List[int]]:
         seq, dims = [], []
         B = feats[0].size(0)
-        for name, x in zip(self.modality_names, feats):
+        for m, (name, x) in enumerate(zip(self.modality_names, feats)):
             if x.dim() == 2:
                 seq.append(0)
             elif x.dim() == 3:
@@ -300,7 +300,7 @@ class HybridFusion(nn.Module):
                 raise RuntimeError(f"features for modality '{name}' must be 2-D or 3-D, got {tuple(x.shape)}")
             if x.size(0) != B:
                 raise RuntimeError(f"batch size mismatch for modality '{name}': {x.size(0)} vs {B}")
-            in_f = self.projections[name][0].in_features
+            in_f = in_dims[m] if in_dims is not None else self.projections[name][0].in_features
             if x.size(-1) != in_f:
                 raise RuntimeError(f"modality '{name}': expected feature dim {in_f}, got {x.size(-1)}")
             dims.append(int(x.size(-1)))
@@ -352,10 +352,10 @@ class HybridFusion(nn.Module):
                 raise KeyError(f"Missing features for modality '{name}' in HybridFusion forward pass.")
             feats.append(modality_features[name].to(device))
         _nat.require_device(ref, "HybridFusion input")
-        seq, dims = self._shapes(feats)
-        # traced (torch.compile, fake tensors): the custom operator; eager: HybridEager
+        # traced (torch.compile, fake tensors): the custom operator; eager: HybridSink / HybridEager
         compiling = not _ops.eager_tensor(ref)
         if compiling:
+            seq, dims = self._shapes(feats)
             for p in self.parameters():
                 if p.device != device or p.dtype != torch.float32:
                     raise RuntimeError("mmfusion HybridFusion needs float32 parameters on the input's device "
@@ -364,25 +364,28 @@ class HybridFusion(nn.Module):
             named = dict(self.named_parameters())
             params = [named[n] for n in self._param_names(pairs)]
         else:
-            pairs, params = self._op_params(device)
+            pairs, params, in_dims = self._op_params(device)
+            seq, dims = self._shapes(feats, in_dims)
         idesc = _ops.hybrid_idesc(batch_size, self.hidden_dim, self.num_heads, self.num_classes, seq, dims,
                                   [(q, k) for q, k, _ in pairs], self.training, return_attention, _precision())
         xs = [_nat.f32c(x) for x in feats]
         if compiling:
-            # (traced by TorchDynamo: the custom operator, its fake kernel and autograd formula)
+            # (traced by TorchDynamo: the custom operator, its fake kernel and autograd formula; the
+            # operator is functional, so the advanced dropout state comes back and is copied in)
             logits, fw, _saved, rng_next, maps = torch.ops.mmfusion.hybrid_fwd(
                 idesc, float(self.dropout.p), self._rng_state, _nat.f32c(modality_mask), xs, params)
+            self._rng_state.copy_(rng_next)     # the device Philox stream advanced by one call
         elif torch.is_grad_enabled() and _ops._sink_ok(params):
             # eager: the parameters' gradients written straight into the module's flat gradient
-            # buffer (mmf_ops.HybridSink: no per-parameter autograd work); params[0] anchors the graph
-            logits, fw, _saved, rng_next, *maps = _ops.HybridSink.apply(
+            # buffer (mmf_ops.HybridSink: no per-parameter autograd work); params[0] anchors the
+            # graph; the library advances the dropout state in the module's buffer itself
+            logits, fw, _saved, *maps = _ops.HybridSink.apply(
                 idesc, float(self.dropout.p), self._rng_state, _nat.f32c(modality_mask), self, params, params[0], *xs)
         else:
             # eager, some parameter frozen or hooked: the same implementation with every parameter an
             # autograd input (mmf_ops.HybridEager)
-            logits, fw, _saved, rng_next, *maps = _ops.HybridEager.apply(
+            logits, fw, _saved, *maps = _ops.HybridEager.apply(
                 idesc, float(self.dropout.p), self._rng_state, _nat.f32c(modality_mask), len(xs), *xs, *params)
-        self._rng_state.copy_(rng_next)     # the device Philox stream advanced by one call
         if dtype != torch.float32 and dtype.is_floating_point:
             logits = logits.to(dtype)
         if return_attention:
@@ -390,7 +393,7 @@ class HybridFusion(nn.Module):
             return logits, {"attention_maps": attention_maps, "fusion_weights": fw.detach()}
         return logits
 
-    def _op_params(self, device) -> Tuple[List[Tuple[int, int, str]], List[torch.Tensor]]:
+    def _op_params(self, device) -> Tuple[List[Tuple[int, int, str]], List[torch.Tensor], List[int]]:
         """(present pairs, the operator's parameter list), cached per set of attention modules (a
         deleted pair changes it) and dropped by every .to() / .cuda() / .float() (_apply), so the
         float32-on-one-device check runs once per cache: an eager step then costs no walk over
@@ -405,12 +408,13 @@ class HybridFusion(nn.Module):
                 if p.device != params[0].device or p.dtype != torch.float32:
                     raise RuntimeError("mmfusion HybridFusion needs float32 parameters on one device "
                                        f"(found {p.dtype} on {p.device})")
-            c = (keys, pairs, params)
+            in_dims = [self.projections[m][0].in_features for m in self.modality_names]
+            c = (keys, pairs, params, in_dims)
             self.__dict__["_mmf_op_params"] = c
         if c[2][0].device != device:
             raise RuntimeError("mmfusion HybridFusion needs float32 parameters on the input's device "
                                f"(found {c[2][0].dtype} on {c[2][0].device})")
-        return c[1], c[2]
+        return c[1], c[2], c[3]
 
     def _grad_sink(self, params: List[torch.Tensor]) -> "_ops.GradSink":
         """The flat gradient buffer the eager backward writes into (mmf_ops.HybridSink)."""
@@ -420,13 +424,20 @@ class HybridFusion(nn.Module):
             self.__dict__["_mmf_grad_sink"] = sk
         return sk
 
-    def mmf_grads_consumed(self) -> None:
-        """A trainer has applied the gradients the parameters' ``.grad`` hold (views of the
-        module's flat gradient buffer): the next backward writes them afresh instead of adding,
-        without the ``.grad`` attributes being reset to None (harness.DPTrainer calls this)."""
+    def mmf_grads_consumed(self) -> bool:
+        """A trainer has applied the gradients the parameters' ``.grad`` hold.  If those are the
+        views of the module's flat gradient buffer (the eager grad-sink path), the next backward
+        writes them afresh instead of adding, with the ``.grad`` attributes left in place: returns
+        True.  Otherwise (a traced backward's outputs, someone else's tensors) returns False and
+        the caller resets ``.grad`` as zero_grad(set_to_none=True) does (harness.DPTrainer)."""
         sk = self.__dict__.get("_mmf_grad_sink")
-        if sk is not None:
-            sk.fresh = True
+        c = self.__dict__.get("_mmf_op_params")
+        if sk is None or c is None or not sk.matches(c[2]):
+            return False
+        if not all(p.grad is v for p, v in zip(c[2], sk.views)):
+            return False
+        sk.fresh = True
+        return True
 
     def _apply(self, fn, *args, **kwargs):
         self.__dict__.pop("_mmf_op_params", None)

@@ -444,7 +444,9 @@ class DPTrainer:
             # attached and mark them consumed -- the next backward writes afresh -- instead of
             # resetting every .grad (one attribute write per parameter and step)
             for m in self._sink_owners:
-                m.mmf_grads_consumed()
+                if not m.mmf_grads_consumed():
+                    for p in m.parameters():
+                        p.grad = None
             for p in self._unsunk:
                 p.grad = None
             self.flat._fresh = [True] * len(self.flat.groups)

@@ -79,11 +79,11 @@ def hybrid_idesc(batch: int, hidden: int, heads: int, classes: int, seq: Sequenc
 
 
 def hybrid_desc(idesc: Sequence[int], dropout: float) -> "_nat.HybridDesc":
-    key = (tuple(int(v) for v in idesc), float(dropout))
+    key = (tuple(idesc), float(dropout))
     d = _HDESC.get(key)
     if d is not None:
         return d
-    v = key[0]
+    v = tuple(int(x) for x in key[0])
     B, M, H, heads, C, training, ret, prec, P = v[:9]
     d = _nat.HybridDesc()
     d.batch, d.num_modalities, d.hidden, d.num_heads, d.num_classes = B, M, H, heads, C
@@ -151,10 +151,12 @@ def _struct_from_ptrs(ptrs: tuple, M: int, P: int) -> "_nat.HybridParams":
 
 
 def hybrid_fwd_impl(idesc: Sequence[int], dropout: float, rng_state: Tensor, mask: Tensor, xs: Sequence[Tensor],
-                    params: Sequence[Tensor]):
+                    params: Sequence[Tensor], rng_inplace: bool = False):
     """mmf_hybrid_forward on the caller's stream -> logits (B, C), fusion_weights (B, M), saved
     (bytes), advanced rng state, attention maps.  (The hybrid_fwd operator's body, and the eager
-    autograd function's: one implementation.)"""
+    autograd functions': one implementation.)  The operator is functional: the library advances a
+    clone of the dropout state, returned; rng_inplace (the eager functions) advances the caller's
+    buffer itself and returns it."""
     L = _nat.lib()
     d = hybrid_desc(idesc, dropout)
     B, M, C, mshapes = _hybrid_meta(idesc)
@@ -163,7 +165,7 @@ def hybrid_fwd_impl(idesc: Sequence[int], dropout: float, rng_state: Tensor, mas
     logits = torch.empty(B, C, dtype=torch.float32, device=dev)
     fw = torch.empty(B, M, dtype=torch.float32, device=dev)
     maps = [torch.empty(s, dtype=torch.float32, device=dev) for s in mshapes]
-    rng_next = rng_state.clone()   # the forward snapshots it into `saved` and advances it
+    rng_next = rng_state if rng_inplace else rng_state.clone()   # snapshot into `saved`, then advanced
     pstruct = _hybrid_params_struct(params, M, d.num_pairs)
     xarr = _nat.ptr_array([x.data_ptr() for x in xs])
     marr = _nat.ptr_array([t.data_ptr() for t in maps]) if maps else None
@@ -302,13 +304,13 @@ class HybridSink(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, idesc, dropout, rng_state, mask, owner, params, anchor, *xs):
-        logits, fw, saved, rng_next, maps = hybrid_fwd_impl(idesc, dropout, rng_state, mask, xs, params)
+        logits, fw, saved, _, maps = hybrid_fwd_impl(idesc, dropout, rng_state, mask, xs, params, rng_inplace=True)
         ctx.set_materialize_grads(False)
         ctx.idesc, ctx.dropout, ctx.owner, ctx.params = idesc, dropout, owner, params
         ctx.need_dx = [bool(n) for n in ctx.needs_input_grad[7:]]
         ctx.save_for_backward(mask, saved, *xs)
-        ctx.mark_non_differentiable(fw, saved, rng_next, *maps)
-        return (logits, fw, saved, rng_next, *maps)
+        ctx.mark_non_differentiable(fw, saved, *maps)
+        return (logits, fw, saved, *maps)
 
     @staticmethod
     def backward(ctx, dlogits, *_unused):
@@ -362,13 +364,13 @@ class HybridEager(torch.autograd.Function):
     @staticmethod
     def forward(ctx, idesc, dropout, rng_state, mask, nx, *tensors):
         xs, params = tensors[:nx], tensors[nx:]
-        logits, fw, saved, rng_next, maps = hybrid_fwd_impl(idesc, dropout, rng_state, mask, xs, params)
+        logits, fw, saved, _, maps = hybrid_fwd_impl(idesc, dropout, rng_state, mask, xs, params, rng_inplace=True)
         ctx.set_materialize_grads(False)
         ctx.idesc, ctx.dropout, ctx.nx = idesc, dropout, nx
         ctx.need_dx = [bool(n) for n in ctx.needs_input_grad[5:5 + nx]]
         ctx.save_for_backward(mask, saved, *xs, *params)
-        ctx.mark_non_differentiable(fw, saved, rng_next, *maps)
-        return (logits, fw, saved, rng_next, *maps)
+        ctx.mark_non_differentiable(fw, saved, *maps)
+        return (logits, fw, saved, *maps)
 
     @staticmethod
     def backward(ctx, dlogits, *_unused):

@@ -70,6 +70,28 @@ def main():
     w = bench.WORKLOADS[args.workload]
     res = {"workload": args.workload}
     for path in args.paths.split(","):
+        try:
+            run_path(args, w, dev, path, res, HybridFusion)
+        except Exception as e:  # noqa: BLE001  (one path failing must not lose the others' numbers)
+            res[path] = {"error": repr(e)[:2000]}
+            print(path, "failed:", repr(e)[:500], flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                json.dump(res, f, indent=1, default=str)
+    try:
+        from torch._dynamo.utils import counters
+        res["inductor_counters"] = {k: dict(v) for k, v in counters.items() if v}
+    except Exception as e:  # noqa: BLE001
+        res["inductor_counters"] = repr(e)
+    txt = json.dumps(res, indent=1, default=str)
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(txt)
+    print(txt)
+
+
+def run_path(args, w, dev, path, res, HybridFusion):
+    if True:
         torch.manual_seed(0)
         names = [f"m{i}" for i in range(w["M"])]
         model = HybridFusion({n: w["D"] for n in names}, hidden_dim=w["H"], num_classes=w["C"],
@@ -90,16 +112,6 @@ def main():
         res[path + "_top_self_cpu_us_per_step"] = [
             (e.key, round(e.self_cpu_time_total / 10, 1), round(e.count / 10, 2)) for e in top]
         print(path, json.dumps(res[path]), flush=True)
-    try:
-        from torch._dynamo.utils import counters
-        res["inductor_counters"] = {k: dict(v) for k, v in counters.items() if v}
-    except Exception as e:  # noqa: BLE001
-        res["inductor_counters"] = repr(e)
-    txt = json.dumps(res, indent=1, default=str)
-    if args.out:
-        with open(args.out, "w") as f:
-            f.write(txt)
-    print(txt)
 
 
 if __name__ == "__main__":
