@@ -99,7 +99,18 @@ def hybrid_desc(idesc: Sequence[int], dropout: float) -> "_nat.HybridDesc":
     return d
 
 
+_HMETA: Dict[tuple, tuple] = {}
+
+
 def _hybrid_meta(idesc: Sequence[int]):
+    key = tuple(idesc)
+    hit = _HMETA.get(key)
+    if hit is None:
+        hit = _HMETA[key] = _hybrid_meta_of(key)
+    return hit
+
+
+def _hybrid_meta_of(idesc: Sequence[int]):
     v = [int(x) for x in idesc]
     B, M, H, heads, C, _, ret, _, P = v[:9]
     seq = [max(s, 1) for s in v[9:9 + M]]
@@ -115,7 +126,7 @@ def _hybrid_params_struct(params: Sequence[Tensor], M: int, P: int) -> "_nat.Hyb
     """The C-ABI parameter (or gradient) struct for these tensors' addresses, cached per address
     set (a training loop passes the same parameters every step; gradient buffers recur through
     the caching allocator)."""
-    return _struct_from_ptrs(tuple(t.data_ptr() for t in params), M, P)
+    return _struct_from_ptrs(tuple(map(Tensor.data_ptr, params)), M, P)
 
 
 def _grad_struct(flat: Tensor, offsets: Sequence[int], M: int, P: int) -> "_nat.HybridParams":
@@ -286,10 +297,11 @@ def _sink_ok(params: Sequence[Tensor]) -> bool:
     contiguous fp32 (the layout), and none with a tensor hook (register_hook can rewrite a
     gradient before accumulation: those parameters go through autograd's AccumulateGrad).
     Post-accumulate-grad hooks are called by the sink path itself, after the gradient lands."""
-    for p in params:
-        if not p.requires_grad or p._backward_hooks:
-            return False
-    return True
+    return all(map(_TRAINABLE, params)) and not any(map(_TENSOR_HOOKS, params))
+
+
+_TRAINABLE = Tensor.requires_grad.__get__
+_TENSOR_HOOKS = Tensor._backward_hooks.__get__
 
 
 class HybridSink(torch.autograd.Function):
