@@ -114,17 +114,16 @@ __device__ __forceinline__ float ld_wt(const float* p) {
 
 // (tile, pair) of this workgroup (one place, so a different layout of the grid changes one
 // function).  Workgroups are dealt to the 8 XCDs round-robin in dispatch order (x fastest), so with
-// the plain (tile, pair) = (blockIdx.x, blockIdx.y) every XCD holds tiles of EVERY pair and fetches
-// every pair's W_k / W_v / W_o into its own L2: 8 copies of ~1.1 MB of weights per launch at C2, the
-// 2x of the measured HBM traffic over the algorithmic bytes (profiles/pmc_traffic_c2_l1_highest.json:
-// 18.1 vs 9.25 MB).  XCD-major instead (the grid a multiple of 8, two-dimensional): the workgroup
-// with dispatch index l is work item w = (l % 8) (N / 8) + l / 8 -- consecutive work items, i.e. the
-// tiles of one or two pairs, on one XCD -- so each XCD fetches at most two pairs' weights.  (Measured
-// in round 4 as time-neutral, 0.0699 / 0.0697 vs 0.0700 / 0.0706 ms, scripts/gpu_l1ab.sh,
-// profiles/r04/l1/ab_xcd/; round 5 adopts it for the traffic.)  MMF_L1_LINEAR_IDS: the plain layout
-// (the A/B build, `make l1lin`).
+// the plain (tile, pair) = (blockIdx.x, blockIdx.y) and a tile count that is a multiple of 8 all the
+// pair workgroups of one tile sit on ONE XCD (the tile's hand-off stays in that XCD's L2), and every
+// XCD fetches every pair's W_k / W_v / W_o into its own L2: 8 copies of ~1.1 MB of weights per
+// launch at C2 (profiles/pmc_traffic_c2_l1_highest.json: 18.1 vs 9.25 MB algorithmic).
+// MMF_L1_XCD_IDS (`make l1xcd`) deals work item w = (l % 8) (N / 8) + l / 8 to dispatch index l
+// instead -- the tiles of one or two pairs on one XCD, so each XCD fetches at most two pairs'
+// weights: 13.3 MB instead of 18.1 MB per fused-step launch, but 43.9 / 44.1 us instead of 42.2 /
+// 42.0 us (round 5, profiles/r05/l1_xcd_ab/): the hand-offs then cross XCDs.  The plain layout stays.
 __device__ __forceinline__ void l1_ids(int& tile, int& pair) {
-#ifndef MMF_L1_LINEAR_IDS
+#ifdef MMF_L1_XCD_IDS
   const unsigned T = gridDim.x, N = gridDim.x * gridDim.y;
   if (gridDim.y > 1 && (N & 7u) == 0) {
     const unsigned l = blockIdx.x + T * blockIdx.y;
