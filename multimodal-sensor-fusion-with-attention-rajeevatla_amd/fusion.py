@@ -379,8 +379,16 @@ class HybridFusion(nn.Module):
             # eager: the parameters' gradients written straight into the module's flat gradient
             # buffer (mmf_ops.HybridSink: no per-parameter autograd work); params[0] anchors the
             # graph; the library advances the dropout state in the module's buffer itself
-            logits, fw, _saved, *maps = _ops.HybridSink.apply(
-                idesc, float(self.dropout.p), self._rng_state, _nat.f32c(modality_mask), self, params, params[0], *xs)
+            ext = _ops.torch_ext()
+            if ext is not None:
+                # (the same in C++: mmf_torch's node, no Python in the backward)
+                logits, fw, *maps = ext.hybrid_sink_forward(
+                    self._grad_sink(params, len(pairs)), ctypes.addressof(_ops.hybrid_desc(idesc, float(self.dropout.p))),
+                    self._rng_state, _nat.f32c(modality_mask), xs)
+            else:
+                logits, fw, _saved, *maps = _ops.HybridSink.apply(
+                    idesc, float(self.dropout.p), self._rng_state, _nat.f32c(modality_mask), self, params, params[0],
+                    *xs)
         else:
             # eager, some parameter frozen or hooked: the same implementation with every parameter an
             # autograd input (mmf_ops.HybridEager)
@@ -416,11 +424,13 @@ class HybridFusion(nn.Module):
                                f"(found {c[2][0].dtype} on {c[2][0].device})")
         return c[1], c[2], c[3]
 
-    def _grad_sink(self, params: List[torch.Tensor]) -> "_ops.GradSink":
-        """The flat gradient buffer the eager backward writes into (mmf_ops.HybridSink)."""
+    def _grad_sink(self, params: List[torch.Tensor], num_pairs: Optional[int] = None):
+        """The flat gradient buffer the eager backward writes into (mmf_ops.make_grad_sink: the C++
+        node's or mmf_ops.HybridSink's)."""
         sk = self.__dict__.get("_mmf_grad_sink")
         if sk is None or not sk.matches(params):
-            sk = _ops.GradSink(params)
+            P = len(self.present_pairs()) if num_pairs is None else num_pairs
+            sk = _ops.make_grad_sink(params, self.num_modalities, P)
             self.__dict__["_mmf_grad_sink"] = sk
         return sk
 
@@ -434,6 +444,8 @@ class HybridFusion(nn.Module):
         c = self.__dict__.get("_mmf_op_params")
         if sk is None or c is None or not sk.matches(c[2]):
             return False
+        if not isinstance(sk, _ops.GradSink):
+            return sk.consumed()   # (mmf_torch.Sink: the same check in C++)
         if not all(p.grad is v for p, v in zip(c[2], sk.views)):
             return False
         sk.fresh = True

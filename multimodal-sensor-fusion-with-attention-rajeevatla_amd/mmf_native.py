@@ -244,7 +244,13 @@ def require_device(t: torch.Tensor, what: str) -> None:
             "kernels on a ROCm device (MI355X). Move the module and inputs to 'cuda'.")
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_ptr(device: torch.device) -> int:
+    """The current HIP stream of `device` (torch's raw-handle accessor: no Stream object per call)."""
+    if _RAW_STREAM is not None and device.index is not None:
+        return _RAW_STREAM(device.index)
     return torch.cuda.current_stream(device).cuda_stream
 
 

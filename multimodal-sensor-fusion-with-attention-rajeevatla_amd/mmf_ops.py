@@ -31,7 +31,7 @@ from __future__ import annotations
 import ctypes
 import os
 import sys
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import torch
 from torch import Tensor
@@ -290,6 +290,41 @@ class GradSink:
 
     def matches(self, params: Sequence[Tensor]) -> bool:
         return len(params) == len(self.views) and params[0].device == self.flat.device
+
+
+_EXT: Any = False   # mmf_torch once loaded and bound; None when not built or MMF_NO_TORCH_EXT is set
+
+
+def torch_ext():
+    """The mmf_torch extension (csrc/torch_bind.cpp: HybridFusion's and the cross-entropy's eager
+    autograd nodes in C++ over this library's C-ABI), bound to the entry points of the library
+    mmf_native loaded; None when it is not built (mmf_build.build_torch_ext) or MMF_NO_TORCH_EXT=1
+    -- then the Python twins (HybridSink, CrossEntropyEager) run the same entry points."""
+    global _EXT
+    if _EXT is False:
+        ext = None
+        if not os.environ.get("MMF_NO_TORCH_EXT"):
+            try:
+                import mmf_torch as ext
+            except ImportError:
+                ext = None
+        if ext is not None:
+            L = _nat.lib()
+            ext.bind({n: ctypes.cast(getattr(L, n), ctypes.c_void_p).value
+                      for n in ("mmf_hybrid_saved_bytes", "mmf_hybrid_workspace_bytes", "mmf_hybrid_forward",
+                                "mmf_hybrid_backward", "mmf_cross_entropy_ls", "mmf_last_error")})
+        _EXT = ext
+    return _EXT
+
+
+def make_grad_sink(params: Sequence[Tensor], M: int, P: int):
+    """The module's flat gradient buffer: mmf_torch.Sink (the C++ node writes into it) when the
+    extension is loaded, GradSink otherwise -- one layout (flat_offsets), the same attributes."""
+    ext = torch_ext()
+    if ext is None:
+        return GradSink(params)
+    offsets, nelem = flat_offsets([p.numel() for p in params])
+    return ext.Sink(list(params), offsets, nelem, M, P)
 
 
 def _sink_ok(params: Sequence[Tensor]) -> bool:
@@ -856,5 +891,8 @@ def cross_entropy(logits: Tensor, labels: Tensor, label_smoothing: float = 0.0, 
         import torch.nn.functional as F
         return F.cross_entropy(logits, labels, label_smoothing=label_smoothing, ignore_index=ignore_index)
     if eager_tensor(logits):
+        ext = torch_ext()
+        if ext is not None:
+            return ext.cross_entropy(logits.contiguous(), labels.contiguous(), float(label_smoothing))
         return CrossEntropyEager.apply(logits.contiguous(), labels.contiguous(), float(label_smoothing))
     return torch.ops.mmfusion.cross_entropy_ls_fwd(logits.contiguous(), labels.contiguous(), float(label_smoothing))[0]
