@@ -33,6 +33,7 @@ configs that train encoders (C3 PAMAP2, C4 MHAD), one process per GPU:
 from __future__ import annotations
 
 import math
+import operator
 import os
 import sys
 from typing import Any, Dict, List, Optional, Sequence
@@ -158,6 +159,9 @@ class MultimodalFusionModel(nn.Module):
 
 
 # ----------------------------------------------------------------------------- flat buffers + bucketed all-reduce
+_GRAD = torch.Tensor.grad.__get__   # (p.grad as a C-level callable: map() over parameters)
+
+
 class FlatGradBuckets:
     """All parameters of `modules` in one flat fp32 buffer and their gradients in a second
     one, exchanged in buckets.
@@ -274,7 +278,7 @@ class FlatGradBuckets:
             return None
         params, views = self.groups[0], self._gviews[0]
         last = self._direct_last
-        if last is not None and all(p.grad is g for p, g in zip(params, last[0])):
+        if last is not None and all(map(operator.is_, map(_GRAD, params), last[0])):
             return last[1]   # the same gradient tensors as the last validated step (a grad sink)
         g0 = params[0].grad
         if g0 is None or g0.dtype != torch.float32 or g0.device != self.grad.device:
