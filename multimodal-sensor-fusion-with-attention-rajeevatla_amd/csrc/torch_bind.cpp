@@ -177,7 +177,7 @@ struct HybridSinkBackward : public Node {
 
   variable_list apply(variable_list&& grads) override {
     const size_t nx = xs_.size();
-    variable_list out(nx + 1);
+    variable_list out(nx);
     if (grads.empty() || !grads[0].defined()) return out;
     if (!saved_.defined())
       throw std::runtime_error(
@@ -284,11 +284,10 @@ std::vector<at::Tensor> hybrid_sink_forward(const std::shared_ptr<Sink>& sink, u
                   d.return_attention ? mp : nullptr, stream_of(mask)),
         "HybridFusion forward");
   if (at::GradMode::is_enabled()) {
-    // the modality inputs and one anchor parameter (so a graph exists when no input requires grad)
+    // edges to the modality inputs only: the parameters are outside the graph (the node writes
+    // their gradients itself), and logits has this node as grad_fn even when no input requires grad
     auto node = std::shared_ptr<HybridSinkBackward>(new HybridSinkBackward(), torch::autograd::deleteNode);
-    variable_list inputs(xs.begin(), xs.end());
-    inputs.push_back(s.params[0]);
-    node->set_next_edges(torch::autograd::collect_next_edges(inputs));
+    node->set_next_edges(torch::autograd::collect_next_edges(xs));
     node->sink = sink;
     node->desc = d;
     node->mask_ = SavedVariable(mask, false);

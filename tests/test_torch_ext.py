@@ -41,8 +41,9 @@ class Stubs:
     """C-callable stand-ins for the entry points the nodes call; they record calls and write
     grad_value into every parameter gradient, dx_value into every requested dx."""
 
-    def __init__(self, numels, M, P):
+    def __init__(self, numels, M, P, light=False):
         self.numels, self.M, self.P = numels, M, P
+        self.light = light   # (host-cost models: record calls only, write nothing)
         self.grad_value, self.dx_value = 1.0, 2.0
         self.fwd_calls = self.bwd_calls = 0
         self.last_dlogits = None
@@ -53,6 +54,8 @@ class Stubs:
 
         def fwd(d, W, x, mask, rng, saved, logits, fw, maps, stream):
             self.fwd_calls += 1
+            if self.light:
+                return 0
             desc = ctypes.cast(d, ctypes.POINTER(nat.HybridDesc)).contents
             n = desc.batch * desc.num_classes
             (ctypes.c_float * n).from_address(logits)[:] = [0.5] * n
@@ -60,6 +63,8 @@ class Stubs:
 
         def bwd(d, W, x, mask, saved, dlogits, ws, G, dx, stream):
             self.bwd_calls += 1
+            if self.light:
+                return 0
             desc = ctypes.cast(d, ctypes.POINTER(nat.HybridDesc)).contents
             n = desc.batch * desc.num_classes
             self.last_dlogits = list((ctypes.c_float * n).from_address(dlogits))
@@ -214,3 +219,13 @@ def test_library_error_surfaces(ext):
     with pytest.raises(RuntimeError, match=r"HybridFusion forward failed \(code 2\): stub"):
         fwd()
     ext.bind(st.addrs)
+
+
+def test_no_input_requires_grad_still_trains_parameters(ext):
+    model, params, sink, st, xs, fwd, labels = _setup(ext, need_x=(False, False, False))
+    model.zero_grad(set_to_none=True)
+    logits = fwd()[0]
+    assert logits.requires_grad and logits.grad_fn.name() == "HybridSinkBackward"
+    ext.cross_entropy(logits, labels, 0.05).backward()
+    assert st.bwd_calls == 1 and all(torch.all(p.grad == 1.0) for p in params)
+    assert all(x.grad is None for x in xs)
