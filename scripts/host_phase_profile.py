@@ -64,6 +64,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--out", default=None)
     ap.add_argument("--paths", default="module,compiled,compiled_traceable")
+    ap.add_argument("--trace", default=None, help="directory: write each path's 10-step CPU chrome trace there")
     args = ap.parse_args()
     from fusion import HybridFusion
     dev = torch.device("cuda", 0)
@@ -107,6 +108,9 @@ def run_path(args, w, dev, path, res, HybridFusion):
             for _ in range(10):
                 r.step()
             torch.cuda.synchronize()
+        if args.trace:
+            os.makedirs(args.trace, exist_ok=True)
+            prof.export_chrome_trace(os.path.join(args.trace, path + ".json"))
         ka = prof.key_averages()
         top = sorted(ka, key=lambda e: -e.self_cpu_time_total)[:25]
         res[path + "_top_self_cpu_us_per_step"] = [

@@ -27,6 +27,8 @@ def _run(ext_on, seq, steps=3):
         torch.manual_seed(0)
         dims = {"a": 24, "b": 32, "c": 16}
         model = HybridFusion(dims, hidden_dim=64, num_classes=5, num_heads=4, dropout=0.1).cuda()
+        # (the dropout stream's seed counts module constructions: pin it so both runs draw alike)
+        model._rng_state.copy_(torch.tensor([0x5EED1234, 0], dtype=torch.int64))
         B = 16
         g = torch.Generator().manual_seed(1)
         shape = (lambda d: (B, seq, d)) if seq else (lambda d: (B, d))
