@@ -145,6 +145,17 @@ struct Sink {
     return g;
   }
 
+  // the node keeps autograd's semantics for these parameters: every one trainable and none with a
+  // tensor hook (register_hook can rewrite a gradient before accumulation: those modules go through
+  // the per-parameter path, mmf_ops.HybridEager); post-accumulate hooks the node calls itself.
+  // Conservative: a parameter whose hooks were all removed keeps an empty hook wrapper here, so
+  // false sends the caller to the exact Python check (mmf_ops._sink_ok)
+  bool ok() const {
+    for (const auto& p : params)
+      if (!p.requires_grad() || !torch::autograd::impl::hooks(p).empty()) return false;
+    return true;
+  }
+
   bool matches(const std::vector<at::Tensor>& ps) const {
     return ps.size() == params.size() && ps[0].device() == flat.device();
   }
@@ -345,6 +356,7 @@ PYBIND11_MODULE(mmf_torch, m) {
       .def_readonly("nelem", &Sink::nelem)
       .def_readwrite("fresh", &Sink::fresh)
       .def("matches", &Sink::matches)
+      .def("ok", &Sink::ok)
       .def("consumed", &Sink::consumed);
   m.def("hybrid_sink_forward", &hybrid_sink_forward);
   m.def("cross_entropy", &cross_entropy);

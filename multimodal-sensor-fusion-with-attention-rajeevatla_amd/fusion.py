@@ -49,6 +49,8 @@ import mmf_native as _nat  # noqa: E402
 import mmf_ops as _ops  # noqa: E402
 from attention import CrossModalAttention, _new_rng_state, _precision  # noqa: E402
 
+_SHAPE = torch.Tensor.shape.__get__   # (x.shape as a C-level callable: map() over the inputs)
+
 
 # --------------------------------------------------------------------------
 # Early fusion (plumbing, torch) and Late fusion (torch classifiers + HIP weighting).
@@ -364,7 +366,25 @@ class HybridFusion(nn.Module):
             named = dict(self.named_parameters())
             params = [named[n] for n in self._param_names(pairs)]
         else:
-            pairs, params, in_dims = self._op_params(device)
+            pairs, params, in_dims, descs = self._op_params(device)
+            ext = _ops.torch_ext()
+            if ext is not None:
+                # eager through mmf_torch's C++ node: the shape checks and the descriptor once per input
+                # signature; the parameters' gradients written straight into the module's flat gradient
+                # buffer (no per-parameter autograd work), the dropout state advanced in place
+                key = (tuple(map(_SHAPE, feats)), self.training, return_attention, _precision(), self.dropout.p)
+                addr = descs.get(key)
+                if addr is None:
+                    seq, dims = self._shapes(feats, in_dims)
+                    idesc = _ops.hybrid_idesc(batch_size, self.hidden_dim, self.num_heads, self.num_classes, seq, dims,
+                                              [(q, k) for q, k, _ in pairs], self.training, return_attention,
+                                              _precision())
+                    addr = descs[key] = ctypes.addressof(_ops.hybrid_desc(idesc, float(self.dropout.p)))
+                sink = self._grad_sink(params, len(pairs))
+                if not torch.is_grad_enabled() or sink.ok() or _ops._sink_ok(params):
+                    logits, fw, *maps = ext.hybrid_sink_forward(sink, addr, self._rng_state, _nat.f32c(modality_mask),
+                                                                [_nat.f32c(x) for x in feats])
+                    return self._finish(logits, fw, maps, pairs, dtype, return_attention)
             seq, dims = self._shapes(feats, in_dims)
         idesc = _ops.hybrid_idesc(batch_size, self.hidden_dim, self.num_heads, self.num_classes, seq, dims,
                                   [(q, k) for q, k, _ in pairs], self.training, return_attention, _precision())
@@ -376,24 +396,19 @@ class HybridFusion(nn.Module):
                 idesc, float(self.dropout.p), self._rng_state, _nat.f32c(modality_mask), xs, params)
             self._rng_state.copy_(rng_next)     # the device Philox stream advanced by one call
         elif torch.is_grad_enabled() and _ops._sink_ok(params):
-            # eager: the parameters' gradients written straight into the module's flat gradient
-            # buffer (mmf_ops.HybridSink: no per-parameter autograd work); params[0] anchors the
-            # graph; the library advances the dropout state in the module's buffer itself
-            ext = _ops.torch_ext()
-            if ext is not None:
-                # (the same in C++: mmf_torch's node, no Python in the backward)
-                logits, fw, *maps = ext.hybrid_sink_forward(
-                    self._grad_sink(params, len(pairs)), ctypes.addressof(_ops.hybrid_desc(idesc, float(self.dropout.p))),
-                    self._rng_state, _nat.f32c(modality_mask), xs)
-            else:
-                logits, fw, _saved, *maps = _ops.HybridSink.apply(
-                    idesc, float(self.dropout.p), self._rng_state, _nat.f32c(modality_mask), self, params, params[0],
-                    *xs)
+            # eager without the C++ extension: the Python twin of its node (mmf_ops.HybridSink);
+            # params[0] anchors the graph
+            logits, fw, _saved, *maps = _ops.HybridSink.apply(
+                idesc, float(self.dropout.p), self._rng_state, _nat.f32c(modality_mask), self, params, params[0], *xs)
         else:
             # eager, some parameter frozen or hooked: the same implementation with every parameter an
             # autograd input (mmf_ops.HybridEager)
             logits, fw, _saved, *maps = _ops.HybridEager.apply(
                 idesc, float(self.dropout.p), self._rng_state, _nat.f32c(modality_mask), len(xs), *xs, *params)
+        return self._finish(logits, fw, maps, pairs, dtype, return_attention)
+
+    @staticmethod
+    def _finish(logits, fw, maps, pairs, dtype, return_attention):
         if dtype != torch.float32 and dtype.is_floating_point:
             logits = logits.to(dtype)
         if return_attention:
@@ -401,11 +416,12 @@ class HybridFusion(nn.Module):
             return logits, {"attention_maps": attention_maps, "fusion_weights": fw.detach()}
         return logits
 
-    def _op_params(self, device) -> Tuple[List[Tuple[int, int, str]], List[torch.Tensor], List[int]]:
-        """(present pairs, the operator's parameter list), cached per set of attention modules (a
-        deleted pair changes it) and dropped by every .to() / .cuda() / .float() (_apply), so the
-        float32-on-one-device check runs once per cache: an eager step then costs no walk over
-        the module tree."""
+    def _op_params(self, device) -> Tuple[List[Tuple[int, int, str]], List[torch.Tensor], List[int], Dict[tuple, int]]:
+        """(present pairs, the operator's parameter list, the modalities' input widths, the eager
+        path's descriptor cache: input signature -> mmf_hybrid_desc address), cached per set of
+        attention modules (a deleted pair changes it) and dropped by every .to() / .cuda() /
+        .float() (_apply), so the float32-on-one-device check runs once per cache: an eager step
+        then costs no walk over the module tree."""
         keys = tuple(self.attention_modules.keys())
         c = self.__dict__.get("_mmf_op_params")
         if c is None or c[0] != keys:
@@ -417,18 +433,18 @@ class HybridFusion(nn.Module):
                     raise RuntimeError("mmfusion HybridFusion needs float32 parameters on one device "
                                        f"(found {p.dtype} on {p.device})")
             in_dims = [self.projections[m][0].in_features for m in self.modality_names]
-            c = (keys, pairs, params, in_dims)
+            c = (keys, pairs, params, in_dims, {})
             self.__dict__["_mmf_op_params"] = c
         if c[2][0].device != device:
             raise RuntimeError("mmfusion HybridFusion needs float32 parameters on the input's device "
                                f"(found {c[2][0].dtype} on {c[2][0].device})")
-        return c[1], c[2], c[3]
+        return c[1], c[2], c[3], c[4]
 
     def _grad_sink(self, params: List[torch.Tensor], num_pairs: Optional[int] = None):
         """The flat gradient buffer the eager backward writes into (mmf_ops.make_grad_sink: the C++
         node's or mmf_ops.HybridSink's)."""
         sk = self.__dict__.get("_mmf_grad_sink")
-        if sk is None or not sk.matches(params):
+        if sk is None or not sk.matches(params) or isinstance(sk, _ops.GradSink) != (_ops.torch_ext() is None):
             P = len(self.present_pairs()) if num_pairs is None else num_pairs
             sk = _ops.make_grad_sink(params, self.num_modalities, P)
             self.__dict__["_mmf_grad_sink"] = sk

@@ -107,7 +107,7 @@ def _setup(ext, need_x=(True, False, True)):
     torch.manual_seed(0)
     dims = {"a": 6, "b": 5, "c": 4}
     model = HybridFusion(dims, hidden_dim=8, num_classes=3, num_heads=2, dropout=0.1)
-    pairs, params, in_dims = model._op_params(torch.device("cpu"))
+    pairs, params, in_dims, _ = model._op_params(torch.device("cpu"))
     M, P = 3, len(pairs)
     st = Stubs([p.numel() for p in params], M, P)
     ext.bind(st.addrs)
@@ -229,3 +229,45 @@ def test_no_input_requires_grad_still_trains_parameters(ext):
     ext.cross_entropy(logits, labels, 0.05).backward()
     assert st.bwd_calls == 1 and all(torch.all(p.grad == 1.0) for p in params)
     assert all(x.grad is None for x in xs)
+
+
+def test_sink_ok_sees_frozen_and_hooked_parameters(ext):
+    model, params, sink, *_ = _setup(ext)
+    assert sink.ok()
+    params[3].requires_grad_(False)
+    assert not sink.ok()
+    params[3].requires_grad_(True)
+    h = params[7].register_hook(lambda g: g * 2)
+    assert not sink.ok()
+    assert not mmf_ops._sink_ok(params)
+    h.remove()
+    # (the removed hook leaves an empty wrapper: ok() is conservative, the Python check exact)
+    assert mmf_ops._sink_ok(params)
+
+
+def test_module_forward_uses_node_and_caches_descriptors(ext, monkeypatch):
+    """HybridFusion.forward's eager branch on host tensors with the stub entry points: the C++ node,
+    one descriptor per input signature, and the parameters' .grad as the sink's views."""
+    torch.manual_seed(0)
+    dims = {"a": 6, "b": 5, "c": 4}
+    model = HybridFusion(dims, hidden_dim=8, num_classes=3, num_heads=2, dropout=0.1)
+    pairs, params, in_dims, descs = model._op_params(torch.device("cpu"))
+    st = Stubs([p.numel() for p in params], 3, len(pairs))
+    ext.bind(st.addrs)
+    monkeypatch.setattr(mmf_ops, "_EXT", ext)
+    monkeypatch.setattr(nat, "require_device", lambda t, what: None)
+    monkeypatch.setattr(mmf_ops, "eager_tensor", lambda t: type(t) in (torch.Tensor, torch.nn.Parameter))
+    feats = {k: torch.randn(4, d, requires_grad=True) for k, d in dims.items()}
+    mask = torch.ones(4, 3)
+    for _ in range(2):
+        logits = model(feats, mask)
+    assert logits.grad_fn.name() == "HybridSinkBackward" and len(descs) == 1
+    model({k: v[:2] for k, v in feats.items()}, mask[:2])
+    model.eval()
+    model(feats, mask)
+    assert len(descs) == 3
+    model.train()
+    ext.cross_entropy(model(feats, mask), torch.zeros(4, dtype=torch.long), 0.05).backward()
+    sink = model._grad_sink(params)
+    assert all(p.grad is v for p, v in zip(params, sink.views)) and torch.all(feats["a"].grad == 2.0)
+    assert model.mmf_grads_consumed() and sink.fresh
