@@ -360,6 +360,18 @@ int mmf_clip_adamw_apply_dev(int64_t n, float* param, const float* grad, float* 
  * mmf_cross_entropy_ls's grad_scale does). */
 int mmf_grad_accumulate(int64_t n, const float* src, float* dst, void* stream);
 
+/* The bf16-operand GEMM forms of the "medium" plans, for tests and diagnostics:
+ * C (M x N fp32, ldc) = sum over k of A(m, k) B(n, k), with A stored [m][k] (a_kmajor = 0, lda)
+ * or [k][m] (a_kmajor = 1), B likewise; bf16 (__bf16) operands, 16-byte aligned, lda / ldb
+ * multiples of 8; fp32 accumulation.  Forms: (0, 0), (1, 1) and (0, 1) -- the Q/K projections,
+ * the weight gradients, dZ.  nsplit > 1 (k-major A): split-K slabs in `workspace`
+ * (mmf_gemm_bf16_workspace_bytes) reduced in a fixed order; bias_grad (k-major A, may be NULL):
+ * also write the row sums of A over k (a weight gradient's bias gradient). */
+size_t mmf_gemm_bf16_workspace_bytes(int32_t M, int32_t N, int32_t K, int32_t nsplit);
+int mmf_gemm_bf16(int32_t M, int32_t N, int32_t K, const void* A, int32_t lda, int32_t a_kmajor, const void* B,
+                  int32_t ldb, int32_t b_kmajor, float* C, int32_t ldc, void* workspace, int32_t nsplit,
+                  float* bias_grad, void* stream);
+
 /* Global-norm gradient clipping (torch.nn.utils.clip_grad_norm_(max_norm,
  * norm_type=2) as Lightning applies gradient_clip_val, src/train.py:416-430,
  * config/base.yaml:74 gradient_clip_norm): over the flat gradient scaled by

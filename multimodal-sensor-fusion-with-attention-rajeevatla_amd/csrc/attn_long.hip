@@ -146,11 +146,23 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
   const int64_t q_off = (int64_t)b * Lq * P.ldq + col0, k_off = (int64_t)b * Lk * P.ldk + col0;   // elements
   float* dQg = P.dq + (int64_t)b * Lq * P.ldq + col0;
   float* dKg = P.dk + (int64_t)b * Lk * P.ldk + col0;
+  // bf16 dQ / dK (AttnPair::dqk_bf16): the same element offsets, 2-byte elements
+  const bool dqb = P.dqk_bf16 != 0;
+  __bf16* dQh = reinterpret_cast<__bf16*>(P.dq) + (int64_t)b * Lq * P.ldq + col0;
+  __bf16* dKh = reinterpret_cast<__bf16*>(P.dk) + (int64_t)b * Lk * P.ldk + col0;
 
   if (P.kmask_mode == 1 && P.kmask[(int64_t)b * P.kmask_ld] == 0.f) {
     // masked key modality: every probability is 0 (src/attention.py:127-129), so are dQ, dK, D
-    for (int i = t; i < Lq * hd; i += LF_NT) dQg[(int64_t)(i / hd) * P.ldq + i % hd] = 0.f;
-    for (int i = t; i < Lk * hd; i += LF_NT) dKg[(int64_t)(i / hd) * P.ldk + i % hd] = 0.f;
+    for (int i = t; i < Lq * hd; i += LF_NT) {
+      const int64_t o = (int64_t)(i / hd) * P.ldq + i % hd;
+      if (dqb) dQh[o] = (__bf16)0.f;
+      else dQg[o] = 0.f;
+    }
+    for (int i = t; i < Lk * hd; i += LF_NT) {
+      const int64_t o = (int64_t)(i / hd) * P.ldk + i % hd;
+      if (dqb) dKh[o] = (__bf16)0.f;
+      else dKg[o] = 0.f;
+    }
     for (int i = t; i < Lq; i += LF_NT) P.dsum[bh * Lq + i] = 0.f;
     return;
   }
@@ -374,7 +386,10 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int qq = qbase + 4 * j + e;
-          if (qq < Lq) dQg[(int64_t)qq * P.ldq + d] = av[e] * scale;
+          if (qq < Lq) {
+            if (dqb) dQh[(int64_t)qq * P.ldq + d] = (__bf16)(av[e] * scale);
+            else dQg[(int64_t)qq * P.ldq + d] = av[e] * scale;
+          }
         }
       }
     }
@@ -390,7 +405,11 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
       const int d = 32 * dt + r;
       if (d >= hd) continue;
 #pragma unroll
-      for (int e = 0; e < 16; ++e) dKg[(int64_t)(kt * 32 + acc_row(e, hh)) * P.ldk + d] = dk[i][dt][e] * scale;
+      for (int e = 0; e < 16; ++e) {
+        const int64_t o = (int64_t)(kt * 32 + acc_row(e, hh)) * P.ldk + d;
+        if (dqb) dKh[o] = (__bf16)(dk[i][dt][e] * scale);
+        else dKg[o] = dk[i][dt][e] * scale;
+      }
     }
   }
 }
@@ -649,6 +668,7 @@ bool attn_long_fused_ok(const AttnPair* pairs, int npairs, int hd, float drop_p)
     if (P.Lk <= 128 || P.Lk > LF_MAXK || P.Lk % 32 != 0 || P.Lq < 1 || P.kmask_mode == 2) return false;
     if (P.ldq % 4 != 0 || P.ldk % 4 != 0 || ((uintptr_t)P.q & 15) != 0 || ((uintptr_t)P.k & 15) != 0) return false;
     if (P.qk_bf16 && (hd % 8 != 0 || P.ldq % 8 != 0 || P.ldk % 8 != 0)) return false;
+    if (P.dqk_bf16 && !P.qk_bf16) return false;
     if (!P.dq || !P.dk || !P.dsum || !P.dpbar || !P.lse) return false;
     if (drop_p > 0.f && (!P.keep_bits || P.kw_ld < P.Lk / 32)) return false;
   }
@@ -783,9 +803,10 @@ hipError_t launch_attn_long_fused_bwd(const AttnPair* pairs, int npairs, int B, 
         a.p[n] = ps[done++];
         const double lq = a.p[n].Lq, lk = a.p[n].Lk, H = (double)heads * hd;
         const double esz = a.p[n].qk_bf16 ? 2.0 : 4.0;   // Q / K as stored (bf16 at "medium", §4.4)
+        const double gsz = a.p[n].dqk_bf16 ? 2.0 : 4.0;  // dQ / dK as stored
         fl += 2.0 * (2.0 * B * lq * lk * H);          // dQ and dK contractions (S recompute not counted)
-        // Q, K in (as stored); dQ, dK out (fp32); the keep words in; lse, dpbar, D sums in (small)
-        by += esz * (B * lq * H + B * lk * H) + 4.0 * (B * lq * H + B * lk * H) +
+        // Q, K in (as stored); dQ, dK out (as stored); the keep words in; lse, dpbar, D sums in (small)
+        by += esz * (B * lq * H + B * lk * H) + gsz * (B * lq * H + B * lk * H) +
               (bits ? 4.0 * B * heads * lq * (lk / 32) : 0.0) + 4.0 * B * heads * (2.0 * lq + lk);
         ++n;
       }

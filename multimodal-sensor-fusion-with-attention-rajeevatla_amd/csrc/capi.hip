@@ -555,6 +555,42 @@ int mmf_grad_accumulate(int64_t n, const float* src, float* dst, void* stream) {
   return MMF_OK;
 }
 
+size_t mmf_gemm_bf16_workspace_bytes(int32_t M, int32_t N, int32_t K, int32_t nsplit) {
+  if (M < 1 || N < 1 || K < 1 || nsplit < 1) return 0;
+  int ns = nsplit, kchunk = 0;
+  split_rows(K, ns, kchunk, nsplit);
+  return ((((size_t)ns * M * N * 4) + 255) & ~size_t(255)) + ((((size_t)ns * M * 4) + 255) & ~size_t(255)) + 256;
+}
+
+int mmf_gemm_bf16(int32_t M, int32_t N, int32_t K, const void* A, int32_t lda, int32_t a_kmajor, const void* B,
+                  int32_t ldb, int32_t b_kmajor, float* C, int32_t ldc, void* workspace, int32_t nsplit,
+                  float* bias_grad, void* stream) {
+  if (M < 1 || N < 1 || K < 1 || !A || !B || !C || ldc < N || nsplit < 1)
+    return fail(MMF_EINVAL, "bad bf16 GEMM arguments");
+  if (a_kmajor && !b_kmajor) return fail(MMF_EINVAL, "bf16 GEMM: A k-major needs B k-major");
+  if ((nsplit > 1 || bias_grad) && (!workspace || !a_kmajor))
+    return fail(MMF_EINVAL, "bf16 GEMM: split-K / bias rows need a workspace and a k-major A");
+  const int amode = a_kmajor ? MODE_KR : MODE_RK, bmode = b_kmajor ? MODE_KR : MODE_RK;
+  hipStream_t st = (hipStream_t)stream;
+  const Operand a = opnd(static_cast<const float*>(A), lda), b = opnd(static_cast<const float*>(B), ldb);
+  if (nsplit == 1 && !bias_grad) {
+    GemmJob j = make_job(M, N, C, ldc, 0);
+    add_src(j, a, b, K);
+    if (!gemm_b16_ok(j, amode, bmode)) return fail(MMF_EINVAL, "bf16 GEMM: operand alignment / extents");
+    STAGE_TRY("gemm_bf16", launch_gemm_b16(&j, 1, st, amode, bmode));
+    return MMF_OK;
+  }
+  if (ldc != N) return fail(MMF_EINVAL, "bf16 GEMM: split-K writes a dense C (ldc == N)");
+  WgradPlan wp;
+  wp.split_hint = nsplit;
+  Bump bw(workspace);
+  plan_wgrad(wp, bw, M, N, K, a, b, C, bias_grad, bias_grad != nullptr);
+  if (!gemm_b16_ok(wp.jobs[0], amode, bmode)) return fail(MMF_EINVAL, "bf16 GEMM: operand alignment / extents");
+  STAGE_TRY("gemm_bf16", launch_gemm_b16(wp.jobs.data(), 1, st, amode, bmode));
+  STAGE_TRY("gemm_bf16_reduce", launch_reduce(wp.reds.data(), 1, st));
+  return MMF_OK;
+}
+
 int mmf_adamw_step_dev(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                        int64_t* step_dev, const float* lr_dev, const float* grad_coef_dev, float beta1,
                        float beta2, float eps, float weight_decay, float grad_scale, void* stream) {

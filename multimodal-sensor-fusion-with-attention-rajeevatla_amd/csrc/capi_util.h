@@ -163,6 +163,7 @@ struct WgradPlan {
   std::vector<GemmJob> jobs;
   std::vector<ReduceJob> reds;
   int split_hint = 0;   // > 0: split count of the next plan_wgrad (set per job by the caller)
+  std::vector<GemmJob> jobs_b16;   // bf16-operand KR x KR jobs (launch_gemm_b16), reduced with the rest
 };
 
 // has_db: the layer has a bias whose gradient (row sums) is produced too.  It is

@@ -384,6 +384,46 @@ __device__ __forceinline__ bf16x8 frag_b16(const float* lds, int e, int u, int h
   return *reinterpret_cast<const bf16x8*>(lds + e * 16 + (slot << 2));
 }
 
+// k-strided bf16 tiles (B16 = 2 / 3: an operand stored [k][e], e contiguous -- the dQ / dK /
+// P_m rows of a weight gradient, the W_q / W_k rows of dZ): a [32 k][128 e] image of 256-B rows,
+// 16-B chunk ch (e = 8 ch .. 8 ch + 7) of row r at slot ch ^ xkr(r) -- the layout on which both the
+// LDS-DMA fill and the transposed fragment reads are conflict-free (cdna_hip_programming.md T10,
+// image (b)).  One 1-KB DMA piece = 4 k rows: lane L fills slot L & 15 of row 4 ins + L / 16 by
+// choosing its source chunk.  The MFMA fragment (lane r = l & 31 of half h: e row r, k = 8 h + j)
+// is two ds_read_b64_tr_b16, each a 4 (k) x 16 (e) block delivered column-major.
+__device__ __forceinline__ int xkr(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+__device__ __forceinline__ void stage_tile_b16_kr(float* lds, const Operand& op, int64_t boff, int e0, int eext,
+                                                  int k0, int kend, int wave, int lane) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int ins = wave * 2 + u;
+    const int row = 4 * ins + (lane >> 4);
+    const int ch = (lane & 15) ^ xkr(row);
+    const int k = min(k0 + row, kend - 1);
+    const int e = min(e0 + 8 * ch, eext - 8);
+    const __bf16* src = reinterpret_cast<const __bf16*>(op.ptr) + boff + (int64_t)k * op.ld + e;
+    __builtin_amdgcn_global_load_lds((const void*)src,
+                                     (__attribute__((address_space(3))) void*)(lds + ins * 256), 16, 0, 0);
+  }
+}
+__device__ __forceinline__ void zero_tail_b16_kr(float* lds, int kv) {
+  for (int idx = threadIdx.x; idx < 32 * 16; idx += NT)
+    if ((idx >> 4) >= kv) *reinterpret_cast<f32x4*>(lds + idx * 4) = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+typedef __bf16 bf16x4g __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4g lds_bf16x4g;
+__device__ __forceinline__ int kr_off(int row, int e) { return 256 * row + 16 * ((e >> 3) ^ xkr(row)) + 2 * (e & 7); }
+// fragment of k-step u (16 k) for e rows e_base .. e_base + 31
+__device__ __forceinline__ bf16x8 frag_b16_kr(const float* lds, int e_base, int u, int lane) {
+  const char* img = reinterpret_cast<const char*>(lds);
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int e = e_base + 16 * (g & 1) + 4 * p;
+  const int k0 = 16 * u + 8 * (g >> 1) + q;
+  const bf16x4g lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4g*)(img + kr_off(k0, e)));
+  const bf16x4g hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4g*)(img + kr_off(k0 + 4, e)));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -393,10 +433,13 @@ __device__ __forceinline__ void lds_barrier() {
 // (source, k0) cursor over one tile's contraction
 struct KCursor { int si, k0, kend; };
 
-// B16: both operands bf16 in HBM (RK / RK, BF = 1, DK = 32 bf16 k per tile; stage_tile_b16)
+// B16: both operands bf16 in HBM (BF = 1, DK = 32 bf16 k per tile): 1 RK / RK (stage_tile_b16),
+// 2 KR / KR (stage_tile_b16_kr: weight gradients), 3 RK / KR (dZ = dQ W_q)
 template <int AMODE, int BMODE, int DK, int NSTAGE, int BF = 0, int B16 = 0>
 __global__ __launch_bounds__(NT, (NSTAGE * (B16 ? DK / 2 : DK) <= 32 ? 4 : 2)) void gemm_lds_kernel(const GemmArgs args) {
-  static_assert(!B16 || (AMODE == MODE_RK && BMODE == MODE_RK && BF == 1 && DK == 32), "bf16-operand form");
+  static_assert(!B16 || (BF == 1 && DK == 32 && AMODE == (B16 == 2 ? MODE_KR : MODE_RK) &&
+                         BMODE == (B16 == 1 ? MODE_RK : MODE_KR)),
+                "bf16-operand form");
   constexpr int DTILE = B16 ? BM * DK / 2 : BM * DK;   // floats per operand tile
   constexpr int DMA_PER_TILE = B16 ? 2 * (BM * DK / 2048) : 2 * (BM * DK / 1024);  // glds per wave per (A, B) pair
   int local;
@@ -463,8 +506,14 @@ __global__ __launch_bounds__(NT, (NSTAGE * (B16 ? DK / 2 : DK) <= 32 ? 4 : 2)) v
     }
     float* At = lds + buf * 2 * DTILE;
     if constexpr (B16) {
-      stage_tile_b16(At, opA, offA + seg * opA.seg_stride, T.i0, G.M, k.k0, k.kend, wave, lane);
-      stage_tile_b16(At + DTILE, opB, offB + seg * opB.seg_stride, T.j0, G.N, k.k0, k.kend, wave, lane);
+      if constexpr (AMODE == MODE_KR)
+        stage_tile_b16_kr(At, opA, offA + seg * opA.seg_stride, T.i0, G.M, k.k0, k.kend, wave, lane);
+      else
+        stage_tile_b16(At, opA, offA + seg * opA.seg_stride, T.i0, G.M, k.k0, k.kend, wave, lane);
+      if constexpr (BMODE == MODE_KR)
+        stage_tile_b16_kr(At + DTILE, opB, offB + seg * opB.seg_stride, T.j0, G.N, k.k0, k.kend, wave, lane);
+      else
+        stage_tile_b16(At + DTILE, opB, offB + seg * opB.seg_stride, T.j0, G.N, k.k0, k.kend, wave, lane);
     } else {
       stage_tile<AMODE, DK>(At, opA, offA + seg * opA.seg_stride, T.i0, G.M, k.k0, k.kend, wave, lane);
       stage_tile<BMODE, DK>(At + DTILE, opB, offB + seg * opB.seg_stride, T.j0, G.N, k.k0, k.kend, wave, lane);
@@ -500,8 +549,10 @@ __global__ __launch_bounds__(NT, (NSTAGE * (B16 ? DK / 2 : DK) <= 32 ? 4 : 2)) v
       const int kv = cur.kend - cur.k0;
       if (kv < DK) {
         if constexpr (B16) {
-          zero_tail_b16(At, kv);
-          zero_tail_b16(Bt, kv);
+          if constexpr (AMODE == MODE_KR) zero_tail_b16_kr(At, kv);
+          else zero_tail_b16(At, kv);
+          if constexpr (BMODE == MODE_KR) zero_tail_b16_kr(Bt, kv);
+          else zero_tail_b16(Bt, kv);
         } else {
           zero_tail<AMODE, DK>(At, kv);
           zero_tail<BMODE, DK>(Bt, kv);
@@ -512,6 +563,13 @@ __global__ __launch_bounds__(NT, (NSTAGE * (B16 ? DK / 2 : DK) <= 32 ? 4 : 2)) v
         stage(nissued % NSTAGE, iss);
         iss = advance(iss);
         ++nissued;
+      }
+      if (B16 && AMODE == MODE_KR && want_db) {
+        // bias grad of a TN dW from the bf16 A image (thread: row t&127, k half t>>7)
+        const int row = t & (BM - 1), kh = t >> 7;
+        const char* img = reinterpret_cast<const char*>(At);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) dbsum += (float)*reinterpret_cast<const __bf16*>(img + kr_off(kh * 16 + q, row));
       }
       if (!B16 && want_db) {
         // bias grad of a TN dW: row sums of A over this k-tile (thread: row t&127, k half t>>7)
@@ -528,9 +586,11 @@ if constexpr (B16) {
         for (int u = 0; u < DK / 16; ++u) {
           bf16x8 av[2], bv[2];
 #pragma unroll
-          for (int a = 0; a < 2; ++a) av[a] = frag_b16(At, wm * 64 + a * 32 + c, u, h);
+          for (int a = 0; a < 2; ++a)
+            av[a] = AMODE == MODE_KR ? frag_b16_kr(At, wm * 64 + a * 32, u, lane) : frag_b16(At, wm * 64 + a * 32 + c, u, h);
 #pragma unroll
-          for (int b = 0; b < 2; ++b) bv[b] = frag_b16(Bt, wn * 64 + b * 32 + c, u, h);
+          for (int b = 0; b < 2; ++b)
+            bv[b] = BMODE == MODE_KR ? frag_b16_kr(Bt, wn * 64 + b * 32, u, lane) : frag_b16(Bt, wn * 64 + b * 32 + c, u, h);
 #pragma unroll
           for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -1519,35 +1579,51 @@ hipError_t launch_cvt_bf16(const CvtArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-bool gemm_b16_ok(const GemmJob& J) {
+// bf16 operands in HBM: 16-B aligned rows (ld % 8), k a multiple of 8 along an RK operand's rows,
+// the e extent a multiple of 8 along a KR operand's rows; split-K slabs of whole 32-k tiles
+bool gemm_b16_ok(const GemmJob& J, int amode, int bmode) {
   const GemmGroup& g = J.g;
-  if ((g.epi & EPI_PARTIAL) || g.nbatch > 1 || g.seg_rows > 0) return false;
+  if (g.nbatch > 1 || g.seg_rows > 0) return false;
+  if ((g.epi & EPI_PARTIAL) && (g.kchunk % 32 != 0 || g.nsplit < 1)) return false;
+  if (g.part_db && amode != MODE_KR) return false;
   for (int s = 0; s < J.nsrc; ++s) {
     const GemmSrc& x = J.src[s];
-    for (const Operand* o : {&x.a, &x.b})
+    const Operand* ops[2] = {&x.a, &x.b};
+    const int modes[2] = {amode, bmode}, ext[2] = {g.M, g.N};
+    for (int i = 0; i < 2; ++i) {
+      const Operand* o = ops[i];
       if (o->row_div != 1 || o->seg_stride != 0 || o->ld % 8 != 0 || ((uintptr_t)o->ptr & 15) != 0) return false;
-    if (x.K % 8 != 0 || x.K < 8) return false;
+      if (modes[i] == MODE_KR ? (ext[i] % 8 != 0 || ext[i] < 8) : (x.K % 8 != 0 || x.K < 8)) return false;
+    }
   }
   return true;
 }
 
-hipError_t launch_gemm_b16(const GemmJob* jobs_in, int njobs, hipStream_t st) {
+hipError_t launch_gemm_b16(const GemmJob* jobs_in, int njobs, hipStream_t st, int amode, int bmode) {
   if (njobs <= 0) return hipSuccess;
+  const int form = amode == MODE_RK && bmode == MODE_RK ? 1 : amode == MODE_KR && bmode == MODE_KR ? 2
+                 : amode == MODE_RK && bmode == MODE_KR ? 3 : 0;
+  if (form == 0) return hipErrorInvalidValue;
   for (int i = 0; i < njobs; ++i)
-    if (!gemm_b16_ok(jobs_in[i]) || jobs_in[i].nsrc > GEMM_MAX_SRCS) return hipErrorInvalidValue;
+    if (!gemm_b16_ok(jobs_in[i], amode, bmode) || jobs_in[i].nsrc > GEMM_MAX_SRCS) return hipErrorInvalidValue;
   // longest contraction first, then clustered by the most-shared operand (launch_gemm's order)
   std::vector<int> order(njobs);
   std::vector<double> work(njobs);
   std::map<uintptr_t, int> uses;
+  bool any_partial = false;
   for (int i = 0; i < njobs; ++i) {
     order[i] = i;
+    const GemmGroup& g = jobs_in[i].g;
+    const bool partial = (g.epi & EPI_PARTIAL) != 0;
+    any_partial |= partial;
     double kk = 0.0;
     for (int s = 0; s < jobs_in[i].nsrc; ++s) kk += jobs_in[i].src[s].K;
-    work[i] = kk;
+    work[i] = partial ? (double)g.kchunk : kk;
     ++uses[(uintptr_t)jobs_in[i].src[0].a.ptr];
     ++uses[(uintptr_t)jobs_in[i].src[0].b.ptr];
   }
-  const bool ilv_on = gemm_interleave_mode() != 0;
+  const int ilv_mode = gemm_interleave_mode();
+  const bool ilv_on = ilv_mode == 2 || (ilv_mode == 1 && !any_partial);
   std::vector<uintptr_t> share(njobs, 0);
   for (int i = 0; i < njobs; ++i) {
     const uintptr_t a = (uintptr_t)jobs_in[i].src[0].a.ptr, b = (uintptr_t)jobs_in[i].src[0].b.ptr;
@@ -1561,8 +1637,8 @@ hipError_t launch_gemm_b16(const GemmJob* jobs_in, int njobs, hipStream_t st) {
   while (done < njobs) {
     GemmArgs args;
     memset(&args, 0, sizeof(args));
-    args.amode = MODE_RK;
-    args.bmode = MODE_RK;
+    args.amode = amode;
+    args.bmode = bmode;
     int ng = 0, ns = 0, max_blocks = 0;
     while (done < njobs && ng < GEMM_MAX_GROUPS) {
       const GemmJob& J = jobs_in[order[done]];
@@ -1572,9 +1648,10 @@ hipError_t launch_gemm_b16(const GemmJob* jobs_in, int njobs, hipStream_t st) {
       g.src_begin = ns;
       g.src_count = J.nsrc;
       for (int s = 0; s < J.nsrc; ++s) args.s[ns++] = J.src[s];
+      const bool partial = (g.epi & EPI_PARTIAL) != 0;
       args.tile_off[ng] = max_blocks;
       args.g[ng++] = g;
-      max_blocks += ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+      max_blocks += ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN) * (partial ? g.nsplit : 1);
       ++done;
     }
     args.ngroups = ng;
@@ -1588,14 +1665,20 @@ hipError_t launch_gemm_b16(const GemmJob* jobs_in, int njobs, hipStream_t st) {
     double fl = 0.0, by = 0.0;
     for (int gi = 0; gi < ng; ++gi) {
       const GemmGroup& g = args.g[gi];
+      const bool partial = (g.epi & EPI_PARTIAL) != 0;
       for (int si = g.src_begin; si < g.src_begin + g.src_count; ++si) {
         fl += 2.0 * g.M * g.N * args.s[si].K;
         by += 2.0 * ((double)g.M + g.N) * args.s[si].K;   // bf16 operands
       }
-      by += ((g.epi & EPI_BF16) ? 2.0 : 4.0) * g.M * g.N + ((g.epi & EPI_BF16COPY) ? 2.0 * g.M * g.N : 0.0);
+      by += partial ? 4.0 * g.nsplit * g.M * g.N
+                    : ((g.epi & EPI_BF16) ? 2.0 : 4.0) * g.M * g.N + ((g.epi & EPI_BF16COPY) ? 2.0 * g.M * g.N : 0.0);
     }
-    ProfLaunch prof_(st, "gemm_lds_kernel<0, 0, 32, 3, 1, 1>", fl, by);
-    mmf_launch((gemm_lds_kernel<MODE_RK, MODE_RK, 32, 3, 1, 1>), dim3(max_blocks, 1), dim3(NT), 0, st, args);
+    static const char* const kName[4] = {"", "gemm_lds_kernel<0, 0, 32, 3, 1, 1>", "gemm_lds_kernel<1, 1, 32, 3, 1, 2>",
+                                         "gemm_lds_kernel<0, 1, 32, 3, 1, 3>"};
+    ProfLaunch prof_(st, kName[form], fl, by);
+    if (form == 1) mmf_launch((gemm_lds_kernel<MODE_RK, MODE_RK, 32, 3, 1, 1>), dim3(max_blocks, 1), dim3(NT), 0, st, args);
+    else if (form == 2) mmf_launch((gemm_lds_kernel<MODE_KR, MODE_KR, 32, 3, 1, 2>), dim3(max_blocks, 1), dim3(NT), 0, st, args);
+    else mmf_launch((gemm_lds_kernel<MODE_RK, MODE_KR, 32, 3, 1, 3>), dim3(max_blocks, 1), dim3(NT), 0, st, args);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

@@ -110,6 +110,20 @@ bool qk_gemm_b16(const mmf_hybrid_desc* d) {
   return n > 0 && 2 * n <= CVT_MAX;
 }
 
+// The backward on bf16 dQ / dK ("medium", every pair a bf16 Q/K pair of the one-pass kernels):
+// attn_poolL_bwd_fused_bf16 stores dQ / dK as bf16 -- the rounding their GEMM consumers' MFMA
+// operands get anyway -- and the dZ GEMM (dQ W_q + dK W_k, RK x KR on the forward's W_q / W_k
+// copies) and the pairs' weight gradients (dQ^T P_q, dK^T P_k: KR x KR on the P_m copies) run the
+// LDS-DMA kernel's bf16-operand forms: half the bytes written by the attention backward and read
+// by both GEMMs.  The value-path term E_m is then materialised (pool_e) instead of riding in the
+// dZ GEMM as K = heads sources.  MMF_NO_DQK_B16=1: fp32 dQ / dK (A/B).
+bool dqk_b16_on(const mmf_hybrid_desc* d) {
+  if (!d->training || !qk_gemm_b16(d) || getenv("MMF_NO_DQK_B16")) return false;
+  for (int g = 0; g < d->num_pairs; ++g)
+    if (!pair_qk_bf16(d, g)) return false;
+  return d->num_pairs > 0;
+}
+
 // The head (tail or generic) takes mean_L P_m from per-tile column sums written by the
 // projection GEMM's epilogue when every 128-row tile lies inside one sample (pooled plan):
 // L / 128 rows per sample instead of L (C5: the generic head read 400 MB with one
@@ -341,10 +355,16 @@ void plan_wgrads(const mmf_hybrid_desc* d, const float* const* x, const float* m
       plan_zero(wp, H, H, g->k[p].w, g->k[p].b);
       continue;
     }
+    const bool b16 = dqk_b16_on(d);
+    // (bf16: dQ / dK and the P_m copies as __bf16 addresses, launch_gemm_b16's KR x KR form)
+    const float* pq = b16 ? reinterpret_cast<const float*>(s.Pb[q]) : s.P[q];
+    const float* pk = b16 ? reinterpret_cast<const float*>(s.Pb[k]) : s.P[k];
     wp.split_hint = hint(B * lq);
-    plan_wgrad(wp, bw, H, H, B * lq, opnd(w.dQ[p], H), opnd(s.P[q], H), g->q[p].w, g->q[p].b);
+    plan_wgrad(wp, bw, H, H, B * lq, opnd(w.dQ[p], H), opnd(pq, H), g->q[p].w, g->q[p].b);
+    if (b16) { wp.jobs_b16.push_back(wp.jobs.back()); wp.jobs.pop_back(); }
     wp.split_hint = hint(B * lk);
-    plan_wgrad(wp, bw, H, H, B * lk, opnd(w.dK[p], H), opnd(s.P[k], H), g->k[p].w, g->k[p].b);
+    plan_wgrad(wp, bw, H, H, B * lk, opnd(w.dK[p], H), opnd(pk, H), g->k[p].w, g->k[p].b);
+    if (b16) { wp.jobs_b16.push_back(wp.jobs.back()); wp.jobs.pop_back(); }
     wp.split_hint = 0;
   }
   for (int m = 0; m < M && want_proj; ++m) {
@@ -468,6 +488,7 @@ AttnPair make_pair(const mmf_hybrid_desc* d, const Saved& s, const float* mask, 
   a.kw_ld = kw_ld(a.Lk);
   a.pstore = s.pst[g];
   a.qk_bf16 = pair_qk_bf16(d, g) ? 1 : 0;
+  a.dqk_bf16 = a.qk_bf16 && dqk_b16_on(d) ? 1 : 0;
   return a;
 }
 
@@ -631,7 +652,7 @@ namespace {
 // (pbarT against the per-sample dU) when a 128-row tile never straddles two
 // samples and the pbarT rows are float4-able; otherwise pool_e materialises E_m.
 bool poole_in_dz(const mmf_hybrid_desc* d, int m) {
-  if (getenv("MMF_NO_POOLE")) return false;
+  if (getenv("MMF_NO_POOLE") || dqk_b16_on(d)) return false;
   return Lm(d, m) % 128 == 0 && d->hidden % 4 == 0 && d->num_heads % 4 == 0;
 }
 
@@ -1162,6 +1183,8 @@ static int hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W,
       return wa > wb;
     });
     STAGE_TRY("bwd.wgrad_gemm", launch_gemm(wp.jobs.data(), (int)wp.jobs.size(), MODE_KR, MODE_KR, p, rng, st));
+    if (!wp.jobs_b16.empty())
+      STAGE_TRY("bwd.wgrad_gemm", launch_gemm_b16(wp.jobs_b16.data(), (int)wp.jobs_b16.size(), st, MODE_KR, MODE_KR));
     STAGE_TRY("bwd.wgrad_reduce", launch_reduce(wp.reds.data(), (int)wp.reds.size(), st));
     return MMF_OK;
   }
@@ -1184,11 +1207,15 @@ static int hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W,
       j.g.gate = s.P[m];
       j.g.ld_gate = H;
       j.g.gate_scale = gscale;
+      const bool b16 = dqk_b16_on(d);
       for (int g = 0; g < d->num_pairs; ++g) {
         const bool sk = single_key(d, g);
-        if (d->pair_q[g] == m && !sk) add_src(j, opnd(w.dQ[g], H), opnd(W->q[g].w, H), H);
+        // (bf16: dQ / dK and the forward's W_q / W_k copies, launch_gemm_b16's RK x KR form)
+        const float* wq = b16 ? reinterpret_cast<const float*>(s.Wqb[g]) : W->q[g].w;
+        const float* wk = b16 ? reinterpret_cast<const float*>(s.Wkb[g]) : W->k[g].w;
+        if (d->pair_q[g] == m && !sk) add_src(j, opnd(w.dQ[g], H), opnd(wq, H), H);
         if (d->pair_k[g] == m) {
-          if (!sk) add_src(j, opnd(w.dK[g], H), opnd(W->k[g].w, H), H);
+          if (!sk) add_src(j, opnd(w.dK[g], H), opnd(wk, H), H);
           if (!pool) add_src(j, opnd(w.dV[g], H), opnd(W->v[g].w, H), H);
         }
       }
@@ -1206,7 +1233,8 @@ static int hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W,
       if (j.nsrc > GEMM_MAX_SRCS) return fail(MMF_ELIMIT, "too many gradient sources");
       jobs.push_back(j);
     }
-    STAGE_TRY("bwd.dZ_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, 0.f, rng, st));
+    if (dqk_b16_on(d)) STAGE_TRY("bwd.dZ_gemm", launch_gemm_b16(jobs.data(), (int)jobs.size(), st, MODE_RK, MODE_KR));
+    else STAGE_TRY("bwd.dZ_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, 0.f, rng, st));
   }
   // (5) dX_m = (dZ_m W_m) * mask * input-dropout'
   {
@@ -1231,6 +1259,8 @@ static int hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W,
     return wa > wb;
   });
   STAGE_TRY("bwd.wgrad_gemm", launch_gemm(wp.jobs.data(), (int)wp.jobs.size(), MODE_KR, MODE_KR, p, rng, st));
+  if (!wp.jobs_b16.empty())
+    STAGE_TRY("bwd.wgrad_gemm", launch_gemm_b16(wp.jobs_b16.data(), (int)wp.jobs_b16.size(), st, MODE_KR, MODE_KR));
   STAGE_TRY("bwd.wgrad_reduce", launch_reduce(wp.reds.data(), (int)wp.reds.size(), st));
   return MMF_OK;
 }

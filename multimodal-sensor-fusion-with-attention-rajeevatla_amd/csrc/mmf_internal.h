@@ -229,15 +229,18 @@ struct ReduceJob {
   int32_t nbatch, bs_out, bs_db;   // batch i: part += i*nsplit*M*N, out += i*bs_out, db += i*bs_db
 };
 // "medium" GEMMs whose operands are BOTH bf16 copies in HBM (Operand.ptr holds a __bf16 address,
-// ld in elements): RK x RK only, K % 8 == 0, 16-B aligned rows, no split-K / batch / segments.
-// The LDS-DMA kernel's B16 form (DK = 32): half the operand bytes and LDS reads, no conversion.
-hipError_t launch_gemm_b16(const GemmJob* jobs, int njobs, hipStream_t st);
+// ld in elements): RK x RK (Q/K projections), KR x KR (weight gradients, split-K slabs allowed, the
+// bias row sums from the bf16 A) or RK x KR (dZ); 16-B aligned rows, K % 8 == 0 along RK rows,
+// the output extent % 8 == 0 along KR rows; no batch / segments.  The LDS-DMA kernel's B16 forms
+// (DK = 32): half the operand bytes and LDS reads, no conversion; KR tiles read through
+// ds_read_b64_tr_b16.
+hipError_t launch_gemm_b16(const GemmJob* jobs, int njobs, hipStream_t st, int amode = MODE_RK, int bmode = MODE_RK);
 constexpr int CVT_MAX = 64;
 struct CvtArgs {
   const float* src[CVT_MAX]; __bf16* dst[CVT_MAX]; int64_t n[CVT_MAX]; int32_t count;
 };
 hipError_t launch_cvt_bf16(const CvtArgs& a, hipStream_t st);
-bool gemm_b16_ok(const GemmJob& J);
+bool gemm_b16_ok(const GemmJob& J, int amode = MODE_RK, int bmode = MODE_RK);
 hipError_t launch_reduce(const ReduceJob* jobs, int njobs, hipStream_t st);
 
 // ---------------------------------------------------------------------------
@@ -273,6 +276,10 @@ struct AttnPair {
   // Q and K rows stored as bf16 (ldq / ldk in elements): "medium" long-key pairs on the one-pass
   // kernels (attn_long.hip), whose projections the Q/K GEMM writes in bf16 (EPI_BF16)
   int32_t qk_bf16;
+  // dQ and dK written as bf16 (the fused one-pass backward; ldq / ldk in elements): "medium" with
+  // every Q/K pair bf16, whose dZ and weight-gradient GEMMs then read bf16 operands (hybrid.hip
+  // dqk_b16_on)
+  int32_t dqk_bf16;
 };
 
 constexpr int ATTN_MAX_PAIRS = 12;

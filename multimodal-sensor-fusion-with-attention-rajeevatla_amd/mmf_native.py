@@ -50,7 +50,7 @@ EXPORTED_SYMBOLS = (
     "mmf_adaptive_weights_backward",
     "mmf_cma_saved_bytes", "mmf_cma_workspace_bytes", "mmf_cma_forward", "mmf_cma_backward",
     "mmf_cross_entropy_ls", "mmf_adamw_step", "mmf_adamw_step_dev", "mmf_grad_clip_workspace_bytes",
-    "mmf_grad_clip_coef", "mmf_clip_adamw_step_dev", "mmf_clip_adamw_apply_dev", "mmf_grad_accumulate", "mmf_profile_begin", "mmf_profile_end",
+    "mmf_grad_clip_coef", "mmf_clip_adamw_step_dev", "mmf_clip_adamw_apply_dev", "mmf_grad_accumulate", "mmf_gemm_bf16_workspace_bytes", "mmf_gemm_bf16", "mmf_profile_begin", "mmf_profile_end",
     "mmf_last_error", "mmf_version",
     "mmf_attention_pool_workspace_bytes", "mmf_attention_pool_forward", "mmf_attention_pool_backward",
     "mmf_late_fusion_workspace_bytes", "mmf_late_fusion_forward", "mmf_late_fusion_backward",
@@ -174,6 +174,11 @@ def lib() -> ctypes.CDLL:
     L.mmf_clip_adamw_apply_dev.restype = c_int32
     L.mmf_grad_accumulate.argtypes = [c_int64, vp, vp, vp]
     L.mmf_grad_accumulate.restype = c_int32
+    L.mmf_gemm_bf16_workspace_bytes.argtypes = [c_int32, c_int32, c_int32, c_int32]
+    L.mmf_gemm_bf16_workspace_bytes.restype = sz
+    L.mmf_gemm_bf16.argtypes = [c_int32, c_int32, c_int32, vp, c_int32, c_int32, vp, c_int32, c_int32, vp, c_int32,
+                                vp, c_int32, vp, vp]
+    L.mmf_gemm_bf16.restype = c_int32
     L.mmf_profile_begin.argtypes = []
     L.mmf_profile_begin.restype = None
     L.mmf_profile_end.argtypes = [ctypes.c_char_p, c_size_t]

@@ -1,0 +1,80 @@
+"""The LDS-DMA GEMM's bf16-operand forms (csrc/gemm.hip gemm_lds_kernel<..., B16>) through
+mmf_gemm_bf16: RK x RK (the "medium" Q/K projections), KR x KR (the pairs' weight gradients, with
+split-K slabs, their fixed-order reduce and the bias row sums) and RK x KR (dZ), against an fp32
+matmul of the same bf16 values.  Ragged extents (tiles and k-tails past the data), padded leading
+dimensions."""
+
+import ctypes
+import os
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "multimodal-sensor-fusion-with-attention-rajeevatla_amd")]
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(M, N, K, a_kmajor, b_kmajor, nsplit=1, bias=False, pad=8, seed=0):
+    import mmf_native as nat
+    L = nat.lib()
+    g = torch.Generator().manual_seed(seed)
+    a = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    b = torch.randn(N, K, generator=g).to(torch.bfloat16)
+    dev = "cuda"
+
+    def store(x, kmajor):
+        # x (e, k) -> device storage [e][k] or [k][e], leading dimension padded by `pad`
+        src = x.t() if kmajor else x
+        buf = torch.zeros(src.shape[0], src.shape[1] + pad, dtype=torch.bfloat16)
+        buf[:, :src.shape[1]] = src
+        return buf.to(dev), buf.shape[1]
+
+    A, lda = store(a, a_kmajor)
+    B, ldb = store(b, b_kmajor)
+    C = torch.full((M, N), float("nan"), device=dev)
+    ws = None
+    if nsplit > 1 or bias:
+        ws = torch.empty(L.mmf_gemm_bf16_workspace_bytes(M, N, K, nsplit), dtype=torch.uint8, device=dev)
+    db = torch.full((M,), float("nan"), device=dev) if bias else None
+    rc = L.mmf_gemm_bf16(M, N, K, A.data_ptr(), lda, int(a_kmajor), B.data_ptr(), ldb, int(b_kmajor), C.data_ptr(), N,
+                         None if ws is None else ws.data_ptr(), nsplit, None if db is None else db.data_ptr(),
+                         nat.stream_ptr(torch.device(dev, 0)))
+    nat.check(rc, "mmf_gemm_bf16")
+    torch.cuda.synchronize()
+    ref = a.float() @ b.float().t()
+    tol = 1e-4 * ref.abs().max().item() + 1e-4
+    err = (C.cpu() - ref).abs().max().item()
+    assert err <= tol, f"C max err {err} (tol {tol})"
+    if bias:
+        rs = a.float().sum(1)
+        berr = (db.cpu() - rs).abs().max().item()
+        assert berr <= 1e-4 * rs.abs().max().item() + 1e-4, f"bias rows max err {berr}"
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 384, 264), (130, 136, 40), (512, 256, 256)])
+def test_rk_rk(M, N, K):
+    _run(M, N, K, False, False)
+
+
+@pytest.mark.parametrize("M,N,K,nsplit,bias", [(256, 256, 1000, 1, False), (136, 256, 4096, 5, True),
+                                               (256, 264, 65, 1, True), (384, 128, 8192, 16, True)])
+def test_kr_kr(M, N, K, nsplit, bias):
+    _run(M, N, K, True, True, nsplit=nsplit, bias=bias)
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 256, 512), (1024, 256, 2560), (64, 72, 24)])
+def test_rk_kr(M, N, K):
+    _run(M, N, K, False, True)
+
+
+def test_bad_layouts_refused():
+    import mmf_native as nat
+    L = nat.lib()
+    x = torch.zeros(64, 64, dtype=torch.bfloat16, device="cuda")
+    c = torch.zeros(64, 64, device="cuda")
+    s = nat.stream_ptr(torch.device("cuda", 0))
+    assert L.mmf_gemm_bf16(64, 64, 64, x.data_ptr(), 64, 1, x.data_ptr(), 64, 0, c.data_ptr(), 64, None, 1, None, s) != 0
+    assert L.mmf_gemm_bf16(64, 64, 64, x.data_ptr(), 60, 0, x.data_ptr(), 64, 0, c.data_ptr(), 64, None, 1, None, s) != 0
