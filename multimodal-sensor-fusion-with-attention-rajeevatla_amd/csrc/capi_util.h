@@ -164,6 +164,7 @@ struct WgradPlan {
   std::vector<ReduceJob> reds;
   int split_hint = 0;   // > 0: split count of the next plan_wgrad (set per job by the caller)
   std::vector<GemmJob> jobs_b16;   // bf16-operand KR x KR jobs (launch_gemm_b16), reduced with the rest
+  bool size_only = false;          // a workspace-sizing pass: take the slabs, keep no jobs
 };
 
 // has_db: the layer has a bias whose gradient (row sums) is produced too.  It is
@@ -180,6 +181,7 @@ inline void plan_wgrad(WgradPlan& wp, Bump& ws, int M, int N, int rows, Operand 
   j.g.nsplit = nsplit;
   j.g.kchunk = kchunk;
   j.g.part_db = part_db;
+  if (wp.size_only) return;
   add_src(j, a, b, rows);
   wp.jobs.push_back(j);
   ReduceJob r;
@@ -209,6 +211,7 @@ inline void plan_wgrad_batched(WgradPlan& wp, Bump& ws, int M, int N, int rows, 
   j.g.nbatch = nbatch;
   j.g.bs_a = bs_a;
   j.g.bs_b = bs_b;
+  if (wp.size_only) return;
   add_src(j, a, b, rows);
   wp.jobs.push_back(j);
   ReduceJob r;
@@ -226,6 +229,7 @@ inline void plan_wgrad_batched(WgradPlan& wp, Bump& ws, int M, int N, int rows, 
 // A weight (and bias) gradient that is exactly zero: a reduce job over no slabs, so the
 // split-K reduce launch writes the zeros (no launch of its own).
 inline void plan_zero(WgradPlan& wp, int M, int N, float* out_w, float* out_b) {
+  if (wp.size_only) return;
   ReduceJob r;
   memset(&r, 0, sizeof(r));
   r.nbatch = 1;

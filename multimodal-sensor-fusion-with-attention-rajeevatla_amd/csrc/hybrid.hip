@@ -361,10 +361,10 @@ void plan_wgrads(const mmf_hybrid_desc* d, const float* const* x, const float* m
     const float* pk = b16 ? reinterpret_cast<const float*>(s.Pb[k]) : s.P[k];
     wp.split_hint = hint(B * lq);
     plan_wgrad(wp, bw, H, H, B * lq, opnd(w.dQ[p], H), opnd(pq, H), g->q[p].w, g->q[p].b);
-    if (b16) { wp.jobs_b16.push_back(wp.jobs.back()); wp.jobs.pop_back(); }
+    if (b16 && !wp.size_only) { wp.jobs_b16.push_back(wp.jobs.back()); wp.jobs.pop_back(); }
     wp.split_hint = hint(B * lk);
     plan_wgrad(wp, bw, H, H, B * lk, opnd(w.dK[p], H), opnd(pk, H), g->k[p].w, g->k[p].b);
-    if (b16) { wp.jobs_b16.push_back(wp.jobs.back()); wp.jobs.pop_back(); }
+    if (b16 && !wp.size_only) { wp.jobs_b16.push_back(wp.jobs.back()); wp.jobs.pop_back(); }
     wp.split_hint = 0;
   }
   for (int m = 0; m < M && want_proj; ++m) {
@@ -397,6 +397,7 @@ size_t workspace_bytes(const mmf_hybrid_desc* d) {
   for (int part = 0; part < 3; ++part) {
     Bump b = bw;
     WgradPlan wp;
+    wp.size_only = true;
     plan_wgrads(d, nullptr, nullptr, nullptr, s, w, nullptr, b, wp, part);
     top = std::max(top, b.off);
   }

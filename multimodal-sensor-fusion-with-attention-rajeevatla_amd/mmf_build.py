@@ -29,16 +29,17 @@ def build_torch_ext(force: bool = False) -> str:
     if not force and os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps):
         return out
     tlib = ce.library_paths()[0]
+    tmp = f"{out}.{os.getpid()}.tmp"   # (concurrent builders -- pytest workers -- each write their own)
     abi = int(bool(torch._C._GLIBCXX_USE_CXX11_ABI))
     rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
     cmd = (["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-w", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
             "-DTORCH_EXTENSION_NAME=mmf_torch", "-DTORCH_API_INCLUDE_EXTENSION_H", "-D__HIP_PLATFORM_AMD__=1",
             "-DUSE_ROCM", f"-I{rocm}/include", f"-I{INCLUDE}", f"-I{sysconfig.get_paths()['include']}"]
            + [f"-I{p}" for p in ce.include_paths()]
-           + [src, "-o", out + ".tmp", f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+           + [src, "-o", tmp, f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
               "-ltorch_python", f"-Wl,-rpath,{tlib}"])
     subprocess.run(cmd, check=True)
-    os.replace(out + ".tmp", out)
+    os.replace(tmp, out)
     return out
 
 
