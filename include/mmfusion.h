@@ -361,16 +361,18 @@ int mmf_clip_adamw_apply_dev(int64_t n, float* param, const float* grad, float* 
 int mmf_grad_accumulate(int64_t n, const float* src, float* dst, void* stream);
 
 /* The bf16-operand GEMM forms of the "medium" plans, for tests and diagnostics:
- * C (M x N fp32, ldc) = sum over k of A(m, k) B(n, k), with A stored [m][k] (a_kmajor = 0, lda)
- * or [k][m] (a_kmajor = 1), B likewise; bf16 (__bf16) operands, 16-byte aligned, lda / ldb
- * multiples of 8; fp32 accumulation.  Forms: (0, 0), (1, 1) and (0, 1) -- the Q/K projections,
- * the weight gradients, dZ.  nsplit > 1 (k-major A): split-K slabs in `workspace`
- * (mmf_gemm_bf16_workspace_bytes) reduced in a fixed order; bias_grad (k-major A, may be NULL):
- * also write the row sums of A over k (a weight gradient's bias gradient). */
+ * C (M x N, ldc) = sum over k of A(m, k) B(n, k) (+ bias[n]), with A stored [m][k] (a_kmajor = 0,
+ * lda) or [k][m] (a_kmajor = 1), B likewise; bf16 (__bf16) operands, 16-byte aligned, lda / ldb
+ * multiples of 8; fp32 accumulation; C fp32, or bf16 with c_bf16 = 1 (rounded to nearest even).
+ * Forms: (0, 0), (1, 1) and (0, 1) -- the Q/K projections (bf16 C with bias: the weight-stationary
+ * kernel when M and N are multiples of 128 and 32 | K <= 256), the weight gradients, dZ.
+ * nsplit > 1 (k-major A, fp32 C): split-K slabs in `workspace` (mmf_gemm_bf16_workspace_bytes)
+ * reduced in a fixed order; bias_grad (k-major A, may be NULL): also write the row sums of A over k
+ * (a weight gradient's bias gradient). */
 size_t mmf_gemm_bf16_workspace_bytes(int32_t M, int32_t N, int32_t K, int32_t nsplit);
 int mmf_gemm_bf16(int32_t M, int32_t N, int32_t K, const void* A, int32_t lda, int32_t a_kmajor, const void* B,
-                  int32_t ldb, int32_t b_kmajor, float* C, int32_t ldc, void* workspace, int32_t nsplit,
-                  float* bias_grad, void* stream);
+                  int32_t ldb, int32_t b_kmajor, const float* bias, void* C, int32_t ldc, int32_t c_bf16,
+                  void* workspace, int32_t nsplit, float* bias_grad, void* stream);
 
 /* Global-norm gradient clipping (torch.nn.utils.clip_grad_norm_(max_norm,
  * norm_type=2) as Lightning applies gradient_clip_val, src/train.py:416-430,

@@ -563,18 +563,19 @@ size_t mmf_gemm_bf16_workspace_bytes(int32_t M, int32_t N, int32_t K, int32_t ns
 }
 
 int mmf_gemm_bf16(int32_t M, int32_t N, int32_t K, const void* A, int32_t lda, int32_t a_kmajor, const void* B,
-                  int32_t ldb, int32_t b_kmajor, float* C, int32_t ldc, void* workspace, int32_t nsplit,
-                  float* bias_grad, void* stream) {
+                  int32_t ldb, int32_t b_kmajor, const float* bias, void* C, int32_t ldc, int32_t c_bf16,
+                  void* workspace, int32_t nsplit, float* bias_grad, void* stream) {
   if (M < 1 || N < 1 || K < 1 || !A || !B || !C || ldc < N || nsplit < 1)
     return fail(MMF_EINVAL, "bad bf16 GEMM arguments");
   if (a_kmajor && !b_kmajor) return fail(MMF_EINVAL, "bf16 GEMM: A k-major needs B k-major");
-  if ((nsplit > 1 || bias_grad) && (!workspace || !a_kmajor))
-    return fail(MMF_EINVAL, "bf16 GEMM: split-K / bias rows need a workspace and a k-major A");
+  if ((nsplit > 1 || bias_grad) && (!workspace || !a_kmajor || bias || c_bf16))
+    return fail(MMF_EINVAL, "bf16 GEMM: split-K / bias rows need a workspace, a k-major A and an fp32 C");
   const int amode = a_kmajor ? MODE_KR : MODE_RK, bmode = b_kmajor ? MODE_KR : MODE_RK;
   hipStream_t st = (hipStream_t)stream;
   const Operand a = opnd(static_cast<const float*>(A), lda), b = opnd(static_cast<const float*>(B), ldb);
   if (nsplit == 1 && !bias_grad) {
-    GemmJob j = make_job(M, N, C, ldc, 0);
+    GemmJob j = make_job(M, N, static_cast<float*>(C), ldc, (bias ? EPI_BIAS : 0) | (c_bf16 ? EPI_BF16 : 0));
+    j.g.bias = bias;
     add_src(j, a, b, K);
     if (!gemm_b16_ok(j, amode, bmode)) return fail(MMF_EINVAL, "bf16 GEMM: operand alignment / extents");
     STAGE_TRY("gemm_bf16", launch_gemm_b16(&j, 1, st, amode, bmode));
@@ -584,7 +585,7 @@ int mmf_gemm_bf16(int32_t M, int32_t N, int32_t K, const void* A, int32_t lda, i
   WgradPlan wp;
   wp.split_hint = nsplit;
   Bump bw(workspace);
-  plan_wgrad(wp, bw, M, N, K, a, b, C, bias_grad, bias_grad != nullptr);
+  plan_wgrad(wp, bw, M, N, K, a, b, static_cast<float*>(C), bias_grad, bias_grad != nullptr);
   if (!gemm_b16_ok(wp.jobs[0], amode, bmode)) return fail(MMF_EINVAL, "bf16 GEMM: operand alignment / extents");
   STAGE_TRY("gemm_bf16", launch_gemm_b16(wp.jobs.data(), 1, st, amode, bmode));
   STAGE_TRY("gemm_bf16_reduce", launch_reduce(wp.reds.data(), 1, st));

@@ -864,6 +864,179 @@ if constexpr (BF != 0) {
   }
 }
 
+// ------------------------------------------------------------------ weight-stationary bf16 kernel
+// Y (rows x N <= 128, bf16) = X (rows x K, bf16) W^T (+ bias) for 32 <= K <= 256 (32 | K): the "medium"
+// Q / K projections of the long-key pairs (src/attention.py:104-105 at C5: 60 GEMMs of
+// 65536 x 256 x 256, each split into two 128-column groups).  The LDS-DMA kernel's 128 x 128 tile
+// restages W's 64 KB k-strip from L2 for every tile and its 8 k-tiles leave prologue and epilogue
+// exposed (0.11 of the bf16 peak at C5); here each wave loads its 64 columns of W^T once into
+// registers (128 VGPRs at K = 256, the B fragments of v_mfma_f32_32x32x16_bf16) and keeps them
+// while the workgroup walks a contiguous run of row tiles; X streams through a 6-deep LDS-DMA ring
+// of the RK bf16 tiles (stage_tile_b16: [128 rows][32 k], 8 KB), which runs ahead across tile
+// boundaries; the epilogue stores 4 bf16 per lane straight from the accumulators.  Persistent
+// grid, 2 workgroups per CU; the two column groups of one GEMM are adjacent, so their workgroups
+// (16 apart in dispatch order at C5: the same XCD) read the same X rows at about the same time.
+constexpr int WSR16_NS = 6, WSR16_NKS = 16;   // ring depth, max 16-deep k-steps (K <= 256)
+typedef __bf16 bf16x4s __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(NT, 2) void gemm_wsr_b16_kernel(const GemmArgs args, int total_items, int K) {
+  constexpr int DTILE = BM * 32 / 2;   // floats per bf16 tile
+  __shared__ __attribute__((aligned(16))) float ring[WSR16_NS * DTILE];
+  const int t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nkt = K / 32, nks = K / 16;
+
+  const int nwg = gridDim.x;
+  const int item0 = (int)(((int64_t)blockIdx.x * total_items) / nwg);
+  const int item1 = (int)(((int64_t)(blockIdx.x + 1) * total_items) / nwg);
+  if (item0 >= item1) return;
+
+  const int nflat = (item1 - item0) * nkt;
+  auto item_group = [&](int item, int& rowtile) {
+    int g = 0;
+#pragma unroll
+    for (int i = 1; i < GEMM_MAX_GROUPS; ++i)
+      if (i < args.ngroups && item >= args.tile_off[i]) g = i;
+    rowtile = item - args.tile_off[g];
+    return g;
+  };
+  int di = item0, dk = 0, drt = 0;
+  int dg = item_group(item0, drt);
+  const int g_first = dg, rt_first = drt;
+  auto issue = [&](int f) {
+    const int slot = f % WSR16_NS;
+    const GemmSrc& S = args.s[args.g[dg].src_begin];
+    stage_tile_b16(ring + slot * DTILE, S.a, 0, drt * BM, args.g[dg].M, dk * 32, K, wave, lane);
+    if (++dk == nkt) {
+      dk = 0;
+      ++di;
+      ++drt;
+      while (dg + 1 < args.ngroups && di >= args.tile_off[dg + 1]) { ++dg; drt = di - args.tile_off[dg]; }
+    }
+  };
+  // as gemm_wsr_kernel: 2 LDS-DMAs per wave per k-tile, 16 epilogue stores per wave per row tile
+  auto wait_ahead = [&](int ahead, bool stores_younger) {
+    if (stores_younger) {
+      switch (ahead) {
+        case 0: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(22)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+      }
+    } else {
+      switch (ahead) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+      }
+    }
+  };
+  static_assert(WSR16_NS - 2 <= 4, "wait_ahead covers 4 tiles ahead");
+
+  int nissued = 0;
+  for (; nissued < WSR16_NS - 1 && nissued < nflat; ++nissued) issue(nissued);
+
+  bf16x8 breg[2][WSR16_NKS];
+  float bias[2];
+  int cur_g = -1;
+  int f = 0;
+  int epi_mark = 0;
+  int g = g_first, rt = rt_first;
+  for (int item = item0; item < item1; ++item, ++rt) {
+    while (g + 1 < args.ngroups && item >= args.tile_off[g + 1]) { ++g; rt = item - args.tile_off[g]; }
+    const GemmGroup& G = args.g[g];
+    if (g != cur_g) {
+      // this group's W^T slice for the wave's 64 columns: breg[b][s] = W[col][16 s + 8 h .. + 7]
+      cur_g = g;
+      const GemmSrc& S = args.s[G.src_begin];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int col = wn * 64 + b * 32 + c;
+        const bool ok = col < G.N;
+        const __bf16* wrow = reinterpret_cast<const __bf16*>(S.b.ptr) + (int64_t)(ok ? col : 0) * S.b.ld + 8 * h;
+#pragma unroll
+        for (int m = 0; m < WSR16_NKS; ++m) {
+          bf16x8 z;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) z[e] = (__bf16)0.f;
+          breg[b][m] = (ok && m < nks) ? *reinterpret_cast<const bf16x8*>(wrow + 16 * m) : z;
+        }
+        bias[b] = (ok && (G.epi & EPI_BIAS)) ? G.bias[col] : 0.f;
+      }
+      __builtin_amdgcn_s_waitcnt(0x0F70);   // (see gemm_wsr_kernel: retire these loads visibly)
+    }
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+#pragma unroll
+    for (int kt = 0; kt < WSR16_NKS / 2; ++kt) {
+      if (kt < nkt) {
+        wait_ahead(nissued - f - 1, f < epi_mark);
+        lds_barrier();
+        if (nissued < nflat) issue(nissued++);
+        const float* At = ring + (f % WSR16_NS) * DTILE;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          bf16x8 av[2];
+#pragma unroll
+          for (int a = 0; a < 2; ++a) av[a] = frag_b16(At, wm * 64 + a * 32 + c, u, h);
+#pragma unroll
+          for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[a], breg[b][2 * kt + u], acc[a][b], 0, 0, 0);
+        }
+        ++f;
+      }
+    }
+    // epilogue: v = alpha*acc + bias[j], 4x4 transpose across the lane quad, 4 bf16 per store
+    const int x = c & 3;
+    const int i0 = rt * BM + wm * 64;
+    __bf16* Cb = reinterpret_cast<__bf16*>(G.C);
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = acc[a][b][4 * q + e] * G.alpha + bias[b];
+          {
+            const bool up = (x & 2) != 0;
+            const float s0 = dpp<DPP_XOR2>(up ? v[0] : v[2]);
+            const float s1 = dpp<DPP_XOR2>(up ? v[1] : v[3]);
+            if (up) { v[0] = s0; v[1] = s1; } else { v[2] = s0; v[3] = s1; }
+          }
+          {
+            const bool odd = (x & 1) != 0;
+            const float s0 = dpp<DPP_XOR1>(odd ? v[0] : v[1]);
+            const float s1 = dpp<DPP_XOR1>(odd ? v[2] : v[3]);
+            if (odd) { v[0] = s0; v[2] = s1; } else { v[1] = s0; v[3] = s1; }
+          }
+          const int row = i0 + a * 32 + 8 * q + 4 * h + x;
+          const int col = wn * 64 + b * 32 + (c & ~3);
+          if (col < G.N) {
+            bf16x4s o;
+            o[0] = (__bf16)v[0]; o[1] = (__bf16)v[1]; o[2] = (__bf16)v[2]; o[3] = (__bf16)v[3];
+            *reinterpret_cast<bf16x4s*>(Cb + (int64_t)row * G.ldc + col) = o;
+          }
+        }
+      }
+    epi_mark = nissued;
+  }
+}
+
 // ------------------------------------------------------------------ generic kernel
 struct TileRegs { float4 v[4]; };
 
@@ -1599,8 +1772,71 @@ bool gemm_b16_ok(const GemmJob& J, int amode, int bmode) {
   return true;
 }
 
+// gemm_wsr_b16_kernel's jobs: one source, bf16 output (+ bias), whole 128-row tiles and 128-column
+// groups (the wait counts assume every store is issued), 32 | K <= 256
+bool job_wsr_b16(const GemmJob& J) {
+  const GemmGroup& g = J.g;
+  if (J.nsrc != 1 || g.nbatch > 1 || g.seg_rows > 0 || !(g.epi & EPI_BF16) || (g.epi & ~(EPI_BIAS | EPI_BF16))) return false;
+  const GemmSrc& s = J.src[0];
+  return g.M % BM == 0 && g.N % BN == 0 && s.K % 32 == 0 && s.K >= 32 && s.K <= 16 * WSR16_NKS && s.a.row_div == 1 &&
+         s.b.row_div == 1 && s.a.seg_stride == 0 && s.a.ld % 8 == 0 && s.b.ld % 8 == 0 && aligned16(s.a.ptr) &&
+         aligned16(s.b.ptr) && g.ldc % 4 == 0 && ((uintptr_t)g.C & 7) == 0;
+}
+
+hipError_t launch_wsr_b16(const GemmJob* jobs, int njobs, hipStream_t st) {
+  // every job split into its 128-column groups, adjacent (see the kernel)
+  std::vector<GemmJob> parts;
+  std::vector<int> first;   // the job's first column group (its X rows counted once)
+  for (int i = 0; i < njobs; ++i)
+    for (int c0 = 0; c0 < jobs[i].g.N; c0 += BN) {
+      first.push_back(c0 == 0);
+      GemmJob p = jobs[i];
+      p.g.N = BN;
+      p.g.C = reinterpret_cast<float*>(reinterpret_cast<__bf16*>(jobs[i].g.C) + c0);
+      if (p.g.bias) p.g.bias = jobs[i].g.bias + c0;
+      p.src[0].b.ptr = reinterpret_cast<const float*>(reinterpret_cast<const __bf16*>(jobs[i].src[0].b.ptr) +
+                                                      (int64_t)c0 * jobs[i].src[0].b.ld);
+      parts.push_back(p);
+    }
+  for (size_t done = 0; done < parts.size();) {
+    GemmArgs args;
+    memset(&args, 0, sizeof(args));
+    args.amode = MODE_RK;
+    args.bmode = MODE_RK;
+    int ng = 0, items = 0;
+    double fl = 0.0, by = 0.0;
+    const int K = parts[done].src[0].K;
+    while (done < parts.size() && ng < GEMM_MAX_GROUPS && parts[done].src[0].K == K) {
+      GemmGroup g = parts[done].g;
+      g.nbatch = 1;
+      g.src_begin = ng;
+      g.src_count = 1;
+      args.s[ng] = parts[done].src[0];
+      args.tile_off[ng] = items;
+      args.g[ng++] = g;
+      items += g.M / BM;
+      fl += 2.0 * g.M * g.N * K;
+      // X rows once per GEMM (the two column groups share them through L2), W, Y in bf16
+      by += 2.0 * (first[done] ? (double)g.M * K : 0.0) + 2.0 * g.N * K + 2.0 * g.M * g.N;
+      ++done;
+    }
+    args.ngroups = ng;
+    const int grid = std::min(items, 2 * cu_count());
+    ProfLaunch prof_(st, "gemm_wsr_b16_kernel", fl, by);
+    mmf_launch(gemm_wsr_b16_kernel, dim3(grid), dim3(NT), 0, st, args, items, K);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 hipError_t launch_gemm_b16(const GemmJob* jobs_in, int njobs, hipStream_t st, int amode, int bmode) {
   if (njobs <= 0) return hipSuccess;
+  if (amode == MODE_RK && bmode == MODE_RK && !getenv("MMF_NO_WSR16")) {
+    bool wsr = true;
+    for (int i = 0; i < njobs && wsr; ++i) wsr = job_wsr_b16(jobs_in[i]);
+    if (wsr) return launch_wsr_b16(jobs_in, njobs, st);
+  }
   const int form = amode == MODE_RK && bmode == MODE_RK ? 1 : amode == MODE_KR && bmode == MODE_KR ? 2
                  : amode == MODE_RK && bmode == MODE_KR ? 3 : 0;
   if (form == 0) return hipErrorInvalidValue;

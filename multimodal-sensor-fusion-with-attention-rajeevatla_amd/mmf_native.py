@@ -176,8 +176,8 @@ def lib() -> ctypes.CDLL:
     L.mmf_grad_accumulate.restype = c_int32
     L.mmf_gemm_bf16_workspace_bytes.argtypes = [c_int32, c_int32, c_int32, c_int32]
     L.mmf_gemm_bf16_workspace_bytes.restype = sz
-    L.mmf_gemm_bf16.argtypes = [c_int32, c_int32, c_int32, vp, c_int32, c_int32, vp, c_int32, c_int32, vp, c_int32,
-                                vp, c_int32, vp, vp]
+    L.mmf_gemm_bf16.argtypes = [c_int32, c_int32, c_int32, vp, c_int32, c_int32, vp, c_int32, c_int32, vp, vp,
+                                c_int32, c_int32, vp, c_int32, vp, vp]
     L.mmf_gemm_bf16.restype = c_int32
     L.mmf_profile_begin.argtypes = []
     L.mmf_profile_begin.restype = None

@@ -1,8 +1,8 @@
-"""The LDS-DMA GEMM's bf16-operand forms (csrc/gemm.hip gemm_lds_kernel<..., B16>) through
-mmf_gemm_bf16: RK x RK (the "medium" Q/K projections), KR x KR (the pairs' weight gradients, with
-split-K slabs, their fixed-order reduce and the bias row sums) and RK x KR (dZ), against an fp32
-matmul of the same bf16 values.  Ragged extents (tiles and k-tails past the data), padded leading
-dimensions."""
+"""The bf16-operand GEMM forms (csrc/gemm.hip gemm_lds_kernel<..., B16>, gemm_wsr_b16_kernel)
+through mmf_gemm_bf16: RK x RK (the "medium" Q/K projections: bf16 output with bias on the
+weight-stationary kernel), KR x KR (the pairs' weight gradients, with split-K slabs, their
+fixed-order reduce and the bias row sums) and RK x KR (dZ), against an fp32 matmul of the same bf16
+values.  Ragged extents (tiles and k-tails past the data), padded leading dimensions."""
 
 import ctypes
 import os
@@ -17,7 +17,7 @@ sys.path[:0] = [os.path.join(ROOT, "multimodal-sensor-fusion-with-attention-raje
 pytestmark = pytest.mark.gpu
 
 
-def _run(M, N, K, a_kmajor, b_kmajor, nsplit=1, bias=False, pad=8, seed=0):
+def _run(M, N, K, a_kmajor, b_kmajor, nsplit=1, bias=False, pad=8, seed=0, c_bf16=False, add_bias=False):
     import mmf_native as nat
     L = nat.lib()
     g = torch.Generator().manual_seed(seed)
@@ -34,17 +34,28 @@ def _run(M, N, K, a_kmajor, b_kmajor, nsplit=1, bias=False, pad=8, seed=0):
 
     A, lda = store(a, a_kmajor)
     B, ldb = store(b, b_kmajor)
-    C = torch.full((M, N), float("nan"), device=dev)
+    C = torch.full((M, N), float("nan"), device=dev, dtype=torch.bfloat16 if c_bf16 else torch.float32)
+    bvec = torch.randn(N, generator=g).to(dev) if add_bias else None
     ws = None
     if nsplit > 1 or bias:
         ws = torch.empty(L.mmf_gemm_bf16_workspace_bytes(M, N, K, nsplit), dtype=torch.uint8, device=dev)
     db = torch.full((M,), float("nan"), device=dev) if bias else None
-    rc = L.mmf_gemm_bf16(M, N, K, A.data_ptr(), lda, int(a_kmajor), B.data_ptr(), ldb, int(b_kmajor), C.data_ptr(), N,
+    rc = L.mmf_gemm_bf16(M, N, K, A.data_ptr(), lda, int(a_kmajor), B.data_ptr(), ldb, int(b_kmajor),
+                         None if bvec is None else bvec.data_ptr(), C.data_ptr(), N, int(c_bf16),
                          None if ws is None else ws.data_ptr(), nsplit, None if db is None else db.data_ptr(),
                          nat.stream_ptr(torch.device(dev, 0)))
     nat.check(rc, "mmf_gemm_bf16")
     torch.cuda.synchronize()
     ref = a.float() @ b.float().t()
+    if bvec is not None:
+        ref = ref + bvec.cpu()
+    if c_bf16:
+        # rounded once to bf16 (nearest even): within half a bf16 ulp of the fp32 result, plus the
+        # accumulation-order difference
+        tol = 2.0 ** -8 * ref.abs() + 1e-4 * ref.abs().max().item() + 1e-4
+        err_t = (C.float().cpu() - ref).abs()
+        assert bool((err_t <= tol).all()), f"C max err {err_t.max().item()}"
+        return
     tol = 1e-4 * ref.abs().max().item() + 1e-4
     err = (C.cpu() - ref).abs().max().item()
     assert err <= tol, f"C max err {err} (tol {tol})"
@@ -57,6 +68,17 @@ def _run(M, N, K, a_kmajor, b_kmajor, nsplit=1, bias=False, pad=8, seed=0):
 @pytest.mark.parametrize("M,N,K", [(256, 384, 264), (130, 136, 40), (512, 256, 256)])
 def test_rk_rk(M, N, K):
     _run(M, N, K, False, False)
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 256, 256), (1024, 128, 96), (384, 384, 32)])
+def test_rk_rk_weight_stationary_bf16_out(M, N, K):
+    # (M, N multiples of 128, 32 | K <= 256, bf16 C + bias: gemm_wsr_b16_kernel)
+    _run(M, N, K, False, False, c_bf16=True, add_bias=True)
+
+
+def test_rk_rk_bf16_out_lds_kernel():
+    # (a ragged M: the LDS-DMA kernel's B16 form with the bf16 epilogue)
+    _run(200, 256, 256, False, False, c_bf16=True, add_bias=True)
 
 
 @pytest.mark.parametrize("M,N,K,nsplit,bias", [(256, 256, 1000, 1, False), (136, 256, 4096, 5, True),
@@ -76,5 +98,7 @@ def test_bad_layouts_refused():
     x = torch.zeros(64, 64, dtype=torch.bfloat16, device="cuda")
     c = torch.zeros(64, 64, device="cuda")
     s = nat.stream_ptr(torch.device("cuda", 0))
-    assert L.mmf_gemm_bf16(64, 64, 64, x.data_ptr(), 64, 1, x.data_ptr(), 64, 0, c.data_ptr(), 64, None, 1, None, s) != 0
-    assert L.mmf_gemm_bf16(64, 64, 64, x.data_ptr(), 60, 0, x.data_ptr(), 64, 0, c.data_ptr(), 64, None, 1, None, s) != 0
+    assert L.mmf_gemm_bf16(64, 64, 64, x.data_ptr(), 64, 1, x.data_ptr(), 64, 0, None, c.data_ptr(), 64, 0, None, 1,
+                           None, s) != 0
+    assert L.mmf_gemm_bf16(64, 64, 64, x.data_ptr(), 60, 0, x.data_ptr(), 64, 0, None, c.data_ptr(), 64, 0, None, 1,
+                           None, s) != 0
