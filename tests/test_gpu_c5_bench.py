@@ -28,7 +28,7 @@ from test_gpu_bf16 import group_scale, logits_ok, norm_ok
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-EXPECT = ["attn_poolL_fwd_fused_bf16<true", "attn_poolL_bwd_fused_bf16<true, ", "gemm_lds_kernel<0, 0, 32, 3, 1, 1>",
+EXPECT = ["attn_poolL_fwd_fused_bf16<true", "attn_poolL_bwd_fused_bf16<true, ", "gemm_wsr_b16_kernel",
           "gemm_lds_kernel<1, 1, 32, 3, 1, 2>", "gemm_lds_kernel<0, 1, 32, 3, 1, 3>", "pool_e_kernel",
           "cvt_bf16_kernel", "attn_keep_words_kernel"]
 
