@@ -900,9 +900,11 @@ if constexpr (BF != 0) {
 // boundaries; the epilogue stores 4 bf16 per lane straight from the accumulators.  Persistent
 // grid, 2 workgroups per CU; the two column groups of one GEMM are adjacent, so their workgroups
 // (16 apart in dispatch order at C5: the same XCD) read the same X rows at about the same time.
-constexpr int WSR16_NS = 6, WSR16_NKS = 16;   // ring depth, max 16-deep k-steps (K <= 256)
+constexpr int WSR16_NKS = 16;   // max 16-deep k-steps (K <= 256)
 typedef __bf16 bf16x4s __attribute__((ext_vector_type(4)));
 
+// WSR16_NS: the ring depth (tiles of 8 KB; WSR16_NS - 1 in flight ahead of the one being consumed)
+template <int WSR16_NS>
 __global__ __launch_bounds__(NT, 2) void gemm_wsr_b16_kernel(const GemmArgs args, int total_items, int K) {
   constexpr int DTILE = BM * 32 / 2;   // floats per bf16 tile
   __shared__ __attribute__((aligned(16))) float ring[WSR16_NS * DTILE];
@@ -941,26 +943,19 @@ __global__ __launch_bounds__(NT, 2) void gemm_wsr_b16_kernel(const GemmArgs args
     }
   };
   // as gemm_wsr_kernel: 2 LDS-DMAs per wave per k-tile, 16 epilogue stores per wave per row tile
+  // (vmcnt counts both, in issue order; the counter holds up to 63)
   auto wait_ahead = [&](int ahead, bool stores_younger) {
-    if (stores_younger) {
-      switch (ahead) {
-        case 0: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-        case 1: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
-        case 2: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
-        case 3: asm volatile("s_waitcnt vmcnt(22)" ::: "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
-      }
-    } else {
-      switch (ahead) {
-        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-        case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-        case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-        case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-      }
+    const int n = 2 * ahead + (stores_younger ? 16 : 0);
+    switch (n) {
+#define MMF_WC(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+      MMF_WC(0) MMF_WC(2) MMF_WC(4) MMF_WC(6) MMF_WC(8) MMF_WC(10) MMF_WC(12) MMF_WC(14) MMF_WC(16)
+      MMF_WC(18) MMF_WC(20) MMF_WC(22) MMF_WC(24) MMF_WC(26) MMF_WC(28) MMF_WC(30) MMF_WC(32) MMF_WC(34)
+      MMF_WC(36) MMF_WC(38) MMF_WC(40) MMF_WC(42)
+#undef MMF_WC
+      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     }
   };
-  static_assert(WSR16_NS - 2 <= 4, "wait_ahead covers 4 tiles ahead");
+  static_assert(2 * (WSR16_NS - 2) + 16 <= 42, "wait_ahead's table");
 
   int nissued = 0;
   for (; nissued < WSR16_NS - 1 && nissued < nflat; ++nissued) issue(nissued);
@@ -1846,8 +1841,15 @@ hipError_t launch_wsr_b16(const GemmJob* jobs, int njobs, hipStream_t st) {
     }
     args.ngroups = ng;
     const int grid = std::min(items, 2 * cu_count());
-    ProfLaunch prof_(st, "gemm_wsr_b16_kernel", fl, by);
-    mmf_launch(gemm_wsr_b16_kernel, dim3(grid), dim3(NT), 0, st, args, items, K);
+    // ring depth: 9 tiles (72 KB: two workgroups per CU), MMF_WSR16_NS=6 the first form (A/B)
+    const char* ns = getenv("MMF_WSR16_NS");
+    if (ns && ns[0] == '6') {
+      ProfLaunch prof_(st, "gemm_wsr_b16_kernel<6>", fl, by);
+      mmf_launch(gemm_wsr_b16_kernel<6>, dim3(grid), dim3(NT), 0, st, args, items, K);
+    } else {
+      ProfLaunch prof_(st, "gemm_wsr_b16_kernel<9>", fl, by);
+      mmf_launch(gemm_wsr_b16_kernel<9>, dim3(grid), dim3(NT), 0, st, args, items, K);
+    }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
