@@ -1745,6 +1745,10 @@ __global__ __launch_bounds__(256) void cvt_bf16_kernel(const CvtArgs a) {
   const float* s = a.src[q];
   __bf16* d = a.dst[q];
   const int64_t n = a.n[q];
+  if (float* d32 = a.dst32[q]) {   // (fp32 copy: the concatenated Q/K bias vectors)
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) d32[i] = s[i];
+    return;
+  }
   for (int64_t i = 4 * ((int64_t)blockIdx.x * 256 + threadIdx.x); i < n; i += 4 * (int64_t)gridDim.x * 256) {
     if (i + 4 <= n) {
       const float4 v = *reinterpret_cast<const float4*>(s + i);
@@ -1761,11 +1765,11 @@ hipError_t launch_cvt_bf16(const CvtArgs& a, hipStream_t st) {
   int64_t mx = 0;
   double by = 0.0;
   for (int i = 0; i < a.count; ++i) {
-    if (((uintptr_t)a.src[i] & 15) != 0) return hipErrorInvalidValue;
-    mx = std::max<int64_t>(mx, a.n[i]);
-    by += 6.0 * a.n[i];
+    if (!a.dst32[i] && ((uintptr_t)a.src[i] & 15) != 0) return hipErrorInvalidValue;
+    mx = std::max<int64_t>(mx, a.dst32[i] ? a.n[i] : a.n[i] / 4);   // elements (copy) / float4s per thread pass
+    by += (a.dst32[i] ? 8.0 : 6.0) * a.n[i];
   }
-  const int gx = (int)std::min<int64_t>((mx / 4 + 255) / 256, 64);
+  const int gx = (int)std::min<int64_t>((mx + 255) / 256, 64);
   ProfLaunch prof_(st, "cvt_bf16_kernel", 0.0, by);
   mmf_launch(cvt_bf16_kernel, dim3(std::max(gx, 1), a.count), dim3(256), 0, st, a);
   return hipGetLastError();
@@ -1797,7 +1801,10 @@ bool job_wsr_b16(const GemmJob& J) {
   const GemmGroup& g = J.g;
   if (J.nsrc != 1 || g.nbatch > 1 || g.seg_rows > 0 || !(g.epi & EPI_BF16) || (g.epi & ~(EPI_BIAS | EPI_BF16))) return false;
   const GemmSrc& s = J.src[0];
-  return g.M % BM == 0 && g.N % BN == 0 && s.K % 32 == 0 && s.K >= 32 && s.K <= 16 * WSR16_NKS && s.a.row_div == 1 &&
+  // (N <= 256: wider outputs -- the concatenated Q / K blocks -- would re-read X per 128-column group;
+  // the LDS-DMA kernel's XCD-aware tile order reads it once)
+  return g.M % BM == 0 && g.N % BN == 0 && g.N <= 2 * BN && s.K % 32 == 0 && s.K >= 32 && s.K <= 16 * WSR16_NKS &&
+         s.a.row_div == 1 &&
          s.b.row_div == 1 && s.a.seg_stride == 0 && s.a.ld % 8 == 0 && s.b.ld % 8 == 0 && aligned16(s.a.ptr) &&
          aligned16(s.b.ptr) && g.ldc % 4 == 0 && ((uintptr_t)g.C & 7) == 0;
 }

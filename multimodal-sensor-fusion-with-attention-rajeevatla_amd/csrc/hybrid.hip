@@ -110,6 +110,23 @@ bool qk_gemm_b16(const mmf_hybrid_desc* d) {
   return n > 0 && 2 * n <= CVT_MAX;
 }
 
+// The Q / K projections concatenated per modality ("medium", qk_gemm_b16): modality m's Q (pairs
+// with query m) and K (pairs with key m) are column blocks of one (B L_m) x (ncat_m H) bf16 matrix,
+// written by ONE bf16 GEMM of P_m against the stacked W_q / W_k copies (C5: 6 GEMMs of N = 2 560 in
+// place of 60 of N = 256, each P_m row read once); the attention kernels read Q / K (and write dQ /
+// dK) through ld = ncat_m H; the dZ GEMM is then one K = ncat_m H source.  Columns in pair order, a
+// pair's Q before its K.  MMF_NO_QK_CAT=1: one Q / K buffer per pair (A/B).
+bool qk_cat_on(const mmf_hybrid_desc* d) { return qk_gemm_b16(d) && !getenv("MMF_NO_QK_CAT"); }
+void qk_cols(const mmf_hybrid_desc* d, int* qcol, int* kcol, int* ncat) {
+  for (int m = 0; m < d->num_modalities; ++m) ncat[m] = 0;
+  for (int g = 0; g < d->num_pairs; ++g) {
+    qcol[g] = kcol[g] = -1;
+    if (single_key(d, g) || wide_pair(d, g)) continue;
+    qcol[g] = ncat[d->pair_q[g]]++;
+    kcol[g] = ncat[d->pair_k[g]]++;
+  }
+}
+
 // The backward on bf16 dQ / dK ("medium", every pair a bf16 Q/K pair of the one-pass kernels):
 // attn_poolL_bwd_fused_bf16 stores dQ / dK as bf16 -- the rounding their GEMM consumers' MFMA
 // operands get anyway -- and the dZ GEMM (dQ W_q + dK W_k, RK x KR on the forward's W_q / W_k
@@ -149,12 +166,23 @@ struct Saved {
   float *pooled, *scores, *weights, *fused, *h1;
   __bf16* Pb[MMF_MAX_MODALITIES];                  // bf16 copies of P_m (qk_gemm_b16)
   __bf16 *Wqb[MMF_MAX_PAIRS], *Wkb[MMF_MAX_PAIRS];  // bf16 copies of W_q / W_k (qk_gemm_b16)
+  int32_t ldq[MMF_MAX_PAIRS], ldk[MMF_MAX_PAIRS];   // elements between Q (K) rows: H, or ncat H (qk_cat_on)
+  // qk_cat_on: per modality the Q / K block matrix, the stacked W copies (Wqb / Wkb point into
+  // them), the stacked biases, the column count; per pair its Q / K column slots
+  __bf16* QKc[MMF_MAX_MODALITIES];
+  __bf16* Wc[MMF_MAX_MODALITIES];
+  float* bc[MMF_MAX_MODALITIES];
+  int32_t ncat[MMF_MAX_MODALITIES];
+  int32_t qcol[MMF_MAX_PAIRS], kcol[MMF_MAX_PAIRS];
 };
 
 void layout_saved(const mmf_hybrid_desc* d, Bump& bp, Saved& s) {
   memset(&s, 0, sizeof(s));
   const size_t B = d->batch, H = d->hidden, M = d->num_modalities, nh = d->num_heads;
   const bool pool = use_pool(d);
+  const bool cat = qk_cat_on(d);
+  if (cat) qk_cols(d, s.qcol, s.kcol, s.ncat);
+  for (int g = 0; g < d->num_pairs; ++g) s.ldq[g] = s.ldk[g] = (int32_t)H;
   s.rng = bp.take<RngSnap>(1);
   for (int m = 0; m < d->num_modalities; ++m) s.Xd[m] = bp.take<float>(B * Lm(d, m) * d->in_dim[m]);
   for (int m = 0; m < d->num_modalities; ++m) s.P[m] = bp.take<float>(B * Lm(d, m) * H);
@@ -164,8 +192,10 @@ void layout_saved(const mmf_hybrid_desc* d, Bump& bp, Saved& s) {
     const size_t lq = Lm(d, d->pair_q[g]), lk = Lm(d, d->pair_k[g]);
     const bool sk = single_key(d, g), wide = wide_pair(d, g);
     if (!sk) {
-      s.Q[g] = bp.take<float>(B * lq * H);
-      s.K[g] = bp.take<float>(B * lk * H);
+      if (!cat) {
+        s.Q[g] = bp.take<float>(B * lq * H);
+        s.K[g] = bp.take<float>(B * lk * H);
+      }
       if (!wide) s.lse[g] = bp.take<float>(B * nh * lq);
     }
     if (wide) {
@@ -197,11 +227,31 @@ void layout_saved(const mmf_hybrid_desc* d, Bump& bp, Saved& s) {
     for (int g = 0; g < d->num_pairs; ++g)
       if (!single_key(d, g) && !wide_pair(d, g)) {
         used[d->pair_q[g]] = used[d->pair_k[g]] = true;
-        s.Wqb[g] = bp.take<__bf16>(H * H);
-        s.Wkb[g] = bp.take<__bf16>(H * H);
+        if (!cat) {
+          s.Wqb[g] = bp.take<__bf16>(H * H);
+          s.Wkb[g] = bp.take<__bf16>(H * H);
+        }
       }
     for (int m = 0; m < d->num_modalities; ++m)
       if (used[m]) s.Pb[m] = bp.take<__bf16>(B * Lm(d, m) * H);
+  }
+  if (cat) {
+    for (int m = 0; m < d->num_modalities; ++m)
+      if (s.ncat[m] > 0) {
+        s.QKc[m] = bp.take<__bf16>(B * Lm(d, m) * s.ncat[m] * H);
+        s.Wc[m] = bp.take<__bf16>((size_t)s.ncat[m] * H * H);
+        s.bc[m] = bp.take<float>((size_t)s.ncat[m] * H);
+      }
+    for (int g = 0; g < d->num_pairs; ++g) {
+      if (s.qcol[g] < 0) continue;
+      const int q = d->pair_q[g], k = d->pair_k[g];
+      s.Q[g] = reinterpret_cast<float*>(s.QKc[q] + (size_t)s.qcol[g] * H);
+      s.K[g] = reinterpret_cast<float*>(s.QKc[k] + (size_t)s.kcol[g] * H);
+      s.ldq[g] = s.ncat[q] * (int32_t)H;
+      s.ldk[g] = s.ncat[k] * (int32_t)H;
+      s.Wqb[g] = s.Wc[q] + (size_t)s.qcol[g] * H * H;
+      s.Wkb[g] = s.Wc[k] + (size_t)s.kcol[g] * H * H;
+    }
   }
 }
 
@@ -213,12 +263,18 @@ struct Ws {
   float *dS[MMF_MAX_PAIRS], *dPd[MMF_MAX_PAIRS];                             // wide pairs
   float* E[MMF_MAX_MODALITIES];                                              // pooled
   float* dZ[MMF_MAX_MODALITIES];
+  // qk_cat_on: per modality the dQ / dK block matrix (the layout of Saved::QKc: fp32-sized, bf16
+  // when dqk_b16_on); dQ / dK point into it
+  float* dQc[MMF_MAX_MODALITIES];
 };
 
 void layout_ws(const mmf_hybrid_desc* d, Bump& bp, Ws& w) {
   memset(&w, 0, sizeof(w));
   const size_t B = d->batch, H = d->hidden, M = d->num_modalities, nh = d->num_heads;
   const bool pool = use_pool(d);
+  const bool cat = qk_cat_on(d), b16 = dqk_b16_on(d);
+  int qcol[MMF_MAX_PAIRS], kcol[MMF_MAX_PAIRS], ncat[MMF_MAX_MODALITIES];
+  if (cat) qk_cols(d, qcol, kcol, ncat);
   w.dz1 = bp.take<float>(B * H);
   w.dfused = bp.take<float>(B * H);
   w.cvec = bp.take<float>(B * M * H);
@@ -226,8 +282,10 @@ void layout_ws(const mmf_hybrid_desc* d, Bump& bp, Ws& w) {
   for (int g = 0; g < d->num_pairs; ++g) {
     const size_t lq = Lm(d, d->pair_q[g]), lk = Lm(d, d->pair_k[g]);
     if (!single_key(d, g)) {
-      w.dQ[g] = bp.take<float>(B * lq * H);
-      w.dK[g] = bp.take<float>(B * lk * H);
+      if (!cat) {
+        w.dQ[g] = bp.take<float>(B * lq * H);
+        w.dK[g] = bp.take<float>(B * lk * H);
+      }
       w.dsum[g] = bp.take<float>(B * nh * lq);
     }
     if (wide_pair(d, g)) {
@@ -246,6 +304,20 @@ void layout_ws(const mmf_hybrid_desc* d, Bump& bp, Ws& w) {
   for (int m = 0; m < d->num_modalities; ++m) {
     if (pool) w.E[m] = bp.take<float>(B * Lm(d, m) * H);
     w.dZ[m] = bp.take<float>(B * Lm(d, m) * H);
+  }
+  if (cat) {
+    for (int m = 0; m < d->num_modalities; ++m)
+      if (ncat[m] > 0) w.dQc[m] = bp.take<float>(B * Lm(d, m) * ncat[m] * H);
+    // (element offsets of the column slots: bf16 or fp32 elements, as the attention backward writes)
+    auto slot = [&](int m, int col) -> float* {
+      return b16 ? reinterpret_cast<float*>(reinterpret_cast<__bf16*>(w.dQc[m]) + (size_t)col * H)
+                 : w.dQc[m] + (size_t)col * H;
+    };
+    for (int g = 0; g < d->num_pairs; ++g) {
+      if (qcol[g] < 0) continue;
+      w.dQ[g] = slot(d->pair_q[g], qcol[g]);
+      w.dK[g] = slot(d->pair_k[g], kcol[g]);
+    }
   }
 }
 
@@ -360,10 +432,10 @@ void plan_wgrads(const mmf_hybrid_desc* d, const float* const* x, const float* m
     const float* pq = b16 ? reinterpret_cast<const float*>(s.Pb[q]) : s.P[q];
     const float* pk = b16 ? reinterpret_cast<const float*>(s.Pb[k]) : s.P[k];
     wp.split_hint = hint(B * lq);
-    plan_wgrad(wp, bw, H, H, B * lq, opnd(w.dQ[p], H), opnd(pq, H), g->q[p].w, g->q[p].b);
+    plan_wgrad(wp, bw, H, H, B * lq, opnd(w.dQ[p], s.ldq[p]), opnd(pq, H), g->q[p].w, g->q[p].b);
     if (b16 && !wp.size_only) { wp.jobs_b16.push_back(wp.jobs.back()); wp.jobs.pop_back(); }
     wp.split_hint = hint(B * lk);
-    plan_wgrad(wp, bw, H, H, B * lk, opnd(w.dK[p], H), opnd(pk, H), g->k[p].w, g->k[p].b);
+    plan_wgrad(wp, bw, H, H, B * lk, opnd(w.dK[p], s.ldk[p]), opnd(pk, H), g->k[p].w, g->k[p].b);
     if (b16 && !wp.size_only) { wp.jobs_b16.push_back(wp.jobs.back()); wp.jobs.pop_back(); }
     wp.split_hint = 0;
   }
@@ -481,7 +553,9 @@ AttnPair make_pair(const mmf_hybrid_desc* d, const Saved& s, const float* mask, 
   a.q = s.Q[g]; a.k = s.K[g]; a.v = s.V[g]; a.o = s.O[g]; a.lse = s.lse[g];
   a.kmask = mask + k; a.kmask_mode = 1; a.kmask_ld = d->num_modalities;
   a.Lq = Lm(d, q); a.Lk = Lm(d, k);
-  a.ldq = a.ldk = a.ldv = a.ldo = d->hidden;
+  a.ldv = a.ldo = d->hidden;
+  a.ldq = s.ldq[g];
+  a.ldk = s.ldk[g];
   a.drop_site = SITE_ATTN + g;
   a.pbar = s.pbar[g];
   a.pbarT = s.pbarT[g];
@@ -817,7 +891,40 @@ static int hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, 
                                            const_cast<uint64_t*>(rng_state)));
   }
   // (2) Q/K (and V for the general plan) projections of every present pair (attention.py:104-106)
-  if (d->num_pairs && qk_gemm_b16(d)) {
+  if (d->num_pairs && qk_cat_on(d)) {
+    // the stacked bf16 W copies and fp32 biases per modality, then one bf16 GEMM per modality
+    // writing every Q / K column block of it (see qk_cat_on)
+    std::vector<CvtArgs> cvs(1);
+    memset(&cvs[0], 0, sizeof(CvtArgs));
+    auto add_cvt = [&](const float* src, __bf16* dst, float* dst32, int64_t n) {
+      if (cvs.back().count == CVT_MAX) {
+        cvs.emplace_back();
+        memset(&cvs.back(), 0, sizeof(CvtArgs));
+      }
+      CvtArgs& c = cvs.back();
+      c.src[c.count] = src; c.dst[c.count] = dst; c.dst32[c.count] = dst32; c.n[c.count++] = n;
+    };
+    for (int g = 0; g < d->num_pairs; ++g) {
+      if (s.qcol[g] < 0) continue;
+      const int q = d->pair_q[g], k = d->pair_k[g];
+      add_cvt(W->q[g].w, s.Wqb[g], nullptr, (int64_t)H * H);
+      add_cvt(W->k[g].w, s.Wkb[g], nullptr, (int64_t)H * H);
+      add_cvt(W->q[g].b, nullptr, s.bc[q] + (size_t)s.qcol[g] * H, H);
+      add_cvt(W->k[g].b, nullptr, s.bc[k] + (size_t)s.kcol[g] * H, H);
+    }
+    std::vector<GemmJob> jobs;
+    auto bop = [](const __bf16* p, int ld) { return opnd(reinterpret_cast<const float*>(p), ld); };
+    for (int m = 0; m < M; ++m) {
+      if (s.ncat[m] <= 0) continue;
+      const int N = s.ncat[m] * H;
+      GemmJob j = make_job(B * Lm(d, m), N, reinterpret_cast<float*>(s.QKc[m]), N, EPI_BIAS | EPI_BF16);
+      j.g.bias = s.bc[m];
+      add_src(j, bop(s.Pb[m], H), bop(s.Wc[m], H), H);
+      jobs.push_back(j);
+    }
+    for (const CvtArgs& c : cvs) STAGE_TRY("fwd.qk_cvt", launch_cvt_bf16(c, st));
+    STAGE_TRY("fwd.qkv_gemm", launch_gemm_b16(jobs.data(), (int)jobs.size(), st));
+  } else if (d->num_pairs && qk_gemm_b16(d)) {
     // bf16 copies of W_q / W_k, then one bf16-operand GEMM launch over every Q / K projection
     CvtArgs cv;
     memset(&cv, 0, sizeof(cv));
@@ -1209,15 +1316,22 @@ static int hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W,
       j.g.ld_gate = H;
       j.g.gate_scale = gscale;
       const bool b16 = dqk_b16_on(d);
-      for (int g = 0; g < d->num_pairs; ++g) {
-        const bool sk = single_key(d, g);
-        // (bf16: dQ / dK and the forward's W_q / W_k copies, launch_gemm_b16's RK x KR form)
-        const float* wq = b16 ? reinterpret_cast<const float*>(s.Wqb[g]) : W->q[g].w;
-        const float* wk = b16 ? reinterpret_cast<const float*>(s.Wkb[g]) : W->k[g].w;
-        if (d->pair_q[g] == m && !sk) add_src(j, opnd(w.dQ[g], H), opnd(wq, H), H);
-        if (d->pair_k[g] == m) {
-          if (!sk) add_src(j, opnd(w.dK[g], H), opnd(wk, H), H);
-          if (!pool) add_src(j, opnd(w.dV[g], H), opnd(W->v[g].w, H), H);
+      if (b16 && qk_cat_on(d)) {
+        // one source: the modality's dQ / dK block matrix against its stacked W copies (K = ncat H,
+        // the slots in the order the separate sources had)
+        if (s.ncat[m] > 0)
+          add_src(j, opnd(w.dQc[m], s.ncat[m] * H), opnd(reinterpret_cast<const float*>(s.Wc[m]), H), s.ncat[m] * H);
+      } else {
+        for (int g = 0; g < d->num_pairs; ++g) {
+          const bool sk = single_key(d, g);
+          // (bf16: dQ / dK and the forward's W_q / W_k copies, launch_gemm_b16's RK x KR form)
+          const float* wq = b16 ? reinterpret_cast<const float*>(s.Wqb[g]) : W->q[g].w;
+          const float* wk = b16 ? reinterpret_cast<const float*>(s.Wkb[g]) : W->k[g].w;
+          if (d->pair_q[g] == m && !sk) add_src(j, opnd(w.dQ[g], s.ldq[g]), opnd(wq, H), H);
+          if (d->pair_k[g] == m) {
+            if (!sk) add_src(j, opnd(w.dK[g], s.ldk[g]), opnd(wk, H), H);
+            if (!pool) add_src(j, opnd(w.dV[g], H), opnd(W->v[g].w, H), H);
+          }
         }
       }
       if (pe) {

@@ -237,7 +237,8 @@ struct ReduceJob {
 hipError_t launch_gemm_b16(const GemmJob* jobs, int njobs, hipStream_t st, int amode = MODE_RK, int bmode = MODE_RK);
 constexpr int CVT_MAX = 64;
 struct CvtArgs {
-  const float* src[CVT_MAX]; __bf16* dst[CVT_MAX]; int64_t n[CVT_MAX]; int32_t count;
+  // dst[i] (bf16, round to nearest even) or, where dst32[i] is set, an fp32 copy into dst32[i]
+  const float* src[CVT_MAX]; __bf16* dst[CVT_MAX]; float* dst32[CVT_MAX]; int64_t n[CVT_MAX]; int32_t count;
 };
 hipError_t launch_cvt_bf16(const CvtArgs& a, hipStream_t st);
 bool gemm_b16_ok(const GemmJob& J, int amode = MODE_RK, int bmode = MODE_RK);
