@@ -115,8 +115,11 @@ bool qk_gemm_b16(const mmf_hybrid_desc* d) {
 // written by ONE bf16 GEMM of P_m against the stacked W_q / W_k copies (C5: 6 GEMMs of N = 2 560 in
 // place of 60 of N = 256, each P_m row read once); the attention kernels read Q / K (and write dQ /
 // dK) through ld = ncat_m H; the dZ GEMM is then one K = ncat_m H source.  Columns in pair order, a
-// pair's Q before its K.  MMF_NO_QK_CAT=1: one Q / K buffer per pair (A/B).
-bool qk_cat_on(const mmf_hybrid_desc* d) { return qk_gemm_b16(d) && !getenv("MMF_NO_QK_CAT"); }
+// pair's Q before its K.  Opt-in (MMF_QK_CAT=1): measured at C5 it is slower -- 13.05 / 13.35 ms
+// against 12.62 / 12.62 (profiles/r05/c5_qk_cat/): the 2 560-column GEMM on the LDS-DMA kernel
+// (1.75 ms) loses to the weight-stationary per-pair GEMMs (1.46 ms), and the attention kernels'
+// head-slice rows 5 KB apart instead of 512 B cost them 2-3 %.
+bool qk_cat_on(const mmf_hybrid_desc* d) { return qk_gemm_b16(d) && getenv("MMF_QK_CAT"); }
 void qk_cols(const mmf_hybrid_desc* d, int* qcol, int* kcol, int* ncat) {
   for (int m = 0; m < d->num_modalities; ++m) ncat[m] = 0;
   for (int g = 0; g < d->num_pairs; ++g) {
