@@ -470,10 +470,7 @@ struct FwdLds {
   static constexpr int BYTES = S + 2 * NW * LF_QB * 4;       // 28 KB (8 waves) / 48 KB (16)
 };
 
-// ONEBAR: one barrier per query block -- each wave exponentiates against its own row max and the
-// waves' (max, sum) pairs combine at that barrier (exp2(m_w - m) rescales); otherwise the global
-// row max first (barrier A), then the sums (barrier B)
-template <bool DROP, int NW = 16, bool ONEBAR = true>
+template <bool DROP, int NW = 16>
 __global__ __launch_bounds__(NW * 64, 1) void attn_poolL_fwd_fused_bf16(const AttnArgs A) {
   constexpr int NTW = NW * 64, TPW = 16 / NW;   // threads; key tiles per wave (Lk <= 512)
   using L_ = FwdLds<NW>;
@@ -586,76 +583,33 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_poolL_fwd_fused_bf16(const At
       }
     }
     mx = max_xor32(mx) * sl2;   // log2 units (max(s) * c == max(s * c) for c > 0)
-    float m, l, mw;             // the row's max over every key, its sum, this wave's max
-    if constexpr (ONEBAR) {
-      // exponents against the wave's own row max (no barrier for the global one): the waves'
-      // (max, sum) pairs meet once, at barrier B, and each wave's P' carries exp2(m_w - m)
-      mw = mx;
-      const float mref = mw == -INFINITY ? 0.f : mw;
-      float ls = 0.f;
+    if (hh == 0) Mpart[buf * NW * 32 + w * 32 + r] = mx;
+    if (has_next) q_store(buf ^ 1, nv);
+    __syncthreads();   // (A) row maxima, next query block
+    if (has_next) scores(buf ^ 1, sn);
+    float m = -INFINITY;
 #pragma unroll
-      for (int i = 0; i < TPW; ++i) {
-        if (w + NW * i >= nkt) continue;   // wave-uniform
-        f32x2 pr[8];
+    for (int ww = 0; ww < NW; ++ww) m = fmaxf(m, Mpart[buf * NW * 32 + ww * 32 + r]);
+    const float mref = m == -INFINITY ? 0.f : m;
+    // row sums as packed trees (v_pk_add_f32, two adds per instruction, no serial chain)
+    float ls = 0.f;
 #pragma unroll
-        for (int e = 0; e < 16; e += 2) {
-          x[i][e] = __builtin_amdgcn_exp2f(__builtin_fmaf(x[i][e], sl2, -mref));
-          x[i][e + 1] = __builtin_amdgcn_exp2f(__builtin_fmaf(x[i][e + 1], sl2, -mref));
-          pr[e >> 1] = f32x2{x[i][e], x[i][e + 1]};
-        }
-        ls += tree_sum<8>(pr);
+    for (int i = 0; i < TPW; ++i) {
+      if (w + NW * i >= nkt) continue;   // wave-uniform
+      f32x2 pr[8];
+#pragma unroll
+      for (int e = 0; e < 16; e += 2) {
+        x[i][e] = __builtin_amdgcn_exp2f(__builtin_fmaf(x[i][e], sl2, -mref));
+        x[i][e + 1] = __builtin_amdgcn_exp2f(__builtin_fmaf(x[i][e + 1], sl2, -mref));
+        pr[e >> 1] = f32x2{x[i][e], x[i][e + 1]};
       }
-      ls = sum_xor32(ls);
-      if (hh == 0) {
-        Mpart[buf * NW * 32 + w * 32 + r] = mw;
-        Spart[buf * NW * 32 + w * 32 + r] = ls;
-      }
-      if (has_next) q_store(buf ^ 1, nv);
-      __syncthreads();   // (B) row maxima and sums, next query block
-      if (has_next) scores(buf ^ 1, sn);
-      float mv[NW], sp[NW];
-#pragma unroll
-      for (int ww = 0; ww < NW; ++ww) {
-        mv[ww] = Mpart[buf * NW * 32 + ww * 32 + r];
-        sp[ww] = Spart[buf * NW * 32 + ww * 32 + r];
-      }
-      m = -INFINITY;
-#pragma unroll
-      for (int ww = 0; ww < NW; ++ww) m = fmaxf(m, mv[ww]);
-#pragma unroll
-      for (int ww = 0; ww < NW; ++ww) sp[ww] = mv[ww] == -INFINITY ? 0.f : sp[ww] * __builtin_amdgcn_exp2f(mv[ww] - m);
-#pragma unroll
-      for (int n = NW / 2; n >= 1; n /= 2)
-#pragma unroll
-        for (int i = 0; i < n; ++i) sp[i] += sp[i + n];
-      l = sp[0];
-    } else {
-      if (hh == 0) Mpart[buf * NW * 32 + w * 32 + r] = mx;
-      if (has_next) q_store(buf ^ 1, nv);
-      __syncthreads();   // (A) row maxima, next query block
-      if (has_next) scores(buf ^ 1, sn);
-      m = -INFINITY;
-#pragma unroll
-      for (int ww = 0; ww < NW; ++ww) m = fmaxf(m, Mpart[buf * NW * 32 + ww * 32 + r]);
-      mw = m;
-      const float mref = m == -INFINITY ? 0.f : m;
-      // row sums as packed trees (v_pk_add_f32, two adds per instruction, no serial chain)
-      float ls = 0.f;
-#pragma unroll
-      for (int i = 0; i < TPW; ++i) {
-        if (w + NW * i >= nkt) continue;   // wave-uniform
-        f32x2 pr[8];
-#pragma unroll
-        for (int e = 0; e < 16; e += 2) {
-          x[i][e] = __builtin_amdgcn_exp2f(__builtin_fmaf(x[i][e], sl2, -mref));
-          x[i][e + 1] = __builtin_amdgcn_exp2f(__builtin_fmaf(x[i][e + 1], sl2, -mref));
-          pr[e >> 1] = f32x2{x[i][e], x[i][e + 1]};
-        }
-        ls += tree_sum<8>(pr);
-      }
-      ls = sum_xor32(ls);
-      if (hh == 0) Spart[buf * NW * 32 + w * 32 + r] = ls;
-      __syncthreads();   // (B) row sums
+      ls += tree_sum<8>(pr);
+    }
+    ls = sum_xor32(ls);
+    if (hh == 0) Spart[buf * NW * 32 + w * 32 + r] = ls;
+    __syncthreads();   // (B) row sums
+    float l;
+    {
       float sp[NW];   // (scalar tree: packed adds would need the ds_read2 pairs re-registered)
 #pragma unroll
       for (int ww = 0; ww < NW; ++ww) sp[ww] = Spart[buf * NW * 32 + ww * 32 + r];
@@ -666,10 +620,8 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_poolL_fwd_fused_bf16(const At
       l = sp[0];
     }
     if (w == 0 && hh == 0 && qvalid) P.lse[bh * Lq + q] = l > 0.f ? (m + __log2f(l)) * (1.f / LF_LOG2E) : -INFINITY;
-    // P' / Lq of this lane's query (0 for a query past Lq), with this wave's exponent reference
-    const float cq = (qvalid && l > 0.f && mw != -INFINITY)
-                         ? inv_keep * __builtin_amdgcn_exp2f(mw - m) * __builtin_amdgcn_rcpf(l * (float)Lq)
-                         : 0.f;
+    // P' / Lq of this lane's query (0 for a query past Lq)
+    const float cq = (qvalid && l > 0.f) ? inv_keep * __builtin_amdgcn_rcpf(l * (float)Lq) : 0.f;
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
       const int kt = w + NW * i;
@@ -823,9 +775,6 @@ hipError_t launch_attn_long_fused_fwd(const AttnPair* pairs, int npairs, int B, 
     if (w8) {
       if (drop) mmf_launch(attn_poolL_fwd_fused_bf16<true, 8>, grid, dim3(8 * 64), 0, st, a);
       else mmf_launch(attn_poolL_fwd_fused_bf16<false, 8>, grid, dim3(8 * 64), 0, st, a);
-    } else if (getenv("MMF_FWD_TWOBAR")) {   // (the two-barrier form, A/B)
-      if (drop) mmf_launch((attn_poolL_fwd_fused_bf16<true, 16, false>), grid, dim3(16 * 64), 0, st, a);
-      else mmf_launch((attn_poolL_fwd_fused_bf16<false, 16, false>), grid, dim3(16 * 64), 0, st, a);
     } else {
       if (drop) mmf_launch(attn_poolL_fwd_fused_bf16<true, 16>, grid, dim3(16 * 64), 0, st, a);
       else mmf_launch(attn_poolL_fwd_fused_bf16<false, 16>, grid, dim3(16 * 64), 0, st, a);
