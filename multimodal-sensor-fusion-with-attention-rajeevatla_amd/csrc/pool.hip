@@ -228,80 +228,6 @@ __global__ __launch_bounds__(NT) void pool_u_grp_kernel(const PoolGrpArgs a) {
 
 // dpbar_row[j] = P_k[b][j] . dU_row + dObar_row . b_v,row: half a wave per key, lanes over the
 // columns, every row's dot summed over the 32 lanes (permlane / DPP)
-// pool_u_grp_kernel with the key range split over the 4 waves (R <= 24 rows, H <= 256): each wave
-// reads a quarter of P_k[b]'s rows once and accumulates all R rows of U (pool_u_grp_kernel's waves
-// each read the whole P_k[b] for a quarter of the rows: 4 reads of every row from L2, 0.25 ms at
-// C5), then the four partial U's meet in LDS (over the no longer needed pbar image).
-constexpr int POOL_SPLIT_ROWS = 24;
-__global__ __launch_bounds__(NT) void pool_u_grp_split_kernel(const PoolGrpArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];   // [R][Lk] pbar, then [3][R][H] partials
-  const int b = blockIdx.x, gi = blockIdx.y, t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int beg = a.gbeg[gi], heads = a.heads, H = a.H, H4 = H / 4;
-  const int R = a.gcnt[gi] * heads, Lk = a.p[beg].Lk;
-  for (int i = t; i < R * Lk; i += NT) {
-    const int row = i / Lk, j = i - row * Lk;
-    const PoolPair& P = a.p[beg + row / heads];
-    sm[i] = P.pbar[((int64_t)b * heads + row % heads) * Lk + j];
-  }
-  __syncthreads();
-  for (int row = wave; row < R; row += NT / 64) {
-    float s = 0.f;
-    for (int j = lane; j < Lk; j += 64) s += sm[row * Lk + j];
-    s = sum64(s);
-    if (lane == 0) a.p[beg + row / heads].r[(int64_t)b * heads + row % heads] = s;
-  }
-  const int c4 = lane;
-  const bool col = c4 < H4;
-  float4 acc[POOL_SPLIT_ROWS];
-#pragma unroll
-  for (int i = 0; i < POOL_SPLIT_ROWS; ++i) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  const int jper = (Lk + 3) / 4, j0 = wave * jper, j1 = min(Lk, j0 + jper);
-  const float* pk = a.p[beg].pk + (int64_t)b * Lk * H + 4 * (col ? c4 : 0);
-  int j = j0;
-  for (; j + 2 <= j1; j += 2) {
-    const float4 v0 = *reinterpret_cast<const float4*>(pk + (int64_t)j * H);
-    const float4 v1 = *reinterpret_cast<const float4*>(pk + (int64_t)(j + 1) * H);
-#pragma unroll
-    for (int row = 0; row < POOL_SPLIT_ROWS; ++row) {
-      if (row < R) {
-        const float w0 = sm[row * Lk + j], w1 = sm[row * Lk + j + 1];
-        acc[row].x += w0 * v0.x + w1 * v1.x; acc[row].y += w0 * v0.y + w1 * v1.y;
-        acc[row].z += w0 * v0.z + w1 * v1.z; acc[row].w += w0 * v0.w + w1 * v1.w;
-      }
-    }
-  }
-  if (j < j1) {
-    const float4 v0 = *reinterpret_cast<const float4*>(pk + (int64_t)j * H);
-#pragma unroll
-    for (int row = 0; row < POOL_SPLIT_ROWS; ++row) {
-      if (row < R) {
-        const float w0 = sm[row * Lk + j];
-        acc[row].x += w0 * v0.x; acc[row].y += w0 * v0.y; acc[row].z += w0 * v0.z; acc[row].w += w0 * v0.w;
-      }
-    }
-  }
-  __syncthreads();   // (the pbar image is read no more)
-  float4* part = reinterpret_cast<float4*>(sm);   // [3][R][H4]: waves 1..3; wave 0 sums
-  if (col && wave > 0) {
-#pragma unroll
-    for (int row = 0; row < POOL_SPLIT_ROWS; ++row)
-      if (row < R) part[((wave - 1) * R + row) * H4 + c4] = acc[row];
-  }
-  __syncthreads();
-  if (!col || wave != 0) return;
-#pragma unroll
-  for (int row = 0; row < POOL_SPLIT_ROWS; ++row) {
-    if (row >= R) continue;
-    float4 s = acc[row];
-#pragma unroll
-    for (int ww = 0; ww < 3; ++ww) {
-      const float4 v = part[(ww * R + row) * H4 + c4];
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-    }
-    *reinterpret_cast<float4*>(a.p[beg + row / heads].u + ((int64_t)b * heads + row % heads) * H + 4 * c4) = s;
-  }
-}
-
 __global__ __launch_bounds__(NT) void pool_dpbar_grp_kernel(const PoolGrpArgs a) {
   extern __shared__ __attribute__((aligned(16))) float dug[];   // [R][H]
   __shared__ float dr_s[POOL_GRP_ROWS];
@@ -369,11 +295,9 @@ bool launch_pool_grouped(bool fwd, const PoolPair* pairs, int npairs, int B, int
     groups[i].push_back(g);
   }
   if (groups.size() == (size_t)npairs) return false;   // nothing shared
-  bool split = fwd && H / 4 <= 64 && !getenv("MMF_POOLU_NOSPLIT");
   for (auto& gr : groups) {
     const int R = (int)gr.size() * heads, Lk = pairs[gr[0]].Lk;
     if (R > POOL_GRP_ROWS || (size_t)R * (fwd ? Lk : H) * sizeof(float) > 64 * 1024) return false;
-    split = split && R <= POOL_SPLIT_ROWS && (size_t)3 * R * H * sizeof(float) <= 64 * 1024;
   }
   size_t gi = 0;
   while (gi < groups.size()) {
@@ -388,7 +312,6 @@ bool launch_pool_grouped(bool fwd, const PoolPair* pairs, int npairs, int B, int
       const int Lk = pairs[groups[gi][0]].Lk, R = a.gcnt[ng] * heads;
       for (int g : groups[gi]) a.p[np++] = pairs[g];
       shm = std::max(shm, (size_t)R * (fwd ? Lk : H) * sizeof(float));
-      if (split) shm = std::max(shm, (size_t)3 * R * H * sizeof(float));
       fl += 2.0 * B * R * Lk * H;
       by += 4.0 * B * ((double)Lk * H + R * (Lk + H));   // P_k once per group
       ++ng;
@@ -396,9 +319,8 @@ bool launch_pool_grouped(bool fwd, const PoolPair* pairs, int npairs, int B, int
     }
     a.ngroups = ng;
     a.B = B; a.heads = heads; a.hd = hd; a.H = H;
-    ProfLaunch prof_(st, fwd ? (split ? "pool_u_grp_split_kernel" : "pool_u_grp_kernel") : "pool_dpbar_grp_kernel", fl, by);
-    if (fwd && split) mmf_launch(pool_u_grp_split_kernel, dim3(B, ng), dim3(NT), (uint32_t)shm, st, a);
-    else if (fwd) mmf_launch(pool_u_grp_kernel, dim3(B, ng), dim3(NT), (uint32_t)shm, st, a);
+    ProfLaunch prof_(st, fwd ? "pool_u_grp_kernel" : "pool_dpbar_grp_kernel", fl, by);
+    if (fwd) mmf_launch(pool_u_grp_kernel, dim3(B, ng), dim3(NT), (uint32_t)shm, st, a);
     else mmf_launch(pool_dpbar_grp_kernel, dim3(B, ng), dim3(NT), (uint32_t)shm, st, a);
     err = hipGetLastError();
     if (err != hipSuccess) return true;
