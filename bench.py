@@ -392,7 +392,8 @@ def main(argv=None):
     avg_ms = {k: t / n for k, (t, n) in per_stage.items()}
     kernels = kernel_table(launches, args.profile_steps)
 
-    graph = args.path == "step" and not args.no_graph
+    # (the launch-lean L = 1 step runs eagerly: HybridTrainStep.replay_pays)
+    graph = args.path == "step" and not args.no_graph and trainer.replay_pays()
     if graph:
         trainer.capture()
     for _ in range(args.warmup):
@@ -440,6 +441,8 @@ def main(argv=None):
         lens = Ls[0] if len(set(Ls)) == 1 else Ls
         mask_note = "" if w["keep"] >= 1 else f", modality masks keep={w['keep']} (+1% all-masked rows)"
         path_note = ("fused step (flat buffers, one hipGraph)" if graph else
+                     "fused step, eager launches (the 3-launch L = 1 step: a graph replay's boundary costs "
+                     "more than the dispatches it saves)" if args.path == "step" and not args.no_graph else
                      "fused step, eager" if args.path == "step" else
                      "nn.Module forward + autograd backward, eager (src/train.py's call path)"
                      if args.path == "module" else

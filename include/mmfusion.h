@@ -307,6 +307,11 @@ int mmf_adamw_step(int64_t n, float* param, const float* grad, float* exp_avg, f
  * points into -- and advance *step_dev, for mmf_clip_adamw_apply_dev (the L = 1 plan fills them in
  * its weight-gradient launch; others run the reduction pass of mmf_clip_adamw_step_dev here). */
 size_t mmf_hybrid_train_sync_bytes(const mmf_hybrid_desc* d);
+/* 1 when the launch-lean L = 1 plan serves this descriptor (2-D inputs, fp32 "highest", every
+ * ordered pair present, H <= 128, ...; given 16-byte aligned inputs and weights, as torch
+ * allocates them): its training step is three short launches, so a caller may prefer eager
+ * dispatch to a graph replay, whose boundary costs more on this stack (bench.py --workload c2_l1). */
+int mmf_hybrid_lean_l1(const mmf_hybrid_desc* d);
 /* Status of the train steps issued on `sync` so far: reads the sync buffer's error word on `stream`
  * (a 4-byte device-to-host copy, then a stream synchronize).  The launch-lean L = 1 step's waiting
  * workgroups poll for their tile's head a bounded number of times (co-residency is checked against

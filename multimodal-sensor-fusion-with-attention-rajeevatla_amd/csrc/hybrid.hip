@@ -605,17 +605,25 @@ SkPair make_sk(const mmf_hybrid_desc* d, const Saved& s, const float* mask, int 
 // slots (Ob = O = P' V, Ab = A, dOb = dV, dU = dP_k|g), so both plans size the buffers alike; the
 // choice depends only on the descriptor and the pointers forward and backward both receive.
 // MMF_NO_L1_LEAN=1: the general single-key plan (A/B).
-bool lean_l1(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, const float* const* x) {
+// the descriptor half of lean_l1 (the other half: 16-B aligned inputs and weights)
+bool lean_l1_desc(const mmf_hybrid_desc* d) {
   const bool off = getenv("MMF_NO_L1_LEAN") != nullptr;
   const int M = d->num_modalities, H = d->hidden;
-  if (off || d->matmul_precision != MMF_PRECISION_HIGHEST || !W || !x) return false;
+  if (off || d->matmul_precision != MMF_PRECISION_HIGHEST) return false;
   if (M < 2 || M > L1_MAXM || d->num_pairs != M * (M - 1)) return false;
   if (H % 4 != 0 || H > L1_MAXH || d->num_heads > 8 || d->num_classes > L1_MAXC) return false;
   unsigned seen = 0;
   for (int g = 0; g < d->num_pairs; ++g) seen |= 1u << (d->pair_q[g] * L1_MAXM + d->pair_k[g]);
   if (__builtin_popcount(seen) != d->num_pairs) return false;
-  for (int m = 0; m < M; ++m) {
+  for (int m = 0; m < M; ++m)
     if (Lm(d, m) != 1 || d->in_dim[m] % 4 != 0 || d->in_dim[m] > L1_MAXD) return false;
+  return true;
+}
+
+bool lean_l1(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, const float* const* x) {
+  const int M = d->num_modalities;
+  if (!W || !x || !lean_l1_desc(d)) return false;
+  for (int m = 0; m < M; ++m) {
     if (!aligned16(x[m]) || !aligned16(W->proj[m].w)) return false;
   }
   for (int g = 0; g < d->num_pairs; ++g)
@@ -1387,6 +1395,11 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
                         const float* mask, const void* saved, const float* dlogits, void* workspace,
                         const mmf_hybrid_grads* G, float* const* dx, void* stream) {
   return hybrid_backward(d, W, x, mask, saved, dlogits, workspace, G, dx, stream, false);
+}
+
+int mmf_hybrid_lean_l1(const mmf_hybrid_desc* d) {
+  if (check_hybrid(d) != MMF_OK) return 0;
+  return lean_l1_desc(d) ? 1 : 0;
 }
 
 size_t mmf_hybrid_train_sync_bytes(const mmf_hybrid_desc* d) {

@@ -50,7 +50,7 @@ EXPORTED_SYMBOLS = (
     "mmf_adaptive_weights_backward",
     "mmf_cma_saved_bytes", "mmf_cma_workspace_bytes", "mmf_cma_forward", "mmf_cma_backward",
     "mmf_cross_entropy_ls", "mmf_adamw_step", "mmf_adamw_step_dev", "mmf_grad_clip_workspace_bytes",
-    "mmf_grad_clip_coef", "mmf_clip_adamw_step_dev", "mmf_clip_adamw_apply_dev", "mmf_grad_accumulate", "mmf_gemm_bf16_workspace_bytes", "mmf_gemm_bf16", "mmf_profile_begin", "mmf_profile_end",
+    "mmf_grad_clip_coef", "mmf_clip_adamw_step_dev", "mmf_clip_adamw_apply_dev", "mmf_grad_accumulate", "mmf_gemm_bf16_workspace_bytes", "mmf_gemm_bf16", "mmf_hybrid_lean_l1", "mmf_profile_begin", "mmf_profile_end",
     "mmf_last_error", "mmf_version",
     "mmf_attention_pool_workspace_bytes", "mmf_attention_pool_forward", "mmf_attention_pool_backward",
     "mmf_late_fusion_workspace_bytes", "mmf_late_fusion_forward", "mmf_late_fusion_backward",
@@ -130,6 +130,8 @@ def lib() -> ctypes.CDLL:
     L.mmf_hybrid_backward.restype = c_int32
     L.mmf_hybrid_train_sync_bytes.argtypes = [POINTER(HybridDesc)]
     L.mmf_hybrid_train_sync_bytes.restype = sz
+    L.mmf_hybrid_lean_l1.argtypes = [POINTER(HybridDesc)]
+    L.mmf_hybrid_lean_l1.restype = c_int32
     L.mmf_hybrid_train_status.argtypes = [POINTER(HybridDesc), vp, c_int32, vp]
     L.mmf_hybrid_train_status.restype = c_int32
     L.mmf_hybrid_train_step.argtypes = [POINTER(HybridDesc), POINTER(HybridParams), vp, vp, vp, c_float, c_float,

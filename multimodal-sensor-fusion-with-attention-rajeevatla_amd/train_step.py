@@ -284,6 +284,15 @@ class HybridTrainStep:
         _nat.check(rc, "clip + AdamW")
 
     # ---------------------------------------------------------------- driver
+    def replay_pays(self) -> bool:
+        """Whether capturing the step into a graph makes it faster.  Not for the launch-lean L = 1
+        plan in one process (mmf_hybrid_lean_l1): its step is three short launches, and the graph
+        replay's boundary costs more than the dispatches it saves -- C2-L1 0.0607-0.0615 ms per
+        step replayed against 0.0573-0.0574 ms launched eagerly (profiles/r05/l1_eager/).  bench.py
+        asks this; capture() still captures when called."""
+        L = _nat.lib()
+        return not (self.world == 1 and not self.overlap and L.mmf_hybrid_lean_l1(ctypes.byref(self.plan.desc)) == 1)
+
     def capture(self) -> None:
         """Capture fwd+CE+bwd (and clip + AdamW when single-process) into one hipGraph; with
         several ranks, the train step's two parts into two graphs (the exchange of the first

@@ -139,3 +139,16 @@ def test_matmul_precision_follows_torch(nat):
             assert nat.matmul_precision() == want, mode
     finally:
         torch.set_float32_matmul_precision(prev)
+
+
+def test_lean_l1_query(nat):
+    """mmf_hybrid_lean_l1: the launch-lean L = 1 plan serves 2-D inputs at fp32 "highest" with every
+    ordered pair present (bench.py then launches its step eagerly, HybridTrainStep.replay_pays)."""
+    L = nat.lib()
+    d = _desc(nat)
+    assert L.mmf_hybrid_lean_l1(ctypes.byref(d)) == 1
+    for m in range(3):
+        d.seq_len[m] = 128
+    assert L.mmf_hybrid_lean_l1(ctypes.byref(d)) == 0
+    assert L.mmf_hybrid_lean_l1(ctypes.byref(_desc(nat, matmul_precision=nat.PRECISION_MEDIUM))) == 0
+    assert L.mmf_hybrid_lean_l1(ctypes.byref(_desc(nat, num_heads=3))) == 0   # invalid descriptor
