@@ -153,6 +153,23 @@ def rel_err(got, ref) -> float:
     return float((got - ref).abs().max() / max(float(ref.abs().max()), 1e-6))
 
 
+def diff_report(got, ref, rtol: float, atol: float = 0.0) -> str:
+    """For an assertion message: the largest |got - ref|, where it is, the two values there and
+    the bound close() applies."""
+    got = torch.as_tensor(got).double().cpu()
+    ref = torch.as_tensor(ref).double().cpu()
+    if got.shape != ref.shape or ref.numel() == 0:
+        return f"shapes {tuple(got.shape)} vs {tuple(ref.shape)}"
+    d = (got - ref).abs()
+    i = int(d.argmax())
+    idx = np.unravel_index(i, tuple(ref.shape))
+    bound = rtol * float(ref.abs().max()) + atol
+    nbad = int((d > bound).sum())
+    return (f"max|diff| {float(d.flatten()[i]):.3e} at {tuple(int(v) for v in idx)} (got "
+            f"{float(got.flatten()[i]):.6e}, ref {float(ref.flatten()[i]):.6e}), bound {bound:.3e}, "
+            f"{nbad} of {ref.numel()} elements over")
+
+
 def close(got, ref, rtol: float, atol: float = 0.0) -> bool:
     """max|got-ref| <= rtol*max|ref| + atol.  atol only matters for tensors whose
     reference is mathematically zero (e.g. key_proj.bias grads: softmax is
