@@ -124,6 +124,90 @@ __device__ __forceinline__ bf16x8 row_chunk(const float* base, bool bf, int64_t 
   return to_bf16x8(a, b);
 }
 
+#ifdef MMF_STAMPS
+// Diagnostic build only (make stampsl): per-phase s_memtime sums over the query blocks of wave 0
+// (slots 0..4) and of the first wave of the younger half (slots 5..8), and the workgroup's
+// s_memrealtime lifetime (slot 9, 100 MHz); read by mmf_long_stamps_read (scripts/attn_stamps.py
+// long / longf).  Never in the product library.
+__device__ __forceinline__ unsigned long long ls_now() {
+  unsigned long long t_;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t_;
+}
+__device__ __forceinline__ unsigned long long ls_rt() {
+  unsigned long long t_;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t_;
+}
+#define LS_DECL                                       \
+  unsigned long long ls_acc[5] = {0, 0, 0, 0, 0};     \
+  const unsigned long long ls_rt0 = ls_rt();          \
+  unsigned long long ls_prev = ls_now();
+#define LS_MARK(k)                                    \
+  {                                                   \
+    const unsigned long long t_ = ls_now();           \
+    ls_acc[k] += t_ - ls_prev;                        \
+    ls_prev = t_;                                     \
+  }
+#define LS_STORE(w, wy)                                                                        \
+  {                                                                                            \
+    const unsigned long long rt_ = ls_rt();                                                    \
+    const int sid_ = blockIdx.y * gridDim.x + blockIdx.x;                                      \
+    if ((threadIdx.x & 63) == 0 && sid_ < STAMP_WG) {                                          \
+      if ((w) == 0) {                                                                          \
+        for (int k_ = 0; k_ < 5; ++k_) g_mmf_stamps[sid_][k_] = ls_acc[k_];                   \
+        g_mmf_stamps[sid_][9] = rt_ - ls_rt0;                                                  \
+      } else if ((w) == (wy)) {                                                                \
+        for (int k_ = 0; k_ < 4; ++k_) g_mmf_stamps[sid_][5 + k_] = ls_acc[k_];               \
+      }                                                                                        \
+    }                                                                                          \
+  }
+#else
+#define LS_DECL
+#define LS_MARK(k)
+#define LS_STORE(w, wy)
+#endif
+
+// Prefetches that stay in flight: ONE unconditional load at a clamped, in-bounds address and no
+// use of the loaded register until the consumer (the image store a phase later, or the next
+// block).  A guarded load (a per-lane zero fill) or a shift / conversion right behind the load
+// is a use: the compiler waits for it there (s_waitcnt vmcnt(0) behind every prefetch: three
+// global round trips exposed in every query block of both kernels).  Validity is applied where
+// the value is consumed (chunk_keep).  fp32 Q / K storage converts at the load (row_chunk: its
+// wait stays; not the bf16 path the "medium" plan runs).
+// The prefetches go through buffer loads: a wave-uniform resource (base, size) in SGPRs, a
+// lane offset fixed for the whole kernel and a per-block scalar offset, so the loop builds no
+// 64-bit VGPR addresses (a rebuilt address register that had been a load's destination was
+// another wait, for every store in flight).  Reads past the size return zeros.
+// a wave-uniform pointer the compiler computed in VGPRs (64-bit offset arithmetic goes to the
+// VALU) back into SGPRs: a VGPR buffer resource turns each load into a waterfall loop
+template <class T>
+__device__ __forceinline__ T* sgpr_ptr(T* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<T*>(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
+}
+__device__ __forceinline__ bf16x8 buf_b128(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+__device__ __forceinline__ uint32_t buf_b32(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
+}
+__device__ __forceinline__ bf16x8 chunk_keep(bf16x8 v, bool valid) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 u = __builtin_bit_cast(u32x4, v);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) u[j] = valid ? u[j] : 0u;
+  return __builtin_bit_cast(bf16x8, u);
+}
+
 // FULL: Lk == LF_MAXK, every wave's two key tiles exist (no per-tile guards, whose skip
 // paths made the compiler zero-fill the tiles' registers every query block)
 template <bool BITS, bool FULL>
@@ -132,7 +216,9 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
   const AttnPair& P = A.p[blockIdx.y];
   if ((int)blockIdx.x >= A.B * A.heads) return;
   const int head = blockIdx.x % A.heads, b = blockIdx.x / A.heads;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, hh = lane >> 5, r = lane & 31;
+  // (w through readfirstlane: the compiler then knows it is wave-uniform, so the `w < 4` guards
+  // around the prefetches are scalar branches and their buffer resources stay in SGPRs)
+  const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6), hh = lane >> 5, r = lane & 31;
   // transposed-read addressing: lane 4 qp + pp of each 16-lane group g16 names row qp,
   // columns 4 pp .. 4 pp + 3 of the group's 16 columns (16 (g16 & 1) ..)
   const int g16 = lane >> 4, qp = (lane & 15) >> 2, pp = lane & 3;
@@ -192,22 +278,36 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
     for (int k = t; k < Lk; k += LF_NT) gs[k] = P.dpbar[bh * Lk + k] * gsc;
   }
   // query block images: threads 0..255 stage row t >> 3, chunk t & 7; threads 256..287 the LSE
+  // (raw prefetches; waves 0-3 the Q chunks, wave 4 the LSE -- wave-uniform guards)
+  // (the resources are rebuilt at each use from the wave-uniform bases: held across the loop,
+  // they were kept in VGPRs and every load became a waterfall loop)
+  const uint32_t q_voff = (uint32_t)((((t >> 3) & 31) * P.ldq + 8 * (t & 7)) * 2);
+  const __bf16* q_u = sgpr_ptr(reinterpret_cast<const __bf16*>(P.q) + q_off);
+  const float* lse_u = sgpr_ptr(P.lse + bh * Lq);
+  const uint32_t q_bytes = (uint32_t)(((int64_t)(Lq - 1) * P.ldq + hd) * 2);
   auto q_load = [&](int qb, bf16x8& v, float& l) {
     const int row = (t >> 3) & 31, q = qb * LF_QB + row;
-    v = row_chunk(P.q, qkb, q_off + (int64_t)(q < Lq ? q : 0) * P.ldq, t & 7, hd, t < 256 && q < Lq);
-    const int ql = qb * LF_QB + (t & 31);
-    l = (t >= 256 && t < 256 + LF_QB && ql < Lq) ? P.lse[bh * Lq + ql] : -INFINITY;
+    if (w < 4) {
+      if (qkb) v = buf_b128(buf_rsrc(q_u, q_bytes), q_voff, (uint32_t)(qb * LF_QB * P.ldq * 2));
+      else v = row_chunk(P.q, false, q_off + (int64_t)(q < Lq ? q : 0) * P.ldq, t & 7, hd, q < Lq);
+    }
+    if (w == 4) l = __uint_as_float(buf_b32(buf_rsrc(lse_u, (uint32_t)Lq * 4u), (uint32_t)(t & 31) * 4u, (uint32_t)(qb * LF_QB * 4)));
   };
-  auto q_store = [&](int buf, const bf16x8& v, float l) {
-    if (t < 256) *reinterpret_cast<bf16x8*>(lds + OFF_Q + buf * 4096 + img_off(t >> 3, t & 7)) = v;
+  auto q_store = [&](int qb, int buf, const bf16x8& v, float l) {
+    const int q = qb * LF_QB + ((t >> 3) & 31);
+    if (t < 256)
+      *reinterpret_cast<bf16x8*>(lds + OFF_Q + buf * 4096 + img_off(t >> 3, t & 7)) =
+          chunk_keep(v, q < Lq && 8 * (t & 7) < hd);
     // log2 units; +inf for an invalid or fully masked query: every p = exp2(s - inf) = 0
-    if (t >= 256 && t < 256 + LF_QB) lse_s[buf * LF_QB + (t - 256)] = l == -INFINITY ? INFINITY : l * LF_LOG2E;
+    const int ql = qb * LF_QB + (t & 31);
+    if (t >= 256 && t < 256 + LF_QB)
+      lse_s[buf * LF_QB + (t - 256)] = (ql >= Lq || l == -INFINITY) ? INFINITY : l * LF_LOG2E;
   };
   {
     bf16x8 v;
     float l;
     q_load(0, v, l);
-    q_store(0, v, l);
+    q_store(0, 0, v, l);
   }
   __syncthreads();
 
@@ -218,34 +318,51 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
     for (int dt = 0; dt < 2; ++dt) dk[i][dt] = zero16f();
   char* Sw = lds + OFF_S + w * 2048;
   float* redw = reinterpret_cast<float*>(lds + OFF_R) + w * 2048;
-  uint32_t nwords[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};   // keep words of query block 0 (all kept: no dropout)
-  if (BITS && r < Lq) {
+  // the keep words of a query block as loaded (raw prefetch; the half shift and the validity
+  // applied by the block that uses them)
+  // (words of missing tiles, kt >= nkt, are read from wherever they land and never used)
+  const uint32_t kw_voff = (uint32_t)((r * kwl + w) * 4);
+  const uint32_t* kw_u = sgpr_ptr(P.keep_bits + bh * Lq * kwl);
+  auto kw_fetch = [&](int qb, uint32_t (&raw)[2]) {
+    const __amdgpu_buffer_rsrc_t rk = buf_rsrc(kw_u, (uint32_t)((int64_t)Lq * kwl * 4));
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int kt = w + 8 * i;
-      if (FULL || kt < nkt) nwords[i] = P.keep_bits[(bh * Lq + r) * kwl + kt] >> (4 * hh);
-    }
+    for (int i = 0; i < 2; ++i) raw[i] = buf_b32(rk, kw_voff + 32u * i, (uint32_t)(qb * LF_QB * kwl * 4));
+  };
+  // keep words of the next block, shifted to this lane's half and validated at the END of the
+  // block that loaded them (a loop-carried raw register would be copied at the loop head, a use
+  // that waits for the load issued just before it)
+  auto kw_finish = [&](int qb, const uint32_t (&raw)[2], uint32_t (&wd)[2]) {
+    const bool ok = qb * LF_QB + r < Lq;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) wd[i] = ((FULL || w + 8 * i < nkt) && ok) ? raw[i] >> (4 * hh) : 0xFFFFFFFFu;
+  };
+  uint32_t nwords[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
+  if (BITS) {
+    uint32_t raw[2];
+    kw_fetch(0, raw);
+    kw_finish(0, raw, nwords);
   }
 
+  // the younger half (waves 4-7: the arbitration losers, the pole at both barriers) issues at
+  // priority 1 (MI355X_MICROARCH "two waves per SIMD" item 4; C5 4.20 -> 4.13 ms of this kernel
+  // per step; MMF_LONG_NO_PRIO builds the A/B arm)
+#ifndef MMF_LONG_NO_PRIO
+  if (w >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
+  LS_DECL
   for (int qb = 0; qb < nqb; ++qb) {
     const int buf = qb & 1, qbase = qb * LF_QB;
     const bool has_next = qb + 1 < nqb;
     bf16x8 nv;
-    float nl = -INFINITY;
+    float nl;   // (no initial value: a register write here waited for every store in flight)
     if (has_next) q_load(qb + 1, nv, nl);   // in flight during this block
     const char* Qi = lds + OFF_Q + buf * 4096;
     const int q = qbase + r;
     const bool qvalid = q < Lq;
     // this block's keep words (loaded during the previous block), the next block's in flight
-    uint32_t words[2] = {nwords[0], nwords[1]};
-    if (BITS && has_next) {
-      const int qn = q + LF_QB;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int kt = w + 8 * i;
-        nwords[i] = ((FULL || kt < nkt) && qn < Lq) ? P.keep_bits[(bh * Lq + qn) * kwl + kt] >> (4 * hh) : 0xFFFFFFFFu;
-      }
-    }
+    const uint32_t words[2] = {nwords[0], nwords[1]};
+    uint32_t nraw[2];
+    if (BITS && has_next) kw_fetch(qb + 1, nraw);
     bf16x8 qf[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(Qi + img_off(r, 2 * s + hh));
@@ -287,8 +404,9 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
       for (int e = 0; e < 8; ++e) dpp[8 * i + e] = f32x2{pk[i][2 * e], pk[i][2 * e + 1]};
     const float Dp = sum_xor32(tree_sum<16>(dpp));
     if (hh == 0) Dpart[buf * 256 + w * 32 + r] = Dp;
-    if (has_next) q_store(buf ^ 1, nv, nl);
-    __syncthreads();   // (A) partial D's, next query block
+    LS_MARK(0)
+    __syncthreads();   // (A) partial D's
+    LS_MARK(1)
 
     float D = 0.f;
 #pragma unroll
@@ -364,7 +482,14 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
         *reinterpret_cast<float4*>(redw + red_off(d, 2 * g + hh)) =
             make_float4(dq[dt][4 * g], dq[dt][4 * g + 1], dq[dt][4 * g + 2], dq[dt][4 * g + 3]);
     }
-    __syncthreads();   // (B) partial dQ's
+    // the next query block's images: its loads (issued at the top of this block) have had
+    // phases 1 and 2 to land; buffer buf ^ 1 was last read in the previous block's phase 2
+    if (has_next) q_store(qb + 1, buf ^ 1, nv, nl);
+    // (here, not after this block's dQ stores: vmcnt counts stores, so a wait there is for them)
+    if (BITS && has_next) kw_finish(qb + 1, nraw, nwords);
+    LS_MARK(2)
+    __syncthreads();   // (B) partial dQ's, next query block
+    LS_MARK(3)
 
     {
       const int d = t & 63, j = t >> 6;   // queries 4j .. 4j+3 of column d
@@ -383,17 +508,26 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
       }
       const float av[4] = {a01.x, a01.y, a23.x, a23.y};
       if (d < hd) {
+        // one 64-bit row offset per block, the 4 rows by 32-bit steps (per-element 64-bit
+        // products were 24 integer multiplies per block)
+        const int q0 = qbase + 4 * j, ld = P.ldq;
+        const int64_t o0 = (int64_t)q0 * ld + d;
+        if (dqb) {
+          __bf16* dst = dQh + o0;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int qq = qbase + 4 * j + e;
-          if (qq < Lq) {
-            if (dqb) dQh[(int64_t)qq * P.ldq + d] = (__bf16)(av[e] * scale);
-            else dQg[(int64_t)qq * P.ldq + d] = av[e] * scale;
-          }
+          for (int e = 0; e < 4; ++e)
+            if (q0 + e < Lq) dst[e * ld] = (__bf16)(av[e] * scale);
+        } else {
+          float* dst = dQg + o0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (q0 + e < Lq) dst[e * ld] = av[e] * scale;
         }
       }
     }
+    LS_MARK(4)
   }
+  LS_STORE(w, 4)
 
   // dK: lane = d, registers = keys 32 kt + acc_row(e, hh)
 #pragma unroll
@@ -479,7 +613,9 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_poolL_fwd_fused_bf16(const At
   const AttnPair& P = A.p[blockIdx.y];
   if ((int)blockIdx.x >= A.B * A.heads) return;
   const int head = blockIdx.x % A.heads, b = blockIdx.x / A.heads;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, hh = lane >> 5, r = lane & 31;
+  // (w through readfirstlane: the compiler then knows it is wave-uniform, so the `w < 4` guards
+  // around the prefetches are scalar branches and their buffer resources stay in SGPRs)
+  const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6), hh = lane >> 5, r = lane & 31;
   const int g16 = lane >> 4, qp = (lane & 15) >> 2, pp = lane & 3;
   const int hd = A.hd, col0 = head * hd;
   const int Lq = P.Lq, Lk = P.Lk, nkt = Lk >> 5, nqb = (Lq + LF_QB - 1) / LF_QB, kwl = P.kw_ld;
@@ -513,17 +649,27 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_poolL_fwd_fused_bf16(const At
     for (int s4 = 0; s4 < 4; ++s4)
       kf[i][s4] = row_chunk(P.k, qkb, k_off + (int64_t)(krow < Lk ? krow : 0) * P.ldk, 2 * s4 + hh, hd, krow < Lk);
   }
+  // (raw prefetches through buffer loads: waves 0-3 stage the Q chunks)
+  const uint32_t q_voff = (uint32_t)((((t >> 3) & 31) * P.ldq + 8 * (t & 7)) * 2);
+  const __bf16* q_u = sgpr_ptr(reinterpret_cast<const __bf16*>(P.q) + q_off);
+  const uint32_t q_bytes = (uint32_t)(((int64_t)(Lq - 1) * P.ldq + hd) * 2);
   auto q_load = [&](int qb, bf16x8& v) {
     const int q = qb * LF_QB + ((t >> 3) & 31);
-    v = row_chunk(P.q, qkb, q_off + (int64_t)(q < Lq ? q : 0) * P.ldq, t & 7, hd, t < 256 && q < Lq);
+    if (w < 4) {
+      if (qkb) v = buf_b128(buf_rsrc(q_u, q_bytes), q_voff, (uint32_t)(qb * LF_QB * P.ldq * 2));
+      else v = row_chunk(P.q, false, q_off + (int64_t)(q < Lq ? q : 0) * P.ldq, t & 7, hd, q < Lq);
+    }
   };
-  auto q_store = [&](int buf, const bf16x8& v) {
-    if (t < 256) *reinterpret_cast<bf16x8*>(lds + FOFF_Q + buf * 4096 + img_off(t >> 3, t & 7)) = v;
+  auto q_store = [&](int qb, int buf, const bf16x8& v) {
+    const int q = qb * LF_QB + ((t >> 3) & 31);
+    if (t < 256)
+      *reinterpret_cast<bf16x8*>(lds + FOFF_Q + buf * 4096 + img_off(t >> 3, t & 7)) =
+          chunk_keep(v, q < Lq && 8 * (t & 7) < hd);
   };
   {
     bf16x8 v;
     q_load(0, v);
-    q_store(0, v);
+    q_store(0, 0, v);
   }
   __syncthreads();
 
@@ -552,25 +698,53 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_poolL_fwd_fused_bf16(const At
   };
   f32x16 sn[TPW];
   scores(0, sn);
+  // Loads run two query blocks ahead of their LDS store: the images of block qb + 1 are stored
+  // before barrier A of block qb (block qb + 1's products are issued right after it), so their
+  // loads are issued at the top of block qb - 1 (one whole block of latency cover; issued at
+  // the top of block qb, phase 1 alone -- a few hundred cycles -- had to cover them).  The keep
+  // words of block qb + 1 likewise load during block qb.
+  bf16x8 nv;
+  if (nqb > 1) q_load(1, nv);
+  // raw keep words (the half shift and validity applied by the block that uses them)
+  const uint32_t* kw_u = sgpr_ptr(P.keep_bits + bh * Lq * kwl);
+  const uint32_t kw_voff = (uint32_t)((r * kwl + w) * 4);
+  auto kw_load = [&](int qb, uint32_t (&kw)[TPW]) {
+    const __amdgpu_buffer_rsrc_t rk = buf_rsrc(kw_u, (uint32_t)((int64_t)Lq * kwl * 4));
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) kw[i] = buf_b32(rk, kw_voff + 4u * NW * i, (uint32_t)(qb * LF_QB * kwl * 4));
+  };
+  // shifted to this lane's half and validated at the end of the block that loaded them (see the
+  // backward's kw_finish)
+  auto kw_finish = [&](int qb, const uint32_t (&raw)[TPW], uint32_t (&wd)[TPW]) {
+    const bool ok = qb * LF_QB + r < Lq;
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) wd[i] = (ok && w + NW * i < nkt) ? raw[i] >> (4 * hh) : 0xFFFFFFFFu;
+  };
+  uint32_t kwn[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) kwn[i] = 0xFFFFFFFFu;
+  if (DROP) {
+    uint32_t raw[TPW];
+    kw_load(0, raw);
+    kw_finish(0, raw, kwn);
+  }
 
+#ifndef MMF_LONG_NO_PRIO
+  if (w >= NW / 2) __builtin_amdgcn_s_setprio(1);   // (the younger half, as the backward)
+#endif
+  LS_DECL
   for (int qb = 0; qb < nqb; ++qb) {
     const int buf = qb & 1, qbase = qb * LF_QB;
     const bool has_next = qb + 1 < nqb;
-    bf16x8 nv;
-    if (has_next) q_load(qb + 1, nv);
+    bf16x8 nv2;
+    if (qb + 2 < nqb) q_load(qb + 2, nv2);
     const int q = qbase + r;
     const bool qvalid = q < Lq;
     // the keep words of the own tiles (attn_keep_words_kernel), consumed after barrier B
-    uint32_t kw[TPW];
+    uint32_t kw[TPW], kraw[TPW];
 #pragma unroll
-    for (int i = 0; i < TPW; ++i) kw[i] = 0xFFFFFFFFu;
-    if (DROP && qvalid) {
-#pragma unroll
-      for (int i = 0; i < TPW; ++i) {
-        const int kt = w + NW * i;
-        if (kt < nkt) kw[i] = P.keep_bits[(bh * Lq + q) * kwl + kt] >> (4 * hh);
-      }
-    }
+    for (int i = 0; i < TPW; ++i) kw[i] = kwn[i];
+    if (DROP && has_next) kw_load(qb + 1, kraw);
     float x[TPW][16];
     float mx = -INFINITY;
 #pragma unroll
@@ -584,8 +758,10 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_poolL_fwd_fused_bf16(const At
     }
     mx = max_xor32(mx) * sl2;   // log2 units (max(s) * c == max(s * c) for c > 0)
     if (hh == 0) Mpart[buf * NW * 32 + w * 32 + r] = mx;
-    if (has_next) q_store(buf ^ 1, nv);
+    if (has_next) q_store(qb + 1, buf ^ 1, nv);
+    LS_MARK(0)
     __syncthreads();   // (A) row maxima, next query block
+    LS_MARK(1)
     if (has_next) scores(buf ^ 1, sn);
     float m = -INFINITY;
 #pragma unroll
@@ -607,7 +783,13 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_poolL_fwd_fused_bf16(const At
     }
     ls = sum_xor32(ls);
     if (hh == 0) Spart[buf * NW * 32 + w * 32 + r] = ls;
+    LS_MARK(2)
     __syncthreads();   // (B) row sums
+    LS_MARK(3)
+    // the loads issued at the top of this block have had phases 1 and 2 (and nothing stored
+    // since: vmcnt counts stores too)
+    nv = nv2;
+    if (DROP && has_next) kw_finish(qb + 1, kraw, kwn);
     float l;
     {
       float sp[NW];   // (scalar tree: packed adds would need the ds_read2 pairs re-registered)
@@ -646,7 +828,9 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_poolL_fwd_fused_bf16(const At
         cs[i] = mfma_bf16(ones, pb, cs[i]);
       }
     }
+    LS_MARK(4)
   }
+  LS_STORE(w, NW / 2)
   // pbar: lane = key, every register the same column sum
 #pragma unroll
   for (int i = 0; i < TPW; ++i) {
@@ -833,3 +1017,10 @@ hipError_t launch_attn_long_fused_bwd(const AttnPair* pairs, int npairs, int B, 
 }
 
 }  // namespace mmf
+
+#ifdef MMF_STAMPS
+extern "C" int mmf_long_stamps_read(void* out, size_t bytes) {   // attn_long.hip phase stamps
+  if (bytes > sizeof(mmf::g_mmf_stamps)) bytes = sizeof(mmf::g_mmf_stamps);
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mmf::g_mmf_stamps), bytes) == hipSuccess ? 0 : 3;
+}
+#endif

@@ -3,6 +3,11 @@
 
 Build: make -C <pkg>/csrc stamps (stampsf for the forward, argument "fwd").  Run (box):
   MMF_LIB_PATH=<pkg>/csrc/libmmfusion_stamps.so MMF_ATTN_BWD=v1 python scripts/attn_stamps.py
+Long-key fused kernels (attn_long.hip, C5 medium; make stampsl):
+  MMF_LIB_PATH=<pkg>/csrc/libmmfusion_stampsl.so python scripts/attn_stamps.py long   (backward)
+  MMF_LIB_PATH=<pkg>/csrc/libmmfusion_stampsl.so MMF_NO_LONG_BWD_STAMP=1 ... longf  (forward: the
+  forward's stamps are overwritten by the backward's, so the bwd stamps are read after a forward-only
+  pass: see main_long)
 Stamps (s_memtime, wave 0 of every workgroup): 0 start, 1 K/Q images loaded, 2 S/P/D,
 3 dS, 4 dQ stored, 5 dK quarters, 6 dK stored.  Prints per-phase mean cycles, the
 workgroup lifetime, and how the start times of the workgroups on one CU are spread
@@ -27,8 +32,55 @@ from train_step import HybridTrainStep  # noqa: E402
 import bench  # noqa: E402
 
 
+def main_long(kernel):
+    """attn_long.hip stamps: per workgroup, phase sums over the query blocks of wave 0 (slots 0-4:
+    to barrier A, barrier A wait, to barrier B, barrier B wait, after B) and of the first wave of
+    the younger half (slots 5-8), the s_memrealtime lifetime in slot 9.  The last launch of the
+    step is read: the backward's last launch ("long"), or for "longf" a forward-only pass."""
+    w = bench.WORKLOADS["c5"]
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    names = [f"m{i}" for i in range(w["M"])]
+    model = HybridFusion({n: w["D"] for n in names}, hidden_dim=w["H"], num_classes=w["C"], num_heads=w["heads"],
+                         dropout=0.1).to(dev)
+    torch.set_float32_matmul_precision("medium")
+    feats, mask, labels = bench.make_inputs(w, w["B"], 42, dev)
+    step = HybridTrainStep(model, feats, mask, labels)
+    L = mmf_native.lib()
+    reader = L.mmf_long_stamps_read
+    reader.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    for _ in range(int(os.environ.get("STAMPS_WARM", "3"))):
+        step.forward_backward()
+    if kernel == "longf":
+        model.train()
+        with torch.no_grad():
+            model(dict(zip(names, feats)), mask)
+    torch.cuda.synchronize()
+    buf = np.zeros((8192, 10), dtype=np.uint64)
+    assert reader(buf.ctypes.data, buf.nbytes) == 0
+    nwg = w["B"] * w["heads"] * 10
+    st = buf[:nwg].astype(np.int64)
+    ok = st[:, 9] > 0
+    st = st[ok]
+    if kernel == "long":
+        ph = ["S/P/D partial", "barrier A", "dS + dQ/dK MFMA + partial dQ", "barrier B", "dQ reduce + store"]
+    else:
+        ph = ["loads + max", "barrier A", "next S + exp + sums", "barrier B", "P' tile + colsum"]
+    tot0 = st[:, 0:5].sum(axis=1)
+    out = {"kernel": kernel, "workgroups": int(ok.sum()),
+           "wave0_loop_cycles_mean": float(tot0.mean()),
+           "wave0_phase_mean_cycles": {n: float(st[:, i].mean()) for i, n in enumerate(ph)},
+           "wave0_phase_share": {n: round(float(st[:, i].mean() / tot0.mean()), 3) for i, n in enumerate(ph)},
+           "younger_phase_mean_cycles": {n: float(st[:, 5 + i].mean()) for i, n in enumerate(ph[:4])},
+           "wg_lifetime_us_median": float(np.median(st[:, 9]) * 0.01),
+           "shader_clock_ghz_median": float(np.median(tot0 / st[:, 9] * 0.1))}
+    print(json.dumps(out, indent=1))
+
+
 def main():
     kernel = sys.argv[1] if len(sys.argv) > 1 else "attn"
+    if kernel in ("long", "longf"):
+        return main_long(kernel)
     w = bench.WORKLOADS["c2"]
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
