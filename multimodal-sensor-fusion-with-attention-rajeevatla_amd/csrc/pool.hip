@@ -280,12 +280,207 @@ __global__ __launch_bounds__(NT) void pool_dpbar_grp_kernel(const PoolGrpArgs a)
   }
 }
 
+// ---- the grouped pools on the fp32 matrix cores (round 5) ----
+// Both are small-side GEMMs per (sample, group): U = pbar P_k (M = R <= 32 rows, N = H, K = Lk) and
+// dpbar^T = P_k dU^T (M = Lk, N = R, K = H).  The VALU forms above spent their time on the dot
+// products and, for dpbar, on a 32-lane reduction per (row, key): 0.37 / 0.25 ms per C5 step for
+// 0.40 GB of P_k each.  32x32x2 f32 MFMAs, fp32 products and sums as before (other order).  The
+// P_k operand streams from HBM as float4 per lane (each element is used once per workgroup) by
+// permuting the MFMA's K or N index: dpbar -- lane half h takes columns c0 + 4h .. +3 and MFMA i
+// of a quad contracts column c0 + 4h + i on both operands; U -- lane n' holds columns 4n' .. 4n'+3
+// of a key row and MFMA i produces the interleaved column tile {4n' + i}.
+constexpr int POOL_MFMA_HMAX = 256;
+__device__ __forceinline__ f32x16 mfma_f32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// dpbar_row[j] = P_k[b][j] . dU_row + dObar_row . b_v,row; wave w takes key tiles w, w + 4, ...
+__global__ __launch_bounds__(NT) void pool_dpbar_mfma_kernel(const PoolGrpArgs a) {
+  constexpr int LDU = POOL_MFMA_HMAX + 4;   // (+4 floats: the 32 rows' float4 reads spread over the banks)
+  __shared__ __attribute__((aligned(16))) float dus[POOL_GRP_ROWS * LDU];   // dU, rows >= R zero
+  __shared__ float dr_s[POOL_GRP_ROWS];
+  const int b = blockIdx.x, gi = blockIdx.y, t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int beg = a.gbeg[gi], heads = a.heads, H = a.H, hd = a.hd;
+  const int R = a.gcnt[gi] * heads, Lk = a.p[beg].Lk;
+  for (int i = t; i < POOL_GRP_ROWS * H; i += NT) {
+    const int row = i / H, c = i - row * H;
+    dus[row * LDU + c] = row < R ? a.p[beg + row / heads].du[((int64_t)b * heads + row % heads) * H + c] : 0.f;
+  }
+  for (int row = w; row < R; row += NT / 64) {
+    const PoolPair& P = a.p[beg + row / heads];
+    const int hh = row % heads;
+    float s = 0.f;
+    for (int d = lane; d < hd; d += 64) s += P.dob[(int64_t)b * H + hh * hd + d] * P.bv[hh * hd + d];
+    s = sum64(s);
+    if (lane == 0) dr_s[row] = s;
+  }
+  __syncthreads();
+  const int n = lane & 31, h = lane >> 5;
+  const float* pk = a.p[beg].pk + (int64_t)b * Lk * H;
+  const float* du_row = dus + n * LDU + 4 * h;
+  for (int jt = w; jt < Lk / 32; jt += NT / 64) {
+    const float* arow = pk + (int64_t)(jt * 32 + n) * H + 4 * h;
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    // the row's float4s in chunks of 8 (32 registers), the next chunk issued before this one's MFMAs
+    float4 av[2][8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) av[0][k] = k * 8 < H ? *reinterpret_cast<const float4*>(arow + 8 * k) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int ch = 0; ch < POOL_MFMA_HMAX / 64; ++ch) {
+      const int cur = ch & 1;
+      if (ch + 1 < POOL_MFMA_HMAX / 64 && (ch + 1) * 64 < H) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int c0 = (ch + 1) * 64 + 8 * k;
+          av[cur ^ 1][k] = c0 < H ? *reinterpret_cast<const float4*>(arow + c0) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+      if (ch * 64 >= H) break;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int c0 = ch * 64 + 8 * k;
+        if (c0 >= H) break;
+        const float4 bv = *reinterpret_cast<const float4*>(du_row + c0);
+        const float4 x = av[cur][k];
+        acc = mfma_f32(x.x, bv.x, acc);
+        acc = mfma_f32(x.y, bv.y, acc);
+        acc = mfma_f32(x.z, bv.z, acc);
+        acc = mfma_f32(x.w, bv.w, acc);
+      }
+    }
+    // C[j][r]: lane (r = n) holds keys jt * 32 + 8 g + 4 h + 0..3 in registers 4 g .. 4 g + 3
+    if (n < R) {
+      float* dst = a.p[beg + n / heads].dpbar + ((int64_t)b * heads + n % heads) * Lk + jt * 32 + 4 * h;
+      const float dr = dr_s[n];
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<float4*>(dst + 8 * g) =
+            make_float4(acc[4 * g] + dr, acc[4 * g + 1] + dr, acc[4 * g + 2] + dr, acc[4 * g + 3] + dr);
+    }
+  }
+}
+
+// U_row = pbar_row P_k[b] and r_row = sum_j pbar_row[j].  Waves (cb, kh): column block cb of 128
+// (lane n' holds columns 4n' .. 4n'+3, MFMA i the interleaved tile {4n' + i}) over key half kh;
+// the two key halves of a column block are summed through LDS (fixed order).  pbar rows at a
+// stride of Lk + 2 floats (the A reads -- 32 rows, one float each -- hit distinct banks; at Lk
+// they were 32-way conflicts); the partials reuse that area once the products are done, so two
+// workgroups fit a CU.
+__global__ __launch_bounds__(NT, 2) void pool_u_mfma_kernel(const PoolGrpArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float pbg[];   // [32][Lk + 2] (rows >= R zero)
+  const int b = blockIdx.x, gi = blockIdx.y, t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int beg = a.gbeg[gi], heads = a.heads, H = a.H;
+  const int R = a.gcnt[gi] * heads, Lk = a.p[beg].Lk, LDP = Lk + 2;
+  // staging: wave w the rows w, w + 4, ...; float4 loads (Lk % 4 == 0), scalar LDS stores
+  for (int row = w; row < POOL_GRP_ROWS; row += NT / 64) {
+    const float* src = row < R ? a.p[beg + row / heads].pbar + ((int64_t)b * heads + row % heads) * Lk : nullptr;
+    for (int c4 = lane; c4 < Lk / 4; c4 += 64) {
+      const float4 v = src ? *reinterpret_cast<const float4*>(src + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      float* d = pbg + row * LDP + 4 * c4;
+      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    }
+  }
+  __syncthreads();
+  for (int row = w; row < R; row += NT / 64) {
+    float s = 0.f;
+    for (int j = lane; j < Lk; j += 64) s += pbg[row * LDP + j];
+    s = sum64(s);
+    if (lane == 0) a.p[beg + row / heads].r[(int64_t)b * heads + row % heads] = s;
+  }
+  const int n = lane & 31, h = lane >> 5;
+  const int cb = w & 1, kh = w >> 1, ncb = H / 128;
+  const int half = Lk / 2, j_beg = kh * half;   // (Lk even)
+  for (int cbb = cb; cbb < 2 * ((ncb + 1) / 2); cbb += 2) {   // (H = 256: one pass; H = 128: wave cb 1 idles)
+    const bool on = cbb < ncb;
+    f32x16 acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+    if (on) {
+      const float* bcol = a.p[beg].pk + ((int64_t)b * Lk + j_beg + h) * H + 128 * cbb + 4 * n;
+      const float* arow = pbg + n * LDP + j_beg + h;
+      // 8 key pairs per chunk: the P_k float4s of the next chunk issued before this one's MFMAs
+      float4 bvv[2][8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        bvv[0][k] = 2 * k < half ? *reinterpret_cast<const float4*>(bcol + (int64_t)2 * k * H) : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int k0 = 0; k0 < half; k0 += 32) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int jj = k0 + 16 + 2 * k;
+          if (jj < half) bvv[1][k] = *reinterpret_cast<const float4*>(bcol + (int64_t)jj * H);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int jj = k0 + 2 * k;
+          if (jj < half) {
+            const float av = arow[jj];
+            const float4 x = bvv[0][k];
+            acc[0] = mfma_f32(av, x.x, acc[0]);
+            acc[1] = mfma_f32(av, x.y, acc[1]);
+            acc[2] = mfma_f32(av, x.z, acc[2]);
+            acc[3] = mfma_f32(av, x.w, acc[3]);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int jj = k0 + 32 + 2 * k;
+          if (jj < half) bvv[0][k] = *reinterpret_cast<const float4*>(bcol + (int64_t)jj * H);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int jj = k0 + 16 + 2 * k;
+          if (jj < half) {
+            const float av = arow[jj];
+            const float4 x = bvv[1][k];
+            acc[0] = mfma_f32(av, x.x, acc[0]);
+            acc[1] = mfma_f32(av, x.y, acc[1]);
+            acc[2] = mfma_f32(av, x.z, acc[2]);
+            acc[3] = mfma_f32(av, x.w, acc[3]);
+          }
+        }
+      }
+    }
+    __syncthreads();   // (every wave's A reads done: the partials reuse the pbar area)
+    float* part = pbg;   // [2 col blocks][32 rows][128]
+    // key half 1 parks its partial in LDS, key half 0 adds it and stores (rows acc_row(e, h),
+    // column 128 cbb + 4 n + i of tile i)
+    if (kh == 1 && on) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        *reinterpret_cast<float4*>(part + (cb * 32 + acc_row(e, h)) * 128 + 4 * n) =
+            make_float4(acc[0][e], acc[1][e], acc[2][e], acc[3][e]);
+    }
+    __syncthreads();
+    if (kh == 0 && on) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = acc_row(e, h);
+        if (row >= R) continue;
+        const float4 o = *reinterpret_cast<const float4*>(part + (cb * 32 + row) * 128 + 4 * n);
+        *reinterpret_cast<float4*>(a.p[beg + row / heads].u + ((int64_t)b * heads + row % heads) * H + 128 * cbb + 4 * n) =
+            make_float4(acc[0][e] + o.x, acc[1][e] + o.y, acc[2][e] + o.z, acc[3][e] + o.w);
+      }
+    }
+    if (cbb + 2 < 2 * ((ncb + 1) / 2)) {   // (another pass re-stages nothing: H > 256 is refused)
+      __syncthreads();
+    }
+  }
+}
+
 // Group the pairs by key modality (same P_k) and launch the grouped kernels; false when the
 // shapes do not fit them (the caller runs the per-pair kernels)
 bool launch_pool_grouped(bool fwd, const PoolPair* pairs, int npairs, int B, int heads, int hd, int H,
                          hipStream_t st, hipError_t& err) {
   err = hipSuccess;
   if (getenv("MMF_POOL_PER_PAIR") || H % 4 != 0 || H > 256 || npairs < 2) return false;
+  // the fp32-MFMA forms (MMF_POOL_VALU=1: the VALU forms, A/B)
+  static const bool valu = getenv("MMF_POOL_VALU") != nullptr;
   std::vector<std::vector<int>> groups;
   std::vector<const float*> keyp;
   for (int g = 0; g < npairs; ++g) {
@@ -295,9 +490,18 @@ bool launch_pool_grouped(bool fwd, const PoolPair* pairs, int npairs, int B, int
     groups[i].push_back(g);
   }
   if (groups.size() == (size_t)npairs) return false;   // nothing shared
+  bool mfma = !valu;
   for (auto& gr : groups) {
     const int R = (int)gr.size() * heads, Lk = pairs[gr[0]].Lk;
     if (R > POOL_GRP_ROWS || (size_t)R * (fwd ? Lk : H) * sizeof(float) > 64 * 1024) return false;
+    // dpbar: H % 8 (the float4 quads), Lk % 32 (key tiles); U: H % 128 (column blocks), Lk even and
+    // the pbar rows + partials in LDS; 16-B aligned P_k rows
+    if (fwd ? (H % 128 != 0 || H > 256 || Lk % 4 != 0 ||
+               (size_t)std::max(POOL_GRP_ROWS * (Lk + 2), 2 * 32 * 128) * 4 > 80 * 1024)
+            : (H % 8 != 0 || Lk % 32 != 0))
+      mfma = false;
+    for (int g : gr)
+      if (((uintptr_t)pairs[g].pk & 15) != 0 || (fwd && ((uintptr_t)pairs[g].pbar & 15) != 0)) mfma = false;
   }
   size_t gi = 0;
   while (gi < groups.size()) {
@@ -311,7 +515,8 @@ bool launch_pool_grouped(bool fwd, const PoolPair* pairs, int npairs, int B, int
       a.gcnt[ng] = (int)groups[gi].size();
       const int Lk = pairs[groups[gi][0]].Lk, R = a.gcnt[ng] * heads;
       for (int g : groups[gi]) a.p[np++] = pairs[g];
-      shm = std::max(shm, (size_t)R * (fwd ? Lk : H) * sizeof(float));
+      shm = std::max(shm, mfma ? (fwd ? (size_t)std::max(POOL_GRP_ROWS * (Lk + 2), 2 * 32 * 128) * 4 : 0)
+                               : (size_t)R * (fwd ? Lk : H) * sizeof(float));
       fl += 2.0 * B * R * Lk * H;
       by += 4.0 * B * ((double)Lk * H + R * (Lk + H));   // P_k once per group
       ++ng;
@@ -319,9 +524,23 @@ bool launch_pool_grouped(bool fwd, const PoolPair* pairs, int npairs, int B, int
     }
     a.ngroups = ng;
     a.B = B; a.heads = heads; a.hd = hd; a.H = H;
-    ProfLaunch prof_(st, fwd ? "pool_u_grp_kernel" : "pool_dpbar_grp_kernel", fl, by);
-    if (fwd) mmf_launch(pool_u_grp_kernel, dim3(B, ng), dim3(NT), (uint32_t)shm, st, a);
-    else mmf_launch(pool_dpbar_grp_kernel, dim3(B, ng), dim3(NT), (uint32_t)shm, st, a);
+    if (mfma) {
+      ProfLaunch prof_(st, fwd ? "pool_u_mfma_kernel" : "pool_dpbar_mfma_kernel", fl, by);
+      if (fwd) {
+        static bool attr = false;
+        if (!attr && shm > 64 * 1024) {
+          (void)hipFuncSetAttribute((const void*)pool_u_mfma_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+          attr = true;
+        }
+        mmf_launch(pool_u_mfma_kernel, dim3(B, ng), dim3(NT), (uint32_t)shm, st, a);
+      } else {
+        mmf_launch(pool_dpbar_mfma_kernel, dim3(B, ng), dim3(NT), 0, st, a);
+      }
+    } else {
+      ProfLaunch prof_(st, fwd ? "pool_u_grp_kernel" : "pool_dpbar_grp_kernel", fl, by);
+      if (fwd) mmf_launch(pool_u_grp_kernel, dim3(B, ng), dim3(NT), (uint32_t)shm, st, a);
+      else mmf_launch(pool_dpbar_grp_kernel, dim3(B, ng), dim3(NT), (uint32_t)shm, st, a);
+    }
     err = hipGetLastError();
     if (err != hipSuccess) return true;
   }
@@ -424,10 +643,91 @@ __global__ __launch_bounds__(NT) void pool_e_blk_kernel(const PoolEArgs a) {
   }
 }
 
+// The same update on the fp32 matrix cores: a 64-row block of one sample per workgroup, wave w
+// the 32-row tile w >> 1 and the 128-column block w & 1 (lane n' holds columns 4n' .. 4n'+3, MFMA
+// i the interleaved tile {4n' + i}, so the row stores are float4); K = sources x heads (padded to
+// even) from LDS, 32x32x2 f32 MFMAs.  The VALU form is bound by its 80 FMAs per float4 stored.
+constexpr int POOLE_MROWS = 64;
+__global__ __launch_bounds__(NT) void pool_e_mfma_kernel(const PoolEArgs a) {
+  __shared__ __attribute__((aligned(16))) float w_s[POOLE_MROWS][POOLE_NSH];
+  __shared__ __attribute__((aligned(16))) float du_s[POOLE_NSH][POOL_MFMA_HMAX];
+  const PoolEMod& E = a.m[blockIdx.y];
+  const int H = a.H, heads = a.heads, L = E.L, nsh = E.nsrc * heads;
+  const int nblk = (L + POOLE_MROWS - 1) / POOLE_MROWS;
+  const int b = blockIdx.x / nblk, j0 = (blockIdx.x % nblk) * POOLE_MROWS;
+  if (b >= a.B) return;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  for (int i = t; i < POOLE_MROWS * POOLE_NSH; i += NT) {
+    const int r = i / POOLE_NSH, q = i % POOLE_NSH, j = min(j0 + r, L - 1);
+    w_s[r][q] = q < nsh ? E.pbar[q / heads][((int64_t)b * heads + q % heads) * L + j] : 0.f;
+  }
+  for (int i = t; i < POOLE_NSH * (H / 4); i += NT) {
+    const int q = i / (H / 4), c4 = i % (H / 4);
+    const float4 v = q < nsh ? *reinterpret_cast<const float4*>(E.du[q / heads] + ((int64_t)b * heads + q % heads) * H + 4 * c4)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+    *reinterpret_cast<float4*>(&du_s[q][4 * c4]) = v;
+  }
+  __syncthreads();
+  const int rt = w >> 1, cb = w & 1, n = lane & 31, h = lane >> 5;
+  if (128 * cb >= H) return;
+  f32x16 acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+  const int ksteps = (nsh + 1) / 2;
+#pragma unroll
+  for (int s2 = 0; s2 < POOLE_NSH / 2; ++s2) {
+    if (s2 < ksteps) {   // (wave-uniform; a guard, not a break: the loop stays unrolled)
+      const float av = w_s[rt * 32 + n][2 * s2 + h];
+      const float4 x = *reinterpret_cast<const float4*>(&du_s[2 * s2 + h][128 * cb + 4 * n]);
+      acc[0] = mfma_f32(av, x.x, acc[0]);
+      acc[1] = mfma_f32(av, x.y, acc[1]);
+      acc[2] = mfma_f32(av, x.z, acc[2]);
+      acc[3] = mfma_f32(av, x.w, acc[3]);
+    }
+  }
+  const int col = 128 * cb + 4 * n;
+  float4 cv = *reinterpret_cast<const float4*>(E.c + (int64_t)b * E.ldc + col);
+  cv = make_float4(cv.x * E.cscale, cv.y * E.cscale, cv.z * E.cscale, cv.w * E.cscale);
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int j = j0 + rt * 32 + acc_row(e, h);
+    if (j < L)
+      *reinterpret_cast<float4*>(E.out + ((int64_t)b * L + j) * H + col) =
+          make_float4(cv.x + acc[0][e], cv.y + acc[1][e], cv.z + acc[2][e], cv.w + acc[3][e]);
+  }
+}
+
 hipError_t launch_pool_e(const PoolEMod* mods, int nmods, int B, int heads, int H, hipStream_t st) {
   if (nmods > 8 || H % 4 != 0) return hipErrorInvalidValue;
   bool blk = H <= 256 && !getenv("MMF_POOLE_FLAT");
   for (int i = 0; i < nmods && blk; ++i) blk = mods[i].nsrc * heads <= POOLE_NSH;
+  // the MFMA form: H % 128 (column blocks), 16-B aligned rows (MMF_POOL_VALU=1: the VALU form)
+  static const bool valu = getenv("MMF_POOL_VALU") != nullptr;
+  bool mf = blk && !valu && H % 128 == 0;
+  for (int i = 0; i < nmods && mf; ++i)
+    mf = ((uintptr_t)mods[i].out & 15) == 0 && ((uintptr_t)mods[i].c & 15) == 0 && mods[i].ldc % 4 == 0;
+  if (mf) {
+    PoolEArgs a;
+    memset(&a, 0, sizeof(a));
+    a.B = B; a.heads = heads; a.H = H;
+    int maxb = 0;
+    double fl = 0.0, by = 0.0;
+    for (int i = 0; i < nmods; ++i) {
+      if (mods[i].nsrc > POOLE_MAX_SRC) return hipErrorInvalidValue;
+      for (int sidx = 0; sidx < mods[i].nsrc; ++sidx)
+        if (((uintptr_t)mods[i].du[sidx] & 15) != 0) return hipErrorInvalidValue;
+      a.m[i] = mods[i];
+      maxb = std::max(maxb, B * ((mods[i].L + POOLE_MROWS - 1) / POOLE_MROWS));
+      fl += 2.0 * B * mods[i].nsrc * heads * mods[i].L * H;
+      by += 4.0 * B * ((double)mods[i].L * H + mods[i].nsrc * heads * (mods[i].L + H) + H);
+    }
+    ProfLaunch prof_(st, "pool_e_mfma_kernel", fl, by);
+    mmf_launch(pool_e_mfma_kernel, dim3(maxb, nmods), dim3(NT), 0, st, a);
+    return hipGetLastError();
+  }
   if (blk) {
     PoolEArgs a;
     memset(&a, 0, sizeof(a));

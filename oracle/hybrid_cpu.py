@@ -129,10 +129,15 @@ def pairs_present(names: Sequence[str], params: Mapping[str, torch.Tensor]) -> L
 
 def hybrid_forward(params: Mapping[str, torch.Tensor], names: Sequence[str],
                    feats: Mapping[str, torch.Tensor], mask: Optional[torch.Tensor],
-                   num_heads: int, p: float = 0.0, train: bool = False, gen=None):
+                   num_heads: int, p: float = 0.0, train: bool = False, gen=None,
+                   taps: Optional[dict] = None):
     """HybridFusion forward (src/fusion.py:331-427) + sequence-mode pooling.
 
     Returns (logits, info) with info = {attention_maps, fusion_weights, pooled}.
+    ``taps`` (a dict, tests only) receives each ReLU's input ``z/<layer>``, its output
+    ``a/<layer>`` (gradient retained) and the layer's input ``in/<layer>``: a test bounds the
+    gradient difference that a pre-activation within rounding of 0 may legitimately show (the
+    kink of ReLU: relu'(z) flips for |z| at rounding level between two fp32 summation orders).
     """
     ref = feats[names[0]]
     B = ref.shape[0]
@@ -143,9 +148,14 @@ def hybrid_forward(params: Mapping[str, torch.Tensor], names: Sequence[str],
     for i, m in enumerate(names):
         x = feats[m]
         mk = mask[:, i].reshape(-1, *([1] * (x.dim() - 1)))
-        z = linear(_dropout(x * mk, p, train, gen, SITE_IN + i), params[f"projections.{m}.0.weight"],
-                   params[f"projections.{m}.0.bias"])
-        P[m] = _dropout(torch.relu(z), p, train, gen, SITE_PROJ + i)
+        xd = _dropout(x * mk, p, train, gen, SITE_IN + i)
+        z = linear(xd, params[f"projections.{m}.0.weight"], params[f"projections.{m}.0.bias"])
+        a = torch.relu(z)
+        if taps is not None:
+            taps[f"in/{m}"], taps[f"z/{m}"], taps[f"a/{m}"] = xd.detach(), z.detach(), a
+            if a.requires_grad:
+                a.retain_grad()
+        P[m] = _dropout(a, p, train, gen, SITE_PROJ + i)
     lists = {m: [P[m]] for m in names}
     maps: Dict[str, torch.Tensor] = {}
     for g, (q, k) in enumerate(pairs_present(names, params)):
@@ -162,8 +172,13 @@ def hybrid_forward(params: Mapping[str, torch.Tensor], names: Sequence[str],
     pooled_t = torch.stack(pooled, 1)
     w = adaptive_weights(params, names, {m: pooled[i] for i, m in enumerate(names)}, mask)
     fused = (pooled_t * w.unsqueeze(-1)).sum(1)
-    h = _dropout(torch.relu(linear(fused, params["classifier.0.weight"], params["classifier.0.bias"])),
-                 p, train, gen, SITE_CLS)
+    zc = linear(fused, params["classifier.0.weight"], params["classifier.0.bias"])
+    ac = torch.relu(zc)
+    if taps is not None:
+        taps["in/cls"], taps["z/cls"], taps["a/cls"] = fused.detach(), zc.detach(), ac
+        if ac.requires_grad:
+            ac.retain_grad()
+    h = _dropout(ac, p, train, gen, SITE_CLS)
     logits = linear(h, params["classifier.3.weight"], params["classifier.3.bias"])
     return logits, {"attention_maps": maps, "fusion_weights": w, "pooled": pooled_t}
 

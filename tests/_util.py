@@ -170,6 +170,31 @@ def diff_report(got, ref, rtol: float, atol: float = 0.0) -> str:
             f"{nbad} of {ref.numel()} elements over")
 
 
+def relu_kink_slack(taps: dict, layer: str, weight: torch.Tensor, rel: float = 1e-5):
+    """Per-element slack of a ReLU layer's weight and bias gradients for pre-activations within
+    rounding of zero.  Where |z| <= rel * (|x| @ |W|^T) (rows of the layer input x), two fp32
+    summation orders may disagree on the sign of z, so relu'(z) -- and with it that row's whole
+    contribution dL/da * x to dW (dL/da to db) -- may be present on one side only.  Returns
+    (slack_w, slack_b): the sums of those contributions' magnitudes (0 where no z is that close)."""
+    x = taps[f"in/{layer}"].double().reshape(-1, weight.shape[1])
+    z = taps[f"z/{layer}"].double().reshape(-1, weight.shape[0])
+    ga = taps[f"a/{layer}"].grad.double().reshape(-1, weight.shape[0]).abs()
+    scale = x.abs() @ weight.detach().double().abs().t()
+    amb = (z.abs() <= rel * scale).double()
+    return (ga * amb).t() @ x.abs(), (ga * amb).sum(0)
+
+
+def close_slack(got, ref, rtol: float, atol: float, slack) -> bool:
+    """close(), with an elementwise allowance ``slack`` added to the bound."""
+    got = torch.as_tensor(got).double().cpu()
+    ref = torch.as_tensor(ref).double().cpu()
+    assert got.shape == ref.shape, (tuple(got.shape), tuple(ref.shape))
+    if ref.numel() == 0:
+        return True
+    bound = rtol * float(ref.abs().max()) + atol
+    return bool(((got - ref).abs() <= bound + torch.as_tensor(slack).double().reshape(ref.shape)).all())
+
+
 def close(got, ref, rtol: float, atol: float = 0.0) -> bool:
     """max|got-ref| <= rtol*max|ref| + atol.  atol only matters for tensors whose
     reference is mathematically zero (e.g. key_proj.bias grads: softmax is

@@ -18,7 +18,7 @@ import pytest
 import torch
 
 from _philox import mask_provider
-from _util import close
+from _util import close, close_slack, diff_report, relu_kink_slack
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -84,10 +84,19 @@ def test_benchmark_step_matches_oracle(env, workload):
     params = {k: v.clone().requires_grad_(True) for k, v in params_cpu.items()}
     xs = {n: f.detach().cpu().clone().requires_grad_(True) for n, f in zip(names, feats)}
     torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    taps = {}
     logits, _ = hybrid_forward(params, names, xs, mask.cpu(), w["heads"], p=0.1, train=True,
-                               gen=mask_provider(seed, offset, 0.1))
+                               gen=mask_provider(seed, offset, 0.1), taps=taps)
     loss = cross_entropy_ls(logits, labels.cpu())
     loss.backward()
+    # ReLU-layer gradients: allowance for pre-activations within rounding of 0 (relu' may flip
+    # between two fp32 summation orders; the module's Philox seed depends on how many modules the
+    # process built before, and some seeds put a |z| ~ 1e-7 where its row's dL/da is large)
+    slack = {}
+    for m in names + ["cls"]:
+        wname = f"projections.{m}.0.weight" if m != "cls" else "classifier.0.weight"
+        sw, sb = relu_kink_slack(taps, m, params[wname])
+        slack[wname], slack[wname[:-len("weight")] + "bias"] = sw, sb
 
     assert close(step.logits.cpu(), logits.detach(), 1e-3, 1e-6 * float(logits.detach().abs().max()))
     assert abs(float(step.loss.item()) - float(loss.detach())) <= 1e-5 * max(1.0, abs(float(loss.detach())))
@@ -95,10 +104,76 @@ def test_benchmark_step_matches_oracle(env, workload):
     scale = max([float(p.grad.abs().max()) for p in params.values()] +
                 [float(x.grad.abs().max()) for x in xs.values()])
     for i, n in enumerate(names):
-        assert close(step.dx[i].cpu(), xs[n].grad, 1e-3, 1e-5 * scale), f"dx/{n}"
+        assert close(step.dx[i].cpu(), xs[n].grad, 1e-3, 1e-5 * scale), \
+            f"dx/{n}: " + diff_report(step.dx[i].cpu(), xs[n].grad, 1e-3, 1e-5 * scale)
     for n, p in params.items():
         g = grads[n].cpu()
         if max(w["L"]) == 0 and (".query_proj." in n or ".key_proj." in n):
             assert torch.all(g == 0), n      # softmax over one key: exact zeros (src/attention.py:118-129)
             continue
-        assert close(g, p.grad, 1e-3, 1e-5 * scale), n
+        if n in slack:
+            assert close_slack(g, p.grad, 1e-3, 1e-5 * scale, slack[n]), \
+                f"{n}: " + diff_report(g, p.grad, 1e-3, 1e-5 * scale)
+            continue
+        assert close(g, p.grad, 1e-3, 1e-5 * scale), f"{n}: " + diff_report(g, p.grad, 1e-3, 1e-5 * scale)
+
+
+def _poison_allocator(dev, big_mb=4096, small_n=512):
+    """Fill the caching allocator's free blocks with NaN: large segments (split later for large
+    requests) and small-pool blocks.  A kernel that reads memory no kernel of the step wrote then
+    produces NaN instead of a silently stale value (the way an earlier test's leftovers crept
+    into a weight gradient only in one test order)."""
+    keep = []
+    for _ in range(big_mb // 256):
+        keep.append(torch.full((256 << 18,), float("nan"), device=dev))
+    for i in range(small_n):
+        keep.append(torch.full((((i % 8) + 1) << 14,), float("nan"), device=dev))
+    torch.cuda.synchronize()
+    del keep
+
+
+@pytest.mark.parametrize("workload", ["c2", "c2_l1"])
+def test_step_reads_no_uninitialized_memory(env, workload):
+    """Every output of the benchmarked step (logits, loss, each parameter gradient, dX) is finite
+    when the step's buffers come from NaN-filled allocator blocks, both for the eager call and
+    for a captured graph's replay; and the poisoned replay equals a replay on zero-filled blocks
+    bit for bit."""
+    bench, fusion, mmf_native, train_step = env
+    prev = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision("highest")
+    dev = torch.device("cuda", 0)
+    w = bench.WORKLOADS[workload]
+    names = [f"m{i}" for i in range(w["M"])]
+
+    def run(poison):
+        torch.cuda.empty_cache()
+        if poison:
+            _poison_allocator(dev)
+        torch.manual_seed(0)
+        model = fusion.HybridFusion({n: w["D"] for n in names}, hidden_dim=w["H"], num_classes=w["C"],
+                                    num_heads=w["heads"], dropout=0.1).to(dev)
+        feats, mask, labels = bench.make_inputs(w, w["B"], 42, dev)
+        step = train_step.HybridTrainStep(model, feats, mask, labels)
+        step.rng.copy_(torch.tensor([0x5EED, 7], dtype=torch.int64))
+        step.forward_backward()
+        torch.cuda.synchronize()
+        eager = [t.detach().cpu().clone() for t in (step.logits, step.grad, *step.dx)]
+        step.capture()
+        step.rng.copy_(torch.tensor([0x5EED, 7], dtype=torch.int64))
+        step.graph.replay()
+        torch.cuda.synchronize()
+        replay = [t.detach().cpu().clone() for t in (step.logits, step.grad, *step.dx)]
+        names_out = ["logits", "grad"] + [f"dx/{n}" for n in names]
+        for n, e, r in zip(names_out, eager, replay):
+            assert torch.isfinite(e).all(), (poison, "eager", n, int((~torch.isfinite(e)).sum()))
+            assert torch.isfinite(r).all(), (poison, "replay", n, int((~torch.isfinite(r)).sum()))
+            assert torch.equal(e, r), (poison, n)
+        return replay
+
+    try:
+        a = run(True)
+        b = run(False)
+    finally:
+        torch.set_float32_matmul_precision(prev)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
