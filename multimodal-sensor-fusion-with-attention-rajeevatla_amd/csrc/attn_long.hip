@@ -389,12 +389,15 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
         const float4 g4 = *reinterpret_cast<const float4*>(gs + kt * 32 + 8 * g + 4 * hh);
         const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < 4; j += 2) {
           const int e = 4 * g + j;
-          const float p = __builtin_amdgcn_exp2f(s[e] * sl2 - lse2);
-          const float gk = keep_sel(words[i], j + 8 * g, gv[j]);
-          pv[i][e] = p;
-          pk[i][e] = p * gk;
+          // (the exp arguments as packed FMAs: 16 v_pk_fma_f32 for the 32 scores)
+          const f32x2 x = f32x2{s[e], s[e + 1]} * f32x2{sl2, sl2} - f32x2{lse2, lse2};
+          const float p0 = __builtin_amdgcn_exp2f(x[0]), p1 = __builtin_amdgcn_exp2f(x[1]);
+          pv[i][e] = p0;
+          pv[i][e + 1] = p1;
+          pk[i][e] = p0 * keep_sel(words[i], j + 8 * g, gv[j]);
+          pk[i][e + 1] = p1 * keep_sel(words[i], j + 1 + 8 * g, gv[j + 1]);
         }
       }
     }
@@ -775,8 +778,9 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_poolL_fwd_fused_bf16(const At
       f32x2 pr[8];
 #pragma unroll
       for (int e = 0; e < 16; e += 2) {
-        x[i][e] = __builtin_amdgcn_exp2f(__builtin_fmaf(x[i][e], sl2, -mref));
-        x[i][e + 1] = __builtin_amdgcn_exp2f(__builtin_fmaf(x[i][e + 1], sl2, -mref));
+        const f32x2 y = f32x2{x[i][e], x[i][e + 1]} * f32x2{sl2, sl2} - f32x2{mref, mref};   // (v_pk_fma_f32)
+        x[i][e] = __builtin_amdgcn_exp2f(y[0]);
+        x[i][e + 1] = __builtin_amdgcn_exp2f(y[1]);
         pr[e >> 1] = f32x2{x[i][e], x[i][e + 1]};
       }
       ls += tree_sum<8>(pr);
