@@ -117,8 +117,8 @@ def kernel_precision(kname):
         return 0
     if "_bf16<" in kname or "_b16_kernel" in kname:   # the bf16-only kernels (attn_poolL_*_fused_bf16<DROP>,
         return 1                                       # gemm_wsr_b16_kernel<NS>)
-    if kname.startswith("gemm_lds_kernel<") and kname.count(",") == 5:
-        return 1                   # the bf16-operand forms: <A, B, 32, 3, 1, B16 form 1 | 2 | 3>
+    if kname.startswith("gemm_lds_kernel<") and kname.count(",") in (5, 6):
+        return 1                   # the bf16-operand forms: <A, B, 32, 3, 1, B16 form 1 | 2 | 3[, WIDE]>
     m = re.search(r"[<, ]([012])(?:, (?:true|false)){0,3}>$", kname)
     return int(m.group(1)) if m else 0
 

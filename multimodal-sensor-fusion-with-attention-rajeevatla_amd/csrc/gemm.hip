@@ -96,8 +96,8 @@ __device__ __forceinline__ int group_of_block(const GemmArgs& args, int& local) 
 // member r % n_in.  Where the sets do not come in multiples of 8 the plain order stays.  (C5 dZ,
 // two column tiles: the A rows were fetched once per column tile, 5.4 GB per step for 3.2 GB of
 // operands.)
-__device__ __forceinline__ bool tile_ctx(const GemmGroup& G, int local, TileCtx& t) {
-  const int tiles_n = (G.N + BN - 1) / BN;
+__device__ __forceinline__ bool tile_ctx(const GemmGroup& G, int local, TileCtx& t, int bn = BN) {
+  const int tiles_n = (G.N + bn - 1) / bn;
   const int tiles_m = (G.M + BM - 1) / BM;
   t.nsplit = (G.epi & EPI_PARTIAL) ? G.nsplit : 1;
   const int per_batch = tiles_m * tiles_n * t.nsplit;
@@ -112,17 +112,17 @@ __device__ __forceinline__ bool tile_ctx(const GemmGroup& G, int local, TileCtx&
     if (t.nsplit > 1) {
       t.split = set;
       t.i0 = (mem / tiles_n) * BM;
-      t.j0 = (mem % tiles_n) * BN;
+      t.j0 = (mem % tiles_n) * bn;
     } else {
       t.split = 0;
       t.i0 = set * BM;
-      t.j0 = mem * BN;
+      t.j0 = mem * bn;
     }
   } else {
     t.split = tile % t.nsplit;
     tile /= t.nsplit;
     t.i0 = (tile / tiles_n) * BM;
-    t.j0 = (tile % tiles_n) * BN;
+    t.j0 = (tile % tiles_n) * bn;
   }
   t.Cb = (G.epi & EPI_PARTIAL) ? G.C + (int64_t)t.batch * t.nsplit * G.M * G.N
                                : G.C + (int64_t)t.batch * G.bs_c;
@@ -458,24 +458,33 @@ __device__ __forceinline__ void lds_barrier() {
 struct KCursor { int si, k0, kend; };
 
 // B16: both operands bf16 in HBM (BF = 1, DK = 32 bf16 k per tile): 1 RK / RK (stage_tile_b16),
-// 2 KR / KR (stage_tile_b16_kr: weight gradients), 3 RK / KR (dZ = dQ W_q)
-template <int AMODE, int BMODE, int DK, int NSTAGE, int BF = 0, int B16 = 0>
+// 2 KR / KR (stage_tile_b16_kr: weight gradients), 3 RK / KR (dZ = dQ W_q).
+// WIDE (B16 forms 2 / 3, N % 256 == 0): 128 x 256 output tiles -- a stage holds A and TWO B
+// tiles, wave (wm, wn) the 64 rows wm and the columns wn * 64 + {0, 32} of each 128-column half
+// (acc[a][b], b >> 1 = half), and the epilogue runs once per half.  With N = 256 (dZ: every
+// modality's H; the weight gradients' H x H) a tile covers every column, so its A rows are read
+// once instead of once per 128-column tile (the second read relied on L2 timing: 1.6 x the
+// operand bytes from HBM at C5).
+template <int AMODE, int BMODE, int DK, int NSTAGE, int BF = 0, int B16 = 0, int WIDE = 0>
 __global__ __launch_bounds__(NT, (NSTAGE * (B16 ? DK / 2 : DK) <= 32 ? 4 : 2)) void gemm_lds_kernel(const GemmArgs args) {
   static_assert(!B16 || (BF == 1 && DK == 32 && AMODE == (B16 == 2 ? MODE_KR : MODE_RK) &&
                          BMODE == (B16 == 1 ? MODE_RK : MODE_KR)),
                 "bf16-operand form");
+  static_assert(!WIDE || B16 >= 2, "WIDE: bf16 forms 2 / 3");
+  constexpr int NB = WIDE ? 2 : 1;                      // B tiles per stage
   constexpr int DTILE = B16 ? BM * DK / 2 : BM * DK;   // floats per operand tile
-  constexpr int DMA_PER_TILE = B16 ? 2 * (BM * DK / 2048) : 2 * (BM * DK / 1024);  // glds per wave per (A, B) pair
+  constexpr int DMA_PER_TILE = B16 ? (1 + NB) * (BM * DK / 2048) : 2 * (BM * DK / 1024);  // glds per wave per stage
   int local;
   const GemmGroup& G = args.g[group_of_block(args, local)];
   TileCtx T;
-  if (!tile_ctx(G, local, T)) return;
+  if (!tile_ctx(G, local, T, NB * BN)) return;
   const int64_t offA = (int64_t)T.batch * G.bs_a, offB = (int64_t)T.batch * G.bs_b;
 
-  // one LDS object: NSTAGE x [A | B] tiles (also the epilogue image) + 128 floats for the row-sum combine
-  __shared__ __attribute__((aligned(16))) float lds[NSTAGE * 2 * DTILE + BM];
-  constexpr int PR = NSTAGE * 2 * DTILE >= 64 * CS ? 64 : 32;   // epilogue rows per LDS pass
-  static_assert(NSTAGE * 2 * DTILE >= PR * CS, "epilogue image does not fit");
+  // one LDS object: NSTAGE x [A | B (| B)] tiles (also the epilogue image) + 128 floats for the row-sum combine
+  constexpr int SSTRIDE = (1 + NB) * DTILE;   // floats per stage
+  __shared__ __attribute__((aligned(16))) float lds[NSTAGE * SSTRIDE + BM];
+  constexpr int PR = NSTAGE * SSTRIDE >= 64 * CS ? 64 : 32;   // epilogue rows per LDS pass
+  static_assert(NSTAGE * SSTRIDE >= PR * CS, "epilogue image does not fit");
 
   const int t = threadIdx.x;
   const int lane = t & 63, wave = t >> 6;
@@ -488,11 +497,11 @@ __global__ __launch_bounds__(NT, (NSTAGE * (B16 ? DK / 2 : DK) <= 32 ? 4 : 2)) v
   if (p > 0.f && args.rng) rs = *args.rng;
   if (args.rng_advance && blockIdx.x == 0 && threadIdx.x == 0) args.rng_advance[1] += 1;   // see launch_gemm
 
-  f32x16 acc[2][2];
+  f32x16 acc[2][2 * NB];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < 2 * NB; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
@@ -528,16 +537,21 @@ __global__ __launch_bounds__(NT, (NSTAGE * (B16 ? DK / 2 : DK) <= 32 ? 4 : 2)) v
       opB = args.s[G.src_begin + k.si].b;
       op_si = k.si;
     }
-    float* At = lds + buf * 2 * DTILE;
+    float* At = lds + buf * SSTRIDE;
     if constexpr (B16) {
       if constexpr (AMODE == MODE_KR)
         stage_tile_b16_kr(At, opA, offA + seg * opA.seg_stride, T.i0, G.M, k.k0, k.kend, wave, lane);
       else
         stage_tile_b16(At, opA, offA + seg * opA.seg_stride, T.i0, G.M, k.k0, k.kend, wave, lane);
-      if constexpr (BMODE == MODE_KR)
-        stage_tile_b16_kr(At + DTILE, opB, offB + seg * opB.seg_stride, T.j0, G.N, k.k0, k.kend, wave, lane);
-      else
-        stage_tile_b16(At + DTILE, opB, offB + seg * opB.seg_stride, T.j0, G.N, k.k0, k.kend, wave, lane);
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        if constexpr (BMODE == MODE_KR)
+          stage_tile_b16_kr(At + (1 + nb) * DTILE, opB, offB + seg * opB.seg_stride, T.j0 + nb * BN, G.N, k.k0, k.kend,
+                            wave, lane);
+        else
+          stage_tile_b16(At + (1 + nb) * DTILE, opB, offB + seg * opB.seg_stride, T.j0 + nb * BN, G.N, k.k0, k.kend,
+                         wave, lane);
+      }
     } else {
       stage_tile<AMODE, DK>(At, opA, offA + seg * opA.seg_stride, T.i0, G.M, k.k0, k.kend, wave, lane);
       stage_tile<BMODE, DK>(At + DTILE, opB, offB + seg * opB.seg_stride, T.j0, G.N, k.k0, k.kend, wave, lane);
@@ -568,15 +582,18 @@ __global__ __launch_bounds__(NT, (NSTAGE * (B16 ? DK / 2 : DK) <= 32 ? 4 : 2)) v
       // the barrier also means every wave is done with the buffer restaged below
       wait_tiles(nissued - tile - 1);
       lds_barrier();
-      float* At = lds + buf * 2 * DTILE;
+      float* At = lds + buf * SSTRIDE;
       float* Bt = At + DTILE;
       const int kv = cur.kend - cur.k0;
       if (kv < DK) {
         if constexpr (B16) {
           if constexpr (AMODE == MODE_KR) zero_tail_b16_kr(At, kv);
           else zero_tail_b16(At, kv);
-          if constexpr (BMODE == MODE_KR) zero_tail_b16_kr(Bt, kv);
-          else zero_tail_b16(Bt, kv);
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb) {
+            if constexpr (BMODE == MODE_KR) zero_tail_b16_kr(Bt + nb * DTILE, kv);
+            else zero_tail_b16(Bt + nb * DTILE, kv);
+          }
         } else {
           zero_tail<AMODE, DK>(At, kv);
           zero_tail<BMODE, DK>(Bt, kv);
@@ -608,17 +625,20 @@ __global__ __launch_bounds__(NT, (NSTAGE * (B16 ? DK / 2 : DK) <= 32 ? 4 : 2)) v
 if constexpr (B16) {
 #pragma unroll
         for (int u = 0; u < DK / 16; ++u) {
-          bf16x8 av[2], bv[2];
+          bf16x8 av[2], bv[2 * NB];
 #pragma unroll
           for (int a = 0; a < 2; ++a)
             av[a] = AMODE == MODE_KR ? frag_b16_kr(At, wm * 64 + a * 32, u, lane) : frag_b16(At, wm * 64 + a * 32 + c, u, h);
 #pragma unroll
-          for (int b = 0; b < 2; ++b)
-            bv[b] = BMODE == MODE_KR ? frag_b16_kr(Bt, wn * 64 + b * 32, u, lane) : frag_b16(Bt, wn * 64 + b * 32 + c, u, h);
+          for (int b = 0; b < 2 * NB; ++b) {
+            const float* Bh = Bt + (b >> 1) * DTILE;   // (the 128-column half)
+            bv[b] = BMODE == MODE_KR ? frag_b16_kr(Bh, wn * 64 + (b & 1) * 32, u, lane)
+                                     : frag_b16(Bh, wn * 64 + (b & 1) * 32 + c, u, h);
+          }
 #pragma unroll
           for (int a = 0; a < 2; ++a)
 #pragma unroll
-            for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[a], bv[b], acc[a][b], 0, 0, 0);
+            for (int b = 0; b < 2 * NB; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[a], bv[b], acc[a][b], 0, 0, 0);
         }
       } else if constexpr (BF != 0) {
         // chunks 2u, 2u+1 (16 k) -> one bf16 MFMA per accumulator
@@ -670,14 +690,24 @@ if constexpr (B16) {
   }
 
   if (want_db) {
-    float* red = lds + NSTAGE * 2 * DTILE;
+    float* red = lds + NSTAGE * SSTRIDE;
     __syncthreads();
     if (t >= BM) red[t - BM] = dbsum;
     __syncthreads();
     if (t < BM && T.i0 + t < G.M)
       T.part_db[(int64_t)T.split * G.M + T.i0 + t] = (dbsum + red[t]) * G.alpha;
   }
-  epilogue<PR>(G, T, acc, lds, rs, p, inv_keep, wm, wn, h, c);
+  if constexpr (WIDE) {
+    // one epilogue per 128-column half (each re-syncs before it reuses the LDS image)
+    f32x16 lo[2][2] = {{acc[0][0], acc[0][1]}, {acc[1][0], acc[1][1]}};
+    epilogue<PR>(G, T, lo, lds, rs, p, inv_keep, wm, wn, h, c);
+    TileCtx T2 = T;
+    T2.j0 += BN;
+    f32x16 hi[2][2] = {{acc[0][2], acc[0][3]}, {acc[1][2], acc[1][3]}};
+    epilogue<PR>(G, T2, hi, lds, rs, p, inv_keep, wm, wn, h, c);
+  } else {
+    epilogue<PR>(G, T, acc, lds, rs, p, inv_keep, wm, wn, h, c);
+  }
 }
 
 // ------------------------------------------------------------------ weight-stationary kernel
@@ -1893,6 +1923,16 @@ hipError_t launch_gemm_b16(const GemmJob* jobs_in, int njobs, hipStream_t st, in
   }
   const int ilv_mode = gemm_interleave_mode();
   const bool ilv_on = ilv_mode == 2 || (ilv_mode == 1 && !any_partial);
+  // 128 x 256 tiles (WIDE) for the weight gradients (form 2) when every job's N is a multiple of
+  // 256: C5 0.89 -> 0.85 ms per step.  dZ (form 3) measured 0.99 -> 1.01 ms with them (its second
+  // column tile already found the A rows in L2: 1.62 -> 1.51 GB read per launch), so it keeps
+  // 128 x 128 unless MMF_GEMM_WIDE_DZ=1; MMF_GEMM_NO_WIDE=1: 128 x 128 everywhere (A/B,
+  // profiles/r05/c5_gemm_wide/)
+  static const bool no_wide = getenv("MMF_GEMM_NO_WIDE") != nullptr;
+  static const bool wide_dz = getenv("MMF_GEMM_WIDE_DZ") != nullptr;
+  bool wide = !no_wide && (form == 2 || (form == 3 && wide_dz));
+  for (int i = 0; i < njobs && wide; ++i) wide = jobs_in[i].g.N % (2 * BN) == 0;
+  const int bn = wide ? 2 * BN : BN;
   std::vector<uintptr_t> share(njobs, 0);
   for (int i = 0; i < njobs; ++i) {
     const uintptr_t a = (uintptr_t)jobs_in[i].src[0].a.ptr, b = (uintptr_t)jobs_in[i].src[0].b.ptr;
@@ -1920,7 +1960,7 @@ hipError_t launch_gemm_b16(const GemmJob* jobs_in, int njobs, hipStream_t st, in
       const bool partial = (g.epi & EPI_PARTIAL) != 0;
       args.tile_off[ng] = max_blocks;
       args.g[ng++] = g;
-      max_blocks += ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN) * (partial ? g.nsplit : 1);
+      max_blocks += ((g.M + BM - 1) / BM) * ((g.N + bn - 1) / bn) * (partial ? g.nsplit : 1);
       ++done;
     }
     args.ngroups = ng;
@@ -1944,9 +1984,13 @@ hipError_t launch_gemm_b16(const GemmJob* jobs_in, int njobs, hipStream_t st, in
     }
     static const char* const kName[4] = {"", "gemm_lds_kernel<0, 0, 32, 3, 1, 1>", "gemm_lds_kernel<1, 1, 32, 3, 1, 2>",
                                          "gemm_lds_kernel<0, 1, 32, 3, 1, 3>"};
-    ProfLaunch prof_(st, kName[form], fl, by);
+    static const char* const kNameW[4] = {"", "", "gemm_lds_kernel<1, 1, 32, 3, 1, 2, 1>",
+                                          "gemm_lds_kernel<0, 1, 32, 3, 1, 3, 1>"};
+    ProfLaunch prof_(st, wide ? kNameW[form] : kName[form], fl, by);
     if (form == 1) mmf_launch((gemm_lds_kernel<MODE_RK, MODE_RK, 32, 3, 1, 1>), dim3(max_blocks, 1), dim3(NT), 0, st, args);
+    else if (form == 2 && wide) mmf_launch((gemm_lds_kernel<MODE_KR, MODE_KR, 32, 3, 1, 2, 1>), dim3(max_blocks, 1), dim3(NT), 0, st, args);
     else if (form == 2) mmf_launch((gemm_lds_kernel<MODE_KR, MODE_KR, 32, 3, 1, 2>), dim3(max_blocks, 1), dim3(NT), 0, st, args);
+    else if (wide) mmf_launch((gemm_lds_kernel<MODE_RK, MODE_KR, 32, 3, 1, 3, 1>), dim3(max_blocks, 1), dim3(NT), 0, st, args);
     else mmf_launch((gemm_lds_kernel<MODE_RK, MODE_KR, 32, 3, 1, 3>), dim3(max_blocks, 1), dim3(NT), 0, st, args);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -82,13 +82,16 @@ def test_rk_rk_bf16_out_lds_kernel():
 
 
 @pytest.mark.parametrize("M,N,K,nsplit,bias", [(256, 256, 1000, 1, False), (136, 256, 4096, 5, True),
-                                               (256, 264, 65, 1, True), (384, 128, 8192, 16, True)])
+                                               (256, 264, 65, 1, True), (384, 128, 8192, 16, True),
+                                               (256, 512, 2048, 8, True)])
 def test_kr_kr(M, N, K, nsplit, bias):
     _run(M, N, K, True, True, nsplit=nsplit, bias=bias)
 
 
-@pytest.mark.parametrize("M,N,K", [(300, 256, 512), (1024, 256, 2560), (64, 72, 24)])
+@pytest.mark.parametrize("M,N,K", [(300, 256, 512), (1024, 256, 2560), (64, 72, 24), (260, 512, 96)])
 def test_rk_kr(M, N, K):
+    # (N % 256 == 0 takes the 128 x 256 WIDE tiles under MMF_GEMM_WIDE_DZ=1: these cases passed
+    # with them as the default, profiles/r05/c5_gemm_wide/pytest.log)
     _run(M, N, K, False, True)
 
 
