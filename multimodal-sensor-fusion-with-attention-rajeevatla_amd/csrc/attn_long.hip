@@ -277,31 +277,36 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
     const float gsc = inv_keep / (float)Lq;   // dP'[q, k] = dpbar[k] / Lq, through the dropout scale
     for (int k = t; k < Lk; k += LF_NT) gs[k] = P.dpbar[bh * Lk + k] * gsc;
   }
-  // query block images: threads 0..255 stage row t >> 3, chunk t & 7; threads 256..287 the LSE
-  // (raw prefetches; waves 0-3 the Q chunks, wave 4 the LSE -- wave-uniform guards)
-  // (the resources are rebuilt at each use from the wave-uniform bases: held across the loop,
-  // they were kept in VGPRs and every load became a waterfall loop)
-  const uint32_t q_voff = (uint32_t)((((t >> 3) & 31) * P.ldq + 8 * (t & 7)) * 2);
+  // query block images: the younger half (waves 4-7, thread tq = t - 256: row tq >> 3, chunk tq & 7)
+  // stages the Q chunks, lanes 0-31 of wave 0 the LSE -- the older half is the pole at both
+  // barriers once the younger issues at priority 1, so the extra work goes to the younger
+  // (raw prefetches, wave-uniform guards; the resources are rebuilt at each use from the
+  // wave-uniform bases: held across the loop, they were kept in VGPRs and every load became a
+  // waterfall loop)
+  constexpr int QW0 = 4, LW = 0;
+  const int tq = t - 64 * QW0;
+  const bool qstage = w >= QW0 && w < QW0 + 4;
+  const uint32_t q_voff = (uint32_t)((((tq >> 3) & 31) * P.ldq + 8 * (tq & 7)) * 2);
   const __bf16* q_u = sgpr_ptr(reinterpret_cast<const __bf16*>(P.q) + q_off);
   const float* lse_u = sgpr_ptr(P.lse + bh * Lq);
   const uint32_t q_bytes = (uint32_t)(((int64_t)(Lq - 1) * P.ldq + hd) * 2);
   auto q_load = [&](int qb, bf16x8& v, float& l) {
-    const int row = (t >> 3) & 31, q = qb * LF_QB + row;
-    if (w < 4) {
+    const int row = (tq >> 3) & 31, q = qb * LF_QB + row;
+    if (qstage) {
       if (qkb) v = buf_b128(buf_rsrc(q_u, q_bytes), q_voff, (uint32_t)(qb * LF_QB * P.ldq * 2));
-      else v = row_chunk(P.q, false, q_off + (int64_t)(q < Lq ? q : 0) * P.ldq, t & 7, hd, q < Lq);
+      else v = row_chunk(P.q, false, q_off + (int64_t)(q < Lq ? q : 0) * P.ldq, tq & 7, hd, q < Lq);
     }
-    if (w == 4) l = __uint_as_float(buf_b32(buf_rsrc(lse_u, (uint32_t)Lq * 4u), (uint32_t)(t & 31) * 4u, (uint32_t)(qb * LF_QB * 4)));
+    if (w == LW) l = __uint_as_float(buf_b32(buf_rsrc(lse_u, (uint32_t)Lq * 4u), (uint32_t)(t & 31) * 4u, (uint32_t)(qb * LF_QB * 4)));
   };
   auto q_store = [&](int qb, int buf, const bf16x8& v, float l) {
-    const int q = qb * LF_QB + ((t >> 3) & 31);
-    if (t < 256)
-      *reinterpret_cast<bf16x8*>(lds + OFF_Q + buf * 4096 + img_off(t >> 3, t & 7)) =
-          chunk_keep(v, q < Lq && 8 * (t & 7) < hd);
+    const int q = qb * LF_QB + ((tq >> 3) & 31);
+    if (qstage)
+      *reinterpret_cast<bf16x8*>(lds + OFF_Q + buf * 4096 + img_off((tq >> 3) & 31, tq & 7)) =
+          chunk_keep(v, q < Lq && 8 * (tq & 7) < hd);
     // log2 units; +inf for an invalid or fully masked query: every p = exp2(s - inf) = 0
     const int ql = qb * LF_QB + (t & 31);
-    if (t >= 256 && t < 256 + LF_QB)
-      lse_s[buf * LF_QB + (t - 256)] = (ql >= Lq || l == -INFINITY) ? INFINITY : l * LF_LOG2E;
+    if (w == LW && lane < LF_QB)
+      lse_s[buf * LF_QB + lane] = (ql >= Lq || l == -INFINITY) ? INFINITY : l * LF_LOG2E;
   };
   {
     bf16x8 v;
@@ -414,7 +419,7 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
     float D = 0.f;
 #pragma unroll
     for (int ww = 0; ww < 8; ++ww) D += Dpart[buf * 256 + ww * 32 + r];
-    if (w == 0 && hh == 0 && qvalid) P.dsum[bh * Lq + q] = D;
+    if (w == 7 && hh == 0 && qvalid) P.dsum[bh * Lq + q] = D;   // (a younger wave: see q_load)
 
     // dS = P (keep g - D) of both tiles first (the bf16 A operands of dQ = dS K, register
     // e = 8 s2 + j): P and keep * P * g die here, before the matrix-core phase
@@ -653,21 +658,25 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_poolL_fwd_fused_bf16(const At
       kf[i][s4] = row_chunk(P.k, qkb, k_off + (int64_t)(krow < Lk ? krow : 0) * P.ldk, 2 * s4 + hh, hd, krow < Lk);
   }
   // (raw prefetches through buffer loads: waves 0-3 stage the Q chunks)
-  const uint32_t q_voff = (uint32_t)((((t >> 3) & 31) * P.ldq + 8 * (t & 7)) * 2);
+  // (the younger half's first 4 waves stage the Q images, as the backward)
+  constexpr int QW0 = NW / 2;
+  const int tq = t - 64 * QW0;
+  const bool qstage = w >= QW0 && w < QW0 + 4;
+  const uint32_t q_voff = (uint32_t)((((tq >> 3) & 31) * P.ldq + 8 * (tq & 7)) * 2);
   const __bf16* q_u = sgpr_ptr(reinterpret_cast<const __bf16*>(P.q) + q_off);
   const uint32_t q_bytes = (uint32_t)(((int64_t)(Lq - 1) * P.ldq + hd) * 2);
   auto q_load = [&](int qb, bf16x8& v) {
-    const int q = qb * LF_QB + ((t >> 3) & 31);
-    if (w < 4) {
+    const int q = qb * LF_QB + ((tq >> 3) & 31);
+    if (qstage) {
       if (qkb) v = buf_b128(buf_rsrc(q_u, q_bytes), q_voff, (uint32_t)(qb * LF_QB * P.ldq * 2));
-      else v = row_chunk(P.q, false, q_off + (int64_t)(q < Lq ? q : 0) * P.ldq, t & 7, hd, q < Lq);
+      else v = row_chunk(P.q, false, q_off + (int64_t)(q < Lq ? q : 0) * P.ldq, tq & 7, hd, q < Lq);
     }
   };
   auto q_store = [&](int qb, int buf, const bf16x8& v) {
-    const int q = qb * LF_QB + ((t >> 3) & 31);
-    if (t < 256)
-      *reinterpret_cast<bf16x8*>(lds + FOFF_Q + buf * 4096 + img_off(t >> 3, t & 7)) =
-          chunk_keep(v, q < Lq && 8 * (t & 7) < hd);
+    const int q = qb * LF_QB + ((tq >> 3) & 31);
+    if (qstage)
+      *reinterpret_cast<bf16x8*>(lds + FOFF_Q + buf * 4096 + img_off((tq >> 3) & 31, tq & 7)) =
+          chunk_keep(v, q < Lq && 8 * (tq & 7) < hd);
   };
   {
     bf16x8 v;
@@ -805,7 +814,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_poolL_fwd_fused_bf16(const At
         for (int i = 0; i < n; ++i) sp[i] += sp[i + n];
       l = sp[0];
     }
-    if (w == 0 && hh == 0 && qvalid) P.lse[bh * Lq + q] = l > 0.f ? (m + __log2f(l)) * (1.f / LF_LOG2E) : -INFINITY;
+    if (w == NW - 1 && hh == 0 && qvalid) P.lse[bh * Lq + q] = l > 0.f ? (m + __log2f(l)) * (1.f / LF_LOG2E) : -INFINITY;
     // P' / Lq of this lane's query (0 for a query past Lq)
     const float cq = (qvalid && l > 0.f) ? inv_keep * __builtin_amdgcn_rcpf(l * (float)Lq) : 0.f;
 #pragma unroll
