@@ -150,10 +150,15 @@ def kernel_table(launches, steps):
             bound, ach, peak, unit = "mfma", flops / sec / 1e12 if sec else 0.0, fpeak, "TFLOP/s"
         else:
             bound, ach, peak, unit = "hbm", nbytes / sec / 1e9 if sec else 0.0, HBM_PEAK_GBS, "GB/s"
+        # the other roof's fraction beside it: a kernel at a small fraction of both (issue- or
+        # latency-bound, e.g. the C5 long-key backward) shows that here, not only its nominal bound
+        mfma_frac = (flops / sec / 1e12) / fpeak if sec else 0.0
+        hbm_frac = (nbytes / sec / 1e9) / HBM_PEAK_GBS if sec else 0.0
         out[kname] = {
             "ms_per_step": round(ms / steps, 4), "launches_per_step": round(n / steps, 2),
             "avg_launch_ms": round(ms / n, 5), "bound": bound, "achieved": round(ach, 2), "peak": peak,
             "unit": unit, "frac": round(ach / peak, 4),
+            "mfma_frac": round(mfma_frac, 4), "hbm_frac": round(hbm_frac, 4),
             "flops_per_launch": flops / n, "bytes_per_launch": nbytes / n,
         }
     return out
@@ -185,7 +190,8 @@ def dominant_roofline(kernels, workload="c2", precision="highest"):
     per_launch = k["flops_per_launch"] if k["bound"] == "mfma" else k["bytes_per_launch"]
     return {
         "bound": k["bound"], "achieved": k["achieved"], "peak": k["peak"], "unit": k["unit"],
-        "frac": k["frac"], "traffic": round(t) if t is not None else None,
+        "frac": k["frac"], "mfma_frac": k["mfma_frac"], "hbm_frac": k["hbm_frac"],
+        "traffic": round(t) if t is not None else None,
         "kernel": kname, "avg_launch_ms": k["avg_launch_ms"], "launches_per_step": k["launches_per_step"],
         "algorithmic_per_launch": round(per_launch),
         "algorithmic_bytes_per_launch": round(k["bytes_per_launch"]),
@@ -477,7 +483,7 @@ def main(argv=None):
                                                   for v in kernels.values()) / 1e9, 2),
             "stage_ms": {k: round(v, 4) for k, v in sorted(avg_ms.items(), key=lambda kv: -kv[1])},
             "kernels": {k: {kk: v[kk] for kk in ("ms_per_step", "launches_per_step", "avg_launch_ms",
-                                                 "bound", "achieved", "unit", "frac")}
+                                                 "bound", "achieved", "unit", "frac", "mfma_frac", "hbm_frac")}
                         for k, v in list(kernels.items())[:12]},
             "loss": round(loss, 5),
         }
