@@ -396,6 +396,24 @@ __device__ __forceinline__ void stage_tile_b16(float* lds, const Operand& op, in
                                      (__attribute__((address_space(3))) void*)(lds + ins * 256), 16, 0, 0);
   }
 }
+// the same tile staged by NWV waves (8 / NWV pieces each)
+template <int NWV>
+__device__ __forceinline__ void stage_tile_b16_nw(float* lds, const Operand& op, int64_t boff, int e0, int eext, int k0,
+                                                  int kend, int wave, int lane) {
+  constexpr int PER_WAVE = BM * 32 * 2 / 1024 / NWV;
+  static_assert(PER_WAVE >= 1, "at most 8 staging waves");
+#pragma unroll
+  for (int u = 0; u < PER_WAVE; ++u) {
+    const int ins = wave * PER_WAVE + u;
+    const int row = ins * 16 + lane / 4;
+    const int slot = (lane & 3) ^ swz<16>(row);
+    const int e = min(e0 + row, eext - 1);
+    const int k = min(k0 + 8 * slot, kend - 8);
+    const __bf16* src = reinterpret_cast<const __bf16*>(op.ptr) + boff + (int64_t)e * op.ld + k;
+    __builtin_amdgcn_global_load_lds((const void*)src,
+                                     (__attribute__((address_space(3))) void*)(lds + ins * 256), 16, 0, 0);
+  }
+}
 __device__ __forceinline__ void zero_tail_b16(float* lds, int kv) {
   for (int idx = threadIdx.x; idx < BM * 4; idx += NT) {
     const int row = idx / 4, slot = idx % 4;
@@ -933,15 +951,19 @@ if constexpr (BF != 0) {
 constexpr int WSR16_NKS = 16;   // max 16-deep k-steps (K <= 256)
 typedef __bf16 bf16x4s __attribute__((ext_vector_type(4)));
 
-// WSR16_NS: the ring depth (tiles of 8 KB; WSR16_NS - 1 in flight ahead of the one being consumed)
-template <int WSR16_NS>
-__global__ __launch_bounds__(NT, 2) void gemm_wsr_b16_kernel(const GemmArgs args, int total_items, int K) {
+// WSR16_NS: the ring depth (tiles of 8 KB; WSR16_NS - 1 in flight ahead of the one being consumed).
+// NWV = 8 (one 512-thread workgroup per CU): 256-column groups, wave (wm, wn) the 64 rows wm and
+// the 64 columns wn of 4 -- both 128-column halves of a GEMM read each staged X tile, so X streams
+// once per 256 columns instead of once per 128 (C5: 10 instead of 20 passes per modality).
+template <int WSR16_NS, int NWV = 4>
+__global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void gemm_wsr_b16_kernel(const GemmArgs args, int total_items, int K) {
   constexpr int DTILE = BM * 32 / 2;   // floats per bf16 tile
+  constexpr int PW = BM * 32 * 2 / 1024 / NWV;   // LDS-DMA pieces per wave per tile
   __shared__ __attribute__((aligned(16))) float ring[WSR16_NS * DTILE];
   const int t = threadIdx.x;
   const int lane = t & 63, wave = t >> 6;
   const int h = lane >> 5, c = lane & 31;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = NWV == 8 ? wave >> 2 : wave >> 1, wn = NWV == 8 ? wave & 3 : wave & 1;
   const int nkt = K / 32, nks = K / 16;
 
   const int nwg = gridDim.x;
@@ -964,7 +986,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_wsr_b16_kernel(const GemmArgs args
   auto issue = [&](int f) {
     const int slot = f % WSR16_NS;
     const GemmSrc& S = args.s[args.g[dg].src_begin];
-    stage_tile_b16(ring + slot * DTILE, S.a, 0, drt * BM, args.g[dg].M, dk * 32, K, wave, lane);
+    stage_tile_b16_nw<NWV>(ring + slot * DTILE, S.a, 0, drt * BM, args.g[dg].M, dk * 32, K, wave, lane);
     if (++dk == nkt) {
       dk = 0;
       ++di;
@@ -972,20 +994,22 @@ __global__ __launch_bounds__(NT, 2) void gemm_wsr_b16_kernel(const GemmArgs args
       while (dg + 1 < args.ngroups && di >= args.tile_off[dg + 1]) { ++dg; drt = di - args.tile_off[dg]; }
     }
   };
-  // as gemm_wsr_kernel: 2 LDS-DMAs per wave per k-tile, 16 epilogue stores per wave per row tile
+  // as gemm_wsr_kernel: PW LDS-DMAs per wave per k-tile, 16 epilogue stores per wave per row tile
   // (vmcnt counts both, in issue order; the counter holds up to 63)
   auto wait_ahead = [&](int ahead, bool stores_younger) {
-    const int n = 2 * ahead + (stores_younger ? 16 : 0);
+    const int n = PW * ahead + (stores_younger ? 16 : 0);
     switch (n) {
 #define MMF_WC(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
-      MMF_WC(0) MMF_WC(2) MMF_WC(4) MMF_WC(6) MMF_WC(8) MMF_WC(10) MMF_WC(12) MMF_WC(14) MMF_WC(16)
-      MMF_WC(18) MMF_WC(20) MMF_WC(22) MMF_WC(24) MMF_WC(26) MMF_WC(28) MMF_WC(30) MMF_WC(32) MMF_WC(34)
-      MMF_WC(36) MMF_WC(38) MMF_WC(40) MMF_WC(42)
+      MMF_WC(0) MMF_WC(1) MMF_WC(2) MMF_WC(3) MMF_WC(4) MMF_WC(5) MMF_WC(6) MMF_WC(7) MMF_WC(8)
+      MMF_WC(9) MMF_WC(10) MMF_WC(11) MMF_WC(12) MMF_WC(13) MMF_WC(14) MMF_WC(15) MMF_WC(16) MMF_WC(17)
+      MMF_WC(18) MMF_WC(19) MMF_WC(20) MMF_WC(21) MMF_WC(22) MMF_WC(23) MMF_WC(24) MMF_WC(25) MMF_WC(26)
+      MMF_WC(27) MMF_WC(28) MMF_WC(29) MMF_WC(30) MMF_WC(31) MMF_WC(32) MMF_WC(33) MMF_WC(34) MMF_WC(35)
+      MMF_WC(36) MMF_WC(37) MMF_WC(38) MMF_WC(39) MMF_WC(40) MMF_WC(41) MMF_WC(42)
 #undef MMF_WC
       default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     }
   };
-  static_assert(2 * (WSR16_NS - 2) + 16 <= 42, "wait_ahead's table");
+  static_assert(PW * (WSR16_NS - 2) + 16 <= 42, "wait_ahead's table");
 
   int nissued = 0;
   for (; nissued < WSR16_NS - 1 && nissued < nflat; ++nissued) issue(nissued);
@@ -1840,14 +1864,20 @@ bool job_wsr_b16(const GemmJob& J) {
 }
 
 hipError_t launch_wsr_b16(const GemmJob* jobs, int njobs, hipStream_t st) {
-  // every job split into its 128-column groups, adjacent (see the kernel)
+  // 8-wave workgroups over 256-column groups when every job is 256 wide (MMF_WSR16_W4=1: 4 waves
+  // over 128-column groups, A/B)
+  static const bool w4 = getenv("MMF_WSR16_W4") != nullptr;
+  bool w8 = !w4;
+  for (int i = 0; i < njobs && w8; ++i) w8 = jobs[i].g.N % (2 * BN) == 0;
+  const int cw = w8 ? 2 * BN : BN;
+  // every job split into its column groups, adjacent (see the kernel)
   std::vector<GemmJob> parts;
   std::vector<int> first;   // the job's first column group (its X rows counted once)
   for (int i = 0; i < njobs; ++i)
-    for (int c0 = 0; c0 < jobs[i].g.N; c0 += BN) {
+    for (int c0 = 0; c0 < jobs[i].g.N; c0 += cw) {
       first.push_back(c0 == 0);
       GemmJob p = jobs[i];
-      p.g.N = BN;
+      p.g.N = cw;
       p.g.C = reinterpret_cast<float*>(reinterpret_cast<__bf16*>(jobs[i].g.C) + c0);
       if (p.g.bias) p.g.bias = jobs[i].g.bias + c0;
       p.src[0].b.ptr = reinterpret_cast<const float*>(reinterpret_cast<const __bf16*>(jobs[i].src[0].b.ptr) +
@@ -1877,6 +1907,15 @@ hipError_t launch_wsr_b16(const GemmJob* jobs, int njobs, hipStream_t st) {
       ++done;
     }
     args.ngroups = ng;
+    if (w8) {
+      // one 8-wave workgroup per CU, a 12-deep ring (96 KB)
+      const int grid = std::min(items, cu_count());
+      ProfLaunch prof_(st, "gemm_wsr_b16_kernel<12, 8>", fl, by);
+      mmf_launch((gemm_wsr_b16_kernel<12, 8>), dim3(grid), dim3(8 * 64), 0, st, args, items, K);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      continue;
+    }
     const int grid = std::min(items, 2 * cu_count());
     // ring depth: 9 tiles (72 KB: two workgroups per CU), MMF_WSR16_NS=6 the first form (A/B)
     const char* ns = getenv("MMF_WSR16_NS");
