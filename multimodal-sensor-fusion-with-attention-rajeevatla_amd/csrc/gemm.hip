@@ -1480,14 +1480,22 @@ __global__ __launch_bounds__(256) void mask_dropout_rows_kernel(const MaskDropAr
         if (drop) v = keep_from(r, e, thr) ? v * inv_keep : 0.f;
         o[e] = v;
       }
-      *reinterpret_cast<float4*>(J.out + base) = make_float4(o[0], o[1], o[2], o[3]);
-      *reinterpret_cast<float4*>(J.out + base + 4) = make_float4(o[4], o[5], o[6], o[7]);
+      if (J.outb) {
+        bf16x8 pk;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) pk[e] = (__bf16)o[e];
+        *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(J.out) + base) = pk;
+      } else {
+        *reinterpret_cast<float4*>(J.out + base) = make_float4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<float4*>(J.out + base + 4) = make_float4(o[4], o[5], o[6], o[7]);
+      }
     } else {
       for (int e = 0; e < 8 && base + e < n; ++e) {
         const int64_t idx = base + e;
         float v = J.x[idx] * a.mask[(idx / D / L) * M + m];
         if (drop) v = keep_from(r, e, thr) ? v * inv_keep : 0.f;
-        J.out[idx] = v;
+        if (J.outb) reinterpret_cast<__bf16*>(J.out)[idx] = (__bf16)v;
+        else J.out[idx] = v;
       }
     }
   }
@@ -1835,7 +1843,7 @@ bool gemm_b16_ok(const GemmJob& J, int amode, int bmode) {
   const GemmGroup& g = J.g;
   if (g.nbatch > 1 || g.seg_rows > 0) return false;
   if ((g.epi & EPI_PARTIAL) && (g.kchunk % 32 != 0 || g.nsplit < 1)) return false;
-  if (g.part_db && amode != MODE_KR) return false;
+  if ((g.epi & EPI_PARTIAL) && g.part_db && amode != MODE_KR) return false;   // (part_db shares colsum's slot)
   for (int s = 0; s < J.nsrc; ++s) {
     const GemmSrc& x = J.src[s];
     const Operand* ops[2] = {&x.a, &x.b};
@@ -1932,18 +1940,30 @@ hipError_t launch_wsr_b16(const GemmJob* jobs, int njobs, hipStream_t st) {
   return hipSuccess;
 }
 
-hipError_t launch_gemm_b16(const GemmJob* jobs_in, int njobs, hipStream_t st, int amode, int bmode) {
-  if (njobs <= 0) return hipSuccess;
+hipError_t launch_gemm_b16(const GemmJob* jobs_in, int njobs, hipStream_t st, int amode, int bmode, float drop_p,
+                           const RngSnap* rng, uint64_t* rng_advance) {
+  if (njobs <= 0) return rng_advance ? launch_rng_advance(rng_advance, st) : hipSuccess;
   if (amode == MODE_RK && bmode == MODE_RK && !getenv("MMF_NO_WSR16")) {
     bool wsr = true;
     for (int i = 0; i < njobs && wsr; ++i) wsr = job_wsr_b16(jobs_in[i]);
-    if (wsr) return launch_wsr_b16(jobs_in, njobs, st);
+    if (wsr) {
+      const hipError_t e = launch_wsr_b16(jobs_in, njobs, st);
+      return (e == hipSuccess && rng_advance) ? launch_rng_advance(rng_advance, st) : e;
+    }
   }
   const int form = amode == MODE_RK && bmode == MODE_RK ? 1 : amode == MODE_KR && bmode == MODE_KR ? 2
                  : amode == MODE_RK && bmode == MODE_KR ? 3 : 0;
   if (form == 0) return hipErrorInvalidValue;
   for (int i = 0; i < njobs; ++i)
-    if (!gemm_b16_ok(jobs_in[i], amode, bmode) || jobs_in[i].nsrc > GEMM_MAX_SRCS) return hipErrorInvalidValue;
+    if (!gemm_b16_ok(jobs_in[i], amode, bmode) || jobs_in[i].nsrc > GEMM_MAX_SRCS) {
+      const GemmJob& J = jobs_in[i];
+      fprintf(stderr, "mmfusion: launch_gemm_b16 form (%d, %d) refused job %d: M %d N %d nsrc %d K %d lda %d ldb %d "
+                      "a %p b %p epi 0x%x nbatch %d seg_rows %d\n", amode, bmode, i, J.g.M, J.g.N, J.nsrc,
+              J.nsrc ? J.src[0].K : 0, J.nsrc ? J.src[0].a.ld : 0, J.nsrc ? J.src[0].b.ld : 0,
+              J.nsrc ? (const void*)J.src[0].a.ptr : nullptr, J.nsrc ? (const void*)J.src[0].b.ptr : nullptr, J.g.epi,
+              J.g.nbatch, J.g.seg_rows);
+      return hipErrorInvalidValue;
+    }
   // longest contraction first, then clustered by the most-shared operand (launch_gemm's order)
   std::vector<int> order(njobs);
   std::vector<double> work(njobs);
@@ -1987,6 +2007,10 @@ hipError_t launch_gemm_b16(const GemmJob* jobs_in, int njobs, hipStream_t st, in
     memset(&args, 0, sizeof(args));
     args.amode = amode;
     args.bmode = bmode;
+    args.drop_p = drop_p;
+    args.rng = rng;
+    args.rng_advance = rng_advance;   // (the first launch)
+    rng_advance = nullptr;
     int ng = 0, ns = 0, max_blocks = 0;
     while (done < njobs && ng < GEMM_MAX_GROUPS) {
       const GemmJob& J = jobs_in[order[done]];
@@ -2081,7 +2105,7 @@ hipError_t launch_mask_dropout(MaskDropArgs a, hipStream_t st) {
     maxblk = std::max<int64_t>(maxblk, (J.rows * J.D + 7) / 8);
   }
   double by = 0.0;
-  for (int m = 0; m < a.n; ++m) by += 8.0 * a.j[m].rows * a.j[m].D;   // read x, write x'
+  for (int m = 0; m < a.n; ++m) by += (a.j[m].outb ? 6.0 : 8.0) * a.j[m].rows * a.j[m].D;   // read x, write x'
   for (int i = 0; i < a.nkw; ++i) {
     const int64_t nw = (int64_t)a.B * a.heads * a.kw[i].Lq * (a.kw[i].Lk / 32);
     if (a.kw[i].Lk % 32 != 0 || nw >= ((int64_t)1 << 31)) return hipErrorInvalidValue;

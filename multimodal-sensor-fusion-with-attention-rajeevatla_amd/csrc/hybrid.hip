@@ -144,6 +144,23 @@ bool dqk_b16_on(const mmf_hybrid_desc* d) {
   return d->num_pairs > 0;
 }
 
+// The modality projections on bf16 operands ("medium", dqk_b16_on): the input-mask kernel stores
+// X'_m as bf16 (the rounding the fp32-operand GEMM gave its MFMA operands in-kernel) and W_proj is
+// converted with the W_q / W_k copies, so the projection GEMM, its weight gradient (dZ^T X') and
+// dX = dZ W run the LDS-DMA kernel's bf16 forms (RK x RK, KR x KR, RK x KR); the dZ GEMM stores dZ
+// as bf16.  Half the bytes of X' (written once, read twice) and dZ (written once, read twice).
+// The projection bias gradient is then the column sum of the bf16 dZ, as the Q / K ones are of
+// the bf16 dQ / dK.  MMF_NO_PROJ_B16=1: the fp32-operand forms (A/B).
+bool proj_b16_on(const mmf_hybrid_desc* d) {
+  if (!dqk_b16_on(d) || qk_cat_on(d) || getenv("MMF_NO_PROJ_B16")) return false;
+  int n = 0;
+  for (int g = 0; g < d->num_pairs; ++g) n += 2;
+  if (d->num_modalities + n > CVT_MAX) return false;
+  for (int m = 0; m < d->num_modalities; ++m)
+    if (d->in_dim[m] % 8 != 0) return false;
+  return d->hidden % 8 == 0;
+}
+
 // The head (tail or generic) takes mean_L P_m from per-tile column sums written by the
 // projection GEMM's epilogue when every 128-row tile lies inside one sample (pooled plan):
 // L / 128 rows per sample instead of L (C5: the generic head read 400 MB with one
@@ -169,6 +186,7 @@ struct Saved {
   float *pooled, *scores, *weights, *fused, *h1;
   __bf16* Pb[MMF_MAX_MODALITIES];                  // bf16 copies of P_m (qk_gemm_b16)
   __bf16 *Wqb[MMF_MAX_PAIRS], *Wkb[MMF_MAX_PAIRS];  // bf16 copies of W_q / W_k (qk_gemm_b16)
+  __bf16* Wpb[MMF_MAX_MODALITIES];                 // bf16 copies of W_proj (proj_b16_on; Xd is then bf16)
   int32_t ldq[MMF_MAX_PAIRS], ldk[MMF_MAX_PAIRS];   // elements between Q (K) rows: H, or ncat H (qk_cat_on)
   // qk_cat_on: per modality the Q / K block matrix, the stacked W copies (Wqb / Wkb point into
   // them), the stacked biases, the column count; per pair its Q / K column slots
@@ -187,7 +205,11 @@ void layout_saved(const mmf_hybrid_desc* d, Bump& bp, Saved& s) {
   if (cat) qk_cols(d, s.qcol, s.kcol, s.ncat);
   for (int g = 0; g < d->num_pairs; ++g) s.ldq[g] = s.ldk[g] = (int32_t)H;
   s.rng = bp.take<RngSnap>(1);
-  for (int m = 0; m < d->num_modalities; ++m) s.Xd[m] = bp.take<float>(B * Lm(d, m) * d->in_dim[m]);
+  const bool pb16 = proj_b16_on(d);
+  for (int m = 0; m < d->num_modalities; ++m)
+    s.Xd[m] = pb16 ? reinterpret_cast<float*>(bp.take<__bf16>(B * Lm(d, m) * d->in_dim[m]))
+                   : bp.take<float>(B * Lm(d, m) * d->in_dim[m]);
+  for (int m = 0; m < d->num_modalities && pb16; ++m) s.Wpb[m] = bp.take<__bf16>(H * d->in_dim[m]);
   for (int m = 0; m < d->num_modalities; ++m) s.P[m] = bp.take<float>(B * Lm(d, m) * H);
   for (int m = 0; m < d->num_modalities; ++m)
     if (pcol_in_proj(d, m)) s.Pcol[m] = bp.take<float>(B * (Lm(d, m) / 128) * H);
@@ -446,6 +468,8 @@ void plan_wgrads(const mmf_hybrid_desc* d, const float* const* x, const float* m
     const int L = Lm(d, m), D = d->in_dim[m];
     wp.split_hint = hint(B * L);
     plan_wgrad(wp, bw, H, D, B * L, opnd(w.dZ[m], H), opnd(s.Xd[m], D), g->proj[m].w, g->proj[m].b);
+    // (proj_b16_on: dZ and X' are bf16, launch_gemm_b16's KR x KR form)
+    if (proj_b16_on(d) && !wp.size_only) { wp.jobs_b16.push_back(wp.jobs.back()); wp.jobs.pop_back(); }
     wp.split_hint = 0;
   }
 }
@@ -851,6 +875,23 @@ static int hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, 
 
   // (1) per-modality projection: P_m = Drop(ReLU(X'_m W_m^T + b_m)), X'_m = Drop(X_m * mask_m)
   //     (fusion.py:364-374); X' is kept for the weight gradient
+  const bool pb16 = proj_b16_on(d);
+  bool qk_cvt_done = false;
+  if (pb16) {
+    // bf16 copies of W_proj and (the Q/K branch below then skips its own launch) W_q / W_k
+    CvtArgs cv;
+    memset(&cv, 0, sizeof(cv));
+    for (int m = 0; m < M; ++m) {
+      cv.src[cv.count] = W->proj[m].w; cv.dst[cv.count] = s.Wpb[m]; cv.n[cv.count++] = (int64_t)H * d->in_dim[m];
+    }
+    for (int g = 0; g < d->num_pairs; ++g) {
+      if (single_key(d, g) || wide_pair(d, g)) continue;
+      cv.src[cv.count] = W->q[g].w; cv.dst[cv.count] = s.Wqb[g]; cv.n[cv.count++] = (int64_t)H * H;
+      cv.src[cv.count] = W->k[g].w; cv.dst[cv.count] = s.Wkb[g]; cv.n[cv.count++] = (int64_t)H * H;
+    }
+    STAGE_TRY("fwd.qk_cvt", launch_cvt_bf16(cv, st));
+    qk_cvt_done = true;
+  }
   {
     MaskDropArgs ma;
     memset(&ma, 0, sizeof(ma));
@@ -861,6 +902,7 @@ static int hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, 
       const int L = Lm(d, m), D = d->in_dim[m];
       ma.j[m].x = x[m]; ma.j[m].out = s.Xd[m]; ma.j[m].rows = (int64_t)B * L; ma.j[m].D = D; ma.j[m].L = L;
       ma.j[m].site = SITE_IN + m;
+      ma.j[m].outb = pb16 ? 1 : 0;
       GemmJob j = make_job(B * L, H, s.P[m], H,
                            EPI_BIAS | EPI_RELU | (drop ? EPI_DROP : 0) | (s.Pcol[m] ? EPI_COLSUM : 0));
       j.g.bias = W->proj[m].b;
@@ -898,8 +940,14 @@ static int hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, 
     }
     STAGE_TRY("fwd.input_mask", launch_mask_dropout(ma, st));
     fork_keep_words();   // the rng snapshot exists from here on
-    STAGE_TRY("fwd.proj_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, p, rng, st,
-                                           const_cast<uint64_t*>(rng_state)));
+    if (pb16) {
+      for (int m = 0; m < M; ++m) jobs[m].src[0].b.ptr = reinterpret_cast<const float*>(s.Wpb[m]);
+      STAGE_TRY("fwd.proj_gemm", launch_gemm_b16(jobs.data(), (int)jobs.size(), st, MODE_RK, MODE_RK, p, rng,
+                                                 const_cast<uint64_t*>(rng_state)));
+    } else {
+      STAGE_TRY("fwd.proj_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_RK, p, rng, st,
+                                             const_cast<uint64_t*>(rng_state)));
+    }
   }
   // (2) Q/K (and V for the general plan) projections of every present pair (attention.py:104-106)
   if (d->num_pairs && qk_cat_on(d)) {
@@ -955,7 +1003,7 @@ static int hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, 
       add_src(jk, bop(s.Pb[k], H), bop(s.Wkb[g], H), H);
       jobs.push_back(jk);
     }
-    STAGE_TRY("fwd.qk_cvt", launch_cvt_bf16(cv, st));
+    if (!qk_cvt_done) STAGE_TRY("fwd.qk_cvt", launch_cvt_bf16(cv, st));
     STAGE_TRY("fwd.qkv_gemm", launch_gemm_b16(jobs.data(), (int)jobs.size(), st));
   } else if (d->num_pairs) {
     std::vector<GemmJob> jobs;
@@ -1313,7 +1361,8 @@ static int hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W,
     for (int m = 0; m < M; ++m) {
       const int L = Lm(d, m);
       const bool pe = pool && poole_in_dz(d, m);
-      GemmJob j = make_job(B * L, H, w.dZ[m], H, EPI_GATE | (pool && !pe ? EPI_ADDMAT : EPI_ROWADD));
+      GemmJob j = make_job(B * L, H, w.dZ[m], H,
+                           EPI_GATE | (pool && !pe ? EPI_ADDMAT : EPI_ROWADD) | (proj_b16_on(d) ? EPI_BF16 : 0));
       if (pool && !pe) {
         j.g.addm = w.E[m];
         j.g.ld_addm = H;
@@ -1364,6 +1413,7 @@ static int hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W,
   }
   // (5) dX_m = (dZ_m W_m) * mask * input-dropout'
   {
+    const bool pb16 = proj_b16_on(d);
     std::vector<GemmJob> jobs;
     for (int m = 0; m < M; ++m) {
       if (!dx || !dx[m]) continue;
@@ -1371,10 +1421,13 @@ static int hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W,
       GemmJob j = make_job(B * L, D, dx[m], D, EPI_ROWSCALE | (drop ? EPI_DROP : 0));
       j.g.rowscale = mask; j.g.rs_div = L; j.g.rs_stride = M; j.g.rs_off = m;
       j.g.drop_site = SITE_IN + m;
-      add_src(j, opnd(w.dZ[m], H), opnd(W->proj[m].w, D), H);
+      // (proj_b16_on: the bf16 dZ against the forward's W_proj copy, launch_gemm_b16's RK x KR form)
+      add_src(j, opnd(w.dZ[m], H), opnd(pb16 ? reinterpret_cast<const float*>(s.Wpb[m]) : W->proj[m].w, D), H);
       jobs.push_back(j);
     }
-    if (!jobs.empty())
+    if (!jobs.empty() && pb16)
+      STAGE_TRY("bwd.dx_gemm", launch_gemm_b16(jobs.data(), (int)jobs.size(), st, MODE_RK, MODE_KR, p, rng));
+    else if (!jobs.empty())
       STAGE_TRY("bwd.dx_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, p, rng, st));
   }
   // (6) every weight gradient: split-K slabs, then one deterministic reduce

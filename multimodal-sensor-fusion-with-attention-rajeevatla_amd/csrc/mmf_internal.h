@@ -198,10 +198,12 @@ int device_cu_count();   // CUs of the current device (cached)
 // X'_m[r][c] = X_m[r][c] * mask[(r / L_m) * M + m] * (keep(site_m, r*D_m + c) ? 1/(1-p) : 0)
 // (the masked, input-dropped modality features of src/fusion.py:364-373,
 // materialised once for the projection GEMM and its weight gradient).
+// outb: X' stored as bf16 (round to nearest even; `out` holds a __bf16 address): the operand the
+// bf16-operand projection GEMM and its weight gradient read (hybrid.hip proj_b16_on)
 struct MaskDropJob {
   const float* x; float* out;
   int64_t rows; int32_t D, L;
-  uint32_t site; int32_t vec;
+  uint32_t site; int32_t vec, outb;
 };
 struct MaskDropArgs {
   MaskDropJob j[8];
@@ -234,8 +236,10 @@ struct ReduceJob {
 // the output extent % 8 == 0 along KR rows; no batch / segments.  The LDS-DMA kernel's B16 forms
 // (DK = 32): half the operand bytes and LDS reads, no conversion; KR tiles read through
 // ds_read_b64_tr_b16.
-hipError_t launch_gemm_b16(const GemmJob* jobs, int njobs, hipStream_t st, int amode = MODE_RK, int bmode = MODE_RK);
-constexpr int CVT_MAX = 64;
+// drop_p / rng / rng_advance: as launch_gemm (EPI_DROP epilogues, the forward's rng advance).
+hipError_t launch_gemm_b16(const GemmJob* jobs, int njobs, hipStream_t st, int amode = MODE_RK, int bmode = MODE_RK,
+                           float drop_p = 0.f, const RngSnap* rng = nullptr, uint64_t* rng_advance = nullptr);
+constexpr int CVT_MAX = 72;
 struct CvtArgs {
   // dst[i] (bf16, round to nearest even) or, where dst32[i] is set, an fp32 copy into dst32[i]
   const float* src[CVT_MAX]; __bf16* dst[CVT_MAX]; float* dst32[CVT_MAX]; int64_t n[CVT_MAX]; int32_t count;
