@@ -313,26 +313,41 @@ __global__ __launch_bounds__(NT) void grad_sumsq_kernel(int64_t n, const float* 
 // Every thread of the block gets the same norm / coef: one partial per thread, a fixed
 // xor-butterfly per wave, the four wave sums in a fixed order (the same bits in every block).
 static_assert(CLIP_BLOCKS == NT, "one clip partial per thread");
-__device__ __forceinline__ void clip_norm_coef(const float* __restrict__ partial, float gscale, float max_norm,
-                                               double* red, float& norm, float& coef) {
+constexpr int CLIP_PER_THREAD = CLIP_SLOTS / CLIP_BLOCKS;
+// (from the thread's partials already in registers: clip_adamw_kernel issues their loads first)
+__device__ __forceinline__ void clip_norm_coef_vals(const float (&pp)[CLIP_PER_THREAD], float gscale, float max_norm,
+                                                    double* red, float& norm, float& coef) {
   const int t = threadIdx.x;
-  double acc = (double)partial[t];
+  double acc = (double)pp[0];
 #pragma unroll
-  for (int r = 1; r < CLIP_SLOTS / CLIP_BLOCKS; ++r) acc += (double)partial[t + r * CLIP_BLOCKS];
+  for (int r = 1; r < CLIP_PER_THREAD; ++r) acc += (double)pp[r];
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
   if ((t & 63) == 0) red[t >> 6] = acc;
-  __syncthreads();
+  // LDS-only barrier (no vmcnt drain: clip_adamw_kernel's AdamW operand loads stay in flight)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
   const double sum = (red[0] + red[1]) + (red[2] + red[3]);
   norm = (float)(sqrt(sum) * (double)gscale);
   coef = 1.f;
   if (max_norm > 0.f) coef = fminf(1.f, max_norm / (norm + 1e-6f));
 }
+__device__ __forceinline__ void clip_norm_coef(const float* __restrict__ partial, float gscale, float max_norm,
+                                               double* red, float& norm, float& coef) {
+  float pp[CLIP_PER_THREAD];
+#pragma unroll
+  for (int r = 0; r < CLIP_PER_THREAD; ++r) pp[r] = partial[threadIdx.x + r * CLIP_BLOCKS];
+  clip_norm_coef_vals(pp, gscale, max_norm, red, norm, coef);
+}
 
 // One AdamW element update (shared by adamw_kernel and clip_adamw_kernel: the same
-// float operations, so the fused and two-call paths agree bit for bit).
+// float operations, so the fused and two-call paths agree bit for bit).  Contraction off: every
+// product and sum rounds on its own, so the backend's fuse-or-not choice (which depends on the
+// surrounding code, e.g. packed math in one caller) cannot make two callers differ.
 __device__ __forceinline__ void adamw_elem(float& p, float g, float& m, float& v, float gs, float lr, float wd,
                                            float b1, float b2, float eps, float step_size, float bc2s) {
+#pragma clang fp contract(off)
   const float gi = g * gs;
   float pi = p * (1.f - lr * wd);
   const float mi = b1 * m + (1.f - b1) * gi;
@@ -348,12 +363,12 @@ __device__ __forceinline__ void adamw_elem(float& p, float g, float& m, float& v
 __device__ __forceinline__ void adamw_range(int64_t n, float* __restrict__ p, const float* __restrict__ g,
                                             float* __restrict__ m, float* __restrict__ v, bool vec, float gs,
                                             float lr, float wd, float b1, float b2, float eps, float step_size,
-                                            float bc2s) {
+                                            float bc2s, int skip = 0) {
   const int64_t tid = (int64_t)blockIdx.x * NT + threadIdx.x, nth = (int64_t)gridDim.x * NT;
   int64_t done = 0;
   if (vec) {
     const int64_t n4 = n / 4;
-    for (int64_t i = tid; i < n4; i += nth) {
+    for (int64_t i = tid + skip * nth; i < n4; i += nth) {
       float4 pv = reinterpret_cast<float4*>(p)[i];
       const float4 gv = reinterpret_cast<const float4*>(g)[i];
       float4 mv = reinterpret_cast<float4*>(m)[i];
@@ -406,6 +421,63 @@ __global__ __launch_bounds__(NT) void adamw_kernel(int64_t n, float* __restrict_
   adamw_range(n, p, g, m, v, vec != 0, gscale, lr, wd, b1, b2, eps, step_size, bc2s);
 }
 
+// (PF: the thread's first two float4 slots are loaded ahead of the clip reduction and the bias
+// corrections, whose dependent chain -- partials -> double sums -> barrier -> pow -- then runs
+// under the loads' latency; clamped addresses: unconditional loads, guarded stores.  Issue order is
+// vmcnt order, so the partials go first and the reduction waits for them only.)
+template <bool PF>
+__device__ __forceinline__ void clip_adamw_body(int64_t n, float* __restrict__ p, const float* __restrict__ g,
+                                                float* __restrict__ m, float* __restrict__ v, const int64_t* step,
+                                                const float* __restrict__ lr_dev, float b1, float b2, float eps,
+                                                float wd, float gscale, const float* __restrict__ partial,
+                                                float max_norm, float* norm_out, float* coef_out, bool vec) {
+  __shared__ double red[NT / 64];
+  const int64_t tid = (int64_t)blockIdx.x * NT + threadIdx.x, nth = (int64_t)gridDim.x * NT;
+  const int64_t n4 = n / 4;
+  float pp[CLIP_PER_THREAD];
+#pragma unroll
+  for (int r = 0; r < CLIP_PER_THREAD; ++r) pp[r] = partial[threadIdx.x + r * CLIP_BLOCKS];
+  const float lr = lr_dev[0];
+  const double st = (double)(*step);
+  float4 pv[2], gv[2], mv[2], vv[2];
+  if constexpr (PF) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int64_t i = min(tid + s * nth, n4 - 1);
+      pv[s] = reinterpret_cast<const float4*>(p)[i];
+      gv[s] = reinterpret_cast<const float4*>(g)[i];
+      mv[s] = reinterpret_cast<const float4*>(m)[i];
+      vv[s] = reinterpret_cast<const float4*>(v)[i];
+    }
+  }
+  float norm, coef;
+  clip_norm_coef_vals(pp, gscale, max_norm, red, norm, coef);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (norm_out) norm_out[0] = norm;
+    if (coef_out) coef_out[0] = coef;
+  }
+  const float bc1 = (float)(1.0 - pow((double)b1, st));
+  const float bc2s = (float)sqrt(1.0 - pow((double)b2, st));
+  const float step_size = lr / bc1;
+  const float gs = gscale * coef;
+  if constexpr (PF) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int64_t i = tid + s * nth;
+      if (i >= n4) continue;
+      adamw_elem(pv[s].x, gv[s].x, mv[s].x, vv[s].x, gs, lr, wd, b1, b2, eps, step_size, bc2s);
+      adamw_elem(pv[s].y, gv[s].y, mv[s].y, vv[s].y, gs, lr, wd, b1, b2, eps, step_size, bc2s);
+      adamw_elem(pv[s].z, gv[s].z, mv[s].z, vv[s].z, gs, lr, wd, b1, b2, eps, step_size, bc2s);
+      adamw_elem(pv[s].w, gv[s].w, mv[s].w, vv[s].w, gs, lr, wd, b1, b2, eps, step_size, bc2s);
+      reinterpret_cast<float4*>(p)[i] = pv[s];
+      reinterpret_cast<float4*>(m)[i] = mv[s];
+      reinterpret_cast<float4*>(v)[i] = vv[s];
+    }
+  }
+  // the remaining float4 slots (all of them without PF) and the scalar tail
+  adamw_range(n, p, g, m, v, vec, gs, lr, wd, b1, b2, eps, step_size, bc2s, PF ? 2 : 0);
+}
+
 // Clip + AdamW in one launch after grad_sumsq_kernel (which advanced *step): every
 // block re-reduces the CLIP_BLOCKS partials itself (the same bits as clip_coef_kernel),
 // block 0 publishes norm / coef.  Same update as adamw_kernel at step *step.
@@ -416,19 +488,12 @@ __global__ __launch_bounds__(NT) void clip_adamw_kernel(int64_t n, float* __rest
                                                         float eps, float wd, float gscale,
                                                         const float* __restrict__ partial, float max_norm,
                                                         float* norm_out, float* coef_out, int vec) {
-  __shared__ double red[NT / 64];
-  float norm, coef;
-  clip_norm_coef(partial, gscale, max_norm, red, norm, coef);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    if (norm_out) norm_out[0] = norm;
-    if (coef_out) coef_out[0] = coef;
-  }
-  const float lr = lr_dev[0];
-  const double st = (double)(*step);
-  const float bc1 = (float)(1.0 - pow((double)b1, st));
-  const float bc2s = (float)sqrt(1.0 - pow((double)b2, st));
-  const float step_size = lr / bc1;
-  adamw_range(n, p, g, m, v, vec != 0, gscale * coef, lr, wd, b1, b2, eps, step_size, bc2s);
+  if (vec && n >= 4)
+    clip_adamw_body<true>(n, p, g, m, v, step, lr_dev, b1, b2, eps, wd, gscale, partial, max_norm, norm_out,
+                          coef_out, true);
+  else
+    clip_adamw_body<false>(n, p, g, m, v, step, lr_dev, b1, b2, eps, wd, gscale, partial, max_norm, norm_out,
+                           coef_out, vec != 0);
 }
 
 __global__ void rng_advance_kernel(uint64_t* state) {
