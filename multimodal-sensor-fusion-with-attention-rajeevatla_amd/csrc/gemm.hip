@@ -178,7 +178,8 @@ __device__ __forceinline__ void epilogue(const GemmGroup& G, const TileCtx& T, f
   const bool vside = nv == 8 && (j0 % 4) == 0 &&
                      (!(epi & EPI_ROWADD) || ((G.ld_rowadd % 4) == 0 && ((uintptr_t)G.rowadd & 15) == 0)) &&
                      (!(epi & EPI_ADDMAT) || ((G.ld_addm % 4) == 0 && ((uintptr_t)G.addm & 15) == 0)) &&
-                     (!(epi & EPI_GATE) || ((G.ld_gate % 4) == 0 && ((uintptr_t)G.gate & 15) == 0));
+                     (!(epi & EPI_GATE) ||
+                      ((G.ld_gate % ((epi & EPI_GATE_B16) ? 8 : 4)) == 0 && ((uintptr_t)G.gate & 15) == 0));
   float bias[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) bias[e] = (!partial && (epi & EPI_BIAS) && e < nv) ? T.biasb[j0 + e] : 0.f;
@@ -229,7 +230,20 @@ __device__ __forceinline__ void epilogue(const GemmGroup& G, const TileCtx& T, f
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += ad[e];
         }
-        if (epi & EPI_GATE) load8(gt, G.gate + (int64_t)i * G.ld_gate + j0, nv, vside);
+        if ((epi & EPI_GATE) && (epi & EPI_GATE_B16)) {
+          // (the bf16 copy of P: 8 signs in one 16-B load)
+          const __bf16* gb = reinterpret_cast<const __bf16*>(G.gate) + (int64_t)i * G.ld_gate + j0;
+          if (vside) {
+            const bf16x8 q = *reinterpret_cast<const bf16x8*>(gb);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) gt[e] = (float)q[e];
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) gt[e] = e < nv ? (float)gb[e] : 0.f;
+          }
+        } else if (epi & EPI_GATE) {
+          load8(gt, G.gate + (int64_t)i * G.ld_gate + j0, nv, vside);
+        }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           if (e >= nv) break;

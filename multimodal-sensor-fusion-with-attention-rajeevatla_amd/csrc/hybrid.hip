@@ -1374,6 +1374,11 @@ static int hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W,
       }
       j.g.gate = s.P[m];
       j.g.ld_gate = H;
+      // (proj_b16_on: the sign of P_m from its bf16 copy -- half the gate bytes; MMF_NO_GATE_B16=1 A/B)
+      if (proj_b16_on(d) && s.Pb[m] && !getenv("MMF_NO_GATE_B16")) {
+        j.g.gate = reinterpret_cast<const float*>(s.Pb[m]);
+        j.g.epi |= EPI_GATE_B16;
+      }
       j.g.gate_scale = gscale;
       const bool b16 = dqk_b16_on(d);
       if (b16 && qk_cat_on(d)) {

@@ -126,7 +126,8 @@ enum : int32_t {
   EPI_ROWSCALE = 32, EPI_PARTIAL = 64, EPI_BIAS_RS = 128, EPI_ADDMAT = 256,
   EPI_COLSUM = 512,
   EPI_BF16 = 1024,     // store C as bf16 (round to nearest even; C holds __bf16, ldc in elements; nbatch 1)
-  EPI_BF16COPY = 2048  // also store a bf16 copy of the final C to `copy` (same ldc; nbatch 1, not with EPI_BF16)
+  EPI_BF16COPY = 2048,  // also store a bf16 copy of the final C to `copy` (same ldc; nbatch 1, not with EPI_BF16)
+  EPI_GATE_B16 = 4096   // with EPI_GATE: `gate` holds a __bf16 matrix (ld_gate in elements; only its sign is read)
 };
 
 // Epilogue order: v = alpha*acc; +bias[j] (x bias_rs[i*ld+off] with EPI_BIAS_RS);
