@@ -2001,9 +2001,14 @@ hipError_t launch_gemm_b16(const GemmJob* jobs_in, int njobs, hipStream_t st, in
   // column tile already found the A rows in L2: 1.62 -> 1.51 GB read per launch), so it keeps
   // 128 x 128 unless MMF_GEMM_WIDE_DZ=1; MMF_GEMM_NO_WIDE=1: 128 x 128 everywhere (A/B,
   // profiles/r05/c5_gemm_wide/)
+  // Round 5, with dZ on bf16 output and gate: RK x KR calls whose every contraction is >= 1 024
+  // (dZ: K = 10 H at C5) take them too -- dZ 0.96 -> 0.92 ms, while dX (K = H) measured 0.21 -> 0.23
+  // with them and keeps 128 x 128 (profiles/r05/c5_wide_dz_long/)
   static const bool no_wide = getenv("MMF_GEMM_NO_WIDE") != nullptr;
   static const bool wide_dz = getenv("MMF_GEMM_WIDE_DZ") != nullptr;
-  bool wide = !no_wide && (form == 2 || (form == 3 && wide_dz));
+  double kmin = 1e30;
+  for (int i = 0; i < njobs; ++i) kmin = std::min(kmin, work[i]);
+  bool wide = !no_wide && (form == 2 || (form == 3 && (wide_dz || (!any_partial && kmin >= 1024.0))));
   for (int i = 0; i < njobs && wide; ++i) wide = jobs_in[i].g.N % (2 * BN) == 0;
   const int bn = wide ? 2 * BN : BN;
   std::vector<uintptr_t> share(njobs, 0);

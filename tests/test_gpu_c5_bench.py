@@ -30,7 +30,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 EXPECT = ["attn_poolL_fwd_fused_bf16<true", "attn_poolL_bwd_fused_bf16<true, ", "gemm_wsr_b16_kernel",
           "gemm_lds_kernel<1, 1, 32, 3, 1, 2, 1>", "gemm_lds_kernel<0, 1, 32, 3, 1, 3>",
-          "gemm_lds_kernel<0, 0, 32, 3, 1, 1>", "pool_e_mfma_kernel",
+          "gemm_lds_kernel<0, 0, 32, 3, 1, 1>", "gemm_lds_kernel<0, 1, 32, 3, 1, 3, 1>", "pool_e_mfma_kernel",
           "pool_u_mfma_kernel", "pool_dpbar_mfma_kernel", "cvt_bf16_kernel", "attn_keep_words_kernel"]
 
 

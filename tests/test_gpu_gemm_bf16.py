@@ -88,10 +88,11 @@ def test_kr_kr(M, N, K, nsplit, bias):
     _run(M, N, K, True, True, nsplit=nsplit, bias=bias)
 
 
-@pytest.mark.parametrize("M,N,K", [(300, 256, 512), (1024, 256, 2560), (64, 72, 24), (260, 512, 96)])
+@pytest.mark.parametrize("M,N,K", [(300, 256, 512), (1024, 256, 2560), (64, 72, 24), (260, 512, 96),
+                                   (300, 512, 1024)])
 def test_rk_kr(M, N, K):
-    # (N % 256 == 0 takes the 128 x 256 WIDE tiles under MMF_GEMM_WIDE_DZ=1: these cases passed
-    # with them as the default, profiles/r05/c5_gemm_wide/pytest.log)
+    # (N % 256 == 0 with K >= 1024 takes the 128 x 256 WIDE tiles by default -- (1024, 256, 2560),
+    # (300, 512, 1024) -- the others under MMF_GEMM_WIDE_DZ=1: profiles/r05/c5_gemm_wide/pytest.log)
     _run(M, N, K, False, True)
 
 
