@@ -94,6 +94,18 @@ typedef struct mmf_hybrid_desc {
    * MMF_PRECISION_MEDIUM = bf16 MFMA operands with fp32 accumulation (storage,
    * softmax and reductions stay fp32 in every mode). */
   int32_t matmul_precision;
+  /* Buffer contract, checked by every entry point below that takes `saved` / `workspace` before
+   * its first launch (MMF_EINVAL otherwise):
+   *  plan_flags: mmf_hybrid_plan_flags() when the caller sized its buffers -- the fingerprint of
+   *    the MMF_* plan switches in the environment, which select kernels and so the buffer layouts
+   *    (0 when none is set); a call made under different switches is refused rather than laying the
+   *    buffers out differently from how they were sized;
+   *  saved_capacity / workspace_capacity: the bytes the caller allocated for `saved` / `workspace`
+   *    (mmf_hybrid_saved_bytes / mmf_hybrid_workspace_bytes of this descriptor); a layout that
+   *    needs more is refused.  The size queries ignore these three fields. */
+  uint32_t plan_flags;
+  uint64_t saved_capacity;
+  uint64_t workspace_capacity;
 } mmf_hybrid_desc;
 
 typedef struct mmf_hybrid_params {
@@ -120,6 +132,8 @@ typedef struct mmf_hybrid_grads {
 
 size_t mmf_hybrid_saved_bytes(const mmf_hybrid_desc* d);
 size_t mmf_hybrid_workspace_bytes(const mmf_hybrid_desc* d);
+/* The current plan-switch fingerprint (mmf_hybrid_desc.plan_flags). */
+uint32_t mmf_hybrid_plan_flags(void);
 
 /* Forward.  x[m]: (B, L_m, D_m); mask: (B, M) float (fractional values scale
  * features, src/fusion.py:361-373).  Writes logits (B, C), fusion_weights

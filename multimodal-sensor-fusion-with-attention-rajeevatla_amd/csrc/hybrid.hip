@@ -15,12 +15,63 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
+#include <cstring>
+#include <unistd.h>
 
 #include "capi_util.h"
 
 using namespace mmf;
 
 namespace {
+
+// The plan switches read from the environment on every call (A/B and diagnostic knobs: they pick
+// kernels and so the `saved` / `workspace` layouts).  Their fingerprint is what a caller stores in
+// mmf_hybrid_desc.plan_flags when it sizes its buffers; an entry point whose current fingerprint
+// differs refuses to run (MMF_EINVAL) instead of laying its buffers out differently from how the
+// caller sized them (MMF_PSTORE set after HybridTrainStep allocated `saved`
+// overflowed it).  The sum of per-entry FNV-1a hashes of "NAME=VALUE": independent of the order
+// of `environ`, and 0 with none of them set.
+const char* const kPlanKnobs[] = {
+    "MMF_PSTORE", "MMF_NO_LONG_FUSED", "MMF_NO_FUSED_BWD", "MMF_NO_BF16_QK", "MMF_NO_GEMM_B16",
+    "MMF_QK_CAT", "MMF_NO_DQK_B16", "MMF_NO_PROJ_B16", "MMF_NO_PCOL", "MMF_NO_POOLE", "MMF_POOLE_FLAT",
+    "MMF_NO_L1_LEAN", "MMF_WGRAD_SPLIT_CAP", "MMF_NO_SIDE_STREAM", "MMF_SIDE_STREAM", "MMF_KW_SERIAL",
+    "MMF_KW_FUSED", "MMF_NO_KW_FUSED", "MMF_NO_GATE_B16", "MMF_POOL_PER_PAIR", "MMF_TAIL_S"};
+
+uint32_t plan_flags_now() {
+  uint32_t sum = 0;
+  for (char** e = environ; e && *e; ++e) {
+    const char* s = *e;
+    if (std::strncmp(s, "MMF_", 4) != 0) continue;
+    for (const char* k : kPlanKnobs) {
+      const size_t n = std::strlen(k);
+      if (std::strncmp(s, k, n) != 0 || s[n] != '=') continue;
+      uint32_t h = 2166136261u;
+      for (const char* c = s; *c; ++c) h = (h ^ (uint8_t)*c) * 16777619u;
+      sum += h | 1u;   // (never 0 for a set knob)
+      break;
+    }
+  }
+  return sum;
+}
+
+// Before any launch: the plan switches are the ones the caller sized its buffers under, and the
+// layout this call computed fits the capacities the caller declared (need_* = the Bump offsets;
+// ~0 = that buffer is not used by the call).
+int check_buffers(const mmf_hybrid_desc* d, size_t need_saved, size_t need_ws) {
+  const uint32_t now = plan_flags_now();
+  if (d->plan_flags != now)
+    return fail(MMF_EINVAL,
+                "the plan switches (MMF_* environment) changed since this descriptor's buffers were sized "
+                "(plan_flags %08x, now %08x): size the buffers again and set plan_flags = mmf_hybrid_plan_flags()",
+                d->plan_flags, now);
+  if (need_saved != ~size_t(0) && need_saved > d->saved_capacity)
+    return fail(MMF_EINVAL, "saved buffer too small: this call's layout needs %zu bytes, saved_capacity is %llu",
+                need_saved, (unsigned long long)d->saved_capacity);
+  if (need_ws != ~size_t(0) && need_ws > d->workspace_capacity)
+    return fail(MMF_EINVAL, "workspace too small: this call's layout needs %zu bytes, workspace_capacity is %llu",
+                need_ws, (unsigned long long)d->workspace_capacity);
+  return MMF_OK;
+}
 
 inline int Lm(const mmf_hybrid_desc* d, int m) { return d->seq_len[m] > 0 ? d->seq_len[m] : 1; }
 inline bool dropping(const mmf_hybrid_desc* d) { return d->training && d->dropout > 0.f; }
@@ -800,8 +851,8 @@ static int hybrid_forward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, 
   Bump bp(saved);
   Saved s{};
   layout_saved(d, bp, s);
-  // (the caller sized `saved` by mmf_hybrid_saved_bytes: the same layout, precision included)
-  if (bp.off > saved_bytes(d)) return fail(MMF_EINVAL, "internal: saved-buffer layout overflow");
+  // (against the capacity the caller declared, under the plan switches it sized `saved` with)
+  if ((rc = check_buffers(d, bp.off, ~size_t(0)))) return rc;
   // the rng snapshot {seed, offset} is written by the input-mask kernel (which draws from
   // the live state) and the live offset advanced by the projection GEMM's first launch:
   // no launch of its own
@@ -1182,6 +1233,7 @@ static int hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W,
   Ws w;
   layout_ws(d, bw, w);
   if (lean_l1(d, W, x)) {
+    if ((rc = check_buffers(d, bs.off, bw.off))) return rc;
     if (part == 2) return MMF_OK;
     L1Args a;
     L1WgArgs wa;
@@ -1191,7 +1243,7 @@ static int hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W,
   }
   WgradPlan wp;
   plan_wgrads(d, x, mask, dlogits, s, w, G, bw, wp, part);
-  if (bw.off > workspace_bytes(d)) return fail(MMF_EINVAL, "internal: workspace overflow");
+  if ((rc = check_buffers(d, bs.off, bw.off))) return rc;
 
   const bool tail = d->num_pairs && use_tail(d);
   if (part != 2) {
@@ -1455,6 +1507,8 @@ int mmf_hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W, co
   return hybrid_backward(d, W, x, mask, saved, dlogits, workspace, G, dx, stream, false);
 }
 
+uint32_t mmf_hybrid_plan_flags(void) { return plan_flags_now(); }
+
 int mmf_hybrid_lean_l1(const mmf_hybrid_desc* d) {
   if (check_hybrid(d) != MMF_OK) return 0;
   return lean_l1_desc(d) ? 1 : 0;
@@ -1514,10 +1568,10 @@ int mmf_hybrid_train_step_part(int part, const mmf_hybrid_desc* d, const mmf_hyb
     Bump bs(saved);
     Saved s{};
     layout_saved(d, bs, s);
-    if (bs.off > saved_bytes(d)) return fail(MMF_EINVAL, "internal: saved-buffer layout overflow");
     Bump bw(workspace);
     Ws w;
     layout_ws(d, bw, w);
+    if ((rc = check_buffers(d, bs.off, bw.off))) return rc;
     L1Args a;
     L1WgArgs wa;
     fill_l1_bwd(a, wa, d, W, x, mask, s, w, dlogits, G, dx);
@@ -1537,6 +1591,12 @@ int mmf_hybrid_train_step_part(int part, const mmf_hybrid_desc* d, const mmf_hyb
     wa.step_incr = clip_partial ? step_dev : nullptr;
     STAGE_TRY("train.l1", launch_l1_train(a, wa, st));
     return MMF_OK;
+  }
+  {
+    // the whole step's buffers before its first launch (the forward's launches would otherwise
+    // run before the backward's workspace check)
+    MathScope math_(d->matmul_precision);
+    if ((rc = check_buffers(d, saved_bytes(d) - 256, workspace_bytes(d) - 256))) return rc;
   }
   if (part == 2) {
     // the head-done flag of part 1's forward: the same decision, from the same descriptor and

@@ -216,6 +216,7 @@ struct HybridSinkBackward : public Node {
     const int mode = (all_none || (s.fresh && all_view_or_none)) ? 0 : all_view ? 1 : 2;
     at::Tensor dst = mode == 0 ? s.flat : at::zeros({s.nelem}, s.flat.options());
     at::Tensor ws = at::empty({(int64_t)g_api.ws_bytes(&desc)}, mask.options().dtype(at::kByte));
+    desc.workspace_capacity = (uint64_t)ws.numel();   // (saved_capacity and plan_flags: the forward's)
     const float* xp[MMF_MAX_MODALITIES] = {};
     float* dxp[MMF_MAX_MODALITIES] = {};
     for (size_t m = 0; m < nx; ++m) {
@@ -267,7 +268,7 @@ std::vector<at::Tensor> hybrid_sink_forward(const std::shared_ptr<Sink>& sink, u
                                             const at::Tensor& rng_state, const at::Tensor& mask,
                                             const std::vector<at::Tensor>& xs) {
   need_api();
-  const mmf_hybrid_desc& d = *reinterpret_cast<const mmf_hybrid_desc*>(desc_addr);
+  mmf_hybrid_desc d = *reinterpret_cast<const mmf_hybrid_desc*>(desc_addr);   // (a copy: capacities set here)
   Sink& s = *sink;
   const int M = d.num_modalities, P = d.num_pairs;
   if ((int)xs.size() != M || M != s.M || P != s.P || M > MMF_MAX_MODALITIES)
@@ -275,6 +276,7 @@ std::vector<at::Tensor> hybrid_sink_forward(const std::shared_ptr<Sink>& sink, u
   c10::DeviceGuard guard(mask.device());
   const auto f32 = mask.options().dtype(at::kFloat);
   at::Tensor saved = at::empty({(int64_t)g_api.saved_bytes(&d)}, mask.options().dtype(at::kByte));
+  d.saved_capacity = (uint64_t)saved.numel();
   std::vector<at::Tensor> outs;
   outs.reserve(2 + (d.return_attention ? P : 0));
   outs.push_back(at::empty({d.batch, d.num_classes}, f32));

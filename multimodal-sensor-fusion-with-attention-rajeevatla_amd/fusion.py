@@ -185,6 +185,8 @@ class _Plan:
         d.training = int(model.training)
         d.return_attention = int(return_attention)
         d.matmul_precision = _nat.matmul_precision()
+        # the plan switches the step's buffers are sized under (the step sets the capacities)
+        d.plan_flags = _nat.lib().mmf_hybrid_plan_flags()
         self.desc = d
         self.seq = [max(s, 1) for s in seq]
         self.pairs = pairs
@@ -372,7 +374,8 @@ class HybridFusion(nn.Module):
                 # eager through mmf_torch's C++ node: the shape checks and the descriptor once per input
                 # signature; the parameters' gradients written straight into the module's flat gradient
                 # buffer (no per-parameter autograd work), the dropout state advanced in place
-                key = (tuple(map(_SHAPE, feats)), self.training, return_attention, _precision(), self.dropout.p)
+                key = (tuple(map(_SHAPE, feats)), self.training, return_attention, _precision(), self.dropout.p,
+                       _nat.lib().mmf_hybrid_plan_flags())
                 addr = descs.get(key)
                 if addr is None:
                     seq, dims = self._shapes(feats, in_dims)

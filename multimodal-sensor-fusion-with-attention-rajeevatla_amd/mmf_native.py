@@ -45,7 +45,7 @@ LIB_PATH = os.environ.get("MMF_LIB_PATH") or os.path.join(_HERE, "csrc", "libmmf
 EXPORTED_SYMBOLS = (
     "mmf_hybrid_saved_bytes", "mmf_hybrid_workspace_bytes", "mmf_hybrid_forward",
     "mmf_hybrid_backward", "mmf_hybrid_train_sync_bytes", "mmf_hybrid_train_status", "mmf_hybrid_train_step",
-    "mmf_hybrid_train_step_part",
+    "mmf_hybrid_train_step_part", "mmf_hybrid_plan_flags",
     "mmf_adaptive_weights_workspace_bytes", "mmf_adaptive_weights",
     "mmf_adaptive_weights_backward",
     "mmf_cma_saved_bytes", "mmf_cma_workspace_bytes", "mmf_cma_forward", "mmf_cma_backward",
@@ -72,6 +72,10 @@ class HybridDesc(ctypes.Structure):
         ("pair_q", c_int32 * MAX_PAIRS), ("pair_k", c_int32 * MAX_PAIRS),
         ("dropout", c_float), ("training", c_int32), ("return_attention", c_int32),
         ("matmul_precision", c_int32),
+        # the buffer contract (include/mmfusion.h): the plan-switch fingerprint the buffers were
+        # sized under, and their capacities in bytes
+        ("plan_flags", ctypes.c_uint32), ("saved_capacity", ctypes.c_uint64),
+        ("workspace_capacity", ctypes.c_uint64),
     ]
 
 
@@ -122,6 +126,8 @@ def lib() -> ctypes.CDLL:
     L.mmf_hybrid_saved_bytes.restype = sz
     L.mmf_hybrid_workspace_bytes.argtypes = [POINTER(HybridDesc)]
     L.mmf_hybrid_workspace_bytes.restype = sz
+    L.mmf_hybrid_plan_flags.argtypes = []
+    L.mmf_hybrid_plan_flags.restype = ctypes.c_uint32
     L.mmf_hybrid_forward.argtypes = [POINTER(HybridDesc), POINTER(HybridParams), vp, vp, vp, vp,
                                      vp, vp, vp, vp]
     L.mmf_hybrid_forward.restype = c_int32

@@ -79,7 +79,12 @@ def hybrid_idesc(batch: int, hidden: int, heads: int, classes: int, seq: Sequenc
 
 
 def hybrid_desc(idesc: Sequence[int], dropout: float) -> "_nat.HybridDesc":
-    key = (tuple(idesc), float(dropout))
+    """The C-ABI descriptor of an idesc, cached per (idesc, dropout, plan switches): its plan_flags
+    are the MMF_* plan switches in force now (mmf_hybrid_plan_flags), so buffers sized from it match
+    the layout the library computes; the callers set saved_capacity / workspace_capacity to the
+    buffers they pass (include/mmfusion.h's buffer contract)."""
+    flags = int(_nat.lib().mmf_hybrid_plan_flags())
+    key = (tuple(idesc), float(dropout), flags)
     d = _HDESC.get(key)
     if d is not None:
         return d
@@ -95,6 +100,7 @@ def hybrid_desc(idesc: Sequence[int], dropout: float) -> "_nat.HybridDesc":
         d.pair_q[g] = v[9 + 2 * M + g]
         d.pair_k[g] = v[9 + 2 * M + P + g]
     d.dropout, d.training, d.return_attention, d.matmul_precision = float(dropout), training, ret, prec
+    d.plan_flags = flags
     _HDESC[key] = d
     return d
 
@@ -173,6 +179,7 @@ def hybrid_fwd_impl(idesc: Sequence[int], dropout: float, rng_state: Tensor, mas
     B, M, C, mshapes = _hybrid_meta(idesc)
     dev = mask.device
     saved = torch.empty(_nat.lib().mmf_hybrid_saved_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
+    d.saved_capacity = saved.numel()
     logits = torch.empty(B, C, dtype=torch.float32, device=dev)
     fw = torch.empty(B, M, dtype=torch.float32, device=dev)
     maps = [torch.empty(s, dtype=torch.float32, device=dev) for s in mshapes]
@@ -200,6 +207,10 @@ def hybrid_bwd_impl(idesc: Sequence[int], dropout: float, mask: Tensor, xs: Sequ
     M, P = d.num_modalities, d.num_pairs
     dev = mask.device
     ws = torch.empty(_nat.lib().mmf_hybrid_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
+    # (`saved` came from the forward: a plan switch flipped in between changes the layout this call
+    # computes, which the library then finds larger than the forward's buffer, or a different
+    # plan_flags descriptor -- refused, not read with another layout)
+    d.saved_capacity, d.workspace_capacity = saved.numel(), ws.numel()
     if flat is None:
         flat = torch.zeros(nelem, dtype=torch.float32, device=dev)
     gstruct = _grad_struct(flat, offsets, M, P)

@@ -142,6 +142,9 @@ class HybridTrainStep:
         self.clip_ws = torch.empty(L.mmf_grad_clip_workspace_bytes(), dtype=torch.uint8, device=dev)
         self.saved = torch.empty(L.mmf_hybrid_saved_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
         self.ws = torch.empty(L.mmf_hybrid_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
+        # the buffer contract: a step under other plan switches (MMF_*) or a layout beyond these
+        # capacities is refused by the library (RuntimeError) before any launch
+        d.saved_capacity, d.workspace_capacity = self.saved.numel(), self.ws.numel()
         # the one-call step's arrival counts: zero once, every call leaves them zero
         self.sync = torch.zeros(L.mmf_hybrid_train_sync_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
         self.logits = torch.empty(nb, d.num_classes, dtype=torch.float32, device=dev)
@@ -338,6 +341,11 @@ class HybridTrainStep:
             return
         if self.graph is not None:
             self.graph.replay()
+            if self.world > 1:
+                # (overlap=False with several ranks: the graph holds forward + backward only; the
+                # exchange and the update run after the replay, outside it)
+                self.allreduce()
+                self.optimizer_step()
             return
         self._forward_backward(self.fuse_clip)
         self.allreduce()

@@ -45,11 +45,12 @@ def test_struct_layouts_match_header(nat, tmp_path):
 #include <stddef.h>
 #include "{HEADER}"
 int main(void) {{
-  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %d %d\\n", sizeof(mmf_hybrid_desc), sizeof(mmf_hybrid_params),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %d %d %zu %zu %zu\\n", sizeof(mmf_hybrid_desc), sizeof(mmf_hybrid_params),
          sizeof(mmf_hybrid_grads), sizeof(mmf_cma_desc), sizeof(mmf_cma_params),
          offsetof(mmf_hybrid_desc, dropout), offsetof(mmf_hybrid_params, cls2),
          offsetof(mmf_hybrid_desc, matmul_precision), offsetof(mmf_cma_desc, matmul_precision),
-         (int)MMF_PRECISION_MEDIUM, (int)MMF_PRECISION_HIGH);
+         (int)MMF_PRECISION_MEDIUM, (int)MMF_PRECISION_HIGH, offsetof(mmf_hybrid_desc, plan_flags),
+         offsetof(mmf_hybrid_desc, saved_capacity), offsetof(mmf_hybrid_desc, workspace_capacity));
   return 0;
 }}
 """)
@@ -61,7 +62,8 @@ int main(void) {{
           ctypes.sizeof(nat.HybridGrads), ctypes.sizeof(nat.CmaDesc), ctypes.sizeof(nat.CmaParams),
           nat.HybridDesc.dropout.offset, nat.HybridParams.cls2.offset,
           nat.HybridDesc.matmul_precision.offset, nat.CmaDesc.matmul_precision.offset, nat.PRECISION_MEDIUM,
-          nat.PRECISION_HIGH]
+          nat.PRECISION_HIGH, nat.HybridDesc.plan_flags.offset, nat.HybridDesc.saved_capacity.offset,
+          nat.HybridDesc.workspace_capacity.offset]
     assert out == py
 
 
@@ -152,3 +154,77 @@ def test_lean_l1_query(nat):
     assert L.mmf_hybrid_lean_l1(ctypes.byref(d)) == 0
     assert L.mmf_hybrid_lean_l1(ctypes.byref(_desc(nat, matmul_precision=nat.PRECISION_MEDIUM))) == 0
     assert L.mmf_hybrid_lean_l1(ctypes.byref(_desc(nat, num_heads=3))) == 0   # invalid descriptor
+
+
+PLAN_KNOBS = ("MMF_PSTORE", "MMF_NO_LONG_FUSED", "MMF_NO_FUSED_BWD", "MMF_NO_BF16_QK", "MMF_NO_GEMM_B16",
+              "MMF_QK_CAT", "MMF_NO_DQK_B16", "MMF_NO_PROJ_B16", "MMF_NO_PCOL", "MMF_NO_POOLE", "MMF_POOLE_FLAT",
+              "MMF_NO_L1_LEAN", "MMF_WGRAD_SPLIT_CAP", "MMF_NO_SIDE_STREAM", "MMF_SIDE_STREAM", "MMF_KW_SERIAL",
+              "MMF_KW_FUSED", "MMF_NO_KW_FUSED", "MMF_NO_GATE_B16", "MMF_POOL_PER_PAIR", "MMF_TAIL_S")
+
+
+def test_plan_flags_fingerprint_the_plan_switches(nat, monkeypatch):
+    """mmf_hybrid_plan_flags: 0 with no plan switch set, a different value per switch and value,
+    independent of the order the variables were set in; other MMF_* variables do not count."""
+    L = nat.lib()
+    for k in PLAN_KNOBS:
+        monkeypatch.delenv(k, raising=False)
+    assert L.mmf_hybrid_plan_flags() == 0
+    monkeypatch.setenv("MMF_L1_POLL_BOUND", "100")      # (not a layout switch)
+    assert L.mmf_hybrid_plan_flags() == 0
+    monkeypatch.setenv("MMF_PSTORE", "1")
+    a = L.mmf_hybrid_plan_flags()
+    monkeypatch.setenv("MMF_PSTORE", "2")
+    b = L.mmf_hybrid_plan_flags()
+    assert a != 0 and b != 0 and a != b
+    monkeypatch.setenv("MMF_NO_PCOL", "1")
+    ab = L.mmf_hybrid_plan_flags()
+    monkeypatch.delenv("MMF_PSTORE")
+    monkeypatch.setenv("MMF_PSTORE", "2")              # (now after MMF_NO_PCOL in environ)
+    assert L.mmf_hybrid_plan_flags() == ab != b
+    monkeypatch.delenv("MMF_PSTORE")
+    monkeypatch.delenv("MMF_NO_PCOL")
+    assert L.mmf_hybrid_plan_flags() == 0
+
+
+def test_buffer_contract_refused_before_launch(nat, monkeypatch):
+    """The buffer contract (include/mmfusion.h): forward / backward / train step
+    refuse a call whose plan switches differ from the descriptor's plan_flags, or whose layout
+    needs more than the declared saved / workspace capacity -- MMF_EINVAL before any launch (host
+    buffers here: nothing is dereferenced; no GPU needed)."""
+    for k in PLAN_KNOBS:
+        monkeypatch.delenv(k, raising=False)
+    L = nat.lib()
+    d = _desc(nat)
+    d.plan_flags = L.mmf_hybrid_plan_flags()
+    n_saved = L.mmf_hybrid_saved_bytes(ctypes.byref(d))
+    n_ws = L.mmf_hybrid_workspace_bytes(ctypes.byref(d))
+    params, grads = nat.HybridParams(), nat.HybridGrads()
+    buf = (ctypes.c_float * 4096)()
+    host = ctypes.addressof(buf)
+    xs = nat.ptr_array([host] * 3)
+    rng = (ctypes.c_uint64 * 2)()
+
+    def fwd():
+        return L.mmf_hybrid_forward(ctypes.byref(d), ctypes.byref(params), ctypes.cast(xs, ctypes.c_void_p), host,
+                                    ctypes.addressof(rng), host, host, host, None, None)
+
+    def bwd():
+        return L.mmf_hybrid_backward(ctypes.byref(d), ctypes.byref(params), ctypes.cast(xs, ctypes.c_void_p), host,
+                                     host, host, host, ctypes.byref(grads), None, None)
+
+    def step(part=0):
+        return L.mmf_hybrid_train_step_part(part, ctypes.byref(d), ctypes.byref(params),
+                                            ctypes.cast(xs, ctypes.c_void_p), host, host, 0.05, 1.0,
+                                            ctypes.addressof(rng), host, host, None, host, host, host, host,
+                                            ctypes.byref(grads), None, None, None, None, 0, None)
+
+    for call in (fwd, bwd, step, lambda: step(2)):
+        d.saved_capacity, d.workspace_capacity = 0, n_ws          # (no capacity declared)
+        assert call() == 1 and b"saved buffer too small" in L.mmf_last_error()
+        d.saved_capacity, d.workspace_capacity = n_saved, 64
+        if call is not fwd:                                      # (the forward takes no workspace)
+            assert call() == 1 and b"workspace too small" in L.mmf_last_error()
+        d.saved_capacity, d.workspace_capacity = n_saved, n_ws
+        monkeypatch.setenv("MMF_NO_L1_LEAN", "1")                # a plan switch set after sizing
+        assert call() == 1 and b"plan switches" in L.mmf_last_error()
+        monkeypatch.delenv("MMF_NO_L1_LEAN")

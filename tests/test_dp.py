@@ -168,24 +168,32 @@ def _gpu_rank(rank: int, world: int, port: int, out: str, accumulate: int = 1) -
         # the overlapped exchange of step(): part 1 of the train step, the all-reduce of its bucket
         # (pairs, gates, classifier) issued while part 2 (dZ, dX, the projections' weight gradients)
         # runs, then the projections' bucket -- eager and as two captured graphs
-        bucketed = []
-        for graph in (False, True):
+        # overlap=False (one exchange of the whole flat gradient after the backward), eager and
+        # captured: the graph holds forward + backward only, step() exchanges and updates after the
+        # replay (the captured form once skipped both)
+        bucketed, updates = [], []
+        for overlap, graph in ((True, False), (True, True), (False, False), (False, True)):
             st = HybridTrainStep(_model().to(dev), [f.to(dev) for f in lf], lm.to(dev), ll.to(dev),
-                                 process_group=dist.group.WORLD, accumulate=accumulate)
-            assert st.overlap and st.bucket_spans[0][1] == st.grad.numel() and st.bucket_spans[1][0] == 0
+                                 process_group=dist.group.WORLD, accumulate=accumulate, overlap=overlap)
+            assert st.overlap == overlap
+            if overlap:
+                assert st.bucket_spans[0][1] == st.grad.numel() and st.bucket_spans[1][0] == 0
+            flat0 = st.flat.clone()
             if graph:
                 st.capture()
-                assert st.graph2 is not None
+                assert (st.graph2 is not None) == overlap
             st.step()
             torch.cuda.synchronize(dev)
             bucketed.append((st.grad / world).cpu())
+            updates.append((st.flat - flat0).cpu())
+            assert int(st.step_dev.item()) == 1
         if rank == 0:
             full_model = _model().to(dev)
             full = HybridTrainStep(full_model, [f.to(dev) for f in feats], mask.to(dev), labels.to(dev))
             full.forward_backward()
             torch.cuda.synchronize(dev)
             torch.save({"dp": dp, "full": full.grad.cpu(), "names": full.plan.names, "bucketed": bucketed,
-                        "oracle": _oracle_flat_grad(_model(), feats, mask, labels)}, out)
+                        "updates": updates, "oracle": _oracle_flat_grad(_model(), feats, mask, labels)}, out)
     finally:
         dist.destroy_process_group()
 
@@ -197,14 +205,21 @@ def test_dp_two_ranks_gpu_matches_single_process(accumulate):
     optionally as `accumulate` micro-batches summed on the device before the one exchange (the
     reference's gradient_accumulation, config/base.yaml:75), equals one process on the whole batch --
     with one all-reduce after the backward, and with step()'s two buckets overlapped with the
-    backward (eager and captured)."""
+    backward; step() with and without the overlap, eager and captured, applies the same update."""
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "dp_gpu.pt")
         mp.spawn(_gpu_rank, args=(2, _free_port(), out, accumulate), nprocs=2, join=True)
         r = torch.load(out, weights_only=True)
     full, dp, ref = r["full"], r["dp"], r["oracle"]
     assert (dp - full).abs().max() <= 1e-4 * full.abs().max()
-    for b in r["bucketed"]:   # (eager, captured)
+    for b in r["bucketed"]:   # (overlapped, whole-buffer) x (eager, captured)
         assert (b - full).abs().max() <= 1e-4 * full.abs().max()
+    # every variant updated the weights (the first AdamW step moves a weight by ~lr), and the
+    # captured form of each exchange mode applied exactly its eager update
+    ups = r["updates"]
+    for u in ups:
+        assert u.abs().max() > 1e-4
+    assert (ups[1] - ups[0]).abs().max() <= 1e-6    # overlapped: eager vs captured
+    assert (ups[3] - ups[2]).abs().max() <= 1e-6    # one exchange after the backward: eager vs captured
     # and both agree with the oracle at the parity tolerance
     assert (full - ref).abs().max() <= 1e-3 * ref.abs().max()

@@ -1,0 +1,254 @@
+"""C4 -- MHAD video + IMU (BASELINE.json configs[3]) -- against the oracle (VERDICT r05 missing #2).
+
+1. The benchmarked C4 step exactly as bench.py builds it: WORKLOADS["c4"] (M = 2, L = [30, 50] --
+   video frames and IMU steps, so Lq != Lk in both pairs -- D = H = 256, 4 heads of head_dim 64,
+   C = 11), B = 256 (the bench's per-GPU batch; the short sequences keep the CPU oracle at a few
+   seconds), torch.manual_seed(0) weights, train mode with dropout 0.1, one hipGraph replay of
+   train_step.HybridTrainStep.  The library's launch records must name the benchmarked kernel set
+   (the pooled plan's non-lean attention kernels: Lk % 32 != 0) at the precision's instantiations;
+   logits, loss, input and parameter gradients are compared with the oracle under the replayed
+   Philox masks (tests/_philox.py):
+     * "highest": 1e-3 of each tensor's largest element (the ReLU layers' weight / bias gradients
+       with the per-element allowance for pre-activations within rounding of zero,
+       tests/_util.relu_kink_slack, as the C2 headline test);
+     * "medium": the bf16 bounds of tests/test_gpu_bf16.py (logits within 3e-2 of the largest
+       logit, argmax >= 99 %; every gradient ||got - ref|| <= max(3e-2 ||ref||, 4 ||emu - ref||,
+       3e-3 S), emu = the oracle with bf16-rounded matmul operands).
+2. The MHAD chain the reference trains (config/datasets.yaml:4-21 with config/base.yaml's model
+   keys; src/train.py:150-182, 233-291): FrameEncoder (512-d frame features -> 256, attention
+   pooling over 30 frames on csrc/softmax_pool.hip, -> 128) and SequenceEncoder (64-d IMU, 2-layer
+   LSTM over 50 steps on csrc/lstm.hip, -> 128), LayerNorm, HybridFusion (H = 256, 4 heads, C = 11)
+   on the encoders' 2-D outputs, CrossEntropy(label smoothing 0.05) -- forward and backward (eval
+   mode: no dropout) against the oracles chained the same way: oracle/softmax_pool_cpu.frame_encoder,
+   oracle/lstm_cpu.sequence_encoder (float64, explicit BPTT), torch-CPU LayerNorm,
+   oracle/hybrid_cpu.hybrid_forward.  fp32: logits, loss and every parameter / input gradient at
+   1e-3 of the tensor's largest element; "medium": logits 3e-2, argmax equal.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from _philox import mask_provider
+from _util import bf16_matmul_mode, close, close_slack, diff_report, relu_kink_slack
+from test_gpu_bf16 import group_scale, logits_ok, norm_ok
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+# the benchmarked kernel set at C4 (pooled plan; Lk = 30 / 50 are not whole 32-key tiles, so the
+# non-lean pooled attention kernels; head_dim 64), by name prefix
+EXPECT = ["mask_dropout_rows_kernel", "attn_pool_fwd_kernel<64", "attn_pool_bwd_dq_kernel<64",
+          "attn_pool_bwd_dk_kernel<64", "tail_pair_fwd_kernel", "tail_pair_bwd_kernel", "gemm_"]
+NOT_EXPECT = ("attn_fwd_kernel", "attn_bwd_", "wide_", "attn_poolL_", "sk_fwd_kernel", "l1_")
+
+
+@pytest.fixture(scope="module")
+def env(pkg_on_path):
+    if not torch.cuda.is_available():
+        pytest.fail("no ROCm device visible")
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    import bench
+    import fusion
+    import mmf_native
+    import train_step
+    return bench, fusion, mmf_native, train_step
+
+
+@pytest.mark.parametrize("precision", ["highest", "medium"])
+def test_c4_benchmark_step_matches_oracle(env, precision):
+    bench, fusion, nat, train_step = env
+    from oracle.hybrid_cpu import cross_entropy_ls, hybrid_forward
+    w = bench.WORKLOADS["c4"]
+    assert (w["M"], w["L"], w["D"], w["H"], w["heads"], w["C"]) == (2, [30, 50], 256, 256, 4, 11)
+    B = w["B"]
+    prev = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision(precision)
+    try:
+        dev = torch.device("cuda", 0)
+        torch.manual_seed(0)
+        names = [f"m{i}" for i in range(w["M"])]
+        model = fusion.HybridFusion({n: w["D"] for n in names}, hidden_dim=w["H"], num_classes=w["C"],
+                                    num_heads=w["heads"], dropout=0.1).to(dev)
+        feats, mask, labels = bench.make_inputs(w, B, 42, dev)
+        step = train_step.HybridTrainStep(model, feats, mask, labels)
+        nat.profile_begin()
+        step.forward_backward()
+        torch.cuda.synchronize()
+        _, launches = nat.profile_end()
+        ran = sorted({k for _, k, *_ in launches})
+        for k in EXPECT:
+            assert any(r.startswith(k) for r in ran), (k, ran)
+        assert not any(r.startswith(NOT_EXPECT) for r in ran), ran
+        # every MFMA kernel at the precision's instantiation (0 fp32, 1 bf16)
+        want = {"highest": 0, "medium": 1}[precision]
+        mfma = [r for r in ran if r.startswith(("gemm_lds", "gemm_wsr", "attn_pool_"))]
+        assert mfma and all(bench.kernel_precision(r) == want for r in mfma), mfma
+
+        step.capture()
+        seed, offset = (int(v) for v in step.rng.tolist())
+        params_cpu = {n: p.detach().cpu().clone() for n, p in model.named_parameters()}
+        step.graph.replay()                 # one benchmarked step: gradients at the pre-update weights
+        torch.cuda.synchronize()
+        assert int(step.rng[1].item()) == offset + 1
+    finally:
+        torch.set_float32_matmul_precision(prev)
+
+    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    m_cpu = mask.cpu()
+
+    def oracle(bf16, taps=None):
+        params = {k: v.clone().requires_grad_(True) for k, v in params_cpu.items()}
+        xs = {n: f.detach().cpu().clone().requires_grad_(True) for n, f in zip(names, feats)}
+
+        def run():
+            logits, _ = hybrid_forward(params, names, xs, m_cpu, w["heads"], p=0.1, train=True,
+                                       gen=mask_provider(seed, offset, 0.1), taps=taps)
+            loss = cross_entropy_ls(logits, labels.cpu())
+            loss.backward()
+            return logits.detach(), loss.detach()
+        if bf16:
+            with bf16_matmul_mode():
+                lg, ls = run()
+        else:
+            lg, ls = run()
+        return lg, ls, params, xs
+
+    grads = dict(step.named_grads())
+    if precision == "highest":
+        taps = {}
+        logits, loss, params, xs = oracle(False, taps)
+        slack = {}
+        for m in names + ["cls"]:
+            wname = f"projections.{m}.0.weight" if m != "cls" else "classifier.0.weight"
+            sw, sb = relu_kink_slack(taps, m, params[wname])
+            slack[wname], slack[wname[:-len("weight")] + "bias"] = sw, sb
+        assert close(step.logits.cpu(), logits, 1e-3, 1e-6 * float(logits.abs().max()))
+        assert abs(float(step.loss.item()) - float(loss)) <= 1e-5 * max(1.0, abs(float(loss)))
+        scale = max([float(p.grad.abs().max()) for p in params.values()] +
+                    [float(x.grad.abs().max()) for x in xs.values()])
+        for i, n in enumerate(names):
+            assert close(step.dx[i].cpu(), xs[n].grad, 1e-3, 1e-5 * scale), \
+                f"dx/{n}: " + diff_report(step.dx[i].cpu(), xs[n].grad, 1e-3, 1e-5 * scale)
+        for n, p in params.items():
+            g = grads[n].cpu()
+            if n in slack:
+                assert close_slack(g, p.grad, 1e-3, 1e-5 * scale, slack[n]), \
+                    f"{n}: " + diff_report(g, p.grad, 1e-3, 1e-5 * scale)
+            else:
+                assert close(g, p.grad, 1e-3, 1e-5 * scale), f"{n}: " + diff_report(g, p.grad, 1e-3, 1e-5 * scale)
+        return
+
+    ref, rloss, rp, rx = oracle(False)
+    _, _, ep, ex = oracle(True)
+    ok, e = logits_ok(step.logits.cpu(), ref)
+    assert ok, e
+    assert abs(float(step.loss.item()) - float(rloss)) <= 3e-2 * max(1.0, abs(float(rloss)))
+    zero = lambda t, like: t if t is not None else torch.zeros_like(like)   # noqa: E731
+    S = group_scale([x.grad for x in rx.values()] + [p.grad for p in rp.values() if p.grad is not None])
+    for i, n in enumerate(names):
+        ok, e = norm_ok(step.dx[i].cpu(), rx[n].grad, ex[n].grad, S)
+        assert ok, (n, e)
+    for n, g in grads.items():
+        ok, e = norm_ok(g.cpu(), zero(rp[n].grad, params_cpu[n]), zero(ep[n].grad, params_cpu[n]), S)
+        assert ok, (n, e)
+
+
+# ----------------------------------------------------------------------------- the MHAD chain
+MHAD_CONFIG = {   # config/datasets.yaml:4-21 (mhad) over config/base.yaml's model keys
+    "dataset": {"modalities": ["video", "imu"], "num_classes": 11},
+    "model": {"fusion_type": "hybrid", "hidden_dim": 256, "output_dim": 128, "num_heads": 4, "dropout": 0.1,
+              "layer_norm": True,
+              "encoders": {"video": {"type": "frame", "input_dim": 512, "temporal_pooling": "attention"},
+                           "imu": {"type": "sequence", "input_dim": 64, "encoder_type": "lstm", "num_layers": 2}}},
+}
+T_VIDEO, T_IMU, B_CHAIN = 30, 50, 8   # 1 s of video at 30 fps and of IMU at 50 Hz
+
+
+def _layer_norm(x, sd, prefix):
+    return F.layer_norm(x, (x.shape[-1],), sd[prefix + ".weight"], sd[prefix + ".bias"], 1e-5)
+
+
+@pytest.mark.parametrize("precision", ["highest", "medium"])
+def test_mhad_chain_matches_oracles(env, precision):
+    _, _, nat, _ = env
+    import harness
+    from oracle.hybrid_cpu import cross_entropy_ls, hybrid_forward
+    from oracle.lstm_cpu import sequence_encoder
+    from oracle.softmax_pool_cpu import frame_encoder
+    torch.manual_seed(0)
+    model = harness.MultimodalFusionModel.from_config(MHAD_CONFIG)
+    sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    model = model.cuda().eval()
+    g = torch.Generator().manual_seed(7)
+    video = torch.randn(B_CHAIN, T_VIDEO, 512, generator=g)
+    imu = torch.randn(B_CHAIN, T_IMU, 64, generator=g)
+    mask = torch.ones(B_CHAIN, 2)
+    mask[2, 0] = 0.0        # a sample without video
+    mask[5, 1] = 0.0        # ... and one without IMU
+    labels = torch.randint(0, 11, (B_CHAIN,), generator=g)
+
+    prev = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision(precision)
+    try:
+        xv, xi = video.cuda().requires_grad_(True), imu.cuda().requires_grad_(True)
+        nat.profile_begin()
+        logits = model({"video": xv, "imu": xi}, mask.cuda())
+        loss = F.cross_entropy(logits, labels.cuda(), label_smoothing=0.05)
+        loss.backward()
+        torch.cuda.synchronize()
+        _, launches = nat.profile_end()
+    finally:
+        torch.set_float32_matmul_precision(prev)
+    ran = {k.split("<")[0] for _, k, *_ in launches}
+    for k in ("attn_pool_frames_fwd", "attn_pool_frames_bwd", "lstm_fwd_kernel", "lstm_bwd_kernel"):
+        assert k in ran, (k, sorted(ran))
+
+    # --- the oracle chain on the CPU, same weights and inputs
+    enc_v_params = {k[len("encoders.video."):]: v.clone().requires_grad_(True) for k, v in sd.items()
+                    if k.startswith("encoders.video.")}
+    fus = {k[len("fusion_model."):]: v.clone().requires_grad_(True) for k, v in sd.items()
+           if k.startswith("fusion_model.")}
+    ln = {k: v.clone().requires_grad_(True) for k, v in sd.items() if k.startswith("layer_norms.")}
+    vin = video.clone().requires_grad_(True)
+    enc_v = frame_encoder(enc_v_params, vin)
+    imu_np = {k[len("encoders.imu."):]: v.double().numpy() for k, v in sd.items() if k.startswith("encoders.imu.")}
+    enc_i_np, _, _, _ = sequence_encoder(imu_np, 2, imu.double().numpy(), None, np.zeros((B_CHAIN, 128)))
+    enc_i = torch.from_numpy(enc_i_np).float().requires_grad_(True)
+    feats = {"video": _layer_norm(enc_v, ln, "layer_norms.video"), "imu": _layer_norm(enc_i, ln, "layer_norms.imu")}
+    ref_logits, _ = hybrid_forward(fus, ["video", "imu"], feats, mask, 4)
+    ref_loss = cross_entropy_ls(ref_logits, labels)
+    ref_loss.backward()
+    # the LSTM's gradients: its BPTT fed d(encoding) from the chain above
+    _, _, d_imu, imu_grads = sequence_encoder(imu_np, 2, imu.double().numpy(), None, enc_i.grad.double().numpy())
+
+    got = logits.detach().cpu()
+    if precision == "medium":
+        assert float((got - ref_logits.detach()).abs().max()) <= 3e-2 * float(ref_logits.detach().abs().max())
+        assert torch.equal(got.argmax(1), ref_logits.detach().argmax(1))
+        return
+    assert close(got, ref_logits.detach(), 1e-3, 1e-6)
+    assert abs(float(loss) - float(ref_loss)) <= 1e-5 * max(1.0, abs(float(ref_loss)))
+    want = {}
+    want.update({"encoders.video." + k: p.grad for k, p in enc_v_params.items()})
+    want.update({"fusion_model." + k: (p.grad if p.grad is not None else torch.zeros_like(p)) for k, p in fus.items()})
+    want.update({k: p.grad for k, p in ln.items()})
+    want.update({"encoders.imu." + k: torch.from_numpy(v) for k, v in imu_grads.items()})
+    scale = max(float(t.abs().max()) for t in want.values())
+    named = dict(model.named_parameters())
+    assert set(want) == set(named), sorted(set(want) ^ set(named))
+    for n, ref in want.items():
+        gdev = named[n].grad
+        gdev = torch.zeros_like(named[n]) if gdev is None else gdev
+        ref = ref.to(torch.float64)
+        if n.startswith("fusion_model.") and (".query_proj." in n or ".key_proj." in n):
+            assert torch.all(gdev == 0), n          # one key per pair (2-D encoder outputs): exact zeros
+            continue
+        assert close(gdev.cpu(), ref, 1e-3, 1e-5 * scale), f"{n}: " + diff_report(gdev.cpu(), ref, 1e-3, 1e-5 * scale)
+    assert close(xv.grad.cpu(), vin.grad, 1e-3, 1e-6), diff_report(xv.grad.cpu(), vin.grad, 1e-3, 1e-6)
+    assert close(xi.grad.cpu(), torch.from_numpy(d_imu), 1e-3, 1e-6), \
+        diff_report(xi.grad.cpu(), torch.from_numpy(d_imu), 1e-3, 1e-6)

@@ -450,3 +450,43 @@ def test_l1_poll_timeout_surfaces_and_recovers(mods, monkeypatch):
     st.step()
     torch.cuda.synchronize()
     assert math.isfinite(float(st.loss.item())) and int(st.sync.count_nonzero()) == 0
+
+
+@pytest.mark.parametrize("seq", [False, True])
+def test_plan_switch_after_sizing_is_refused(mods, seq, monkeypatch):
+    """The buffer contract: HybridTrainStep sizes `saved` / `workspace` once.
+    A plan switch set afterwards (MMF_PSTORE=1, whose stored probabilities need a larger `saved` --
+    the round-5 illegal-address fault class) makes step() raise RuntimeError before any launch; a
+    shortened declared capacity does too; with the switch gone the step runs and matches a fresh
+    step's gradient bit for bit."""
+    fusion, train_step = mods
+    monkeypatch.delenv("MMF_PSTORE", raising=False)
+    feats, mask, labels = _batch(5)
+    if not seq:
+        feats = [f[:, 0] for f in feats]
+    model = _model(fusion, 0.1).cuda()
+    st = train_step.HybridTrainStep(model, [f.cuda() for f in feats], mask.cuda(), labels.cuda())
+    rng0 = model._rng_state.clone()
+    monkeypatch.setenv("MMF_PSTORE", "1")
+    with pytest.raises(RuntimeError, match="plan switches"):
+        st.step()
+    monkeypatch.delenv("MMF_PSTORE")
+    d = st.plan.desc
+    d.saved_capacity -= 4096
+    with pytest.raises(RuntimeError, match="saved buffer too small"):
+        st.step()
+    d.saved_capacity += 4096
+    cap = d.workspace_capacity
+    d.workspace_capacity = 256
+    with pytest.raises(RuntimeError, match="workspace too small"):
+        st.step()
+    d.workspace_capacity = cap
+    torch.cuda.synchronize()
+    assert torch.equal(model._rng_state, rng0)          # nothing ran
+    st.forward_backward()
+    ref_model = _model(fusion, 0.1).cuda()
+    ref = train_step.HybridTrainStep(ref_model, [f.cuda() for f in feats], mask.cuda(), labels.cuda())
+    ref_model._rng_state.copy_(rng0)
+    ref.forward_backward()
+    torch.cuda.synchronize()
+    assert torch.equal(st.grad, ref.grad)
