@@ -397,7 +397,8 @@ int mmf_gemm_bf16(int32_t M, int32_t N, int32_t K, const void* A, int32_t lda, i
  * norm_type=2) as Lightning applies gradient_clip_val, src/train.py:416-430,
  * config/base.yaml:74 gradient_clip_norm): over the flat gradient scaled by
  * grad_scale, total_norm[0] (may be NULL) = ||grad * grad_scale||_2 and
- * clip_coef[0] = min(1, max_norm / (total_norm + 1e-6)) (1 when max_norm <= 0),
+ * clip_coef[0] = min(1, max_norm / (total_norm + 1e-6)) (1 when max_norm <= 0; 0 when total_norm is not
+ * finite, clipping on or off: a step that gave up waiting (mmf_hybrid_train_status) applies a zero gradient),
  * both device floats; feed clip_coef to mmf_adamw_step_dev.  Deterministic
  * fixed-order reduction.  grad 16-byte aligned. */
 size_t mmf_grad_clip_workspace_bytes(void);

@@ -260,9 +260,17 @@ __device__ __forceinline__ void epilogue(const GemmGroup& G, const TileCtx& T, f
           v[e] = x;
         }
       }
-      if (epi & EPI_COLSUM) {   // the final values back into the image for the column sums
-        *reinterpret_cast<f32x4*>(cs + lr * CS + cg) = f32x4{v[0], v[1], v[2], v[3]};
-        *reinterpret_cast<f32x4*>(cs + lr * CS + cg + 4) = f32x4{v[4], v[5], v[6], v[7]};
+      if (epi & EPI_COLSUM) {
+        // the final values back into the image for the column sums.  ds_write_b128 banks are
+        // (a / 4) mod 32 over groups of 8 consecutive lanes, whose 8-column slices lie 32 B apart:
+        // lanes with bit 2 set store their upper half first, so each store instruction covers
+        // all 32 banks once (the plain lo-then-hi order was 2-way conflicted: 43 % of the
+        // projection GEMM's LDS cycles, profiles/r05/close3/pmc_sq_c2.json)
+        const bool sw = (t & 4) != 0;
+        const f32x4 lo = f32x4{v[0], v[1], v[2], v[3]}, hi = f32x4{v[4], v[5], v[6], v[7]};
+        float* row = cs + lr * CS + cg;
+        *reinterpret_cast<f32x4*>(row + (sw ? 4 : 0)) = sw ? hi : lo;
+        *reinterpret_cast<f32x4*>(row + (sw ? 0 : 4)) = sw ? lo : hi;
       }
       if (epi & EPI_BF16COPY) {   // (never with EPI_PARTIAL / EPI_BF16; nbatch 1)
         __bf16* ob = reinterpret_cast<__bf16*>(G.copy) + (int64_t)i * ldc + j0;

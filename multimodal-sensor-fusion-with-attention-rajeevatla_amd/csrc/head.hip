@@ -309,7 +309,8 @@ __global__ __launch_bounds__(NT) void grad_sumsq_kernel(int64_t n, const float* 
   if (t >= 1 && t < CLIP_SLOTS / CLIP_BLOCKS) partial[blockIdx.x + t * CLIP_BLOCKS] = 0.f;
 }
 
-// total_norm = gscale * sqrt(sum); coef = min(1, max_norm / (total_norm + 1e-6)) (1 when max_norm <= 0).
+// total_norm = gscale * sqrt(sum); coef = min(1, max_norm / (total_norm + 1e-6)) (1 when max_norm <= 0;
+// 0 when total_norm is not finite).
 // Every thread of the block gets the same norm / coef: one partial per thread, a fixed
 // xor-butterfly per wave, the four wave sums in a fixed order (the same bits in every block).
 static_assert(CLIP_BLOCKS == NT, "one clip partial per thread");
@@ -332,6 +333,10 @@ __device__ __forceinline__ void clip_norm_coef_vals(const float (&pp)[CLIP_PER_T
   norm = (float)(sqrt(sum) * (double)gscale);
   coef = 1.f;
   if (max_norm > 0.f) coef = fminf(1.f, max_norm / (norm + 1e-6f));
+  // a non-finite norm applies a zero gradient whether clipping is on or not: it is how a train
+  // step whose bounded wait gave up (l1.hip: one +inf partial) keeps its incomplete gradient out of
+  // the update (with clipping on, torch's max_norm / inf is 0 as well; fminf would keep 1 for NaN)
+  if (!(norm <= 3.402823466e38f)) coef = 0.f;
 }
 __device__ __forceinline__ void clip_norm_coef(const float* __restrict__ partial, float gscale, float max_norm,
                                                double* red, float& norm, float& coef) {

@@ -17,6 +17,7 @@
 #include <torch/extension.h>
 #include <torch/csrc/autograd/function.h>
 #include <torch/csrc/autograd/functions/utils.h>
+#include <torch/csrc/autograd/graph_task.h>
 #include <torch/csrc/autograd/saved_variable.h>
 #include <torch/csrc/autograd/variable.h>
 #include <c10/hip/HIPStream.h>
@@ -148,12 +149,24 @@ struct Sink {
   // the node keeps autograd's semantics for these parameters: every one trainable and none with a
   // tensor hook (register_hook can rewrite a gradient before accumulation: those modules go through
   // the per-parameter path, mmf_ops.HybridEager); post-accumulate hooks the node calls itself.
+  // Nor may anything observe the parameters' AccumulateGrad nodes: hooks on an existing grad
+  // accumulator (DistributedDataParallel's reducer registers its all-reduce there; those never run
+  // when the node writes the gradients itself) send the module to the per-parameter path as well.
   // Conservative: a parameter whose hooks were all removed keeps an empty hook wrapper here, so
   // false sends the caller to the exact Python check (mmf_ops._sink_ok)
   bool ok() const {
     for (const auto& p : params)
       if (!p.requires_grad() || !torch::autograd::impl::hooks(p).empty()) return false;
-    return true;
+    return !accumulator_hooked();
+  }
+  // a hook on some parameter's AccumulateGrad node (the exact Python check cannot see these)
+  bool accumulator_hooked() const {
+    for (const auto& p : params) {
+      const auto acc = torch::autograd::impl::try_get_grad_accumulator(p);
+      if (acc && (!acc->post_hooks().empty() || !acc->pre_hooks().empty() || !acc->tensor_pre_hooks().empty()))
+        return true;
+    }
+    return false;
   }
 
   bool matches(const std::vector<at::Tensor>& ps) const {
@@ -177,6 +190,7 @@ struct HybridSinkBackward : public Node {
   SavedVariable mask_;
   std::vector<SavedVariable> xs_;
   at::Tensor saved_;   // the forward's saved bytes (never an output: no reference cycle)
+  std::vector<uint32_t> versions_;   // the parameters' version counters at the forward
 
   std::string name() const override { return "HybridSinkBackward"; }
 
@@ -202,9 +216,22 @@ struct HybridSinkBackward : public Node {
     Sink& s = *sink;
     const auto& params = s.params;
     const size_t np = params.size();
+    // what autograd checks for a saved tensor: a weight modified in place between the forward and
+    // this backward would otherwise be read silently
+    for (size_t i = 0; i < np; ++i)
+      if (params[i]._version() != versions_[i])
+        throw std::runtime_error(
+            "one of the variables needed for gradient computation has been modified by an inplace operation: "
+            "HybridFusion parameter " + std::to_string(i) + " (shape " + c10::str(params[i].sizes()) + ") is at version " +
+            std::to_string(params[i]._version()) + "; expected version " + std::to_string(versions_[i]) +
+            " instead.");
+    // a graph task that asks for some inputs only (torch.autograd.grad(out, inputs), backward(inputs=...))
+    // must leave every parameter's .grad alone: the parameter gradients go to a scratch buffer
+    const auto* exec_info = torch::autograd::get_current_graph_task_exec_info();
+    const bool partial = exec_info && !exec_info->empty();
     // gradient mode (mmf_ops.HybridSink.backward): 0 write into the sink (every .grad None, or the
     // sink's views after a trainer consumed them); 1 add into the sink (its views hold gradients
-    // still to be applied); 2 someone else's .grad tensors: add into them
+    // still to be applied); 2 someone else's .grad tensors: add into them; 3 discard (partial task)
     bool all_none = true, all_view_or_none = true, all_view = true;
     for (size_t i = 0; i < np; ++i) {
       const at::Tensor& g = params[i].grad();
@@ -213,7 +240,7 @@ struct HybridSinkBackward : public Node {
       if (!v) all_view = false;
       if (g.defined() && !v) all_view_or_none = false;
     }
-    const int mode = (all_none || (s.fresh && all_view_or_none)) ? 0 : all_view ? 1 : 2;
+    const int mode = partial ? 3 : (all_none || (s.fresh && all_view_or_none)) ? 0 : all_view ? 1 : 2;
     at::Tensor dst = mode == 0 ? s.flat : at::zeros({s.nelem}, s.flat.options());
     at::Tensor ws = at::empty({(int64_t)g_api.ws_bytes(&desc)}, mask.options().dtype(at::kByte));
     desc.workspace_capacity = (uint64_t)ws.numel();   // (saved_capacity and plan_flags: the forward's)
@@ -230,6 +257,7 @@ struct HybridSinkBackward : public Node {
     check(g_api.bwd(&desc, s.table(), xp, mask.data_ptr<float>(), saved_.data_ptr(), dl.data_ptr<float>(),
                     ws.data_ptr(), &gt, dxp, stream_of(dl)),
           "HybridFusion backward");
+    if (mode == 3) return out;   // (no parameter gradient, no post-accumulate hook: not accumulated)
     if (mode == 0) {
       for (size_t i = 0; i < np; ++i) {
         at::Tensor p = params[i];
@@ -307,6 +335,8 @@ std::vector<at::Tensor> hybrid_sink_forward(const std::shared_ptr<Sink>& sink, u
     node->xs_.reserve(M);
     for (int m = 0; m < M; ++m) node->xs_.emplace_back(xs[m], false);
     node->saved_ = saved;
+    node->versions_.reserve(s.params.size());
+    for (const auto& p : s.params) node->versions_.push_back(p._version());
     torch::autograd::set_history(outs[0], node);
   }
   return outs;
@@ -359,6 +389,7 @@ PYBIND11_MODULE(mmf_torch, m) {
       .def_readwrite("fresh", &Sink::fresh)
       .def("matches", &Sink::matches)
       .def("ok", &Sink::ok)
+      .def("accumulator_hooked", &Sink::accumulator_hooked)
       .def("consumed", &Sink::consumed);
   m.def("hybrid_sink_forward", &hybrid_sink_forward);
   m.def("cross_entropy", &cross_entropy);

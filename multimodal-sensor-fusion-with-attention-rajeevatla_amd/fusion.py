@@ -51,6 +51,18 @@ from attention import CrossModalAttention, _new_rng_state, _precision  # noqa: E
 
 _SHAPE = torch.Tensor.shape.__get__   # (x.shape as a C-level callable: map() over the inputs)
 
+# Bumped whenever any module registers a Parameter (nn.Module.__setattr__ / register_parameter):
+# HybridFusion's cached operator parameter list (_op_params) is only valid for the Parameter
+# objects it was built from.  One integer compare per forward; training steps register nothing.
+_PARAM_GEN = [0]
+
+
+def _param_registered(module, name, param):
+    _PARAM_GEN[0] += 1
+
+
+torch.nn.modules.module.register_module_parameter_registration_hook(_param_registered)
+
 
 # --------------------------------------------------------------------------
 # Early fusion (plumbing, torch) and Late fusion (torch classifiers + HIP weighting).
@@ -384,7 +396,10 @@ class HybridFusion(nn.Module):
                                               _precision())
                     addr = descs[key] = ctypes.addressof(_ops.hybrid_desc(idesc, float(self.dropout.p)))
                 sink = self._grad_sink(params, len(pairs))
-                if not torch.is_grad_enabled() or sink.ok() or _ops._sink_ok(params):
+                # (the grad sink keeps the parameters outside the graph: not with tensor hooks, frozen
+                # parameters or hooks on their AccumulateGrad nodes -- DistributedDataParallel's
+                # reducer -- which would never run; those take HybridEager below)
+                if not torch.is_grad_enabled() or sink.ok() or (_ops._sink_ok(params) and not sink.accumulator_hooked()):
                     logits, fw, *maps = ext.hybrid_sink_forward(sink, addr, self._rng_state, _nat.f32c(modality_mask),
                                                                 [_nat.f32c(x) for x in feats])
                     return self._finish(logits, fw, maps, pairs, dtype, return_attention)
@@ -422,12 +437,16 @@ class HybridFusion(nn.Module):
     def _op_params(self, device) -> Tuple[List[Tuple[int, int, str]], List[torch.Tensor], List[int], Dict[tuple, int]]:
         """(present pairs, the operator's parameter list, the modalities' input widths, the eager
         path's descriptor cache: input signature -> mmf_hybrid_desc address), cached per set of
-        attention modules (a deleted pair changes it) and dropped by every .to() / .cuda() /
-        .float() (_apply), so the float32-on-one-device check runs once per cache: an eager step
-        then costs no walk over the module tree."""
-        keys = tuple(self.attention_modules.keys())
+        attention modules (a deleted pair changes it) and per parameter registration anywhere
+        (_PARAM_GEN: replacing a Parameter object -- `proj[0].weight = nn.Parameter(...)`,
+        load_state_dict(assign=True), weight tying, parametrizations -- registers one), and dropped
+        by every .to() / .cuda() / .float() (_apply), so the float32-on-one-device check runs once
+        per cache: an eager step then costs no walk over the module tree."""
+        keys = (tuple(self.attention_modules.keys()), _PARAM_GEN[0])
         c = self.__dict__.get("_mmf_op_params")
         if c is None or c[0] != keys:
+            # (a new parameter set: the grad sink holding the old tensors goes with it)
+            self.__dict__.pop("_mmf_grad_sink", None)
             pairs = self.present_pairs()
             named = dict(self.named_parameters())
             params = [named[n] for n in self._param_names(pairs)]

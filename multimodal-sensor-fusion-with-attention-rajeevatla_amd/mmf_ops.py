@@ -365,6 +365,7 @@ class HybridSink(torch.autograd.Function):
         logits, fw, saved, _, maps = hybrid_fwd_impl(idesc, dropout, rng_state, mask, xs, params, rng_inplace=True)
         ctx.set_materialize_grads(False)
         ctx.idesc, ctx.dropout, ctx.owner, ctx.params = idesc, dropout, owner, params
+        ctx.versions = [p._version for p in params]   # (autograd's in-place check for saved tensors)
         ctx.need_dx = [bool(n) for n in ctx.needs_input_grad[7:]]
         ctx.save_for_backward(mask, saved, *xs)
         ctx.mark_non_differentiable(fw, saved, *maps)
@@ -377,6 +378,11 @@ class HybridSink(torch.autograd.Function):
             return (None,) * (7 + nx)
         mask, saved, *xs = ctx.saved_tensors
         params = ctx.params
+        for i, (p, v) in enumerate(zip(params, ctx.versions)):
+            if p._version != v:
+                raise RuntimeError("one of the variables needed for gradient computation has been modified by an "
+                                   f"inplace operation: HybridFusion parameter {i} (shape {tuple(p.shape)}) is at "
+                                   f"version {p._version}; expected version {v} instead.")
         sink = ctx.owner._grad_sink(params)
         grads = [p.grad for p in params]
         if all(g is None for g in grads) or (sink.fresh and all(g is None or g is v for g, v in zip(grads, sink.views))):

@@ -399,16 +399,17 @@ def test_l1_poll_timeout_surfaces_and_recovers(mods, monkeypatch):
     the default bound again, the next call on the same buffers equals a fresh step object's call bit
     for bit (logits, loss, dlogits, weights, every gradient, dX, the dropout stream).  A fused step
     (step(): clip partials from the train step) with the timeout reports an infinite norm and a zero
-    clip coefficient (the update applied a zero gradient)."""
+    clip coefficient (the update applied a zero gradient), with clipping on and off."""
     import mmf_native as nat
     fusion, train_step = mods
     feats, mask, labels = _batch(19)
     feats = [f[:, 0] for f in feats]
 
-    def build():
+    def build(clip=1.0):
         model = _model(fusion, 0.3).cuda()
         model._rng_state.copy_(torch.tensor([0x5EED, 3], dtype=torch.int64))
-        return train_step.HybridTrainStep(model, [f.cuda() for f in feats], mask.cuda(), labels.cuda())
+        return train_step.HybridTrainStep(model, [f.cuda() for f in feats], mask.cuda(), labels.cuda(),
+                                          gradient_clip_norm=clip)
 
     def outs(st):
         return [t.detach().cpu().clone() for t in (st.logits, st.losses, st.dlogits, st.fw, st.grad, *st.dx,
@@ -450,6 +451,19 @@ def test_l1_poll_timeout_surfaces_and_recovers(mods, monkeypatch):
     st.step()
     torch.cuda.synchronize()
     assert math.isfinite(float(st.loss.item())) and int(st.sync.count_nonzero()) == 0
+    # clipping off (gradient_clip_norm = 0): the incomplete gradient still stays out of
+    # the update -- coefficient 0, and the first AdamW step with a zero gradient moves the weights by
+    # the decoupled weight decay alone
+    st0 = build(clip=0.0)
+    flat0 = st0.flat.clone()
+    monkeypatch.setenv("MMF_L1_POLL_BOUND", "0")
+    st0.step()
+    torch.cuda.synchronize()
+    monkeypatch.delenv("MMF_L1_POLL_BOUND")
+    assert math.isinf(float(st0.grad_norm.item())) and float(st0.clip_coef.item()) == 0.0
+    torch.testing.assert_close(st0.flat, flat0 * (1 - 1e-3 * 1e-4), rtol=0, atol=1e-6)   # (a gradient step: ~1e-3)
+    with pytest.raises(RuntimeError, match="gave up waiting"):
+        st0.loss
 
 
 @pytest.mark.parametrize("seq", [False, True])
