@@ -10,7 +10,8 @@ O=gpurun_out/$RUN
 mkdir -p "$O"
 PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider"
 timeout -k 10 600 $PYT tests/test_gpu_c4_bench.py "tests/test_gpu_train_step.py::test_plan_switch_after_sizing_is_refused" \
-    "tests/test_dp.py::test_dp_two_ranks_gpu_matches_single_process" > "$O/pytest_new.log" 2>&1
+    "tests/test_dp.py::test_dp_two_ranks_gpu_matches_single_process" tests/test_gpu_torch_ext.py \
+    "tests/test_gpu_train_step.py::test_l1_poll_timeout_surfaces_and_recovers" > "$O/pytest_new.log" 2>&1
 rc=$?; echo "pytest rc=$rc" >> "$O/pytest_new.log"
 [ $rc -ne 0 ] && { echo "new tests failed rc=$rc"; tail -40 "$O/pytest_new.log"; exit $rc; }
 [ "$2" = "quick" ] && { echo done-quick; exit 0; }
