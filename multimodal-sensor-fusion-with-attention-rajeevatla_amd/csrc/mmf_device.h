@@ -10,6 +10,7 @@ namespace mmf {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));   // (a native 4-vector: one b128 LDS store)
 
 // v_mfma_f32_32x32x2_f32: lane l supplies A[i=l&31][k=l>>5] and B[k=l>>5][j=l&31];
 // the 32x32 result sits in 16 regs: col j = l&31, row i = (r&3) + 8*(r>>2) + 4*(l>>5).

@@ -642,7 +642,10 @@ __global__ __launch_bounds__(NT) void tail_dpbar_mfma_kernel(const TailArgs a) {
         const int i = i0 + u * NT + t;
         if (i < KG_ROWS * H4) {
           const int row = i / H4, c4 = (i - row * H4) * 4;
-          *reinterpret_cast<float4*>(&du_s[row * DS + c4]) = row < R ? vv[u] : make_float4(0.f, 0.f, 0.f, 0.f);
+          // (a native 4-vector store: one ds_write_b128, 8 lanes over 32 consecutive banks; the float4
+          // struct's member-wise copy became two ds_write2_b32, 4-way bank-conflicted)
+          const float4 q = row < R ? vv[u] : make_float4(0.f, 0.f, 0.f, 0.f);
+          reinterpret_cast<f32x4v*>(du_s)[(row * DS + c4) >> 2] = f32x4v{q.x, q.y, q.z, q.w};
         }
       }
     }
@@ -651,7 +654,7 @@ __global__ __launch_bounds__(NT) void tail_dpbar_mfma_kernel(const TailArgs a) {
       const int row = i / H4, c4 = (i - row * H4) * 4;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (row < R) v = ld4(a.p[a.kg_pair[kg][row / nh]].dU + ((int64_t)b * nh + row % nh) * H + c4);
-      *reinterpret_cast<float4*>(&du_s[row * DS + c4]) = v;
+      reinterpret_cast<f32x4v*>(du_s)[(row * DS + c4) >> 2] = f32x4v{v.x, v.y, v.z, v.w};
     }
   }
   if (t < R) rowp[t] = a.p[a.kg_pair[kg][t / nh]].dpbar + ((int64_t)b * nh + t % nh) * Lk;

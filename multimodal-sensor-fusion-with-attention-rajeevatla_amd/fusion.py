@@ -370,6 +370,7 @@ class HybridFusion(nn.Module):
         _nat.require_device(ref, "HybridFusion input")
         # traced (torch.compile, fake tensors): the custom operator; eager: HybridSink / HybridEager
         compiling = not _ops.eager_tensor(ref)
+        hooked = False   # a hook on some parameter's AccumulateGrad node (only the extension can see it)
         if compiling:
             seq, dims = self._shapes(feats)
             for p in self.parameters():
@@ -399,7 +400,12 @@ class HybridFusion(nn.Module):
                 # (the grad sink keeps the parameters outside the graph: not with tensor hooks, frozen
                 # parameters or hooks on their AccumulateGrad nodes -- DistributedDataParallel's
                 # reducer -- which would never run; those take HybridEager below)
-                if not torch.is_grad_enabled() or sink.ok() or (_ops._sink_ok(params) and not sink.accumulator_hooked()):
+                if not torch.is_grad_enabled() or sink.ok():
+                    logits, fw, *maps = ext.hybrid_sink_forward(sink, addr, self._rng_state, _nat.f32c(modality_mask),
+                                                                [_nat.f32c(x) for x in feats])
+                    return self._finish(logits, fw, maps, pairs, dtype, return_attention)
+                hooked = sink.accumulator_hooked()
+                if not hooked and _ops._sink_ok(params):
                     logits, fw, *maps = ext.hybrid_sink_forward(sink, addr, self._rng_state, _nat.f32c(modality_mask),
                                                                 [_nat.f32c(x) for x in feats])
                     return self._finish(logits, fw, maps, pairs, dtype, return_attention)
@@ -413,7 +419,7 @@ class HybridFusion(nn.Module):
             logits, fw, _saved, rng_next, maps = torch.ops.mmfusion.hybrid_fwd(
                 idesc, float(self.dropout.p), self._rng_state, _nat.f32c(modality_mask), xs, params)
             self._rng_state.copy_(rng_next)     # the device Philox stream advanced by one call
-        elif torch.is_grad_enabled() and _ops._sink_ok(params):
+        elif torch.is_grad_enabled() and not hooked and _ops._sink_ok(params):
             # eager without the C++ extension: the Python twin of its node (mmf_ops.HybridSink);
             # params[0] anchors the graph
             logits, fw, _saved, *maps = _ops.HybridSink.apply(
