@@ -22,7 +22,8 @@
 //     tile and comes back transposed (ds_read_b64_tr_b16), Q likewise from its block image.
 // Images: 128-B rows with the 16-B chunk c of row r at c ^ swk(r) (conflict-free row reads
 // of the 32x32x16 operands and 4-row transposed reads); the dS tile: 64-B rows, chunk
-// g at g ^ ((q >> 1) & 3); the dQ partials: [d][q] fp32, 16-B chunk j at j ^ f(d).
+// g at g ^ ((q >> 1) & 3), 8-B halves flipped by q bit 3 (ds_off4); the dQ partials: [d][q] fp32,
+// 16-B chunk j at j ^ f(d).
 // Conditions (attn_long_fused_ok): 128 < Lk <= 512, Lk % 32 == 0, no per-key mask,
 // head_dim <= 64 and % 4, float4-able Q / K rows; dropout through the forward's keep words.
 #include <algorithm>
@@ -59,9 +60,15 @@ __device__ __forceinline__ int swk(int row) { return (((row >> 1) & 1) << 2) | (
 __device__ __forceinline__ int img_off(int row, int c) { return row * 128 + 16 * (c ^ swk(row)); }
 // byte offset of the 4 columns d0 .. d0+3 (d0 % 4 == 0) of row `row`
 __device__ __forceinline__ int img_off4(int row, int d0) { return img_off(row, d0 >> 3) + 2 * (d0 & 7); }
-// the dS tile: 64-B rows (32 keys), 16-B chunk g (keys 8g .. 8g+7) at g ^ ((q >> 1) & 3)
+// the dS tile: 64-B rows (32 keys), 16-B chunk g (keys 8g .. 8g+7) at g ^ ((q >> 1) & 3), and
+// within it the 8-B half of keys key0 .. key0+3 (key0 % 4 == 0) flipped by query bit 3: the
+// register-order stores (ds_write_b64, 16 consecutive lanes = queries q .. q+15 of one 4-key
+// group) then cover 16 distinct 8-B bank pairs (queries q and q + 8 shared one before: the 2-way
+// conflict both one-pass kernels showed, 18.95 M cycles each at C5 "medium",
+// profiles/r05/close3/pmc_sq_c5_medium.json); the transposed reads (8 B per lane, a 4-key group
+// of rows q0 .. q0+3 with q0 % 16 < 4 or in 8 .. 11) stay a bijection onto the 256-B bank row.
 __device__ __forceinline__ int ds_off4(int q, int key0) {
-  return q * 64 + 16 * ((key0 >> 3) ^ ((q >> 1) & 3)) + 2 * (key0 & 7);
+  return q * 64 + 16 * ((key0 >> 3) ^ ((q >> 1) & 3)) + 8 * (((key0 >> 2) & 1) ^ ((q >> 3) & 1));
 }
 // the dQ partials: [d][32 q] fp32, 16-B chunk j (queries 4j .. 4j+3) at j ^ f(d)
 __device__ __forceinline__ int red_off(int d, int j) {
