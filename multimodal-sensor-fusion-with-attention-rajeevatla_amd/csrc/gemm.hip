@@ -505,8 +505,8 @@ struct KCursor { int si, k0, kend; };
 // modality's H; the weight gradients' H x H) a tile covers every column, so its A rows are read
 // once instead of once per 128-column tile (the second read relied on L2 timing: 1.6 x the
 // operand bytes from HBM at C5).
-template <int AMODE, int BMODE, int DK, int NSTAGE, int BF = 0, int B16 = 0, int WIDE = 0>
-__global__ __launch_bounds__(NT, (NSTAGE * (B16 ? DK / 2 : DK) <= 32 ? 4 : 2)) void gemm_lds_kernel(const GemmArgs args) {
+template <int AMODE, int BMODE, int DK, int NSTAGE, int BF, int B16, int WIDE, int CHAIN>
+__device__ __forceinline__ void gemm_lds_body(const GemmArgs& args) {
   static_assert(!B16 || (BF == 1 && DK == 32 && AMODE == (B16 == 2 ? MODE_KR : MODE_RK) &&
                          BMODE == (B16 == 1 ? MODE_RK : MODE_KR)),
                 "bf16-operand form");
@@ -515,10 +515,7 @@ __global__ __launch_bounds__(NT, (NSTAGE * (B16 ? DK / 2 : DK) <= 32 ? 4 : 2)) v
   constexpr int DTILE = B16 ? BM * DK / 2 : BM * DK;   // floats per operand tile
   constexpr int DMA_PER_TILE = B16 ? (1 + NB) * (BM * DK / 2048) : 2 * (BM * DK / 1024);  // glds per wave per stage
   int local;
-  const GemmGroup& G = args.g[group_of_block(args, local)];
-  TileCtx T;
-  if (!tile_ctx(G, local, T, NB * BN)) return;
-  const int64_t offA = (int64_t)T.batch * G.bs_a, offB = (int64_t)T.batch * G.bs_b;
+  int gi = group_of_block(args, local);
 
   // one LDS object: NSTAGE x [A | B (| B)] tiles (also the epilogue image) + 128 floats for the row-sum combine
   constexpr int SSTRIDE = (1 + NB) * DTILE;   // floats per stage
@@ -536,6 +533,16 @@ __global__ __launch_bounds__(NT, (NSTAGE * (B16 ? DK / 2 : DK) <= 32 ? 4 : 2)) v
   const float inv_keep = p < 1.f ? 1.f / (1.f - p) : 0.f;
   if (p > 0.f && args.rng) rs = *args.rng;
   if (args.rng_advance && blockIdx.x == 0 && threadIdx.x == 0) args.rng_advance[1] += 1;   // see launch_gemm
+
+  // The tile of the block's group, then of each group chained to it (GemmGroup::chain: a GEMM
+  // whose A operand is this tile's output rows -- dX_m = dZ_m W_m after dZ_m -- run by the same
+  // workgroup on the same rows once the first tile's stores have landed: no launch of its own and
+  // its A rows from L2, not HBM)
+  for (;;) {
+  const GemmGroup& G = args.g[gi];
+  TileCtx T;
+  if (!tile_ctx(G, local, T, NB * BN)) return;
+  const int64_t offA = (int64_t)T.batch * G.bs_a, offB = (int64_t)T.batch * G.bs_b;
 
   f32x16 acc[2][2 * NB];
 #pragma unroll
@@ -748,6 +755,28 @@ if constexpr (B16) {
   } else {
     epilogue<PR>(G, T, acc, lds, rs, p, inv_keep, wm, wn, h, c);
   }
+  if constexpr (!CHAIN) break;
+  if (!G.chain) break;
+  gi = G.chain - 1;
+  // every wave's stores of this tile complete (vmcnt counts stores), every wave past the epilogue's
+  // reads of the LDS image, and the L1 invalidated (agent-scope acquire) before the chained tile's
+  // DMA reads those rows back
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+}
+
+template <int AMODE, int BMODE, int DK, int NSTAGE, int BF = 0, int B16 = 0, int WIDE = 0>
+__global__ __launch_bounds__(NT, (NSTAGE * (B16 ? DK / 2 : DK) <= 32 ? 4 : 2)) void gemm_lds_kernel(const GemmArgs args) {
+  gemm_lds_body<AMODE, BMODE, DK, NSTAGE, BF, B16, WIDE, 0>(args);
+}
+// The same with chained groups (GemmGroup::chain: dX_m after dZ_m), held to 3 waves per SIMD like
+// the plain kernel (168 VGPRs: the chain's loop-carried state must not cost a wave)
+template <int AMODE, int BMODE, int DK, int NSTAGE, int BF = 0>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3)))
+void gemm_lds_chain_kernel(const GemmArgs args) {
+  gemm_lds_body<AMODE, BMODE, DK, NSTAGE, BF, 0, 0, 1>(args);
 }
 
 // ------------------------------------------------------------------ weight-stationary kernel
@@ -1633,7 +1662,7 @@ hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, 
   {
     bool wsr = njobs > 0;
     for (int i = 0; i < njobs && wsr; ++i)
-      wsr = job_wsr(jobs_in[i], amode, bmode) && jobs_in[i].src[0].K == jobs_in[0].src[0].K;
+      wsr = job_wsr(jobs_in[i], amode, bmode) && jobs_in[i].src[0].K == jobs_in[0].src[0].K && !jobs_in[i].chain;
     if (wsr && getenv("MMF_NO_WSR") == nullptr) return launch_wsr(jobs_in, njobs, st, rng_advance);
   }
   // the tiled launches below take the rng advance on their first launch; a call that
@@ -1662,7 +1691,7 @@ hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, 
     };
     for (int i = 0; i < njobs; ++i) {
       const GemmJob& J = jobs_in[i];
-      if (job_fast(J, amode, bmode) || !job_small_slab(J, amode, bmode)) {
+      if (job_fast(J, amode, bmode) || !job_small_slab(J, amode, bmode) || J.chain) {
         rest.push_back(J);
         continue;
       }
@@ -1682,6 +1711,25 @@ hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, 
     jobs_in = rest.data();
     njobs = (int)rest.size();
   }
+  // Chained jobs (GemmJob::chain) ride in their parent's launch when the shapes allow (the same
+  // rows, one column tile each, the parent's fp32 output as the chained job's RK A operand, both on
+  // the LDS-DMA kernel); any other chained job runs as a launch of its own after this call's.
+  auto chain_ok = [&](const GemmJob& J) {
+    const GemmJob* C = J.chain;
+    if (!C || amode != MODE_RK) return false;
+    const GemmGroup &a = J.g, &b = C->g;
+    if (!job_fast(J, amode, bmode) || !job_fast(*C, amode, bmode)) return false;
+    if ((a.epi & (EPI_PARTIAL | EPI_BF16)) || (b.epi & EPI_PARTIAL) || a.nbatch > 1 || b.nbatch > 1) return false;
+    if (a.N > BN || b.N > BN || b.M != a.M || C->nsrc != 1) return false;
+    const GemmSrc& x = C->src[0];
+    return x.a.ptr == a.C && x.a.ld == a.ldc && x.K == a.N && x.a.row_div == 1 && x.a.seg_stride == 0;
+  };
+  std::vector<GemmJob> later;
+  for (int i = 0; i < njobs; ++i)
+    if (jobs_in[i].chain && !chain_ok(jobs_in[i])) {
+      later.push_back(*jobs_in[i].chain);
+      later.back().chain = nullptr;
+    }
   // The jobs of one call are independent outputs, so they may be launched in
   // any order: longest contraction per tile first (the first-dispatched blocks
   // carry the most work), fast-path jobs packed together.
@@ -1731,28 +1779,50 @@ hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, 
     args.rng_advance = rng_advance;
     rng_advance = nullptr;
     int ng = 0, ns = 0, max_blocks = 0;
+    // chained groups go after the launch's own groups (they own no blocks)
+    int nch = 0, nch_src = 0, ch_parent[GEMM_MAX_GROUPS];
+    const GemmJob* ch_job[GEMM_MAX_GROUPS];
     // one launch = consecutive jobs of the same kernel flavour
     const bool fast = job_fast(jobs_in[order[done]], amode, bmode);
-    while (done < njobs && ng < GEMM_MAX_GROUPS) {
+    while (done < njobs && ng + nch < GEMM_MAX_GROUPS) {
       const GemmJob& J = jobs_in[order[done]];
       if (J.nsrc > GEMM_MAX_SRCS) return hipErrorInvalidValue;
-      if (ns + J.nsrc > GEMM_MAX_SRCS) break;
+      const bool ch = J.chain && chain_ok(J);
+      if (ng + nch + (ch ? 2 : 1) > GEMM_MAX_GROUPS) break;
+      if (ns + nch_src + J.nsrc + (ch ? J.chain->nsrc : 0) > GEMM_MAX_SRCS) break;
       if (job_fast(J, amode, bmode) != fast) break;
       GemmGroup g = J.g;
       if (g.nbatch < 1) g.nbatch = 1;
       g.src_begin = ns;
       g.src_count = J.nsrc;
+      g.chain = 0;
       const bool partial = (g.epi & EPI_PARTIAL) != 0;
       for (int s = 0; s < J.nsrc; ++s) args.s[ns++] = J.src[s];
       const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN) * (partial ? g.nsplit : 1) * g.nbatch;
+      if (ch) {
+        ch_parent[nch] = ng;
+        ch_job[nch++] = J.chain;
+        nch_src += J.chain->nsrc;
+      }
       args.tile_off[ng] = max_blocks;
       args.g[ng++] = g;
       max_blocks += tiles;
       ++done;
     }
     if (ng == 0) return hipErrorInvalidValue;
-    args.ngroups = ng;
-    if (ilv_on && ng > 1) {
+    for (int k = 0; k < nch; ++k) {
+      GemmGroup g = ch_job[k]->g;
+      g.nbatch = 1;
+      g.src_begin = ns;
+      g.src_count = ch_job[k]->nsrc;
+      g.chain = 0;
+      for (int s = 0; s < ch_job[k]->nsrc; ++s) args.s[ns++] = ch_job[k]->src[s];
+      args.tile_off[ng + k] = max_blocks;   // (no block maps to a chained group)
+      args.g[ng + k] = g;
+      args.g[ch_parent[k]].chain = ng + k + 1;
+    }
+    args.ngroups = ng + nch;
+    if (ilv_on && ng > 1 && nch == 0) {
       const int T = args.tile_off[1];
       bool even = T > 0 && T % 8 == 0;
       for (int gi = 1; gi < ng && even; ++gi)
@@ -1762,7 +1832,7 @@ hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, 
     if (max_blocks > 0) {
       dim3 grid(max_blocks, 1);
       double fl = 0.0, by = 0.0;
-      for (int gi = 0; gi < ng; ++gi) {
+      for (int gi = 0; gi < args.ngroups; ++gi) {
         const GemmGroup& g = args.g[gi];
         for (int si = g.src_begin; si < g.src_begin + g.src_count; ++si) {
           fl += 2.0 * g.M * g.N * args.s[si].K * g.nbatch;
@@ -1781,7 +1851,12 @@ hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, 
       static const char* const kGenName[4] = {"gemm_generic_kernel<0, 0>", "gemm_generic_kernel<0, 1>",
                                               "gemm_generic_kernel<1, 0>", "gemm_generic_kernel<1, 1>"};
       const int flavour = (amode == MODE_KR ? 2 : 0) + (bmode == MODE_KR ? 1 : 0);
-      ProfLaunch prof_(st, fast ? kLdsName[flavour + 4 * pr] : kGenName[flavour], fl, by);
+      static const char* const kChainName[6] = {
+          "gemm_lds_chain_kernel<0, 0, 16, 3, 0>", "gemm_lds_chain_kernel<0, 1, 16, 3, 0>",
+          "gemm_lds_chain_kernel<0, 0, 16, 3, 1>", "gemm_lds_chain_kernel<0, 1, 16, 3, 1>",
+          "gemm_lds_chain_kernel<0, 0, 16, 3, 2>", "gemm_lds_chain_kernel<0, 1, 16, 3, 2>"};
+      ProfLaunch prof_(st, nch ? kChainName[(bmode == MODE_KR ? 1 : 0) + 2 * pr]
+                               : fast ? kLdsName[flavour + 4 * pr] : kGenName[flavour], fl, by);
 #define MMF_LAUNCH_CFG2(DKV, NSV, BFV)                                                              \
       if (amode == MODE_RK && bmode == MODE_RK)                                                     \
         mmf_launch((gemm_lds_kernel<MODE_RK, MODE_RK, DKV, NSV, BFV>), grid, dim3(NT), 0, st, args); \
@@ -1803,7 +1878,18 @@ hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, 
         mmf_launch((KERNEL<MODE_KR, MODE_KR>), grid, dim3(NT), 0, st, args);       \
       else                                                                                 \
         mmf_launch((KERNEL<MODE_KR, MODE_RK>), grid, dim3(NT), 0, st, args);
-      if (fast) {
+      if (nch) {
+        // (chain_ok: the LDS-DMA kernel, A row-major)
+        if (bmode == MODE_KR) {
+          if (pr == 2) mmf_launch((gemm_lds_chain_kernel<MODE_RK, MODE_KR, 16, 3, 2>), grid, dim3(NT), 0, st, args);
+          else if (pr == 1) mmf_launch((gemm_lds_chain_kernel<MODE_RK, MODE_KR, 16, 3, 1>), grid, dim3(NT), 0, st, args);
+          else mmf_launch((gemm_lds_chain_kernel<MODE_RK, MODE_KR, 16, 3, 0>), grid, dim3(NT), 0, st, args);
+        } else {
+          if (pr == 2) mmf_launch((gemm_lds_chain_kernel<MODE_RK, MODE_RK, 16, 3, 2>), grid, dim3(NT), 0, st, args);
+          else if (pr == 1) mmf_launch((gemm_lds_chain_kernel<MODE_RK, MODE_RK, 16, 3, 1>), grid, dim3(NT), 0, st, args);
+          else mmf_launch((gemm_lds_chain_kernel<MODE_RK, MODE_RK, 16, 3, 0>), grid, dim3(NT), 0, st, args);
+        }
+      } else if (fast) {
         // (DK, ring depth) = (16, 3): measured best of (16|32) x (2|3|4) at C2
         // (profiles/tune_gemm_cfg.sh)
         MMF_LAUNCH_CFG(MMF_GEMM_DK, MMF_GEMM_NS)
@@ -1819,6 +1905,9 @@ hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, 
       rng_advance = args.rng_advance;   // nothing launched: the next launch (or finish) takes it
     }
   }
+  if (!later.empty())
+    if (hipError_t e = launch_gemm(later.data(), (int)later.size(), amode, bmode, drop_p, rng, st, nullptr))
+      return e;
   return left.finish(hipSuccess);
 }
 

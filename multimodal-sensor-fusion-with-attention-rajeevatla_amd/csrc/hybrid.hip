@@ -1407,6 +1407,24 @@ static int hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W,
     STAGE_TRY("bwd.wgrad_reduce", launch_reduce(wp.reds.data(), (int)wp.reds.size(), st));
     return MMF_OK;
   }
+  // (5) dX_m = (dZ_m W_m) * mask * input-dropout' -- built first: on the fp32-operand forms each
+  // rides in its dZ_m job's launch as a chained GEMM (GemmJob::chain: the workgroup that finishes a
+  // dZ_m row tile computes that tile's dX_m rows next, dZ_m from L2), otherwise a launch of its own
+  std::vector<GemmJob> dxjobs(M);
+  std::vector<bool> has_dx(M, false);
+  const bool pb16 = proj_b16_on(d);
+  for (int m = 0; m < M; ++m) {
+    if (!dx || !dx[m]) continue;
+    const int L = Lm(d, m), D = d->in_dim[m];
+    GemmJob j = make_job(B * L, D, dx[m], D, EPI_ROWSCALE | (drop ? EPI_DROP : 0));
+    j.g.rowscale = mask; j.g.rs_div = L; j.g.rs_stride = M; j.g.rs_off = m;
+    j.g.drop_site = SITE_IN + m;
+    // (proj_b16_on: the bf16 dZ against the forward's W_proj copy, launch_gemm_b16's RK x KR form)
+    add_src(j, opnd(w.dZ[m], H), opnd(pb16 ? reinterpret_cast<const float*>(s.Wpb[m]) : W->proj[m].w, D), H);
+    dxjobs[m] = j;
+    has_dx[m] = true;
+  }
+  const bool chain_dx = !dqk_b16_on(d) && !pb16 && !getenv("MMF_NO_DX_CHAIN");
   // (4) dZ_m = gate(P_m) * [direct + sum_q dQ W_q + sum_k dK W_k (+ dV W_v)]
   {
     std::vector<GemmJob> jobs;
@@ -1463,25 +1481,18 @@ static int hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W,
           }
       }
       if (j.nsrc > GEMM_MAX_SRCS) return fail(MMF_ELIMIT, "too many gradient sources");
+      if (chain_dx && has_dx[m]) j.chain = &dxjobs[m];
       jobs.push_back(j);
     }
+    // (the dX_m of a chained launch take its dropout p: the dZ epilogue has no dropout site)
     if (dqk_b16_on(d)) STAGE_TRY("bwd.dZ_gemm", launch_gemm_b16(jobs.data(), (int)jobs.size(), st, MODE_RK, MODE_KR));
-    else STAGE_TRY("bwd.dZ_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, 0.f, rng, st));
+    else STAGE_TRY("bwd.dZ_gemm", launch_gemm(jobs.data(), (int)jobs.size(), MODE_RK, MODE_KR, chain_dx ? p : 0.f, rng, st));
   }
-  // (5) dX_m = (dZ_m W_m) * mask * input-dropout'
-  {
-    const bool pb16 = proj_b16_on(d);
+  // (5) dX_m, unless chained above
+  if (!chain_dx) {
     std::vector<GemmJob> jobs;
-    for (int m = 0; m < M; ++m) {
-      if (!dx || !dx[m]) continue;
-      const int L = Lm(d, m), D = d->in_dim[m];
-      GemmJob j = make_job(B * L, D, dx[m], D, EPI_ROWSCALE | (drop ? EPI_DROP : 0));
-      j.g.rowscale = mask; j.g.rs_div = L; j.g.rs_stride = M; j.g.rs_off = m;
-      j.g.drop_site = SITE_IN + m;
-      // (proj_b16_on: the bf16 dZ against the forward's W_proj copy, launch_gemm_b16's RK x KR form)
-      add_src(j, opnd(w.dZ[m], H), opnd(pb16 ? reinterpret_cast<const float*>(s.Wpb[m]) : W->proj[m].w, D), H);
-      jobs.push_back(j);
-    }
+    for (int m = 0; m < M; ++m)
+      if (has_dx[m]) jobs.push_back(dxjobs[m]);
     if (!jobs.empty() && pb16)
       STAGE_TRY("bwd.dx_gemm", launch_gemm_b16(jobs.data(), (int)jobs.size(), st, MODE_RK, MODE_KR, p, rng));
     else if (!jobs.empty())

@@ -160,6 +160,11 @@ struct GemmGroup {
   int32_t bs_a, bs_b, bs_c, bs_bias, bs_brs;
   int32_t seg_rows;        // rows per segment for operands with seg_stride (a tile never straddles two)
   void* copy;              // EPI_BF16COPY: __bf16 (M, ldc)
+  // 1 + the index in GemmArgs::g of a group chained to this one (0: none): its A operand is this
+  // group's output, one column tile each, the same rows; the block that finishes a tile of this
+  // group runs the chained group's tile of the same rows next (gemm_lds_kernel, fp32 forms).
+  // Chained groups own no blocks of the grid (tile_off = the grid size).  Set by launch_gemm.
+  int32_t chain;
 };
 
 constexpr int GEMM_MAX_GROUPS = 32;   // kernel arguments ~7.8 KB (measured fine on gfx950)
@@ -183,6 +188,10 @@ struct GemmJob {
   GemmGroup g;
   GemmSrc src[GEMM_MAX_SRCS];
   int nsrc;
+  // optional: a job whose one source's A operand is this job's output C (ld = ldc, K = N), run by the
+  // same workgroups right after this job's tiles (launch_gemm checks the shapes; a pair it cannot
+  // chain runs as a launch of its own after this call's)
+  const GemmJob* chain;
 };
 
 // Launches every job (grouped <= GEMM_MAX_GROUPS per launch).  A launch whose
