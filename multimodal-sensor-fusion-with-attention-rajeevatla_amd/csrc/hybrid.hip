@@ -1407,9 +1407,10 @@ static int hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W,
     STAGE_TRY("bwd.wgrad_reduce", launch_reduce(wp.reds.data(), (int)wp.reds.size(), st));
     return MMF_OK;
   }
-  // (5) dX_m = (dZ_m W_m) * mask * input-dropout' -- built first: on the fp32-operand forms each
-  // rides in its dZ_m job's launch as a chained GEMM (GemmJob::chain: the workgroup that finishes a
-  // dZ_m row tile computes that tile's dX_m rows next, dZ_m from L2), otherwise a launch of its own
+  // (5) dX_m = (dZ_m W_m) * mask * input-dropout' -- built first: with MMF_DX_CHAIN=1 (fp32-operand
+  // forms) each rides in its dZ_m job's launch as a chained GEMM (GemmJob::chain: the workgroup that
+  // finishes a dZ_m row tile computes that tile's dX_m rows next, dZ_m from L2), otherwise a launch
+  // of its own
   std::vector<GemmJob> dxjobs(M);
   std::vector<bool> has_dx(M, false);
   const bool pb16 = proj_b16_on(d);
@@ -1424,7 +1425,11 @@ static int hybrid_backward(const mmf_hybrid_desc* d, const mmf_hybrid_params* W,
     dxjobs[m] = j;
     has_dx[m] = true;
   }
-  const bool chain_dx = !dqk_b16_on(d) && !pb16 && !getenv("MMF_NO_DX_CHAIN");
+  // Opt-in (MMF_DX_CHAIN=1): measured at C2 it saves nothing -- the chained kernel took 192.2 us
+  // for what the two launches take in 191.1 (profiles/r06/dx_chain/): every workgroup still runs
+  // dZ's epilogue, then dX's prologue, main loop and epilogue in lockstep with all the others, so
+  // the chain removes only the launch boundary and dZ's HBM re-read, neither of which bounds it
+  const bool chain_dx = !dqk_b16_on(d) && !pb16 && getenv("MMF_DX_CHAIN");
   // (4) dZ_m = gate(P_m) * [direct + sum_q dQ W_q + sum_k dK W_k (+ dV W_v)]
   {
     std::vector<GemmJob> jobs;

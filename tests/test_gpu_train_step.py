@@ -504,3 +504,30 @@ def test_plan_switch_after_sizing_is_refused(mods, seq, monkeypatch):
     ref.forward_backward()
     torch.cuda.synchronize()
     assert torch.equal(st.grad, ref.grad)
+
+
+@pytest.mark.parametrize("seq", [True])
+def test_dx_chained_into_dz_is_bit_exact(mods, seq, monkeypatch):
+    """MMF_DX_CHAIN=1 (opt-in): dX_m computed by the dZ launch's workgroups right after
+    their dZ_m row tiles (gemm_lds_chain_kernel) -- the same tiles, k order and epilogue as the
+    separate dX launch, so logits, every parameter gradient and dX agree bit for bit."""
+    import mmf_native as nat
+    fusion, train_step = mods
+    feats, mask, labels = _batch(23)
+    runs = []
+    for chain in (False, True):
+        if chain:
+            monkeypatch.setenv("MMF_DX_CHAIN", "1")
+        model = _model(fusion, 0.3).cuda()
+        model._rng_state.copy_(torch.tensor([0x5EED, 9], dtype=torch.int64))
+        st = train_step.HybridTrainStep(model, [f.cuda() for f in feats], mask.cuda(), labels.cuda())
+        nat.profile_begin()
+        st.forward_backward()
+        torch.cuda.synchronize()
+        _, launches = nat.profile_end()
+        names = [k for _, k, *_ in launches]
+        assert any(k.startswith("gemm_lds_chain_kernel") for k in names) == chain, names
+        runs.append([t.detach().cpu().clone() for t in (st.logits, st.grad, *st.dx)])
+        monkeypatch.delenv("MMF_DX_CHAIN", raising=False)
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
