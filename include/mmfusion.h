@@ -134,6 +134,15 @@ size_t mmf_hybrid_saved_bytes(const mmf_hybrid_desc* d);
 size_t mmf_hybrid_workspace_bytes(const mmf_hybrid_desc* d);
 /* The current plan-switch fingerprint (mmf_hybrid_desc.plan_flags). */
 uint32_t mmf_hybrid_plan_flags(void);
+/* Inspection (tests, debuggers): where an activation of the last forward lives in `saved`.
+ * what = MMF_SAVED_PROJ, index = modality m: P_m = dropout(ReLU(X'_m W_m^T + b_m)), fp32
+ * (B, L_m, H) row-major (src/fusion.py:364-374); what = MMF_SAVED_CLS_HIDDEN, index 0: the
+ * classifier's hidden layer after its ReLU and dropout, fp32 (B, H) (src/fusion.py:413-419).
+ * The backward takes ReLU'(z) as (value > 0) from these.  Writes the byte offset from the start
+ * of `saved` and the region's size; MMF_EINVAL for an unknown region or index. */
+enum { MMF_SAVED_PROJ = 0, MMF_SAVED_CLS_HIDDEN = 1 };
+int mmf_hybrid_saved_region(const mmf_hybrid_desc* d, int32_t what, int32_t index, uint64_t* offset,
+                            uint64_t* bytes);
 
 /* Forward.  x[m]: (B, L_m, D_m); mask: (B, M) float (fractional values scale
  * features, src/fusion.py:361-373).  Writes logits (B, C), fusion_weights

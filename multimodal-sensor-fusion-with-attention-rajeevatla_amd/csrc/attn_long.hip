@@ -90,14 +90,42 @@ __device__ __forceinline__ bf16x8 to_bf16x8(float4 a, float4 b) {
 __device__ __forceinline__ f32x16 mfma_bf16(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
+// MMF_LONG_PK=0 (A/B build, Makefile `nopk`): the exp arguments and the pair trees below as
+// scalar v_fma / v_add_f32 in the same association (bit-identical results) instead of
+// v_pk_fma_f32 / v_pk_add_f32
+#ifndef MMF_LONG_PK
+#define MMF_LONG_PK 1
+#endif
 // sum of N (a power of two) packed pairs as a tree
 template <int N>
 __device__ __forceinline__ float tree_sum(f32x2* p) {
+#if MMF_LONG_PK
 #pragma unroll
   for (int n = N / 2; n >= 1; n /= 2)
 #pragma unroll
     for (int i = 0; i < n; ++i) p[i] = p[i] + p[i + n];
   return p[0].x + p[0].y;
+#else
+  float a[N], b[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) { a[i] = p[i].x; b[i] = p[i].y; }
+#pragma unroll
+  for (int n = N / 2; n >= 1; n /= 2)
+#pragma unroll
+    for (int i = 0; i < n; ++i) { a[i] = a[i] + a[i + n]; b[i] = b[i] + b[i + n]; }
+  return a[0] + b[0];
+#endif
+}
+// (x0, x1) = (s0, s1) * c - o, one v_pk_fma_f32 or two v_fma_f32
+__device__ __forceinline__ void exp_args2(float s0, float s1, float c, float o, float& x0, float& x1) {
+#if MMF_LONG_PK
+  const f32x2 x = f32x2{s0, s1} * f32x2{c, c} - f32x2{o, o};
+  x0 = x[0];
+  x1 = x[1];
+#else
+  x0 = __builtin_fmaf(s0, c, -o);
+  x1 = __builtin_fmaf(s1, c, -o);
+#endif
 }
 
 __device__ __forceinline__ f32x16 zero16f() {
@@ -404,8 +432,9 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
         for (int j = 0; j < 4; j += 2) {
           const int e = 4 * g + j;
           // (the exp arguments as packed FMAs: 16 v_pk_fma_f32 for the 32 scores)
-          const f32x2 x = f32x2{s[e], s[e + 1]} * f32x2{sl2, sl2} - f32x2{lse2, lse2};
-          const float p0 = __builtin_amdgcn_exp2f(x[0]), p1 = __builtin_amdgcn_exp2f(x[1]);
+          float x0, x1;
+          exp_args2(s[e], s[e + 1], sl2, lse2, x0, x1);
+          const float p0 = __builtin_amdgcn_exp2f(x0), p1 = __builtin_amdgcn_exp2f(x1);
           pv[i][e] = p0;
           pv[i][e + 1] = p1;
           pk[i][e] = p0 * keep_sel(words[i], j + 8 * g, gv[j]);
@@ -509,6 +538,7 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
     {
       const int d = t & 63, j = t >> 6;   // queries 4j .. 4j+3 of column d
       const float* red = reinterpret_cast<const float*>(lds + OFF_R);
+#if MMF_LONG_PK
       f32x2 a01, a23;   // packed adds
       {
         const float4 v = *reinterpret_cast<const float4*>(red + red_off(d, j));
@@ -522,6 +552,18 @@ __global__ __launch_bounds__(LF_NT, 1) void attn_poolL_bwd_fused_bf16(const Attn
         a23 += f32x2{v.z, v.w};
       }
       const float av[4] = {a01.x, a01.y, a23.x, a23.y};
+#else
+      float av[4];
+      {
+        const float4 v = *reinterpret_cast<const float4*>(red + red_off(d, j));
+        av[0] = v.x; av[1] = v.y; av[2] = v.z; av[3] = v.w;
+      }
+#pragma unroll
+      for (int ww = 1; ww < 8; ++ww) {
+        const float4 v = *reinterpret_cast<const float4*>(red + ww * 2048 + red_off(d, j));
+        av[0] += v.x; av[1] += v.y; av[2] += v.z; av[3] += v.w;
+      }
+#endif
       if (d < hd) {
         // one 64-bit row offset per block, the 4 rows by 32-bit steps (per-element 64-bit
         // products were 24 integer multiplies per block)
@@ -794,9 +836,10 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_poolL_fwd_fused_bf16(const At
       f32x2 pr[8];
 #pragma unroll
       for (int e = 0; e < 16; e += 2) {
-        const f32x2 y = f32x2{x[i][e], x[i][e + 1]} * f32x2{sl2, sl2} - f32x2{mref, mref};   // (v_pk_fma_f32)
-        x[i][e] = __builtin_amdgcn_exp2f(y[0]);
-        x[i][e + 1] = __builtin_amdgcn_exp2f(y[1]);
+        float y0, y1;
+        exp_args2(x[i][e], x[i][e + 1], sl2, mref, y0, y1);   // (v_pk_fma_f32)
+        x[i][e] = __builtin_amdgcn_exp2f(y0);
+        x[i][e + 1] = __builtin_amdgcn_exp2f(y1);
         pr[e >> 1] = f32x2{x[i][e], x[i][e + 1]};
       }
       ls += tree_sum<8>(pr);

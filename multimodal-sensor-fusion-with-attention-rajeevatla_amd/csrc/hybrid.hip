@@ -807,6 +807,37 @@ size_t mmf_hybrid_workspace_bytes(const mmf_hybrid_desc* d) {
   return workspace_bytes(d);
 }
 
+int mmf_hybrid_saved_region(const mmf_hybrid_desc* d, int32_t what, int32_t index, uint64_t* offset,
+                            uint64_t* bytes) {
+  int rc = check_hybrid(d);
+  if (rc) return rc;
+  if (!offset || !bytes) return fail(MMF_EINVAL, "saved region: null argument");
+  MathScope math_(d->matmul_precision);
+  // laid out from a stand-in base (never dereferenced; a null base would give null pointers)
+  char* const base = reinterpret_cast<char*>(uintptr_t(1) << 40);
+  Bump bp(base);
+  Saved s{};
+  layout_saved(d, bp, s);
+  const size_t B = d->batch, H = d->hidden;
+  const float* p = nullptr;
+  size_t n = 0;
+  if (what == MMF_SAVED_PROJ) {
+    if (index < 0 || index >= d->num_modalities)
+      return fail(MMF_EINVAL, "saved region: modality %d of %d", index, d->num_modalities);
+    p = s.P[index];
+    n = B * Lm(d, index) * H;
+  } else if (what == MMF_SAVED_CLS_HIDDEN) {
+    if (index != 0) return fail(MMF_EINVAL, "saved region: the classifier hidden layer has index 0 (got %d)", index);
+    p = s.h1;
+    n = B * H;
+  } else {
+    return fail(MMF_EINVAL, "saved region: unknown region %d", what);
+  }
+  *offset = (uint64_t)(reinterpret_cast<const char*>(p) - base);
+  *bytes = n * sizeof(float);
+  return MMF_OK;
+}
+
 namespace {
 
 // dZ_m takes its value-path term E_m as extra K = heads sources of the dZ GEMM

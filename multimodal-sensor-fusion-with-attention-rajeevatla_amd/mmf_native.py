@@ -45,7 +45,7 @@ LIB_PATH = os.environ.get("MMF_LIB_PATH") or os.path.join(_HERE, "csrc", "libmmf
 EXPORTED_SYMBOLS = (
     "mmf_hybrid_saved_bytes", "mmf_hybrid_workspace_bytes", "mmf_hybrid_forward",
     "mmf_hybrid_backward", "mmf_hybrid_train_sync_bytes", "mmf_hybrid_train_status", "mmf_hybrid_train_step",
-    "mmf_hybrid_train_step_part", "mmf_hybrid_plan_flags",
+    "mmf_hybrid_train_step_part", "mmf_hybrid_plan_flags", "mmf_hybrid_saved_region",
     "mmf_adaptive_weights_workspace_bytes", "mmf_adaptive_weights",
     "mmf_adaptive_weights_backward",
     "mmf_cma_saved_bytes", "mmf_cma_workspace_bytes", "mmf_cma_forward", "mmf_cma_backward",
@@ -128,6 +128,9 @@ def lib() -> ctypes.CDLL:
     L.mmf_hybrid_workspace_bytes.restype = sz
     L.mmf_hybrid_plan_flags.argtypes = []
     L.mmf_hybrid_plan_flags.restype = ctypes.c_uint32
+    L.mmf_hybrid_saved_region.argtypes = [POINTER(HybridDesc), c_int32, c_int32, POINTER(ctypes.c_uint64),
+                                          POINTER(ctypes.c_uint64)]
+    L.mmf_hybrid_saved_region.restype = c_int32
     L.mmf_hybrid_forward.argtypes = [POINTER(HybridDesc), POINTER(HybridParams), vp, vp, vp, vp,
                                      vp, vp, vp, vp]
     L.mmf_hybrid_forward.restype = c_int32

@@ -353,3 +353,21 @@ class HybridTrainStep:
 
     def named_grads(self) -> Dict[str, torch.Tensor]:
         return dict(zip(self.plan.names, self.gviews))
+
+    def saved_activation(self, what: str, index: int = 0) -> torch.Tensor:
+        """A view of an activation the last forward left in ``saved`` (the last micro-batch's):
+        ``what = "proj"``: P_m of modality ``index`` after its ReLU and dropout, (micro, L_m, H)
+        (src/fusion.py:364-374); ``what = "cls_hidden"``: the classifier's hidden layer after its
+        ReLU and dropout, (micro, H) (src/fusion.py:413-419).  The backward takes ReLU'(z) as
+        (value > 0) from these (mmf_hybrid_saved_region)."""
+        kinds = {"proj": 0, "cls_hidden": 1}
+        if what not in kinds:
+            raise ValueError(f"saved_activation: what must be one of {sorted(kinds)} (got {what!r})")
+        d = self.plan.desc
+        off, nb = ctypes.c_uint64(), ctypes.c_uint64()
+        _nat.check(_nat.lib().mmf_hybrid_saved_region(ctypes.byref(d), kinds[what], int(index), ctypes.byref(off),
+                                                      ctypes.byref(nb)), "mmf_hybrid_saved_region")
+        flat = self.saved[off.value:off.value + nb.value].view(torch.float32)
+        if what == "cls_hidden":
+            return flat.view(self.micro, d.hidden)
+        return flat.view(self.micro, -1, d.hidden)

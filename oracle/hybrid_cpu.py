@@ -127,17 +127,28 @@ def pairs_present(names: Sequence[str], params: Mapping[str, torch.Tensor]) -> L
     return out
 
 
+def _relu(z: torch.Tensor, layer: str, relu_gate) -> torch.Tensor:
+    """torch.relu, or with the slope given where relu_gate[layer] selects (see hybrid_forward)."""
+    if relu_gate is None or layer not in relu_gate:
+        return torch.relu(z)
+    sel, pos = relu_gate[layer]
+    return torch.where(sel.reshape(z.shape), z * pos.reshape(z.shape).to(z.dtype), torch.relu(z))
+
+
 def hybrid_forward(params: Mapping[str, torch.Tensor], names: Sequence[str],
                    feats: Mapping[str, torch.Tensor], mask: Optional[torch.Tensor],
                    num_heads: int, p: float = 0.0, train: bool = False, gen=None,
-                   taps: Optional[dict] = None):
+                   taps: Optional[dict] = None, relu_gate: Optional[Mapping[str, tuple]] = None):
     """HybridFusion forward (src/fusion.py:331-427) + sequence-mode pooling.
 
     Returns (logits, info) with info = {attention_maps, fusion_weights, pooled}.
     ``taps`` (a dict, tests only) receives each ReLU's input ``z/<layer>``, its output
-    ``a/<layer>`` (gradient retained) and the layer's input ``in/<layer>``: a test bounds the
-    gradient difference that a pre-activation within rounding of 0 may legitimately show (the
-    kink of ReLU: relu'(z) flips for |z| at rounding level between two fp32 summation orders).
+    ``a/<layer>`` (gradient retained) and the layer's input ``in/<layer>`` (layers: the modality
+    names and "cls").  ``relu_gate`` (tests only) maps a layer to ``(sel, pos)``, two bool
+    tensors of z's shape: where ``sel``, the ReLU passes z with slope ``pos`` instead of taking
+    the sign of this computation's own z.  That is the kink of ReLU: for |z| within rounding of
+    0, relu'(z) may differ between two fp32 summation orders, so a test hands the oracle the
+    device's decision there (and only there) and keeps the plain bound everywhere.
     """
     ref = feats[names[0]]
     B = ref.shape[0]
@@ -150,7 +161,7 @@ def hybrid_forward(params: Mapping[str, torch.Tensor], names: Sequence[str],
         mk = mask[:, i].reshape(-1, *([1] * (x.dim() - 1)))
         xd = _dropout(x * mk, p, train, gen, SITE_IN + i)
         z = linear(xd, params[f"projections.{m}.0.weight"], params[f"projections.{m}.0.bias"])
-        a = torch.relu(z)
+        a = _relu(z, m, relu_gate)
         if taps is not None:
             taps[f"in/{m}"], taps[f"z/{m}"], taps[f"a/{m}"] = xd.detach(), z.detach(), a
             if a.requires_grad:
@@ -173,7 +184,7 @@ def hybrid_forward(params: Mapping[str, torch.Tensor], names: Sequence[str],
     w = adaptive_weights(params, names, {m: pooled[i] for i, m in enumerate(names)}, mask)
     fused = (pooled_t * w.unsqueeze(-1)).sum(1)
     zc = linear(fused, params["classifier.0.weight"], params["classifier.0.bias"])
-    ac = torch.relu(zc)
+    ac = _relu(zc, "cls", relu_gate)
     if taps is not None:
         taps["in/cls"], taps["z/cls"], taps["a/cls"] = fused.detach(), zc.detach(), ac
         if ac.requires_grad:

@@ -5,7 +5,9 @@ The module's Philox seed depends on how many modules the process constructed bef
 (attention._new_rng_state), so test order changes the dropout masks a test sees.  This runs the
 test_gpu_headline comparison for `--seeds` consecutive constructions and prints, per seed, the
 worst |got - ref| / bound over logits, dX and every parameter gradient (bound = 1e-3 max|ref| +
-1e-5 scale, as the test), and the tensors over 1.
+1e-5 scale, as the test), and the tensors over 1: against the plain oracle and against the oracle
+given the device's ReLU' decisions for pre-activations within rounding of 0
+(tests/_util.device_relu_gates, as the test), with the number of such elements per layer.
 usage (box): python scripts/seed_sweep.py [--seeds 8] [--workload c2]
 """
 import argparse
@@ -24,17 +26,15 @@ import bench  # noqa: E402
 import fusion  # noqa: E402
 import train_step  # noqa: E402
 from _philox import mask_provider  # noqa: E402
-from _util import relu_kink_slack  # noqa: E402
+from _util import device_relu_gates  # noqa: E402
 from oracle.hybrid_cpu import cross_entropy_ls, hybrid_forward  # noqa: E402
 
 
-def ratio(got, ref, atol, slack=None):
-    """worst |got - ref| / bound (with `slack`: (|got - ref| - slack) / bound) and the count over"""
+def ratio(got, ref, atol):
+    """worst |got - ref| / bound and the count over"""
     got, ref = got.double().cpu(), ref.double().cpu()
     bound = 1e-3 * float(ref.abs().max()) + atol
     d = (got - ref).abs()
-    if slack is not None:
-        d = (d - slack.double().reshape(d.shape)).clamp_min(0)
     return float(d.max()) / bound, int((d > bound).sum())
 
 
@@ -58,35 +58,38 @@ def main():
         params_cpu = {n: p.detach().cpu().clone() for n, p in model.named_parameters()}
         step.forward_backward()
         torch.cuda.synchronize()
-        params = {n: v.clone().requires_grad_(True) for n, v in params_cpu.items()}
-        xs = {n: f.detach().cpu().clone().requires_grad_(True) for n, f in zip(names, feats)}
+        dev_acts = {m: step.saved_activation("proj", i).cpu() for i, m in enumerate(names)}
+        dev_acts["cls"] = step.saved_activation("cls_hidden").cpu()
+
+        def oracle(taps=None, relu_gate=None):
+            params = {n: v.clone().requires_grad_(True) for n, v in params_cpu.items()}
+            xs = {n: f.detach().cpu().clone().requires_grad_(True) for n, f in zip(names, feats)}
+            logits, _ = hybrid_forward(params, names, xs, mask.cpu(), w["heads"], p=0.1, train=True,
+                                       gen=mask_provider(seed, offset, 0.1), taps=taps, relu_gate=relu_gate)
+            cross_entropy_ls(logits, labels.cpu()).backward()
+            return logits.detach(), params, xs
+
+        def compare(logits, params, xs):
+            scale = max([float(p.grad.abs().max()) for p in params.values()] +
+                        [float(x.grad.abs().max()) for x in xs.values()])
+            res = {"logits": ratio(step.logits, logits, 1e-6 * float(logits.abs().max()))}
+            for i, n in enumerate(names):
+                res[f"dx/{n}"] = ratio(step.dx[i], xs[n].grad, 1e-5 * scale)
+            grads = dict(step.named_grads())
+            for n, p in params.items():
+                res[n] = ratio(grads[n], p.grad, 1e-5 * scale)
+            worst = max(res.items(), key=lambda kv: kv[1][0])
+            over = {n: [round(r[0], 3), r[1]] for n, r in res.items() if r[0] > 1}
+            return [worst[0], round(worst[1][0], 4)], over
+
         taps = {}
-        logits, _ = hybrid_forward(params, names, xs, mask.cpu(), w["heads"], p=0.1, train=True,
-                                   gen=mask_provider(seed, offset, 0.1), taps=taps)
-        loss = cross_entropy_ls(logits, labels.cpu())
-        loss.backward()
-        scale = max([float(p.grad.abs().max()) for p in params.values()] +
-                    [float(x.grad.abs().max()) for x in xs.values()])
-        res = {"logits": ratio(step.logits, logits.detach(), 1e-6 * float(logits.detach().abs().max()))}
-        for i, n in enumerate(names):
-            res[f"dx/{n}"] = ratio(step.dx[i], xs[n].grad, 1e-5 * scale)
-        grads = dict(step.named_grads())
-        slack = {}
-        for m in names + ["cls"]:
-            wn = f"projections.{m}.0.weight" if m != "cls" else "classifier.0.weight"
-            sw, sb = relu_kink_slack(taps, m, params[wn])
-            slack[wn], slack[wn[:-len("weight")] + "bias"] = sw, sb
-        kinked = {}
-        for n, p in params.items():
-            res[n] = ratio(grads[n], p.grad, 1e-5 * scale)
-            if n in slack:
-                kinked[n] = ratio(grads[n], p.grad, 1e-5 * scale, slack[n])
-        worst = max(res.items(), key=lambda kv: kv[1][0])
-        over = {n: r for n, r in res.items() if r[0] > 1}
-        print(json.dumps({"k": k, "seed": seed, "offset": offset, "worst": [worst[0], round(worst[1][0], 4)],
-                          "over": {n: [round(r[0], 3), r[1]] for n, r in over.items()},
-                          "worst_relu_layer_with_slack": max(((n, round(r[0], 4)) for n, r in kinked.items()),
-                                                             key=lambda t: t[1])}), flush=True)
+        plain = compare(*oracle(taps=taps))
+        wts = {m: params_cpu[f"projections.{m}.0.weight"] for m in names}
+        wts["cls"] = params_cpu["classifier.0.weight"]
+        gates, band = device_relu_gates(taps, wts, dev_acts)
+        gated = compare(*oracle(relu_gate=gates))
+        print(json.dumps({"k": k, "seed": seed, "offset": offset, "plain": {"worst": plain[0], "over": plain[1]},
+                          "device_relu_gates": {"worst": gated[0], "over": gated[1]}, "band": band}), flush=True)
 
 
 if __name__ == "__main__":

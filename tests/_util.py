@@ -170,29 +170,30 @@ def diff_report(got, ref, rtol: float, atol: float = 0.0) -> str:
             f"{nbad} of {ref.numel()} elements over")
 
 
-def relu_kink_slack(taps: dict, layer: str, weight: torch.Tensor, rel: float = 1e-5):
-    """Per-element slack of a ReLU layer's weight and bias gradients for pre-activations within
-    rounding of zero.  Where |z| <= rel * (|x| @ |W|^T) (rows of the layer input x), two fp32
-    summation orders may disagree on the sign of z, so relu'(z) -- and with it that row's whole
-    contribution dL/da * x to dW (dL/da to db) -- may be present on one side only.  Returns
-    (slack_w, slack_b): the sums of those contributions' magnitudes (0 where no z is that close)."""
-    x = taps[f"in/{layer}"].double().reshape(-1, weight.shape[1])
-    z = taps[f"z/{layer}"].double().reshape(-1, weight.shape[0])
-    ga = taps[f"a/{layer}"].grad.double().reshape(-1, weight.shape[0]).abs()
-    scale = x.abs() @ weight.detach().double().abs().t()
-    amb = (z.abs() <= rel * scale).double()
-    return (ga * amb).t() @ x.abs(), (ga * amb).sum(0)
+def device_relu_gates(taps: dict, weights: dict, dev_acts: dict, rel: float = 1e-5):
+    """The device's ReLU'(z) decisions for the pre-activations within rounding of zero, for
+    hybrid_forward(relu_gate=...) (the ReLU kink).
 
-
-def close_slack(got, ref, rtol: float, atol: float, slack) -> bool:
-    """close(), with an elementwise allowance ``slack`` added to the bound."""
-    got = torch.as_tensor(got).double().cpu()
-    ref = torch.as_tensor(ref).double().cpu()
-    assert got.shape == ref.shape, (tuple(got.shape), tuple(ref.shape))
-    if ref.numel() == 0:
-        return True
-    bound = rtol * float(ref.abs().max()) + atol
-    return bool(((got - ref).abs() <= bound + torch.as_tensor(slack).double().reshape(ref.shape)).all())
+    taps: an oracle pass's taps (z/<layer>, in/<layer>); weights: layer -> its weight (H_out,
+    H_in); dev_acts: layer -> the device's activation after ReLU and dropout (the values its
+    backward takes ReLU' from, as value > 0; HybridTrainStep.saved_activation).  Where
+    |z| <= rel * (|x| @ |W|^T) two fp32 summation orders may disagree on the sign of z; there the
+    oracle is given the device's decision, everywhere else it keeps its own.  Asserted on the way:
+    outside that band every element the device passed (value > 0) has z > 0 in the oracle.
+    Returns ({layer: (sel, pos)}, {layer: number of elements in the band})."""
+    gates, counts = {}, {}
+    for layer, a_dev in dev_acts.items():
+        w = weights[layer].detach().double()
+        z = taps[f"z/{layer}"].double()
+        x = taps[f"in/{layer}"].double().reshape(-1, w.shape[1])
+        scale = (x.abs() @ w.abs().t()).reshape(z.shape)
+        sel = z.abs() <= rel * scale
+        pos = a_dev.detach().cpu().reshape(z.shape) > 0
+        bad = pos & ~sel & ~(z > 0)
+        assert not bool(bad.any()), (layer, int(bad.sum()), "device passed a z the oracle puts clearly <= 0")
+        gates[layer] = (sel, pos)
+        counts[layer] = int(sel.sum())
+    return gates, counts
 
 
 def close(got, ref, rtol: float, atol: float = 0.0) -> bool:

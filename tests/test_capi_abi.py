@@ -228,3 +228,31 @@ def test_buffer_contract_refused_before_launch(nat, monkeypatch):
         monkeypatch.setenv("MMF_NO_L1_LEAN", "1")                # a plan switch set after sizing
         assert call() == 1 and b"plan switches" in L.mmf_last_error()
         monkeypatch.delenv("MMF_NO_L1_LEAN")
+
+
+def test_saved_region_query(nat):
+    """mmf_hybrid_saved_region: the P_m / classifier-hidden regions lie inside `saved`, 256-B
+    aligned, sized (B, L_m, H) / (B, H) fp32, disjoint; unknown regions and indices refused."""
+    L = nat.lib()
+    d = _desc(nat)
+    for m in range(3):
+        d.seq_len[m] = 8 * (m + 1)
+    total = L.mmf_hybrid_saved_bytes(ctypes.byref(d))
+    off, nb = ctypes.c_uint64(), ctypes.c_uint64()
+    spans = []
+    for m in range(3):
+        assert L.mmf_hybrid_saved_region(ctypes.byref(d), 0, m, ctypes.byref(off), ctypes.byref(nb)) == 0
+        assert nb.value == 4 * d.batch * d.seq_len[m] * d.hidden
+        spans.append((off.value, off.value + nb.value))
+    assert L.mmf_hybrid_saved_region(ctypes.byref(d), 1, 0, ctypes.byref(off), ctypes.byref(nb)) == 0
+    assert nb.value == 4 * d.batch * d.hidden
+    spans.append((off.value, off.value + nb.value))
+    for a, b in spans:
+        assert a % 256 == 0 and b <= total
+    spans.sort()
+    assert all(spans[i][1] <= spans[i + 1][0] for i in range(len(spans) - 1))
+    assert L.mmf_hybrid_saved_region(ctypes.byref(d), 0, 3, ctypes.byref(off), ctypes.byref(nb)) != 0
+    assert b"modality" in L.mmf_last_error()
+    assert L.mmf_hybrid_saved_region(ctypes.byref(d), 1, 1, ctypes.byref(off), ctypes.byref(nb)) != 0
+    assert L.mmf_hybrid_saved_region(ctypes.byref(d), 2, 0, ctypes.byref(off), ctypes.byref(nb)) != 0
+    assert b"unknown region" in L.mmf_last_error()

@@ -8,9 +8,9 @@
    (the pooled plan's non-lean attention kernels: Lk % 32 != 0) at the precision's instantiations;
    logits, loss, input and parameter gradients are compared with the oracle under the replayed
    Philox masks (tests/_philox.py):
-     * "highest": 1e-3 of each tensor's largest element (the ReLU layers' weight / bias gradients
-       with the per-element allowance for pre-activations within rounding of zero,
-       tests/_util.relu_kink_slack, as the C2 headline test);
+     * "highest": 1e-3 of each tensor's largest element, the oracle taking the device's ReLU'
+       decision for pre-activations within rounding of zero (tests/_util.device_relu_gates, as
+       the C2 headline test);
      * "medium": the bf16 bounds of tests/test_gpu_bf16.py (logits within 3e-2 of the largest
        logit, argmax >= 99 %; every gradient ||got - ref|| <= max(3e-2 ||ref||, 4 ||emu - ref||,
        3e-3 S), emu = the oracle with bf16-rounded matmul operands).
@@ -33,7 +33,7 @@ import torch
 import torch.nn.functional as F
 
 from _philox import mask_provider
-from _util import bf16_matmul_mode, close, close_slack, diff_report, relu_kink_slack
+from _util import bf16_matmul_mode, close, device_relu_gates, diff_report
 from test_gpu_bf16 import group_scale, logits_ok, norm_ok
 
 pytestmark = pytest.mark.gpu
@@ -97,17 +97,19 @@ def test_c4_benchmark_step_matches_oracle(env, precision):
         assert int(step.rng[1].item()) == offset + 1
     finally:
         torch.set_float32_matmul_precision(prev)
+    dev_acts = {m: step.saved_activation("proj", i).cpu() for i, m in enumerate(names)}
+    dev_acts["cls"] = step.saved_activation("cls_hidden").cpu()
 
     torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
     m_cpu = mask.cpu()
 
-    def oracle(bf16, taps=None):
+    def oracle(bf16, taps=None, relu_gate=None):
         params = {k: v.clone().requires_grad_(True) for k, v in params_cpu.items()}
         xs = {n: f.detach().cpu().clone().requires_grad_(True) for n, f in zip(names, feats)}
 
         def run():
             logits, _ = hybrid_forward(params, names, xs, m_cpu, w["heads"], p=0.1, train=True,
-                                       gen=mask_provider(seed, offset, 0.1), taps=taps)
+                                       gen=mask_provider(seed, offset, 0.1), taps=taps, relu_gate=relu_gate)
             loss = cross_entropy_ls(logits, labels.cpu())
             loss.backward()
             return logits.detach(), loss.detach()
@@ -121,12 +123,11 @@ def test_c4_benchmark_step_matches_oracle(env, precision):
     grads = dict(step.named_grads())
     if precision == "highest":
         taps = {}
-        logits, loss, params, xs = oracle(False, taps)
-        slack = {}
-        for m in names + ["cls"]:
-            wname = f"projections.{m}.0.weight" if m != "cls" else "classifier.0.weight"
-            sw, sb = relu_kink_slack(taps, m, params[wname])
-            slack[wname], slack[wname[:-len("weight")] + "bias"] = sw, sb
+        oracle(False, taps)
+        wts = {m: params_cpu[f"projections.{m}.0.weight"] for m in names}
+        wts["cls"] = params_cpu["classifier.0.weight"]
+        gates, _ = device_relu_gates(taps, wts, dev_acts)
+        logits, loss, params, xs = oracle(False, relu_gate=gates)
         assert close(step.logits.cpu(), logits, 1e-3, 1e-6 * float(logits.abs().max()))
         assert abs(float(step.loss.item()) - float(loss)) <= 1e-5 * max(1.0, abs(float(loss)))
         scale = max([float(p.grad.abs().max()) for p in params.values()] +
@@ -136,11 +137,7 @@ def test_c4_benchmark_step_matches_oracle(env, precision):
                 f"dx/{n}: " + diff_report(step.dx[i].cpu(), xs[n].grad, 1e-3, 1e-5 * scale)
         for n, p in params.items():
             g = grads[n].cpu()
-            if n in slack:
-                assert close_slack(g, p.grad, 1e-3, 1e-5 * scale, slack[n]), \
-                    f"{n}: " + diff_report(g, p.grad, 1e-3, 1e-5 * scale)
-            else:
-                assert close(g, p.grad, 1e-3, 1e-5 * scale), f"{n}: " + diff_report(g, p.grad, 1e-3, 1e-5 * scale)
+            assert close(g, p.grad, 1e-3, 1e-5 * scale), f"{n}: " + diff_report(g, p.grad, 1e-3, 1e-5 * scale)
         return
 
     ref, rloss, rp, rx = oracle(False)

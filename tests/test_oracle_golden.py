@@ -154,3 +154,54 @@ def test_oracle_seqenc_matches_reference(case):
     assert rel_err(torch.from_numpy(dseq), fx["dsequence"]) <= TOL
     for k, g in grads.items():
         assert close(torch.from_numpy(g), fx[f"grad/{k}"], TOL, 1e-7), k
+
+
+def test_oracle_relu_gate_hook():
+    """hybrid_forward(relu_gate=...) (the device's ReLU' decision at pre-activations within rounding
+    of 0, used by the GPU parity tests): an empty selection is the plain oracle bit for bit; a
+    selected element takes the given slope; tests/_util.device_relu_gates refuses a device that
+    passed a pre-activation the oracle puts clearly below 0."""
+    from _util import device_relu_gates, hybrid_inputs, hybrid_state
+    from oracle.hybrid_cpu import hybrid_forward
+    case = HYBRID_CASES[0]
+    sd = hybrid_state(case.names, case.dims, case.hidden, case.classes, case.seed, case.deleted)
+    feats_np, mask_np, grad_np = hybrid_inputs(case)
+
+    def run(taps=None, gate=None):
+        params = {k: torch.from_numpy(v).requires_grad_(True) for k, v in sd.items()}
+        feats = {m: torch.from_numpy(v).requires_grad_(True) for m, v in feats_np.items()}
+        logits, _ = hybrid_forward(params, case.names, feats, torch.from_numpy(mask_np), case.heads,
+                                   taps=taps, relu_gate=gate)
+        (logits * torch.from_numpy(grad_np)).sum().backward()
+        return logits.detach(), {k: p.grad for k, p in params.items()}
+
+    taps = {}
+    base, gbase = run(taps)
+    m = case.names[0]
+    z = taps[f"z/{m}"]
+    none = {m: (torch.zeros_like(z, dtype=torch.bool), torch.zeros_like(z, dtype=torch.bool))}
+    same, gsame = run(gate=none)
+    assert torch.equal(same, base) and all(torch.equal(gsame[k], gbase[k]) for k in gbase if gbase[k] is not None)
+    # one clearly positive pre-activation given slope 0: that activation (only) is 0
+    flat = int((z.reshape(-1) > 0).nonzero()[0])
+    sel = torch.zeros(z.numel(), dtype=torch.bool)
+    sel[flat] = True
+    taps2 = {}
+    cut, _ = run(taps2, gate={m: (sel.reshape(z.shape), torch.zeros_like(z, dtype=torch.bool))})
+    a0, a1 = taps[f"a/{m}"].detach().reshape(-1), taps2[f"a/{m}"].detach().reshape(-1)
+    assert float(a0[flat]) > 0 and float(a1[flat]) == 0.0
+    keep = torch.ones_like(a0, dtype=torch.bool)
+    keep[flat] = False
+    assert torch.equal(a0[keep], a1[keep]) and not torch.equal(cut, base)
+    # device_relu_gates: the oracle's own activations pass; a clearly positive z the "device" passed
+    # as 0 is allowed (dropout), a clearly negative z it passed as > 0 is refused
+    wts = {mm: torch.from_numpy(sd[f"projections.{mm}.0.weight"]) for mm in case.names}
+    acts = {mm: torch.relu(taps[f"z/{mm}"]) for mm in case.names}
+    gates, band = device_relu_gates(taps, wts, acts)
+    assert set(gates) == set(case.names) and all(v >= 0 for v in band.values())
+    neg = int((z.reshape(-1) < -1e-3).nonzero()[0])
+    bad = acts[m].clone().reshape(-1)
+    bad[neg] = 1.0
+    acts[m] = bad.reshape(z.shape)
+    with pytest.raises(AssertionError):
+        device_relu_gates(taps, wts, acts)
