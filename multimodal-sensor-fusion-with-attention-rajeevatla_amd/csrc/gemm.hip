@@ -794,16 +794,24 @@ void gemm_lds_chain_kernel(const GemmArgs args) {
 // a tile is written out.  Persistent grid: 2 workgroups per CU.
 constexpr int WSR_DK = 16, WSR_NS = 6, WSR_NKC = 16;   // k-tile, ring depth, max 8-deep k chunks (K <= 128)
 
-template <int BF>
+// EXT: the extended epilogue (row scale, dropout, column sums) and B stored [k][n] (the modality
+// projections and dX at C2); without it the round-5 kernel (Q / K projections: bias, ReLU)
+template <int BF, bool EXT>
 __global__ __launch_bounds__(NT, 2) void gemm_wsr_kernel(const GemmArgs args, int total_items, int K) {
   constexpr int DTILE = BM * WSR_DK;
   __shared__ __attribute__((aligned(16))) float ring[WSR_NS * DTILE];
+  __shared__ float csx[BN];   // EPI_COLSUM: the lower-half waves' (wm = 1) 64-row column sums
   const int t = threadIdx.x;
   const int lane = t & 63, wave = t >> 6;
   const int h = lane >> 5, c = lane & 31;
   const int wm = wave >> 1, wn = wave & 1;
   const int nkt = K / WSR_DK, nkc = K / 8;
 
+  RngSnap rs{0, 0};
+  const float p = args.drop_p;
+  const float inv_keep = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  const uint32_t thr = p16(p);
+  if (p > 0.f && args.rng) rs = *args.rng;
   if (args.rng_advance && blockIdx.x == 0 && threadIdx.x == 0) args.rng_advance[1] += 1;   // see launch_gemm
   const int nwg = gridDim.x;
   const int item0 = (int)(((int64_t)blockIdx.x * total_items) / nwg);
@@ -883,10 +891,20 @@ __global__ __launch_bounds__(NT, 2) void gemm_wsr_kernel(const GemmArgs args, in
       for (int b = 0; b < 2; ++b) {
         const int col = wn * 64 + b * 32 + c;
         const bool ok = col < G.N;
-        const float* wrow = S.b.ptr + (int64_t)(ok ? col : 0) * S.b.ld + 4 * h;
+        if (EXT && args.bmode == MODE_KR) {
+          // B stored [k][n] (dX = dZ W_proj): the same fragments gathered down column `col`
+          const float* wcol = S.b.ptr + (ok ? col : 0) + (int64_t)(4 * h) * S.b.ld;
 #pragma unroll
-        for (int m = 0; m < WSR_NKC; ++m)
-          breg[b][m] = (ok && m < nkc) ? *reinterpret_cast<const f32x4*>(wrow + 8 * m) : f32x4{0.f, 0.f, 0.f, 0.f};
+          for (int m = 0; m < WSR_NKC; ++m)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              breg[b][m][e] = (ok && m < nkc) ? wcol[(int64_t)(8 * m + e) * S.b.ld] : 0.f;
+        } else {
+          const float* wrow = S.b.ptr + (int64_t)(ok ? col : 0) * S.b.ld + 4 * h;
+#pragma unroll
+          for (int m = 0; m < WSR_NKC; ++m)
+            breg[b][m] = (ok && m < nkc) ? *reinterpret_cast<const f32x4*>(wrow + 8 * m) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
         bias[b] = (ok && (G.epi & EPI_BIAS)) ? G.bias[col] : 0.f;
       }
       // Retire these loads here with a wait the compiler can see (the builtin,
@@ -946,12 +964,20 @@ if constexpr (BF != 0) {
         ++f;
       }
     }
-    // Epilogue straight from the accumulators: v = alpha*acc + bias[j]; relu.
+    // Epilogue straight from the accumulators: v = alpha*acc + bias[j]; relu; rowscale; dropout
+    // (the LDS-DMA kernel's order and keep(site, i*N + j) decisions).
     // Lane (c, h) holds rows 8q+4h+{0..3} of column c; a 4x4 transpose across
     // the lane quad (xor 2, then xor 1) leaves it 4 consecutive columns of one
     // row, stored as one 16-B store (8 rows x 128 B per wave instruction).
     const int x = c & 3;
     const int i0 = rt * BM + wm * 64;
+    const int epi = EXT ? G.epi : 0;
+    const bool drop = (epi & EPI_DROP) && p > 0.f;
+    // EPI_ROWSCALE: one scale per row tile (job_wsr: rs_div % BM == 0), a scalar load
+    float rsc = 1.f;
+    if (epi & EPI_ROWSCALE)
+      rsc = ((const __attribute__((address_space(4))) float*)G.rowscale)[(rt * BM / G.rs_div) * G.rs_stride + G.rs_off];
+    float csum[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};   // EPI_COLSUM
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -980,9 +1006,46 @@ if constexpr (BF != 0) {
           }
           const int row = i0 + a * 32 + 8 * q + 4 * h + x;
           const int col = wn * 64 + b * 32 + (c & ~3);
+          if (epi & EPI_ROWSCALE) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] *= rsc;
+          }
+          if (drop) {
+            // the Philox block of columns (col & ~7) .. +7 of this row (shared with lane c ^ 4),
+            // this lane's four of its eight decisions
+            const uint4 rr = philox_block(rs, G.drop_site, ((uint64_t)row * (uint64_t)G.N + (uint64_t)(col & ~7)) >> 3);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = keep_from(rr, (col & 4) + e, thr) ? v[e] * inv_keep : 0.f;
+          }
+          if (epi & EPI_COLSUM) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) csum[b][e] += v[e];
+          }
           *reinterpret_cast<f32x4*>(G.C + (int64_t)row * G.ldc + col) = f32x4{v[0], v[1], v[2], v[3]};
         }
       }
+    if (epi & EPI_COLSUM) {
+      // per-tile column sums of the stored values (GemmGroup::colsum): each lane's 8 rows (a, q),
+      // then the quad (rows x, xor 1 / 2) and the halves (rows h, xor 32) -- every lane of quad
+      // c & ~3 then holds the wave's 64-row sums of columns (c & ~3) + e; lane (c, h) keeps column
+      // wn*64 + 32 h + c; the wm = 1 waves hand theirs to the wm = 0 waves through LDS (rows 0-63
+      // + rows 64-127, fixed order)
+      float mine = 0.f;
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float sv = csum[b][e];
+          sv += dpp<DPP_XOR1>(sv);
+          sv += dpp<DPP_XOR2>(sv);
+          sv = sum_xor32(sv);
+          if (b == h && e == x) mine = sv;
+        }
+      const int colx = wn * 64 + 32 * h + c;
+      if (wm == 1) csx[colx] = mine;
+      lds_barrier();
+      if (wm == 0 && colx < G.N) G.colsum[(int64_t)rt * G.N + colx] = mine + csx[colx];
+    }
     epi_mark = nissued;
   }
 }
@@ -1584,12 +1647,25 @@ inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 bool job_wsr(const GemmJob& J, int amode, int bmode) {
   const GemmGroup& g = J.g;
-  if (amode != MODE_RK || bmode != MODE_RK || J.nsrc != 1 || g.nbatch > 1) return false;
-  if (g.epi & ~(EPI_BIAS | EPI_RELU)) return false;
+  if (amode != MODE_RK || (bmode != MODE_RK && bmode != MODE_KR) || J.nsrc != 1 || g.nbatch > 1) return false;
+  if (g.epi & ~(EPI_BIAS | EPI_RELU | EPI_DROP | EPI_COLSUM | EPI_ROWSCALE)) return false;
+  // The extended forms (row scale, dropout, column sums, B stored [k][n]) are opt-in
+  // (MMF_WSR_EPI=1): at C2 they would take the modality projections and dX, 768 row tiles each,
+  // which the LDS-DMA kernel runs as one lockstep wave of 3 workgroups per CU in 62 / 59 us; the
+  // persistent weight-stationary grid (2 workgroups per CU, 1-2 tiles each: ~24 us per tile per
+  // workgroup, its register-resident W^T loaded per workgroup) took 75 / 75 us and the step
+  // 0.959-0.972 -> 0.984-0.998 ms (profiles/r06/wsr_epi/).  It pays with many tiles per
+  // workgroup (the Q / K projections: 3072 tiles), not here.
+  static const bool ext_on = getenv("MMF_WSR_EPI") != nullptr;
+  if (!ext_on && (bmode != MODE_RK || (g.epi & ~(EPI_BIAS | EPI_RELU)))) return false;
+  // one row scale per 128-row tile (a scalar load); column sums per tile into colsum
+  if ((g.epi & EPI_ROWSCALE) && (g.rs_div <= 0 || g.rs_div % BM != 0 || !g.rowscale)) return false;
+  if ((g.epi & EPI_COLSUM) && !g.colsum) return false;
   const GemmSrc& s = J.src[0];
+  const bool b_ok = bmode == MODE_RK ? (s.b.ld % 4 == 0 && aligned16(s.b.ptr)) : s.b.ld >= g.N;
   return g.N == BN && g.M % BM == 0 && s.K % WSR_DK == 0 && s.K >= WSR_DK && s.K <= 8 * WSR_NKC &&
-         s.a.row_div == 1 && s.b.row_div == 1 && s.a.ld % 4 == 0 && s.b.ld % 4 == 0 && aligned16(s.a.ptr) &&
-         aligned16(s.b.ptr) && g.ldc % 4 == 0 && aligned16(g.C);
+         s.a.row_div == 1 && s.b.row_div == 1 && s.a.ld % 4 == 0 && aligned16(s.a.ptr) && b_ok &&
+         s.a.seg_stride == 0 && s.b.seg_stride == 0 && g.ldc % 4 == 0 && aligned16(g.C);
 }
 
 int cu_count() {
@@ -1605,12 +1681,15 @@ int cu_count() {
 
 // Every job weight-stationary-eligible with one common K: persistent launches
 // of up to GEMM_MAX_GROUPS groups.
-hipError_t launch_wsr(const GemmJob* jobs, int njobs, hipStream_t st, uint64_t* rng_advance) {
+hipError_t launch_wsr(const GemmJob* jobs, int njobs, hipStream_t st, uint64_t* rng_advance, int bmode, float drop_p,
+                      const RngSnap* rng) {
   for (int done = 0; done < njobs;) {
     GemmArgs args;
     memset(&args, 0, sizeof(args));
     args.amode = MODE_RK;
-    args.bmode = MODE_RK;
+    args.bmode = bmode;
+    args.drop_p = drop_p;
+    args.rng = rng;
     args.rng_advance = rng_advance;
     rng_advance = nullptr;
     int ng = 0, items = 0;
@@ -1632,16 +1711,23 @@ hipError_t launch_wsr(const GemmJob* jobs, int njobs, hipStream_t st, uint64_t* 
     const int K = args.s[0].K;
     const int grid = std::min(items, 2 * cu_count());
     const int pr = math_mode();
-    if (pr == 2) {
-      ProfLaunch prof_(st, "gemm_wsr_kernel<2>", fl, by);
-      mmf_launch(gemm_wsr_kernel<2>, dim3(grid), dim3(NT), 0, st, args, items, K);
-    } else if (pr == 1) {
-      ProfLaunch prof_(st, "gemm_wsr_kernel<1>", fl, by);
-      mmf_launch(gemm_wsr_kernel<1>, dim3(grid), dim3(NT), 0, st, args, items, K);
+    bool ext = bmode != MODE_RK;
+    for (int i = 0; i < ng; ++i) ext = ext || (args.g[i].epi & ~(EPI_BIAS | EPI_RELU)) != 0;
+#define MMF_WSR_LAUNCH(BFV, EXTV, NAME)                                             \
+  {                                                                                 \
+    ProfLaunch prof_(st, NAME, fl, by);                                             \
+    mmf_launch((gemm_wsr_kernel<BFV, EXTV>), dim3(grid), dim3(NT), 0, st, args, items, K); \
+  }
+    if (ext) {
+      if (pr == 2) MMF_WSR_LAUNCH(2, true, "gemm_wsr_kernel<2, true>")
+      else if (pr == 1) MMF_WSR_LAUNCH(1, true, "gemm_wsr_kernel<1, true>")
+      else MMF_WSR_LAUNCH(0, true, "gemm_wsr_kernel<0, true>")
     } else {
-      ProfLaunch prof_(st, "gemm_wsr_kernel<0>", fl, by);
-      mmf_launch(gemm_wsr_kernel<0>, dim3(grid), dim3(NT), 0, st, args, items, K);
+      if (pr == 2) MMF_WSR_LAUNCH(2, false, "gemm_wsr_kernel<2>")
+      else if (pr == 1) MMF_WSR_LAUNCH(1, false, "gemm_wsr_kernel<1>")
+      else MMF_WSR_LAUNCH(0, false, "gemm_wsr_kernel<0>")
     }
+#undef MMF_WSR_LAUNCH
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
@@ -1663,7 +1749,7 @@ hipError_t launch_gemm(const GemmJob* jobs_in, int njobs, int amode, int bmode, 
     bool wsr = njobs > 0;
     for (int i = 0; i < njobs && wsr; ++i)
       wsr = job_wsr(jobs_in[i], amode, bmode) && jobs_in[i].src[0].K == jobs_in[0].src[0].K && !jobs_in[i].chain;
-    if (wsr && getenv("MMF_NO_WSR") == nullptr) return launch_wsr(jobs_in, njobs, st, rng_advance);
+    if (wsr && getenv("MMF_NO_WSR") == nullptr) return launch_wsr(jobs_in, njobs, st, rng_advance, bmode, drop_p, rng);
   }
   // the tiled launches below take the rng advance on their first launch; a call that
   // ends in small slabs only advances with a launch of its own
